@@ -1,0 +1,890 @@
+// =============================================================================
+// TEST INFRASTRUCTURE ONLY — NOT PART OF THE PRODUCT.
+//
+// CPU restatement ("oracle") of VerneMQ's subscription routing index
+// `vmq_reg_trie` and the helpers it depends on.  Only tests/, the smoke()
+// check in __graft_entry__.py and bench.py's cpu_baseline leg may load this.
+// The product (vernemq_amd/, libvmqgpu.so) never links or calls it.
+//
+// Parity pin: the reference is Erlang/OTP and cannot be compiled or run in
+// this container (no erl/erlc).  This restatement is pinned
+// by the golden vectors hand-transcribed from the reference's own tests into
+// tests/golden/*.json (vmq_publish_SUITE pattern_matching_test, vmq_topic
+// eunit KATs, vmq_subscriber eunit KATs, vmq_reg_trie_bench_SUITE fold
+// expectations, vmq_upgrade_SUITE, vmq_subscribe_SUITE).  The three
+// structural quirks Q1–Q3 are NOT covered by any reference
+// test: for those, parity is "unpinned" and rests on this line-by-line
+// reading of the source, recorded as hand-derived fixtures.
+//
+// Style: deliberately literal.  Every ETS table of vmq_reg_trie:init/1
+// (apps/vmq_server/src/vmq_reg_trie.erl:135-143) is a string-keyed hash map
+// whose keys are byte encodings of the Erlang terms; each function follows
+// the Erlang clause it cites (file:line relative to /root/reference).  No
+// interning, no ids: terms stay strings, so this code shares nothing with
+// the product's id-based tables.
+// =============================================================================
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <set>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+using Words = std::vector<std::string>;
+
+// ---------------------------------------------------------------- encoding
+void put_u32(std::string& s, uint32_t v) { s.append(reinterpret_cast<const char*>(&v), 4); }
+void put_str(std::string& s, const std::string& v) { put_u32(s, (uint32_t)v.size()); s += v; }
+std::string enc_words(const Words& w) {
+  std::string s;
+  put_u32(s, (uint32_t)w.size());
+  for (auto& x : w) put_str(s, x);
+  return s;
+}
+
+struct Reader {
+  const uint8_t* p; const uint8_t* e; bool bad = false;
+  uint8_t u8() { if (p + 1 > e) { bad = true; return 0; } return *p++; }
+  uint32_t u32() { if (p + 4 > e) { bad = true; return 0; } uint32_t v; memcpy(&v, p, 4); p += 4; return v; }
+  std::string str() {
+    uint32_t n = u32();
+    if (bad || p + n > e) { bad = true; return {}; }
+    std::string s(reinterpret_cast<const char*>(p), n); p += n; return s;
+  }
+  Words words() { uint32_t n = u32(); Words w; for (uint32_t i = 0; i < n && !bad; i++) w.push_back(str()); return w; }
+};
+
+// Printable, unambiguous rendering of binaries for the canonical table dump.
+std::string esc(const std::string& s) {
+  static const char* hx = "0123456789abcdef";
+  std::string o = "\"";
+  for (unsigned char c : s) {
+    if (c >= 0x20 && c < 0x7f && c != '"' && c != '\\') o += (char)c;
+    else { o += "\\x"; o += hx[c >> 4]; o += hx[c & 15]; }
+  }
+  return o + "\"";
+}
+std::string show_path(const Words& w) {
+  std::string o = "[";
+  for (size_t i = 0; i < w.size(); i++) { if (i) o += ","; o += esc(w[i]); }
+  return o + "]";
+}
+
+// ------------------------------------------------------------- vmq_topic
+// triples/1  apps/vmq_commons/src/vmq_topic.erl:71-77
+struct Triple { bool parent_root; Words parent; std::string word; Words child; };
+std::vector<Triple> triples(const Words& topic) {
+  std::vector<Triple> out;
+  for (size_t i = 0; i < topic.size(); i++) {
+    Triple t;
+    t.parent_root = (i == 0);
+    t.parent.assign(topic.begin(), topic.begin() + i);
+    t.word = topic[i];
+    t.child.assign(topic.begin(), topic.begin() + i + 1);
+    out.push_back(std::move(t));
+  }
+  return out;
+}
+
+// contains_wildcard/1  vmq_topic.erl:91-95
+bool contains_wildcard(const Words& t) {
+  for (size_t i = 0; i < t.size(); i++) {
+    if (t[i] == "+") return true;
+    if (t[i] == "#" && i + 1 == t.size()) return true;
+  }
+  return false;
+}
+
+// validate_topic/2  vmq_topic.erl:82-133.  Error codes mirror the atoms.
+enum { V_OK = 0, V_EMPTY = 1, V_TOO_LONG = 2, V_PLUS_PUB = 3, V_HASH_PUB = 4,
+       V_PLUS_WORD = 5, V_HASH_WORD = 6, V_BAD_SHARED = 7 };
+
+int validate_publish(const std::string& topic, Words& out) {
+  // validate_publish_topic/3  vmq_topic.erl:97-112
+  size_t seg = 0;
+  out.clear();
+  for (;;) {
+    std::string rest = topic.substr(seg);
+    if (rest.compare(0, 2, "+/") == 0 || rest == "+") return V_PLUS_PUB;  // :97-98
+    if (rest == "#") return V_HASH_PUB;                                     // :99
+    size_t L = 0;
+    for (;;) {                                                              // :100-111
+      if (L < rest.size() && rest[L] == '/') { out.push_back(rest.substr(0, L)); seg += L + 1; break; }
+      if (L == rest.size()) { out.push_back(rest); return V_OK; }
+      if (rest[L] == '+') return V_PLUS_WORD;
+      if (rest[L] == '#') return V_HASH_WORD;
+      L++;
+    }
+  }
+}
+
+int validate_shared(const Words& t) {
+  // validate_shared_subscription/1  vmq_topic.erl:131-133
+  if (!t.empty() && t[0] == "$share") return t.size() >= 3 ? V_OK : V_BAD_SHARED;
+  return V_OK;
+}
+
+int validate_subscribe(const std::string& topic, Words& out) {
+  // validate_subscribe_topic/3  vmq_topic.erl:114-129
+  size_t seg = 0;
+  out.clear();
+  for (;;) {
+    std::string rest = topic.substr(seg);
+    if (rest.compare(0, 2, "+/") == 0) { out.push_back("+"); seg += 2; continue; }  // :114
+    if (rest == "+" || rest == "#") { out.push_back(rest); return validate_shared(out); }  // :115-116
+    size_t L = 0;
+    bool next = false;
+    for (;;) {
+      if (L < rest.size() && rest[L] == '/') { out.push_back(rest.substr(0, L)); seg += L + 1; next = true; break; }
+      if (L == rest.size()) { out.push_back(rest); return validate_shared(out); }
+      if (rest[L] == '+') return V_PLUS_WORD;
+      if (rest[L] == '#') return V_HASH_WORD;
+      L++;
+    }
+    if (!next) break;
+  }
+  return V_OK;
+}
+
+int validate_topic(int type, const std::string& topic, Words& out) {
+  if (topic.empty()) return V_EMPTY;                 // vmq_topic.erl:82-83
+  if (topic.size() > 65536) return V_TOO_LONG;       // :84-85 (MAX_LEN :45)
+  return type == 0 ? validate_publish(topic, out) : validate_subscribe(topic, out);
+}
+
+// match/2  vmq_topic.erl:53-65 (naive filter matcher, used as a cross-check)
+bool naive_match(const Words& topic, size_t i, const Words& filt, size_t j) {
+  for (;;) {
+    if (i == topic.size() && j == filt.size()) return true;                  // :53-54
+    if (j < filt.size() && filt[j] == "#" && j + 1 == filt.size()) {
+      // :55 is tried first when the head words are equal; "#" never equals a
+      // publish word (publishes reject '#'), so :59 is what applies.
+      if (i < topic.size() && topic[i] == "#") { i++; j++; continue; }
+      return true;                                                           // :59-60
+    }
+    if (i < topic.size() && j < filt.size() && topic[i] == filt[j]) { i++; j++; continue; }  // :55-56
+    if (i < topic.size() && j < filt.size() && filt[j] == "+") { i++; j++; continue; }      // :57-58
+    return false;                                                            // :61-65
+  }
+}
+
+// ------------------------------------------------------------ ETS tables
+// Erlang terms used as keys, encoded to byte strings.
+std::string node_id_key(const std::string& mp, bool root, const Words& path) {
+  std::string k; put_str(k, mp);
+  if (root) k += 'R'; else { k += 'P'; k += enc_words(path); }
+  return k;
+}
+std::string mp_topic_key(const std::string& mp, const Words& topic) {
+  std::string k; put_str(k, mp); k += enc_words(topic); return k;
+}
+
+// #trie{edge=#trie_edge{node_id, word}, node_id=Child}   vmq_reg_trie.erl:41,43
+struct TrieEdgeVal { std::string mp; bool parent_root; Words parent; std::string word; Words child; };
+// #trie_node{node_id, edge_count=0, topic}                 vmq_reg_trie.erl:42
+struct TrieNodeVal { std::string mp; bool root; Words path; int64_t edge_count; bool has_topic; Words topic; };
+
+struct NodeOrGroup {  // Node atom | {Node, Group}
+  bool is_group = false; std::string node; std::string group;
+  bool operator==(const NodeOrGroup& o) const { return is_group == o.is_group && node == o.node && group == o.group; }
+  std::string show() const { return is_group ? "{" + esc(node) + "," + esc(group) + "}" : esc(node); }
+};
+struct TopicVal { std::string mp; Words topic; int64_t total; std::vector<std::pair<NodeOrGroup, int64_t>> nodes; };
+
+// Values stored in vmq_trie_subs: {SubscriberId, SubInfo} or
+// {Node, Group, SubscriberId, SubInfo}   vmq_reg_trie.erl:445, :500
+struct SubVal {
+  bool is_group = false;
+  std::string node, group, sub_mp, client, subinfo;
+  std::string enc() const {
+    std::string s; s += is_group ? 'G' : 'L';
+    put_str(s, node); put_str(s, group); put_str(s, sub_mp); put_str(s, client); put_str(s, subinfo);
+    return s;
+  }
+  bool operator==(const SubVal& o) const { return enc() == o.enc(); }
+  std::string show() const {
+    std::string sid = "{" + esc(sub_mp) + "," + esc(client) + "}";
+    if (is_group) return "{" + esc(node) + "," + esc(group) + "," + sid + "," + subinfo + "}";
+    return "{" + sid + "," + subinfo + "}";
+  }
+};
+// Keys of vmq_trie_subs: {MP, Topic} or {MP, Group, Topic}
+struct SubKey {
+  bool is_group = false; std::string mp, group; Words topic;
+  std::string enc() const {
+    std::string s; s += is_group ? 'G' : 'L'; put_str(s, mp); put_str(s, group); s += enc_words(topic); return s;
+  }
+  std::string show() const {
+    if (is_group) return "{" + esc(mp) + "," + esc(group) + "," + show_path(topic) + "}";
+    return "{" + esc(mp) + "," + show_path(topic) + "}";
+  }
+};
+struct BagObj { bool fanout; SubVal val; };  // {Key, Val} | {Key, fanout}
+struct SubsEntry { SubKey key; std::vector<BagObj> objs; };
+
+struct RemoteVal { std::string mp; Words topic; std::vector<std::pair<std::string, int64_t>> nodes; };
+
+struct Emission {
+  int kind;  // 1 = {SubscriberId, SubInfo}; 2 = {Node, Group, SubscriberId, SubInfo}; 3 = Node
+  SubVal val; std::string node;
+};
+
+struct Counters { uint64_t s = 0; };
+
+struct Oracle {
+  std::string self_node;   // node()
+  std::unordered_map<std::string, TrieEdgeVal> vmq_trie;           // keypos 2 (edge)
+  std::unordered_map<std::string, TrieNodeVal> vmq_trie_node;      // keypos 2 (node_id)
+  std::unordered_map<std::string, TopicVal> vmq_trie_topic;        // keypos 1
+  std::unordered_map<std::string, SubsEntry> vmq_trie_subs;        // bag
+  std::map<std::string, std::map<std::string, SubVal>> vmq_trie_subs_fanout;  // ordered_set {{Key,Val}}
+  std::unordered_map<std::string, SubKey> fanout_keys;
+  std::unordered_map<std::string, RemoteVal> vmq_trie_remote_subs; // keypos 1
+
+  // --------------------------------------------------- trie maintenance
+  static std::string edge_key(const std::string& mp, bool root, const Words& parent, const std::string& w) {
+    std::string k = node_id_key(mp, root, parent); put_str(k, w); return k;
+  }
+
+  // add_and_inc/2  vmq_reg_trie.erl:409-415
+  template <class K>
+  static void add_and_inc(std::vector<std::pair<K, int64_t>>& nodes, const K& n) {
+    for (auto& e : nodes) if (e.first == n) { e.second += 1; return; }
+    nodes.insert(nodes.begin(), {n, 1});
+  }
+  // rem_and_dec/2  vmq_reg_trie.erl:399-407
+  template <class K>
+  static void rem_and_dec(std::vector<std::pair<K, int64_t>>& nodes, const K& n) {
+    for (size_t i = 0; i < nodes.size(); i++) {
+      if (nodes[i].first == n) {
+        if (nodes[i].second == 1) nodes.erase(nodes.begin() + i);
+        else nodes[i].second -= 1;
+        return;
+      }
+    }
+  }
+
+  // trie_add_path/2  vmq_reg_trie.erl:340-356
+  void trie_add_path(const std::string& mp, const Triple& t) {
+    std::string nk = node_id_key(mp, t.parent_root, t.parent);
+    std::string ek = edge_key(mp, t.parent_root, t.parent, t.word);
+    auto it = vmq_trie_node.find(nk);
+    if (it != vmq_trie_node.end()) {
+      if (vmq_trie.find(ek) == vmq_trie.end()) {
+        it->second.edge_count += 1;
+        vmq_trie[ek] = TrieEdgeVal{mp, t.parent_root, t.parent, t.word, t.child};
+      }
+    } else {
+      vmq_trie_node[nk] = TrieNodeVal{mp, t.parent_root, t.parent, 1, false, {}};
+      vmq_trie[ek] = TrieEdgeVal{mp, t.parent_root, t.parent, t.word, t.child};
+    }
+  }
+
+  // add_complex_topic/4  vmq_reg_trie.erl:318-337
+  void add_complex_topic(const std::string& mp, const Words& topic, const NodeOrGroup& nog, bool wildcard) {
+    if (!wildcard) return;                                  // :318
+    std::string tk = mp_topic_key(mp, topic);
+    auto it = vmq_trie_topic.find(tk);
+    if (it == vmq_trie_topic.end()) {                       // :321-323
+      TopicVal v{mp, topic, 1, {}};
+      v.nodes.push_back({nog, 1});
+      vmq_trie_topic[tk] = v;
+    } else {                                                // :324-326
+      add_and_inc(it->second.nodes, nog);
+      it->second.total += 1;
+    }
+    std::string nk = node_id_key(mp, false, topic);
+    auto nit = vmq_trie_node.find(nk);
+    if (nit != vmq_trie_node.end() && nit->second.has_topic && nit->second.topic == topic) return;  // :330-331
+    for (auto& t : triples(topic)) trie_add_path(mp, t);   // :334
+    // :336 — a fresh #trie_node{} record: edge_count defaults to 0 (Q1).
+    vmq_trie_node[nk] = TrieNodeVal{mp, false, topic, 0, true, topic};
+  }
+
+  // trie_delete_path/2  vmq_reg_trie.erl:427-441
+  void trie_delete_path(const std::string& mp, std::vector<Triple> path_rev) {
+    for (auto& t : path_rev) {
+      vmq_trie.erase(edge_key(mp, t.parent_root, t.parent, t.word));   // :432
+      std::string nk = node_id_key(mp, t.parent_root, t.parent);
+      auto it = vmq_trie_node.find(nk);
+      if (it == vmq_trie_node.end()) return;                           // :439-440
+      if (it->second.edge_count == 1 && !it->second.has_topic) {       // :434-436
+        vmq_trie_node.erase(it);
+        continue;
+      }
+      it->second.edge_count -= 1;                                      // :437-438
+      return;
+    }
+  }
+
+  // trie_delete/2  vmq_reg_trie.erl:417-425
+  void trie_delete(const std::string& mp, const Words& topic) {
+    std::string nk = node_id_key(mp, false, topic);
+    auto it = vmq_trie_node.find(nk);
+    if (it != vmq_trie_node.end() && it->second.edge_count == 0) {
+      vmq_trie_node.erase(it);
+      auto tr = triples(topic);
+      std::reverse(tr.begin(), tr.end());
+      trie_delete_path(mp, tr);
+    }
+  }
+
+  // del_complex_topic/4  vmq_reg_trie.erl:385-397
+  void del_complex_topic(const std::string& mp, const Words& topic, const NodeOrGroup& nog, bool wildcard) {
+    if (!wildcard) return;
+    std::string tk = mp_topic_key(mp, topic);
+    auto it = vmq_trie_topic.find(tk);
+    if (it == vmq_trie_topic.end()) return;                 // :395-396
+    if (it->second.total > 1) {                             // :389-391
+      rem_and_dec(it->second.nodes, nog);
+      it->second.total -= 1;
+    } else if (it->second.total == 1) {                     // :392-394
+      vmq_trie_topic.erase(it);
+      trie_delete(mp, topic);
+    }
+  }
+
+  // insert_trie_subs/2  vmq_reg_trie.erl:448-464
+  void insert_trie_subs(const SubKey& key, const SubVal& val) {
+    std::string k = key.enc();
+    auto it = vmq_trie_subs.find(k);
+    if (it == vmq_trie_subs.end() || it->second.objs.empty()) {      // :451-452
+      vmq_trie_subs[k] = SubsEntry{key, {BagObj{false, val}}};
+      return;
+    }
+    auto& objs = it->second.objs;
+    if (objs.size() == 1 && !objs[0].fanout && objs[0].val == val) return;  // :453-455
+    if (objs.size() == 1 && objs[0].fanout) {                        // :456-457
+      vmq_trie_subs_fanout[k][val.enc()] = val;
+      fanout_keys[k] = key;
+      return;
+    }
+    // :458-463  [E1] -> move both to the fanout table, leave the marker
+    SubVal e1 = objs[0].val;
+    vmq_trie_subs.erase(it);
+    vmq_trie_subs[k] = SubsEntry{key, {BagObj{true, {}}}};
+    vmq_trie_subs_fanout[k][val.enc()] = val;
+    vmq_trie_subs_fanout[k][e1.enc()] = e1;
+    fanout_keys[k] = key;
+  }
+
+  // del_trie_subs/2  vmq_reg_trie.erl:472-496
+  void del_trie_subs(const SubKey& key, const SubVal& val) {
+    std::string k = key.enc();
+    auto it = vmq_trie_subs.find(k);
+    if (it == vmq_trie_subs.end() || it->second.objs.empty()) return;  // :474-476
+    if (it->second.objs.size() == 1 && it->second.objs[0].fanout) {    // :477-493
+      auto fit = vmq_trie_subs_fanout.find(k);
+      if (fit != vmq_trie_subs_fanout.end()) fit->second.erase(val.enc());
+      size_t left = (fit == vmq_trie_subs_fanout.end()) ? 0 : fit->second.size();
+      if (left == 1) {
+        SubVal e = fit->second.begin()->second;
+        vmq_trie_subs_fanout.erase(fit);
+        fanout_keys.erase(k);
+        it->second.objs.clear();                                       // delete_object {Key,fanout}
+        it->second.objs.push_back(BagObj{false, e});
+      }
+      // left >= 2: nothing.  left == 0 cannot happen.
+      return;
+    }
+    vmq_trie_subs.erase(it);                                           // :494-495 (Q3: value-blind)
+  }
+
+  // lookup_subs/1  vmq_reg_trie.erl:87-94
+  std::vector<SubVal> lookup_subs(const SubKey& key) const {
+    std::vector<SubVal> out;
+    auto it = vmq_trie_subs.find(key.enc());
+    if (it == vmq_trie_subs.end()) return out;
+    if (it->second.objs.size() == 1 && it->second.objs[0].fanout) {
+      auto fit = vmq_trie_subs_fanout.find(key.enc());
+      if (fit != vmq_trie_subs_fanout.end()) for (auto& kv : fit->second) out.push_back(kv.second);
+      return out;
+    }
+    for (auto& o : it->second.objs) out.push_back(o.val);
+    return out;
+  }
+
+  // add_remote_subscriber/3  vmq_reg_trie.erl:503-512
+  void add_remote_subscriber(const std::string& mp, const Words& topic, const std::string& node) {
+    std::string k = mp_topic_key(mp, topic);
+    auto it = vmq_trie_remote_subs.find(k);
+    if (it == vmq_trie_remote_subs.end()) {
+      RemoteVal v{mp, topic, {}};
+      v.nodes.push_back({node, 1});
+      vmq_trie_remote_subs[k] = v;
+    } else {
+      add_and_inc(it->second.nodes, node);
+    }
+  }
+  // del_remote_subscriber/3  vmq_reg_trie.erl:527-539
+  void del_remote_subscriber(const std::string& mp, const Words& topic, const std::string& node) {
+    std::string k = mp_topic_key(mp, topic);
+    auto it = vmq_trie_remote_subs.find(k);
+    if (it == vmq_trie_remote_subs.end()) return;
+    rem_and_dec(it->second.nodes, node);
+    if (it->second.nodes.empty()) vmq_trie_remote_subs.erase(it);
+  }
+
+  // handle_add_event/2  vmq_reg_trie.erl:253-264  (also initialize_trie/2 :305-316)
+  int handle_add(const std::string& mp, const std::string& client, const Words& topic,
+                 const std::string& subinfo, const std::string& node) {
+    if (!topic.empty() && topic[0] == "$share" && topic.size() >= 2) {  // :253-256
+      if (topic.size() < 3) return -1;  // triples([]) has no clause in the reference
+      Words t(topic.begin() + 2, topic.end());
+      NodeOrGroup g{true, node, topic[1]};
+      add_complex_topic(mp, t, g, true);
+      SubKey key{true, mp, topic[1], t};                                // add_subscriber_group :443-446
+      SubVal val{true, node, topic[1], mp, client, subinfo};
+      insert_trie_subs(key, val);
+      return 0;
+    }
+    NodeOrGroup n{false, node, {}};
+    add_complex_topic(mp, topic, n, contains_wildcard(topic));
+    if (node == self_node) {                                            // :257-260
+      insert_trie_subs(SubKey{false, mp, {}, topic}, SubVal{false, {}, {}, mp, client, subinfo});  // :498-501
+    } else {                                                            // :261-264
+      add_remote_subscriber(mp, topic, node);
+    }
+    return 0;
+  }
+
+  // handle_delete_event/2  vmq_reg_trie.erl:266-277
+  int handle_delete(const std::string& mp, const std::string& client, const Words& topic,
+                    const std::string& subinfo, const std::string& node) {
+    if (!topic.empty() && topic[0] == "$share" && topic.size() >= 2) {
+      if (topic.size() < 3) return -1;
+      Words t(topic.begin() + 2, topic.end());
+      NodeOrGroup g{true, node, topic[1]};
+      del_complex_topic(mp, t, g, true);
+      del_trie_subs(SubKey{true, mp, topic[1], t}, SubVal{true, node, topic[1], mp, client, subinfo});  // :467-470
+      return 0;
+    }
+    NodeOrGroup n{false, node, {}};
+    del_complex_topic(mp, topic, n, contains_wildcard(topic));
+    if (node == self_node) {
+      del_trie_subs(SubKey{false, mp, {}, topic}, SubVal{false, {}, {}, mp, client, subinfo});  // :522-525
+    } else {
+      del_remote_subscriber(mp, topic, node);
+    }
+    return 0;
+  }
+
+  // ------------------------------------------------------------ matching
+  // trie_match/2,4 and 'trie_match_#'/2  vmq_reg_trie.erl:358-383
+  void trie_match_hash(const std::string& mp, bool root, const Words& node, std::vector<const TrieNodeVal*>& acc, Counters& c) const {
+    c.s++;  // ets:lookup(vmq_trie, #trie_edge{node_id=NodeId, word= <<"#">>})  :378
+    auto it = vmq_trie.find(edge_key(mp, root, node, "#"));
+    if (it == vmq_trie.end()) return;
+    c.s++;  // ets:lookup(vmq_trie_node, {MP, ChildId})  :380
+    auto nit = vmq_trie_node.find(node_id_key(mp, false, it->second.child));
+    if (nit != vmq_trie_node.end()) acc.push_back(&nit->second);
+  }
+  void trie_match(const std::string& mp, bool root, const Words& node, const Words& words, size_t i,
+                  std::vector<const TrieNodeVal*>& acc, Counters& c) const {
+    if (i == words.size()) {                                         // :361-363
+      c.s++;
+      auto nit = vmq_trie_node.find(node_id_key(mp, root, node));
+      if (nit != vmq_trie_node.end()) acc.push_back(&nit->second);
+      trie_match_hash(mp, root, node, acc, c);
+      return;
+    }
+    trie_match_hash(mp, root, node, acc, c);                        // :375 (fold init acc)
+    const std::string plus = "+";
+    for (const std::string* w : {&words[i], &plus}) {                // :366-375
+      c.s++;
+      auto it = vmq_trie.find(edge_key(mp, root, node, *w));
+      if (it != vmq_trie.end()) trie_match(mp, false, it->second.child, words, i + 1, acc, c);
+    }
+  }
+
+  // match/2,4 and match_/3  vmq_reg_trie.erl:279-303
+  void match(const std::string& mp, const Words& topic, std::vector<std::pair<Words, NodeOrGroup>>& out, Counters& c) const {
+    std::vector<const TrieNodeVal*> nodes;
+    trie_match(mp, true, {}, topic, 0, nodes, c);
+    bool dollar = !topic.empty() && !topic[0].empty() && topic[0][0] == '$';
+    for (auto* n : nodes) {
+      if (!n->has_topic) continue;                                   // :297-298
+      if (dollar && ((n->topic.size() == 1 && n->topic[0] == "#") ||
+                     (!n->topic.empty() && n->topic[0] == "+")))
+        continue;                                                    // :285-288 (MQTT-4.7.2-1)
+      c.s++;
+      auto it = vmq_trie_topic.find(mp_topic_key(mp, n->topic));     // :291
+      if (it == vmq_trie_topic.end()) continue;
+      for (auto& e : it->second.nodes) out.push_back({n->topic, e.first});  // match_/3 :301-303
+    }
+  }
+
+  // fold/4, fold_/5, fold__/4  vmq_reg_trie.erl:59-98
+  void fold(const std::string& mp, const Words& topic, std::vector<Emission>& out, Counters& c) const {
+    std::vector<std::pair<Words, NodeOrGroup>> cands;
+    cands.push_back({topic, NodeOrGroup{false, self_node, {}}});    // :62
+    match(mp, topic, cands, c);                                      // :64
+    c.s++;                                                           // get_remote_subscribers :514-520
+    auto rit = vmq_trie_remote_subs.find(mp_topic_key(mp, topic));
+    if (rit != vmq_trie_remote_subs.end())
+      for (auto& e : rit->second.nodes) cands.push_back({topic, NodeOrGroup{false, e.first, {}}});
+    std::vector<std::string> remotes;
+    for (auto& cd : cands) {
+      const NodeOrGroup& nog = cd.second;
+      if (nog.is_group) {                                            // :68-72
+        c.s++;
+        for (auto& v : lookup_subs(SubKey{true, mp, nog.group, cd.first})) out.push_back(Emission{2, v, {}});
+      } else if (nog.node == self_node) {                            // :73-77
+        c.s++;
+        for (auto& v : lookup_subs(SubKey{false, mp, {}, cd.first})) out.push_back(Emission{1, v, {}});
+      } else {                                                       // :78-84
+        if (std::find(remotes.begin(), remotes.end(), nog.node) != remotes.end()) continue;
+        out.push_back(Emission{3, {}, nog.node});
+        remotes.push_back(nog.node);
+      }
+    }
+  }
+
+  // ------------------------------------------------------------- dump
+  std::string dump() const {
+    std::vector<std::string> lines;
+    auto nid = [](const std::string& mp, bool root, const Words& p) {
+      return esc(mp) + "|" + (root ? std::string("root") : show_path(p));
+    };
+    for (auto& kv : vmq_trie) {
+      auto& e = kv.second;
+      lines.push_back("trie " + nid(e.mp, e.parent_root, e.parent) + " " + esc(e.word) + " -> " + show_path(e.child));
+    }
+    for (auto& kv : vmq_trie_node) {
+      auto& n = kv.second;
+      lines.push_back("node " + nid(n.mp, n.root, n.path) + " ec=" + std::to_string(n.edge_count) +
+                      " topic=" + (n.has_topic ? show_path(n.topic) : std::string("undefined")));
+    }
+    for (auto& kv : vmq_trie_topic) {
+      auto& t = kv.second;
+      std::vector<std::string> ns;
+      for (auto& e : t.nodes) ns.push_back(e.first.show() + ":" + std::to_string(e.second));
+      std::sort(ns.begin(), ns.end());
+      std::string l = "topic " + esc(t.mp) + "|" + show_path(t.topic) + " total=" + std::to_string(t.total) + " [";
+      for (size_t i = 0; i < ns.size(); i++) { if (i) l += ","; l += ns[i]; }
+      lines.push_back(l + "]");
+    }
+    for (auto& kv : vmq_trie_subs) {
+      for (auto& o : kv.second.objs)
+        lines.push_back("subs " + kv.second.key.show() + " " + (o.fanout ? std::string("fanout") : o.val.show()));
+    }
+    for (auto& kv : vmq_trie_subs_fanout) {
+      auto kit = fanout_keys.find(kv.first);
+      for (auto& v : kv.second) lines.push_back("fanout " + kit->second.show() + " " + v.second.show());
+    }
+    for (auto& kv : vmq_trie_remote_subs) {
+      auto& r = kv.second;
+      std::vector<std::string> ns;
+      for (auto& e : r.nodes) ns.push_back(esc(e.first) + ":" + std::to_string(e.second));
+      std::sort(ns.begin(), ns.end());
+      std::string l = "remote " + esc(r.mp) + "|" + show_path(r.topic) + " [";
+      for (size_t i = 0; i < ns.size(); i++) { if (i) l += ","; l += ns[i]; }
+      lines.push_back(l + "]");
+    }
+    std::sort(lines.begin(), lines.end());
+    std::string out;
+    for (auto& l : lines) { out += l; out += '\n'; }
+    return out;
+  }
+};
+
+// ----------------------------------------------------- vmq_subscriber
+// subs() = [{Node, CleanSession, [{Topic, SubInfo}]}]   vmq_subscriber.erl:35-38
+struct NodeSubs { std::string node; bool clean; std::vector<std::pair<Words, std::string>> subs; };
+using Subs = std::vector<NodeSubs>;
+using Changes = std::vector<std::pair<std::string, std::vector<std::pair<Words, std::string>>>>;
+
+bool node_subs_eq(const NodeSubs& a, const NodeSubs& b) {
+  return a.node == b.node && a.clean == b.clean && a.subs == b.subs;
+}
+
+// Erlang `--`: remove the first occurrence of each element of B from A.
+std::vector<std::pair<Words, std::string>> list_sub(std::vector<std::pair<Words, std::string>> a,
+                                                     const std::vector<std::pair<Words, std::string>>& b) {
+  for (auto& x : b) {
+    auto it = std::find(a.begin(), a.end(), x);
+    if (it != a.end()) a.erase(it);
+  }
+  return a;
+}
+
+// subtract/2,3  vmq_subscriber.erl:151-169.  Node names are atoms: Erlang
+// compares atoms by their text, which std::string's operator> matches for the
+// ASCII node names used here.
+Changes subtract(const Subs& s1, const Subs& s2) {
+  Changes acc;
+  size_t i = 0, j = 0;
+  while (i < s1.size()) {
+    if (j < s2.size() && node_subs_eq(s1[i], s2[j])) { i++; j++; continue; }           // :154-156
+    if (j < s2.size() && s1[i].node == s2[j].node) {                                    // :157-164
+      auto d = list_sub(s1[i].subs, s2[j].subs);
+      if (!d.empty()) acc.push_back({s1[i].node, d});
+      i++; j++; continue;
+    }
+    if (j < s2.size() && s1[i].node > s2[j].node) { j++; continue; }                    // :165-166
+    acc.push_back({s1[i].node, s1[i].subs}); i++;                                       // :167-168
+  }
+  return acc;                                                                           // :169
+}
+
+// ------------------------------------------------------- input decoding
+bool read_subs(Reader& r, int& tag, Subs& out) {
+  tag = r.u8();
+  out.clear();
+  if (tag == 0 || tag == 1) return !r.bad;   // undefined | '$deleted'
+  if (tag == 2) {
+    uint32_t n = r.u32();
+    for (uint32_t i = 0; i < n && !r.bad; i++) {
+      NodeSubs ns; ns.node = r.str(); ns.clean = r.u8() != 0;
+      uint32_t k = r.u32();
+      for (uint32_t q = 0; q < k && !r.bad; q++) { Words t = r.words(); std::string si = r.str(); ns.subs.push_back({t, si}); }
+      out.push_back(std::move(ns));
+    }
+    return !r.bad;
+  }
+  if (tag == 3) {
+    // v0 format [{Topic, QoS, Node}] — maybe_convert_v0/1,2 vmq_subscriber.erl:136-147:
+    // start from new(false) = [{node(), false, []}] and add/3 each entry.
+    return false;  // handled by the caller (needs node()); see read_subs_v0
+  }
+  r.bad = true;
+  return false;
+}
+
+}  // namespace
+
+// ============================================================== C ABI
+extern "C" {
+
+struct oracle_t { Oracle o; std::string out; };
+
+oracle_t* oracle_new(const char* self_node) {
+  auto* t = new oracle_t();
+  t->o.self_node = self_node ? self_node : "nonode@nohost";
+  return t;
+}
+void oracle_free(oracle_t* t) { delete t; }
+const char* oracle_out(oracle_t* t, size_t* n) { *n = t->out.size(); return t->out.data(); }
+
+// vmq_subscriber:add/3  vmq_subscriber.erl:63-72 (used by the v0 conversion).
+// ukeymerge(1, ukeysort(1, New), Old): on equal topics the NEW entry wins.
+static void subscriber_add(Subs& subs, const Words& topic, const std::string& subinfo, const std::string& node) {
+  for (auto& ns : subs) {
+    if (ns.node == node) {
+      for (auto& s : ns.subs) if (s.first == topic) { s.second = subinfo; return; }
+      ns.subs.push_back({topic, subinfo});
+      std::stable_sort(ns.subs.begin(), ns.subs.end(), [](auto& a, auto& b) { return a.first < b.first; });
+      return;
+    }
+  }
+  // get_node_subs/2 :178-182 — an absent node defaults to CleanSession = true
+  subs.push_back(NodeSubs{node, true, {{topic, subinfo}}});
+  std::stable_sort(subs.begin(), subs.end(), [](auto& a, auto& b) { return a.node < b.node; });
+}
+
+// check_format/1 -> maybe_convert_v0/1,2  vmq_subscriber.erl:130-147.  Tag 3
+// carries the v0 list [{Topic, QoS, Node}]; it is folded into new(false).
+static bool read_any_subs(Reader& r, const std::string& self, int& tag, Subs& out) {
+  if (r.p >= r.e) { r.bad = true; return false; }
+  if (*r.p != 3) return read_subs(r, tag, out);
+  r.u8();
+  tag = 2;
+  out.clear();
+  out.push_back(NodeSubs{self, false, {}});   // new(false)  :43-48
+  uint32_t n = r.u32();
+  for (uint32_t i = 0; i < n && !r.bad; i++) {
+    Words topic = r.words(); std::string si = r.str(); std::string node = r.str();
+    subscriber_add(out, topic, si, node);
+  }
+  return !r.bad;
+}
+
+// Apply a stream of subscriber-store events.  Record types:
+//  1 {updated, {vmq,subscriber}, SubscriberId, Old, New}
+//  2 {deleted, {vmq,subscriber}, SubscriberId, Old}
+//  3 initialize_trie/2 tuple {MP, Topic, {SubscriberId, SubInfo, Node}}  (vmq_reg_trie.erl:305-316)
+// Returns the number of records applied, or -1 on malformed input.
+long oracle_apply(oracle_t* t, const uint8_t* buf, size_t n) {
+  Reader r{buf, buf + n};
+  long applied = 0;
+  Oracle& o = t->o;
+  while (r.p < r.e && !r.bad) {
+    uint8_t type = r.u8();
+    if (type == 3) {
+      std::string mp = r.str(), client = r.str();
+      Words topic = r.words();
+      std::string si = r.str(), node = r.str();
+      if (r.bad || o.handle_add(mp, client, topic, si, node) != 0) return -1;
+      applied++;
+      continue;
+    }
+    std::string mp = r.str(), client = r.str();
+    int tag_old = 0, tag_new = 0;
+    Subs olds, news;
+    if (!read_any_subs(r, o.self_node, tag_old, olds)) return -1;
+    if (type == 1 && !read_any_subs(r, o.self_node, tag_new, news)) return -1;
+    // vmq_subscriber_db:subscribe_db_events/0  vmq_subscriber_db.erl:56-71
+    if (type == 2) {
+      if (tag_old == 0 || tag_old == 1) { applied++; continue; }       // :59-61 ignore
+      // {delete, SubscriberId, Subs}: get_changes/1 vmq_subscriber.erl:50-52
+      for (auto& ns : olds)
+        for (auto& s : ns.subs)
+          if (o.handle_delete(mp, client, s.first, s.second, ns.node) != 0) return -1;
+    } else if (type == 1) {
+      if (tag_old == 0 || tag_old == 1) olds.clear();                  // :64-66
+      if (tag_new != 2) return -1;
+      // handle_event/2 vmq_reg_trie.erl:245-248; get_changes/2 vmq_subscriber.erl:54-58
+      Changes removed = subtract(olds, news);
+      Changes added = subtract(news, olds);
+      for (auto& c : removed)
+        for (auto& s : c.second)
+          if (o.handle_delete(mp, client, s.first, s.second, c.first) != 0) return -1;
+      for (auto& c : added)
+        for (auto& s : c.second)
+          if (o.handle_add(mp, client, s.first, s.second, c.first) != 0) return -1;
+    } else {
+      return -1;
+    }
+    applied++;
+  }
+  return r.bad ? -1 : applied;
+}
+
+// Fold a batch of publishes.  Input: u32 n; per publish: str MP, str ClientId,
+// words.  Output (oracle_out): u32 n; per publish: u32 S_p, u32 R_p, u32 L_p,
+// u32 nemit; per emission u8 kind + strings (see tests/oracle harness).
+long oracle_fold(oracle_t* t, const uint8_t* buf, size_t n) {
+  Reader r{buf, buf + n};
+  uint32_t np = r.u32();
+  std::string& out = t->out;
+  out.clear();
+  put_u32(out, np);
+  std::vector<Emission> em;
+  for (uint32_t i = 0; i < np && !r.bad; i++) {
+    std::string mp = r.str(), client = r.str();
+    Words topic = r.words();
+    em.clear();
+    Counters c;
+    t->o.fold(mp, topic, em, c);
+    put_u32(out, (uint32_t)c.s);
+    put_u32(out, (uint32_t)em.size());
+    put_u32(out, (uint32_t)topic.size());
+    put_u32(out, (uint32_t)em.size());
+    for (auto& e : em) {
+      out += (char)e.kind;
+      if (e.kind == 1) { put_str(out, e.val.sub_mp); put_str(out, e.val.client); put_str(out, e.val.subinfo); }
+      else if (e.kind == 2) { put_str(out, e.val.node); put_str(out, e.val.group); put_str(out, e.val.sub_mp);
+                              put_str(out, e.val.client); put_str(out, e.val.subinfo); }
+      else put_str(out, e.node);
+    }
+  }
+  return r.bad ? -1 : (long)np;
+}
+
+// Timed fold for the CPU baseline: folds the batch `reps` times on `threads`
+// threads (publishes partitioned, tables shared read-only) and returns the
+// wall time in ns; *emissions receives the total emission count of one rep.
+long long oracle_fold_timed(oracle_t* t, const uint8_t* buf, size_t n, int reps, int threads,
+                            unsigned long long* emissions) {
+  Reader r{buf, buf + n};
+  uint32_t np = r.u32();
+  struct P { std::string mp; Words topic; };
+  std::vector<P> pubs(np);
+  for (uint32_t i = 0; i < np && !r.bad; i++) { pubs[i].mp = r.str(); r.str(); pubs[i].topic = r.words(); }
+  if (r.bad) return -1;
+  if (threads < 1) threads = 1;
+  std::vector<unsigned long long> cnt(threads, 0);
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  for (int w = 0; w < threads; w++) {
+    th.emplace_back([&, w]() {
+      std::vector<Emission> em;
+      unsigned long long local = 0;
+      size_t lo = (size_t)np * w / threads, hi = (size_t)np * (w + 1) / threads;
+      for (int rep = 0; rep < reps; rep++)
+        for (size_t i = lo; i < hi; i++) {
+          em.clear();
+          Counters c;
+          t->o.fold(pubs[i].mp, pubs[i].topic, em, c);
+          if (rep == 0) local += em.size();
+        }
+      cnt[w] = local;
+    });
+  }
+  for (auto& x : th) x.join();
+  auto t1 = std::chrono::steady_clock::now();
+  unsigned long long tot = 0;
+  for (auto v : cnt) tot += v;
+  if (emissions) *emissions = tot;
+  return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+}
+
+const char* oracle_dump(oracle_t* t, size_t* n) { t->out = t->o.dump(); *n = t->out.size(); return t->out.data(); }
+
+// stats/0 counts  vmq_reg_trie.erl:101-112 (the ETS sizes; memory is not restated)
+void oracle_sizes(oracle_t* t, uint64_t* out7) {
+  auto& o = t->o;
+  out7[0] = o.vmq_trie.size();
+  out7[1] = o.vmq_trie_node.size();
+  out7[2] = o.vmq_trie_topic.size();
+  uint64_t bag = 0; for (auto& kv : o.vmq_trie_subs) bag += kv.second.objs.size();
+  out7[3] = bag;
+  uint64_t fan = 0; for (auto& kv : o.vmq_trie_subs_fanout) fan += kv.second.size();
+  out7[4] = fan;
+  out7[5] = o.vmq_trie_remote_subs.size();
+  out7[6] = bag + o.vmq_trie_remote_subs.size();   // NrOfSubs + NrOfRemoteSubs
+}
+
+// validate_topic/2 (vmq_topic.erl:82-133).  Output: u32 nwords + words.
+int oracle_validate_topic(oracle_t* t, int type, const uint8_t* topic, size_t n) {
+  Words w;
+  int rc = validate_topic(type, std::string(reinterpret_cast<const char*>(topic), n), w);
+  t->out.clear();
+  if (rc == V_OK) t->out = enc_words(w);
+  return rc;
+}
+
+// vmq_topic:match/2 + the MQTT-4.7.2-1 rule of vmq_reg_trie.erl:283-288.
+int oracle_naive_match(const uint8_t* buf, size_t n) {
+  Reader r{buf, buf + n};
+  Words topic = r.words(), filt = r.words();
+  if (r.bad) return -1;
+  if (!topic.empty() && !topic[0].empty() && topic[0][0] == '$' && !filt.empty() &&
+      (filt[0] == "+" || (filt.size() == 1 && filt[0] == "#")))
+    return 0;
+  return naive_match(topic, 0, filt, 0) ? 1 : 0;
+}
+
+int oracle_contains_wildcard(const uint8_t* buf, size_t n) {
+  Reader r{buf, buf + n};
+  Words w = r.words();
+  return r.bad ? -1 : (contains_wildcard(w) ? 1 : 0);
+}
+
+}  // extern "C"
+
+// vmq_subscriber:get_changes/2 (vmq_subscriber.erl:54-58) for the eunit KATs.
+// Input: subs Old, subs New (as in oracle_apply).  Output: Removed then Added,
+// each u32 nnodes; per node str node, u32 n; per entry words + str subinfo.
+extern "C" int oracle_get_changes(oracle_t* t, const uint8_t* buf, size_t n) {
+  Reader r{buf, buf + n};
+  int ta = 0, tb = 0;
+  Subs a, b;
+  if (!read_any_subs(r, t->o.self_node, ta, a) || !read_any_subs(r, t->o.self_node, tb, b)) return -1;
+  t->out.clear();
+  for (const Changes& c : {subtract(a, b), subtract(b, a)}) {
+    put_u32(t->out, (uint32_t)c.size());
+    for (auto& nc : c) {
+      put_str(t->out, nc.first);
+      put_u32(t->out, (uint32_t)nc.second.size());
+      for (auto& s : nc.second) { t->out += enc_words(s.first); put_str(t->out, s.second); }
+    }
+  }
+  return 0;
+}
