@@ -1,0 +1,230 @@
+/*
+ * vmqg.h — C ABI of libvmqgpu, the MI355X-native subscription matcher that
+ * sits behind VerneMQ's `vmq_reg_view` behaviour.
+ *
+ * Drop-in boundary (all paths relative to the reference checkout):
+ *   apps/vmq_server/src/vmq_reg_view.erl:20-27   -callback fold/4, fold/5
+ *   apps/vmq_server/src/vmq_reg_trie.erl:59-98    fold/4 (what vmqg_match_* replaces)
+ *   apps/vmq_server/src/vmq_reg_trie.erl:240-277  handle_event / handle_add_event /
+ *                                                 handle_delete_event (what vmqg_apply_ops replaces)
+ *   apps/vmq_server/src/vmq_reg_trie.erl:305-316  initialize_trie/2 (bulk vmqg_apply_ops)
+ *   apps/vmq_server/src/vmq_reg_trie.erl:101-118  stats/0 (vmqg_stats)
+ *
+ * The Erlang side (a `vmq_reg_gpu_view` gen_server + erl_nif shim, see
+ * INTEGRATION.md) keeps every Erlang term <-> integer id table: mountpoints,
+ * nodes, SubscriberIds and SubInfos are opaque uint32 ids to this library.
+ * Topic words are interned by the library's own dictionary (vmqg_intern_words)
+ * so that subscription filters and publish topics share one id space.
+ *
+ * Conventions: every call returns 0 (VMQG_OK) or a negative VMQG_E_* code; no
+ * exception crosses the ABI.  The caller owns every buffer; the library never
+ * keeps a caller pointer after a call returns.  One context is not
+ * re-entrant (the NIF batcher serialises calls); separate contexts (one per
+ * GPU) are independent.  vmqg_apply_ops and the match calls on one context
+ * are ordered on the context's stream, so a match batch observes either all
+ * or none of an apply batch (epoch semantics).
+ */
+#ifndef VMQG_H
+#define VMQG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VMQG_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+#define VMQG_OK 0
+#define VMQG_E_INVAL (-1)     /* malformed argument / op                      */
+#define VMQG_E_OVERFLOW (-2)  /* output buffer too small: *out_n = required    */
+#define VMQG_E_NOMEM (-3)     /* host or device allocation failed             */
+#define VMQG_E_DEVICE (-4)    /* no device / HIP runtime error                */
+#define VMQG_E_FRONTIER (-5)  /* a publish exceeded the device scratch limits */
+#define VMQG_E_LIMIT (-6)     /* a configured limit (nodes, mountpoints, ids)  */
+#define VMQG_E_STATE (-7)     /* call not valid for this context kind          */
+
+/* ---- reserved ids ---------------------------------------------------- */
+#define VMQG_WORD_PLUS 0u       /* <<"+">>      */
+#define VMQG_WORD_HASH 1u       /* <<"#">>      */
+#define VMQG_WORD_SHARE 2u      /* <<"$share">> */
+#define VMQG_WORD_UNKNOWN 0xFFFFFFFFu  /* publish word never seen in a filter */
+#define VMQG_NONE 0xFFFFFFFFu
+
+#define VMQG_MAX_NODES 64u      /* cluster nodes addressable in a remote mask  */
+
+/* ---- configuration --------------------------------------------------- */
+#define VMQG_CFG_REPLICA 1u     /* no host engine: device tables arrive as
+                                   images/patches from a primary context */
+
+typedef struct vmqg_config {
+  int32_t device;            /* HIP device ordinal; -1 = host engine only     */
+  uint32_t local_node;       /* node id that plays node() (< max_nodes)       */
+  uint32_t max_nodes;        /* <= VMQG_MAX_NODES                             */
+  uint32_t max_mountpoints;  /* mountpoint ids are dense in [0, max)          */
+  uint32_t flags;            /* VMQG_CFG_*                                    */
+  uint32_t reserved;
+  uint64_t hint_edges;       /* sizing hints; 0 = small defaults, tables grow */
+  uint64_t hint_paths;
+  uint64_t hint_keys;
+  uint64_t hint_records;
+  uint64_t hint_exact;
+} vmqg_config;
+
+/* ---- subscription deltas --------------------------------------------- */
+#define VMQG_OP_ADD 1u   /* handle_add_event/2     vmq_reg_trie.erl:253-264 */
+#define VMQG_OP_DEL 2u   /* handle_delete_event/2  vmq_reg_trie.erl:266-277 */
+
+/* One {Topic, SubInfo, Node} of a vmq_subscriber change list, in the order
+ * vmq_subscriber:fold/3 visits it (vmq_subscriber.erl:184-196): all deletes
+ * of an event before its adds (vmq_reg_trie.erl:245-248).  The topic is the
+ * word-id list exactly as subscribed, "$share"/Group prefix included. */
+typedef struct vmqg_op {
+  uint32_t kind;        /* VMQG_OP_ADD | VMQG_OP_DEL                        */
+  uint32_t mountpoint;  /* MP of the SubscriberId                           */
+  uint32_t word_off;    /* index of the first word id in `words`            */
+  uint32_t nwords;      /* >= 1                                             */
+  uint32_t node;        /* node the subscription lives on                   */
+  uint32_t subscriber;  /* SubscriberId id (opaque)                         */
+  uint32_t subinfo;     /* SubInfo id (opaque)                              */
+  uint32_t reserved;
+} vmqg_op;
+
+/* ---- publishes and matches ------------------------------------------- */
+#define VMQG_PUB_DOLLAR 1u   /* first topic word starts with '$' (MQTT-4.7.2-1) */
+
+typedef struct vmqg_pub {
+  uint32_t mountpoint;
+  uint32_t word_off;    /* index of the first word id in `words`            */
+  uint32_t nwords;      /* >= 1                                             */
+  uint32_t flags;       /* VMQG_PUB_*                                       */
+} vmqg_pub;
+
+#define VMQG_EMIT_LOCAL 1u   /* {SubscriberId, SubInfo}               */
+#define VMQG_EMIT_GROUP 2u   /* {Node, Group, SubscriberId, SubInfo}  */
+#define VMQG_EMIT_REMOTE 3u  /* Node                                  */
+
+/* One FoldFun argument (vmq_reg_trie.erl:83, :97).  16 bytes. */
+typedef struct vmqg_emit {
+  uint32_t kind_node;   /* kind << 24 | node                               */
+  uint32_t group;       /* group word id (kind 2) else VMQG_NONE           */
+  uint32_t subscriber;  /* kinds 1, 2                                      */
+  uint32_t subinfo;     /* kinds 1, 2                                      */
+} vmqg_emit;
+
+typedef struct vmqg_stats_s {
+  uint64_t subs;            /* NrOfSubs + NrOfRemoteSubs (vmq_reg_trie.erl:101-112) */
+  uint64_t device_bytes;    /* device arena size (router_memory analogue)   */
+  uint64_t trie_edges;      /* |vmq_trie|                                   */
+  uint64_t trie_nodes;      /* |vmq_trie_node|                              */
+  uint64_t trie_topics;     /* |vmq_trie_topic|                             */
+  uint64_t subs_objects;    /* |vmq_trie_subs|                              */
+  uint64_t fanout_objects;  /* |vmq_trie_subs_fanout|                       */
+  uint64_t remote_keys;     /* |vmq_trie_remote_subs|                       */
+  uint64_t epoch;           /* apply batches applied                        */
+  uint64_t rebuilds;        /* full device-image rebuilds                   */
+  uint64_t paths;           /* interned trie paths (host)                   */
+  uint64_t words;           /* interned words                               */
+} vmqg_stats_t;
+
+/* ---- lifecycle ------------------------------------------------------- */
+typedef struct vmqg_ctx vmqg_ctx;
+
+int vmqg_abi_version(void);
+
+/* Creates a context.  With cfg->device >= 0 the device arena is allocated on
+ * that HIP device; device = -1 gives a host-engine-only context (tables are
+ * maintained and can be dumped, every match call returns VMQG_E_DEVICE).
+ * *err receives the status when NULL is returned.
+ *   Replaces: vmq_reg_trie:start_link/0 + init/1 (vmq_reg_trie.erl:56-57, 135-151). */
+vmqg_ctx* vmqg_create(const vmqg_config* cfg, int* err);
+void vmqg_destroy(vmqg_ctx* ctx);
+
+/* ---- words ------------------------------------------------------------ */
+/* Interns n words (word i = bytes[offs[i] .. offs[i+1])).  create != 0 adds
+ * unseen words (subscription filters); create == 0 maps unseen words to
+ * VMQG_WORD_UNKNOWN (publish topics).  "+", "#", "$share" always map to the
+ * reserved ids. */
+int vmqg_intern_words(vmqg_ctx* ctx, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
+                      int create, uint32_t* ids_out);
+
+/* Splits a publish topic by vmq_topic:validate_topic(publish, T)
+ * (vmq_topic.erl:82-112) and looks its words up.  Writes at most cap word ids
+ * to words_out and fills *pub (word_off = 0, flags = VMQG_PUB_DOLLAR when the
+ * first word starts with '$').  Returns VMQG_E_INVAL for a topic the
+ * reference rejects. */
+int vmqg_prepare_publish(vmqg_ctx* ctx, uint32_t mountpoint, const uint8_t* topic, size_t len,
+                         uint32_t* words_out, uint32_t cap, vmqg_pub* pub);
+
+/* ---- deltas --------------------------------------------------------- */
+/* Applies a batch of subscribe/unsubscribe ops with the exact semantics of
+ * vmq_reg_trie's event handlers, including the reference's structural
+ * behaviour under churn, then pushes the resulting
+ * table patches to the device (stream-ordered before later matches).  The
+ * batch is validated first; an invalid op rejects the whole batch unchanged.
+ *   Replaces: handle_event/2 (vmq_reg_trie.erl:240-277), initialize_trie/2 (:305-316). */
+int vmqg_apply_ops(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words,
+                   size_t nwords, uint64_t* epoch_out);
+
+/* ---- matching -------------------------------------------------------- */
+/* Host-buffer match of npub publishes.  offsets[0..npub] receives the
+ * exclusive prefix of per-publish emission counts (offsets[npub] = total);
+ * publish i's emissions are out[offsets[i] .. offsets[i+1]).  If total >
+ * out_cap, returns VMQG_E_OVERFLOW with *out_n = total (offsets valid).
+ * Synchronous.  Emission multiset per publish == vmq_reg_trie:fold/4's.
+ *   Replaces: vmq_reg_trie:fold/4 (vmq_reg_trie.erl:59-98) for a batch. */
+int vmqg_match_batch(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const uint32_t* words,
+                     size_t nwords, vmqg_emit* out, size_t out_cap, size_t* out_n,
+                     uint64_t* offsets);
+
+/* Device-buffer match: every pointer is device memory of the context's
+ * device; work is enqueued on `stream` (a hipStream_t, NULL = the context's
+ * own stream) and the call returns without synchronising.  d_offsets needs
+ * npub + 1 entries.  Overflow / scratch errors are latched on the device and
+ * reported by the next vmqg_match_status(). */
+int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub,
+                      const uint32_t* d_words, vmqg_emit* d_out, uint64_t out_cap,
+                      uint64_t* d_offsets, void* stream);
+
+/* Synchronises `stream` and returns the latched status of the previous
+ * vmqg_match_device calls (VMQG_OK, VMQG_E_OVERFLOW, VMQG_E_FRONTIER),
+ * clearing it. */
+int vmqg_match_status(vmqg_ctx* ctx, void* stream);
+
+/* ---- introspection --------------------------------------------------- */
+int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out);
+
+/* Canonical text dump of the six logical tables (one line per ETS object,
+ * sorted; ids printed as mp#N / node#N / sub#N / info#N).  *text is owned by
+ * the context and valid until the next call on it. */
+int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
+
+/* Average duration (ns) of the dominant match kernel over the last
+ * vmqg_match_device calls made with timing enabled (vmqg_set_timing). */
+int vmqg_set_timing(vmqg_ctx* ctx, int enable);
+int vmqg_kernel_times(vmqg_ctx* ctx, double* count_ns, double* emit_ns, uint64_t* launches);
+
+/* ---- replication (one primary, N device replicas) --------------------- */
+/* Device arena of the context: pointer, byte size and the layout descriptor
+ * (opaque, VMQG_LAYOUT_BYTES long) a replica needs to interpret it. */
+#define VMQG_LAYOUT_BYTES 256
+int vmqg_arena(vmqg_ctx* ctx, void** d_ptr, uint64_t* bytes, uint8_t* layout_out);
+
+/* Replica side: adopt `layout` and copy a full arena image from device memory
+ * d_src (same device as ctx) on `stream`. */
+int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, void* stream);
+
+/* Patches produced by the last vmqg_apply_ops on a primary: host bytes
+ * (records of 24 bytes) valid until the next apply; *full_image = 1 when the
+ * apply re-laid out the arena (replicas must reload the full image instead). */
+int vmqg_last_patches(vmqg_ctx* ctx, const void** host_ptr, uint64_t* bytes, int* full_image);
+
+/* Replica side: apply patch records already in device memory on `stream`. */
+int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VMQG_H */

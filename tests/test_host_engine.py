@@ -1,0 +1,92 @@
+"""CPU parity of the delta handling: the product's host engine (libvmqgpu,
+host-only context) and the oracle must hold the same six logical tables —
+object for object — after every event, on the golden scenarios and under
+random churn that exercises Q1-Q3.  No GPU needed (no match calls)."""
+import pytest
+
+from oracle import oracle as O
+from tests import harness as H
+from tests import scenarios as S
+
+SCEN_FILES = ["pattern_matching.json", "upgrade.json", "overlapping_subscriptions.json",
+              "dollar_topics.json", "shared_subscriptions.json", "quirks.json"]
+
+
+def _scen():
+    for f in SCEN_FILES:
+        for sc in S.load(f)["scenarios"]:
+            yield pytest.param(sc, id="%s:%s" % (f, sc["name"]))
+
+
+def _compare(prod, orc, ctx):
+    a = H.normalize_product_dump(prod.view)
+    b = H.normalize_oracle_dump(orc)
+    if a != b:
+        sa, sb = set(a), set(b)
+        raise AssertionError("%s\nonly product: %s\nonly oracle: %s" % (ctx, sorted(sa - sb)[:20],
+                                                                       sorted(sb - sa)[:20]))
+    ps = prod.view.stats_raw()
+    osz = orc.sizes()
+    assert ps["subs"] == osz["stats_subs"], ctx
+    assert ps["trie_edges"] == osz["trie"] and ps["trie_nodes"] == osz["trie_node"], ctx
+    assert ps["trie_topics"] == osz["trie_topic"] and ps["fanout_objects"] == osz["trie_subs_fanout"], ctx
+
+
+@pytest.mark.parametrize("scen", list(_scen()))
+def test_golden_event_streams_same_tables(scen):
+    prod = H.ProductDriver(scen["node"], device=-1)
+    orc = O.TrieOracle(scen["node"])
+    for i, step in enumerate(scen["steps"]):
+        if "event" in step:
+            ev = S.event(step["event"])
+            prod.apply([ev])
+            orc.apply([ev])
+            _compare(prod, orc, "%s step %d" % (scen["name"], i))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_churn_same_tables(seed):
+    wl = H.ChurnWorkload(seed)
+    prod = H.ProductDriver(wl.self_node, device=-1)
+    orc = O.TrieOracle(wl.self_node)
+    for step in range(300):
+        ev = wl.event()
+        prod.apply([ev])
+        orc.apply([ev])
+        if step % 10 == 9:
+            _compare(prod, orc, "seed %d step %d" % (seed, step))
+    _compare(prod, orc, "seed %d end" % seed)
+
+
+def test_batched_events_equal_sequential():
+    """One apply batch of many events == the same events one by one."""
+    wl = H.ChurnWorkload(99)
+    evs = [wl.event() for _ in range(400)]
+    a = H.ProductDriver(wl.self_node, device=-1)
+    a.apply(evs)
+    orc = O.TrieOracle(wl.self_node)
+    orc.apply(evs)
+    _compare(a, orc, "batched")
+
+
+def test_invalid_share_op_rejects_batch():
+    from vernemq_amd import _lib
+    prod = H.ProductDriver("n@h", device=-1)
+    with pytest.raises(_lib.VmqgError) as ei:
+        prod.view.apply_ops([("add", ("", b"x"), (b"a",), 0, "n@h"),
+                             ("add", ("", b"x"), (b"$share", b"g"), 0, "n@h")])
+    assert ei.value.rc == _lib.E_INVAL
+    assert prod.view.stats_raw()["subs"] == 0
+
+
+def test_bulk_growth_rebuilds():
+    """Tables grow past their initial capacity (full re-layout) and stay equal."""
+    prod = H.ProductDriver("n@h", device=-1)
+    orc = O.TrieOracle("n@h")
+    evs = [("updated", ("", b"c%d" % i), None,
+            [("n@h", True, [((b"dev", b"%d" % i, b"+", b"#"), i % 3), ((b"x%d" % (i % 97),), 1)])])
+           for i in range(6000)]
+    prod.apply(evs)
+    orc.apply(evs)
+    assert prod.view.stats_raw()["rebuilds"] >= 2
+    _compare(prod, orc, "bulk")

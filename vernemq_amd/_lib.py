@@ -1,0 +1,139 @@
+"""ctypes binding of libvmqgpu (include/vmqg.h) and its in-tree build.
+
+The library is the product: there is no Python or CPU fallback for matching.
+If ``libvmqgpu.so`` is missing, :func:`lib` raises ``ImportError`` (call
+:func:`build` first, or ``python -c "import __graft_entry__ as g; g.build()"``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libvmqgpu.so")
+HEADER = os.path.join(ROOT, "include", "vmqg.h")
+SOURCES = [os.path.join(HERE, "csrc", f) for f in
+           ("vmqg_engine.cpp", "vmqg_abi.cpp", "vmqg_kernels.hip")]
+DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in
+                  ("vmqg_common.h", "vmqg_engine.h", "vmqg_kernels.h")] + [HEADER]
+
+# ---- status codes / constants (vmqg.h)
+OK, E_INVAL, E_OVERFLOW, E_NOMEM, E_DEVICE, E_FRONTIER, E_LIMIT, E_STATE = 0, -1, -2, -3, -4, -5, -6, -7
+ERRORS = {E_INVAL: "VMQG_E_INVAL", E_OVERFLOW: "VMQG_E_OVERFLOW", E_NOMEM: "VMQG_E_NOMEM",
+          E_DEVICE: "VMQG_E_DEVICE", E_FRONTIER: "VMQG_E_FRONTIER", E_LIMIT: "VMQG_E_LIMIT",
+          E_STATE: "VMQG_E_STATE"}
+WORD_PLUS, WORD_HASH, WORD_SHARE, WORD_UNKNOWN = 0, 1, 2, 0xFFFFFFFF
+NONE = 0xFFFFFFFF
+OP_ADD, OP_DEL = 1, 2
+PUB_DOLLAR = 1
+EMIT_LOCAL, EMIT_GROUP, EMIT_REMOTE = 1, 2, 3
+CFG_REPLICA = 1
+LAYOUT_BYTES = 256
+MAX_NODES = 64
+
+
+class VmqgError(RuntimeError):
+    def __init__(self, rc: int, what: str = ""):
+        super().__init__("%s failed: %s (%d)" % (what, ERRORS.get(rc, "?"), rc))
+        self.rc = rc
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("local_node", ctypes.c_uint32),
+                ("max_nodes", ctypes.c_uint32), ("max_mountpoints", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("hint_edges", ctypes.c_uint64), ("hint_paths", ctypes.c_uint64),
+                ("hint_keys", ctypes.c_uint64), ("hint_records", ctypes.c_uint64),
+                ("hint_exact", ctypes.c_uint64)]
+
+
+class Op(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in
+                ("kind", "mountpoint", "word_off", "nwords", "node", "subscriber", "subinfo", "reserved")]
+
+
+class Pub(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("mountpoint", "word_off", "nwords", "flags")]
+
+
+class Emit(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("kind_node", "group", "subscriber", "subinfo")]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("subs", "device_bytes", "trie_edges", "trie_nodes", "trie_topics", "subs_objects",
+                 "fanout_objects", "remote_keys", "epoch", "rebuilds", "paths", "words")]
+
+
+# (name, restype, argtypes) for every entry point declared in include/vmqg.h
+_P = ctypes.c_void_p
+_U32, _U64, _SZ = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
+SIGNATURES = [
+    ("vmqg_abi_version", ctypes.c_int, []),
+    ("vmqg_create", _P, [ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_int)]),
+    ("vmqg_destroy", None, [_P]),
+    ("vmqg_intern_words", ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
+    ("vmqg_prepare_publish", ctypes.c_int, [_P, _U32, ctypes.c_char_p, _SZ, _P, _U32, ctypes.POINTER(Pub)]),
+    ("vmqg_apply_ops", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, ctypes.POINTER(_U64)]),
+    ("vmqg_match_batch", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
+    ("vmqg_match_device", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),
+    ("vmqg_match_status", ctypes.c_int, [_P, _P]),
+    ("vmqg_stats", ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
+    ("vmqg_dump", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_SZ)]),
+    ("vmqg_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
+    ("vmqg_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
+    ("vmqg_arena", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64), _P]),
+    ("vmqg_replica_load", ctypes.c_int, [_P, _P, _P, _P]),
+    ("vmqg_last_patches", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64),
+                                         ctypes.POINTER(ctypes.c_int)]),
+    ("vmqg_apply_patches_device", ctypes.c_int, [_P, _P, _U64, _P]),
+]
+
+_lib = None
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(s) > t for s in DEPS if os.path.exists(s))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile libvmqgpu.so for gfx950 with hipcc (in-tree)."""
+    if not force and not _stale():
+        return LIB_PATH
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-value", "-Wno-unused-result",
+           "-o", LIB_PATH + ".tmp"] + SOURCES
+    r = subprocess.run(cmd, capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n%s" % (r.stderr if not verbose else ""))
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+def lib():
+    """Load libvmqgpu.so; raises ImportError when the native library is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libvmqgpu.so not built (%s); run vernemq_amd._lib.build()" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != OK:
+        raise VmqgError(rc, what)

@@ -1,0 +1,262 @@
+// extern "C" boundary of libvmqgpu (include/vmqg.h).  No C++ exception and
+// no torch type crosses it; every entry point maps onto the Engine.
+#include <cstring>
+#include <new>
+
+#include "vmqg_engine.h"
+
+using vmqg::Engine;
+
+struct vmqg_ctx {
+  Engine e;
+};
+
+#define GUARD_BEGIN try {
+#define GUARD_END                               \
+  }                                             \
+  catch (const std::bad_alloc&) {               \
+    return VMQG_E_NOMEM;                        \
+  }                                             \
+  catch (...) {                                 \
+    return VMQG_E_INVAL;                        \
+  }
+
+extern "C" {
+
+int vmqg_abi_version(void) { return VMQG_ABI_VERSION; }
+
+vmqg_ctx* vmqg_create(const vmqg_config* cfg, int* err) {
+  int rc = VMQG_OK;
+  vmqg_ctx* c = nullptr;
+  try {
+    if (!cfg) { rc = VMQG_E_INVAL; }
+    else {
+      c = new vmqg_ctx();
+      rc = c->e.init(*cfg);
+      if (rc != VMQG_OK) { delete c; c = nullptr; }
+    }
+  } catch (const std::bad_alloc&) {
+    delete c; c = nullptr; rc = VMQG_E_NOMEM;
+  } catch (...) {
+    delete c; c = nullptr; rc = VMQG_E_INVAL;
+  }
+  if (err) *err = rc;
+  return c;
+}
+
+void vmqg_destroy(vmqg_ctx* ctx) { delete ctx; }
+
+int vmqg_intern_words(vmqg_ctx* ctx, const uint8_t* bytes, const uint64_t* offs, uint32_t n, int create,
+                      uint32_t* ids_out) {
+  if (!ctx || (n && (!bytes || !offs || !ids_out))) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  for (uint32_t i = 0; i < n; i++) {
+    if (offs[i + 1] < offs[i]) return VMQG_E_INVAL;
+    ids_out[i] = ctx->e.intern(bytes + offs[i], offs[i + 1] - offs[i], create != 0);
+  }
+  return VMQG_OK;
+  GUARD_END
+}
+
+// vmq_topic:validate_topic(publish, Topic)  (vmq_topic.erl:82-112): split on
+// '/', keep empty words, reject '+' / '#' anywhere, size 0 or > 65,536.
+int vmqg_prepare_publish(vmqg_ctx* ctx, uint32_t mountpoint, const uint8_t* topic, size_t len,
+                         uint32_t* words_out, uint32_t cap, vmqg_pub* pub) {
+  if (!ctx || !pub || (len && !topic)) return VMQG_E_INVAL;
+  if (len == 0 || len > 65536) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  uint32_t n = 0;
+  size_t start = 0;
+  for (size_t i = 0; i <= len; i++) {
+    if (i < len && (topic[i] == '+' || topic[i] == '#')) return VMQG_E_INVAL;
+    if (i == len || topic[i] == '/') {
+      if (n >= cap) return VMQG_E_OVERFLOW;
+      words_out[n++] = ctx->e.intern(topic + start, i - start, false);
+      start = i + 1;
+    }
+  }
+  pub->mountpoint = mountpoint;
+  pub->word_off = 0;
+  pub->nwords = n;
+  pub->flags = topic[0] == '$' ? VMQG_PUB_DOLLAR : 0u;
+  return VMQG_OK;
+  GUARD_END
+}
+
+int vmqg_apply_ops(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords,
+                   uint64_t* epoch_out) {
+  if (!ctx || (n && !ops) || (nwords && !words)) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  int rc = ctx->e.apply_ops(ops, n, words, nwords);
+  if (epoch_out) *epoch_out = ctx->e.epoch;
+  return rc;
+  GUARD_END
+}
+
+static int grow(void** p, uint64_t* cap, uint64_t need) {
+  if (*cap >= need) return VMQG_OK;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  uint64_t c = 1;
+  while (c < need) c <<= 1;
+  if (hipMalloc(p, c) != hipSuccess) { *cap = 0; return VMQG_E_NOMEM; }
+  *cap = c;
+  return VMQG_OK;
+}
+
+int vmqg_match_batch(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const uint32_t* words, size_t nwords,
+                     vmqg_emit* out, size_t out_cap, size_t* out_n, uint64_t* offsets) {
+  if (!ctx || !offsets || (npub && !pubs) || (nwords && !words) || (out_cap && !out)) return VMQG_E_INVAL;
+  if (npub > 0xFFFFFFF0u) return VMQG_E_LIMIT;
+  GUARD_BEGIN
+  Engine& e = ctx->e;
+  if (!e.has_device) return VMQG_E_DEVICE;
+  for (size_t i = 0; i < npub; i++)
+    if (pubs[i].nwords == 0 || (uint64_t)pubs[i].word_off + pubs[i].nwords > nwords) return VMQG_E_INVAL;
+  hipSetDevice(e.device);
+  int rc;
+  if ((rc = grow(&e.d_pubs, &e.d_pubs_cap, (npub + 1) * sizeof(vmqg_pub)))) return rc;
+  if ((rc = grow(&e.d_words, &e.d_words_cap, (nwords + 1) * sizeof(uint32_t)))) return rc;
+  if ((rc = grow(&e.d_offs, &e.d_offs_cap, (npub + 1) * sizeof(uint64_t)))) return rc;
+  if ((rc = grow(&e.d_out, &e.d_out_cap, (out_cap + 1) * sizeof(vmqg_emit)))) return rc;
+  hipStream_t st = e.stream;
+  if (npub && hipMemcpyAsync(e.d_pubs, pubs, npub * sizeof(vmqg_pub), hipMemcpyHostToDevice, st) != hipSuccess)
+    return VMQG_E_DEVICE;
+  if (nwords && hipMemcpyAsync(e.d_words, words, nwords * 4, hipMemcpyHostToDevice, st) != hipSuccess)
+    return VMQG_E_DEVICE;
+  rc = e.match_device(static_cast<const vmqg_pub*>(e.d_pubs), (uint32_t)npub,
+                      static_cast<const uint32_t*>(e.d_words), static_cast<vmqg::Record*>(e.d_out), out_cap,
+                      static_cast<uint64_t*>(e.d_offs), st);
+  if (rc) return rc;
+  if (hipMemcpyAsync(offsets, e.d_offs, (npub + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st) != hipSuccess)
+    return VMQG_E_DEVICE;
+  rc = e.match_status(st);
+  const uint64_t total = offsets[npub];
+  if (out_n) *out_n = total;
+  if (rc == VMQG_E_OVERFLOW || total > out_cap) return VMQG_E_OVERFLOW;
+  if (rc) return rc;
+  if (total && hipMemcpy(out, e.d_out, total * sizeof(vmqg_emit), hipMemcpyDeviceToHost) != hipSuccess)
+    return VMQG_E_DEVICE;
+  return VMQG_OK;
+  GUARD_END
+}
+
+int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words,
+                      vmqg_emit* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream) {
+  if (!ctx || !d_offsets || (npub && (!d_pubs || !d_words))) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  return ctx->e.match_device(d_pubs, npub, d_words, reinterpret_cast<vmqg::Record*>(d_out), out_cap, d_offsets,
+                             static_cast<hipStream_t>(stream));
+  GUARD_END
+}
+
+int vmqg_match_status(vmqg_ctx* ctx, void* stream) {
+  if (!ctx) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  return ctx->e.match_status(static_cast<hipStream_t>(stream));
+  GUARD_END
+}
+
+int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
+  if (!ctx || !out) return VMQG_E_INVAL;
+  const Engine& e = ctx->e;
+  out->subs = e.n_subs_objects + e.n_remote_keys;
+  out->device_bytes = e.has_device ? e.d_arena_bytes : e.lay.total_bytes;
+  out->trie_edges = e.edge_live;
+  out->trie_nodes = e.n_trie_nodes;
+  out->trie_topics = e.n_trie_topics;
+  out->subs_objects = e.n_subs_objects;
+  out->fanout_objects = e.n_fanout;
+  out->remote_keys = e.n_remote_keys;
+  out->epoch = e.epoch;
+  out->rebuilds = e.rebuilds;
+  out->paths = e.paths.size();
+  out->words = e.word_text.size();
+  return VMQG_OK;
+}
+
+int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len) {
+  if (!ctx || !text || !len) return VMQG_E_INVAL;
+  if (ctx->e.replica) return VMQG_E_STATE;
+  GUARD_BEGIN
+  ctx->e.dump_text = ctx->e.dump();
+  *text = ctx->e.dump_text.data();
+  *len = ctx->e.dump_text.size();
+  return VMQG_OK;
+  GUARD_END
+}
+
+int vmqg_set_timing(vmqg_ctx* ctx, int enable) {
+  if (!ctx) return VMQG_E_INVAL;
+  ctx->e.collect_times();
+  ctx->e.timing = enable != 0;
+  ctx->e.sum_count_ns = ctx->e.sum_emit_ns = 0;
+  ctx->e.n_timed = 0;
+  return VMQG_OK;
+}
+
+int vmqg_kernel_times(vmqg_ctx* ctx, double* count_ns, double* emit_ns, uint64_t* launches) {
+  if (!ctx) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  Engine& e = ctx->e;
+  e.collect_times();
+  if (count_ns) *count_ns = e.n_timed ? e.sum_count_ns / e.n_timed : 0;
+  if (emit_ns) *emit_ns = e.n_timed ? e.sum_emit_ns / e.n_timed : 0;
+  if (launches) *launches = e.n_timed;
+  return VMQG_OK;
+  GUARD_END
+}
+
+int vmqg_arena(vmqg_ctx* ctx, void** d_ptr, uint64_t* bytes, uint8_t* layout_out) {
+  if (!ctx) return VMQG_E_INVAL;
+  if (d_ptr) *d_ptr = ctx->e.d_arena;
+  if (bytes) *bytes = ctx->e.lay.total_bytes;
+  if (layout_out) memcpy(layout_out, &ctx->e.lay, sizeof(vmqg::Layout));
+  return VMQG_OK;
+}
+
+int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, void* stream) {
+  if (!ctx || !layout || !d_src) return VMQG_E_INVAL;
+  Engine& e = ctx->e;
+  if (!e.replica) return VMQG_E_STATE;
+  if (!e.has_device) return VMQG_E_DEVICE;
+  vmqg::Layout L;
+  memcpy(&L, layout, sizeof(L));
+  if (L.magic != vmqg::kLayoutMagic) return VMQG_E_INVAL;
+  hipSetDevice(e.device);
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e.stream;
+  if (e.d_arena_bytes < L.total_bytes) {
+    if (hipDeviceSynchronize() != hipSuccess) return VMQG_E_DEVICE;
+    if (e.d_arena) hipFree(e.d_arena);
+    e.d_arena = nullptr; e.d_arena_bytes = 0;
+    if (hipMalloc(&e.d_arena, L.total_bytes) != hipSuccess) return VMQG_E_NOMEM;
+    e.d_arena_bytes = L.total_bytes;
+  }
+  e.lay = L;
+  if (hipMemcpyAsync(e.d_arena, d_src, L.total_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return VMQG_E_DEVICE;
+  e.epoch++;
+  return VMQG_OK;
+}
+
+int vmqg_last_patches(vmqg_ctx* ctx, const void** host_ptr, uint64_t* bytes, int* full_image) {
+  if (!ctx || !host_ptr || !bytes) return VMQG_E_INVAL;
+  *host_ptr = ctx->e.last_patches.data();
+  *bytes = ctx->e.last_patches.size() * sizeof(vmqg::Patch);
+  if (full_image) *full_image = ctx->e.last_full ? 1 : 0;
+  return VMQG_OK;
+}
+
+int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t bytes, void* stream) {
+  if (!ctx || (bytes && !d_patches) || bytes % sizeof(vmqg::Patch)) return VMQG_E_INVAL;
+  Engine& e = ctx->e;
+  if (!e.has_device || !e.d_arena) return VMQG_E_DEVICE;
+  hipSetDevice(e.device);
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e.stream;
+  if (vmqg::launch_patches(e.d_arena, d_patches, bytes / sizeof(vmqg::Patch), st) != hipSuccess)
+    return VMQG_E_DEVICE;
+  e.epoch++;
+  return VMQG_OK;
+}
+
+}  // extern "C"

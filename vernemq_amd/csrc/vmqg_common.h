@@ -1,0 +1,104 @@
+// Shared host/device definitions of the device image ("arena") that the host
+// engine (vmqg_engine.cpp) maintains and the HIP kernels (vmqg_kernels.hip)
+// read.  Every table lives in ONE device allocation so that a delta batch is
+// a list of 16-byte patches (offset, bytes) and a replica is a plain copy.
+//
+// Layout of the arena (all regions 256-B aligned):
+//   edges   : open-addressed hash (parent path, word) -> child path.
+//             Buckets of 4 x 16-B slots (one 64-B line per probe).
+//             This is vmq_trie (vmq_reg_trie.erl:41,43,138).
+//   nodes   : indexed by path id, 16 B.  Folds vmq_trie_node (:42,139), the
+//             vmq_trie_topic entry of the same path (:140) and the resolved
+//             subscriber-list keys of that entry into one record, so that a
+//             trie hit needs one load to know what it emits.
+//   keydesc : indexed by key id, 8 B {record offset, count} — one
+//             vmq_trie_subs key ({MP,Topic} or {MP,Group,Topic}) (:141-142).
+//   keylist : u32 pool of key ids for filters with >= 2 node entries.
+//   records : 16-B emission records (vmqg_emit) grouped per key.
+//   exact   : open-addressed hash of non-wildcard (MP, Topic) -> {local key,
+//             remote-node mask}: the `{Topic, node()}` candidate of fold/4
+//             (:62) plus vmq_trie_remote_subs (:143, :514-520).
+//   exwords : u32 pool of the exact topics' word ids (exactness check).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define VMQG_HD __host__ __device__ __forceinline__
+#else
+#define VMQG_HD inline
+#endif
+
+namespace vmqg {
+
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;   // slot never used
+constexpr uint32_t kTomb = 0xFFFFFFFEu;    // slot deleted (probe continues)
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kPlus = 0u, kHash = 1u, kShare = 2u, kUnknownWord = 0xFFFFFFFFu;
+
+// node record flags (low 8 bits of NodeRec.meta; nkeys in the high 24 bits)
+constexpr uint32_t kNodeRec = 1u;       // vmq_trie_node record exists
+constexpr uint32_t kNodeTopic = 2u;     // ... and its `topic` field is set
+constexpr uint32_t kNodeFilter = 4u;    // vmq_trie_topic entry exists for the path
+constexpr uint32_t kNodeDollarSkip = 8u;  // path is [#] or starts with + (:285-288)
+constexpr uint32_t kNodeEmits = kNodeRec | kNodeTopic | kNodeFilter;
+
+struct alignas(16) EdgeSlot { uint32_t parent, word, child, pad; };
+struct alignas(16) NodeRec { uint32_t meta, key, rmask_lo, rmask_hi; };
+struct alignas(8) KeyDesc { uint32_t off, count; };
+struct alignas(16) Record { uint32_t kind_node, group, subscriber, subinfo; };
+struct alignas(16) ExactSlot {
+  uint64_t fp;
+  uint32_t mp, nwords;     // nwords == kEmpty / kTomb marks free slots
+  uint32_t key, words_off;
+  uint64_t rmask;
+};
+static_assert(sizeof(EdgeSlot) == 16 && sizeof(NodeRec) == 16 && sizeof(Record) == 16, "");
+static_assert(sizeof(ExactSlot) == 32 && sizeof(KeyDesc) == 8, "");
+
+constexpr uint32_t kEdgeSlotsPerBucket = 4;
+constexpr uint32_t kExactSlotsPerBucket = 2;
+
+// Arena layout.  Fixed-size POD: it is what a replica needs to read an image
+// (VMQG_LAYOUT_BYTES in vmqg.h bounds it).
+struct Layout {
+  uint64_t magic;
+  uint64_t total_bytes;
+  uint64_t edge_off, node_off, keydesc_off, keylist_off, rec_off, exact_off, exwords_off;
+  uint64_t edge_buckets;     // power of two
+  uint64_t node_cap;         // path ids
+  uint64_t key_cap;          // key ids
+  uint64_t keylist_cap;      // u32 entries
+  uint64_t rec_cap;          // records
+  uint64_t exact_buckets;    // power of two
+  uint64_t exwords_cap;      // u32 entries
+  uint64_t max_mountpoints;
+  uint64_t local_node;
+  uint64_t pad[14];
+};
+static_assert(sizeof(Layout) == 256, "layout must be 256 bytes");
+constexpr uint64_t kLayoutMagic = 0x31676D7176ull;  // "vmqg1"
+
+// 24-byte patch record: write 16 bytes at arena offset `off` (16-B aligned).
+struct Patch { uint64_t off; uint32_t data[4]; };
+static_assert(sizeof(Patch) == 24, "");
+
+VMQG_HD uint64_t mix64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+VMQG_HD uint64_t edge_hash(uint32_t parent, uint32_t word) {
+  return mix64(((uint64_t)parent << 32) | word);
+}
+// Exact-topic fingerprint: an order-sensitive sum of per-position mixes, so
+// a wave can compute it lane-parallel.  Equal fingerprints are verified
+// word by word (exwords), so collisions cost a compare, never a wrong match.
+VMQG_HD uint64_t fp_word(uint32_t word, uint32_t pos) {
+  return mix64(((uint64_t)word << 32) ^ (uint64_t)(pos * 0x9E3779B9u + 1u));
+}
+VMQG_HD uint64_t fp_final(uint64_t sum, uint32_t mp, uint32_t nwords) {
+  return mix64(sum + mix64(((uint64_t)mp << 32) | nwords));
+}
+
+}  // namespace vmqg

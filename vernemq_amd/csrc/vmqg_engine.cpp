@@ -1,0 +1,867 @@
+// Host engine: interned restatement of vmq_reg_trie's delta handling over
+// the device-image mirror.  See vmqg_engine.h for the data model; every
+// state-machine function cites the Erlang clause it reproduces
+// (apps/vmq_server/src/vmq_reg_trie.erl unless noted).
+#include "vmqg_engine.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace vmqg {
+
+static uint64_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+static uint64_t align256(uint64_t v) { return (v + 255) & ~255ull; }
+
+Engine::~Engine() {
+  if (has_device) {
+    hipSetDevice(device);
+    if (stream) hipStreamSynchronize(stream);
+    for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
+    for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
+    if (ev_match_done) hipEventDestroy(ev_match_done);
+    hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_deferred); hipFree(d_scan_tmp);
+    hipFree(d_gstack); hipFree(d_gcand); hipFree(d_gkeys);
+    hipFree(d_pubs); hipFree(d_words); hipFree(d_offs); hipFree(d_out);
+    if (h_patch_stage) hipHostFree(h_patch_stage);
+    if (stream) hipStreamDestroy(stream);
+  }
+}
+
+int Engine::init(const vmqg_config& c) {
+  cfg = c;
+  if (cfg.max_nodes == 0) cfg.max_nodes = VMQG_MAX_NODES;
+  if (cfg.max_mountpoints == 0) cfg.max_mountpoints = 1024;
+  if (cfg.max_nodes > VMQG_MAX_NODES || cfg.local_node >= cfg.max_nodes) return VMQG_E_LIMIT;
+  if (cfg.max_mountpoints > (1u << 24)) return VMQG_E_LIMIT;
+  replica = (cfg.flags & VMQG_CFG_REPLICA) != 0;
+  // reserved words
+  for (const char* s : {"+", "#", "$share"}) intern(reinterpret_cast<const uint8_t*>(s), strlen(s), true);
+  if (!replica) {
+    paths.resize(cfg.max_mountpoints);
+    for (uint32_t m = 0; m < cfg.max_mountpoints; m++) {
+      paths[m].parent = kNone; paths[m].word = kNone; paths[m].mp = m; paths[m].depth = 0;
+    }
+    rebuild(0);
+  }
+  if (cfg.device >= 0) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || cfg.device >= n) return VMQG_E_DEVICE;
+    device = cfg.device;
+    if (hipSetDevice(device) != hipSuccess) return VMQG_E_DEVICE;
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VMQG_E_DEVICE;
+    if (hipEventCreateWithFlags(&ev_match_done, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
+    has_device = true;
+    if (hipMalloc(&d_status, 64) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_deferred, sizeof(uint32_t) * deferred_cap) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_gstack, sizeof(uint2) * (uint64_t)g_waves * g_scap) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_gcand, sizeof(uint32_t) * (uint64_t)g_waves * g_ccap) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_gkeys, sizeof(uint2) * (uint64_t)g_waves * g_kcap) != hipSuccess) return VMQG_E_NOMEM;
+    if (!replica) {
+      int rc = upload();
+      if (rc) return rc;
+    }
+  }
+  return VMQG_OK;
+}
+
+// ------------------------------------------------------------ dictionary
+uint32_t Engine::intern(const uint8_t* b, size_t n, bool create) {
+  std::string s(reinterpret_cast<const char*>(b), n);
+  auto it = word_index.find(s);
+  if (it != word_index.end()) return it->second;
+  if (!create) return kUnknownWord;
+  uint32_t id = (uint32_t)word_text.size();
+  word_text.push_back(s);
+  word_index.emplace(std::move(s), id);
+  return id;
+}
+
+// ------------------------------------------------------------- paths/keys
+uint32_t Engine::path_child(uint32_t parent, uint32_t word, bool create) {
+  const uint64_t k = ((uint64_t)parent << 32) | word;
+  auto it = path_index.find(k);
+  if (it != path_index.end()) return it->second;
+  if (!create) return kNone;
+  const uint32_t id = (uint32_t)paths.size();
+  PathInfo pi;
+  pi.parent = parent; pi.word = word; pi.mp = paths[parent].mp; pi.depth = paths[parent].depth + 1;
+  // MQTT-4.7.2-1 filters: exactly [#], or starting with + (vmq_reg_trie.erl:285-288)
+  pi.first_plus = pi.depth == 1 ? (word == kPlus) : paths[parent].first_plus;
+  pi.dollar_skip = pi.first_plus || (pi.depth == 1 && word == kHash);
+  paths.push_back(std::move(pi));
+  path_index.emplace(k, id);
+  return id;
+}
+
+bool Engine::path_chain(uint32_t mp, const uint32_t* w, uint32_t L, bool create, std::vector<uint32_t>& chain) {
+  chain.resize(L + 1);
+  chain[0] = mp;
+  for (uint32_t i = 0; i < L; i++) {
+    chain[i + 1] = path_child(chain[i], w[i], create);
+    if (chain[i + 1] == kNone) return false;
+  }
+  return true;
+}
+
+uint32_t Engine::topic_id(uint32_t mp, const uint32_t* w, uint32_t L, bool create) {
+  std::string k(reinterpret_cast<const char*>(&mp), 4);
+  k.append(reinterpret_cast<const char*>(w), (size_t)L * 4);
+  auto it = topic_index.find(k);
+  if (it != topic_index.end()) return it->second;
+  if (!create) return kNone;
+  const uint32_t id = (uint32_t)topics.size();
+  TopicInfo t;
+  t.mp = mp;
+  t.words.assign(w, w + L);
+  t.exact_ok = 1;
+  for (uint32_t i = 0; i < L; i++) if (w[i] == kPlus || w[i] == kHash) t.exact_ok = 0;
+  topics.push_back(std::move(t));
+  topic_index.emplace(std::move(k), id);
+  return id;
+}
+
+uint32_t Engine::local_key(uint32_t tid, bool create) {
+  if (topics[tid].local_key != kNone || !create) return topics[tid].local_key;
+  const uint32_t k = (uint32_t)keys.size();
+  keys.emplace_back();
+  keys[k].topic_id = tid;
+  topics[tid].local_key = k;
+  mark_key(k);
+  return k;
+}
+
+uint32_t Engine::group_key(uint32_t tid, uint32_t group, bool create) {
+  const uint64_t gk = ((uint64_t)tid << 32) | group;
+  auto it = group_key_index.find(gk);
+  if (it != group_key_index.end()) return it->second;
+  if (!create) return kNone;
+  const uint32_t k = (uint32_t)keys.size();
+  keys.emplace_back();
+  keys[k].topic_id = tid;
+  keys[k].group = group;
+  group_key_index.emplace(gk, k);
+  mark_key(k);
+  return k;
+}
+
+// ------------------------------------------------------------------ mirror
+void Engine::touch(uint64_t off, uint64_t bytes) {
+  if (full_image) return;
+  for (uint64_t c = off >> 4, e = (off + bytes + 15) >> 4; c < e; c++) {
+    uint64_t& w = dirty_bits[c >> 6];
+    const uint64_t bit = 1ull << (c & 63);
+    if (!(w & bit)) { w |= bit; dirty_chunks.push_back(c); }
+  }
+}
+
+uint64_t Engine::edge_find(uint32_t parent, uint32_t word) {
+  EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
+  const uint64_t mask = lay.edge_buckets - 1;
+  uint64_t b = edge_hash(parent, word) & mask;
+  for (uint64_t i = 0; i < lay.edge_buckets; i++, b = (b + 1) & mask) {
+    for (uint32_t j = 0; j < kEdgeSlotsPerBucket; j++) {
+      const EdgeSlot& s = t[b * kEdgeSlotsPerBucket + j];
+      if (s.parent == parent && s.word == word) return b * kEdgeSlotsPerBucket + j;
+      if (s.parent == kEmpty) return ~0ull;
+    }
+  }
+  return ~0ull;
+}
+
+void Engine::edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
+  if (edge_find(parent, word) != ~0ull) return;   // ets:insert of an identical #trie{}
+  EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
+  const uint64_t mask = lay.edge_buckets - 1;
+  uint64_t b = edge_hash(parent, word) & mask;
+  for (uint64_t i = 0; i < lay.edge_buckets; i++, b = (b + 1) & mask) {
+    for (uint32_t j = 0; j < kEdgeSlotsPerBucket; j++) {
+      const uint64_t si = b * kEdgeSlotsPerBucket + j;
+      EdgeSlot& s = t[si];
+      if (s.parent == kEmpty || s.parent == kTomb) {
+        if (s.parent == kTomb) edge_tomb--;
+        s = EdgeSlot{parent, word, child, 0};
+        edge_live++;
+        touch(lay.edge_off + si * sizeof(EdgeSlot), sizeof(EdgeSlot));
+        return;
+      }
+    }
+  }
+}
+
+void Engine::edge_erase(uint32_t parent, uint32_t word) {
+  const uint64_t si = edge_find(parent, word);
+  if (si == ~0ull) return;
+  EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
+  t[si] = EdgeSlot{kTomb, kTomb, kTomb, 0};
+  edge_live--; edge_tomb++;
+  touch(lay.edge_off + si * sizeof(EdgeSlot), sizeof(EdgeSlot));
+}
+
+Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale) const {
+  Layout L{};
+  L.magic = kLayoutMagic;
+  L.max_mountpoints = cfg.max_mountpoints;
+  L.local_node = cfg.local_node;
+  uint64_t recs = 0, kl = 0, xw = 0, ex = 0;
+  for (auto& k : keys) recs += next_pow2(k.vals.size() ? k.vals.size() : 1);
+  for (auto& p : paths) if (p.filter && p.nodes.size() >= 2) kl += p.nodes.size();
+  for (auto& t : topics) {
+    const bool has = t.exact_ok && ((t.local_key != kNone && !keys[t.local_key].vals.empty()) || !t.remote.empty());
+    if (has) { ex++; xw += t.words.size(); }
+  }
+  const uint64_t edges_need = edge_live + extra_edges;
+  const uint64_t edge_slots = next_pow2(std::max<uint64_t>(4096, std::max<uint64_t>(edges_need * 2, cfg.hint_edges * 2)));
+  L.edge_buckets = edge_slots / kEdgeSlotsPerBucket;
+  L.node_cap = std::max<uint64_t>({4096, paths.size() + paths.size() / 2, cfg.hint_paths + cfg.max_mountpoints});
+  L.key_cap = std::max<uint64_t>({4096, keys.size() + keys.size() / 2, cfg.hint_keys});
+  L.keylist_cap = std::max<uint64_t>(4096, kl * 2);
+  L.rec_cap = std::max<uint64_t>({16384, recs * 2, cfg.hint_records * 2});
+  const uint64_t exact_slots = next_pow2(std::max<uint64_t>(4096, std::max<uint64_t>(ex * 2 + 1024, cfg.hint_exact * 2)));
+  L.exact_buckets = exact_slots / kExactSlotsPerBucket;
+  L.exwords_cap = std::max<uint64_t>(16384, xw * 2);
+  uint64_t o = 0;
+  L.edge_buckets *= scale; L.node_cap *= scale; L.key_cap *= scale; L.keylist_cap *= scale;
+  L.rec_cap *= scale; L.exact_buckets *= scale; L.exwords_cap *= scale;
+  L.edge_off = o;    o = align256(o + L.edge_buckets * kEdgeSlotsPerBucket * sizeof(EdgeSlot));
+  L.node_off = o;    o = align256(o + L.node_cap * sizeof(NodeRec));
+  L.keydesc_off = o; o = align256(o + L.key_cap * sizeof(KeyDesc));
+  L.keylist_off = o; o = align256(o + L.keylist_cap * sizeof(uint32_t));
+  L.rec_off = o;     o = align256(o + L.rec_cap * sizeof(Record));
+  L.exact_off = o;   o = align256(o + L.exact_buckets * kExactSlotsPerBucket * sizeof(ExactSlot));
+  L.exwords_off = o; o = align256(o + L.exwords_cap * sizeof(uint32_t));
+  L.total_bytes = o;
+  return L;
+}
+
+// Re-lay the arena out from the logical state (tables rehashed without
+// tombstones, record/keylist/exword pools compacted).  The next upload
+// ships the whole image.
+void Engine::rebuild(uint64_t extra_edges) {
+  std::vector<EdgeSlot> live;
+  if (!mirror.empty()) {
+    const EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
+    for (uint64_t i = 0; i < lay.edge_buckets * kEdgeSlotsPerBucket; i++)
+      if (t[i].parent != kEmpty && t[i].parent != kTomb) live.push_back(t[i]);
+  }
+  for (uint32_t scale = 1;; scale *= 2) {
+    edge_live = edge_tomb = 0;
+    lay = plan_layout(std::max<uint64_t>(extra_edges, live.size()), scale);
+    mirror.assign(lay.total_bytes / 8, 0);
+    memset(region<uint8_t>(lay.edge_off), 0xFF, lay.edge_buckets * kEdgeSlotsPerBucket * sizeof(EdgeSlot));
+    memset(region<uint8_t>(lay.exact_off), 0xFF, lay.exact_buckets * kExactSlotsPerBucket * sizeof(ExactSlot));
+    dirty_bits.assign((lay.total_bytes / 16 + 63) / 64, 0);
+    dirty_chunks.clear();
+    full_image = true;
+    exact_live = exact_tomb = 0;
+    rec_top = rec_garbage = kl_top = kl_garbage = xw_top = xw_garbage = 0;
+    for (auto& e : live) edge_insert(e.parent, e.word, e.child);
+    for (auto& k : keys) { k.off = 0; k.cap = 0; }
+    for (auto& t : topics) { t.slot = ~0ull; t.words_off = kNone; }
+    for (auto& p : paths) p.kl_n = 0;
+    bool ok = true;
+    for (uint32_t p = 0; ok && p < paths.size(); p++) ok = write_path(p);
+    for (uint32_t k = 0; ok && k < keys.size(); k++) ok = write_key(k);
+    for (uint32_t t = 0; ok && t < topics.size(); t++) ok = write_topic(t);
+    if (ok) break;
+  }
+  for (auto& k : keys) k.dirty = 0;
+  for (auto& p : paths) p.dirty = 0;
+  for (auto& t : topics) t.dirty = 0;
+  dirty_keys.clear(); dirty_paths.clear(); dirty_topics.clear();
+  rebuilds++;
+}
+
+bool Engine::write_key(uint32_t k) {
+  KeyInfo& K = keys[k];
+  if (k >= lay.key_cap) return false;
+  const uint64_t n = K.vals.size();
+  if (n > K.cap) {
+    const uint64_t cap = next_pow2(n);
+    if (rec_top + cap > lay.rec_cap) return false;
+    rec_garbage += K.cap;
+    K.off = rec_top; K.cap = cap; rec_top += cap;
+  }
+  if (n) {
+    memcpy(region<Record>(lay.rec_off) + K.off, K.vals.data(), n * sizeof(Record));
+    touch(lay.rec_off + K.off * sizeof(Record), n * sizeof(Record));
+  }
+  KeyDesc* kd = region<KeyDesc>(lay.keydesc_off) + k;
+  kd->off = (uint32_t)K.off; kd->count = (uint32_t)n;
+  touch(lay.keydesc_off + (uint64_t)k * sizeof(KeyDesc), sizeof(KeyDesc));
+  return true;
+}
+
+bool Engine::write_path(uint32_t p) {
+  if (p >= lay.node_cap) return false;
+  PathInfo& P = paths[p];
+  NodeRec r{0, kNone, 0, 0};
+  uint32_t flags = 0;
+  if (P.rec) flags |= kNodeRec;
+  if (P.rec && P.topic_set) flags |= kNodeTopic;
+  if (P.filter) flags |= kNodeFilter;
+  if (P.dollar_skip) flags |= kNodeDollarSkip;
+  std::vector<uint32_t> ks;
+  uint64_t rmask = 0;
+  if (P.filter) {
+    // match_/3 (:301-303): one candidate per node-list entry
+    for (auto& e : P.nodes) {
+      if (e.first.group != kNone) ks.push_back(group_key(P.topic_id, e.first.group, true));   // :68-72
+      else if (e.first.node == cfg.local_node) ks.push_back(local_key(P.topic_id, true));     // :73-77
+      else rmask |= 1ull << e.first.node;                                                      // :78-84
+    }
+  }
+  if (keys.size() > lay.key_cap) return false;
+  if (ks.size() == 1) r.key = ks[0];
+  else if (ks.size() >= 2) {
+    if (kl_top + ks.size() > lay.keylist_cap) return false;
+    kl_garbage += P.kl_n;
+    r.key = (uint32_t)kl_top;
+    memcpy(region<uint32_t>(lay.keylist_off) + kl_top, ks.data(), ks.size() * 4);
+    touch(lay.keylist_off + kl_top * 4, ks.size() * 4);
+    kl_top += ks.size();
+    P.kl_n = (uint32_t)ks.size();
+  }
+  r.meta = flags | ((uint32_t)ks.size() << 8);
+  r.rmask_lo = (uint32_t)rmask; r.rmask_hi = (uint32_t)(rmask >> 32);
+  *(region<NodeRec>(lay.node_off) + p) = r;
+  touch(lay.node_off + (uint64_t)p * sizeof(NodeRec), sizeof(NodeRec));
+  return true;
+}
+
+uint64_t Engine::exact_fp(const TopicInfo& t) const {
+  uint64_t s = 0;
+  for (uint32_t i = 0; i < t.words.size(); i++) s += fp_word(t.words[i], i);
+  return fp_final(s, t.mp, (uint32_t)t.words.size());
+}
+
+bool Engine::write_topic(uint32_t ti) {
+  TopicInfo& t = topics[ti];
+  const bool has = t.exact_ok && ((t.local_key != kNone && !keys[t.local_key].vals.empty()) || !t.remote.empty());
+  ExactSlot* tab = region<ExactSlot>(lay.exact_off);
+  if (!has) {
+    if (t.slot != ~0ull) {
+      ExactSlot& s = tab[t.slot];
+      s.nwords = kTomb;
+      touch(lay.exact_off + t.slot * sizeof(ExactSlot), sizeof(ExactSlot));
+      t.slot = ~0ull;
+      xw_garbage += t.words.size();
+      t.words_off = kNone;
+      exact_live--; exact_tomb++;
+    }
+    return true;
+  }
+  uint64_t rmask = 0;
+  for (auto& r : t.remote) rmask |= 1ull << r.first;
+  const uint32_t key = (t.local_key != kNone && !keys[t.local_key].vals.empty()) ? t.local_key : kNone;
+  if (t.slot == ~0ull) {
+    if ((exact_live + exact_tomb + 1) * 10 > lay.exact_buckets * kExactSlotsPerBucket * 7) return false;
+    if (xw_top + t.words.size() > lay.exwords_cap) return false;
+    t.words_off = (uint32_t)xw_top;
+    memcpy(region<uint32_t>(lay.exwords_off) + xw_top, t.words.data(), t.words.size() * 4);
+    touch(lay.exwords_off + xw_top * 4, t.words.size() * 4);
+    xw_top += t.words.size();
+    const uint64_t fp = exact_fp(t);
+    const uint64_t mask = lay.exact_buckets - 1;
+    uint64_t b = fp & mask;
+    for (;;) {
+      uint64_t found = ~0ull;
+      for (uint32_t j = 0; j < kExactSlotsPerBucket; j++) {
+        ExactSlot& s = tab[b * kExactSlotsPerBucket + j];
+        if (s.nwords == kEmpty || s.nwords == kTomb) { found = b * kExactSlotsPerBucket + j; break; }
+      }
+      if (found != ~0ull) {
+        if (tab[found].nwords == kTomb) exact_tomb--;
+        exact_live++;
+        t.slot = found;
+        tab[found].fp = fp; tab[found].mp = t.mp; tab[found].nwords = (uint32_t)t.words.size();
+        tab[found].words_off = t.words_off;
+        break;
+      }
+      b = (b + 1) & mask;
+    }
+  }
+  ExactSlot& s = tab[t.slot];
+  s.key = key;
+  s.rmask = rmask;
+  touch(lay.exact_off + t.slot * sizeof(ExactSlot), sizeof(ExactSlot));
+  return true;
+}
+
+bool Engine::flush_incremental() {
+  // paths first: resolving a node list may (defensively) create a key
+  for (size_t i = 0; i < dirty_paths.size(); i++) if (!write_path(dirty_paths[i])) return false;
+  for (size_t i = 0; i < dirty_keys.size(); i++) if (!write_key(dirty_keys[i])) return false;
+  for (size_t i = 0; i < dirty_topics.size(); i++) if (!write_topic(dirty_topics[i])) return false;
+  return true;
+}
+
+// ------------------------------------------------------- state machine
+// add_and_inc/2 (:409-415) and rem_and_dec/2 (:399-407)
+template <class K>
+static void add_and_inc(std::vector<std::pair<K, int64_t>>& v, const K& n) {
+  for (auto& e : v) if (e.first == n) { e.second++; return; }
+  v.insert(v.begin(), {n, 1});
+}
+template <class K>
+static void rem_and_dec(std::vector<std::pair<K, int64_t>>& v, const K& n) {
+  for (size_t i = 0; i < v.size(); i++)
+    if (v[i].first == n) { if (v[i].second == 1) v.erase(v.begin() + i); else v[i].second--; return; }
+}
+
+static bool contains_wildcard(const uint32_t* w, uint32_t L) {   // vmq_topic.erl:91-95
+  for (uint32_t i = 0; i < L; i++) if (w[i] == kPlus) return true;
+  return L > 0 && w[L - 1] == kHash;
+}
+
+// trie_add_path/2 (:340-356)
+void Engine::trie_add_path(uint32_t parent, uint32_t word, uint32_t child) {
+  PathInfo& P = paths[parent];
+  if (P.rec) {
+    if (edge_find(parent, word) == ~0ull) {
+      P.ec++;
+      mark_path(parent);
+      edge_insert(parent, word, child);
+    }
+  } else {
+    P.rec = 1; P.ec = 1; P.topic_set = 0;
+    n_trie_nodes++;
+    mark_path(parent);
+    edge_insert(parent, word, child);
+  }
+}
+
+// add_complex_topic/4 (:318-337)
+void Engine::add_complex_topic(uint32_t mp, const uint32_t* w, uint32_t L, Nog nog, bool wildcard) {
+  if (!wildcard) return;
+  std::vector<uint32_t> chain;
+  path_chain(mp, w, L, true, chain);
+  const uint32_t p = chain[L];
+  if (paths[p].topic_id == kNone) paths[p].topic_id = topic_id(mp, w, L, true);
+  PathInfo& P = paths[p];
+  if (!P.filter) { P.filter = 1; P.total = 1; P.nodes.assign(1, {nog, 1}); n_trie_topics++; }  // :321-323
+  else { add_and_inc(P.nodes, nog); P.total++; }                                                  // :324-326
+  mark_path(p);
+  if (P.rec && P.topic_set) return;                                                                // :330-331
+  for (uint32_t i = 0; i < L; i++) trie_add_path(chain[i], w[i], chain[i + 1]);                  // :334
+  PathInfo& Q = paths[p];
+  if (!Q.rec) n_trie_nodes++;
+  Q.rec = 1; Q.ec = 0; Q.topic_set = 1;   // :336 — fresh record, edge_count 0 (Q1)
+  mark_path(p);
+}
+
+// trie_delete/2 (:417-425) + trie_delete_path/2 (:427-441)
+void Engine::trie_delete(uint32_t p, const std::vector<uint32_t>& chain, const uint32_t* w, uint32_t L) {
+  PathInfo& P = paths[p];
+  if (!(P.rec && P.ec == 0)) return;
+  P.rec = 0; P.topic_set = 0;
+  n_trie_nodes--;
+  mark_path(p);
+  for (int64_t i = (int64_t)L - 1; i >= 0; i--) {
+    const uint32_t parent = chain[i];
+    edge_erase(parent, w[i]);
+    PathInfo& Q = paths[parent];
+    if (!Q.rec) return;                                  // :439-440
+    if (Q.ec == 1 && !Q.topic_set) {                     // :434-436
+      Q.rec = 0; n_trie_nodes--; mark_path(parent);
+      continue;
+    }
+    Q.ec--; mark_path(parent);                           // :437-438
+    return;
+  }
+}
+
+// del_complex_topic/4 (:385-397)
+void Engine::del_complex_topic(uint32_t mp, const uint32_t* w, uint32_t L, Nog nog, bool wildcard) {
+  if (!wildcard) return;
+  std::vector<uint32_t> chain;
+  if (!path_chain(mp, w, L, false, chain)) return;
+  const uint32_t p = chain[L];
+  PathInfo& P = paths[p];
+  if (!P.filter) return;
+  if (P.total > 1) { rem_and_dec(P.nodes, nog); P.total--; mark_path(p); }           // :389-391
+  else if (P.total == 1) {                                                            // :392-394
+    P.filter = 0; P.total = 0; P.nodes.clear(); n_trie_topics--; mark_path(p);
+    trie_delete(p, chain, w, L);
+  }
+}
+
+// insert_trie_subs/2 (:448-464)
+void Engine::insert_trie_subs(uint32_t key, const Record& v) {
+  KeyInfo& K = keys[key];
+  const size_t n = K.vals.size();
+  RecordEq eq;
+  if (n == 1 && eq(K.vals[0], v)) return;                     // :453-455 duplicate
+  if (n >= 2) {
+    if (K.idx) { if (K.idx->count(v)) return; }
+    else for (auto& x : K.vals) if (eq(x, v)) return;         // fanout set: no duplicates
+  }
+  if (n == 0) n_subs_objects++;                               // :451-452
+  if (n == 1) n_fanout += 2;                                  // :458-463 promote both
+  else if (n >= 2) n_fanout++;                                // :456-457
+  K.vals.push_back(v);
+  if (!K.idx && K.vals.size() > 32) {
+    K.idx.reset(new std::unordered_map<Record, uint32_t, RecordHash, RecordEq>());
+    for (uint32_t i = 0; i < K.vals.size(); i++) (*K.idx)[K.vals[i]] = i;
+  } else if (K.idx) {
+    (*K.idx)[v] = (uint32_t)K.vals.size() - 1;
+  }
+  mark_key(key);
+}
+
+// del_trie_subs/2 (:472-496)
+void Engine::del_trie_subs(uint32_t key, const Record& v) {
+  KeyInfo& K = keys[key];
+  const size_t n = K.vals.size();
+  if (n == 0) return;                                         // :474-476
+  if (n == 1) {                                               // :494-495 value-blind (Q3)
+    K.vals.clear();
+    n_subs_objects--;
+    mark_key(key);
+    return;
+  }
+  // :477-493 fanout: delete the object, fold back when one remains
+  size_t pos = ~(size_t)0;
+  if (K.idx) { auto it = K.idx->find(v); if (it != K.idx->end()) pos = it->second; }
+  else { RecordEq eq; for (size_t i = 0; i < n; i++) if (eq(K.vals[i], v)) { pos = i; break; } }
+  if (pos == ~(size_t)0) return;
+  if (K.idx) {
+    K.idx->erase(v);
+    if (pos != n - 1) { K.vals[pos] = K.vals[n - 1]; (*K.idx)[K.vals[pos]] = (uint32_t)pos; }
+  } else if (pos != n - 1) {
+    K.vals[pos] = K.vals[n - 1];
+  }
+  K.vals.pop_back();
+  if (n - 1 == 1) n_fanout -= 2; else n_fanout -= 1;
+  mark_key(key);
+}
+
+// handle_add_event/2 (:253-264)
+void Engine::handle_add(const vmqg_op& op, const uint32_t* w) {
+  const uint32_t L = op.nwords, mp = op.mountpoint;
+  if (L >= 2 && w[0] == kShare) {                                  // :253-256
+    const uint32_t G = w[1];
+    add_complex_topic(mp, w + 2, L - 2, Nog{op.node, G}, true);
+    const uint32_t tid = topic_id(mp, w + 2, L - 2, true);
+    const uint32_t k = group_key(tid, G, true);                    // add_subscriber_group :443-446
+    insert_trie_subs(k, Record{(VMQG_EMIT_GROUP << 24) | op.node, G, op.subscriber, op.subinfo});
+    return;
+  }
+  const bool wc = contains_wildcard(w, L);
+  add_complex_topic(mp, w, L, Nog{op.node, kNone}, wc);
+  const uint32_t tid = topic_id(mp, w, L, true);
+  if (op.node == cfg.local_node) {                                 // :257-260
+    const uint32_t k = local_key(tid, true);                       // add_subscriber :498-501
+    insert_trie_subs(k, Record{(VMQG_EMIT_LOCAL << 24) | op.node, kNone, op.subscriber, op.subinfo});
+    mark_topic(tid);
+  } else {                                                         // :261-264, add_remote_subscriber :503-512
+    TopicInfo& t = topics[tid];
+    if (t.remote.empty()) n_remote_keys++;
+    add_and_inc(t.remote, op.node);
+    mark_topic(tid);
+  }
+}
+
+// handle_delete_event/2 (:266-277)
+void Engine::handle_delete(const vmqg_op& op, const uint32_t* w) {
+  const uint32_t L = op.nwords, mp = op.mountpoint;
+  if (L >= 2 && w[0] == kShare) {
+    const uint32_t G = w[1];
+    del_complex_topic(mp, w + 2, L - 2, Nog{op.node, G}, true);
+    const uint32_t tid = topic_id(mp, w + 2, L - 2, false);
+    if (tid == kNone) return;
+    const uint32_t k = group_key(tid, G, false);                   // del_subscriber_group :467-470
+    if (k != kNone) del_trie_subs(k, Record{(VMQG_EMIT_GROUP << 24) | op.node, G, op.subscriber, op.subinfo});
+    return;
+  }
+  del_complex_topic(mp, w, L, Nog{op.node, kNone}, contains_wildcard(w, L));
+  const uint32_t tid = topic_id(mp, w, L, false);
+  if (tid == kNone) return;
+  if (op.node == cfg.local_node) {
+    const uint32_t k = local_key(tid, false);                      // del_subscriber :522-525
+    if (k != kNone) del_trie_subs(k, Record{(VMQG_EMIT_LOCAL << 24) | op.node, kNone, op.subscriber, op.subinfo});
+    mark_topic(tid);
+  } else {                                                         // del_remote_subscriber :527-539
+    TopicInfo& t = topics[tid];
+    if (t.remote.empty()) return;
+    rem_and_dec(t.remote, op.node);
+    if (t.remote.empty()) n_remote_keys--;
+    mark_topic(tid);
+  }
+}
+
+int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords) {
+  if (replica) return VMQG_E_STATE;
+  // validate the whole batch before touching state
+  uint64_t add_words = 0;
+  for (size_t i = 0; i < n; i++) {
+    const vmqg_op& o = ops[i];
+    if (o.kind != VMQG_OP_ADD && o.kind != VMQG_OP_DEL) return VMQG_E_INVAL;
+    if (o.mountpoint >= cfg.max_mountpoints || o.node >= cfg.max_nodes) return VMQG_E_LIMIT;
+    if (o.nwords == 0 || (uint64_t)o.word_off + o.nwords > nwords) return VMQG_E_INVAL;
+    const uint32_t* w = words + o.word_off;
+    for (uint32_t j = 0; j < o.nwords; j++) if (w[j] >= word_text.size()) return VMQG_E_INVAL;
+    // [<<"$share">>, Group] has no topic: triples([]) has no clause (vmq_topic.erl:71)
+    if (o.nwords == 2 && w[0] == kShare) return VMQG_E_INVAL;
+    if (o.kind == VMQG_OP_ADD) add_words += o.nwords;
+  }
+  // the edge table must absorb every edge this batch could add
+  if ((edge_live + edge_tomb + add_words) * 10 > lay.edge_buckets * kEdgeSlotsPerBucket * 7) rebuild(add_words);
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t* w = words + ops[i].word_off;
+    if (ops[i].kind == VMQG_OP_ADD) handle_add(ops[i], w);
+    else handle_delete(ops[i], w);
+  }
+  const bool garbage_heavy = rec_garbage > lay.rec_cap / 2 || kl_garbage > lay.keylist_cap / 2 ||
+                             xw_garbage > lay.exwords_cap / 2 ||
+                             exact_tomb * 4 > lay.exact_buckets * kExactSlotsPerBucket;
+  if (full_image || garbage_heavy || !flush_incremental()) rebuild(0);
+  for (uint32_t k : dirty_keys) keys[k].dirty = 0;
+  for (uint32_t p : dirty_paths) paths[p].dirty = 0;
+  for (uint32_t t : dirty_topics) topics[t].dirty = 0;
+  dirty_keys.clear(); dirty_paths.clear(); dirty_topics.clear();
+  epoch++;
+  return upload();
+}
+
+// --------------------------------------------------------------- device
+int Engine::upload() {
+  last_patches.clear();
+  last_full = full_image;
+  if (!full_image) {
+    last_patches.reserve(dirty_chunks.size());
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(mirror.data());
+    for (uint64_t c : dirty_chunks) {
+      Patch p;
+      p.off = c * 16;
+      memcpy(p.data, base + p.off, 16);
+      last_patches.push_back(p);
+      dirty_bits[c >> 6] = 0;
+    }
+    dirty_chunks.clear();
+  }
+  if (!has_device) { full_image = false; return VMQG_OK; }
+  hipSetDevice(device);
+  // tables must not change under a match still reading them
+  if (hipStreamWaitEvent(stream, ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
+  if (full_image) {
+    if (d_arena_bytes < lay.total_bytes) {
+      if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
+      if (hipEventSynchronize(ev_match_done) != hipSuccess) return VMQG_E_DEVICE;
+      if (d_arena) hipFree(d_arena);
+      d_arena = nullptr; d_arena_bytes = 0;
+      if (hipMalloc(&d_arena, lay.total_bytes) != hipSuccess) return VMQG_E_NOMEM;
+      d_arena_bytes = lay.total_bytes;
+    }
+    if (hipMemcpyAsync(d_arena, mirror.data(), lay.total_bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
+      return VMQG_E_DEVICE;
+    if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
+    full_image = false;
+    std::fill(dirty_bits.begin(), dirty_bits.end(), 0);
+    return VMQG_OK;
+  }
+  const uint64_t np = last_patches.size();
+  if (np == 0) return VMQG_OK;
+  if (h_patch_cap < np) {
+    if (h_patch_stage) hipHostFree(h_patch_stage);
+    h_patch_stage = nullptr;
+    h_patch_cap = next_pow2(np);
+    if (hipHostMalloc(&h_patch_stage, h_patch_cap * sizeof(Patch)) != hipSuccess) { h_patch_cap = 0; return VMQG_E_NOMEM; }
+  }
+  if (d_patch_cap < np) {
+    if (d_patch) hipFree(d_patch);
+    d_patch = nullptr;
+    d_patch_cap = next_pow2(np);
+    if (hipMalloc(&d_patch, d_patch_cap * sizeof(Patch)) != hipSuccess) { d_patch_cap = 0; return VMQG_E_NOMEM; }
+  }
+  memcpy(h_patch_stage, last_patches.data(), np * sizeof(Patch));
+  if (hipMemcpyAsync(d_patch, h_patch_stage, np * sizeof(Patch), hipMemcpyHostToDevice, stream) != hipSuccess)
+    return VMQG_E_DEVICE;
+  if (launch_patches(d_arena, d_patch, np, stream) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
+  return VMQG_OK;
+}
+
+int Engine::ensure_match_scratch(uint64_t npub) {
+  const uint64_t need = scan_tmp_elems(npub + 1);
+  if (need > scan_tmp_cap) {
+    if (d_scan_tmp) hipFree(d_scan_tmp);
+    d_scan_tmp = nullptr;
+    scan_tmp_cap = next_pow2(need);
+    if (hipMalloc(&d_scan_tmp, scan_tmp_cap * sizeof(uint64_t)) != hipSuccess) { scan_tmp_cap = 0; return VMQG_E_NOMEM; }
+  }
+  return VMQG_OK;
+}
+
+MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, Record* out,
+                           uint64_t out_cap, uint64_t* offs) const {
+  MatchArgs a{};
+  a.edges = reinterpret_cast<const EdgeSlot*>(d_arena + lay.edge_off);
+  a.edge_mask = lay.edge_buckets - 1;
+  a.nodes = reinterpret_cast<const NodeRec*>(d_arena + lay.node_off);
+  a.node_cap = lay.node_cap;
+  a.keydesc = reinterpret_cast<const KeyDesc*>(d_arena + lay.keydesc_off);
+  a.key_cap = lay.key_cap;
+  a.keylist = reinterpret_cast<const uint32_t*>(d_arena + lay.keylist_off);
+  a.records = reinterpret_cast<const Record*>(d_arena + lay.rec_off);
+  a.exact = reinterpret_cast<const ExactSlot*>(d_arena + lay.exact_off);
+  a.exact_mask = lay.exact_buckets - 1;
+  a.exwords = reinterpret_cast<const uint32_t*>(d_arena + lay.exwords_off);
+  a.max_mp = (uint32_t)lay.max_mountpoints;
+  a.local_node = (uint32_t)lay.local_node;
+  a.pubs = pubs; a.words = words; a.npub = npub;
+  a.offsets = offs; a.out = out; a.out_cap = out_cap;
+  a.status = d_status; a.deferred = d_deferred; a.deferred_cap = deferred_cap; a.g_waves = g_waves;
+  a.g_stack = d_gstack; a.g_cand = d_gcand; a.g_keys = d_gkeys;
+  a.g_scap = g_scap; a.g_ccap = g_ccap; a.g_kcap = g_kcap;
+  return a;
+}
+
+int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t* d_words_, Record* d_out_,
+                         uint64_t out_cap, uint64_t* d_offsets, hipStream_t st) {
+  if (!has_device) return VMQG_E_DEVICE;
+  if (!d_arena) return VMQG_E_STATE;
+  hipSetDevice(device);
+  if (!st) st = stream;
+  int rc = ensure_match_scratch(npub);
+  if (rc) return rc;
+  const MatchArgs a = args_for(d_pubs_, npub, d_words_, d_out_, out_cap, d_offsets);
+  if (hipMemsetAsync(d_status, 0, 8, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipMemsetAsync(d_offsets + npub, 0, 8, st) != hipSuccess) return VMQG_E_DEVICE;
+  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
+  if (timing) {
+    hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2); hipEventCreate(&e3);
+    hipEventRecord(e0, st);
+  }
+  if (npub && launch_match(a, 0, false, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (timing) hipEventRecord(e1, st);
+  if (npub && launch_match(a, 0, true, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_scan(d_offsets, (uint64_t)npub + 1, d_scan_tmp, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (timing) hipEventRecord(e2, st);
+  if (npub && launch_match(a, 1, false, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (timing) { hipEventRecord(e3, st); t_count.push_back({e0, e1}); t_emit.push_back({e2, e3}); }
+  if (npub && launch_match(a, 1, true, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
+  return VMQG_OK;
+}
+
+int Engine::match_status(hipStream_t st) {
+  if (!has_device) return VMQG_E_DEVICE;
+  hipSetDevice(device);
+  if (!st) st = stream;
+  uint32_t h[2] = {0, 0};
+  if (hipMemcpyAsync(h, d_status, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipMemsetAsync(d_status, 0, 8, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (h[1] & (2u | 1u)) return VMQG_E_FRONTIER;
+  if (h[1] & 4u) return VMQG_E_OVERFLOW;
+  if (h[1] & 8u) return VMQG_E_DEVICE;
+  return VMQG_OK;
+}
+
+void Engine::collect_times() {
+  if (!has_device) return;
+  hipSetDevice(device);
+  for (size_t i = 0; i < t_count.size(); i++) {
+    float a = 0, b = 0;
+    hipEventSynchronize(t_emit[i].second);
+    hipEventElapsedTime(&a, t_count[i].first, t_count[i].second);
+    hipEventElapsedTime(&b, t_emit[i].first, t_emit[i].second);
+    sum_count_ns += a * 1e6; sum_emit_ns += b * 1e6; n_timed++;
+    hipEventDestroy(t_count[i].first); hipEventDestroy(t_count[i].second);
+    hipEventDestroy(t_emit[i].first); hipEventDestroy(t_emit[i].second);
+  }
+  t_count.clear(); t_emit.clear();
+}
+
+// ------------------------------------------------------------------ dump
+static std::string esc(const std::string& s) {
+  static const char* hx = "0123456789abcdef";
+  std::string o = "\"";
+  for (unsigned char c : s) {
+    if (c >= 0x20 && c < 0x7f && c != '"' && c != '\\') o += (char)c;
+    else { o += "\\x"; o += hx[c >> 4]; o += hx[c & 15]; }
+  }
+  return o + "\"";
+}
+
+std::string Engine::dump() {
+  std::vector<std::string> lines;
+  auto path_words = [&](uint32_t p) {
+    std::vector<uint32_t> w;
+    while (paths[p].parent != kNone) { w.push_back(paths[p].word); p = paths[p].parent; }
+    std::reverse(w.begin(), w.end());
+    return w;
+  };
+  auto show_words = [&](const std::vector<uint32_t>& w) {
+    std::string o = "[";
+    for (size_t i = 0; i < w.size(); i++) { if (i) o += ","; o += esc(word_text[w[i]]); }
+    return o + "]";
+  };
+  auto nid = [&](uint32_t p) {
+    return "mp#" + std::to_string(paths[p].mp) + "|" +
+           (paths[p].parent == kNone ? std::string("root") : show_words(path_words(p)));
+  };
+  const EdgeSlot* et = region<EdgeSlot>(lay.edge_off);
+  for (uint64_t i = 0; i < lay.edge_buckets * kEdgeSlotsPerBucket; i++) {
+    const EdgeSlot& e = et[i];
+    if (e.parent == kEmpty || e.parent == kTomb) continue;
+    lines.push_back("trie " + nid(e.parent) + " " + esc(word_text[e.word]) + " -> " + show_words(path_words(e.child)));
+  }
+  auto show_nog = [&](const Nog& n) {
+    return n.group == kNone ? "node#" + std::to_string(n.node)
+                            : "{node#" + std::to_string(n.node) + "," + esc(word_text[n.group]) + "}";
+  };
+  for (uint32_t p = 0; p < paths.size(); p++) {
+    const PathInfo& P = paths[p];
+    if (P.rec)
+      lines.push_back("node " + nid(p) + " ec=" + std::to_string(P.ec) + " topic=" +
+                      (P.topic_set ? show_words(path_words(p)) : std::string("undefined")));
+    if (P.filter) {
+      std::string l = "topic mp#" + std::to_string(P.mp) + "|" + show_words(path_words(p)) +
+                      " total=" + std::to_string(P.total) + " [";
+      for (size_t i = 0; i < P.nodes.size(); i++) {
+        if (i) l += ",";
+        l += show_nog(P.nodes[i].first) + ":" + std::to_string(P.nodes[i].second);
+      }
+      lines.push_back(l + "]");
+    }
+  }
+  auto show_key = [&](const KeyInfo& K) {
+    const TopicInfo& t = topics[K.topic_id];
+    if (K.group != kNone)
+      return "{mp#" + std::to_string(t.mp) + "," + esc(word_text[K.group]) + "," + show_words(t.words) + "}";
+    return "{mp#" + std::to_string(t.mp) + "," + show_words(t.words) + "}";
+  };
+  auto show_val = [&](const Record& r) {
+    const uint32_t kind = r.kind_node >> 24, node = r.kind_node & 0xFFFFFF;
+    const std::string sid = "sub#" + std::to_string(r.subscriber), si = "info#" + std::to_string(r.subinfo);
+    if (kind == VMQG_EMIT_GROUP)
+      return "{node#" + std::to_string(node) + "," + esc(word_text[r.group]) + "," + sid + "," + si + "}";
+    return "{" + sid + "," + si + "}";
+  };
+  for (const KeyInfo& K : keys) {
+    if (K.vals.empty()) continue;
+    if (K.vals.size() == 1) { lines.push_back("subs " + show_key(K) + " " + show_val(K.vals[0])); continue; }
+    lines.push_back("subs " + show_key(K) + " fanout");
+    for (auto& v : K.vals) lines.push_back("fanout " + show_key(K) + " " + show_val(v));
+  }
+  for (const TopicInfo& t : topics) {
+    if (t.remote.empty()) continue;
+    std::string l = "remote mp#" + std::to_string(t.mp) + "|" + show_words(t.words) + " [";
+    for (size_t i = 0; i < t.remote.size(); i++) {
+      if (i) l += ",";
+      l += "node#" + std::to_string(t.remote[i].first) + ":" + std::to_string(t.remote[i].second);
+    }
+    lines.push_back(l + "]");
+  }
+  std::sort(lines.begin(), lines.end());
+  std::string out;
+  for (auto& l : lines) { out += l; out += '\n'; }
+  return out;
+}
+
+}  // namespace vmqg

@@ -1,0 +1,175 @@
+// Host engine of libvmqgpu: owns the authoritative subscription state with
+// the semantics of vmq_reg_trie's event handlers and keeps a byte-exact host
+// mirror of the device arena.  Every table mutation is written to the mirror
+// and recorded as a dirty 16-B chunk; vmqg_apply_ops ships the dirty chunks
+// as patches (or, after a re-layout, the whole image) to the device.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "vmqg_common.h"
+#include "vmqg_kernels.h"
+
+namespace vmqg {
+
+// NodeOrGroup of a vmq_trie_topic node list: Node | {Node, Group}
+struct Nog {
+  uint32_t node, group;  // group == kNone for a plain node
+  bool operator==(const Nog& o) const { return node == o.node && group == o.group; }
+};
+
+struct PathInfo {
+  uint32_t parent, word, mp, depth;
+  uint32_t topic_id = kNone;        // (MP, path words) term, once known
+  uint32_t kl_n = 0;                // keylist entries owned (garbage accounting)
+  uint8_t rec = 0, topic_set = 0;   // vmq_trie_node record / its topic field
+  uint8_t filter = 0;               // vmq_trie_topic entry exists
+  uint8_t dollar_skip = 0, first_plus = 0, dirty = 0;
+  int64_t ec = 0;                   // edge_count
+  int64_t total = 0;                // vmq_trie_topic TotalCnt
+  std::vector<std::pair<Nog, int64_t>> nodes;   // vmq_trie_topic node list
+};
+
+struct RecordHash {
+  size_t operator()(const Record& r) const {
+    return (size_t)mix64(((uint64_t)r.kind_node << 32 | r.group) ^ mix64((uint64_t)r.subscriber << 32 | r.subinfo));
+  }
+};
+struct RecordEq {
+  bool operator()(const Record& a, const Record& b) const {
+    return a.kind_node == b.kind_node && a.group == b.group && a.subscriber == b.subscriber && a.subinfo == b.subinfo;
+  }
+};
+
+// One vmq_trie_subs key ({MP,Topic} or {MP,Group,Topic}) with its values.
+struct KeyInfo {
+  uint32_t topic_id = kNone, group = kNone;   // group != kNone: a $share group key
+  uint8_t dirty = 0;
+  std::vector<Record> vals;
+  std::unique_ptr<std::unordered_map<Record, uint32_t, RecordHash, RecordEq>> idx;
+  uint64_t off = 0, cap = 0;                  // record range in the arena
+};
+
+// One (MP, Topic) term: the local key, the vmq_trie_remote_subs entry and
+// the exact-table slot that serves both to publishes.
+struct TopicInfo {
+  uint32_t mp;
+  std::vector<uint32_t> words;
+  uint32_t local_key = kNone;
+  uint8_t dirty = 0, exact_ok = 0;
+  std::vector<std::pair<uint32_t, int64_t>> remote;
+  uint64_t slot = ~0ull;
+  uint32_t words_off = kNone;
+};
+
+struct Engine {
+  vmqg_config cfg{};
+  bool replica = false;
+  bool has_device = false;
+
+  // ---- dictionary
+  std::unordered_map<std::string, uint32_t> word_index;
+  std::vector<std::string> word_text;
+
+  // ---- logical state
+  std::vector<PathInfo> paths;                              // ids [0, max_mp) are roots
+  std::unordered_map<uint64_t, uint32_t> path_index;        // parent<<32|word -> path
+  std::vector<KeyInfo> keys;
+  std::unordered_map<uint64_t, uint32_t> group_key_index;   // topic<<32|group -> key
+  std::vector<TopicInfo> topics;
+  std::unordered_map<std::string, uint32_t> topic_index;    // (mp, words) -> topic
+  uint64_t n_trie_nodes = 0, n_trie_topics = 0, n_subs_objects = 0, n_fanout = 0, n_remote_keys = 0;
+
+  // ---- mirror of the device arena
+  Layout lay{};
+  std::vector<uint64_t> mirror;     // lay.total_bytes / 8 words
+  std::vector<uint64_t> dirty_bits; // one bit per 16-B chunk
+  std::vector<uint64_t> dirty_chunks;
+  std::vector<uint32_t> dirty_paths, dirty_keys, dirty_topics;
+  uint64_t edge_live = 0, edge_tomb = 0, exact_live = 0, exact_tomb = 0;
+  uint64_t rec_top = 0, rec_garbage = 0, kl_top = 0, kl_garbage = 0, xw_top = 0, xw_garbage = 0;
+  bool full_image = false;          // the pending upload is a whole image
+  uint64_t epoch = 0, rebuilds = 0;
+  std::vector<Patch> last_patches;
+  bool last_full = false;
+
+  // ---- device
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
+  Patch* h_patch_stage = nullptr; uint64_t h_patch_cap = 0;
+  Patch* d_patch = nullptr; uint64_t d_patch_cap = 0;
+  uint32_t* d_status = nullptr; uint32_t* d_deferred = nullptr; uint32_t deferred_cap = 65536;
+  uint64_t* d_scan_tmp = nullptr; uint64_t scan_tmp_cap = 0;
+  uint2* d_gstack = nullptr; uint32_t* d_gcand = nullptr; uint2* d_gkeys = nullptr;
+  uint32_t g_waves = 16, g_scap = 1u << 15, g_ccap = 1u << 15, g_kcap = 1u << 15;
+  // host-buffer match staging
+  void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
+  void* d_words = nullptr; uint64_t d_words_cap = 0;
+  void* d_offs = nullptr; uint64_t d_offs_cap = 0;
+  void* d_out = nullptr; uint64_t d_out_cap = 0;
+  hipEvent_t ev_match_done = nullptr;
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_emit;
+  double sum_count_ns = 0, sum_emit_ns = 0; uint64_t n_timed = 0;
+
+  std::string dump_text;
+
+  ~Engine();
+  int init(const vmqg_config& c);
+
+  // dictionary
+  uint32_t intern(const uint8_t* b, size_t n, bool create);
+
+  // state machine (vmq_reg_trie.erl:253-539)
+  int apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords);
+  void handle_add(const vmqg_op& op, const uint32_t* w);
+  void handle_delete(const vmqg_op& op, const uint32_t* w);
+  void add_complex_topic(uint32_t mp, const uint32_t* w, uint32_t L, Nog nog, bool wildcard);
+  void del_complex_topic(uint32_t mp, const uint32_t* w, uint32_t L, Nog nog, bool wildcard);
+  void trie_add_path(uint32_t parent, uint32_t word, uint32_t child);
+  void trie_delete(uint32_t p, const std::vector<uint32_t>& chain, const uint32_t* w, uint32_t L);
+  void insert_trie_subs(uint32_t key, const Record& v);
+  void del_trie_subs(uint32_t key, const Record& v);
+
+  uint32_t path_child(uint32_t parent, uint32_t word, bool create);
+  bool path_chain(uint32_t mp, const uint32_t* w, uint32_t L, bool create, std::vector<uint32_t>& chain);
+  uint32_t topic_id(uint32_t mp, const uint32_t* w, uint32_t L, bool create);
+  uint32_t local_key(uint32_t tid, bool create);
+  uint32_t group_key(uint32_t tid, uint32_t group, bool create);
+  void mark_path(uint32_t p) { if (!paths[p].dirty) { paths[p].dirty = 1; dirty_paths.push_back(p); } }
+  void mark_key(uint32_t k) { if (!keys[k].dirty) { keys[k].dirty = 1; dirty_keys.push_back(k); } }
+  void mark_topic(uint32_t t) { if (!topics[t].dirty) { topics[t].dirty = 1; dirty_topics.push_back(t); } }
+
+  // mirror
+  template <class T> T* region(uint64_t off) { return reinterpret_cast<T*>(reinterpret_cast<uint8_t*>(mirror.data()) + off); }
+  void touch(uint64_t off, uint64_t bytes);
+  uint64_t edge_find(uint32_t parent, uint32_t word) ;
+  void edge_insert(uint32_t parent, uint32_t word, uint32_t child);
+  void edge_erase(uint32_t parent, uint32_t word);
+  Layout plan_layout(uint64_t extra_edges, uint32_t scale) const;
+  void rebuild(uint64_t extra_edges);
+  bool flush_incremental();
+  bool write_key(uint32_t k);
+  bool write_path(uint32_t p);
+  bool write_topic(uint32_t t);
+  uint64_t exact_fp(const TopicInfo& t) const;
+
+  // device
+  int upload();
+  int ensure_match_scratch(uint64_t npub);
+  MatchArgs args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, Record* out, uint64_t out_cap,
+                     uint64_t* offs) const;
+  int match_device(const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words, Record* d_out,
+                   uint64_t out_cap, uint64_t* d_offsets, hipStream_t st);
+  int match_status(hipStream_t st);
+  void collect_times();
+
+  std::string dump();
+};
+
+}  // namespace vmqg
