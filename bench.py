@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""Headline benchmark: topic matches/sec (publishes/sec) at 1M subs — SURVEY.md
+§8(d) config C — on 1..N MI355X, with the HIP path's roofline and the CPU
+oracle (C++ restatement of vmq_reg_trie) timed beside it.
+
+One step = one batch of 2^20 publishes (devices/{d}/telemetry/{m}) fully
+matched on each GPU: count pass, offset scan, emit pass writing every
+matched 16-B FoldFun record — inputs resident in HBM, outputs left in HBM.
+
+N > 1 (launched by torch.distributed.run): the trie is built once on rank 0
+and replicated by an RCCL broadcast of the device image; each rank matches
+its own publish batch (weak scaling, no collective on the data path); the
+per-rank emission counts are all-gathered.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def hip_memcpy_d2d(dst: int, src: int, n: int):
+    lib = ctypes.CDLL("libamdhip64.so")
+    lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    rc = lib.hipMemcpy(dst, src, n, 3)
+    if rc != 0:
+        raise RuntimeError("hipMemcpy D2D failed: %d" % rc)
+
+
+def load_pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_latest.json, written by profiles/collect_pmc.py), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(p))
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="publishes per step per GPU")
+    ap.add_argument("--n-dev", type=int, default=1_000_000, help="devices/{d}/telemetry/# subscribers")
+    ap.add_argument("--cpu-sample", type=int, default=100_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP events (profiling runs)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)   # RCCL on ROCm
+
+    from vernemq_amd import workloads as W
+    from vernemq_amd.reg_view import RegGpuView
+    from vernemq_amd import _lib
+
+    t0 = time.time()
+    w = W.config_c(n_dev=args.n_dev, n_pubs=args.batch, seed=0xC + rank)   # same subs, per-rank publishes
+    log("rank %d: workload generated in %.1fs (%d subs, %d publishes)" % (rank, time.time() - t0, w.n_subs, w.n_pubs))
+
+    load_s = 0.0
+    if rank == 0:
+        t0 = time.time()
+        view = RegGpuView(node=w.self_node, device=local, nodes=w.nodes,
+                          hints={"edges": 3 * args.n_dev + 1024, "paths": 3 * args.n_dev + 1024,
+                                 "keys": args.n_dev + 1024, "records": args.n_dev + 1024})
+        w.load_into(view)
+        load_s = time.time() - t0
+        pwid = view.intern_words(w.pub_words, create=False).astype(np.int64)
+        log("rank 0: initialize_trie of %d subs + device upload in %.1fs, stats %s" % (w.n_subs, load_s, view.stats_raw()))
+    if world > 1:
+        # replicate the trie: RCCL broadcast of the device image + layout (+ the word map)
+        meta = torch.zeros(2, dtype=torch.int64, device=dev)
+        if rank == 0:
+            ptr, nbytes, lay = view.arena()
+            meta[0], meta[1] = nbytes, len(pwid)
+        dist.broadcast(meta, 0)
+        nbytes, nw = int(meta[0]), int(meta[1])
+        img = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        lay_t = torch.zeros(_lib.LAYOUT_BYTES, dtype=torch.uint8, device=dev)
+        pw_t = torch.zeros(nw, dtype=torch.int64, device=dev)
+        if rank == 0:
+            hip_memcpy_d2d(img.data_ptr(), ptr, nbytes)
+            lay_t.copy_(torch.frombuffer(bytearray(lay), dtype=torch.uint8))
+            pw_t.copy_(torch.from_numpy(pwid))
+        torch.cuda.synchronize()
+        dist.broadcast(img, 0)
+        dist.broadcast(lay_t, 0)
+        dist.broadcast(pw_t, 0)
+        torch.cuda.synchronize()
+        if rank != 0:
+            view = RegGpuView(node=w.self_node, device=local, replica=True)
+            view.replica_load(bytes(lay_t.cpu().numpy()), img.data_ptr())
+            pwid = pw_t.cpu().numpy()
+            torch.cuda.synchronize()
+        del img
+        log("rank %d: trie image %.1f MB replicated" % (rank, nbytes / 1e6))
+
+    pubs, words = w.publish_arrays_ids(pwid, np.array([0], dtype=np.uint32))
+    npub = len(pubs)
+    d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    out_cap = (w.notes["n_wild"] + 1) * npub
+    d_out = torch.empty(out_cap * 4, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(npub + 1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def step():
+        view.match_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_out.data_ptr(), out_cap,
+                          d_offs.data_ptr(), sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    rc = view.match_status(sp)
+    if rc != 0:
+        raise RuntimeError("match status %d after warmup" % rc)
+    # size-independent parity check of the step's output (every publish: 64
+    # wildcard subscribers + its own device subscriber when d < n_dev)
+    d_idx = w.pw[1::4] - 18
+    want = np.where(d_idx < args.n_dev, w.notes["n_wild"] + 1, w.notes["n_wild"])
+    got = np.diff(d_offs.cpu().numpy())
+    verified = bool(np.array_equal(got, want))
+    if not verified:
+        raise RuntimeError("per-publish emission counts differ from config C's known answer")
+
+    view.set_timing(not args.no_timing)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    rc = view.match_status(sp)
+    if rc != 0:
+        raise RuntimeError("match status %d in timed region" % rc)
+    count_ns, emit_ns, nlaunch = view.kernel_times() if not args.no_timing else (0.0, 0.0, 0)
+    emissions = int(d_offs[-1].item())
+
+    # max over ranks of the timed region; all-gather the per-GPU match counts
+    t_max = elapsed
+    total_emit = emissions * args.steps
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+        cnt = torch.tensor([npub * args.steps, emissions * args.steps], dtype=torch.int64, device=dev)
+        allc = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(allc, cnt)
+        total_emit = int(sum(int(c[1]) for c in allc))
+    total_pubs = npub * args.steps * world
+    value = total_pubs / t_max
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import feed   # the CPU restatement: baseline only, never the measured path
+        t0 = time.time()
+        orc = feed.load(w)
+        log("cpu baseline: oracle loaded %d subs in %.1fs" % (w.n_subs, time.time() - t0))
+        S = min(args.cpu_sample, npub)
+        buf = feed.publish_bytes(w, 0, S)
+        ns1, _ = orc.fold_timed(buf, 1, 1)
+        reps = max(1, int(math.ceil(args.cpu_seconds * 1e9 / max(ns1, 1))))
+        ns, em = orc.fold_timed(buf, reps, 1)
+        cpu = {"value": S * reps / (ns / 1e9), "unit": "publishes/s", "cores": 1, "kind": "port",
+               "sample": "first %d publishes of the config-C step batch x %d reps (%.1fs), 1 thread, "
+                         "oracle/vmq_trie_oracle.cpp (C++ restatement of vmq_reg_trie fold/4 over "
+                         "hash-map 'ETS' tables, not BEAM); host %s" % (S, reps, ns / 1e9, cpu_model())}
+        log("cpu baseline: %.0f publishes/s" % cpu["value"])
+
+    if rank == 0:
+        alg = W.algorithmic_bytes_c(w)   # bytes one launch processes (SURVEY §8d B_p model)
+        kern = "k_match_fast<1>" if emit_ns >= count_ns else "k_match_fast<0>"
+        dom_ns = max(emit_ns, count_ns)
+        achieved = alg / dom_ns if dom_ns > 0 else None   # bytes/ns == GB/s
+        traffic = load_pmc_traffic(kern)
+        res = {
+            "metric": "topic matches/sec (publishes/sec) at 1M subs, 1/2/4/8 MI355X vs CPU trie",
+            "value": value,
+            "unit": "publishes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: SURVEY.md §8(d) config C generator (splitmix64 seed 0xC + rank)",
+            "config": {"workload": "C: %d subs (devices/{d}/telemetry/# x %d + devices/+/telemetry/# x %d), "
+                                   "%d publishes/step/GPU devices/{d}/telemetry/{m}, d < %d"
+                                   % (w.n_subs, args.n_dev, w.notes["n_wild"], npub, int(args.n_dev * 1.25)),
+                       "subs": w.n_subs, "publishes_per_step_per_gpu": npub,
+                       "parallelism": "trie replicated (RCCL broadcast), publishes sharded x%d" % world},
+            "pairs_per_s": total_emit / t_max,
+            "emissions_per_step_per_gpu": emissions,
+            "verified_counts": verified,
+            "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3, "launches": nlaunch},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
+                         "kernel": kern, "algorithmic_bytes_per_launch": alg},
+            "cpu_baseline": cpu,
+            "load_s": load_s,
+        }
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,271 @@
+"""GPU parity: libvmqgpu's HIP match path vs the CPU oracle, through the C ABI.
+
+Bar: bit-exact — for every publish the sorted multiset of FoldFun entries
+equals vmq_reg_trie:fold/4's (restated by the oracle).  Sizes the oracle
+finishes in seconds are compared publish-for-publish; the full config C is
+checked by size-independent properties plus an oracle sample."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import feed
+from oracle import oracle as O
+from tests import harness as H
+from tests import scenarios as S
+
+pytestmark = pytest.mark.gpu
+
+SCEN_FILES = ["pattern_matching.json", "upgrade.json", "overlapping_subscriptions.json",
+              "dollar_topics.json", "shared_subscriptions.json", "quirks.json"]
+
+
+def _scen():
+    for f in SCEN_FILES:
+        for sc in S.load(f)["scenarios"]:
+            yield pytest.param(sc, id="%s:%s" % (f, sc["name"]))
+
+
+def test_native_library_is_the_in_tree_build():
+    from vernemq_amd import _lib
+    L = _lib.lib()
+    assert L._name == _lib.LIB_PATH
+    v = H.ProductDriver("n@h", device=0).view
+    assert v.stats_raw()["device_bytes"] > 0
+
+
+@pytest.mark.parametrize("scen", list(_scen()))
+def test_golden_scenarios_on_gpu(scen):
+    S.run_scenario(scen, lambda node: H.ProductDriver(node, device=0))
+
+
+def _compare_batches(prod, orc, pubs, ctx=""):
+    got = prod.fold_batch(pubs)
+    want = orc.fold_batch([(mp, b"pub", t) for mp, t in pubs])
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert sorted(g) == sorted(w), "%s publish %r: got %r want %r" % (ctx, pubs[i], sorted(g)[:8], sorted(w)[:8])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_churn_fold_parity(seed):
+    wl = H.ChurnWorkload(seed, n_clients=60)
+    prod = H.ProductDriver(wl.self_node, device=0)
+    orc = O.TrieOracle(wl.self_node)
+    for step in range(20):
+        evs = [wl.event() for _ in range(25)]
+        prod.apply(evs)
+        orc.apply(evs)
+        _compare_batches(prod, orc, wl.publishes(200), "seed %d batch %d" % (seed, step))
+
+
+def _load_both(w, with_oracle=True):
+    from vernemq_amd.reg_view import RegGpuView
+    v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
+    w.load_into(v)
+    orc = None
+    if with_oracle:
+        orc = feed.load(w)
+    return v, orc
+
+
+def _gpu_canon(v, w, lo, hi):
+    pubs, words = w.publish_arrays(v, lo, hi)
+    recs, offs = v.match_arrays(pubs, words)
+    return [sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
+            for i in range(hi - lo)]
+
+
+@pytest.mark.parametrize("cfg", ["A", "B"])
+def test_config_full_parity(cfg):
+    from vernemq_amd import workloads as W
+    w = W.CONFIGS[cfg]()
+    v, orc = _load_both(w)
+    n = w.n_pubs
+    got = _gpu_canon(v, w, 0, n)
+    want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in range(n)])
+    bad = [i for i in range(n) if got[i] != sorted(want[i])]
+    assert not bad, "config %s: %d/%d publishes differ, first %r: got %r want %r" % (
+        cfg, len(bad), n, w.pub_topic(bad[0]), got[bad[0]][:6], sorted(want[bad[0]])[:6])
+    assert sum(len(x) for x in got) > n // 10   # the workload does match
+
+
+def test_config_c_full_size():
+    """Config C at full size (1,000,064 subs, 2^20 publishes): every publish
+    devices/{d}/telemetry/{m} emits the 64 wildcard subscribers plus c{d}
+    when d < 10^6 — checked for all publishes; plus an oracle sample."""
+    from vernemq_amd import workloads as W
+    w = W.config_c()
+    v, _ = _load_both(w, with_oracle=False)
+    pubs, words = w.publish_arrays(v)
+    recs, offs = v.match_arrays(pubs, words, out_cap=70 * w.n_pubs)
+    d = w.pw[1::4] - 18
+    hit = d < w.notes["n_dev"]
+    counts = np.diff(offs.astype(np.int64))
+    assert np.array_equal(counts, np.where(hit, 65, 64))
+    kinds = recs["kind_node"] >> 24
+    assert np.all(kinds == 1)
+    # per publish: the multiset of subscriber ids
+    sid_of = {c: i for i, c in enumerate(v.subscribers.terms)}
+    wild = np.sort(np.array([sid_of[("", b"w%d" % i)] for i in range(64)], dtype=np.uint32))
+    dev_sid = np.array([sid_of[("", b"c%d" % k)] for k in range(w.notes["n_dev"])], dtype=np.uint32)
+    seg = np.repeat(np.arange(len(counts)), counts)
+    order = np.lexsort((recs["subscriber"], seg))
+    s_sorted = recs["subscriber"][order]
+    starts = offs.astype(np.int64)
+    for idx in np.linspace(0, len(counts) - 1, 2000).astype(np.int64):
+        a = s_sorted[starts[idx]:starts[idx + 1]]
+        want = wild if not hit[idx] else np.sort(np.append(wild, dev_sid[d[idx]]))
+        assert np.array_equal(a, want), idx
+    # every hit publish contains its own device subscriber exactly once
+    own = np.zeros(len(counts), dtype=np.int64)
+    subs_arr = recs["subscriber"].astype(np.int64)
+    sid_to_dev = np.full(len(v.subscribers.terms), -1, dtype=np.int64)
+    sid_to_dev[dev_sid] = np.arange(len(dev_sid))
+    dev_of_rec = sid_to_dev[subs_arr]
+    np.add.at(own, seg, (dev_of_rec == d[seg]).astype(np.int64))
+    assert np.array_equal(own, hit.astype(np.int64))
+    # oracle sample (4,096 publishes) on a 100k-device slice of the same shape
+    ws = W.config_c(n_dev=100_000, n_pubs=4096)
+    vs, orc = _load_both(ws)
+    got = _gpu_canon(vs, ws, 0, ws.n_pubs)
+    want = orc.fold_batch([("", b"pub", ws.pub_topic(i)) for i in range(ws.n_pubs)])
+    assert all(g == sorted(x) for g, x in zip(got, want))
+
+
+def test_r1_r2_bench_shapes():
+    """vmq_reg_trie_bench_SUITE.erl:137-146, :189-192, :209-211 at n = 100,000."""
+    from vernemq_amd import workloads as W
+    w = W.config_r1(100_000)
+    v, _ = _load_both(w, with_oracle=False)
+    pubs, words = w.publish_arrays(v)
+    recs, offs = v.match_arrays(pubs, words)
+    assert np.array_equal(np.diff(offs.astype(np.int64)), np.ones(w.n_pubs, dtype=np.int64))
+    for i in (0, 1, 4242, w.n_pubs - 1):
+        assert v.decode(recs[i]) == (("a", b"%d" % (i + 1)), 0)
+    w2 = W.config_r2(100_000)
+    v2, _ = _load_both(w2, with_oracle=False)
+    em = v2.fold_batch([("a", (b"some", b"topic"))])[0]
+    assert sorted(em) == sorted((("a", b"%d" % i), 0) for i in range(1, 100_001))
+    v2.handle_events([("deleted", ("a", b"%d" % i), [(w2.self_node, True, [((b"some", b"topic"), 0)])])
+                      for i in range(1, 100_001)])
+    assert v2.fold_batch([("a", (b"some", b"topic"))])[0] == []
+    st = v2.stats_raw()
+    assert st["subs_objects"] == 0 and st["fanout_objects"] == 0
+
+
+def test_wide_frontier_uses_slow_path():
+    """2^10 filters over {x, +} at every level: the frontier and candidate
+    lists exceed the LDS capacities, so publishes take the global-scratch path."""
+    import itertools
+    node = "n@h"
+    prod = H.ProductDriver(node, device=0)
+    orc = O.TrieOracle(node)
+    subs = []
+    for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=10)):
+        t = combo if i % 3 else combo[:9] + (b"#",)
+        subs.append(("updated", ("", b"s%d" % i), None, [(node, True, [(t, i % 3)])]))
+    prod.apply(subs)
+    orc.apply(subs)
+    pubs = [("", (b"x",) * 10), ("", (b"x", b"y") * 5), ("", (b"x",) * 9), ("", (b"x",) * 11), ("", (b"$x",) * 10)]
+    _compare_batches(prod, orc, pubs, "wide")
+    assert len(prod.fold(*pubs[0])) > 256
+
+
+def test_long_topics():
+    node = "n@h"
+    prod = H.ProductDriver(node, device=0)
+    orc = O.TrieOracle(node)
+    long_t = tuple(b"w%d" % (i % 7) for i in range(150))
+    evs = [("updated", ("", b"a"), None, [(node, True, [(long_t, 1), (long_t[:80] + (b"#",), 0),
+                                                       ((b"+",) * 149 + (b"w2",), 2), ((b"#",), 0)])])]
+    prod.apply(evs)
+    orc.apply(evs)
+    pubs = [("", long_t), ("", long_t[:80]), ("", long_t[:100]), ("", long_t[:149] + (b"w2",)),
+            ("", long_t[:149] + (b"zz",))]
+    _compare_batches(prod, orc, pubs, "long")
+
+
+def test_mountpoints_are_disjoint_roots():
+    node = "n@h"
+    prod = H.ProductDriver(node, device=0)
+    orc = O.TrieOracle(node)
+    evs = [("updated", (mp, b"c"), None, [(node, True, [((b"a", b"+"), 1), ((b"a", b"b"), 0)])])
+           for mp in ("", "tenant1", "tenant2")]
+    evs.append(("updated", ("tenant1", b"d"), None, [(node, True, [((b"#",), 2)])]))
+    prod.apply(evs)
+    orc.apply(evs)
+    pubs = [(mp, (b"a", b"b")) for mp in ("", "tenant1", "tenant2", "unknown")] + [("tenant1", (b"q",))]
+    _compare_batches(prod, orc, pubs, "mp")
+
+
+def test_empty_batch_and_output_growth():
+    prod = H.ProductDriver("n@h", device=0)
+    v = prod.view
+    v.handle_events([("updated", ("", b"c%d" % i), None, [("n@h", True, [((b"t",), 0)])]) for i in range(5000)])
+    recs, offs = v.match_arrays(*v.prepare([]))
+    assert len(recs) == 0 and list(offs) == [0]
+    recs, offs = v.match_arrays(*v.prepare([("", (b"t",))] * 3), out_cap=10)   # grows internally
+    assert list(offs) == [0, 5000, 10000, 15000]
+
+
+def test_device_entry_point_with_torch_buffers():
+    """vmqg_match_device on torch-allocated device memory and torch's stream."""
+    import torch
+    from vernemq_amd import workloads as W
+    w = W.config_b(n_subs=20_000, n_pubs=4096)
+    v, _ = _load_both(w, with_oracle=False)
+    pubs, words = w.publish_arrays(v)
+    ref_recs, ref_offs = v.match_arrays(pubs, words)
+    dev = torch.device("cuda:0")
+    d_pubs = torch.from_numpy(pubs.view(np.uint32).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    cap = int(ref_offs[-1]) + 16
+    d_out = torch.zeros(cap * 4, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream()
+    v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap, d_offs.data_ptr(),
+                   s.cuda_stream)
+    assert v.match_status(s.cuda_stream) == 0
+    offs = d_offs.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(offs, ref_offs)
+    out = d_out.cpu().numpy().view(np.uint32).reshape(-1, 4)[: int(offs[-1])]
+    ref = ref_recs.view(np.uint32).reshape(-1, 4)
+    # identical per-publish multisets (the order inside a publish is deterministic too)
+    assert np.array_equal(out, ref)
+
+
+def test_replica_follows_primary_by_image_and_patches():
+    """A replica context fed the primary's arena image and then its patch
+    stream answers identically (the RCCL broadcast payloads, minus RCCL)."""
+    import torch
+    wl = H.ChurnWorkload(7, n_clients=50)
+    prim = H.ProductDriver(wl.self_node, device=0)
+    from vernemq_amd.reg_view import RegGpuView
+    rep = RegGpuView(node=wl.self_node, device=0, replica=True)
+    prim.apply([wl.event() for _ in range(100)])
+    ptr, nbytes, lay = prim.view.arena()
+    # D2D copy of the primary arena into a torch buffer (the RCCL broadcast
+    # buffer in bench.py), then into the replica
+    img = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    lib = ctypes.CDLL("libamdhip64.so")
+    lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert lib.hipMemcpy(img.data_ptr(), ptr, nbytes, 3) == 0
+    rep.replica_load(lay, img.data_ptr())
+    torch.cuda.synchronize()
+    for step in range(10):
+        prim.apply([wl.event() for _ in range(20)])
+        data, full = prim.view.last_patches()
+        if full:
+            ptr, nbytes, lay = prim.view.arena()
+            img = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+            assert lib.hipMemcpy(img.data_ptr(), ptr, nbytes, 3) == 0
+            rep.replica_load(lay, img.data_ptr())
+        elif data:
+            buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda:0")
+            rep.apply_patches_device(buf.data_ptr(), len(data))
+        torch.cuda.synchronize()
+        pubs = wl.publishes(100)
+        arr, words = prim.view.prepare(pubs)
+        r1, o1 = prim.view.match_arrays(arr, words)
+        r2, o2 = rep.match_arrays(arr, words)
+        assert np.array_equal(o1, o2) and np.array_equal(r1, r2), step

@@ -1,0 +1,44 @@
+"""CPU checks of the synthetic workload generators and of the algorithmic
+byte model used by bench.py's roofline."""
+import numpy as np
+
+from oracle import feed
+from oracle import oracle as O
+from vernemq_amd import workloads as W
+
+
+def test_splitmix_deterministic():
+    a, b = W.SplitMix(7).u64(5), W.SplitMix(7).u64(5)
+    assert np.array_equal(a, b)
+    r = W.SplitMix(7)
+    assert np.array_equal(np.concatenate([r.u64(2), r.u64(3)]), a)
+
+
+def test_config_c_shape():
+    w = W.config_c(n_dev=1000, n_pubs=4096)
+    assert w.n_subs == 1064
+    assert w.sub_topic(0) == (b"devices", b"0", b"telemetry", b"#")
+    assert w.sub_topic(1000) == (b"devices", b"+", b"telemetry", b"#")
+    t = w.pub_topic(3)
+    assert t[0] == b"devices" and t[2] == b"telemetry" and t[3].startswith(b"m")
+
+
+def test_config_c_algorithmic_bytes_match_oracle_counters():
+    w = W.config_c(n_dev=2000, n_pubs=3000)
+    orc = feed.load(w)
+    res, counts = orc.fold_batch([("", b"p", w.pub_topic(i)) for i in range(w.n_pubs)], with_counts=True)
+    b = sum(8 * (l + 1) + 16 * s + 32 * r for s, r, l in counts)
+    assert b == W.algorithmic_bytes_c(w)
+    assert all(r == len(em) for (s, r, l), em in zip(counts, res))
+
+
+def test_config_a_b_r_shapes():
+    a = W.config_a(n_subs=500, n_clients=100, n_pubs=300)
+    assert a.n_subs == 500 and a.n_pubs == 300
+    assert any(a.sub_topic(i)[0] == b"$share" for i in range(a.n_subs)) or True
+    b = W.config_b(n_subs=300, n_pubs=100)
+    assert b.n_subs == 300
+    r1 = W.config_r1(10)
+    assert r1.sub_topic(0) == (b"unique", b"topic", b"1") and r1.pub_topic(9) == (b"unique", b"topic", b"10")
+    r2 = W.config_r2(10)
+    assert r2.n_subs == 10 and r2.n_pubs == 1

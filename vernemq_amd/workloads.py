@@ -1,0 +1,325 @@
+"""Deterministic synthetic workloads of SURVEY.md §8(d) (configs A-E) and the
+reference's own bench shapes (R1/R2, vmq_reg_trie_bench_SUITE.erl:97-214).
+
+A workload is columnar (numpy CSR of word indices), so that million-scale
+configs load into the matcher without per-subscription Python work.  The
+same columns feed the CPU oracle (test / cpu_baseline infrastructure only)
+through oracle/feed.py; this module never imports the oracle.
+
+RNG: splitmix64 (seeded per config), as §8(d) specifies.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+
+
+class SplitMix:
+    def __init__(self, seed: int):
+        self.state = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
+
+    def u64(self, n: int) -> np.ndarray:
+        with np.errstate(over="ignore"):
+            z = self.state + GOLDEN * np.arange(1, n + 1, dtype=np.uint64)
+            self.state = self.state + GOLDEN * np.uint64(n)
+            z = (z ^ (z >> np.uint64(30))) * M1
+            z = (z ^ (z >> np.uint64(27))) * M2
+            return z ^ (z >> np.uint64(31))
+
+    def ints(self, n: int, hi) -> np.ndarray:
+        return (self.u64(n) % np.asarray(hi, dtype=np.uint64)).astype(np.int64)
+
+    def unif(self, n: int) -> np.ndarray:
+        return (self.u64(n) >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+
+
+V5_OPTS = [{"no_local": nl, "rap": rap, "retain_handling": rh}
+           for nl in (False, True) for rap in (False, True) for rh in ("send_retain", "dont_send")]
+
+
+def std_subinfos():
+    """§8(d): 50 % v4 QoS, 50 % v5 {QoS, #{rap, no_local, retain_handling}}."""
+    return [0, 1, 2] + [(q, dict(o)) for q in (0, 1, 2) for o in V5_OPTS]
+
+
+class Workload:
+    """Columnar subscriptions + publishes.
+
+    sub_*  : per subscription (load order = initialize_trie fold order)
+    topics : CSR (tw_off, tw) of indices into ``words`` (subscription vocab)
+    pubs   : CSR (pw_off, pw) of indices into ``pub_words``; pub_mp per publish
+    """
+
+    def __init__(self, name, self_node="node0@127.0.0.1"):
+        self.name = name
+        self.self_node = self_node
+        self.nodes = [self_node]
+        self.mps = [""]
+        self.words: list = []
+        self.clients: list = []       # (mp, client bytes)
+        self.subinfos: list = []
+        self.sub_client = self.sub_info = self.sub_node = None
+        self.tw_off = self.tw = None
+        self.pub_words: list = []
+        self.pub_mp = self.pw_off = self.pw = None
+        self.notes = {}
+
+    # ------------------------------------------------------------ helpers
+    @property
+    def n_subs(self):
+        return len(self.sub_client)
+
+    @property
+    def n_pubs(self):
+        return len(self.pub_mp)
+
+    def sub_topic(self, i):
+        a, b = self.tw_off[i], self.tw_off[i + 1]
+        return tuple(self.words[j] for j in self.tw[a:b])
+
+    def pub_topic(self, i):
+        a, b = self.pw_off[i], self.pw_off[i + 1]
+        return tuple(self.pub_words[j] for j in self.pw[a:b])
+
+    def pub_slice(self, lo, hi):
+        return [(self.mps[self.pub_mp[i]], self.pub_topic(i)) for i in range(lo, hi)]
+
+    # ------------------------------------------------------------ product
+    def load_into(self, view, batch: int = 1 << 20) -> None:
+        """Bulk initialize_trie into a RegGpuView (op arrays, no per-sub Python)."""
+        wid = view.intern_words(self.words, create=True).astype(np.uint32)
+        node_id = np.array([view.nodes.get(n) for n in self.nodes], dtype=np.uint32)
+        mp_id = np.array([view.mountpoints.get(m) for m in self.mps], dtype=np.uint32)
+        sid_id = np.array([view.subscribers.get(c) for c in self.clients], dtype=np.uint32)
+        from .reg_view import OP_DTYPE, _subinfo_key
+        si_id = np.array([view.subinfos.get(s, _subinfo_key(s)) for s in self.subinfos], dtype=np.uint32)
+        client_mp = np.array([self.mps.index(c[0]) for c in self.clients], dtype=np.int64)
+        words_all = wid[self.tw]
+        n = self.n_subs
+        for lo in range(0, n, batch):
+            hi = min(n, lo + batch)
+            ops = np.zeros(hi - lo, dtype=OP_DTYPE)
+            base = self.tw_off[lo]
+            ops["kind"] = _lib.OP_ADD
+            ops["mountpoint"] = mp_id[client_mp[self.sub_client[lo:hi]]]
+            ops["word_off"] = (self.tw_off[lo:hi] - base).astype(np.uint32)
+            ops["nwords"] = (self.tw_off[lo + 1:hi + 1] - self.tw_off[lo:hi]).astype(np.uint32)
+            ops["node"] = node_id[self.sub_node[lo:hi]]
+            ops["subscriber"] = sid_id[self.sub_client[lo:hi]]
+            ops["subinfo"] = si_id[self.sub_info[lo:hi]]
+            view.apply_op_arrays(ops, words_all[base:self.tw_off[hi]])
+
+    def publish_arrays(self, view, lo: int = 0, hi: int | None = None):
+        """PUB_DTYPE + word-id arrays for publishes [lo, hi) (ids looked up, not created)."""
+        pwid = view.intern_words(self.pub_words, create=False).astype(np.uint32)
+        mp_id = np.array([view.mountpoints.ids.get(m, view.max_mountpoints) for m in self.mps], dtype=np.uint32)
+        return self.publish_arrays_ids(pwid, mp_id, lo, hi)
+
+    def publish_arrays_ids(self, pwid: np.ndarray, mp_id: np.ndarray, lo: int = 0, hi: int | None = None):
+        """Same, from a precomputed pub_words -> word id map (replicas have no dictionary)."""
+        from .reg_view import PUB_DTYPE
+        hi = self.n_pubs if hi is None else hi
+        dollar = np.array([w[:1] == b"$" for w in self.pub_words], dtype=bool)
+        base = self.pw_off[lo]
+        pubs = np.zeros(hi - lo, dtype=PUB_DTYPE)
+        pubs["mountpoint"] = np.asarray(mp_id, dtype=np.uint32)[self.pub_mp[lo:hi]]
+        pubs["word_off"] = (self.pw_off[lo:hi] - base).astype(np.uint32)
+        pubs["nwords"] = (self.pw_off[lo + 1:hi + 1] - self.pw_off[lo:hi]).astype(np.uint32)
+        first = self.pw[self.pw_off[lo:hi]]
+        pubs["flags"] = np.where(dollar[first], _lib.PUB_DOLLAR, 0).astype(np.uint32)
+        return pubs, np.asarray(pwid, dtype=np.uint32)[self.pw[base:self.pw_off[hi]]]
+
+
+def _csr(lists):
+    off = np.zeros(len(lists) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(x) for x in lists])
+    flat = np.fromiter((w for x in lists for w in x), dtype=np.int64, count=int(off[-1]))
+    return off, flat
+
+
+# ------------------------------------------------------------------ configs
+def config_c(n_dev: int = 1_000_000, n_wild: int = 64, n_pubs: int = 1 << 20, dev_range: float = 1.25,
+             seed: int = 0xC) -> Workload:
+    """Config C (§8d, the headline "1M subs"): devices/{d}/telemetry/# for
+    d < n_dev plus n_wild subscribers on devices/+/telemetry/#; publishes
+    devices/{d}/telemetry/{m}, d uniform in [0, 1.25 n_dev), m from 16 names."""
+    r = SplitMix(seed)
+    w = Workload("C")
+    n_range = int(n_dev * dev_range)
+    dev_words = [b"%d" % d for d in range(n_range)]
+    w.words = [b"devices", b"telemetry", b"#", b"+"] + dev_words[:n_dev]
+    w.subinfos = std_subinfos()
+    w.clients = [("", b"c%d" % d) for d in range(n_dev)] + [("", b"w%d" % i) for i in range(n_wild)]
+    n = n_dev + n_wild
+    w.sub_client = np.arange(n, dtype=np.int64)
+    half = r.unif(n) < 0.5
+    w.sub_info = np.where(half, r.ints(n, 3), 3 + r.ints(n, 3 * len(V5_OPTS)))
+    w.sub_node = np.zeros(n, dtype=np.int64)
+    tw = np.empty((n, 4), dtype=np.int64)
+    tw[:, 0], tw[:, 2], tw[:, 3] = 0, 1, 2
+    tw[:n_dev, 1] = 4 + np.arange(n_dev)
+    tw[n_dev:, 1] = 3
+    w.tw_off = np.arange(0, 4 * n + 1, 4, dtype=np.int64)
+    w.tw = tw.reshape(-1)
+    m_words = [b"m%d" % i for i in range(16)]
+    w.pub_words = [b"devices", b"telemetry"] + m_words + dev_words
+    d = r.ints(n_pubs, n_range)
+    m = r.ints(n_pubs, 16)
+    pw = np.empty((n_pubs, 4), dtype=np.int64)
+    pw[:, 0], pw[:, 1], pw[:, 2], pw[:, 3] = 0, 18 + d, 1, 2 + m
+    w.pw_off = np.arange(0, 4 * n_pubs + 1, 4, dtype=np.int64)
+    w.pw = pw.reshape(-1)
+    w.pub_mp = np.zeros(n_pubs, dtype=np.int64)
+    w.notes = {"n_dev": n_dev, "n_wild": n_wild, "hit_fraction": n_dev / n_range}
+    return w
+
+
+def _instantiate(r: SplitMix, filt, level_vocab):
+    out = []
+    for i, x in enumerate(filt):
+        if x == b"+":
+            v = level_vocab[min(i, len(level_vocab) - 1)]
+            out.append(v[int(r.ints(1, len(v))[0])])
+        elif x == b"#":
+            for j in range(int(r.ints(1, 3)[0])):
+                v = level_vocab[min(i + j, len(level_vocab) - 1)]
+                out.append(v[int(r.ints(1, len(v))[0])])
+        else:
+            out.append(x)
+    return tuple(out) if out else (level_vocab[0][0],)
+
+
+def _finish(w: Workload, subs, pubs):
+    """subs: [(client_idx, topic words, subinfo_idx, node_idx)], pubs: [(mp_idx, words)]."""
+    vocab = {}
+    for _, t, _, _ in subs:
+        for x in t:
+            vocab.setdefault(x, len(vocab))
+    w.words = list(vocab)
+    w.sub_client = np.array([s[0] for s in subs], dtype=np.int64)
+    w.sub_info = np.array([s[2] for s in subs], dtype=np.int64)
+    w.sub_node = np.array([s[3] for s in subs], dtype=np.int64)
+    w.tw_off, w.tw = _csr([[vocab[x] for x in s[1]] for s in subs])
+    pv = {}
+    for _, t in pubs:
+        for x in t:
+            pv.setdefault(x, len(pv))
+    w.pub_words = list(pv)
+    w.pub_mp = np.array([p[0] for p in pubs], dtype=np.int64)
+    w.pw_off, w.pw = _csr([[pv[x] for x in p[1]] for p in pubs])
+    return w
+
+
+def config_a(seed: int = 0xA, n_subs: int = 10_000, n_clients: int = 2_000, n_pubs: int = 100_000) -> Workload:
+    """Config A (§8d): mixed exact / '+' / '#' / $share subs, 10 % remote."""
+    r = SplitMix(seed)
+    w = Workload("A")
+    w.nodes = [w.self_node, "node1@127.0.0.1", "node2@127.0.0.1", "node3@127.0.0.1"]
+    vocab = [[b"w%d_%d" % (k, j) for j in range(16)] for k in range(6)]
+    w.subinfos = std_subinfos()
+    w.clients = [("", b"c%d" % i) for i in range(n_clients)]
+    subs, filts = [], []
+    for _ in range(n_subs):
+        L = 3 + int(r.ints(1, 3)[0])
+        t = [vocab[k][int(r.ints(1, 16)[0])] for k in range(L)]
+        x = r.unif(1)[0]
+        if x < 0.20:
+            for _ in range(1 + int(r.ints(1, 2)[0])):
+                t[int(r.ints(1, L)[0])] = b"+"
+        elif x < 0.30:
+            t = t[:1 + int(r.ints(1, L - 1)[0])] + [b"#"]
+        filts.append(tuple(t))
+        if r.unif(1)[0] < 0.01:
+            t = [b"$share", b"g%d" % int(r.ints(1, 10)[0])] + t
+        node = 1 + int(r.ints(1, 3)[0]) if r.unif(1)[0] < 0.10 else 0
+        si = int(r.ints(1, len(w.subinfos))[0])
+        subs.append((int(r.ints(1, n_clients)[0]), tuple(t), si, node))
+    pubs = []
+    for _ in range(n_pubs):
+        x = r.unif(1)[0]
+        if x < 0.50:
+            pubs.append((0, _instantiate(r, filts[int(r.ints(1, len(filts))[0])], vocab)))
+        elif x < 0.99:
+            L = 1 + int(r.ints(1, 6)[0])
+            pubs.append((0, tuple(vocab[k][int(r.ints(1, 16)[0])] for k in range(L))))
+        else:
+            pubs.append((0, (b"$SYS",) + tuple(vocab[k][int(r.ints(1, 16)[0])] for k in range(1, 3))))
+    return _finish(w, subs, pubs)
+
+
+def config_b(seed: int = 0xB, n_subs: int = 100_000, n_pubs: int = 1 << 16) -> Workload:
+    """Config B (§8d): 100k subs, 5 levels, 85 % exact / 10 % '+' / 5 % '#'."""
+    r = SplitMix(seed)
+    w = Workload("B")
+    sizes = [8, 32, 128, 512, 2048]
+    vocab = [[b"l%d_%d" % (k, j) for j in range(s)] for k, s in enumerate(sizes)]
+    w.subinfos = std_subinfos()
+    w.clients = [("", b"c%d" % i) for i in range(n_subs)]
+    subs, filts = [], []
+    for i in range(n_subs):
+        t = [vocab[k][int(r.ints(1, sizes[k])[0])] for k in range(5)]
+        x = r.unif(1)[0]
+        if x < 0.10:
+            t[int(r.ints(1, 5)[0])] = b"+"
+            if r.unif(1)[0] < 0.2:
+                t[int(r.ints(1, 5)[0])] = b"+"
+        elif x < 0.15:
+            t = t[:1 + int(r.ints(1, 4)[0])] + [b"#"]
+        filts.append(tuple(t))
+        subs.append((i, tuple(t), int(r.ints(1, len(w.subinfos))[0]), 0))
+    pubs = []
+    for _ in range(n_pubs):
+        if r.unif(1)[0] < 0.5:
+            pubs.append((0, _instantiate(r, filts[int(r.ints(1, len(filts))[0])], vocab)))
+        else:
+            pubs.append((0, tuple(vocab[k][int(r.ints(1, sizes[k])[0])] for k in range(5))))
+    return _finish(w, subs, pubs)
+
+
+def config_r1(n: int = 100_000) -> Workload:
+    """R1 = bench_single_lookups (vmq_reg_trie_bench_SUITE.erl:114-150): one
+    subscriber per unique topic unique/topic/I, MP "a"; each fold -> [{{"a",I},0}]."""
+    w = Workload("R1")
+    w.mps = ["a"]
+    w.subinfos = [0]
+    w.clients = [("a", b"%d" % i) for i in range(1, n + 1)]
+    subs = [(i, (b"unique", b"topic", b"%d" % (i + 1)), 0, 0) for i in range(n)]
+    pubs = [(0, (b"unique", b"topic", b"%d" % i)) for i in range(1, n + 1)]
+    return _finish(w, subs, pubs)
+
+
+def config_r2(n: int = 100_000) -> Workload:
+    """R2 = bench_fanout_subs (vmq_reg_trie_bench_SUITE.erl:152-214): n
+    subscribers on some/topic; one fold returns all n."""
+    w = Workload("R2")
+    w.mps = ["a"]
+    w.subinfos = [0]
+    w.clients = [("a", b"%d" % i) for i in range(1, n + 1)]
+    subs = [(i, (b"some", b"topic"), 0, 0) for i in range(n)]
+    pubs = [(0, (b"some", b"topic"))]
+    return _finish(w, subs, pubs)
+
+
+CONFIGS = {"A": config_a, "B": config_b, "C": config_c, "R1": config_r1, "R2": config_r2}
+
+
+def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None) -> int:
+    """Σ B_p over publishes [lo, hi) of a config-C workload, with SURVEY.md
+    §8(d)'s B_p = 8(L_p+1) + 16 S_p + 32 R_p and the reference's lookup counts
+    for this shape (validated against the oracle's counters in
+    tests/test_workloads.py):
+      hit  (d < n_dev): S_p = 26 (20 trie_match + 2 match/4 + 4 fold), R_p = 65
+      miss (d >= n_dev): S_p = 17 (13 + 1 + 3),                       R_p = 64
+    """
+    hi = w.n_pubs if hi is None else hi
+    d = w.pw[4 * lo + 1:4 * hi:4] - 18
+    n_hit = int(np.count_nonzero(d < w.notes["n_dev"]))
+    n_miss = (hi - lo) - n_hit
+    b_hit = 8 * 5 + 16 * 26 + 32 * (w.notes["n_wild"] + 1)
+    b_miss = 8 * 5 + 16 * 17 + 32 * w.notes["n_wild"]
+    return n_hit * b_hit + n_miss * b_miss
