@@ -13,7 +13,6 @@ its own publish batch (weak scaling, no collective on the data path); the
 per-rank emission counts are all-gathered.  Rank 0 prints ONE JSON line.
 """
 import argparse
-import ctypes
 import json
 import math
 import os
@@ -42,17 +41,9 @@ def cpu_model():
     return "unknown"
 
 
-def hip_memcpy_d2d(dst: int, src: int, n: int):
-    lib = ctypes.CDLL("libamdhip64.so")
-    lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    rc = lib.hipMemcpy(dst, src, n, 3)
-    if rc != 0:
-        raise RuntimeError("hipMemcpy D2D failed: %d" % rc)
-
-
 def load_pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_latest.json, written by profiles/collect_pmc.py), or None."""
+    (profiles/pmc_latest.json, written by tools/summarize_prof.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         d = json.load(open(p))
@@ -87,7 +78,6 @@ def main():
 
     from vernemq_amd import workloads as W
     from vernemq_amd.reg_view import RegGpuView
-    from vernemq_amd import _lib
 
     t0 = time.time()
     w = W.config_c(n_dev=args.n_dev, n_pubs=args.batch, seed=0xC + rank)   # same subs, per-rank publishes
@@ -104,31 +94,18 @@ def main():
         pwid = view.intern_words(w.pub_words, create=False).astype(np.int64)
         log("rank 0: initialize_trie of %d subs + device upload in %.1fs, stats %s" % (w.n_subs, load_s, view.stats_raw()))
     if world > 1:
-        # replicate the trie: RCCL broadcast of the device image + layout (+ the word map)
-        meta = torch.zeros(2, dtype=torch.int64, device=dev)
-        if rank == 0:
-            ptr, nbytes, lay = view.arena()
-            meta[0], meta[1] = nbytes, len(pwid)
-        dist.broadcast(meta, 0)
-        nbytes, nw = int(meta[0]), int(meta[1])
-        img = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        lay_t = torch.zeros(_lib.LAYOUT_BYTES, dtype=torch.uint8, device=dev)
-        pw_t = torch.zeros(nw, dtype=torch.int64, device=dev)
-        if rank == 0:
-            hip_memcpy_d2d(img.data_ptr(), ptr, nbytes)
-            lay_t.copy_(torch.frombuffer(bytearray(lay), dtype=torch.uint8))
-            pw_t.copy_(torch.from_numpy(pwid))
-        torch.cuda.synchronize()
-        dist.broadcast(img, 0)
-        dist.broadcast(lay_t, 0)
-        dist.broadcast(pw_t, 0)
-        torch.cuda.synchronize()
+        # replicate the trie: RCCL broadcast of the device image + layout
+        # (vernemq_amd.dist.ImageSync), then of rank 0's publish word map
+        from vernemq_amd import dist as vd
         if rank != 0:
             view = RegGpuView(node=w.self_node, device=local, replica=True)
-            view.replica_load(bytes(lay_t.cpu().numpy()), img.data_ptr())
-            pwid = pw_t.cpu().numpy()
-            torch.cuda.synchronize()
-        del img
+        sync = vd.ImageSync(dist, view, dev)
+        nbytes = sync.full()
+        pw_t = torch.zeros(len(w.pub_words), dtype=torch.int64, device=dev)
+        if rank == 0:
+            pw_t.copy_(torch.from_numpy(pwid))
+        dist.broadcast(pw_t, 0)
+        pwid = pw_t.cpu().numpy()
         log("rank %d: trie image %.1f MB replicated" % (rank, nbytes / 1e6))
 
     pubs, words = w.publish_arrays_ids(pwid, np.array([0], dtype=np.uint32))
@@ -184,10 +161,8 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
-        cnt = torch.tensor([npub * args.steps, emissions * args.steps], dtype=torch.int64, device=dev)
-        allc = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(allc, cnt)
-        total_emit = int(sum(int(c[1]) for c in allc))
+        allc = vd.gather_counts(dist, [npub * args.steps, emissions * args.steps], dev)   # per-GPU counts
+        total_emit = int(allc[:, 1].sum())
     total_pubs = npub * args.steps * world
     value = total_pubs / t_max
 

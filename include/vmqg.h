@@ -212,6 +212,10 @@ int vmqg_kernel_times(vmqg_ctx* ctx, double* count_ns, double* emit_ns, uint64_t
 #define VMQG_LAYOUT_BYTES 256
 int vmqg_arena(vmqg_ctx* ctx, void** d_ptr, uint64_t* bytes, uint8_t* layout_out);
 
+/* Primary side: copy the host mirror of the arena (byte-identical to the
+ * device image) to host memory dst (cap >= bytes from vmqg_arena). */
+int vmqg_export_image(vmqg_ctx* ctx, void* dst, uint64_t cap);
+
 /* Replica side: adopt `layout` and copy a full arena image from device memory
  * d_src (same device as ctx) on `stream`. */
 int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, void* stream);

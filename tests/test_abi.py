@@ -1,0 +1,111 @@
+"""CPU checks of the C ABI boundary (include/vmqg.h): the library loads,
+exports every declared entry point, its structs have the header's layout,
+and a host-only context fails loudly on match calls (no CPU fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from vernemq_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vmqg.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*[\w\s\*]+?\b(vmqg_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_every_declared_symbol_is_exported():
+    L = _lib.lib()
+    decl = declared_functions()
+    assert len(decl) >= 18
+    missing = [f for f in decl if not hasattr(L, f)]
+    assert not missing, missing
+    bound = {name for name, _, _ in _lib.SIGNATURES}
+    assert set(decl) == bound, set(decl) ^ bound
+    assert L.vmqg_abi_version() == 1
+
+
+def test_struct_layouts_match_header(tmp_path):
+    prog = tmp_path / "sz.c"
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "vmqg.h"\n'
+                    'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(vmqg_config),'
+                    ' sizeof(vmqg_op), sizeof(vmqg_pub), sizeof(vmqg_emit), sizeof(vmqg_stats_t),'
+                    ' offsetof(vmqg_config, hint_edges), offsetof(vmqg_op, subinfo));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(prog),
+                    "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = [ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.Op), ctypes.sizeof(_lib.Pub), ctypes.sizeof(_lib.Emit),
+            ctypes.sizeof(_lib.Stats), _lib.Config.hint_edges.offset, _lib.Op.subinfo.offset]
+    assert got == want
+    from vernemq_amd.reg_view import EMIT_DTYPE, OP_DTYPE, PUB_DTYPE
+    assert (OP_DTYPE.itemsize, PUB_DTYPE.itemsize, EMIT_DTYPE.itemsize) == (got[1], got[2], got[3])
+
+
+def test_host_only_context_refuses_to_match():
+    from vernemq_amd.reg_view import RegGpuView
+    v = RegGpuView(device=-1)
+    v.handle_event(("updated", ("", b"c"), None, [("nonode@nohost", True, [((b"a",), 0)])]))
+    with pytest.raises(_lib.VmqgError) as ei:
+        v.fold_batch([("", (b"a",))])
+    assert ei.value.rc == _lib.E_DEVICE
+
+
+def test_create_rejects_bad_config():
+    L = _lib.lib()
+    cfg = _lib.Config()
+    cfg.device = -1
+    cfg.local_node = 70
+    cfg.max_nodes = 64
+    err = ctypes.c_int(0)
+    assert not L.vmqg_create(ctypes.byref(cfg), ctypes.byref(err))
+    assert err.value == _lib.E_LIMIT
+    assert not L.vmqg_create(None, ctypes.byref(err))
+    assert err.value == _lib.E_INVAL
+
+
+def test_prepare_publish_follows_validate_topic():
+    """vmqg_prepare_publish splits and rejects exactly like
+    vmq_topic:validate_topic(publish, _) on the reference KATs."""
+    from tests import scenarios as S
+    from vernemq_amd.reg_view import RegGpuView
+    v = RegGpuView(device=-1)
+    v.intern_words([b"foo", b"baz"], create=True)
+    L = _lib.lib()
+    for c in S.load("topic_validation.json")["cases"]:
+        if c["type"] != "publish":
+            continue
+        t = c["topic"].encode()
+        words = np.zeros(64, dtype=np.uint32)
+        pub = _lib.Pub()
+        rc = L.vmqg_prepare_publish(v.handle, 0, t, len(t), words.ctypes.data, 64, ctypes.byref(pub))
+        if "ok" in c:
+            assert rc == 0 and pub.nwords == len(c["ok"]), c
+            for i, w in enumerate(c["ok"]):
+                want = v._words.get(w.encode(), _lib.WORD_UNKNOWN)
+                assert words[i] == want, (c, i)
+        else:
+            assert rc == _lib.E_INVAL, c
+    t = b"$SYS/x"
+    assert L.vmqg_prepare_publish(v.handle, 0, t, len(t), words.ctypes.data, 64, ctypes.byref(pub)) == 0
+    assert pub.flags == _lib.PUB_DOLLAR and pub.nwords == 2
+
+
+def test_intern_reserved_words():
+    from vernemq_amd.reg_view import RegGpuView
+    v = RegGpuView(device=-1)
+    L = _lib.lib()
+    blob = b"+#$sharefoo"
+    offs = np.array([0, 1, 2, 8, 11], dtype=np.uint64)
+    ids = np.zeros(4, dtype=np.uint32)
+    assert L.vmqg_intern_words(v.handle, blob, offs.ctypes.data, 4, 0, ids.ctypes.data) == 0
+    assert list(ids) == [_lib.WORD_PLUS, _lib.WORD_HASH, _lib.WORD_SHARE, _lib.WORD_UNKNOWN]
+    assert L.vmqg_intern_words(v.handle, blob, offs.ctypes.data, 4, 1, ids.ctypes.data) == 0
+    assert ids[3] == 3

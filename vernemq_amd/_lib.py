@@ -87,6 +87,7 @@ SIGNATURES = [
     ("vmqg_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
     ("vmqg_arena", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64), _P]),
+    ("vmqg_export_image", ctypes.c_int, [_P, _P, _U64]),
     ("vmqg_replica_load", ctypes.c_int, [_P, _P, _P, _P]),
     ("vmqg_last_patches", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64),
                                          ctypes.POINTER(ctypes.c_int)]),
@@ -118,6 +119,18 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB_PATH
 
 
+def _share_torch_hip_runtime():
+    """PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7) and
+    fails to initialise if the system runtime was loaded into the process
+    first.  Loading torch's copy first makes our DT_NEEDED libamdhip64.so.7
+    resolve to it, so the process has ONE HIP runtime and torch tensors,
+    streams and RCCL buffers are shared with libvmqgpu."""
+    try:
+        import torch  # noqa: F401
+    except Exception:   # no torch: the system runtime is used (e.g. an Erlang NIF host)
+        pass
+
+
 def lib():
     """Load libvmqgpu.so; raises ImportError when the native library is absent."""
     global _lib
@@ -125,6 +138,7 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError("libvmqgpu.so not built (%s); run vernemq_amd._lib.build()" % LIB_PATH)
+    _share_torch_hip_runtime()
     L = ctypes.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         f = getattr(L, name)

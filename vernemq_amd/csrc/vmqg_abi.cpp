@@ -215,6 +215,15 @@ int vmqg_arena(vmqg_ctx* ctx, void** d_ptr, uint64_t* bytes, uint8_t* layout_out
   return VMQG_OK;
 }
 
+int vmqg_export_image(vmqg_ctx* ctx, void* dst, uint64_t cap) {
+  if (!ctx || !dst) return VMQG_E_INVAL;
+  Engine& e = ctx->e;
+  if (e.replica) return VMQG_E_STATE;
+  if (cap < e.lay.total_bytes) return VMQG_E_OVERFLOW;
+  memcpy(dst, e.mirror.data(), e.lay.total_bytes);
+  return VMQG_OK;
+}
+
 int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, void* stream) {
   if (!ctx || !layout || !d_src) return VMQG_E_INVAL;
   Engine& e = ctx->e;

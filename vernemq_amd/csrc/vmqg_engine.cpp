@@ -24,6 +24,7 @@ Engine::~Engine() {
     for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (ev_match_done) hipEventDestroy(ev_match_done);
     hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_deferred); hipFree(d_scan_tmp);
+    hipFree(d_keycache);
     hipFree(d_gstack); hipFree(d_gcand); hipFree(d_gkeys);
     hipFree(d_pubs); hipFree(d_words); hipFree(d_offs); hipFree(d_out);
     if (h_patch_stage) hipHostFree(h_patch_stage);
@@ -693,6 +694,12 @@ int Engine::ensure_match_scratch(uint64_t npub) {
     scan_tmp_cap = next_pow2(need);
     if (hipMalloc(&d_scan_tmp, scan_tmp_cap * sizeof(uint64_t)) != hipSuccess) { scan_tmp_cap = 0; return VMQG_E_NOMEM; }
   }
+  if (npub > keycache_cap) {
+    if (d_keycache) hipFree(d_keycache);
+    d_keycache = nullptr;
+    keycache_cap = next_pow2(npub);
+    if (hipMalloc(&d_keycache, keycache_cap * 32) != hipSuccess) { keycache_cap = 0; return VMQG_E_NOMEM; }
+  }
   return VMQG_OK;
 }
 
@@ -714,6 +721,7 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.local_node = (uint32_t)lay.local_node;
   a.pubs = pubs; a.words = words; a.npub = npub;
   a.offsets = offs; a.out = out; a.out_cap = out_cap;
+  a.keycache = d_keycache;
   a.status = d_status; a.deferred = d_deferred; a.deferred_cap = deferred_cap; a.g_waves = g_waves;
   a.g_stack = d_gstack; a.g_cand = d_gcand; a.g_keys = d_gkeys;
   a.g_scap = g_scap; a.g_ccap = g_ccap; a.g_kcap = g_kcap;

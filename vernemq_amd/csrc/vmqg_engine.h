@@ -105,6 +105,7 @@ struct Engine {
   Patch* d_patch = nullptr; uint64_t d_patch_cap = 0;
   uint32_t* d_status = nullptr; uint32_t* d_deferred = nullptr; uint32_t deferred_cap = 65536;
   uint64_t* d_scan_tmp = nullptr; uint64_t scan_tmp_cap = 0;
+  void* d_keycache = nullptr; uint64_t keycache_cap = 0;   // publishes
   uint2* d_gstack = nullptr; uint32_t* d_gcand = nullptr; uint2* d_gkeys = nullptr;
   uint32_t g_waves = 16, g_scap = 1u << 15, g_ccap = 1u << 15, g_kcap = 1u << 15;
   // host-buffer match staging

@@ -18,6 +18,7 @@ struct MatchArgs {
   uint32_t max_mp, local_node;
   const vmqg_pub* pubs; const uint32_t* words; uint32_t npub, pad0;
   uint64_t* offsets;                              // npub + 1
+  void* keycache;                                 // npub x 32 B (COUNT -> EMIT)
   Record* out; uint64_t out_cap;
   uint32_t* status;                               // [0] deferred count, [1] error bits
   uint32_t* deferred; uint32_t deferred_cap, g_waves;

@@ -1,25 +1,27 @@
 // HIP kernels for gfx950 (MI355X): the publish -> matched-subscriber path of
 // vmq_reg_trie:fold/4 (apps/vmq_server/src/vmq_reg_trie.erl:59-98).
 //
-// One wavefront (64 lanes) owns one publish at a time (grid-stride over the
-// batch).  The wave walks the trie breadth-in-chunks: up to 64 frontier
-// entries {path, depth} are popped from an LDS stack, one per lane, and each
-// active lane issues its three edge probes ('#', the publish word, '+') as
-// independent 64-B bucket loads before resolving any of them — the
-// lookups of trie_match/4 and 'trie_match_#'/2 (:358-383) for 64 frontier
-// nodes in one memory round trip.  '#' children and end-of-topic nodes are
-// compacted (ballot + mbcnt) into an LDS candidate list; the candidates'
-// node records (match/4, :283-303) are then loaded 64 at a time and their
-// subscriber-list keys compacted into an LDS key list.  The exact-topic probe
-// (the `{Topic, node()}` candidate and get_remote_subscribers/2, :62, :514-520)
-// runs wave-uniformly.  Remote nodes are OR-ed into a 64-bit mask, which is
-// exactly the `Remotes` dedupe of fold_/5 (:78-84).
+// Work unit: a GROUP of G lanes owns one publish (G = 8 on the fast path, so
+// a 64-lane wavefront keeps 8 publishes in flight; G = 64 on the slow path).
+// The group walks the trie in chunks: up to G frontier entries {path, depth}
+// are popped from the group's LDS stack, one per lane, and each active lane
+// issues its three edge probes ('#', the publish word, '+') as independent
+// 64-B bucket loads before resolving any of them — the ets:lookup calls of
+// trie_match/4 and 'trie_match_#'/2 (:358-383), many frontier nodes and many
+// publishes per memory round trip.  '#' children and end-of-topic nodes are
+// compacted (ballot + mbcnt) into an LDS candidate list; their node records
+// (match/4, :283-303) give the subscriber-list keys, compacted into an LDS
+// key list.  The exact-topic probe (the `{Topic, node()}` candidate and
+// get_remote_subscribers/2, :62, :514-520) is a fingerprint lookup computed
+// group-parallel.  Remote nodes are OR-ed into a 64-bit mask: exactly the
+// `Remotes` dedupe of fold_/5 (:78-84).
 //
-// Two passes per batch: COUNT writes each publish's emission count, a
-// device scan turns counts into offsets, EMIT re-walks and writes the 16-B
-// records (lookup_subs + fold__, :87-98) with coalesced 1-KiB wave stores.
-// A publish whose frontier / candidate / key lists overflow LDS is deferred
-// to the SLOW instantiation (same code, scratch in global memory).
+// Passes per batch: COUNT (walk; per-publish emission count, plus a 32-B key
+// cache {total, nk, remote mask, <=2 x (record off, count)}), a device scan
+// (counts -> offsets), EMIT (records from the key cache; re-walk only for
+// publishes with > 2 keys), writing the 16-B records (lookup_subs + fold__,
+// :87-98) group-contiguously.  Publishes that overflow the LDS lists go to
+// the SLOW instantiation (G = 64, scratch in global memory).
 #include <hip/hip_runtime.h>
 
 #include "vmqg_common.h"
@@ -27,44 +29,57 @@
 
 namespace vmqg {
 
-constexpr int kWaves = 4;         // waves per 256-thread block
-constexpr uint32_t kSCap = 256;   // LDS frontier stack entries per wave
-constexpr uint32_t kCCap = 256;   // LDS candidate entries per wave
-constexpr uint32_t kKCap = 256;   // LDS key entries per wave
-
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+constexpr int kWaves = 4;          // waves per 256-thread block
+constexpr int kFastG = 8;          // lanes per publish on the fast path
+constexpr uint32_t kSCap = 64;     // LDS frontier entries per group (fast path)
+constexpr uint32_t kCCap = 32;     // LDS candidates per group
+constexpr uint32_t kKCap = 32;     // LDS keys per group
+constexpr uint32_t kRewalk = 0xFFFFFFFFu;   // key cache: EMIT must re-walk
+constexpr uint32_t kBigFanout = 256;        // records copied by the whole wave
 
 __device__ __forceinline__ uint32_t prefix_bits(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const uint32_t l = lane_id();
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t t = __shfl_up(v, o, 64);
-    if (l >= (uint32_t)o) v += t;
+// G consecutive lanes of a wavefront acting as one unit.
+template <int G>
+struct Group {
+  uint32_t lane, gidx;
+  uint64_t mask;
+  __device__ Group() {
+    const uint32_t l = __lane_id();
+    lane = l % G;
+    gidx = l / G;
+    mask = G == 64 ? ~0ull : (((1ull << G) - 1) << (gidx * G));
   }
-  return v;
-}
-
-__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+  __device__ uint64_t ballot(bool p) const { return __ballot(p) & mask; }
+  __device__ uint32_t incl_scan(uint32_t v) const {
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
-    v |= ((uint64_t)hi << 32) | lo;
+    for (int o = 1; o < G; o <<= 1) {
+      const uint32_t t = __shfl_up(v, o, G);
+      if (lane >= (uint32_t)o) v += t;
+    }
+    return v;
   }
-  return v;
-}
-
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+  __device__ uint32_t last(uint32_t v) const { return __shfl(v, G - 1, G); }
+  __device__ uint32_t bcast(uint32_t v, uint32_t src) const { return __shfl(v, (int)src, G); }
+  __device__ uint64_t or64(uint64_t v) const {
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
-    v += ((uint64_t)hi << 32) | lo;
+    for (int o = G / 2; o >= 1; o >>= 1) {
+      const uint32_t lo = __shfl_xor((uint32_t)v, o, G), hi = __shfl_xor((uint32_t)(v >> 32), o, G);
+      v |= ((uint64_t)hi << 32) | lo;
+    }
+    return v;
   }
-  return v;
-}
+  __device__ uint64_t sum64(uint64_t v) const {
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) {
+      const uint32_t lo = __shfl_xor((uint32_t)v, o, G), hi = __shfl_xor((uint32_t)(v >> 32), o, G);
+      v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+  }
+};
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 
@@ -92,62 +107,61 @@ __device__ __noinline__ uint32_t probe_rest(const EdgeSlot* t, uint64_t mask, ui
   for (uint64_t i = 0; i < mask; i++) {
     b = (b + 1) & mask;
     uint32_t c = kNone;
-    int r = scan_bucket(load_bucket(t, b), parent, word, c);
+    const int r = scan_bucket(load_bucket(t, b), parent, word, c);
     if (r == 1) return c;
     if (r == 0) return kNone;
   }
   return kNone;
 }
 
-// ------------------------------------------------------------- scratch
-template <bool SLOW>
 struct Scratch {
-  uint2* stack;   // {path, depth}
-  uint32_t* cand; // path ids
-  uint2* keys;    // key id, then {record off, cumulative start}
+  uint2* stack;    // {path, depth}
+  uint32_t* cand;  // path ids
+  uint2* keys;     // key id, then {record off, cumulative start}
   uint32_t scap, ccap, kcap;
 };
 
 enum : uint32_t { kErrDeferFull = 1u, kErrFrontier = 2u, kErrOverflow = 4u, kErrMismatch = 8u };
 
-// ------------------------------------------------------------- one publish
-template <int MODE, bool SLOW>
-__device__ void match_publish(const MatchArgs& a, uint32_t p, const Scratch<SLOW>& s) {
-  const uint32_t lane = lane_id();
-  const vmqg_pub pub = a.pubs[p];
+// Per-publish result of the walk: keys[0..nk) hold {record off, cum start}.
+struct Matched {
+  uint32_t nk, ksum, total;
+  uint64_t rmask;
+  bool overflow;
+};
+
+// ----------------------------------------------------- walk + resolution
+template <int G>
+__device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const Scratch& s, const Group<G>& g) {
   const uint32_t L = pub.nwords;
   const uint32_t* w = a.words + pub.word_off;
   const bool dollar = (pub.flags & VMQG_PUB_DOLLAR) != 0;
-  // lane i keeps word i (i < 64) in a register; deeper words come from memory
-  const uint32_t wreg = lane < L ? w[lane] : kUnknownWord;
-
-  bool overflow = false;
-  uint32_t nc = 0;   // candidates
-  uint32_t sp = 0;   // stack depth
-
-  if (pub.mountpoint < a.max_mp && L > 0) {
-    if (lane == 0) s.stack[0] = make_uint2(pub.mountpoint, 0u);  // {MP, root}
+  const bool mp_ok = pub.mountpoint < a.max_mp && L > 0;
+  // lane i of the group keeps word i (i < G); deeper words come from memory
+  const uint32_t wreg = g.lane < L ? w[g.lane] : kUnknownWord;
+  Matched m{0, 0, 0, 0, false};
+  uint32_t nc = 0, sp = 0;
+  if (mp_ok) {
+    if (g.lane == 0) s.stack[0] = make_uint2(pub.mountpoint, 0u);   // {MP, root}
     sp = 1;
   }
   wave_sync();
 
-  // ---- trie walk: trie_match/4 + 'trie_match_#'/2  (vmq_reg_trie.erl:358-383)
+  // ---- trie_match/4 + 'trie_match_#'/2  (vmq_reg_trie.erl:358-383)
   while (sp > 0) {
-    const uint32_t k = sp < 64u ? sp : 64u;
+    const uint32_t k = sp < (uint32_t)G ? sp : (uint32_t)G;
     const uint32_t base = sp - k;
-    const bool act = lane < k;
+    const bool act = g.lane < k;
     uint32_t node = 0, d = 0;
-    if (act) { const uint2 e = s.stack[base + lane]; node = e.x; d = e.y; }
+    if (act) { const uint2 e = s.stack[base + g.lane]; node = e.x; d = e.y; }
     sp = base;
     wave_sync();
     const bool at_end = act && d == L;
-    // every lane takes part in the shuffle (the source lane may be inactive)
-    const uint32_t wsh = __shfl(wreg, (int)(d & 63u), 64);
+    const uint32_t wsh = g.bcast(wreg, d % G);   // all group lanes take part
     uint32_t wd = kUnknownWord;
-    if (act && !at_end) wd = d < 64u ? wsh : w[d];
+    if (act && !at_end) wd = d < (uint32_t)G ? wsh : w[d];
     const bool do_w = act && !at_end && wd != kPlus && wd != kHash && wd != kUnknownWord;
     const bool do_p = act && !at_end;
-    // issue the three bucket loads before resolving any of them
     const uint64_t bh = edge_hash(node, kHash) & a.edge_mask;
     const uint64_t bw = edge_hash(node, wd) & a.edge_mask;
     const uint64_t bp = edge_hash(node, kPlus) & a.edge_mask;
@@ -156,23 +170,22 @@ __device__ void match_publish(const MatchArgs& a, uint32_t p, const Scratch<SLOW
     if (do_w) Bw = load_bucket(a.edges, bw);
     if (do_p) Bp = load_bucket(a.edges, bp);
     uint32_t hc = kNone, wc = kNone, pc = kNone;
-    if (act) { int r = scan_bucket(Bh, node, kHash, hc); if (r == 2) hc = probe_rest(a.edges, a.edge_mask, bh, node, kHash); }
-    if (do_w) { int r = scan_bucket(Bw, node, wd, wc); if (r == 2) wc = probe_rest(a.edges, a.edge_mask, bw, node, wd); }
-    if (do_p) { int r = scan_bucket(Bp, node, kPlus, pc); if (r == 2) pc = probe_rest(a.edges, a.edge_mask, bp, node, kPlus); }
+    if (act) { if (scan_bucket(Bh, node, kHash, hc) == 2) hc = probe_rest(a.edges, a.edge_mask, bh, node, kHash); }
+    if (do_w) { if (scan_bucket(Bw, node, wd, wc) == 2) wc = probe_rest(a.edges, a.edge_mask, bw, node, wd); }
+    if (do_p) { if (scan_bucket(Bp, node, kPlus, pc) == 2) pc = probe_rest(a.edges, a.edge_mask, bp, node, kPlus); }
 
     // candidates: the '#' child (:377-383) and, with no words left, the node itself (:361-363)
-    const uint64_t m_hc = __ballot(hc != kNone), m_end = __ballot(at_end);
-    const uint32_t n_new_c = (uint32_t)(__popcll(m_hc) + __popcll(m_end));
-    // frontier pushes: the W and '+' children (:364-375)
-    const uint64_t m_wc = __ballot(wc != kNone), m_pc = __ballot(pc != kNone);
-    const uint32_t n_new_s = (uint32_t)(__popcll(m_wc) + __popcll(m_pc));
-    if (nc + n_new_c > s.ccap || sp + n_new_s > s.scap) { overflow = true; break; }
+    const uint64_t m_hc = g.ballot(hc != kNone), m_end = g.ballot(at_end);
+    const uint32_t n_hc = (uint32_t)__popcll(m_hc), n_new_c = n_hc + (uint32_t)__popcll(m_end);
+    // frontier: the W and '+' children (:364-375)
+    const uint64_t m_wc = g.ballot(wc != kNone), m_pc = g.ballot(pc != kNone);
+    const uint32_t n_pc = (uint32_t)__popcll(m_pc), n_new_s = n_pc + (uint32_t)__popcll(m_wc);
+    if (nc + n_new_c > s.ccap || sp + n_new_s > s.scap) { m.overflow = true; break; }
     if (hc != kNone) s.cand[nc + prefix_bits(m_hc)] = hc;
-    if (at_end) s.cand[nc + __popcll(m_hc) + prefix_bits(m_end)] = node;
+    if (at_end) s.cand[nc + n_hc + prefix_bits(m_end)] = node;
     nc += n_new_c;
-    // push '+' children first so that the W branch is popped first (any order is valid)
     if (pc != kNone) s.stack[sp + prefix_bits(m_pc)] = make_uint2(pc, d + 1);
-    if (wc != kNone) s.stack[sp + __popcll(m_pc) + prefix_bits(m_wc)] = make_uint2(wc, d + 1);
+    if (wc != kNone) s.stack[sp + n_pc + prefix_bits(m_wc)] = make_uint2(wc, d + 1);
     sp += n_new_s;
     wave_sync();
   }
@@ -180,29 +193,26 @@ __device__ void match_publish(const MatchArgs& a, uint32_t p, const Scratch<SLOW
   // ---- candidates -> subscriber-list keys: match/4, match_/3 (:283-303)
   uint64_t rmask = 0;
   uint32_t nk = 0;
-  if (!overflow) {
-    for (uint32_t c0 = 0; c0 < nc; c0 += 64) {
-      const uint32_t ci = c0 + lane;
-      uint32_t nkeys = 0, key = kNone, meta = 0;
-      uint64_t rm = 0;
+  if (!m.overflow) {
+    for (uint32_t c0 = 0; c0 < nc; c0 += G) {
+      const uint32_t ci = c0 + g.lane;
+      uint32_t nkeys = 0, key = kNone;
       if (ci < nc) {
         const uint32_t path = s.cand[ci];
         if (path < a.node_cap) {
           const uint4 r = *reinterpret_cast<const uint4*>(a.nodes + path);
-          meta = r.x;
-          const bool valid = (meta & kNodeEmits) == kNodeEmits &&
-                             !(dollar && (meta & kNodeDollarSkip));  // MQTT-4.7.2-1 (:285-288)
+          const bool valid = (r.x & kNodeEmits) == kNodeEmits &&
+                             !(dollar && (r.x & kNodeDollarSkip));   // MQTT-4.7.2-1 (:285-288)
           if (valid) {
-            nkeys = meta >> 8;
+            nkeys = r.x >> 8;
             key = r.y;
-            rm = ((uint64_t)r.w << 32) | r.z;
+            rmask |= ((uint64_t)r.w << 32) | r.z;
           }
         }
       }
-      rmask |= rm;
-      const uint32_t incl = wave_incl_scan(nkeys);
-      const uint32_t tot = __shfl(incl, 63, 64);
-      if (nk + tot > s.kcap) { overflow = true; break; }
+      const uint32_t incl = g.incl_scan(nkeys);
+      const uint32_t tot = g.last(incl);
+      if (nk + tot > s.kcap) { m.overflow = true; break; }
       const uint32_t at = nk + incl - nkeys;
       if (nkeys == 1) s.keys[at] = make_uint2(key, 0u);
       else for (uint32_t j = 0; j < nkeys; j++) s.keys[at + j] = make_uint2(a.keylist[key + j], 0u);
@@ -212,10 +222,10 @@ __device__ void match_publish(const MatchArgs& a, uint32_t p, const Scratch<SLOW
   wave_sync();
 
   // ---- the exact candidate {Topic, node()} and remote exact subscribers (:62, :514-520)
-  if (!overflow && pub.mountpoint < a.max_mp) {
+  if (!m.overflow && mp_ok) {
     uint64_t part = 0;
-    for (uint32_t i = lane; i < L; i += 64) part += fp_word(i < 64 ? wreg : w[i], i);
-    const uint64_t fp = fp_final(wave_sum64(part), pub.mountpoint, L);
+    for (uint32_t i = g.lane; i < L; i += G) part += fp_word(i < (uint32_t)G ? wreg : w[i], i);
+    const uint64_t fp = fp_final(g.sum64(part), pub.mountpoint, L);
     uint64_t b = fp & a.exact_mask;
     for (uint64_t iter = 0; iter <= a.exact_mask; iter++) {
       const ExactSlot* bk = a.exact + b * kExactSlotsPerBucket;
@@ -224,15 +234,14 @@ __device__ void match_publish(const MatchArgs& a, uint32_t p, const Scratch<SLOW
         const ExactSlot e = bk[j];
         if (e.nwords == kEmpty) { seen_empty = true; break; }
         if (e.fp != fp || e.mp != pub.mountpoint || e.nwords != L) continue;
-        // exactness: compare the stored words lane-parallel
-        bool diff = false;
-        for (uint32_t i = lane; i < L; i += 64) diff |= a.exwords[e.words_off + i] != (i < 64 ? wreg : w[i]);
-        if (__ballot(diff) != 0) continue;
+        bool diff = false;   // exactness: compare the stored words group-parallel
+        for (uint32_t i = g.lane; i < L; i += G) diff |= a.exwords[e.words_off + i] != (i < (uint32_t)G ? wreg : w[i]);
+        if (g.ballot(diff) != 0) continue;
         found = true;
         rmask |= e.rmask;
         if (e.key != kNone) {
-          if (nk + 1 > s.kcap) overflow = true;
-          else { if (lane == 0) s.keys[nk] = make_uint2(e.key, 0u); nk += 1; }
+          if (nk + 1 > s.kcap) m.overflow = true;
+          else { if (g.lane == 0) s.keys[nk] = make_uint2(e.key, 0u); nk += 1; }
         }
       }
       if (found || seen_empty) break;
@@ -240,95 +249,178 @@ __device__ void match_publish(const MatchArgs& a, uint32_t p, const Scratch<SLOW
     }
   }
   wave_sync();
-  rmask = wave_or64(rmask) & ~(1ull << a.local_node);
+  m.rmask = g.or64(rmask) & ~(1ull << a.local_node);
+  if (m.overflow) return m;
 
-  if (overflow) {
-    if (MODE == 0) {
-      if (lane == 0) {
-        if (SLOW) {
-          atomicOr(&a.status[1], kErrFrontier);
-          a.offsets[p] = 0;
-        } else {
-          const uint32_t idx = atomicAdd(&a.status[0], 1u);
-          if (idx < a.deferred_cap) a.deferred[idx] = p;
-          else atomicOr(&a.status[1], kErrDeferFull);
-          a.offsets[p] = 0;
-        }
-      }
-    }
-    return;
-  }
-
-  // ---- record counts per key: lookup_subs/1 (:87-94)
+  // ---- record ranges per key: lookup_subs/1 (:87-94)
   uint32_t ksum = 0;
-  for (uint32_t k0 = 0; k0 < nk; k0 += 64) {
-    const uint32_t ki = k0 + lane;
+  for (uint32_t k0 = 0; k0 < nk; k0 += G) {
+    const uint32_t ki = k0 + g.lane;
     uint32_t cnt = 0, off = 0;
     if (ki < nk) {
       const uint32_t key = s.keys[ki].x;
       if (key < a.key_cap) { const uint2 kd = *reinterpret_cast<const uint2*>(a.keydesc + key); off = kd.x; cnt = kd.y; }
     }
-    const uint32_t incl = wave_incl_scan(cnt);
+    const uint32_t incl = g.incl_scan(cnt);
     wave_sync();
     if (ki < nk) s.keys[ki] = make_uint2(off, ksum + incl - cnt);
-    ksum += __shfl(incl, 63, 64);
+    ksum += g.last(incl);
   }
-  const uint32_t nrem = (uint32_t)__popcll(rmask);
-  const uint32_t total = ksum + nrem;
+  wave_sync();
+  m.nk = nk;
+  m.ksum = ksum;
+  m.total = ksum + (uint32_t)__popcll(m.rmask);
+  return m;
+}
 
-  if (MODE == 0) {
-    if (lane == 0) a.offsets[p] = total;
+// r-th emission of a publish whose keys are {off, cum start} in `keys`.
+__device__ __forceinline__ uint4 emission(const MatchArgs& a, const uint2* keys, uint32_t nk, uint32_t ksum,
+                                          uint64_t rmask, uint32_t r) {
+  if (r < ksum) {
+    uint32_t lo = 0, hi = nk;   // last key whose cumulative start <= r
+    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (keys[mid].y <= r) lo = mid; else hi = mid; }
+    const uint2 kk = keys[lo];
+    return *reinterpret_cast<const uint4*>(a.records + kk.x + (r - kk.y));
+  }
+  // j-th remote node of the mask, in node order (fold_/5 :78-84)
+  uint64_t m = rmask;
+  for (uint32_t j = r - ksum; j > 0; j--) m &= m - 1;
+  return make_uint4((VMQG_EMIT_REMOTE << 24) | (uint32_t)__builtin_ctzll(m), kNone, kNone, kNone);
+}
+
+__device__ __forceinline__ void store_rec(Record* out, uint64_t i, uint4 v) {
+  *reinterpret_cast<uint4*>(out + i) = v;
+}
+
+// ------------------------------------------------------------ COUNT pass
+template <int G, bool SLOW>
+__device__ void count_publish(const MatchArgs& a, uint32_t p, const Scratch& s, const Group<G>& g) {
+  const vmqg_pub pub = a.pubs[p];
+  const Matched m = walk_publish<G>(a, pub, s, g);
+  if (g.lane != 0) return;
+  uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
+  if (m.overflow) {
+    if (SLOW) {
+      atomicOr(&a.status[1], kErrFrontier);
+    } else {
+      const uint32_t idx = atomicAdd(&a.status[0], 1u);
+      if (idx < a.deferred_cap) a.deferred[idx] = p;
+      else atomicOr(&a.status[1], kErrDeferFull);
+    }
+    a.offsets[p] = 0;
+    kc[0] = make_uint4(0, kRewalk, 0, 0);
     return;
   }
-
-  // ---- EMIT: fold__/4 (:96-98) — one FoldFun argument per record
-  const uint64_t obase = a.offsets[p], oend = a.offsets[p + 1];
-  if (oend > a.out_cap) { if (lane == 0) atomicOr(&a.status[1], kErrOverflow); return; }
-  if (oend - obase != total) { if (lane == 0) atomicOr(&a.status[1], kErrMismatch); return; }
-  wave_sync();
-  for (uint32_t r = lane; r < total; r += 64) {
-    uint4 v;
-    if (r < ksum) {
-      uint32_t lo = 0, hi = nk;  // last key with cum_start <= r
-      while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (s.keys[mid].y <= r) lo = mid; else hi = mid; }
-      const uint2 kk = s.keys[lo];
-      v = *reinterpret_cast<const uint4*>(a.records + kk.x + (r - kk.y));
-    } else {
-      // j-th remote node of the mask, in node order (fold_/5 :78-84)
-      uint64_t m = rmask;
-      for (uint32_t j = r - ksum; j > 0; j--) m &= m - 1;
-      const uint32_t node = (uint32_t)__builtin_ctzll(m);
-      v = make_uint4((VMQG_EMIT_REMOTE << 24) | node, kNone, kNone, kNone);
-    }
-    *reinterpret_cast<uint4*>(a.out + obase + r) = v;
+  a.offsets[p] = m.total;
+  // key cache: total, nk, remote mask, up to two {record off, count}
+  if (m.nk <= 2) {
+    const uint2 k0 = m.nk > 0 ? s.keys[0] : make_uint2(0, 0);
+    const uint2 k1 = m.nk > 1 ? s.keys[1] : make_uint2(0, m.ksum);
+    const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
+    kc[0] = make_uint4(m.total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
+    kc[1] = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
+  } else {
+    kc[0] = make_uint4(m.total, kRewalk, 0, 0);
   }
 }
 
+// ------------------------------------------------------------- EMIT pass
+template <int G, bool SLOW>
+__device__ void emit_publish(const MatchArgs& a, uint32_t p, bool valid, const Scratch& s, const Group<G>& g) {
+  // every group of the wave reaches this function (valid or not): the big
+  // fan-out loop below is wave-wide
+  uint32_t total = 0, nk = 0, ksum = 0;
+  uint64_t rmask = 0, obase = 0;
+  bool ok = valid;
+  if (valid) {
+    const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+    const uint4 h = kc[0];
+    obase = a.offsets[p];
+    const uint64_t oend = a.offsets[p + 1];
+    if (h.y == kRewalk) {
+      const vmqg_pub pub = a.pubs[p];
+      const Matched m = walk_publish<G>(a, pub, s, g);
+      if (m.overflow) {
+        ok = false;   // handled by the slow pass (or latched as an error there)
+      } else {
+        total = m.total; nk = m.nk; ksum = m.ksum; rmask = m.rmask;
+      }
+    } else {
+      total = h.x; nk = h.y; rmask = ((uint64_t)h.w << 32) | h.z;
+      const uint4 k = kc[1];
+      ksum = k.y + k.w;
+      if (g.lane == 0) {
+        s.keys[0] = make_uint2(k.x, 0u);
+        s.keys[1] = make_uint2(k.z, k.y);
+      }
+      nk = nk < 2 ? nk : 2;
+    }
+    if (ok && oend > a.out_cap) { if (g.lane == 0) atomicOr(&a.status[1], kErrOverflow); ok = false; }
+    if (ok && oend - obase != total) { if (g.lane == 0) atomicOr(&a.status[1], kErrMismatch); ok = false; }
+  }
+  wave_sync();
+  const bool big = ok && total > kBigFanout;
+  if (ok && !big) {
+    for (uint32_t r = g.lane; r < total; r += G)
+      store_rec(a.out, obase + r, emission(a, s.keys, nk == 0 ? 1 : nk, ksum, rmask, r));
+  }
+  if (G < 64) {
+    // wave-cooperative copy of large fan-outs (lookup_subs on a fanout key)
+    uint64_t bigm = __ballot(big && g.lane == 0);
+    while (bigm) {
+      const uint32_t src = (uint32_t)__builtin_ctzll(bigm);
+      bigm &= bigm - 1;
+      const uint32_t t = __shfl(total, (int)src, 64), kn = __shfl(nk, (int)src, 64), ks = __shfl(ksum, (int)src, 64);
+      const uint64_t rm = ((uint64_t)__shfl((uint32_t)(rmask >> 32), (int)src, 64) << 32) |
+                          __shfl((uint32_t)rmask, (int)src, 64);
+      const uint64_t ob = ((uint64_t)__shfl((uint32_t)(obase >> 32), (int)src, 64) << 32) |
+                          __shfl((uint32_t)obase, (int)src, 64);
+      const uint2* keys = s.keys + (int64_t)((src / G) - g.gidx) * (int64_t)(s.kcap);
+      for (uint32_t r = __lane_id(); r < t; r += 64) store_rec(a.out, ob + r, emission(a, keys, kn == 0 ? 1 : kn, ks, rm, r));
+    }
+  } else if (big) {
+    for (uint32_t r = g.lane; r < total; r += G)
+      store_rec(a.out, obase + r, emission(a, s.keys, nk == 0 ? 1 : nk, ksum, rmask, r));
+  }
+}
+
+// --------------------------------------------------------------- kernels
 template <int MODE>
 __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
-  __shared__ uint2 st[kWaves][kSCap];
-  __shared__ uint32_t cd[kWaves][kCCap];
-  __shared__ uint2 ky[kWaves][kKCap];
+  constexpr int G = kFastG, GPW = 64 / G;   // groups per wave
+  __shared__ uint2 st[kWaves * GPW][kSCap];
+  __shared__ uint32_t cd[kWaves * GPW][kCCap];
+  __shared__ uint2 ky[kWaves * GPW][kKCap];
+  const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
-  Scratch<false> s{st[wv], cd[wv], ky[wv], kSCap, kCCap, kKCap};
-  const uint32_t nwaves = gridDim.x * kWaves;
-  for (uint32_t p = blockIdx.x * kWaves + wv; p < a.npub; p += nwaves) {
-    match_publish<MODE, false>(a, p, s);
+  const uint32_t slot = wv * GPW + g.gidx;
+  const Scratch s{st[slot], cd[slot], ky[slot], kSCap, kCCap, kKCap};
+  const uint32_t stride = gridDim.x * kWaves * GPW;
+  for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
+    const uint32_t p = base + g.gidx;
+    if (MODE == 0) {
+      if (p < a.npub) count_publish<G, false>(a, p, s, g);
+    } else {
+      emit_publish<G, false>(a, p, p < a.npub, s, g);
+    }
     wave_sync();
   }
 }
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_match_slow(MatchArgs a) {
+  const Group<64> g;
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * kWaves + wv;
-  Scratch<true> s{a.g_stack + (uint64_t)gw * a.g_scap, a.g_cand + (uint64_t)gw * a.g_ccap,
+  const Scratch s{a.g_stack + (uint64_t)gw * a.g_scap, a.g_cand + (uint64_t)gw * a.g_ccap,
                   a.g_keys + (uint64_t)gw * a.g_kcap, a.g_scap, a.g_ccap, a.g_kcap};
   uint32_t n = a.status[0];
   if (n > a.deferred_cap) n = a.deferred_cap;
   const uint32_t nwaves = gridDim.x * kWaves;
   for (uint32_t d = gw; d < n; d += nwaves) {
-    match_publish<MODE, true>(a, a.deferred[d], s);
+    const uint32_t p = a.deferred[d];
+    if (MODE == 0) count_publish<64, true>(a, p, s, g);
+    else emit_publish<64, true>(a, p, true, s, g);
     wave_sync();
   }
 }
@@ -348,7 +440,7 @@ __global__ __launch_bounds__(256) void k_scan_tiles(uint64_t* v, uint64_t n, uin
   part[threadIdx.x] = acc;
   __syncthreads();
   for (uint32_t o = 1; o < kScanBlock; o <<= 1) {
-    uint64_t t = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    const uint64_t t = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
     __syncthreads();
     part[threadIdx.x] += t;
     __syncthreads();
@@ -389,7 +481,7 @@ hipError_t launch_scan(uint64_t* v, uint64_t n, uint64_t* tmp, hipStream_t st) {
     return hipGetLastError();
   }
   k_scan_tiles<<<(uint32_t)tiles, kScanBlock, 0, st>>>(v, n, tmp);
-  hipError_t e = launch_scan(tmp, tiles, tmp + tiles, st);
+  const hipError_t e = launch_scan(tmp, tiles, tmp + tiles, st);
   if (e != hipSuccess) return e;
   k_scan_add<<<(uint32_t)tiles, kScanBlock, 0, st>>>(v, n, tmp);
   return hipGetLastError();
@@ -401,15 +493,13 @@ uint64_t scan_tmp_elems(uint64_t n) {
   return tot + 1;
 }
 
-uint32_t fast_grid(uint32_t npub) {
-  const uint32_t want = div_up(npub, kWaves);
-  const uint32_t cap = 256u * 16u;  // grid-stride beyond 16 blocks per CU
-  return want < 1 ? 1 : (want < cap ? want : cap);
-}
-
 hipError_t launch_match(const MatchArgs& a, int mode, bool slow, hipStream_t st) {
   if (!slow) {
-    const uint32_t g = fast_grid(a.npub);
+    const uint32_t per_block = kWaves * (64 / kFastG);
+    uint32_t g = div_up(a.npub, per_block);
+    const uint32_t cap = 256u * 8u;   // grid-stride beyond 8 blocks per CU
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
     if (mode == 0) k_match_fast<0><<<g, 256, 0, st>>>(a);
     else k_match_fast<1><<<g, 256, 0, st>>>(a);
   } else {

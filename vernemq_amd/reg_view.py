@@ -267,6 +267,13 @@ class RegGpuView:
         _lib.check(self._L.vmqg_arena(self._h, ctypes.byref(p), ctypes.byref(b), lay), "vmqg_arena")
         return p.value or 0, b.value, bytes(lay)
 
+    def export_image(self) -> "np.ndarray":
+        """Host copy of the arena image (primary): what replicas receive."""
+        _, nbytes, _ = self.arena()
+        img = np.empty(nbytes, dtype=np.uint8)
+        _lib.check(self._L.vmqg_export_image(self._h, img.ctypes.data, nbytes), "vmqg_export_image")
+        return img
+
     def replica_load(self, layout: bytes, d_src: int, stream: int = 0):
         lay = (ctypes.c_uint8 * _lib.LAYOUT_BYTES).from_buffer_copy(layout)
         _lib.check(self._L.vmqg_replica_load(self._h, lay, d_src, stream or None), "vmqg_replica_load")
