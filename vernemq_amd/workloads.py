@@ -308,18 +308,22 @@ def config_r2(n: int = 100_000) -> Workload:
 CONFIGS = {"A": config_a, "B": config_b, "C": config_c, "R1": config_r1, "R2": config_r2}
 
 
-def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None) -> int:
+def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None, part: str = "all") -> int:
     """Σ B_p over publishes [lo, hi) of a config-C workload, with SURVEY.md
     §8(d)'s B_p = 8(L_p+1) + 16 S_p + 32 R_p and the reference's lookup counts
     for this shape (validated against the oracle's counters in
     tests/test_workloads.py):
       hit  (d < n_dev): S_p = 26 (20 trie_match + 2 match/4 + 4 fold), R_p = 65
       miss (d >= n_dev): S_p = 17 (13 + 1 + 3),                       R_p = 64
+    part: "all" = B_p; "lookup" = 8(L_p+1) + 16 S_p (the walk, COUNT kernel);
+    "emit" = 32 R_p (record read + write, EMIT kernel).
     """
     hi = w.n_pubs if hi is None else hi
     d = w.pw[4 * lo + 1:4 * hi:4] - 18
     n_hit = int(np.count_nonzero(d < w.notes["n_dev"]))
     n_miss = (hi - lo) - n_hit
-    b_hit = 8 * 5 + 16 * 26 + 32 * (w.notes["n_wild"] + 1)
-    b_miss = 8 * 5 + 16 * 17 + 32 * w.notes["n_wild"]
-    return n_hit * b_hit + n_miss * b_miss
+    look_hit, look_miss = 8 * 5 + 16 * 26, 8 * 5 + 16 * 17
+    emit_hit, emit_miss = 32 * (w.notes["n_wild"] + 1), 32 * w.notes["n_wild"]
+    look = n_hit * look_hit + n_miss * look_miss
+    emit = n_hit * emit_hit + n_miss * emit_miss
+    return {"all": look + emit, "lookup": look, "emit": emit}[part]
