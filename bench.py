@@ -42,14 +42,19 @@ def cpu_model():
 
 
 def load_pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_latest.json, written by tools/summarize_prof.py), or None."""
+    """HBM bytes per launch of the kernel whose name starts with `kernel`
+    (e.g. "k_match_fast<1" = EMIT) from the committed rocprofv3 PMC summary
+    (profiles/pmc_latest.json, written by tools/summarize_prof.py), or None.
+    Read bytes are 2 x FETCH_SIZE (gfx950 correction), writes WRITE_SIZE."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
-        d = json.load(open(p))
-        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+        d = json.load(open(p))["kernels"]
     except (OSError, KeyError, ValueError):
         return None
+    cands = [v for k, v in d.items() if k.startswith(kernel) and "hbm_bytes_per_launch" in v]
+    if not cands:
+        return None
+    return max(cands, key=lambda v: v.get("total_ns", 0))["hbm_bytes_per_launch"]
 
 
 def main():
@@ -190,7 +195,7 @@ def main():
         alg = {"count": W.algorithmic_bytes_c(w, part="lookup"), "emit": W.algorithmic_bytes_c(w, part="emit"),
                "all": W.algorithmic_bytes_c(w)}
         dom = "emit" if emit_ns >= count_ns else "count"
-        kern = {"emit": "k_match_fast<1>", "count": "k_match_fast<0>"}[dom]
+        kern = {"emit": "k_match_fast<1", "count": "k_match_fast<0"}[dom]
         dom_ns = max(emit_ns, count_ns)
         achieved = alg[dom] / dom_ns if dom_ns > 0 else None   # bytes/ns == GB/s
         traffic = load_pmc_traffic(kern)

@@ -127,6 +127,8 @@ typedef struct vmqg_stats_s {
   uint64_t rebuilds;        /* full device-image rebuilds                   */
   uint64_t paths;           /* interned trie paths (host)                   */
   uint64_t words;           /* interned words                               */
+  uint64_t deferred_tier1;  /* publishes of the last checked match batch that  */
+  uint64_t deferred_tier2;  /* overflowed the fast / the mid LDS lists         */
 } vmqg_stats_t;
 
 /* ---- lifecycle ------------------------------------------------------- */
@@ -200,6 +202,11 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out);
  * sorted; ids printed as mp#N / node#N / sub#N / info#N).  *text is owned by
  * the context and valid until the next call on it. */
 int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
+
+/* Tuning knobs of the match kernels (no effect on results):
+ *   "fast_g"    2 | 4 | 8  lanes per publish in the fast tier (default 2)
+ *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1) */
+int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the dominant match kernel over the last
  * vmqg_match_device calls made with timing enabled (vmqg_set_timing). */

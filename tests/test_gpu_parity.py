@@ -40,7 +40,7 @@ def test_golden_scenarios_on_gpu(scen):
 
 
 def _compare_batches(prod, orc, pubs, ctx=""):
-    got = prod.fold_batch(pubs)
+    got = prod.fold_batch(pubs)   # (vmqg_match_batch checks status -> deferred counters in stats)
     want = orc.fold_batch([(mp, b"pub", t) for mp, t in pubs])
     for i, (g, w) in enumerate(zip(got, want)):
         assert sorted(g) == sorted(w), "%s publish %r: got %r want %r" % (ctx, pubs[i], sorted(g)[:8], sorted(w)[:8])
@@ -153,22 +153,29 @@ def test_r1_r2_bench_shapes():
     assert st["subs_objects"] == 0 and st["fanout_objects"] == 0
 
 
-def test_wide_frontier_uses_slow_path():
-    """2^10 filters over {x, +} at every level: the frontier and candidate
-    lists exceed the LDS capacities, so publishes take the global-scratch path."""
+@pytest.mark.parametrize("levels,tier", [(7, 1), (10, 2)])
+def test_wide_frontier_deferred_tiers(levels, tier):
+    """2^levels filters over {x, +} at every level: the frontier / candidate
+    lists overflow the fast tier's LDS lists (levels 7: the mid tier takes
+    them) or also the mid tier's (levels 10: global-memory scratch)."""
     import itertools
     node = "n@h"
     prod = H.ProductDriver(node, device=0)
     orc = O.TrieOracle(node)
     subs = []
-    for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=10)):
-        t = combo if i % 3 else combo[:9] + (b"#",)
+    for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=levels)):
+        t = combo if i % 3 else combo[:levels - 1] + (b"#",)
         subs.append(("updated", ("", b"s%d" % i), None, [(node, True, [(t, i % 3)])]))
     prod.apply(subs)
     orc.apply(subs)
-    pubs = [("", (b"x",) * 10), ("", (b"x", b"y") * 5), ("", (b"x",) * 9), ("", (b"x",) * 11), ("", (b"$x",) * 10)]
-    _compare_batches(prod, orc, pubs, "wide")
-    assert len(prod.fold(*pubs[0])) > 256
+    pubs = [("", (b"x",) * levels), ("", (b"x", b"y") * (levels // 2) + (b"x",) * (levels % 2)),
+            ("", (b"x",) * (levels - 1)), ("", (b"x",) * (levels + 1)), ("", (b"$x",) * levels)] + \
+           [("", (b"q%d" % i,)) for i in range(40)]
+    _compare_batches(prod, orc, pubs, "wide%d" % levels)
+    st = prod.view.stats_raw()
+    assert st["deferred_tier1"] >= 1
+    assert (st["deferred_tier2"] >= 1) == (tier == 2)
+    assert len(prod.fold(*pubs[0])) > 64
 
 
 def test_long_topics():

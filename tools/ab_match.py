@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of match-kernel tuning options on one device, one process
+(cdna_hip_programming.md §5.4 rule 24): config C is loaded once, each round
+runs every variant for `steps` steps; medians of the per-variant step time
+and of the COUNT / EMIT kernel times are printed as JSON."""
+import argparse
+import itertools
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--fast-g", default="4,8")
+    ap.add_argument("--nt", default="0,1")
+    ap.add_argument("--n-dev", type=int, default=1_000_000)
+    args = ap.parse_args()
+    import torch
+    from vernemq_amd import workloads as W
+    from vernemq_amd.reg_view import RegGpuView
+    dev = torch.device("cuda", 0)
+    w = W.config_c(n_dev=args.n_dev)
+    v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
+    w.load_into(v)
+    pubs, words = w.publish_arrays(v)
+    d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    cap = 66 * len(pubs)
+    d_out = torch.empty(cap * 4, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+    variants = list(itertools.product([int(x) for x in args.fast_g.split(",")],
+                                      [int(x) for x in args.nt.split(",")]))
+    res = {str(vv): {"step_us": [], "count_us": [], "emit_us": []} for vv in variants}
+    ref = None
+    for rnd in range(args.rounds):
+        for vv in variants:
+            v.set_option("fast_g", vv[0])
+            v.set_option("nt_stores", vv[1])
+            v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap,
+                           d_offs.data_ptr(), sp)
+            torch.cuda.synchronize()
+            assert v.match_status(sp) == 0
+            if ref is None:
+                ref = d_offs.clone()
+            assert torch.equal(ref, d_offs)
+            v.set_timing(True)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap,
+                               d_offs.data_ptr(), sp)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / args.steps
+            c, e, _ = v.kernel_times()
+            v.set_timing(False)
+            r = res[str(vv)]
+            r["step_us"].append(dt * 1e6)
+            r["count_us"].append(c / 1e3)
+            r["emit_us"].append(e / 1e3)
+    out = {k: {m: statistics.median(x) for m, x in d.items()} for k, d in res.items()}
+    print(json.dumps({"variants": "(fast_g, nt_stores)", "median": out, "rounds": args.rounds}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -65,7 +65,8 @@ class Emit(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("subs", "device_bytes", "trie_edges", "trie_nodes", "trie_topics", "subs_objects",
-                 "fanout_objects", "remote_keys", "epoch", "rebuilds", "paths", "words")]
+                 "fanout_objects", "remote_keys", "epoch", "rebuilds", "paths", "words",
+                 "deferred_tier1", "deferred_tier2")]
 
 
 # (name, restype, argtypes) for every entry point declared in include/vmqg.h
@@ -83,6 +84,7 @@ SIGNATURES = [
     ("vmqg_match_status", ctypes.c_int, [_P, _P]),
     ("vmqg_stats", ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
     ("vmqg_dump", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_SZ)]),
+    ("vmqg_set_option", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int64]),
     ("vmqg_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
     ("vmqg_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),

@@ -1,6 +1,7 @@
 // extern "C" boundary of libvmqgpu (include/vmqg.h).  No C++ exception and
 // no torch type crosses it; every entry point maps onto the Engine.
 #include <cstring>
+#include <string>
 #include <new>
 
 #include "vmqg_engine.h"
@@ -172,6 +173,8 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->rebuilds = e.rebuilds;
   out->paths = e.paths.size();
   out->words = e.word_text.size();
+  out->deferred_tier1 = e.last_deferred[0];
+  out->deferred_tier2 = e.last_deferred[1];
   return VMQG_OK;
 }
 
@@ -184,6 +187,21 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len) {
   *len = ctx->e.dump_text.size();
   return VMQG_OK;
   GUARD_END
+}
+
+int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
+  if (!ctx || !name) return VMQG_E_INVAL;
+  Engine& e = ctx->e;
+  const std::string n(name);
+  if (n == "fast_g") {
+    if (value != 2 && value != 4 && value != 8) return VMQG_E_INVAL;
+    e.opt_fast_g = (uint32_t)value;
+  } else if (n == "nt_stores") {
+    e.opt_flags = value ? (e.opt_flags | vmqg::kOptNtStores) : (e.opt_flags & ~vmqg::kOptNtStores);
+  } else {
+    return VMQG_E_INVAL;
+  }
+  return VMQG_OK;
 }
 
 int vmqg_set_timing(vmqg_ctx* ctx, int enable) {

@@ -5,20 +5,23 @@
 //
 // Layout of the arena (all regions 256-B aligned):
 //   edges   : open-addressed hash (parent path, word) -> child path.
-//             Buckets of 4 x 16-B slots (one 64-B line per probe).
+//             Buckets of 4 x 16-B slots (one 64-B line per probe).  The
+//             slot's 4th word caches the CHILD's edge flags (has a '#' /
+//             '+' edge), so the walk never issues a probe that must miss.
 //             This is vmq_trie (vmq_reg_trie.erl:41,43,138).
-//   nodes   : indexed by path id, 16 B.  Folds vmq_trie_node (:42,139), the
+//   nodes   : indexed by path id, 32 B.  Folds vmq_trie_node (:42,139), the
 //             vmq_trie_topic entry of the same path (:140) and the resolved
-//             subscriber-list keys of that entry into one record, so that a
-//             trie hit needs one load to know what it emits.
+//             subscriber-list keys of that entry (the first one inline as
+//             {record off, count}) into one record, so that a trie hit needs
+//             one load to know what it emits.
 //   keydesc : indexed by key id, 8 B {record offset, count} — one
 //             vmq_trie_subs key ({MP,Topic} or {MP,Group,Topic}) (:141-142).
 //   keylist : u32 pool of key ids for filters with >= 2 node entries.
 //   records : 16-B emission records (vmqg_emit) grouped per key.
-//   exact   : open-addressed hash of non-wildcard (MP, Topic) -> {local key,
-//             remote-node mask}: the `{Topic, node()}` candidate of fold/4
-//             (:62) plus vmq_trie_remote_subs (:143, :514-520).
-//   exwords : u32 pool of the exact topics' word ids (exactness check).
+//   exact   : open-addressed hash of non-wildcard (MP, Topic) -> {local key's
+//             record off + count, remote-node mask}: the `{Topic, node()}`
+//             candidate of fold/4 (:62) plus vmq_trie_remote_subs (:143, :514-520).
+//   exwords : u32 pool: per exact topic its MP then its word ids (exactness check).
 #pragma once
 #include <stdint.h>
 
@@ -42,17 +45,23 @@ constexpr uint32_t kNodeFilter = 4u;    // vmq_trie_topic entry exists for the p
 constexpr uint32_t kNodeDollarSkip = 8u;  // path is [#] or starts with + (:285-288)
 constexpr uint32_t kNodeEmits = kNodeRec | kNodeTopic | kNodeFilter;
 
-struct alignas(16) EdgeSlot { uint32_t parent, word, child, pad; };
-struct alignas(16) NodeRec { uint32_t meta, key, rmask_lo, rmask_hi; };
+// child flags cached in EdgeSlot.flags
+constexpr uint32_t kHasHash = 1u;   // the child has a '#' edge
+constexpr uint32_t kHasPlus = 2u;   // the child has a '+' edge
+constexpr uint32_t kHasAll = kHasHash | kHasPlus;
+
+struct alignas(16) EdgeSlot { uint32_t parent, word, child, flags; };
+// meta = flags | nkeys << 8; nkeys == 1: {off0, cnt0} inline; nkeys >= 2: key = keylist offset
+struct alignas(16) NodeRec { uint32_t meta, key, rmask_lo, rmask_hi, off0, cnt0, pad0, pad1; };
 struct alignas(8) KeyDesc { uint32_t off, count; };
 struct alignas(16) Record { uint32_t kind_node, group, subscriber, subinfo; };
 struct alignas(16) ExactSlot {
   uint64_t fp;
-  uint32_t mp, nwords;     // nwords == kEmpty / kTomb marks free slots
-  uint32_t key, words_off;
-  uint64_t rmask;
+  uint32_t nwords, words_off;   // nwords == kEmpty / kTomb marks free slots; exwords[words_off] = MP
+  uint32_t off, count;          // the local {MP,Topic} key's records (count 0: none)
+  uint64_t rmask;               // remote nodes with exact subscriptions
 };
-static_assert(sizeof(EdgeSlot) == 16 && sizeof(NodeRec) == 16 && sizeof(Record) == 16, "");
+static_assert(sizeof(EdgeSlot) == 16 && sizeof(NodeRec) == 32 && sizeof(Record) == 16, "");
 static_assert(sizeof(ExactSlot) == 32 && sizeof(KeyDesc) == 8, "");
 
 constexpr uint32_t kEdgeSlotsPerBucket = 4;

@@ -23,7 +23,7 @@ Engine::~Engine() {
     for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (ev_match_done) hipEventDestroy(ev_match_done);
-    hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_deferred); hipFree(d_scan_tmp);
+    hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_deferred); hipFree(d_deferred2); hipFree(d_scan_tmp);
     hipFree(d_keycache);
     hipFree(d_gstack); hipFree(d_gcand); hipFree(d_gkeys);
     hipFree(d_pubs); hipFree(d_words); hipFree(d_offs); hipFree(d_out);
@@ -58,6 +58,7 @@ int Engine::init(const vmqg_config& c) {
     has_device = true;
     if (hipMalloc(&d_status, 64) != hipSuccess) return VMQG_E_NOMEM;
     if (hipMalloc(&d_deferred, sizeof(uint32_t) * deferred_cap) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_deferred2, sizeof(uint32_t) * deferred_cap) != hipSuccess) return VMQG_E_NOMEM;
     if (hipMalloc(&d_gstack, sizeof(uint2) * (uint64_t)g_waves * g_scap) != hipSuccess) return VMQG_E_NOMEM;
     if (hipMalloc(&d_gcand, sizeof(uint32_t) * (uint64_t)g_waves * g_ccap) != hipSuccess) return VMQG_E_NOMEM;
     if (hipMalloc(&d_gkeys, sizeof(uint2) * (uint64_t)g_waves * g_kcap) != hipSuccess) return VMQG_E_NOMEM;
@@ -173,6 +174,29 @@ uint64_t Engine::edge_find(uint32_t parent, uint32_t word) {
   return ~0ull;
 }
 
+// Flags of `child` as cached in its incoming edge slot: does it have a '#'
+// edge, a '+' edge?  (Lets the walk skip probes that must miss.)
+uint32_t Engine::child_flags(uint32_t child) {
+  uint32_t f = 0;
+  if (edge_find(child, kHash) != ~0ull) f |= kHasHash;
+  if (edge_find(child, kPlus) != ~0ull) f |= kHasPlus;
+  return f;
+}
+
+// `node` gained or lost a '#' / '+' edge: refresh the flags in its incoming slot.
+void Engine::refresh_incoming_flags(uint32_t node) {
+  const PathInfo& P = paths[node];
+  if (P.parent == kNone) return;   // roots are always probed for both
+  const uint64_t si = edge_find(P.parent, P.word);
+  if (si == ~0ull) return;
+  EdgeSlot& s = region<EdgeSlot>(lay.edge_off)[si];
+  const uint32_t f = child_flags(node);
+  if (s.flags != f) {
+    s.flags = f;
+    touch(lay.edge_off + si * sizeof(EdgeSlot), sizeof(EdgeSlot));
+  }
+}
+
 void Engine::edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
   if (edge_find(parent, word) != ~0ull) return;   // ets:insert of an identical #trie{}
   EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
@@ -184,9 +208,10 @@ void Engine::edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
       EdgeSlot& s = t[si];
       if (s.parent == kEmpty || s.parent == kTomb) {
         if (s.parent == kTomb) edge_tomb--;
-        s = EdgeSlot{parent, word, child, 0};
+        s = EdgeSlot{parent, word, child, child_flags(child)};
         edge_live++;
         touch(lay.edge_off + si * sizeof(EdgeSlot), sizeof(EdgeSlot));
+        if (word == kHash || word == kPlus) refresh_incoming_flags(parent);
         return;
       }
     }
@@ -200,6 +225,7 @@ void Engine::edge_erase(uint32_t parent, uint32_t word) {
   t[si] = EdgeSlot{kTomb, kTomb, kTomb, 0};
   edge_live--; edge_tomb++;
   touch(lay.edge_off + si * sizeof(EdgeSlot), sizeof(EdgeSlot));
+  if (word == kHash || word == kPlus) refresh_incoming_flags(parent);
 }
 
 Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale) const {
@@ -212,7 +238,7 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale) const {
   for (auto& p : paths) if (p.filter && p.nodes.size() >= 2) kl += p.nodes.size();
   for (auto& t : topics) {
     const bool has = t.exact_ok && ((t.local_key != kNone && !keys[t.local_key].vals.empty()) || !t.remote.empty());
-    if (has) { ex++; xw += t.words.size(); }
+    if (has) { ex++; xw += t.words.size() + 1; }
   }
   const uint64_t edges_need = edge_live + extra_edges;
   const uint64_t edge_slots = next_pow2(std::max<uint64_t>(4096, std::max<uint64_t>(edges_need * 2, cfg.hint_edges * 2)));
@@ -264,8 +290,8 @@ void Engine::rebuild(uint64_t extra_edges) {
     for (auto& t : topics) { t.slot = ~0ull; t.words_off = kNone; }
     for (auto& p : paths) p.kl_n = 0;
     bool ok = true;
-    for (uint32_t p = 0; ok && p < paths.size(); p++) ok = write_path(p);
     for (uint32_t k = 0; ok && k < keys.size(); k++) ok = write_key(k);
+    for (uint32_t p = 0; ok && p < paths.size(); p++) ok = write_path(p);
     for (uint32_t t = 0; ok && t < topics.size(); t++) ok = write_topic(t);
     if (ok) break;
   }
@@ -299,7 +325,7 @@ bool Engine::write_key(uint32_t k) {
 bool Engine::write_path(uint32_t p) {
   if (p >= lay.node_cap) return false;
   PathInfo& P = paths[p];
-  NodeRec r{0, kNone, 0, 0};
+  NodeRec r{0, kNone, 0, 0, 0, 0, 0, 0};
   uint32_t flags = 0;
   if (P.rec) flags |= kNodeRec;
   if (P.rec && P.topic_set) flags |= kNodeTopic;
@@ -308,16 +334,25 @@ bool Engine::write_path(uint32_t p) {
   std::vector<uint32_t> ks;
   uint64_t rmask = 0;
   if (P.filter) {
-    // match_/3 (:301-303): one candidate per node-list entry
+    // match_/3 (:301-303): one candidate per node-list entry; a key that does
+    // not exist in vmq_trie_subs contributes nothing (lookup_subs -> [])
     for (auto& e : P.nodes) {
-      if (e.first.group != kNone) ks.push_back(group_key(P.topic_id, e.first.group, true));   // :68-72
-      else if (e.first.node == cfg.local_node) ks.push_back(local_key(P.topic_id, true));     // :73-77
-      else rmask |= 1ull << e.first.node;                                                      // :78-84
+      if (e.first.group != kNone) {                                                   // :68-72
+        const uint32_t k = group_key(P.topic_id, e.first.group, false);
+        if (k != kNone) ks.push_back(k);
+      } else if (e.first.node == cfg.local_node) {                                     // :73-77
+        const uint32_t k = local_key(P.topic_id, false);
+        if (k != kNone) ks.push_back(k);
+      } else {
+        rmask |= 1ull << e.first.node;                                                 // :78-84
+      }
     }
   }
-  if (keys.size() > lay.key_cap) return false;
-  if (ks.size() == 1) r.key = ks[0];
-  else if (ks.size() >= 2) {
+  if (ks.size() == 1) {
+    r.key = ks[0];
+    r.off0 = (uint32_t)keys[ks[0]].off;
+    r.cnt0 = (uint32_t)keys[ks[0]].vals.size();
+  } else if (ks.size() >= 2) {
     if (kl_top + ks.size() > lay.keylist_cap) return false;
     kl_garbage += P.kl_n;
     r.key = (uint32_t)kl_top;
@@ -341,7 +376,8 @@ uint64_t Engine::exact_fp(const TopicInfo& t) const {
 
 bool Engine::write_topic(uint32_t ti) {
   TopicInfo& t = topics[ti];
-  const bool has = t.exact_ok && ((t.local_key != kNone && !keys[t.local_key].vals.empty()) || !t.remote.empty());
+  const bool local = t.local_key != kNone && !keys[t.local_key].vals.empty();
+  const bool has = t.exact_ok && (local || !t.remote.empty());
   ExactSlot* tab = region<ExactSlot>(lay.exact_off);
   if (!has) {
     if (t.slot != ~0ull) {
@@ -349,7 +385,7 @@ bool Engine::write_topic(uint32_t ti) {
       s.nwords = kTomb;
       touch(lay.exact_off + t.slot * sizeof(ExactSlot), sizeof(ExactSlot));
       t.slot = ~0ull;
-      xw_garbage += t.words.size();
+      xw_garbage += t.words.size() + 1;
       t.words_off = kNone;
       exact_live--; exact_tomb++;
     }
@@ -357,14 +393,15 @@ bool Engine::write_topic(uint32_t ti) {
   }
   uint64_t rmask = 0;
   for (auto& r : t.remote) rmask |= 1ull << r.first;
-  const uint32_t key = (t.local_key != kNone && !keys[t.local_key].vals.empty()) ? t.local_key : kNone;
   if (t.slot == ~0ull) {
     if ((exact_live + exact_tomb + 1) * 10 > lay.exact_buckets * kExactSlotsPerBucket * 7) return false;
-    if (xw_top + t.words.size() > lay.exwords_cap) return false;
+    if (xw_top + t.words.size() + 1 > lay.exwords_cap) return false;
     t.words_off = (uint32_t)xw_top;
-    memcpy(region<uint32_t>(lay.exwords_off) + xw_top, t.words.data(), t.words.size() * 4);
-    touch(lay.exwords_off + xw_top * 4, t.words.size() * 4);
-    xw_top += t.words.size();
+    uint32_t* xw = region<uint32_t>(lay.exwords_off) + xw_top;
+    xw[0] = t.mp;
+    memcpy(xw + 1, t.words.data(), t.words.size() * 4);
+    touch(lay.exwords_off + xw_top * 4, (t.words.size() + 1) * 4);
+    xw_top += t.words.size() + 1;
     const uint64_t fp = exact_fp(t);
     const uint64_t mask = lay.exact_buckets - 1;
     uint64_t b = fp & mask;
@@ -378,7 +415,8 @@ bool Engine::write_topic(uint32_t ti) {
         if (tab[found].nwords == kTomb) exact_tomb--;
         exact_live++;
         t.slot = found;
-        tab[found].fp = fp; tab[found].mp = t.mp; tab[found].nwords = (uint32_t)t.words.size();
+        tab[found].fp = fp;
+        tab[found].nwords = (uint32_t)t.words.size();
         tab[found].words_off = t.words_off;
         break;
       }
@@ -386,16 +424,23 @@ bool Engine::write_topic(uint32_t ti) {
     }
   }
   ExactSlot& s = tab[t.slot];
-  s.key = key;
+  s.off = local ? (uint32_t)keys[t.local_key].off : 0;
+  s.count = local ? (uint32_t)keys[t.local_key].vals.size() : 0;
   s.rmask = rmask;
   touch(lay.exact_off + t.slot * sizeof(ExactSlot), sizeof(ExactSlot));
   return true;
 }
 
 bool Engine::flush_incremental() {
-  // paths first: resolving a node list may (defensively) create a key
+  // keys first (record ranges), then the paths and exact slots that inline them
+  for (size_t i = 0; i < dirty_keys.size(); i++) {
+    const uint32_t k = dirty_keys[i];
+    if (!write_key(k)) return false;
+    const TopicInfo& t = topics[keys[k].topic_id];
+    if (t.path != kNone) mark_path(t.path);
+    if (keys[k].group == kNone) mark_topic(keys[k].topic_id);
+  }
   for (size_t i = 0; i < dirty_paths.size(); i++) if (!write_path(dirty_paths[i])) return false;
-  for (size_t i = 0; i < dirty_keys.size(); i++) if (!write_key(dirty_keys[i])) return false;
   for (size_t i = 0; i < dirty_topics.size(); i++) if (!write_topic(dirty_topics[i])) return false;
   return true;
 }
@@ -441,7 +486,10 @@ void Engine::add_complex_topic(uint32_t mp, const uint32_t* w, uint32_t L, Nog n
   std::vector<uint32_t> chain;
   path_chain(mp, w, L, true, chain);
   const uint32_t p = chain[L];
-  if (paths[p].topic_id == kNone) paths[p].topic_id = topic_id(mp, w, L, true);
+  if (paths[p].topic_id == kNone) {
+    paths[p].topic_id = topic_id(mp, w, L, true);
+    topics[paths[p].topic_id].path = p;
+  }
   PathInfo& P = paths[p];
   if (!P.filter) { P.filter = 1; P.total = 1; P.nodes.assign(1, {nog, 1}); n_trie_topics++; }  // :321-323
   else { add_and_inc(P.nodes, nog); P.total++; }                                                  // :324-326
@@ -722,9 +770,11 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.pubs = pubs; a.words = words; a.npub = npub;
   a.offsets = offs; a.out = out; a.out_cap = out_cap;
   a.keycache = d_keycache;
-  a.status = d_status; a.deferred = d_deferred; a.deferred_cap = deferred_cap; a.g_waves = g_waves;
+  a.status = d_status; a.deferred = d_deferred; a.deferred2 = d_deferred2;
+  a.deferred_cap = deferred_cap; a.g_waves = g_waves;
   a.g_stack = d_gstack; a.g_cand = d_gcand; a.g_keys = d_gkeys;
   a.g_scap = g_scap; a.g_ccap = g_ccap; a.g_kcap = g_kcap;
+  a.fast_g = opt_fast_g; a.opts = opt_flags;
   return a;
 }
 
@@ -737,21 +787,24 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   int rc = ensure_match_scratch(npub);
   if (rc) return rc;
   const MatchArgs a = args_for(d_pubs_, npub, d_words_, d_out_, out_cap, d_offsets);
-  if (hipMemsetAsync(d_status, 0, 8, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipMemsetAsync(d_status, 0, 16, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipMemsetAsync(d_offsets + npub, 0, 8, st) != hipSuccess) return VMQG_E_DEVICE;
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
   if (timing) {
     hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2); hipEventCreate(&e3);
     hipEventRecord(e0, st);
   }
-  if (npub && launch_match(a, 0, false, st) != hipSuccess) return VMQG_E_DEVICE;
+  // COUNT: fast tier, then the tiers that take what the previous one deferred
+  if (npub && launch_match(a, 0, 0, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) hipEventRecord(e1, st);
-  if (npub && launch_match(a, 0, true, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (npub && launch_match(a, 0, 1, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (npub && launch_match(a, 0, 2, st) != hipSuccess) return VMQG_E_DEVICE;
   if (launch_scan(d_offsets, (uint64_t)npub + 1, d_scan_tmp, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) hipEventRecord(e2, st);
-  if (npub && launch_match(a, 1, false, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (npub && launch_match(a, 1, 0, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) { hipEventRecord(e3, st); t_count.push_back({e0, e1}); t_emit.push_back({e2, e3}); }
-  if (npub && launch_match(a, 1, true, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (npub && launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (npub && launch_match(a, 1, 2, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
@@ -760,10 +813,12 @@ int Engine::match_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
   if (!st) st = stream;
-  uint32_t h[2] = {0, 0};
-  if (hipMemcpyAsync(h, d_status, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
+  uint32_t h[4] = {0, 0, 0, 0};
+  if (hipMemcpyAsync(h, d_status, 16, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
-  if (hipMemsetAsync(d_status, 0, 8, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipMemsetAsync(d_status, 0, 16, st) != hipSuccess) return VMQG_E_DEVICE;
+  last_deferred[0] = h[0];
+  last_deferred[1] = h[2];
   if (h[1] & (2u | 1u)) return VMQG_E_FRONTIER;
   if (h[1] & 4u) return VMQG_E_OVERFLOW;
   if (h[1] & 8u) return VMQG_E_DEVICE;

@@ -60,6 +60,7 @@ struct TopicInfo {
   uint32_t mp;
   std::vector<uint32_t> words;
   uint32_t local_key = kNone;
+  uint32_t path = kNone;            // trie path of the same (MP, Topic), once created
   uint8_t dirty = 0, exact_ok = 0;
   std::vector<std::pair<uint32_t, int64_t>> remote;
   uint64_t slot = ~0ull;
@@ -103,7 +104,8 @@ struct Engine {
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
   Patch* h_patch_stage = nullptr; uint64_t h_patch_cap = 0;
   Patch* d_patch = nullptr; uint64_t d_patch_cap = 0;
-  uint32_t* d_status = nullptr; uint32_t* d_deferred = nullptr; uint32_t deferred_cap = 65536;
+  uint32_t* d_status = nullptr; uint32_t* d_deferred = nullptr; uint32_t* d_deferred2 = nullptr;
+  uint32_t deferred_cap = 1u << 20;
   uint64_t* d_scan_tmp = nullptr; uint64_t scan_tmp_cap = 0;
   void* d_keycache = nullptr; uint64_t keycache_cap = 0;   // publishes
   uint2* d_gstack = nullptr; uint32_t* d_gcand = nullptr; uint2* d_gkeys = nullptr;
@@ -115,6 +117,8 @@ struct Engine {
   void* d_out = nullptr; uint64_t d_out_cap = 0;
   hipEvent_t ev_match_done = nullptr;
   bool timing = false;
+  uint32_t opt_fast_g = 2, opt_flags = kOptNtStores;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
+  uint32_t last_deferred[2] = {0, 0};   // tier-1 / tier-2 publishes of the last checked batch
   std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_emit;
   double sum_count_ns = 0, sum_emit_ns = 0; uint64_t n_timed = 0;
 
@@ -152,6 +156,8 @@ struct Engine {
   uint64_t edge_find(uint32_t parent, uint32_t word) ;
   void edge_insert(uint32_t parent, uint32_t word, uint32_t child);
   void edge_erase(uint32_t parent, uint32_t word);
+  uint32_t child_flags(uint32_t child);
+  void refresh_incoming_flags(uint32_t node);
   Layout plan_layout(uint64_t extra_edges, uint32_t scale) const;
   void rebuild(uint64_t extra_edges);
   bool flush_incremental();

@@ -30,12 +30,9 @@
 namespace vmqg {
 
 constexpr int kWaves = 4;          // waves per 256-thread block
-constexpr int kFastG = 8;          // lanes per publish on the fast path
-constexpr uint32_t kSCap = 64;     // LDS frontier entries per group (fast path)
-constexpr uint32_t kCCap = 32;     // LDS candidates per group
-constexpr uint32_t kKCap = 32;     // LDS keys per group
+// fast-tier LDS lists per group, sized so a block stays near 28 KiB
+template <int G> struct FastCaps { static constexpr uint32_t S = 8 * G, C = 4 * G, K = 4 * G; };
 constexpr uint32_t kRewalk = 0xFFFFFFFFu;   // key cache: EMIT must re-walk
-constexpr uint32_t kBigFanout = 256;        // records copied by the whole wave
 
 __device__ __forceinline__ uint32_t prefix_bits(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -91,28 +88,42 @@ __device__ __forceinline__ Bucket load_bucket(const EdgeSlot* t, uint64_t b) {
   return Bucket{p[0], p[1], p[2], p[3]};
 }
 
-// 1 = found (child set), 0 = absent (an empty slot ends the chain), 2 = go on
-__device__ __forceinline__ int scan_bucket(const Bucket& B, uint32_t parent, uint32_t word, uint32_t& child) {
-  if (B.s0.x == parent && B.s0.y == word) { child = B.s0.z; return 1; }
-  if (B.s1.x == parent && B.s1.y == word) { child = B.s1.z; return 1; }
-  if (B.s2.x == parent && B.s2.y == word) { child = B.s2.z; return 1; }
-  if (B.s3.x == parent && B.s3.y == word) { child = B.s3.z; return 1; }
+// 1 = found (child + the child's edge flags set), 0 = absent (an empty slot
+// ends the chain), 2 = go on with the next bucket
+__device__ __forceinline__ int scan_bucket(const Bucket& B, uint32_t parent, uint32_t word, uint32_t& child,
+                                           uint32_t& cflags) {
+  if (B.s0.x == parent && B.s0.y == word) { child = B.s0.z; cflags = B.s0.w; return 1; }
+  if (B.s1.x == parent && B.s1.y == word) { child = B.s1.z; cflags = B.s1.w; return 1; }
+  if (B.s2.x == parent && B.s2.y == word) { child = B.s2.z; cflags = B.s2.w; return 1; }
+  if (B.s3.x == parent && B.s3.y == word) { child = B.s3.z; cflags = B.s3.w; return 1; }
   if (B.s0.x == kEmpty || B.s1.x == kEmpty || B.s2.x == kEmpty || B.s3.x == kEmpty) return 0;
   return 2;
 }
 
 // Continue a probe chain from bucket b+1 (rare: the first bucket was full).
-__device__ __noinline__ uint32_t probe_rest(const EdgeSlot* t, uint64_t mask, uint64_t b, uint32_t parent,
-                                            uint32_t word) {
+__device__ __noinline__ uint2 probe_rest(const EdgeSlot* t, uint64_t mask, uint64_t b, uint32_t parent,
+                                         uint32_t word) {
   for (uint64_t i = 0; i < mask; i++) {
     b = (b + 1) & mask;
-    uint32_t c = kNone;
-    const int r = scan_bucket(load_bucket(t, b), parent, word, c);
-    if (r == 1) return c;
-    if (r == 0) return kNone;
+    uint32_t c = kNone, f = 0;
+    const int r = scan_bucket(load_bucket(t, b), parent, word, c, f);
+    if (r == 1) return make_uint2(c, f);
+    if (r == 0) break;
   }
-  return kNone;
+  return make_uint2(kNone, 0u);
 }
+
+__device__ __forceinline__ void probe(const EdgeSlot* t, uint64_t mask, uint64_t b, const Bucket& B,
+                                      uint32_t parent, uint32_t word, uint32_t& child, uint32_t& cflags) {
+  if (scan_bucket(B, parent, word, child, cflags) == 2) {
+    const uint2 r = probe_rest(t, mask, b, parent, word);
+    child = r.x;
+    cflags = r.y;
+  }
+}
+
+constexpr uint32_t kDepthMask = 0x0FFFFFFFu;   // frontier entry: {path, depth | child flags << 28}
+constexpr uint32_t kUnresolved = 0xFFFFFFFFu;  // key list entry still holds a key id
 
 struct Scratch {
   uint2* stack;    // {path, depth}
@@ -142,7 +153,7 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
   Matched m{0, 0, 0, 0, false};
   uint32_t nc = 0, sp = 0;
   if (mp_ok) {
-    if (g.lane == 0) s.stack[0] = make_uint2(pub.mountpoint, 0u);   // {MP, root}
+    if (g.lane == 0) s.stack[0] = make_uint2(pub.mountpoint, kHasAll << 28);   // {MP, root}: probe all
     sp = 1;
   }
   wave_sync();
@@ -152,27 +163,29 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
     const uint32_t k = sp < (uint32_t)G ? sp : (uint32_t)G;
     const uint32_t base = sp - k;
     const bool act = g.lane < k;
-    uint32_t node = 0, d = 0;
-    if (act) { const uint2 e = s.stack[base + g.lane]; node = e.x; d = e.y; }
+    uint32_t node = 0, d = 0, fl = 0;
+    if (act) { const uint2 e = s.stack[base + g.lane]; node = e.x; d = e.y & kDepthMask; fl = e.y >> 28; }
     sp = base;
     wave_sync();
     const bool at_end = act && d == L;
     const uint32_t wsh = g.bcast(wreg, d % G);   // all group lanes take part
     uint32_t wd = kUnknownWord;
     if (act && !at_end) wd = d < (uint32_t)G ? wsh : w[d];
+    // the node's cached edge flags skip '#' / '+' probes that must miss
+    const bool do_h = act && (fl & kHasHash);
     const bool do_w = act && !at_end && wd != kPlus && wd != kHash && wd != kUnknownWord;
-    const bool do_p = act && !at_end;
+    const bool do_p = act && !at_end && (fl & kHasPlus);
     const uint64_t bh = edge_hash(node, kHash) & a.edge_mask;
     const uint64_t bw = edge_hash(node, wd) & a.edge_mask;
     const uint64_t bp = edge_hash(node, kPlus) & a.edge_mask;
     Bucket Bh{}, Bw{}, Bp{};
-    if (act) Bh = load_bucket(a.edges, bh);
+    if (do_h) Bh = load_bucket(a.edges, bh);
     if (do_w) Bw = load_bucket(a.edges, bw);
     if (do_p) Bp = load_bucket(a.edges, bp);
-    uint32_t hc = kNone, wc = kNone, pc = kNone;
-    if (act) { if (scan_bucket(Bh, node, kHash, hc) == 2) hc = probe_rest(a.edges, a.edge_mask, bh, node, kHash); }
-    if (do_w) { if (scan_bucket(Bw, node, wd, wc) == 2) wc = probe_rest(a.edges, a.edge_mask, bw, node, wd); }
-    if (do_p) { if (scan_bucket(Bp, node, kPlus, pc) == 2) pc = probe_rest(a.edges, a.edge_mask, bp, node, kPlus); }
+    uint32_t hc = kNone, wc = kNone, pc = kNone, hf = 0, wf = 0, pf = 0;
+    if (do_h) probe(a.edges, a.edge_mask, bh, Bh, node, kHash, hc, hf);
+    if (do_w) probe(a.edges, a.edge_mask, bw, Bw, node, wd, wc, wf);
+    if (do_p) probe(a.edges, a.edge_mask, bp, Bp, node, kPlus, pc, pf);
 
     // candidates: the '#' child (:377-383) and, with no words left, the node itself (:361-363)
     const uint64_t m_hc = g.ballot(hc != kNone), m_end = g.ballot(at_end);
@@ -184,8 +197,8 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
     if (hc != kNone) s.cand[nc + prefix_bits(m_hc)] = hc;
     if (at_end) s.cand[nc + n_hc + prefix_bits(m_end)] = node;
     nc += n_new_c;
-    if (pc != kNone) s.stack[sp + prefix_bits(m_pc)] = make_uint2(pc, d + 1);
-    if (wc != kNone) s.stack[sp + n_pc + prefix_bits(m_wc)] = make_uint2(wc, d + 1);
+    if (pc != kNone) s.stack[sp + prefix_bits(m_pc)] = make_uint2(pc, (d + 1) | (pf << 28));
+    if (wc != kNone) s.stack[sp + n_pc + prefix_bits(m_wc)] = make_uint2(wc, (d + 1) | (wf << 28));
     sp += n_new_s;
     wave_sync();
   }
@@ -196,16 +209,19 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
   if (!m.overflow) {
     for (uint32_t c0 = 0; c0 < nc; c0 += G) {
       const uint32_t ci = c0 + g.lane;
-      uint32_t nkeys = 0, key = kNone;
+      uint32_t nkeys = 0, key = kNone, off0 = 0, cnt0 = 0;
       if (ci < nc) {
         const uint32_t path = s.cand[ci];
         if (path < a.node_cap) {
           const uint4 r = *reinterpret_cast<const uint4*>(a.nodes + path);
+          const uint2 r2 = *reinterpret_cast<const uint2*>(&a.nodes[path].off0);
           const bool valid = (r.x & kNodeEmits) == kNodeEmits &&
                              !(dollar && (r.x & kNodeDollarSkip));   // MQTT-4.7.2-1 (:285-288)
           if (valid) {
             nkeys = r.x >> 8;
             key = r.y;
+            off0 = r2.x;
+            cnt0 = r2.y;
             rmask |= ((uint64_t)r.w << 32) | r.z;
           }
         }
@@ -214,8 +230,8 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
       const uint32_t tot = g.last(incl);
       if (nk + tot > s.kcap) { m.overflow = true; break; }
       const uint32_t at = nk + incl - nkeys;
-      if (nkeys == 1) s.keys[at] = make_uint2(key, 0u);
-      else for (uint32_t j = 0; j < nkeys; j++) s.keys[at + j] = make_uint2(a.keylist[key + j], 0u);
+      if (nkeys == 1) s.keys[at] = make_uint2(off0, cnt0);   // resolved inline
+      else for (uint32_t j = 0; j < nkeys; j++) s.keys[at + j] = make_uint2(a.keylist[key + j], kUnresolved);
       nk += tot;
     }
   }
@@ -233,15 +249,17 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
       for (uint32_t j = 0; j < kExactSlotsPerBucket && !found; j++) {
         const ExactSlot e = bk[j];
         if (e.nwords == kEmpty) { seen_empty = true; break; }
-        if (e.fp != fp || e.mp != pub.mountpoint || e.nwords != L) continue;
-        bool diff = false;   // exactness: compare the stored words group-parallel
-        for (uint32_t i = g.lane; i < L; i += G) diff |= a.exwords[e.words_off + i] != (i < (uint32_t)G ? wreg : w[i]);
+        if (e.fp != fp || e.nwords != L) continue;
+        // exactness: the stored MP and words, compared group-parallel
+        const uint32_t* xw = a.exwords + e.words_off;
+        bool diff = g.lane == 0 && xw[0] != pub.mountpoint;
+        for (uint32_t i = g.lane; i < L; i += G) diff |= xw[1 + i] != (i < (uint32_t)G ? wreg : w[i]);
         if (g.ballot(diff) != 0) continue;
         found = true;
         rmask |= e.rmask;
-        if (e.key != kNone) {
+        if (e.count != 0) {
           if (nk + 1 > s.kcap) m.overflow = true;
-          else { if (g.lane == 0) s.keys[nk] = make_uint2(e.key, 0u); nk += 1; }
+          else { if (g.lane == 0) s.keys[nk] = make_uint2(e.off, e.count); nk += 1; }
         }
       }
       if (found || seen_empty) break;
@@ -258,8 +276,9 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
     const uint32_t ki = k0 + g.lane;
     uint32_t cnt = 0, off = 0;
     if (ki < nk) {
-      const uint32_t key = s.keys[ki].x;
-      if (key < a.key_cap) { const uint2 kd = *reinterpret_cast<const uint2*>(a.keydesc + key); off = kd.x; cnt = kd.y; }
+      const uint2 e = s.keys[ki];
+      if (e.y != kUnresolved) { off = e.x; cnt = e.y; }
+      else if (e.x < a.key_cap) { const uint2 kd = *reinterpret_cast<const uint2*>(a.keydesc + e.x); off = kd.x; cnt = kd.y; }
     }
     const uint32_t incl = g.incl_scan(cnt);
     wave_sync();
@@ -288,25 +307,45 @@ __device__ __forceinline__ uint4 emission(const MatchArgs& a, const uint2* keys,
   return make_uint4((VMQG_EMIT_REMOTE << 24) | (uint32_t)__builtin_ctzll(m), kNone, kNone, kNone);
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
 __device__ __forceinline__ void store_rec(Record* out, uint64_t i, uint4 v) {
-  *reinterpret_cast<uint4*>(out + i) = v;
+  if (NT) {
+    u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + i));
+  } else {
+    *reinterpret_cast<uint4*>(out + i) = v;
+  }
+}
+
+// Tiers: 0 = fast (G = kFastG lanes per publish, small LDS lists),
+// 1 = mid (G = 64, one publish per wave, large LDS lists, publishes deferred
+// by tier 0), 2 = slow (G = 64, global-memory lists, deferred by tier 1).
+template <int TIER>
+__device__ __forceinline__ void defer_or_fail(const MatchArgs& a, uint32_t p) {
+  if (TIER == 0) {
+    const uint32_t idx = atomicAdd(&a.status[0], 1u);
+    if (idx < a.deferred_cap) a.deferred[idx] = p;
+    else atomicOr(&a.status[1], kErrDeferFull);
+  } else if (TIER == 1) {
+    const uint32_t idx = atomicAdd(&a.status[2], 1u);
+    if (idx < a.deferred_cap) a.deferred2[idx] = p;
+    else atomicOr(&a.status[1], kErrDeferFull);
+  } else {
+    atomicOr(&a.status[1], kErrFrontier);
+  }
 }
 
 // ------------------------------------------------------------ COUNT pass
-template <int G, bool SLOW>
+template <int G, int TIER>
 __device__ void count_publish(const MatchArgs& a, uint32_t p, const Scratch& s, const Group<G>& g) {
   const vmqg_pub pub = a.pubs[p];
   const Matched m = walk_publish<G>(a, pub, s, g);
   if (g.lane != 0) return;
   uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
   if (m.overflow) {
-    if (SLOW) {
-      atomicOr(&a.status[1], kErrFrontier);
-    } else {
-      const uint32_t idx = atomicAdd(&a.status[0], 1u);
-      if (idx < a.deferred_cap) a.deferred[idx] = p;
-      else atomicOr(&a.status[1], kErrDeferFull);
-    }
+    defer_or_fail<TIER>(a, p);
     a.offsets[p] = 0;
     kc[0] = make_uint4(0, kRewalk, 0, 0);
     return;
@@ -325,102 +364,129 @@ __device__ void count_publish(const MatchArgs& a, uint32_t p, const Scratch& s, 
 }
 
 // ------------------------------------------------------------- EMIT pass
-template <int G, bool SLOW>
-__device__ void emit_publish(const MatchArgs& a, uint32_t p, bool valid, const Scratch& s, const Group<G>& g) {
-  // every group of the wave reaches this function (valid or not): the big
-  // fan-out loop below is wave-wide
+// Per-group result of the resolve step, staged in LDS for the wave copy.
+struct GroupMeta {
+  uint32_t rel, span, nk, ksum;   // output start relative to the wave's first publish, length
+  uint32_t rm_lo, rm_hi, ok, pad;
+};
+
+// EMIT for the GPW consecutive publishes [first, first + n) of one wave.
+// Resolve (key cache or re-walk) is per group; the copy is wave-wide over
+// the wave's contiguous output range, so every store instruction writes
+// 64 x 16 B = 1 KiB contiguous.
+template <int G, int GPW, bool NT>
+__device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const Scratch& s, const Group<G>& g,
+                          GroupMeta* gm, const uint2* keys_wave, uint32_t kstride) {
+  const uint32_t p = first + g.gidx;
+  const bool valid = g.gidx < n;
   uint32_t total = 0, nk = 0, ksum = 0;
-  uint64_t rmask = 0, obase = 0;
+  uint64_t rmask = 0, obase = 0, oend = 0;
   bool ok = valid;
   if (valid) {
     const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
     const uint4 h = kc[0];
     obase = a.offsets[p];
-    const uint64_t oend = a.offsets[p + 1];
+    oend = a.offsets[p + 1];
     if (h.y == kRewalk) {
-      const vmqg_pub pub = a.pubs[p];
-      const Matched m = walk_publish<G>(a, pub, s, g);
-      if (m.overflow) {
-        ok = false;   // handled by the slow pass (or latched as an error there)
-      } else {
-        total = m.total; nk = m.nk; ksum = m.ksum; rmask = m.rmask;
-      }
+      const Matched m = walk_publish<G>(a, a.pubs[p], s, g);
+      if (m.overflow) ok = false;   // written by the next tier
+      else { total = m.total; nk = m.nk; ksum = m.ksum; rmask = m.rmask; }
     } else {
-      total = h.x; nk = h.y; rmask = ((uint64_t)h.w << 32) | h.z;
+      total = h.x; nk = h.y < 2 ? h.y : 2; rmask = ((uint64_t)h.w << 32) | h.z;
       const uint4 k = kc[1];
       ksum = k.y + k.w;
       if (g.lane == 0) {
         s.keys[0] = make_uint2(k.x, 0u);
         s.keys[1] = make_uint2(k.z, k.y);
       }
-      nk = nk < 2 ? nk : 2;
     }
     if (ok && oend > a.out_cap) { if (g.lane == 0) atomicOr(&a.status[1], kErrOverflow); ok = false; }
     if (ok && oend - obase != total) { if (g.lane == 0) atomicOr(&a.status[1], kErrMismatch); ok = false; }
   }
+  const uint64_t wbase = a.offsets[first];
+  const uint64_t wend = a.offsets[first + n];
+  const uint32_t T = wend > a.out_cap ? 0 : (uint32_t)(wend - wbase);
+  if (g.lane == 0)
+    gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : T, (uint32_t)(oend - obase), nk == 0 ? 1 : nk,
+                           ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), ok ? 1u : 0u, 0u};
   wave_sync();
-  const bool big = ok && total > kBigFanout;
-  if (ok && !big) {
-    for (uint32_t r = g.lane; r < total; r += G)
-      store_rec(a.out, obase + r, emission(a, s.keys, nk == 0 ? 1 : nk, ksum, rmask, r));
-  }
-  if (G < 64) {
-    // wave-cooperative copy of large fan-outs (lookup_subs on a fanout key)
-    uint64_t bigm = __ballot(big && g.lane == 0);
-    while (bigm) {
-      const uint32_t src = (uint32_t)__builtin_ctzll(bigm);
-      bigm &= bigm - 1;
-      const uint32_t t = __shfl(total, (int)src, 64), kn = __shfl(nk, (int)src, 64), ks = __shfl(ksum, (int)src, 64);
-      const uint64_t rm = ((uint64_t)__shfl((uint32_t)(rmask >> 32), (int)src, 64) << 32) |
-                          __shfl((uint32_t)rmask, (int)src, 64);
-      const uint64_t ob = ((uint64_t)__shfl((uint32_t)(obase >> 32), (int)src, 64) << 32) |
-                          __shfl((uint32_t)obase, (int)src, 64);
-      const uint2* keys = s.keys + (int64_t)((src / G) - g.gidx) * (int64_t)(s.kcap);
-      for (uint32_t r = __lane_id(); r < t; r += 64) store_rec(a.out, ob + r, emission(a, keys, kn == 0 ? 1 : kn, ks, rm, r));
+  // 4 records per lane in flight: all loads issued before the stores
+  uint32_t j = 0;
+  for (uint32_t r0 = __lane_id(); r0 < T; r0 += 256) {
+    uint4 v[4];
+    bool w[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t r = r0 + 64 * u;
+      w[u] = false;
+      if (r < T) {
+        while (j + 1 < (uint32_t)GPW && gm[j + 1].rel <= r) j++;
+        const GroupMeta m = gm[j];
+        if (m.ok) {
+          const uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
+          v[u] = emission(a, keys_wave + (uint64_t)j * kstride, m.nk, m.ksum, rm, r - m.rel);
+          w[u] = true;
+        }
+      }
     }
-  } else if (big) {
-    for (uint32_t r = g.lane; r < total; r += G)
-      store_rec(a.out, obase + r, emission(a, s.keys, nk == 0 ? 1 : nk, ksum, rmask, r));
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (w[u]) store_rec<NT>(a.out, wbase + r0 + 64 * u, v[u]);
   }
+  wave_sync();
 }
 
 // --------------------------------------------------------------- kernels
-template <int MODE>
+template <int MODE, int G, bool NT>
 __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
-  constexpr int G = kFastG, GPW = 64 / G;   // groups per wave
-  __shared__ uint2 st[kWaves * GPW][kSCap];
-  __shared__ uint32_t cd[kWaves * GPW][kCCap];
-  __shared__ uint2 ky[kWaves * GPW][kKCap];
+  constexpr int GPW = 64 / G;   // groups (publishes) per wave
+  constexpr uint32_t SC = FastCaps<G>::S, CC = FastCaps<G>::C, KC = FastCaps<G>::K;
+  __shared__ uint2 st[kWaves * GPW][SC];
+  __shared__ uint32_t cd[kWaves * GPW][CC];
+  __shared__ uint2 ky[kWaves * GPW][KC];
+  __shared__ GroupMeta gm[kWaves][GPW];
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t slot = wv * GPW + g.gidx;
-  const Scratch s{st[slot], cd[slot], ky[slot], kSCap, kCCap, kKCap};
+  const Scratch s{st[slot], cd[slot], ky[slot], SC, CC, KC};
   const uint32_t stride = gridDim.x * kWaves * GPW;
   for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
-    const uint32_t p = base + g.gidx;
+    const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
     if (MODE == 0) {
-      if (p < a.npub) count_publish<G, false>(a, p, s, g);
+      if (g.gidx < n) count_publish<G, 0>(a, base + g.gidx, s, g);
     } else {
-      emit_publish<G, false>(a, p, p < a.npub, s, g);
+      emit_wave<G, GPW, NT>(a, base, n, s, g, gm[wv], ky[wv * GPW], KC);
     }
     wave_sync();
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256) void k_match_slow(MatchArgs a) {
+// Tiers 1 and 2: one publish per wave from the deferred lists.
+template <int MODE, int TIER>
+__global__ __launch_bounds__(256) void k_match_deferred(MatchArgs a) {
+  constexpr uint32_t kMidCap = 256;
+  __shared__ uint2 st[TIER == 1 ? kWaves : 1][TIER == 1 ? kMidCap : 1];
+  __shared__ uint32_t cd[TIER == 1 ? kWaves : 1][TIER == 1 ? kMidCap : 1];
+  __shared__ uint2 ky[TIER == 1 ? kWaves : 1][TIER == 1 ? kMidCap : 1];
+  __shared__ GroupMeta gm[kWaves][1];
   const Group<64> g;
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * kWaves + wv;
-  const Scratch s{a.g_stack + (uint64_t)gw * a.g_scap, a.g_cand + (uint64_t)gw * a.g_ccap,
-                  a.g_keys + (uint64_t)gw * a.g_kcap, a.g_scap, a.g_ccap, a.g_kcap};
-  uint32_t n = a.status[0];
+  Scratch s;
+  if (TIER == 1) {
+    s = Scratch{st[wv], cd[wv], ky[wv], kMidCap, kMidCap, kMidCap};
+  } else {
+    s = Scratch{a.g_stack + (uint64_t)gw * a.g_scap, a.g_cand + (uint64_t)gw * a.g_ccap,
+                a.g_keys + (uint64_t)gw * a.g_kcap, a.g_scap, a.g_ccap, a.g_kcap};
+  }
+  const uint32_t* list = TIER == 1 ? a.deferred : a.deferred2;
+  uint32_t n = TIER == 1 ? a.status[0] : a.status[2];
   if (n > a.deferred_cap) n = a.deferred_cap;
   const uint32_t nwaves = gridDim.x * kWaves;
   for (uint32_t d = gw; d < n; d += nwaves) {
-    const uint32_t p = a.deferred[d];
-    if (MODE == 0) count_publish<64, true>(a, p, s, g);
-    else emit_publish<64, true>(a, p, true, s, g);
+    const uint32_t p = list[d];
+    if (MODE == 0) count_publish<64, TIER>(a, p, s, g);
+    else emit_wave<64, 1, false>(a, p, 1, s, g, gm[wv], s.keys, 0);
     wave_sync();
   }
 }
@@ -493,19 +559,30 @@ uint64_t scan_tmp_elems(uint64_t n) {
   return tot + 1;
 }
 
-hipError_t launch_match(const MatchArgs& a, int mode, bool slow, hipStream_t st) {
-  if (!slow) {
-    const uint32_t per_block = kWaves * (64 / kFastG);
-    uint32_t g = div_up(a.npub, per_block);
+hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) {
+  if (tier == 0) {
+    const uint32_t G = (a.fast_g == 2 || a.fast_g == 8) ? a.fast_g : 4;
+    const bool nt = (a.opts & kOptNtStores) != 0;
+    uint32_t g = div_up(a.npub, kWaves * (64 / G));
     const uint32_t cap = 256u * 8u;   // grid-stride beyond 8 blocks per CU
     if (g > cap) g = cap;
     if (g < 1) g = 1;
-    if (mode == 0) k_match_fast<0><<<g, 256, 0, st>>>(a);
-    else k_match_fast<1><<<g, 256, 0, st>>>(a);
+#define VMQG_FAST(GG)                                                       \
+    if (mode == 0) k_match_fast<0, GG, false><<<g, 256, 0, st>>>(a);        \
+    else if (nt) k_match_fast<1, GG, true><<<g, 256, 0, st>>>(a);           \
+    else k_match_fast<1, GG, false><<<g, 256, 0, st>>>(a);
+    if (G == 2) { VMQG_FAST(2) }
+    else if (G == 4) { VMQG_FAST(4) }
+    else { VMQG_FAST(8) }
+#undef VMQG_FAST
+  } else if (tier == 1) {
+    const uint32_t g = 256;   // reads its list length on the device; exits at once when empty
+    if (mode == 0) k_match_deferred<0, 1><<<g, 256, 0, st>>>(a);
+    else k_match_deferred<1, 1><<<g, 256, 0, st>>>(a);
   } else {
     const uint32_t g = a.g_waves / kWaves;
-    if (mode == 0) k_match_slow<0><<<g, 256, 0, st>>>(a);
-    else k_match_slow<1><<<g, 256, 0, st>>>(a);
+    if (mode == 0) k_match_deferred<0, 2><<<g, 256, 0, st>>>(a);
+    else k_match_deferred<1, 2><<<g, 256, 0, st>>>(a);
   }
   return hipGetLastError();
 }

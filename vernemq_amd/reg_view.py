@@ -251,6 +251,10 @@ class RegGpuView:
     def match_status(self, stream: int = 0) -> int:
         return self._L.vmqg_match_status(self._h, stream or None)
 
+    def set_option(self, name: str, value: int):
+        """Kernel tuning knob (vmqg_set_option): "fast_g" 4|8, "nt_stores" 0|1."""
+        _lib.check(self._L.vmqg_set_option(self._h, name.encode(), int(value)), "vmqg_set_option")
+
     def set_timing(self, on: bool):
         _lib.check(self._L.vmqg_set_timing(self._h, 1 if on else 0), "vmqg_set_timing")
 
