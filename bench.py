@@ -68,7 +68,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP events (profiling runs)")
+    ap.add_argument("--config", default="C", choices=["C", "D"],
+                    help="C: headline (1M subs); D: 10M subs with $share groups under 1%%/s churn")
+    ap.add_argument("--d-scale", type=float, default=1.0)
+    ap.add_argument("--churn-batch", type=int, default=10_000)
     args = ap.parse_args()
+    if args.config == "D":
+        return bench_d(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -235,6 +241,90 @@ def main():
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def bench_d(args):
+    """Config D: 10M subscriptions (8M exact, 1M '+'/'#', 1M
+    $share members on 4 nodes) under churn.  One step = one delta batch of
+    `churn_batch` ops (50/50 sub/unsub, host engine + device patches) followed
+    by one match batch of 2^20 publishes; 10 steps/s of 10k ops is the
+    configured 1 %/s churn.  Single GPU; prints one JSON line."""
+    import torch
+    from vernemq_amd import workloads as W
+    from vernemq_amd.reg_view import RegGpuView
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    t0 = time.time()
+    w = W.config_d(scale=args.d_scale, n_pubs=args.batch)
+    n_live = w.notes["n_live"]
+    view = RegGpuView(node=w.self_node, device=0, nodes=w.nodes,
+                      hints={"edges": 4 * n_live // 5, "paths": 4 * n_live // 5, "keys": n_live,
+                             "records": n_live * 11 // 10, "exact": n_live})
+    ids = w.load_into(view, n=n_live)
+    load_s = time.time() - t0
+    log("config D: %d live subs loaded in %.1fs, %s" % (n_live, load_s, view.stats_raw()))
+    ch = W.Churn(w)
+    pubs, words = w.publish_arrays(view)
+    npub = len(pubs)
+    d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    d_offs = torch.zeros(npub + 1, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+    # size the output from a first count
+    recs, offs = None, None
+    out_cap = 8 * npub
+    d_out = torch.empty(out_cap * 4, dtype=torch.int32, device=dev)
+
+    def match():
+        nonlocal out_cap, d_out
+        view.match_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_out.data_ptr(), out_cap,
+                          d_offs.data_ptr(), sp)
+
+    match()
+    torch.cuda.synchronize()
+    need = int(d_offs[-1].item())
+    view.match_status(sp)
+    out_cap = int(need * 1.2) + 1024
+    d_out = torch.empty(out_cap * 4, dtype=torch.int32, device=dev)
+    batches = [ch.batch(args.churn_batch) for _ in range(args.warmup + args.steps)]
+    for k in range(args.warmup):
+        view.apply_op_arrays(*ch.ops(ids, *batches[k]))
+        match()
+    torch.cuda.synchronize()
+    if view.match_status(sp) != 0:
+        raise RuntimeError("match status after warmup")
+    apply_s = 0.0
+    emitted = 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        ops, wds = ch.ops(ids, *batches[k])
+        ta = time.perf_counter()
+        view.apply_op_arrays(ops, wds)            # host engine + patch upload (synchronous)
+        apply_s += time.perf_counter() - ta
+        match()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    rc = view.match_status(sp)
+    if rc != 0:
+        raise RuntimeError("match status %d" % rc)
+    emitted = int(d_offs[-1].item())
+    st = view.stats_raw()
+    res = {
+        "metric": "publishes/sec under churn (config D, 10M subs incl. $share, 1%/s deltas)",
+        "value": npub * args.steps / el, "unit": "publishes/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic: SURVEY.md §8(d) config D generator (splitmix64 seed 0xD), scale %g" % args.d_scale,
+        "config": {"workload": "D: %d live subs, %d-op delta batch + %d publishes per step" %
+                               (n_live, args.churn_batch, npub)},
+        "deltas_per_s_applied": args.churn_batch * args.steps / apply_s if apply_s else None,
+        "apply_ms_per_batch": apply_s * 1e3 / args.steps,
+        "emissions_last_step": emitted, "load_s": load_s,
+        "arena_bytes": st["device_bytes"], "rebuilds": st["rebuilds"],
+        "deferred": [st["deferred_tier1"], st["deferred_tier2"]],
+    }
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -43,3 +43,11 @@ def load(w):
     o = TrieOracle(w.self_node)
     o.apply_raw(init_bytes(w))
     return o
+
+
+def load_prefix(w, n: int):
+    """A TrieOracle holding workload w's first n subscriptions."""
+    from .oracle import TrieOracle
+    o = TrieOracle(w.self_node)
+    o.apply_raw(init_bytes(w, 0, n))
+    return o

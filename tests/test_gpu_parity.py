@@ -276,3 +276,64 @@ def test_replica_follows_primary_by_image_and_patches():
         r1, o1 = prim.view.match_arrays(arr, words)
         r2, o2 = rep.match_arrays(arr, words)
         assert np.array_equal(o1, o2) and np.array_equal(r1, r2), step
+
+
+def _config_d_expected_counts(w, live, pubs_lo, pubs_hi):
+    """Known answer per publish of config D from the live mask: state
+    publishes emit every live exact subscriber of (s, d); alarm publishes
+    every live site/s/+/alarm/# subscriber; jobs/q/x publishes every live
+    member of every group on q once per distinct node hosting a live member
+    of that group (Q2, vmq_reg_trie.erl:68-72, 301-303)."""
+    from collections import Counter, defaultdict
+    idx = np.flatnonzero(live)
+    topics = {}
+    exact, alarm = Counter(), Counter()
+    groups = defaultdict(list)
+    for i in idx:
+        t = w.sub_topic(i)
+        if t[0] == b"site" and t[2] == b"dev":
+            exact[(t[1], t[3])] += 1
+        elif t[0] == b"site":
+            alarm[t[1]] += 1
+        else:
+            groups[(t[1], t[3])].append(w.sub_node[i])
+    jobs = Counter()
+    for (g, q), nodes in groups.items():
+        jobs[q] += len(nodes) * len(set(nodes))
+    out = []
+    for i in range(pubs_lo, pubs_hi):
+        t = w.pub_topic(i)
+        if t[0] == b"jobs":
+            out.append(jobs[t[1]])
+        elif t[2] == b"dev":
+            out.append(exact[(t[1], t[3])])
+        else:
+            out.append(alarm[t[1]])
+    return np.array(out, dtype=np.int64)
+
+
+def test_config_d_churn_parity():
+    """Config D at 1/20 scale (500k subs incl. $share groups over 4 nodes):
+    after every churn batch, all publishes match the known answer and a
+    sample matches the oracle publish for publish."""
+    from vernemq_amd import workloads as W
+    from vernemq_amd.reg_view import RegGpuView
+    w = W.config_d(scale=0.05, n_pubs=20_000)
+    v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
+    ids = w.load_into(v, n=w.notes["n_live"])
+    orc = feed.load_prefix(w, w.notes["n_live"])
+    ch = W.Churn(w)
+    pubs, words = w.publish_arrays(v)
+    for step in range(4):
+        if step:
+            dels, adds = ch.batch(5000)
+            ops, wds = ch.ops(ids, dels, adds)
+            v.apply_op_arrays(ops, wds)
+            orc.apply(ch.events(dels, adds))
+        recs, offs = v.match_arrays(pubs, words)
+        counts = np.diff(offs.astype(np.int64))
+        assert np.array_equal(counts, _config_d_expected_counts(w, ch.live, 0, w.n_pubs)), step
+        sample = list(range(0, w.n_pubs, 40))
+        got = [sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1]))) for i in sample]
+        want = orc.fold_batch([("", b"pub", w.pub_topic(i)) for i in sample])
+        assert all(g == sorted(x) for g, x in zip(got, want)), step

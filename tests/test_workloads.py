@@ -42,3 +42,26 @@ def test_config_a_b_r_shapes():
     assert r1.sub_topic(0) == (b"unique", b"topic", b"1") and r1.pub_topic(9) == (b"unique", b"topic", b"10")
     r2 = W.config_r2(10)
     assert r2.n_subs == 10 and r2.n_pubs == 1
+
+
+def test_config_d_churn_tables_match_oracle():
+    """Config D at 1/500 scale: bulk load + 6 churn batches through the host
+    engine (op arrays) and the oracle (events) give identical tables."""
+    from tests import harness as H
+    from tests.test_host_engine import _compare
+    from vernemq_amd.reg_view import RegGpuView
+    w = W.config_d(scale=0.002, n_pubs=100)
+    v = RegGpuView(node=w.self_node, device=-1, nodes=w.nodes)
+    ids = w.load_into(v, n=w.notes["n_live"])
+    orc = feed.load_prefix(w, w.notes["n_live"])
+    ch = W.Churn(w)
+    for _ in range(6):
+        dels, adds = ch.batch(400)
+        ops, words = ch.ops(ids, dels, adds)
+        v.apply_op_arrays(ops, words)
+        orc.apply(ch.events(dels, adds))
+
+    class P:
+        view = v
+    _compare(P, orc, "config D churn")
+    assert v.stats_raw()["subs"] > 0

@@ -228,14 +228,14 @@ void Engine::edge_erase(uint32_t parent, uint32_t word) {
   if (word == kHash || word == kPlus) refresh_incoming_flags(parent);
 }
 
-Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale) const {
+Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) const {
   Layout L{};
   L.magic = kLayoutMagic;
   L.max_mountpoints = cfg.max_mountpoints;
   L.local_node = cfg.local_node;
   uint64_t recs = 0, kl = 0, xw = 0, ex = 0;
   for (auto& k : keys) recs += next_pow2(k.vals.size() ? k.vals.size() : 1);
-  for (auto& p : paths) if (p.filter && p.nodes.size() >= 2) kl += p.nodes.size();
+  for (auto& p : paths) if (p.filter && p.nodes.size() >= 2) kl += next_pow2(p.nodes.size());
   for (auto& t : topics) {
     const bool has = t.exact_ok && ((t.local_key != kNone && !keys[t.local_key].vals.empty()) || !t.remote.empty());
     if (has) { ex++; xw += t.words.size() + 1; }
@@ -251,6 +251,15 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale) const {
   L.exact_buckets = exact_slots / kExactSlotsPerBucket;
   L.exwords_cap = std::max<uint64_t>(16384, xw * 2);
   uint64_t o = 0;
+  if (!compact && lay.total_bytes) {   // a growth re-layout never shrinks a region
+    L.edge_buckets = std::max<uint64_t>(L.edge_buckets, lay.edge_buckets);
+    L.node_cap = std::max<uint64_t>(L.node_cap, lay.node_cap);
+    L.key_cap = std::max<uint64_t>(L.key_cap, lay.key_cap);
+    L.keylist_cap = std::max<uint64_t>(L.keylist_cap, lay.keylist_cap);
+    L.rec_cap = std::max<uint64_t>(L.rec_cap, lay.rec_cap);
+    L.exact_buckets = std::max<uint64_t>(L.exact_buckets, lay.exact_buckets);
+    L.exwords_cap = std::max<uint64_t>(L.exwords_cap, lay.exwords_cap);
+  }
   L.edge_buckets *= scale; L.node_cap *= scale; L.key_cap *= scale; L.keylist_cap *= scale;
   L.rec_cap *= scale; L.exact_buckets *= scale; L.exwords_cap *= scale;
   L.edge_off = o;    o = align256(o + L.edge_buckets * kEdgeSlotsPerBucket * sizeof(EdgeSlot));
@@ -267,7 +276,7 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale) const {
 // Re-lay the arena out from the logical state (tables rehashed without
 // tombstones, record/keylist/exword pools compacted).  The next upload
 // ships the whole image.
-void Engine::rebuild(uint64_t extra_edges) {
+void Engine::rebuild(uint64_t extra_edges, bool compact) {
   std::vector<EdgeSlot> live;
   if (!mirror.empty()) {
     const EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
@@ -276,7 +285,7 @@ void Engine::rebuild(uint64_t extra_edges) {
   }
   for (uint32_t scale = 1;; scale *= 2) {
     edge_live = edge_tomb = 0;
-    lay = plan_layout(std::max<uint64_t>(extra_edges, live.size()), scale);
+    lay = plan_layout(std::max<uint64_t>(extra_edges, live.size()), scale, compact);
     mirror.assign(lay.total_bytes / 8, 0);
     memset(region<uint8_t>(lay.edge_off), 0xFF, lay.edge_buckets * kEdgeSlotsPerBucket * sizeof(EdgeSlot));
     memset(region<uint8_t>(lay.exact_off), 0xFF, lay.exact_buckets * kExactSlotsPerBucket * sizeof(ExactSlot));
@@ -286,9 +295,9 @@ void Engine::rebuild(uint64_t extra_edges) {
     exact_live = exact_tomb = 0;
     rec_top = rec_garbage = kl_top = kl_garbage = xw_top = xw_garbage = 0;
     for (auto& e : live) edge_insert(e.parent, e.word, e.child);
-    for (auto& k : keys) { k.off = 0; k.cap = 0; }
+    for (auto& k : keys) { k.off = 0; k.cap = 0; k.dirty_pos.clear(); }
     for (auto& t : topics) { t.slot = ~0ull; t.words_off = kNone; }
-    for (auto& p : paths) p.kl_n = 0;
+    for (auto& p : paths) { p.kl_off = 0; p.kl_cap = 0; }
     bool ok = true;
     for (uint32_t k = 0; ok && k < keys.size(); k++) ok = write_key(k);
     for (uint32_t p = 0; ok && p < paths.size(); p++) ok = write_path(p);
@@ -306,16 +315,22 @@ bool Engine::write_key(uint32_t k) {
   KeyInfo& K = keys[k];
   if (k >= lay.key_cap) return false;
   const uint64_t n = K.vals.size();
-  if (n > K.cap) {
+  Record* recs = region<Record>(lay.rec_off);
+  if (n > K.cap) {   // relocate: the whole list is written at its new range
     const uint64_t cap = next_pow2(n);
     if (rec_top + cap > lay.rec_cap) return false;
     rec_garbage += K.cap;
     K.off = rec_top; K.cap = cap; rec_top += cap;
-  }
-  if (n) {
-    memcpy(region<Record>(lay.rec_off) + K.off, K.vals.data(), n * sizeof(Record));
+    memcpy(recs + K.off, K.vals.data(), n * sizeof(Record));
     touch(lay.rec_off + K.off * sizeof(Record), n * sizeof(Record));
+  } else {           // in place: only the slots insert / swap-remove changed
+    for (uint32_t pos : K.dirty_pos) {
+      if (pos >= n) continue;
+      recs[K.off + pos] = K.vals[pos];
+      touch(lay.rec_off + (K.off + pos) * sizeof(Record), sizeof(Record));
+    }
   }
+  K.dirty_pos.clear();
   KeyDesc* kd = region<KeyDesc>(lay.keydesc_off) + k;
   kd->off = (uint32_t)K.off; kd->count = (uint32_t)n;
   touch(lay.keydesc_off + (uint64_t)k * sizeof(KeyDesc), sizeof(KeyDesc));
@@ -353,13 +368,19 @@ bool Engine::write_path(uint32_t p) {
     r.off0 = (uint32_t)keys[ks[0]].off;
     r.cnt0 = (uint32_t)keys[ks[0]].vals.size();
   } else if (ks.size() >= 2) {
-    if (kl_top + ks.size() > lay.keylist_cap) return false;
-    kl_garbage += P.kl_n;
-    r.key = (uint32_t)kl_top;
-    memcpy(region<uint32_t>(lay.keylist_off) + kl_top, ks.data(), ks.size() * 4);
-    touch(lay.keylist_off + kl_top * 4, ks.size() * 4);
-    kl_top += ks.size();
-    P.kl_n = (uint32_t)ks.size();
+    if (ks.size() > P.kl_cap) {   // grow: a new range; the old one becomes garbage
+      const uint64_t cap = next_pow2(ks.size());
+      if (kl_top + cap > lay.keylist_cap) return false;
+      kl_garbage += P.kl_cap;
+      P.kl_off = (uint32_t)kl_top;
+      P.kl_cap = (uint32_t)cap;
+      kl_top += cap;
+    }
+    r.key = P.kl_off;
+    uint32_t* kl = region<uint32_t>(lay.keylist_off) + P.kl_off;
+    for (size_t i = 0; i < ks.size(); i++) {
+      if (kl[i] != ks[i]) { kl[i] = ks[i]; touch(lay.keylist_off + (P.kl_off + i) * 4, 4); }
+    }
   }
   r.meta = flags | ((uint32_t)ks.size() << 8);
   r.rmask_lo = (uint32_t)rmask; r.rmask_hi = (uint32_t)(rmask >> 32);
@@ -552,6 +573,7 @@ void Engine::insert_trie_subs(uint32_t key, const Record& v) {
   if (n == 1) n_fanout += 2;                                  // :458-463 promote both
   else if (n >= 2) n_fanout++;                                // :456-457
   K.vals.push_back(v);
+  K.dirty_pos.push_back((uint32_t)K.vals.size() - 1);
   if (!K.idx && K.vals.size() > 32) {
     K.idx.reset(new std::unordered_map<Record, uint32_t, RecordHash, RecordEq>());
     for (uint32_t i = 0; i < K.vals.size(); i++) (*K.idx)[K.vals[i]] = i;
@@ -583,6 +605,7 @@ void Engine::del_trie_subs(uint32_t key, const Record& v) {
   } else if (pos != n - 1) {
     K.vals[pos] = K.vals[n - 1];
   }
+  if (pos != n - 1) K.dirty_pos.push_back((uint32_t)pos);
   K.vals.pop_back();
   if (n - 1 == 1) n_fanout -= 2; else n_fanout -= 1;
   mark_key(key);
@@ -655,7 +678,9 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
     for (uint32_t j = 0; j < o.nwords; j++) if (w[j] >= word_text.size()) return VMQG_E_INVAL;
     // [<<"$share">>, Group] has no topic: triples([]) has no clause (vmq_topic.erl:71)
     if (o.nwords == 2 && w[0] == kShare) return VMQG_E_INVAL;
-    if (o.kind == VMQG_OP_ADD) add_words += o.nwords;
+    // only wildcard and $share topics enter the trie (add_complex_topic/4 :318-319)
+    if (o.kind == VMQG_OP_ADD && ((o.nwords >= 3 && w[0] == kShare) || contains_wildcard(w, o.nwords)))
+      add_words += o.nwords;
   }
   // the edge table must absorb every edge this batch could add
   if ((edge_live + edge_tomb + add_words) * 10 > lay.edge_buckets * kEdgeSlotsPerBucket * 7) rebuild(add_words);
@@ -667,7 +692,8 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
   const bool garbage_heavy = rec_garbage > lay.rec_cap / 2 || kl_garbage > lay.keylist_cap / 2 ||
                              xw_garbage > lay.exwords_cap / 2 ||
                              exact_tomb * 4 > lay.exact_buckets * kExactSlotsPerBucket;
-  if (full_image || garbage_heavy || !flush_incremental()) rebuild(0);
+  if (garbage_heavy) rebuild(0, true);                // compaction
+  else if (!flush_incremental()) rebuild(0);         // growth (writes every dirty item too)
   for (uint32_t k : dirty_keys) keys[k].dirty = 0;
   for (uint32_t p : dirty_paths) paths[p].dirty = 0;
   for (uint32_t t : dirty_topics) topics[t].dirty = 0;

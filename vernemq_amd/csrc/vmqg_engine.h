@@ -25,7 +25,7 @@ struct Nog {
 struct PathInfo {
   uint32_t parent, word, mp, depth;
   uint32_t topic_id = kNone;        // (MP, path words) term, once known
-  uint32_t kl_n = 0;                // keylist entries owned (garbage accounting)
+  uint32_t kl_off = 0, kl_cap = 0;  // keylist range owned by this path
   uint8_t rec = 0, topic_set = 0;   // vmq_trie_node record / its topic field
   uint8_t filter = 0;               // vmq_trie_topic entry exists
   uint8_t dollar_skip = 0, first_plus = 0, dirty = 0;
@@ -52,6 +52,7 @@ struct KeyInfo {
   std::vector<Record> vals;
   std::unique_ptr<std::unordered_map<Record, uint32_t, RecordHash, RecordEq>> idx;
   uint64_t off = 0, cap = 0;                  // record range in the arena
+  std::vector<uint32_t> dirty_pos;            // record slots changed since the last flush
 };
 
 // One (MP, Topic) term: the local key, the vmq_trie_remote_subs entry and
@@ -158,8 +159,8 @@ struct Engine {
   void edge_erase(uint32_t parent, uint32_t word);
   uint32_t child_flags(uint32_t child);
   void refresh_incoming_flags(uint32_t node);
-  Layout plan_layout(uint64_t extra_edges, uint32_t scale) const;
-  void rebuild(uint64_t extra_edges);
+  Layout plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) const;
+  void rebuild(uint64_t extra_edges, bool compact = false);
   bool flush_incremental();
   bool write_key(uint32_t k);
   bool write_path(uint32_t p);

@@ -90,29 +90,50 @@ class Workload:
         return [(self.mps[self.pub_mp[i]], self.pub_topic(i)) for i in range(lo, hi)]
 
     # ------------------------------------------------------------ product
-    def load_into(self, view, batch: int = 1 << 20) -> None:
-        """Bulk initialize_trie into a RegGpuView (op arrays, no per-sub Python)."""
+    def bind(self, view):
+        """Intern this workload's terms in `view`; returns the id maps
+        (word, node, mountpoint-of-client, subscriber, subinfo)."""
+        from .reg_view import _subinfo_key
         wid = view.intern_words(self.words, create=True).astype(np.uint32)
         node_id = np.array([view.nodes.get(n) for n in self.nodes], dtype=np.uint32)
         mp_id = np.array([view.mountpoints.get(m) for m in self.mps], dtype=np.uint32)
         sid_id = np.array([view.subscribers.get(c) for c in self.clients], dtype=np.uint32)
-        from .reg_view import OP_DTYPE, _subinfo_key
         si_id = np.array([view.subinfos.get(s, _subinfo_key(s)) for s in self.subinfos], dtype=np.uint32)
-        client_mp = np.array([self.mps.index(c[0]) for c in self.clients], dtype=np.int64)
-        words_all = wid[self.tw]
-        n = self.n_subs
+        mp_index = {m: i for i, m in enumerate(self.mps)}
+        client_mp = np.array([mp_index[c[0]] for c in self.clients], dtype=np.int64)
+        return {"wid": wid, "node": node_id, "client_mp": mp_id[client_mp], "sid": sid_id, "si": si_id}
+
+    def op_arrays(self, ids, idx: np.ndarray, kind: int):
+        """OP_DTYPE + word-id arrays for subscriptions `idx` (one op each)."""
+        from .reg_view import OP_DTYPE
+        idx = np.asarray(idx, dtype=np.int64)
+        lens = self.tw_off[idx + 1] - self.tw_off[idx]
+        ops = np.zeros(len(idx), dtype=OP_DTYPE)
+        ops["kind"] = kind
+        ops["mountpoint"] = ids["client_mp"][self.sub_client[idx]]
+        woff = np.zeros(len(idx), dtype=np.int64)
+        if len(idx):
+            woff[1:] = np.cumsum(lens)[:-1]
+        ops["word_off"] = woff.astype(np.uint32)
+        ops["nwords"] = lens.astype(np.uint32)
+        ops["node"] = ids["node"][self.sub_node[idx]]
+        ops["subscriber"] = ids["sid"][self.sub_client[idx]]
+        ops["subinfo"] = ids["si"][self.sub_info[idx]]
+        # gather the word ids of every selected topic
+        total = int(lens.sum())
+        rep = np.repeat(self.tw_off[idx] - woff, lens)
+        words = ids["wid"][self.tw[np.arange(total, dtype=np.int64) + rep]] if total else np.zeros(0, np.uint32)
+        return ops, words
+
+    def load_into(self, view, batch: int = 1 << 20, n: int | None = None):
+        """Bulk initialize_trie of subscriptions [0, n) into a RegGpuView (op
+        arrays, no per-subscription Python).  Returns the id maps."""
+        ids = self.bind(view)
+        n = self.n_subs if n is None else n
         for lo in range(0, n, batch):
-            hi = min(n, lo + batch)
-            ops = np.zeros(hi - lo, dtype=OP_DTYPE)
-            base = self.tw_off[lo]
-            ops["kind"] = _lib.OP_ADD
-            ops["mountpoint"] = mp_id[client_mp[self.sub_client[lo:hi]]]
-            ops["word_off"] = (self.tw_off[lo:hi] - base).astype(np.uint32)
-            ops["nwords"] = (self.tw_off[lo + 1:hi + 1] - self.tw_off[lo:hi]).astype(np.uint32)
-            ops["node"] = node_id[self.sub_node[lo:hi]]
-            ops["subscriber"] = sid_id[self.sub_client[lo:hi]]
-            ops["subinfo"] = si_id[self.sub_info[lo:hi]]
-            view.apply_op_arrays(ops, words_all[base:self.tw_off[hi]])
+            ops, words = self.op_arrays(ids, np.arange(lo, min(n, lo + batch)), _lib.OP_ADD)
+            view.apply_op_arrays(ops, words)
+        return ids
 
     def publish_arrays(self, view, lo: int = 0, hi: int | None = None):
         """PUB_DTYPE + word-id arrays for publishes [lo, hi) (ids looked up, not created)."""
@@ -305,7 +326,146 @@ def config_r2(n: int = 100_000) -> Workload:
     return _finish(w, subs, pubs)
 
 
-CONFIGS = {"A": config_a, "B": config_b, "C": config_c, "R1": config_r1, "R2": config_r2}
+def config_d(scale: float = 1.0, seed: int = 0xD, n_pubs: int = 1 << 20, extra: float = 0.1) -> Workload:
+    """Config D (§8d) at `scale` (1.0 = 10M subs):
+      8M exact   site/{s}/dev/{d}/state   (s < 1000, d < 8000 at scale 1)
+      1M         site/{s}/+/alarm/#       (s uniform)
+      1M         $share/g{g}/jobs/{g mod 1000}/+ : 10,000 groups x 100 members,
+                 member m on node m mod 4 (so each member is emitted 4 times, Q2)
+    plus `extra` x that many not-yet-live subscriptions of the same shapes for
+    the churn (1 %/s = 10 batches/s of 10,000 ops at scale 1, 50/50 sub/unsub).
+    Publishes: 70 % site/s/dev/d/state, 25 % site/s/x{k}/alarm/z{j}, 5 % jobs/q/x{k}."""
+    r = SplitMix(seed)
+    w = Workload("D")
+    w.nodes = [w.self_node, "node1@127.0.0.1", "node2@127.0.0.1", "node3@127.0.0.1"]
+    n_s = max(2, int(1000 * scale))
+    n_d = 8000
+    n_exact = n_s * n_d
+    n_alarm = max(1, int(1_000_000 * scale))
+    n_groups = max(1, int(10_000 * scale))
+    n_members = 100
+    n_jobs = n_groups * n_members
+    n_live = n_exact + n_alarm + n_jobs
+    n_extra = int(n_live * extra)
+    n_q = max(1, min(1000, n_groups))
+    words = [b"site", b"dev", b"state", b"+", b"#", b"alarm", b"$share", b"jobs"]
+    s_base = len(words)
+    words += [b"%d" % i for i in range(max(n_s, n_d, n_q))]
+    g_base = len(words)
+    words += [b"g%d" % g for g in range(n_groups)]
+    w.words = words
+    w.subinfos = std_subinfos()
+    num = lambda x: s_base + np.asarray(x, dtype=np.int64)
+    # --- live subscriptions, then the churn pool of not-yet-live ones
+    kinds = []      # (topics [n, L] array, clients, nodes)
+    # exact
+    i = np.arange(n_exact + n_extra * 8 // 10, dtype=np.int64)
+    s_i = np.where(i < n_exact, i // n_d, r.ints(len(i), n_s))
+    d_i = np.where(i < n_exact, i % n_d, r.ints(len(i), n_d))
+    t = np.stack([np.zeros_like(i), num(s_i), np.ones_like(i), num(d_i), np.full_like(i, 2)], axis=1)
+    kinds.append(("e", t, np.zeros_like(i)))
+    # alarm
+    i = np.arange(n_alarm + n_extra // 10, dtype=np.int64)
+    t = np.stack([np.zeros_like(i), num(r.ints(len(i), n_s)), np.full_like(i, 3), np.full_like(i, 5),
+                  np.full_like(i, 4)], axis=1)
+    kinds.append(("a", t, np.zeros_like(i)))
+    # $share jobs
+    i = np.arange(n_jobs + n_extra // 10, dtype=np.int64)
+    g_i = np.where(i < n_jobs, i // n_members, r.ints(len(i), n_groups))
+    m_i = np.where(i < n_jobs, i % n_members, n_members + i)
+    t = np.stack([np.full_like(i, 6), g_base + g_i, np.full_like(i, 7), num(g_i % n_q), np.full_like(i, 3)], axis=1)
+    kinds.append(("j", t, m_i % 4))
+    live_n = [n_exact, n_alarm, n_jobs]
+    # order: all live subscriptions first (load order), then the pools
+    topics, clients, nodes, live_parts, pool_parts = [], [], [], [], []
+    cbase = 0
+    for (tag, t, nd), ln in zip(kinds, live_n):
+        n = len(t)
+        live_parts.append((t[:ln], nd[:ln], cbase, ln))
+        pool_parts.append((t[ln:], nd[ln:], cbase + ln, n - ln))
+        clients += [("", b"%s%d" % (tag.encode(), k)) for k in range(n)]
+        cbase += n
+    rows, cl, nod = [], [], []
+    for t, nd, c0, n in live_parts + pool_parts:
+        rows.append(t)
+        cl.append(np.arange(c0, c0 + n, dtype=np.int64))
+        nod.append(nd)
+    T = np.concatenate(rows)
+    w.clients = clients
+    w.sub_client = np.concatenate(cl)
+    w.sub_node = np.concatenate(nod).astype(np.int64)
+    w.sub_info = r.ints(len(T), len(w.subinfos))
+    w.tw_off = np.arange(0, 5 * len(T) + 1, 5, dtype=np.int64)
+    w.tw = T.reshape(-1)
+    w.notes = {"n_live": n_live, "n_pool": len(T) - n_live, "n_s": n_s, "n_d": n_d, "n_q": n_q,
+               "groups": n_groups, "members": n_members}
+    # publishes
+    pw = [b"site", b"dev", b"state", b"alarm", b"jobs"]
+    pn_base = len(pw)
+    pw += [b"%d" % k for k in range(max(n_s, n_d, n_q))]
+    px_base = len(pw)
+    pw += [b"x%d" % k for k in range(16)] + [b"z%d" % k for k in range(16)]
+    w.pub_words = pw
+    u = r.unif(n_pubs)
+    a1, a2, a3 = r.ints(n_pubs, n_s), r.ints(n_pubs, n_d), r.ints(n_pubs, 16)
+    is_state, is_alarm = u < 0.70, (u >= 0.70) & (u < 0.95)
+    rows = np.zeros((n_pubs, 5), dtype=np.int64)
+    lens = np.where(is_state | is_alarm, 5, 3)
+    rows[:, 0] = np.where(is_state | is_alarm, 0, 4)
+    rows[:, 1] = pn_base + np.where(is_state | is_alarm, a1, a1 % n_q)
+    rows[:, 2] = np.where(is_state, 1, px_base + a3)
+    rows[:, 3] = np.where(is_state, pn_base + a2, 3)
+    rows[:, 4] = np.where(is_state, 2, px_base + 16 + a3)
+    w.pw_off = np.zeros(n_pubs + 1, dtype=np.int64)
+    w.pw_off[1:] = np.cumsum(lens)
+    w.pw = rows.reshape(-1)[(np.arange(5)[None, :] < lens[:, None]).reshape(-1)]
+    w.pub_mp = np.zeros(n_pubs, dtype=np.int64)
+    return w
+
+
+class Churn:
+    """Config D's subscription churn: each batch unsubscribes `n/2` live
+    subscriptions chosen uniformly and subscribes `n/2` not-live ones (the
+    pool).  Every churn subscriber holds exactly one subscription, so a batch
+    is also expressible as subscriber-store events for the oracle."""
+
+    def __init__(self, w: Workload, seed: int = 0xD0):
+        self.w = w
+        self.r = SplitMix(seed)
+        self.live = np.zeros(w.n_subs, dtype=bool)
+        self.live[:w.notes["n_live"]] = True
+
+    def batch(self, n: int):
+        half = n // 2
+        live_idx = np.flatnonzero(self.live)
+        dead_idx = np.flatnonzero(~self.live)
+        dels = live_idx[np.unique(self.r.ints(half, len(live_idx)))]
+        adds = dead_idx[np.unique(self.r.ints(half, len(dead_idx)))] if len(dead_idx) else dead_idx
+        self.live[dels] = False
+        self.live[adds] = True
+        return dels, adds
+
+    def ops(self, ids, dels, adds):
+        """Deletes first, then adds (the order handle_event/2 uses within an event)."""
+        from .reg_view import OP_DTYPE
+        o1, w1 = self.w.op_arrays(ids, dels, _lib.OP_DEL)
+        o2, w2 = self.w.op_arrays(ids, adds, _lib.OP_ADD)
+        o2["word_off"] += len(w1)
+        return np.concatenate([o1, o2]).astype(OP_DTYPE), np.concatenate([w1, w2]).astype(np.uint32)
+
+    def events(self, dels, adds):
+        w = self.w
+        ev = []
+        for i in dels:
+            sid = w.clients[w.sub_client[i]]
+            ev.append(("deleted", sid, [(w.nodes[w.sub_node[i]], True, [(w.sub_topic(i), w.subinfos[w.sub_info[i]])])]))
+        for i in adds:
+            sid = w.clients[w.sub_client[i]]
+            ev.append(("updated", sid, None, [(w.nodes[w.sub_node[i]], True, [(w.sub_topic(i), w.subinfos[w.sub_info[i]])])]))
+        return ev
+
+
+CONFIGS = {"A": config_a, "B": config_b, "C": config_c, "D": config_d, "R1": config_r1, "R2": config_r2}
 
 
 def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None, part: str = "all") -> int:
