@@ -68,24 +68,36 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP events (profiling runs)")
-    ap.add_argument("--config", default="C", choices=["C", "D"],
-                    help="C: headline (1M subs); D: 10M subs with $share groups under 1%%/s churn")
+    ap.add_argument("--config", default="C", choices=["A", "B", "C", "D", "E", "R1", "R2"],
+                    help="C: headline (1M subs); D: 10M subs with $share groups under 1%%/s churn; "
+                         "A, B, E, R1, R2: the other SURVEY §8d shapes (secondary lines)")
+    ap.add_argument("--e-scale", type=float, default=0.2, help="config E scale (1.0 = 50M subs)")
     ap.add_argument("--d-scale", type=float, default=1.0)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--force-device", type=int, default=-1, help="rehearsal: every rank on this device")
     ap.add_argument("--churn-batch", type=int, default=10_000)
+    ap.add_argument("--churn-rate-batches", type=float, default=10.0, help="delta batches per second (1%%/s at 10M)")
     args = ap.parse_args()
     if args.config == "D":
         return bench_d(args)
+    if args.config != "C":
+        return bench_other(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.force_device >= 0:
+        local = args.force_device
     import torch
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)   # RCCL on ROCm
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)   # RCCL on ROCm
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from vernemq_amd import workloads as W
     from vernemq_amd.reg_view import RegGpuView
@@ -243,12 +255,78 @@ def main():
         dist.destroy_process_group()
 
 
+def bench_other(args):
+    """Secondary lines: configs A, B, E and the reference's bench shapes
+    R1/R2 on one GPU (publishes/s, pairs/s; no roofline: their per-publish
+    lookup counts are only known to the oracle)."""
+    import torch
+    from vernemq_amd import workloads as W
+    from vernemq_amd.reg_view import RegGpuView
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    t0 = time.time()
+    if args.config == "E":
+        w = W.config_e(scale=args.e_scale, n_pubs=args.batch)
+    elif args.config in ("R1", "R2"):
+        w = W.CONFIGS[args.config](100_000)
+    else:
+        w = W.CONFIGS[args.config]()
+    view = RegGpuView(node=w.self_node, device=0, nodes=w.nodes, max_mountpoints=max(1024, len(w.mps) + 1))
+    w.load_into(view)
+    load_s = time.time() - t0
+    log("config %s: %d subs loaded in %.1fs, %s" % (args.config, w.n_subs, load_s, view.stats_raw()))
+    pubs, words = w.publish_arrays(view)
+    npub = len(pubs)
+    d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    d_offs = torch.zeros(npub + 1, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+    out_cap = 16 * npub + 1024
+    d_out = torch.empty(out_cap * 4, dtype=torch.int32, device=dev)
+    view.match_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_out.data_ptr(), out_cap, d_offs.data_ptr(), sp)
+    torch.cuda.synchronize()
+    need = int(d_offs[-1].item())
+    view.match_status(sp)
+    if need > out_cap:
+        out_cap = need + 1024
+        d_out = torch.empty(out_cap * 4, dtype=torch.int32, device=dev)
+    step = lambda: view.match_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_out.data_ptr(), out_cap,
+                                     d_offs.data_ptr(), sp)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if view.match_status(sp) != 0:
+        raise RuntimeError("match status after warmup")
+    view.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if view.match_status(sp) != 0:
+        raise RuntimeError("match status in timed region")
+    c, e, _ = view.kernel_times()
+    em = int(d_offs[-1].item())
+    st = view.stats_raw()
+    print(json.dumps({
+        "metric": "publishes/sec (config %s)" % args.config, "value": npub * args.steps / el, "unit": "publishes/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic: SURVEY.md §8(d) config %s generator" % args.config,
+        "config": {"workload": "%s: %d subs, %d publishes per step" % (args.config, w.n_subs, npub)},
+        "pairs_per_s": em * args.steps / el, "emissions_per_step": em,
+        "kernel_us": {"count": c / 1e3, "emit": e / 1e3}, "load_s": load_s, "arena_bytes": st["device_bytes"],
+        "deferred": [st["deferred_tier1"], st["deferred_tier2"]]}), flush=True)
+
+
 def bench_d(args):
     """Config D: 10M subscriptions (8M exact, 1M '+'/'#', 1M
-    $share members on 4 nodes) under churn.  One step = one delta batch of
-    `churn_batch` ops (50/50 sub/unsub, host engine + device patches) followed
-    by one match batch of 2^20 publishes; 10 steps/s of 10k ops is the
-    configured 1 %/s churn.  Single GPU; prints one JSON line."""
+    $share members on 4 nodes) under 1 %/s churn: 10 delta batches per second
+    of 10k ops (50/50 sub/unsub, host engine + device patches).  One step =
+    one churn period: the match batches (2^20 publishes each) that fit in
+    100 ms of GPU time are queued, then the period's delta batch is applied
+    (its host work overlaps the queued matches; the patches land after them,
+    stream-ordered).  Single GPU; prints one JSON line."""
     import torch
     from vernemq_amd import workloads as W
     from vernemq_amd.reg_view import RegGpuView
@@ -293,16 +371,26 @@ def bench_d(args):
     torch.cuda.synchronize()
     if view.match_status(sp) != 0:
         raise RuntimeError("match status after warmup")
+    # GPU time of one match batch -> match batches per 100 ms churn period
+    t0 = time.perf_counter()
+    for _ in range(5):
+        match()
+    torch.cuda.synchronize()
+    t_match = (time.perf_counter() - t0) / 5
+    period = 1.0 / args.churn_rate_batches
+    per_period = max(1, int(period / t_match))
+    log("config D: match batch %.2f ms -> %d match batches per %.0f ms churn period" %
+        (t_match * 1e3, per_period, period * 1e3))
     apply_s = 0.0
-    emitted = 0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
+        for _ in range(per_period):
+            match()                                   # queued on the GPU
         ops, wds = ch.ops(ids, *batches[k])
         ta = time.perf_counter()
-        view.apply_op_arrays(ops, wds)            # host engine + patch upload (synchronous)
+        view.apply_op_arrays(ops, wds)                # host engine overlaps the queued matches
         apply_s += time.perf_counter() - ta
-        match()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     rc = view.match_status(sp)
@@ -312,15 +400,17 @@ def bench_d(args):
     st = view.stats_raw()
     res = {
         "metric": "publishes/sec under churn (config D, 10M subs incl. $share, 1%/s deltas)",
-        "value": npub * args.steps / el, "unit": "publishes/s", "n_gpus": 1, "steps": args.steps,
+        "value": npub * args.steps * per_period / el, "unit": "publishes/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic: SURVEY.md §8(d) config D generator (splitmix64 seed 0xD), scale %g" % args.d_scale,
         "config": {"workload": "D: %d live subs, %d-op delta batch + %d publishes per step" %
                                (n_live, args.churn_batch, npub)},
-        "deltas_per_s_applied": args.churn_batch * args.steps / apply_s if apply_s else None,
+        "deltas_per_s": args.churn_batch * args.steps / el,
         "apply_ms_per_batch": apply_s * 1e3 / args.steps,
-        "emissions_last_step": emitted, "load_s": load_s,
+        "match_batches_per_delta_batch": per_period,
+        "pairs_per_s": emitted * args.steps * per_period / el,
+        "emissions_per_match_batch": emitted, "load_s": load_s,
         "arena_bytes": st["device_bytes"], "rebuilds": st["rebuilds"],
         "deferred": [st["deferred_tier1"], st["deferred_tier2"]],
     }

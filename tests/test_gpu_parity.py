@@ -337,3 +337,16 @@ def test_config_d_churn_parity():
         got = [sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1]))) for i in sample]
         want = orc.fold_batch([("", b"pub", w.pub_topic(i)) for i in sample])
         assert all(g == sorted(x) for g, x in zip(got, want)), step
+
+
+def test_config_e_multitenant_parity():
+    """Config E shape at 1/500 scale (100k subs over 1,000 Zipf-sized
+    mountpoints, 12-level topics, hot-topic skew): every publish vs the oracle."""
+    from vernemq_amd import workloads as W
+    w = W.config_e(scale=0.002, n_pubs=8192)
+    v, orc = _load_both(w)
+    got = _gpu_canon(v, w, 0, w.n_pubs)
+    want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in range(w.n_pubs)])
+    bad = [i for i in range(w.n_pubs) if got[i] != sorted(want[i])]
+    assert not bad, (len(bad), w.pub_topic(bad[0]))
+    assert sum(len(x) for x in got) > w.n_pubs // 4

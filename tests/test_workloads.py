@@ -65,3 +65,17 @@ def test_config_d_churn_tables_match_oracle():
         view = v
     _compare(P, orc, "config D churn")
     assert v.stats_raw()["subs"] > 0
+
+
+def test_config_e_tables_match_oracle():
+    from tests.test_host_engine import _compare
+    from vernemq_amd.reg_view import RegGpuView
+    w = W.config_e(scale=0.0004, n_pubs=10)
+    v = RegGpuView(node=w.self_node, device=-1, nodes=w.nodes)
+    w.load_into(v)
+    orc = feed.load(w)
+
+    class P:
+        view = v
+    _compare(P, orc, "config E")
+    assert v.stats_raw()["trie_edges"] > 1000

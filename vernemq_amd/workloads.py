@@ -465,7 +465,82 @@ class Churn:
         return ev
 
 
-CONFIGS = {"A": config_a, "B": config_b, "C": config_c, "D": config_d, "R1": config_r1, "R2": config_r2}
+def _zipf_cdf(n: int, s: float) -> np.ndarray:
+    p = 1.0 / np.arange(1, n + 1, dtype=np.float64) ** s
+    return np.cumsum(p / p.sum())
+
+
+def config_e(scale: float = 1.0, seed: int = 0xE, n_pubs: int = 1 << 20, n_mps: int = 1000,
+             levels: int = 12, vocab: int = 64, n_hot: int = 1_000_000) -> Workload:
+    """Config E (§8d) at `scale` (1.0 = 50M subscriptions): `n_mps`
+    mountpoints t{n} with Zipf(1.0) sizes; topics of `levels` words from
+    `vocab` words per level; 80 % exact, 15 % with 1-3 '+', 5 % truncated +
+    '#'.  Publishes: Zipf(1.1) over `n_hot` hot topics (half instantiate a
+    random filter, half random), each in its filter's / a size-weighted MP."""
+    r = SplitMix(seed)
+    w = Workload("E")
+    n = max(1000, int(50_000_000 * scale))
+    n_hot = max(100, min(n_hot, n))
+    w.mps = ["t%d" % k for k in range(n_mps)]
+    mp_cdf = _zipf_cdf(n_mps, 1.0)
+    sub_mp = np.searchsorted(mp_cdf, r.unif(n), side="right").clip(0, n_mps - 1)
+    lvl = [[b"l%d_%d" % (k, j) for j in range(vocab)] for k in range(levels)]
+    w.words = [b"+", b"#"] + [x for lv in lvl for x in lv]
+    base = lambda k: 2 + k * vocab
+    T = np.empty((n, levels), dtype=np.int64)
+    for k in range(levels):
+        T[:, k] = base(k) + r.ints(n, vocab)
+    u = r.unif(n)
+    plus = (u >= 0.80) & (u < 0.95)
+    hashed = u >= 0.95
+    for _ in range(3):   # 1-3 '+' levels (duplicates collapse)
+        pos = r.ints(n, levels)
+        sel = plus & (r.unif(n) < 0.75)
+        T[sel, pos[sel]] = 0
+    first_plus = plus & ~(T == 0).any(axis=1)
+    T[first_plus, r.ints(n, levels)[first_plus]] = 0
+    cut = 1 + r.ints(n, levels - 1)      # '#' filters: keep 1..L-1 words then '#'
+    lens = np.where(hashed, cut + 1, levels)
+    T[hashed, cut[hashed]] = 1
+    w.tw_off = np.zeros(n + 1, dtype=np.int64)
+    w.tw_off[1:] = np.cumsum(lens)
+    w.tw = T.reshape(-1)[(np.arange(levels)[None, :] < lens[:, None]).reshape(-1)]
+    w.subinfos = std_subinfos()
+    w.sub_info = r.ints(n, len(w.subinfos))
+    w.sub_node = np.zeros(n, dtype=np.int64)
+    w.clients = [(w.mps[m], b"c%d" % i) for i, m in enumerate(sub_mp)]
+    w.sub_client = np.arange(n, dtype=np.int64)
+    # hot topics: half instantiate a filter (same MP), half random (size-weighted MP)
+    src = r.ints(n_hot, n)
+    inst = r.unif(n_hot) < 0.5
+    H = np.empty((n_hot, levels), dtype=np.int64)
+    for k in range(levels):
+        H[:, k] = base(k) + r.ints(n_hot, vocab)
+    hl = np.full(n_hot, levels, dtype=np.int64)
+    fl = lens[src]
+    ft = T[src]
+    # instantiated: copy the filter words, '+' -> random word, '#' -> 0-2 random words
+    for k in range(levels):
+        keep = inst & (k < fl) & (ft[:, k] > 1)
+        H[keep, k] = ft[keep, k]
+    has_hash = inst & (ft[np.arange(n_hot), np.minimum(fl - 1, levels - 1)] == 1)
+    extra = r.ints(n_hot, 3)
+    hl = np.where(inst, np.where(has_hash, np.minimum(fl - 1 + extra, levels), fl), hl)
+    hl = np.maximum(hl, 1)
+    hot_mp = np.where(inst, sub_mp[src], np.searchsorted(mp_cdf, r.unif(n_hot), side="right").clip(0, n_mps - 1))
+    pick = np.searchsorted(_zipf_cdf(n_hot, 1.1), r.unif(n_pubs), side="right").clip(0, n_hot - 1)
+    plen = hl[pick]
+    w.pub_words = w.words
+    w.pw_off = np.zeros(n_pubs + 1, dtype=np.int64)
+    w.pw_off[1:] = np.cumsum(plen)
+    w.pw = H[pick].reshape(-1)[(np.arange(levels)[None, :] < plen[:, None]).reshape(-1)]
+    w.pub_mp = hot_mp[pick]
+    w.notes = {"n_subs": n, "n_mps": n_mps, "levels": levels, "vocab": vocab, "n_hot": n_hot}
+    return w
+
+
+CONFIGS = {"A": config_a, "B": config_b, "C": config_c, "D": config_d, "E": config_e,
+           "R1": config_r1, "R2": config_r2}
 
 
 def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None, part: str = "all") -> int:
