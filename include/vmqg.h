@@ -205,7 +205,10 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
 
 /* Tuning knobs of the match kernels (no effect on results):
  *   "fast_g"    2 | 4 | 8  lanes per publish in the fast tier (default 2)
- *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1) */
+ *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
+ *   "fused"     0 | 1      1: one-pass kernel (walk, count, look-back offsets,
+ *                          emit in one launch); 0 (default): COUNT / scan / EMIT
+ *   "unroll"    4 | 8      records in flight per lane in the copy (default 4) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the dominant match kernel over the last

@@ -20,6 +20,17 @@ SCEN_FILES = ["pattern_matching.json", "upgrade.json", "overlapping_subscription
               "dollar_topics.json", "shared_subscriptions.json", "quirks.json"]
 
 
+# Both match pipelines of libvmqgpu: the one-pass kernel (default) and the
+# COUNT / scan / EMIT passes (vmqg_set_option "fused").
+PIPELINES = [pytest.param(1, id="fused"), pytest.param(0, id="passes")]
+
+
+def _driver(node, fused=1, **kw):
+    d = H.ProductDriver(node, device=0, **kw)
+    d.view.set_option("fused", fused)
+    return d
+
+
 def _scen():
     for f in SCEN_FILES:
         for sc in S.load(f)["scenarios"]:
@@ -34,9 +45,10 @@ def test_native_library_is_the_in_tree_build():
     assert v.stats_raw()["device_bytes"] > 0
 
 
+@pytest.mark.parametrize("fused", PIPELINES)
 @pytest.mark.parametrize("scen", list(_scen()))
-def test_golden_scenarios_on_gpu(scen):
-    S.run_scenario(scen, lambda node: H.ProductDriver(node, device=0))
+def test_golden_scenarios_on_gpu(scen, fused):
+    S.run_scenario(scen, lambda node: _driver(node, fused))
 
 
 def _compare_batches(prod, orc, pubs, ctx=""):
@@ -46,10 +58,11 @@ def _compare_batches(prod, orc, pubs, ctx=""):
         assert sorted(g) == sorted(w), "%s publish %r: got %r want %r" % (ctx, pubs[i], sorted(g)[:8], sorted(w)[:8])
 
 
+@pytest.mark.parametrize("fused", PIPELINES)
 @pytest.mark.parametrize("seed", range(4))
-def test_random_churn_fold_parity(seed):
+def test_random_churn_fold_parity(seed, fused):
     wl = H.ChurnWorkload(seed, n_clients=60)
-    prod = H.ProductDriver(wl.self_node, device=0)
+    prod = _driver(wl.self_node, fused)
     orc = O.TrieOracle(wl.self_node)
     for step in range(20):
         evs = [wl.event() for _ in range(25)]
@@ -58,9 +71,10 @@ def test_random_churn_fold_parity(seed):
         _compare_batches(prod, orc, wl.publishes(200), "seed %d batch %d" % (seed, step))
 
 
-def _load_both(w, with_oracle=True):
+def _load_both(w, with_oracle=True, fused=1):
     from vernemq_amd.reg_view import RegGpuView
     v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
+    v.set_option("fused", fused)
     w.load_into(v)
     orc = None
     if with_oracle:
@@ -75,11 +89,12 @@ def _gpu_canon(v, w, lo, hi):
             for i in range(hi - lo)]
 
 
+@pytest.mark.parametrize("fused", PIPELINES)
 @pytest.mark.parametrize("cfg", ["A", "B"])
-def test_config_full_parity(cfg):
+def test_config_full_parity(cfg, fused):
     from vernemq_amd import workloads as W
     w = W.CONFIGS[cfg]()
-    v, orc = _load_both(w)
+    v, orc = _load_both(w, fused=fused)
     n = w.n_pubs
     got = _gpu_canon(v, w, 0, n)
     want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in range(n)])
@@ -153,14 +168,16 @@ def test_r1_r2_bench_shapes():
     assert st["subs_objects"] == 0 and st["fanout_objects"] == 0
 
 
+@pytest.mark.parametrize("fused", PIPELINES)
 @pytest.mark.parametrize("levels,tier", [(7, 1), (10, 2)])
-def test_wide_frontier_deferred_tiers(levels, tier):
+def test_wide_frontier_deferred_tiers(levels, tier, fused):
     """2^levels filters over {x, +} at every level: the frontier / candidate
     lists overflow the fast tier's LDS lists (levels 7: the mid tier takes
-    them) or also the mid tier's (levels 10: global-memory scratch)."""
+    them) or also the mid tier's (levels 10: global-memory scratch).  The
+    one-pass kernel has one such path: a whole wave with global scratch."""
     import itertools
     node = "n@h"
-    prod = H.ProductDriver(node, device=0)
+    prod = _driver(node, fused)
     orc = O.TrieOracle(node)
     subs = []
     for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=levels)):
@@ -174,13 +191,14 @@ def test_wide_frontier_deferred_tiers(levels, tier):
     _compare_batches(prod, orc, pubs, "wide%d" % levels)
     st = prod.view.stats_raw()
     assert st["deferred_tier1"] >= 1
-    assert (st["deferred_tier2"] >= 1) == (tier == 2)
+    assert (st["deferred_tier2"] >= 1) == (tier == 2 and not fused)
     assert len(prod.fold(*pubs[0])) > 64
 
 
-def test_long_topics():
+@pytest.mark.parametrize("fused", PIPELINES)
+def test_long_topics(fused):
     node = "n@h"
-    prod = H.ProductDriver(node, device=0)
+    prod = _driver(node, fused)
     orc = O.TrieOracle(node)
     long_t = tuple(b"w%d" % (i % 7) for i in range(150))
     evs = [("updated", ("", b"a"), None, [(node, True, [(long_t, 1), (long_t[:80] + (b"#",), 0),
@@ -205,8 +223,9 @@ def test_mountpoints_are_disjoint_roots():
     _compare_batches(prod, orc, pubs, "mp")
 
 
-def test_empty_batch_and_output_growth():
-    prod = H.ProductDriver("n@h", device=0)
+@pytest.mark.parametrize("fused", PIPELINES)
+def test_empty_batch_and_output_growth(fused):
+    prod = _driver("n@h", fused)
     v = prod.view
     v.handle_events([("updated", ("", b"c%d" % i), None, [("n@h", True, [((b"t",), 0)])]) for i in range(5000)])
     recs, offs = v.match_arrays(*v.prepare([]))
@@ -312,7 +331,8 @@ def _config_d_expected_counts(w, live, pubs_lo, pubs_hi):
     return np.array(out, dtype=np.int64)
 
 
-def test_config_d_churn_parity():
+@pytest.mark.parametrize("fused", PIPELINES)
+def test_config_d_churn_parity(fused):
     """Config D at 1/20 scale (500k subs incl. $share groups over 4 nodes):
     after every churn batch, all publishes match the known answer and a
     sample matches the oracle publish for publish."""
@@ -320,6 +340,7 @@ def test_config_d_churn_parity():
     from vernemq_amd.reg_view import RegGpuView
     w = W.config_d(scale=0.05, n_pubs=20_000)
     v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
+    v.set_option("fused", fused)
     ids = w.load_into(v, n=w.notes["n_live"])
     orc = feed.load_prefix(w, w.notes["n_live"])
     ch = W.Churn(w)
@@ -339,12 +360,13 @@ def test_config_d_churn_parity():
         assert all(g == sorted(x) for g, x in zip(got, want)), step
 
 
-def test_config_e_multitenant_parity():
+@pytest.mark.parametrize("fused", PIPELINES)
+def test_config_e_multitenant_parity(fused):
     """Config E shape at 1/500 scale (100k subs over 1,000 Zipf-sized
     mountpoints, 12-level topics, hot-topic skew): every publish vs the oracle."""
     from vernemq_amd import workloads as W
     w = W.config_e(scale=0.002, n_pubs=8192)
-    v, orc = _load_both(w)
+    v, orc = _load_both(w, fused=fused)
     got = _gpu_canon(v, w, 0, w.n_pubs)
     want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in range(w.n_pubs)])
     bad = [i for i in range(w.n_pubs) if got[i] != sorted(want[i])]

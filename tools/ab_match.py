@@ -21,38 +21,56 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--fast-g", default="4,8")
-    ap.add_argument("--nt", default="0,1")
+    ap.add_argument("--nt", default="1")
+    ap.add_argument("--fused", default="0,1")
+    ap.add_argument("--unroll", default="4")
+    ap.add_argument("--config", default="C", choices=["C", "D"])
     ap.add_argument("--n-dev", type=int, default=1_000_000)
     args = ap.parse_args()
     import torch
     from vernemq_amd import workloads as W
     from vernemq_amd.reg_view import RegGpuView
     dev = torch.device("cuda", 0)
-    w = W.config_c(n_dev=args.n_dev)
-    v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
-    w.load_into(v)
+    if args.config == "C":
+        w = W.config_c(n_dev=args.n_dev)
+        v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
+        w.load_into(v)
+    else:
+        w = W.config_d(n_pubs=1 << 20)
+        n_live = w.notes["n_live"]
+        v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes,
+                       hints={"edges": 4 * n_live // 5, "paths": 4 * n_live // 5, "keys": n_live,
+                              "records": n_live * 11 // 10, "exact": n_live})
+        w.load_into(v, n=n_live)
     pubs, words = w.publish_arrays(v)
     d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
     d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
-    cap = 66 * len(pubs)
+    cap = 66 * len(pubs) if args.config == "C" else 520 * len(pubs)
     d_out = torch.empty(cap * 4, dtype=torch.int32, device=dev)
     d_offs = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream().cuda_stream
     variants = list(itertools.product([int(x) for x in args.fast_g.split(",")],
-                                      [int(x) for x in args.nt.split(",")]))
+                                      [int(x) for x in args.nt.split(",")],
+                                      [int(x) for x in args.fused.split(",")],
+                                      [int(x) for x in args.unroll.split(",")]))
     res = {str(vv): {"step_us": [], "count_us": [], "emit_us": []} for vv in variants}
     ref = None
     for rnd in range(args.rounds):
         for vv in variants:
             v.set_option("fast_g", vv[0])
             v.set_option("nt_stores", vv[1])
+            v.set_option("fused", vv[2])
+            v.set_option("unroll", vv[3])
             v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap,
                            d_offs.data_ptr(), sp)
             torch.cuda.synchronize()
-            assert v.match_status(sp) == 0
+            assert v.match_status(sp) == 0, vv
+            tot = int(d_offs[-1].item())
+            digest = (d_offs.clone(), d_out[: 4 * tot].view(-1, 4).to(torch.int64).sum(0).cpu())
             if ref is None:
-                ref = d_offs.clone()
-            assert torch.equal(ref, d_offs)
+                ref = digest
+            assert torch.equal(ref[0], digest[0]), ("offsets differ", vv)
+            assert torch.equal(ref[1], digest[1]), ("record checksum differs", vv)
             v.set_timing(True)
             t0 = time.perf_counter()
             for _ in range(args.steps):
@@ -67,7 +85,7 @@ def main():
             r["count_us"].append(c / 1e3)
             r["emit_us"].append(e / 1e3)
     out = {k: {m: statistics.median(x) for m, x in d.items()} for k, d in res.items()}
-    print(json.dumps({"variants": "(fast_g, nt_stores)", "median": out, "rounds": args.rounds}, indent=1))
+    print(json.dumps({"variants": "(fast_g, nt_stores, fused, unroll)", "config": args.config, "median": out, "rounds": args.rounds}, indent=1))
 
 
 if __name__ == "__main__":

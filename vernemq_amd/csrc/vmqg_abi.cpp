@@ -198,6 +198,11 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
     e.opt_fast_g = (uint32_t)value;
   } else if (n == "nt_stores") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptNtStores) : (e.opt_flags & ~vmqg::kOptNtStores);
+  } else if (n == "fused") {
+    e.opt_fused = value != 0;
+  } else if (n == "unroll") {
+    if (value != 4 && value != 8) return VMQG_E_INVAL;
+    e.opt_unroll = (uint32_t)value;
   } else {
     return VMQG_E_INVAL;
   }

@@ -23,9 +23,9 @@ Engine::~Engine() {
     for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (ev_match_done) hipEventDestroy(ev_match_done);
-    hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_deferred); hipFree(d_deferred2); hipFree(d_scan_tmp);
+    hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_deferred);
     hipFree(d_keycache);
-    hipFree(d_gstack); hipFree(d_gcand); hipFree(d_gkeys);
+    hipFree(d_lookback); hipFree(d_ostack); hipFree(d_ocand); hipFree(d_okeys);
     hipFree(d_pubs); hipFree(d_words); hipFree(d_offs); hipFree(d_out);
     if (h_patch_stage) hipHostFree(h_patch_stage);
     if (stream) hipStreamDestroy(stream);
@@ -58,10 +58,8 @@ int Engine::init(const vmqg_config& c) {
     has_device = true;
     if (hipMalloc(&d_status, 64) != hipSuccess) return VMQG_E_NOMEM;
     if (hipMalloc(&d_deferred, sizeof(uint32_t) * deferred_cap) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_deferred2, sizeof(uint32_t) * deferred_cap) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_gstack, sizeof(uint2) * (uint64_t)g_waves * g_scap) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_gcand, sizeof(uint32_t) * (uint64_t)g_waves * g_ccap) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_gkeys, sizeof(uint2) * (uint64_t)g_waves * g_kcap) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cu_count < 1)
+      cu_count = 256;
     if (!replica) {
       int rc = upload();
       if (rc) return rc;
@@ -85,8 +83,8 @@ uint32_t Engine::intern(const uint8_t* b, size_t n, bool create) {
 // ------------------------------------------------------------- paths/keys
 uint32_t Engine::path_child(uint32_t parent, uint32_t word, bool create) {
   const uint64_t k = ((uint64_t)parent << 32) | word;
-  auto it = path_index.find(k);
-  if (it != path_index.end()) return it->second;
+  const uint32_t found = path_index.find(k);
+  if (found != FlatIndex::kVoid) return found;
   if (!create) return kNone;
   const uint32_t id = (uint32_t)paths.size();
   PathInfo pi;
@@ -95,7 +93,7 @@ uint32_t Engine::path_child(uint32_t parent, uint32_t word, bool create) {
   pi.first_plus = pi.depth == 1 ? (word == kPlus) : paths[parent].first_plus;
   pi.dollar_skip = pi.first_plus || (pi.depth == 1 && word == kHash);
   paths.push_back(std::move(pi));
-  path_index.emplace(k, id);
+  path_index.insert(k, id);
   return id;
 }
 
@@ -109,11 +107,19 @@ bool Engine::path_chain(uint32_t mp, const uint32_t* w, uint32_t L, bool create,
   return true;
 }
 
+static uint64_t topic_hash(uint32_t mp, const uint32_t* w, uint32_t L) {
+  uint64_t h = mix64(((uint64_t)mp << 32) | L);
+  for (uint32_t i = 0; i < L; i++) h = mix64(h ^ ((uint64_t)w[i] * 0x9E3779B97F4A7C15ull + i));
+  return h;
+}
+
 uint32_t Engine::topic_id(uint32_t mp, const uint32_t* w, uint32_t L, bool create) {
-  std::string k(reinterpret_cast<const char*>(&mp), 4);
-  k.append(reinterpret_cast<const char*>(w), (size_t)L * 4);
-  auto it = topic_index.find(k);
-  if (it != topic_index.end()) return it->second;
+  const uint64_t h = topic_hash(mp, w, L);
+  const uint32_t found = topic_index.find(h, [&](uint32_t id) {
+    const TopicInfo& t = topics[id];
+    return t.mp == mp && t.words.size() == L && std::equal(t.words.begin(), t.words.end(), w);
+  });
+  if (found != FlatIndex::kVoid) return found;
   if (!create) return kNone;
   const uint32_t id = (uint32_t)topics.size();
   TopicInfo t;
@@ -122,7 +128,7 @@ uint32_t Engine::topic_id(uint32_t mp, const uint32_t* w, uint32_t L, bool creat
   t.exact_ok = 1;
   for (uint32_t i = 0; i < L; i++) if (w[i] == kPlus || w[i] == kHash) t.exact_ok = 0;
   topics.push_back(std::move(t));
-  topic_index.emplace(std::move(k), id);
+  topic_index.insert(h, id);
   return id;
 }
 
@@ -138,14 +144,14 @@ uint32_t Engine::local_key(uint32_t tid, bool create) {
 
 uint32_t Engine::group_key(uint32_t tid, uint32_t group, bool create) {
   const uint64_t gk = ((uint64_t)tid << 32) | group;
-  auto it = group_key_index.find(gk);
-  if (it != group_key_index.end()) return it->second;
+  const uint32_t found = group_key_index.find(gk);
+  if (found != FlatIndex::kVoid) return found;
   if (!create) return kNone;
   const uint32_t k = (uint32_t)keys.size();
   keys.emplace_back();
   keys[k].topic_id = tid;
   keys[k].group = group;
-  group_key_index.emplace(gk, k);
+  group_key_index.insert(gk, k);
   mark_key(k);
   return k;
 }
@@ -160,45 +166,23 @@ void Engine::touch(uint64_t off, uint64_t bytes) {
   }
 }
 
-uint64_t Engine::edge_find(uint32_t parent, uint32_t word) {
-  EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
-  const uint64_t mask = lay.edge_buckets - 1;
-  uint64_t b = edge_hash(parent, word) & mask;
-  for (uint64_t i = 0; i < lay.edge_buckets; i++, b = (b + 1) & mask) {
-    for (uint32_t j = 0; j < kEdgeSlotsPerBucket; j++) {
-      const EdgeSlot& s = t[b * kEdgeSlotsPerBucket + j];
-      if (s.parent == parent && s.word == word) return b * kEdgeSlotsPerBucket + j;
-      if (s.parent == kEmpty) return ~0ull;
-    }
-  }
-  return ~0ull;
-}
-
-// Flags of `child` as cached in its incoming edge slot: does it have a '#'
-// edge, a '+' edge?  (Lets the walk skip probes that must miss.)
-uint32_t Engine::child_flags(uint32_t child) {
-  uint32_t f = 0;
-  if (edge_find(child, kHash) != ~0ull) f |= kHasHash;
-  if (edge_find(child, kPlus) != ~0ull) f |= kHasPlus;
-  return f;
-}
-
-// `node` gained or lost a '#' / '+' edge: refresh the flags in its incoming slot.
+// `node` gained or lost a '#' / '+' edge: refresh the child flags cached in
+// its incoming slot (they let the walk skip probes that must miss).
 void Engine::refresh_incoming_flags(uint32_t node) {
   const PathInfo& P = paths[node];
-  if (P.parent == kNone) return;   // roots are always probed for both
-  const uint64_t si = edge_find(P.parent, P.word);
-  if (si == ~0ull) return;
-  EdgeSlot& s = region<EdgeSlot>(lay.edge_off)[si];
-  const uint32_t f = child_flags(node);
-  if (s.flags != f) {
-    s.flags = f;
-    touch(lay.edge_off + si * sizeof(EdgeSlot), sizeof(EdgeSlot));
+  if (P.parent == kNone || P.in_slot == ~0ull) return;   // roots are always probed for both
+  EdgeSlot& s = region<EdgeSlot>(lay.edge_off)[P.in_slot];
+  if (s.flags != P.eflags) {
+    s.flags = P.eflags;
+    touch(lay.edge_off + P.in_slot * sizeof(EdgeSlot), sizeof(EdgeSlot));
   }
 }
 
+// (parent, word) -> child.  Path ids are interned by (parent, word), so the
+// edge exists iff the child's in_slot is set (ets:insert of an identical
+// #trie{} is a no-op).
 void Engine::edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
-  if (edge_find(parent, word) != ~0ull) return;   // ets:insert of an identical #trie{}
+  if (paths[child].in_slot != ~0ull) return;
   EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
   const uint64_t mask = lay.edge_buckets - 1;
   uint64_t b = edge_hash(parent, word) & mask;
@@ -208,24 +192,32 @@ void Engine::edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
       EdgeSlot& s = t[si];
       if (s.parent == kEmpty || s.parent == kTomb) {
         if (s.parent == kTomb) edge_tomb--;
-        s = EdgeSlot{parent, word, child, child_flags(child)};
+        s = EdgeSlot{parent, word, child, paths[child].eflags};
         edge_live++;
+        paths[child].in_slot = si;
         touch(lay.edge_off + si * sizeof(EdgeSlot), sizeof(EdgeSlot));
-        if (word == kHash || word == kPlus) refresh_incoming_flags(parent);
+        if (word == kHash || word == kPlus) {
+          paths[parent].eflags |= word == kHash ? kHasHash : kHasPlus;
+          refresh_incoming_flags(parent);
+        }
         return;
       }
     }
   }
 }
 
-void Engine::edge_erase(uint32_t parent, uint32_t word) {
-  const uint64_t si = edge_find(parent, word);
+void Engine::edge_erase(uint32_t parent, uint32_t word, uint32_t child) {
+  const uint64_t si = paths[child].in_slot;
   if (si == ~0ull) return;
   EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
   t[si] = EdgeSlot{kTomb, kTomb, kTomb, 0};
+  paths[child].in_slot = ~0ull;
   edge_live--; edge_tomb++;
   touch(lay.edge_off + si * sizeof(EdgeSlot), sizeof(EdgeSlot));
-  if (word == kHash || word == kPlus) refresh_incoming_flags(parent);
+  if (word == kHash || word == kPlus) {
+    paths[parent].eflags &= ~(word == kHash ? kHasHash : kHasPlus);
+    refresh_incoming_flags(parent);
+  }
 }
 
 Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) const {
@@ -294,6 +286,7 @@ void Engine::rebuild(uint64_t extra_edges, bool compact) {
     full_image = true;
     exact_live = exact_tomb = 0;
     rec_top = rec_garbage = kl_top = kl_garbage = xw_top = xw_garbage = 0;
+    for (auto& p : paths) p.in_slot = ~0ull;
     for (auto& e : live) edge_insert(e.parent, e.word, e.child);
     for (auto& k : keys) { k.off = 0; k.cap = 0; k.dirty_pos.clear(); }
     for (auto& t : topics) { t.slot = ~0ull; t.words_off = kNone; }
@@ -488,7 +481,7 @@ static bool contains_wildcard(const uint32_t* w, uint32_t L) {   // vmq_topic.er
 void Engine::trie_add_path(uint32_t parent, uint32_t word, uint32_t child) {
   PathInfo& P = paths[parent];
   if (P.rec) {
-    if (edge_find(parent, word) == ~0ull) {
+    if (paths[child].in_slot == ~0ull) {
       P.ec++;
       mark_path(parent);
       edge_insert(parent, word, child);
@@ -532,7 +525,7 @@ void Engine::trie_delete(uint32_t p, const std::vector<uint32_t>& chain, const u
   mark_path(p);
   for (int64_t i = (int64_t)L - 1; i >= 0; i--) {
     const uint32_t parent = chain[i];
-    edge_erase(parent, w[i]);
+    edge_erase(parent, w[i], chain[i + 1]);
     PathInfo& Q = paths[parent];
     if (!Q.rec) return;                                  // :439-440
     if (Q.ec == 1 && !Q.topic_set) {                     // :434-436
@@ -705,6 +698,12 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
 // --------------------------------------------------------------- device
 int Engine::upload() {
   last_patches.clear();
+  if (!full_image && dirty_chunks.size() * sizeof(Patch) > lay.total_bytes / 2) {
+    // patches would outweigh the image (bulk loads): ship the image instead
+    full_image = true;
+    std::fill(dirty_bits.begin(), dirty_bits.end(), 0);
+    dirty_chunks.clear();
+  }
   last_full = full_image;
   if (!full_image) {
     last_patches.reserve(dirty_chunks.size());
@@ -761,19 +760,42 @@ int Engine::upload() {
 }
 
 int Engine::ensure_match_scratch(uint64_t npub) {
-  const uint64_t need = scan_tmp_elems(npub + 1);
-  if (need > scan_tmp_cap) {
-    if (d_scan_tmp) hipFree(d_scan_tmp);
-    d_scan_tmp = nullptr;
-    scan_tmp_cap = next_pow2(need);
-    if (hipMalloc(&d_scan_tmp, scan_tmp_cap * sizeof(uint64_t)) != hipSuccess) { scan_tmp_cap = 0; return VMQG_E_NOMEM; }
-  }
   if (npub > keycache_cap) {
     if (d_keycache) hipFree(d_keycache);
     d_keycache = nullptr;
     keycache_cap = next_pow2(npub);
     if (hipMalloc(&d_keycache, keycache_cap * 32) != hipSuccess) { keycache_cap = 0; return VMQG_E_NOMEM; }
   }
+  return VMQG_OK;
+}
+
+// Look-back granules for `granules` tiles / chunks; advances the call's tag.
+int Engine::ensure_lookback(uint64_t granules, hipStream_t st) {
+  if (granules > lookback_cap) {
+    if (d_lookback) { hipStreamSynchronize(st); hipFree(d_lookback); }
+    d_lookback = nullptr;
+    lookback_cap = next_pow2(std::max<uint64_t>(granules, 1024));
+    if (hipMalloc(&d_lookback, lookback_cap * 8) != hipSuccess) { lookback_cap = 0; return VMQG_E_NOMEM; }
+    if (hipMemsetAsync(d_lookback, 0, lookback_cap * 8, st) != hipSuccess) return VMQG_E_DEVICE;
+    lb_tag = 0;
+  }
+  if (++lb_tag >= (1u << 20)) {   // granule tags are 20 bits: clear before reuse
+    if (hipMemsetAsync(d_lookback, 0, lookback_cap * 8, st) != hipSuccess) return VMQG_E_DEVICE;
+    lb_tag = 1;
+  }
+  return VMQG_OK;
+}
+
+// Global scratch (o_cap stack / candidate / key entries) for `waves` waves.
+int Engine::ensure_wave_scratch(uint32_t waves, hipStream_t st) {
+  if (o_waves >= waves) return VMQG_OK;
+  if (d_ostack) { hipStreamSynchronize(st); hipFree(d_ostack); hipFree(d_ocand); hipFree(d_okeys); }
+  d_ostack = nullptr; d_ocand = nullptr; d_okeys = nullptr; o_waves = 0;
+  const uint64_t n = (uint64_t)waves * o_cap;
+  if (hipMalloc(&d_ostack, n * sizeof(uint2)) != hipSuccess || hipMalloc(&d_ocand, n * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&d_okeys, n * sizeof(uint2)) != hipSuccess)
+    return VMQG_E_NOMEM;
+  o_waves = waves;
   return VMQG_OK;
 }
 
@@ -796,11 +818,13 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.pubs = pubs; a.words = words; a.npub = npub;
   a.offsets = offs; a.out = out; a.out_cap = out_cap;
   a.keycache = d_keycache;
-  a.status = d_status; a.deferred = d_deferred; a.deferred2 = d_deferred2;
-  a.deferred_cap = deferred_cap; a.g_waves = g_waves;
-  a.g_stack = d_gstack; a.g_cand = d_gcand; a.g_keys = d_gkeys;
-  a.g_scap = g_scap; a.g_ccap = g_ccap; a.g_kcap = g_kcap;
+  a.status = d_status; a.deferred = d_deferred;
+  a.deferred_cap = deferred_cap;
   a.fast_g = opt_fast_g; a.opts = opt_flags;
+  a.lookback = d_lookback; a.lb_tag = lb_tag;
+  a.nchunks = (uint32_t)(((uint64_t)npub + fused_chunk(opt_fast_g) - 1) / fused_chunk(opt_fast_g));
+  a.o_stack = d_ostack; a.o_cand = d_ocand; a.o_keys = d_okeys;
+  a.o_cap = o_cap; a.o_waves = o_waves;
   return a;
 }
 
@@ -810,27 +834,45 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   if (!d_arena) return VMQG_E_STATE;
   hipSetDevice(device);
   if (!st) st = stream;
-  int rc = ensure_match_scratch(npub);
-  if (rc) return rc;
-  const MatchArgs a = args_for(d_pubs_, npub, d_words_, d_out_, out_cap, d_offsets);
   if (hipMemsetAsync(d_status, 0, 16, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (hipMemsetAsync(d_offsets + npub, 0, 8, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (npub == 0) return hipMemsetAsync(d_offsets, 0, 8, st) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
+  int rc;
+  if (opt_fused) {
+    // one launch: walk + count + look-back offsets + emit (k_match_fused)
+    const uint32_t CH = fused_chunk(opt_fast_g);
+    const uint32_t nchunks = (uint32_t)(((uint64_t)npub + CH - 1) / CH);
+    const uint32_t per_cu = (uint32_t)std::max(1, fused_blocks_per_cu(opt_fast_g, opt_unroll));
+    if ((rc = ensure_lookback(nchunks, st)) || (rc = ensure_wave_scratch(per_cu * cu_count * 4, st))) return rc;
+    const MatchArgs a = args_for(d_pubs_, npub, d_words_, d_out_, out_cap, d_offsets);
+    const uint32_t grid = std::min<uint32_t>(nchunks, per_cu * cu_count);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
+    if (launch_fused(a, grid, opt_unroll, st) != hipSuccess) return VMQG_E_DEVICE;
+    if (timing) { hipEventRecord(e1, st); t_emit.push_back({e0, e1}); t_count.push_back({nullptr, nullptr}); }
+    if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
+    return VMQG_OK;
+  }
+  // COUNT (fast groups, then the wave path for what they deferred), one-launch
+  // scan of the counts, EMIT (same two tiers)
+  const uint32_t per_cu = (uint32_t)std::max(1, wave_blocks_per_cu());
+  if ((rc = ensure_match_scratch(npub)) || (rc = ensure_lookback(scan_tiles(npub), st)) ||
+      (rc = ensure_wave_scratch(per_cu * cu_count * 4, st)))
+    return rc;
+  MatchArgs a = args_for(d_pubs_, npub, d_words_, d_out_, out_cap, d_offsets);
+  a.o_waves = per_cu * cu_count * 4;   // the wave kernel's grid
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
   if (timing) {
     hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2); hipEventCreate(&e3);
     hipEventRecord(e0, st);
   }
-  // COUNT: fast tier, then the tiers that take what the previous one deferred
-  if (npub && launch_match(a, 0, 0, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 0, 0, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) hipEventRecord(e1, st);
-  if (npub && launch_match(a, 0, 1, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (npub && launch_match(a, 0, 2, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (launch_scan(d_offsets, (uint64_t)npub + 1, d_scan_tmp, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 0, 1, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_scan(a, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) hipEventRecord(e2, st);
-  if (npub && launch_match(a, 1, 0, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 1, 0, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) { hipEventRecord(e3, st); t_count.push_back({e0, e1}); t_emit.push_back({e2, e3}); }
-  if (npub && launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (npub && launch_match(a, 1, 2, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
@@ -847,7 +889,7 @@ int Engine::match_status(hipStream_t st) {
   last_deferred[1] = h[2];
   if (h[1] & (2u | 1u)) return VMQG_E_FRONTIER;
   if (h[1] & 4u) return VMQG_E_OVERFLOW;
-  if (h[1] & 8u) return VMQG_E_DEVICE;
+  if (h[1] & (8u | 16u)) return VMQG_E_DEVICE;   // count mismatch, look-back timeout
   return VMQG_OK;
 }
 
@@ -857,10 +899,10 @@ void Engine::collect_times() {
   for (size_t i = 0; i < t_count.size(); i++) {
     float a = 0, b = 0;
     hipEventSynchronize(t_emit[i].second);
-    hipEventElapsedTime(&a, t_count[i].first, t_count[i].second);
+    if (t_count[i].first) hipEventElapsedTime(&a, t_count[i].first, t_count[i].second);   // null: fused call
     hipEventElapsedTime(&b, t_emit[i].first, t_emit[i].second);
     sum_count_ns += a * 1e6; sum_emit_ns += b * 1e6; n_timed++;
-    hipEventDestroy(t_count[i].first); hipEventDestroy(t_count[i].second);
+    if (t_count[i].first) { hipEventDestroy(t_count[i].first); hipEventDestroy(t_count[i].second); }
     hipEventDestroy(t_emit[i].first); hipEventDestroy(t_emit[i].second);
   }
   t_count.clear(); t_emit.clear();

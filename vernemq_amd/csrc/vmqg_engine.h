@@ -6,6 +6,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -22,8 +23,57 @@ struct Nog {
   bool operator==(const Nog& o) const { return node == o.node && group == o.group; }
 };
 
+// Open-addressed uint64 -> uint32 index (linear probing, load <= 1/2, no
+// erase: paths, topics and keys are interned for the context's lifetime).
+// Several values may share a key (topic_index keys by a 64-bit hash of MP +
+// words): find() takes a predicate that verifies the stored value.
+class FlatIndex {
+ public:
+  static constexpr uint32_t kVoid = 0xFFFFFFFFu;
+  void reserve(uint64_t n) { if (n * 2 > slots_.size()) regrow(n * 2); }
+  // first value stored under `key` for which ok(value) holds, else kVoid
+  template <class Ok>
+  uint32_t find(uint64_t key, Ok ok) const {
+    if (slots_.empty()) return kVoid;
+    const uint64_t m = slots_.size() - 1;
+    for (uint64_t i = mix64(key) & m;; i = (i + 1) & m) {
+      const Slot& s = slots_[i];
+      if (s.val == kVoid) return kVoid;
+      if (s.key == key && ok(s.val)) return s.val;
+    }
+  }
+  uint32_t find(uint64_t key) const { return find(key, [](uint32_t) { return true; }); }
+  void insert(uint64_t key, uint32_t val) {
+    if ((n_ + 1) * 2 > slots_.size()) regrow(std::max<uint64_t>(1024, slots_.size() * 2));
+    put(key, val);
+    n_++;
+  }
+  uint64_t size() const { return n_; }
+
+ private:
+  struct Slot { uint64_t key; uint32_t val; };
+  void put(uint64_t key, uint32_t val) {
+    const uint64_t m = slots_.size() - 1;
+    uint64_t i = mix64(key) & m;
+    while (slots_[i].val != kVoid) i = (i + 1) & m;
+    slots_[i] = Slot{key, val};
+  }
+  void regrow(uint64_t want) {
+    uint64_t cap = 1;
+    while (cap < want) cap <<= 1;
+    std::vector<Slot> old;
+    old.swap(slots_);
+    slots_.assign(cap, Slot{0, kVoid});
+    for (const Slot& s : old) if (s.val != kVoid) put(s.key, s.val);
+  }
+  std::vector<Slot> slots_;
+  uint64_t n_ = 0;
+};
+
 struct PathInfo {
   uint32_t parent, word, mp, depth;
+  uint64_t in_slot = ~0ull;         // edge-table slot of the edge (parent, word) -> this path, if present
+  uint8_t eflags = 0;               // this path's own '#' / '+' edges present (kHasHash | kHasPlus)
   uint32_t topic_id = kNone;        // (MP, path words) term, once known
   uint32_t kl_off = 0, kl_cap = 0;  // keylist range owned by this path
   uint8_t rec = 0, topic_set = 0;   // vmq_trie_node record / its topic field
@@ -79,11 +129,11 @@ struct Engine {
 
   // ---- logical state
   std::vector<PathInfo> paths;                              // ids [0, max_mp) are roots
-  std::unordered_map<uint64_t, uint32_t> path_index;        // parent<<32|word -> path
+  FlatIndex path_index;                                     // parent<<32|word -> path
   std::vector<KeyInfo> keys;
-  std::unordered_map<uint64_t, uint32_t> group_key_index;   // topic<<32|group -> key
+  FlatIndex group_key_index;                                // topic<<32|group -> key
   std::vector<TopicInfo> topics;
-  std::unordered_map<std::string, uint32_t> topic_index;    // (mp, words) -> topic
+  FlatIndex topic_index;                                    // hash(mp, words) -> topic (verified)
   uint64_t n_trie_nodes = 0, n_trie_topics = 0, n_subs_objects = 0, n_fanout = 0, n_remote_keys = 0;
 
   // ---- mirror of the device arena
@@ -105,12 +155,9 @@ struct Engine {
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
   Patch* h_patch_stage = nullptr; uint64_t h_patch_cap = 0;
   Patch* d_patch = nullptr; uint64_t d_patch_cap = 0;
-  uint32_t* d_status = nullptr; uint32_t* d_deferred = nullptr; uint32_t* d_deferred2 = nullptr;
+  uint32_t* d_status = nullptr; uint32_t* d_deferred = nullptr;
   uint32_t deferred_cap = 1u << 20;
-  uint64_t* d_scan_tmp = nullptr; uint64_t scan_tmp_cap = 0;
   void* d_keycache = nullptr; uint64_t keycache_cap = 0;   // publishes
-  uint2* d_gstack = nullptr; uint32_t* d_gcand = nullptr; uint2* d_gkeys = nullptr;
-  uint32_t g_waves = 16, g_scap = 1u << 15, g_ccap = 1u << 15, g_kcap = 1u << 15;
   // host-buffer match staging
   void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
   void* d_words = nullptr; uint64_t d_words_cap = 0;
@@ -119,6 +166,12 @@ struct Engine {
   hipEvent_t ev_match_done = nullptr;
   bool timing = false;
   uint32_t opt_fast_g = 2, opt_flags = kOptNtStores;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
+  uint32_t opt_fused = 0, opt_unroll = 4;              // one-pass kernel (A/B: slower, off); its copy unroll
+  // look-back granules (tagged per call), global scratch of the wave path
+  uint64_t* d_lookback = nullptr; uint64_t lookback_cap = 0; uint32_t lb_tag = 0;
+  uint2* d_ostack = nullptr; uint32_t* d_ocand = nullptr; uint2* d_okeys = nullptr;
+  uint32_t o_cap = 4096, o_waves = 0;
+  int cu_count = 0;
   uint32_t last_deferred[2] = {0, 0};   // tier-1 / tier-2 publishes of the last checked batch
   std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_emit;
   double sum_count_ns = 0, sum_emit_ns = 0; uint64_t n_timed = 0;
@@ -154,10 +207,8 @@ struct Engine {
   // mirror
   template <class T> T* region(uint64_t off) { return reinterpret_cast<T*>(reinterpret_cast<uint8_t*>(mirror.data()) + off); }
   void touch(uint64_t off, uint64_t bytes);
-  uint64_t edge_find(uint32_t parent, uint32_t word) ;
   void edge_insert(uint32_t parent, uint32_t word, uint32_t child);
-  void edge_erase(uint32_t parent, uint32_t word);
-  uint32_t child_flags(uint32_t child);
+  void edge_erase(uint32_t parent, uint32_t word, uint32_t child);
   void refresh_incoming_flags(uint32_t node);
   Layout plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) const;
   void rebuild(uint64_t extra_edges, bool compact = false);
@@ -170,6 +221,8 @@ struct Engine {
   // device
   int upload();
   int ensure_match_scratch(uint64_t npub);
+  int ensure_lookback(uint64_t granules, hipStream_t st);
+  int ensure_wave_scratch(uint32_t waves, hipStream_t st);
   MatchArgs args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, Record* out, uint64_t out_cap,
                      uint64_t* offs) const;
   int match_device(const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words, Record* d_out,

@@ -319,36 +319,46 @@ __device__ __forceinline__ void store_rec(Record* out, uint64_t i, uint4 v) {
   }
 }
 
-// Tiers: 0 = fast (G = kFastG lanes per publish, small LDS lists),
-// 1 = mid (G = 64, one publish per wave, large LDS lists, publishes deferred
-// by tier 0), 2 = slow (G = 64, global-memory lists, deferred by tier 1).
+// Tiers: 0 = fast (G = fast_g lanes per publish, small LDS lists); 1 = wave
+// (G = 64, one publish per wave, publishes deferred by tier 0): 256-entry LDS
+// lists first, the wave's global scratch (o_cap entries) when those overflow.
 template <int TIER>
 __device__ __forceinline__ void defer_or_fail(const MatchArgs& a, uint32_t p) {
   if (TIER == 0) {
     const uint32_t idx = atomicAdd(&a.status[0], 1u);
     if (idx < a.deferred_cap) a.deferred[idx] = p;
     else atomicOr(&a.status[1], kErrDeferFull);
-  } else if (TIER == 1) {
-    const uint32_t idx = atomicAdd(&a.status[2], 1u);
-    if (idx < a.deferred_cap) a.deferred2[idx] = p;
-    else atomicOr(&a.status[1], kErrDeferFull);
   } else {
     atomicOr(&a.status[1], kErrFrontier);
   }
 }
 
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= (uint32_t)o) v += t;
+  }
+  return v;
+}
+
 // ------------------------------------------------------------ COUNT pass
+// Returns false when the walk overflowed `s`.  Tier 0 defers the publish;
+// tier 1 returns to its caller, which retries with global scratch (tier 2
+// role: an overflow there is a frontier error).
 template <int G, int TIER>
-__device__ void count_publish(const MatchArgs& a, uint32_t p, const Scratch& s, const Group<G>& g) {
+__device__ bool count_publish(const MatchArgs& a, uint32_t p, const Scratch& s, const Group<G>& g) {
   const vmqg_pub pub = a.pubs[p];
   const Matched m = walk_publish<G>(a, pub, s, g);
-  if (g.lane != 0) return;
+  if (m.overflow && TIER == 1) return false;
+  if (g.lane != 0) return !m.overflow;
   uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
   if (m.overflow) {
     defer_or_fail<TIER>(a, p);
     a.offsets[p] = 0;
     kc[0] = make_uint4(0, kRewalk, 0, 0);
-    return;
+    return false;
   }
   a.offsets[p] = m.total;
   // key cache: total, nk, remote mask, up to two {record off, count}
@@ -361,22 +371,24 @@ __device__ void count_publish(const MatchArgs& a, uint32_t p, const Scratch& s, 
   } else {
     kc[0] = make_uint4(m.total, kRewalk, 0, 0);
   }
+  return true;
 }
 
 // ------------------------------------------------------------- EMIT pass
 // Per-group result of the resolve step, staged in LDS for the wave copy.
 struct GroupMeta {
   uint32_t rel, span, nk, ksum;   // output start relative to the wave's first publish, length
-  uint32_t rm_lo, rm_hi, ok, pad;
+  uint32_t rm_lo, rm_hi, ok, crel;   // crel: start among the wave's copied (ok) records
 };
 
 // EMIT for the GPW consecutive publishes [first, first + n) of one wave.
 // Resolve (key cache or re-walk) is per group; the copy is wave-wide over
-// the wave's contiguous output range, so every store instruction writes
-// 64 x 16 B = 1 KiB contiguous.
-template <int G, int GPW, bool NT>
-__device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const Scratch& s, const Group<G>& g,
-                          GroupMeta* gm, const uint2* keys_wave, uint32_t kstride) {
+// the wave's output range minus the ranges of publishes a later tier
+// writes, so every store instruction writes up to 64 x 16 B = 1 KiB
+// contiguous.  `s2` (tier 1): global scratch for a re-walk that overflows `s`.
+template <int G, int GPW, bool NT, int U>
+__device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const Scratch& s, const Scratch* s2,
+                          const Group<G>& g, GroupMeta* gm, const uint2* keys_wave, uint32_t kstride) {
   const uint32_t p = first + g.gidx;
   const bool valid = g.gidx < n;
   uint32_t total = 0, nk = 0, ksum = 0;
@@ -388,8 +400,12 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
     obase = a.offsets[p];
     oend = a.offsets[p + 1];
     if (h.y == kRewalk) {
-      const Matched m = walk_publish<G>(a, a.pubs[p], s, g);
-      if (m.overflow) ok = false;   // written by the next tier
+      Matched m = walk_publish<G>(a, a.pubs[p], s, g);
+      if (m.overflow && s2) {
+        m = walk_publish<G>(a, a.pubs[p], *s2, g);
+        keys_wave = s2->keys;   // G == 64: one publish per wave
+      }
+      if (m.overflow) ok = false;   // written by the next tier (or a latched frontier error)
       else { total = m.total; nk = m.nk; ksum = m.ksum; rmask = m.rmask; }
     } else {
       total = h.x; nk = h.y < 2 ? h.y : 2; rmask = ((uint64_t)h.w << 32) | h.z;
@@ -404,34 +420,43 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
     if (ok && oend - obase != total) { if (g.lane == 0) atomicOr(&a.status[1], kErrMismatch); ok = false; }
   }
   const uint64_t wbase = a.offsets[first];
-  const uint64_t wend = a.offsets[first + n];
-  const uint32_t T = wend > a.out_cap ? 0 : (uint32_t)(wend - wbase);
   if (g.lane == 0)
-    gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : T, (uint32_t)(oend - obase), nk == 0 ? 1 : nk,
-                           ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), ok ? 1u : 0u, 0u};
+    gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : 0u, ok ? (uint32_t)(oend - obase) : 0u,
+                           nk == 0 ? 1 : nk, ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), ok ? 1u : 0u, 0u};
   wave_sync();
-  // 4 records per lane in flight: all loads issued before the stores
+  // compact the copied ranges: crel = exclusive scan of the ok spans
+  const uint32_t lane = __lane_id();
+  uint32_t Tok;
+  if (GPW == 1) {
+    Tok = gm[0].span;
+  } else {
+    const uint32_t sp = lane < (uint32_t)GPW ? gm[lane].span : 0u;
+    const uint32_t incl = wave_incl_scan32(sp);
+    if (lane < (uint32_t)GPW) gm[lane].crel = incl - sp;
+    Tok = __shfl(incl, GPW - 1, 64);
+    wave_sync();
+  }
+  // U records per lane in flight: all loads issued before the stores
   uint32_t j = 0;
-  for (uint32_t r0 = __lane_id(); r0 < T; r0 += 256) {
-    uint4 v[4];
-    bool w[4];
+  for (uint32_t r0 = lane; r0 < Tok; r0 += 64 * U) {
+    uint4 v[U];
+    uint64_t dst[U];
+    bool w[U];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < U; u++) {
       const uint32_t r = r0 + 64 * u;
-      w[u] = false;
-      if (r < T) {
-        while (j + 1 < (uint32_t)GPW && gm[j + 1].rel <= r) j++;
+      w[u] = r < Tok;
+      if (w[u]) {
+        while (j + 1 < (uint32_t)GPW && gm[j + 1].crel <= r) j++;
         const GroupMeta m = gm[j];
-        if (m.ok) {
-          const uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
-          v[u] = emission(a, keys_wave + (uint64_t)j * kstride, m.nk, m.ksum, rm, r - m.rel);
-          w[u] = true;
-        }
+        const uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
+        v[u] = emission(a, keys_wave + (uint64_t)j * kstride, m.nk, m.ksum, rm, r - m.crel);
+        dst[u] = wbase + m.rel + (r - m.crel);
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++)
-      if (w[u]) store_rec<NT>(a.out, wbase + r0 + 64 * u, v[u]);
+    for (int u = 0; u < U; u++)
+      if (w[u]) store_rec<NT>(a.out, dst[u], v[u]);
   }
   wave_sync();
 }
@@ -455,77 +480,366 @@ __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
     if (MODE == 0) {
       if (g.gidx < n) count_publish<G, 0>(a, base + g.gidx, s, g);
     } else {
-      emit_wave<G, GPW, NT>(a, base, n, s, g, gm[wv], ky[wv * GPW], KC);
+      emit_wave<G, GPW, NT, 4>(a, base, n, s, nullptr, g, gm[wv], ky[wv * GPW], KC);
     }
     wave_sync();
   }
 }
 
-// Tiers 1 and 2: one publish per wave from the deferred lists.
-template <int MODE, int TIER>
-__global__ __launch_bounds__(256) void k_match_deferred(MatchArgs a) {
+// Tier 1: one publish per wave from the deferred list; LDS lists, then the
+// wave's global scratch.
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
   constexpr uint32_t kMidCap = 256;
-  __shared__ uint2 st[TIER == 1 ? kWaves : 1][TIER == 1 ? kMidCap : 1];
-  __shared__ uint32_t cd[TIER == 1 ? kWaves : 1][TIER == 1 ? kMidCap : 1];
-  __shared__ uint2 ky[TIER == 1 ? kWaves : 1][TIER == 1 ? kMidCap : 1];
+  __shared__ uint2 st[kWaves][kMidCap];
+  __shared__ uint32_t cd[kWaves][kMidCap];
+  __shared__ uint2 ky[kWaves][kMidCap];
   __shared__ GroupMeta gm[kWaves][1];
   const Group<64> g;
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t gw = blockIdx.x * kWaves + wv;
-  Scratch s;
-  if (TIER == 1) {
-    s = Scratch{st[wv], cd[wv], ky[wv], kMidCap, kMidCap, kMidCap};
-  } else {
-    s = Scratch{a.g_stack + (uint64_t)gw * a.g_scap, a.g_cand + (uint64_t)gw * a.g_ccap,
-                a.g_keys + (uint64_t)gw * a.g_kcap, a.g_scap, a.g_ccap, a.g_kcap};
-  }
-  const uint32_t* list = TIER == 1 ? a.deferred : a.deferred2;
-  uint32_t n = TIER == 1 ? a.status[0] : a.status[2];
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
+  const Scratch s{st[wv], cd[wv], ky[wv], kMidCap, kMidCap, kMidCap};
+  const Scratch so{a.o_stack + gw * a.o_cap, a.o_cand + gw * a.o_cap, a.o_keys + gw * a.o_cap,
+                   a.o_cap, a.o_cap, a.o_cap};
+  uint32_t n = a.status[0];
   if (n > a.deferred_cap) n = a.deferred_cap;
   const uint32_t nwaves = gridDim.x * kWaves;
-  for (uint32_t d = gw; d < n; d += nwaves) {
-    const uint32_t p = list[d];
-    if (MODE == 0) count_publish<64, TIER>(a, p, s, g);
-    else emit_wave<64, 1, false>(a, p, 1, s, g, gm[wv], s.keys, 0);
+  for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
+    const uint32_t p = a.deferred[d];
+    if (MODE == 0) {
+      if (!count_publish<64, 1>(a, p, s, g)) {
+        if (__lane_id() == 0) atomicAdd(&a.status[2], 1u);
+        count_publish<64, 2>(a, p, so, g);
+      }
+    } else {
+      emit_wave<64, 1, NT, 8>(a, p, 1, s, &so, g, gm[wv], s.keys, 0);
+    }
     wave_sync();
   }
 }
 
+// ------------------------------------------------------ fused single pass
+// k_match_fused: one launch does what COUNT + scan + EMIT do above.  A block
+// takes chunks of CH = 4 * (64 / G) consecutive publishes by ticket (so a
+// chunk's predecessors are always owned by running blocks) and for each:
+//   1. walks every publish with G lanes (fast LDS lists, as COUNT);
+//   2. publishes that overflow the fast lists are walked again by a whole
+//      wave with global scratch (o_stack / o_cand / o_keys) — their count;
+//   3. scans the chunk's counts (per wave, then across the 4 waves);
+//   4. gets the chunk's output base by decoupled look-back over the
+//      predecessors' 8-B {tag, flag, value} granules (agent-scope relaxed
+//      atomics: the granule is its own flag, cdna_hip_programming.md G16 R2);
+//   5. writes offsets[] for its publishes;
+//   6. copies the fast publishes' records wave-wide (contiguous, NT stores),
+//      skipping the ranges of the wave-path publishes;
+//   7. re-walks each wave-path publish with a whole wave and copies its
+//      records.
+// The walk of one chunk overlaps the record stores of the other blocks on
+// the CU, which a COUNT -> EMIT kernel boundary forbids.
+constexpr uint64_t kLbValueMask = (1ull << 42) - 1;
+constexpr uint64_t kLbAgg = 1, kLbIncl = 2;
+constexpr uint32_t kErrLookback = 16u;
+constexpr uint32_t kSpinLimit = 1u << 26;
+
+__device__ __forceinline__ uint64_t lb_pack(uint32_t tag, uint64_t flag, uint64_t v) {
+  return ((uint64_t)tag << 44) | (flag << 42) | (v & kLbValueMask);
+}
+__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t x) {
+  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive output base of `chunk`, computed by one whole wave.  Posts the
+// chunk's aggregate first so successors can pass over it, then looks back
+// 64 predecessors per round (lane i reads chunk - 1 - i - 64 r): the nearest
+// predecessor with an inclusive prefix ends the walk, the aggregates of the
+// ones in between are summed.  A round retries while any granule it needs
+// is not yet posted (tag of an earlier call).
+__device__ uint64_t lookback(const MatchArgs& a, uint32_t chunk, uint64_t agg) {
+  const uint32_t lane = __lane_id();
+  uint64_t* lb = a.lookback;
+  if (chunk == 0) {
+    if (lane == 0) lb_store(lb, lb_pack(a.lb_tag, kLbIncl, agg));
+    return 0;
+  }
+  if (lane == 0) lb_store(lb + chunk, lb_pack(a.lb_tag, kLbAgg, agg));
+  uint64_t excl = 0;
+  int64_t top = (int64_t)chunk - 1;
+  for (uint32_t spins = 0;;) {
+    const int64_t j = top - (int64_t)lane;
+    uint64_t x = 0;
+    bool ready = false;
+    if (j >= 0) { x = lb_load(lb + j); ready = (uint32_t)(x >> 44) == a.lb_tag; }
+    const uint64_t incl = __ballot(ready && ((x >> 42) & 3) == kLbIncl);
+    const uint64_t waiting = __ballot(j >= 0 && !ready);
+    const uint32_t stop = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;   // nearest inclusive predecessor
+    const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);       // lanes 0..stop
+    if (waiting & need) {
+      if (++spins > kSpinLimit) { if (lane == 0) atomicOr(&a.status[1], kErrLookback); break; }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    uint64_t v = (lane <= stop && j >= 0) ? (x & kLbValueMask) : 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
+      v += ((uint64_t)hi << 32) | lo;
+    }
+    excl += v;
+    if (stop < 64) break;
+    top -= 64;
+  }
+  if (lane == 0) lb_store(lb + chunk, lb_pack(a.lb_tag, kLbIncl, excl + agg));
+  return excl;
+}
+
+struct FusedMeta {               // per publish of the chunk
+  uint32_t rel, span, crel, ok;  // output start / length relative to the wave; start among ok records
+  uint32_t nk, ksum, rm_lo, rm_hi;
+};
+
+// Wave path (G = 64, global scratch) of the fused kernel: a publish whose
+// frontier / candidate / key lists overflow the fast LDS lists.  Kept out of
+// line so the fast walk's register budget is not the sum of both paths.
+__device__ __noinline__ uint32_t wave_path_count(const MatchArgs& a, uint32_t p, const Scratch& so) {
+  const Group<64> g64;
+  const Matched mo = walk_publish<64>(a, a.pubs[p], so, g64);
+  return mo.overflow ? kNone : mo.total;
+}
+
+template <bool NT, int U>
+__device__ __noinline__ void wave_path_emit(const MatchArgs& a, uint32_t p, const Scratch& so, uint64_t ob,
+                                            uint32_t want) {
+  const Group<64> g64;
+  const uint32_t lane = __lane_id();
+  const Matched mo = walk_publish<64>(a, a.pubs[p], so, g64);
+  if (mo.overflow) return;   // latched by the count
+  if (mo.total != want) { if (lane == 0) atomicOr(&a.status[1], kErrMismatch); return; }
+  uint32_t kk = 0;
+  for (uint32_t r0 = lane; r0 < mo.total; r0 += 64 * U) {
+    uint4 v[U];
+    bool w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t r = r0 + 64 * u;
+      w[u] = r < mo.total;
+      if (w[u]) {
+        if (r < mo.ksum) {
+          while (kk + 1 < mo.nk && so.keys[kk + 1].y <= r) kk++;
+          const uint2 kd = so.keys[kk];
+          v[u] = *reinterpret_cast<const uint4*>(a.records + kd.x + (r - kd.y));
+        } else {
+          v[u] = emission(a, so.keys, 1, mo.ksum, mo.rmask, r);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (w[u]) store_rec<NT>(a.out, ob + r0 + 64 * u, v[u]);
+  }
+}
+
+template <int G, bool NT, int U>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_match_fused(MatchArgs a) {
+  constexpr int GPW = 64 / G;                 // publishes per wave
+  constexpr uint32_t CH = kWaves * GPW;       // publishes per chunk
+  constexpr uint32_t SC = FastCaps<G>::S, CC = FastCaps<G>::C, KC = FastCaps<G>::K;
+  __shared__ uint2 st[CH][SC];
+  __shared__ uint32_t cd[CH][CC];
+  __shared__ uint2 ky[CH][KC];
+  __shared__ FusedMeta fm[CH];
+  __shared__ uint32_t tot[CH], ovl[CH];
+  __shared__ uint64_t wtot[kWaves];
+  __shared__ uint32_t s_chunk, s_novf;
+  __shared__ uint64_t s_base;
+  const Group<G> g;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = __lane_id();
+  const uint32_t slot = wv * GPW + g.gidx;
+  const Scratch s{st[slot], cd[slot], ky[slot], SC, CC, KC};
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
+  const Scratch so{a.o_stack + gw * a.o_cap, a.o_cand + gw * a.o_cap, a.o_keys + gw * a.o_cap,
+                   a.o_cap, a.o_cap, a.o_cap};
+  for (;;) {
+    if (threadIdx.x == 0) { s_chunk = atomicAdd(&a.status[3], 1u); s_novf = 0; }
+    __syncthreads();
+    const uint32_t chunk = s_chunk;
+    if (chunk >= a.nchunks) break;
+    const uint32_t base = chunk * CH;
+
+    // 1. fast walks (trie_match/4 + match/4 + lookup_subs/1 of every publish)
+    const uint32_t p = base + slot;
+    const bool have = p < a.npub;
+    Matched m{0, 0, 0, 0, false};
+    if (have) m = walk_publish<G>(a, a.pubs[p], s, g);
+    if (g.lane == 0) {
+      const bool ok = have && !m.overflow;
+      tot[slot] = ok ? m.total : 0;
+      fm[slot] = FusedMeta{0, 0, 0, ok ? 1u : 0u, m.nk == 0 ? 1u : m.nk, m.ksum, (uint32_t)m.rmask,
+                           (uint32_t)(m.rmask >> 32)};
+      if (have && m.overflow) ovl[atomicAdd(&s_novf, 1u)] = slot;
+    }
+    __syncthreads();
+
+    // 2. publishes that overflowed the fast lists: counted by whole waves
+    const uint32_t novf = s_novf;
+    for (uint32_t k = wv; k < novf; k += kWaves) {
+      const uint32_t j = ovl[k];
+      const uint32_t t = wave_path_count(a, base + j, so);
+      if (lane == 0) {
+        if (t == kNone) atomicOr(&a.status[1], kErrFrontier);
+        else tot[j] = t;
+      }
+    }
+    if (threadIdx.x == 0 && novf) atomicAdd(&a.status[0], novf);
+    __syncthreads();
+
+    // 3. offsets inside the chunk: per-wave scans of the counts and of the
+    //    fast publishes' counts, then the waves' totals
+    const uint32_t me = wv * GPW + lane;
+    const uint32_t cnt = lane < (uint32_t)GPW ? tot[me] : 0u;
+    const uint32_t cnt_ok = lane < (uint32_t)GPW && fm[me].ok ? cnt : 0u;
+    const uint32_t incl = wave_incl_scan32(cnt);
+    const uint32_t incl_ok = wave_incl_scan32(cnt_ok);
+    const uint32_t wsum = __shfl(incl, 63, 64), wsum_ok = __shfl(incl_ok, 63, 64);
+    if (lane < (uint32_t)GPW) { fm[me].rel = incl - cnt; fm[me].span = cnt; fm[me].crel = incl_ok - cnt_ok; }
+    if (lane == 0) wtot[wv] = wsum;
+    __syncthreads();
+    uint64_t wrel = 0, agg = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < (uint32_t)kWaves; w++) { if (w < wv) wrel += wtot[w]; agg += wtot[w]; }
+
+    // 4. chunk base: decoupled look-back
+    if (wv == 0) {
+      const uint64_t b = lookback(a, chunk, agg);
+      if (lane == 0) s_base = b;
+    }
+    __syncthreads();
+    const uint64_t cbase = s_base;
+    const bool fits = cbase + agg <= a.out_cap;
+    if (threadIdx.x == 0 && !fits) atomicOr(&a.status[1], kErrOverflow);
+
+    // 5. offsets (exclusive prefix; the batch's last publish also writes the total)
+    if (lane < (uint32_t)GPW) {
+      const uint32_t pp = base + me;
+      if (pp < a.npub) a.offsets[pp] = cbase + wrel + (incl - cnt);
+      if (pp + 1 == a.npub) a.offsets[a.npub] = cbase + agg;
+    }
+
+    // 6. fast publishes: one contiguous copy per wave, U records per lane in flight
+    if (fits) {
+      const uint64_t wbase = cbase + wrel;
+      const FusedMeta* wm = fm + wv * GPW;
+      uint32_t j = 0;
+      for (uint32_t r0 = lane; r0 < wsum_ok; r0 += 64 * U) {
+        uint4 v[U];
+        uint64_t dst[U];
+        bool w[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t r = r0 + 64 * u;
+          w[u] = r < wsum_ok;
+          if (w[u]) {
+            while (j + 1 < (uint32_t)GPW && wm[j + 1].crel <= r) j++;
+            const FusedMeta mm = wm[j];
+            const uint64_t rm = ((uint64_t)mm.rm_hi << 32) | mm.rm_lo;
+            v[u] = emission(a, ky[wv * GPW + j], mm.nk, mm.ksum, rm, r - mm.crel);
+            dst[u] = wbase + mm.rel + (r - mm.crel);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if (w[u]) store_rec<NT>(a.out, dst[u], v[u]);
+      }
+    }
+
+    // 7. wave-path publishes: re-walk, then a 64-lane copy in key order
+    for (uint32_t k = wv; fits && k < novf; k += kWaves) {
+      const uint32_t j = ovl[k];
+      uint64_t ob = cbase + fm[j].rel;   // + the totals of the waves before publish j's
+      for (uint32_t w = 0; w < j / GPW; w++) ob += wtot[w];
+      wave_path_emit<NT, U>(a, base + j, so, ob, tot[j]);
+    }
+    __syncthreads();   // LDS is reused by the next chunk
+  }
+}
+
+uint32_t fused_chunk(uint32_t fast_g) { return kWaves * (64 / fast_g); }
+
+template <int GG, int U>
+static hipError_t launch_fused_g(const MatchArgs& a, uint32_t grid, bool nt, hipStream_t st) {
+  if (nt) k_match_fused<GG, true, U><<<grid, 256, 0, st>>>(a);
+  else k_match_fused<GG, false, U><<<grid, 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fused(const MatchArgs& a, uint32_t grid, uint32_t unroll, hipStream_t st) {
+  const bool nt = (a.opts & kOptNtStores) != 0;
+  if (grid < 1) grid = 1;
+  if (a.fast_g == 2) return unroll == 8 ? launch_fused_g<2, 8>(a, grid, nt, st) : launch_fused_g<2, 4>(a, grid, nt, st);
+  if (a.fast_g == 8) return unroll == 8 ? launch_fused_g<8, 8>(a, grid, nt, st) : launch_fused_g<8, 4>(a, grid, nt, st);
+  return unroll == 8 ? launch_fused_g<4, 8>(a, grid, nt, st) : launch_fused_g<4, 4>(a, grid, nt, st);
+}
+
+int fused_blocks_per_cu(uint32_t fast_g, uint32_t unroll) {
+  int n = 0;
+  const void* f;
+  if (fast_g == 2) f = unroll == 8 ? (const void*)k_match_fused<2, true, 8> : (const void*)k_match_fused<2, true, 4>;
+  else if (fast_g == 8) f = unroll == 8 ? (const void*)k_match_fused<8, true, 8> : (const void*)k_match_fused<8, true, 4>;
+  else f = unroll == 8 ? (const void*)k_match_fused<4, true, 8> : (const void*)k_match_fused<4, true, 4>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) return 0;
+  return n;
+}
+
 // ------------------------------------------------------------------ scan
-// In-place exclusive scan of n u64 values (n-1 counts followed by a 0 slot
-// gives offsets[n-1] = total).  Block = 256 threads x 8 items.
+// Exclusive scan of the per-publish counts in offsets[0, npub) into
+// offsets[0, npub] (offsets[npub] = total) in ONE launch: tiles of 2,048
+// taken by ticket, chained by the same decoupled look-back as the fused
+// kernel.  Slot npub is never read (no memset before the COUNT pass).
 constexpr uint32_t kScanItems = 8, kScanBlock = 256, kScanTile = kScanItems * kScanBlock;
 
-__global__ __launch_bounds__(256) void k_scan_tiles(uint64_t* v, uint64_t n, uint64_t* tile_sums) {
+__global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
   __shared__ uint64_t part[kScanBlock];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
-  uint64_t x[kScanItems];
-  uint64_t acc = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < kScanItems; i++) { x[i] = base + i < n ? v[base + i] : 0; acc += x[i]; }
-  part[threadIdx.x] = acc;
-  __syncthreads();
-  for (uint32_t o = 1; o < kScanBlock; o <<= 1) {
-    const uint64_t t = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+  __shared__ uint32_t s_tile;
+  __shared__ uint64_t s_base;
+  const uint64_t n = (uint64_t)a.npub + 1;
+  const uint32_t ntiles = (uint32_t)((n + kScanTile - 1) / kScanTile);
+  uint64_t* v = a.offsets;
+  for (;;) {
+    if (threadIdx.x == 0) s_tile = atomicAdd(&a.status[3], 1u);
     __syncthreads();
-    part[threadIdx.x] += t;
+    const uint32_t tile = s_tile;
+    if (tile >= ntiles) break;
+    const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint64_t x[kScanItems];
+    uint64_t acc = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kScanItems; i++) { x[i] = base + i < a.npub ? v[base + i] : 0; acc += x[i]; }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t o = 1; o < kScanBlock; o <<= 1) {
+      const uint64_t t = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+      __syncthreads();
+      part[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (threadIdx.x < 64) {
+      const uint64_t b = lookback(a, tile, part[kScanBlock - 1]);
+      if (threadIdx.x == 0) s_base = b;
+    }
+    __syncthreads();
+    uint64_t run = s_base + part[threadIdx.x] - acc;
+#pragma unroll
+    for (uint32_t i = 0; i < kScanItems; i++) {
+      if (base + i < n) v[base + i] = run;
+      run += x[i];
+    }
     __syncthreads();
   }
-  uint64_t run = part[threadIdx.x] - acc;
-#pragma unroll
-  for (uint32_t i = 0; i < kScanItems; i++) {
-    if (base + i < n) v[base + i] = run;
-    run += x[i];
-  }
-  if (threadIdx.x == kScanBlock - 1 && tile_sums) tile_sums[blockIdx.x] = part[kScanBlock - 1];
 }
 
-__global__ __launch_bounds__(256) void k_scan_add(uint64_t* v, uint64_t n, const uint64_t* tile_offs) {
-  const uint64_t add = tile_offs[blockIdx.x];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-  for (uint32_t i = threadIdx.x; i < kScanTile; i += kScanBlock)
-    if (base + i < n) v[base + i] += add;
-}
+uint32_t scan_tiles(uint64_t npub) { return (uint32_t)((npub + 1 + kScanTile - 1) / kScanTile); }
 
 // ---------------------------------------------------------------- patches
 __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uint32_t* patches, uint64_t n) {
@@ -539,30 +853,17 @@ __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uin
 // ---------------------------------------------------------------- launch
 static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-hipError_t launch_scan(uint64_t* v, uint64_t n, uint64_t* tmp, hipStream_t st) {
-  // tmp must hold scan_tmp_elems(n) u64
-  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
-  if (tiles <= 1) {
-    k_scan_tiles<<<1, kScanBlock, 0, st>>>(v, n, nullptr);
-    return hipGetLastError();
-  }
-  k_scan_tiles<<<(uint32_t)tiles, kScanBlock, 0, st>>>(v, n, tmp);
-  const hipError_t e = launch_scan(tmp, tiles, tmp + tiles, st);
-  if (e != hipSuccess) return e;
-  k_scan_add<<<(uint32_t)tiles, kScanBlock, 0, st>>>(v, n, tmp);
+hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
+  uint32_t g = scan_tiles(a.npub);
+  if (g > 2048) g = 2048;
+  k_scan_offsets<<<g, kScanBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 
-uint64_t scan_tmp_elems(uint64_t n) {
-  uint64_t tot = 0;
-  for (uint64_t t = (n + kScanTile - 1) / kScanTile; t > 1; t = (t + kScanTile - 1) / kScanTile) tot += t;
-  return tot + 1;
-}
-
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) {
+  const bool nt = (a.opts & kOptNtStores) != 0;
   if (tier == 0) {
     const uint32_t G = (a.fast_g == 2 || a.fast_g == 8) ? a.fast_g : 4;
-    const bool nt = (a.opts & kOptNtStores) != 0;
     uint32_t g = div_up(a.npub, kWaves * (64 / G));
     const uint32_t cap = 256u * 8u;   // grid-stride beyond 8 blocks per CU
     if (g > cap) g = cap;
@@ -575,16 +876,21 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) 
     else if (G == 4) { VMQG_FAST(4) }
     else { VMQG_FAST(8) }
 #undef VMQG_FAST
-  } else if (tier == 1) {
-    const uint32_t g = 256;   // reads its list length on the device; exits at once when empty
-    if (mode == 0) k_match_deferred<0, 1><<<g, 256, 0, st>>>(a);
-    else k_match_deferred<1, 1><<<g, 256, 0, st>>>(a);
   } else {
-    const uint32_t g = a.g_waves / kWaves;
-    if (mode == 0) k_match_deferred<0, 2><<<g, 256, 0, st>>>(a);
-    else k_match_deferred<1, 2><<<g, 256, 0, st>>>(a);
+    // reads its list length on the device (exits at once when empty); one
+    // wave per deferred publish, as many waves as have global scratch
+    const uint32_t g = a.o_waves / kWaves;
+    if (mode == 0) k_match_wave<0, false><<<g, 256, 0, st>>>(a);
+    else if (nt) k_match_wave<1, true><<<g, 256, 0, st>>>(a);
+    else k_match_wave<1, false><<<g, 256, 0, st>>>(a);
   }
   return hipGetLastError();
+}
+
+int wave_blocks_per_cu() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)k_match_wave<1, true>, 256, 0) != hipSuccess) return 0;
+  return n;
 }
 
 hipError_t launch_patches(uint8_t* arena, const void* d_patches, uint64_t n, hipStream_t st) {
