@@ -207,15 +207,17 @@ def main():
         log("cpu baseline: %.0f publishes/s" % cpu["value"])
 
     if rank == 0:
-        # algorithmic bytes (SURVEY §8d B_p) split by the kernel that does the
-        # work: the lookups 8(L+1)+16 S_p are the walk (COUNT), the records
-        # 32 R_p are copied by EMIT; the pipeline figure uses the whole B_p.
+        # roofline of the dominant kernel (EMIT): its compulsory HBM bytes per
+        # launch (records written + key cache / offsets read + each distinct
+        # record read once, W.algorithmic_bytes_c "emit_compulsory") over its
+        # average launch time from HIP events on the launch stream.  SURVEY
+        # §8(d)'s B_p (16-B lookups + 32 B per emission) is reported as
+        # `survey_model`: it charges an HBM read for every emission of the
+        # L2-resident fan-out list, so it can exceed what the chip moves.
         alg = {"count": W.algorithmic_bytes_c(w, part="lookup"), "emit": W.algorithmic_bytes_c(w, part="emit"),
-               "all": W.algorithmic_bytes_c(w)}
-        dom = "emit" if emit_ns >= count_ns else "count"
-        kern = {"emit": "k_match_fast<1", "count": "k_match_fast<0"}[dom]
-        dom_ns = max(emit_ns, count_ns)
-        achieved = alg[dom] / dom_ns if dom_ns > 0 else None   # bytes/ns == GB/s
+               "all": W.algorithmic_bytes_c(w), "emit_compulsory": W.algorithmic_bytes_c(w, part="emit_compulsory")}
+        kern = "k_match_fast<1"
+        achieved = alg["emit_compulsory"] / emit_ns if emit_ns > 0 else None   # bytes/ns == GB/s
         traffic = load_pmc_traffic(kern)
         pipe_ns = t_max * 1e9 / args.steps
         res = {
@@ -242,11 +244,17 @@ def main():
             "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3, "launches": nlaunch},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
-                         "kernel": kern, "algorithmic_bytes_per_launch": alg[dom]},
-            "pipeline_roofline": {"achieved": alg["all"] / pipe_ns, "frac": alg["all"] / pipe_ns / PEAK_HBM_GBS,
-                                  "algorithmic_bytes_per_step": alg["all"],
-                                  "emit_kernel_achieved": alg["emit"] / emit_ns if emit_ns else None,
-                                  "count_kernel_achieved": alg["count"] / count_ns if count_ns else None},
+                         "kernel": "k_match_fast<1,2,true> (EMIT)",
+                         "algorithmic_bytes_per_launch": alg["emit_compulsory"],
+                         "bytes_model": "16 B written per emission + 40 B read per publish + 16 B per distinct "
+                                        "record (workloads.algorithmic_bytes_c emit_compulsory)"},
+            "count_kernel": {"kernel": "k_match_fast<0,2,false> (COUNT)", "us": count_ns / 1e3 if count_ns else None,
+                             "lookup_bytes_model": alg["count"],
+                             "achieved": alg["count"] / count_ns if count_ns else None},
+            "survey_model": {"bytes_per_step": alg["all"], "achieved_per_step": alg["all"] / pipe_ns,
+                             "emit_achieved": alg["emit"] / emit_ns if emit_ns else None,
+                             "note": "SURVEY 8(d) B_p = 8(L+1) + 16 S_p + 32 R_p; charges an HBM read per emission "
+                                     "of the cache-resident fan-out list, so it can exceed the HBM peak"},
             "cpu_baseline": cpu,
             "load_s": load_s,
         }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 CSV output into profiles/.
 
-usage: summarize_prof.py <stats_dir> <fetch_dir> <write_dir> <out_json> [tag]
+usage: summarize_prof.py <stats_dir> <fetch_dir> <write_dir> <out_json> [tag] [l2_dir] [lds_dir]
 
 * kernel-trace stats: copied verbatim (…_kernel_stats.csv) — the average
   duration per kernel that bench.py's HIP-event timing must agree with;
@@ -9,7 +9,9 @@ usage: summarize_prof.py <stats_dir> <fetch_dir> <write_dir> <out_json> [tag]
   mean per dispatch, in bytes = KB x 1024.  gfx950 correction (MI355X_MICROARCH.md
   §HBM): FETCH_SIZE reads half of a wide coalesced read stream, so the
   corrected read bytes are 2 x FETCH_SIZE; WRITE_SIZE is exact for 16-B/lane
-  streaming stores.  Both raw and corrected numbers are kept.
+  streaming stores.  Both raw and corrected numbers are kept;
+* optional passes: L2 hit rate TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum),
+  LDS bank conflicts SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (cycles).
 """
 import csv
 import glob
@@ -57,6 +59,12 @@ def main():
                                        "total_ns": float(col(row, "totaldurationns"))}
     fetch = pmc(fdir, "FETCH_SIZE")
     write = pmc(wdir, "WRITE_SIZE")
+    l2dir = sys.argv[6] if len(sys.argv) > 6 else None
+    ldsdir = sys.argv[7] if len(sys.argv) > 7 else None
+    hit = pmc(l2dir, "TCC_HIT_sum") if l2dir else {}
+    miss = pmc(l2dir, "TCC_MISS_sum") if l2dir else {}
+    bank = pmc(ldsdir, "SQ_LDS_BANK_CONFLICT") if ldsdir else {}
+    ldsact = pmc(ldsdir, "SQ_LDS_IDX_ACTIVE") if ldsdir else {}
     kernels = {}
     for name in set(fetch) | set(write) | set(stats):
         short = name.split("(")[0].replace("void ", "").replace("vmqg::", "")
@@ -72,10 +80,16 @@ def main():
             ent["write_bytes"] = wk * 1024
         if fk is not None and wk is not None:
             ent["hbm_bytes_per_launch"] = 2 * fk * 1024 + wk * 1024
+        if name in hit and name in miss and hit[name] + miss[name] > 0:
+            ent["l2_hit_rate"] = hit[name] / (hit[name] + miss[name])
+        if name in bank and ldsact.get(name):
+            ent["lds_bank_conflict_frac"] = bank[name] / ldsact[name]
+            ent["lds_bank_conflict_cycles"] = bank[name]
         kernels[short] = ent
     json.dump({"tag": tag, "kernels": kernels,
-               "notes": "rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE and --pmc WRITE_SIZE "
-                        "runs of the same bench command; read bytes = 2 x FETCH_SIZE (gfx950 correction)"},
+               "notes": "rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE, --pmc WRITE_SIZE, "
+                        "--pmc TCC_HIT_sum TCC_MISS_sum and --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE runs "
+                        "of the same bench command; read bytes = 2 x FETCH_SIZE (gfx950 correction)"},
               open(out, "w"), indent=1, sort_keys=True)
     print(json.dumps(kernels, indent=1, sort_keys=True))
 

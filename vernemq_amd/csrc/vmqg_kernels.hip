@@ -553,10 +553,13 @@ __device__ __forceinline__ uint64_t lb_load(uint64_t* p) {
 
 // Exclusive output base of `chunk`, computed by one whole wave.  Posts the
 // chunk's aggregate first so successors can pass over it, then looks back
-// 64 predecessors per round (lane i reads chunk - 1 - i - 64 r): the nearest
-// predecessor with an inclusive prefix ends the walk, the aggregates of the
-// ones in between are summed.  A round retries while any granule it needs
-// is not yet posted (tag of an earlier call).
+// over 64 x kLbDepth predecessors per round (lane i loads chunk - 1 - i - 64 k
+// for k < kLbDepth, all loads in flight together): the nearest predecessor
+// with an inclusive prefix ends the walk, the aggregates of the ones in
+// between are summed.  A round is retried while a granule it needs is not
+// yet posted (tag of an earlier call).
+constexpr int kLbDepth = 4;
+
 __device__ uint64_t lookback(const MatchArgs& a, uint32_t chunk, uint64_t agg) {
   const uint32_t lane = __lane_id();
   uint64_t* lb = a.lookback;
@@ -568,28 +571,41 @@ __device__ uint64_t lookback(const MatchArgs& a, uint32_t chunk, uint64_t agg) {
   uint64_t excl = 0;
   int64_t top = (int64_t)chunk - 1;
   for (uint32_t spins = 0;;) {
-    const int64_t j = top - (int64_t)lane;
-    uint64_t x = 0;
-    bool ready = false;
-    if (j >= 0) { x = lb_load(lb + j); ready = (uint32_t)(x >> 44) == a.lb_tag; }
-    const uint64_t incl = __ballot(ready && ((x >> 42) & 3) == kLbIncl);
-    const uint64_t waiting = __ballot(j >= 0 && !ready);
-    const uint32_t stop = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;   // nearest inclusive predecessor
-    const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);       // lanes 0..stop
-    if (waiting & need) {
+    uint64_t x[kLbDepth];
+#pragma unroll
+    for (int k = 0; k < kLbDepth; k++) {
+      const int64_t j = top - (int64_t)lane - 64 * k;
+      x[k] = j >= 0 ? lb_load(lb + j) : 0;
+    }
+    uint64_t sum = 0;
+    bool done = false, retry = false;
+#pragma unroll
+    for (int k = 0; k < kLbDepth; k++) {
+      if (done || retry) continue;
+      const int64_t j = top - (int64_t)lane - 64 * k;
+      const bool ready = j >= 0 && (uint32_t)(x[k] >> 44) == a.lb_tag;
+      const uint64_t incl = __ballot(ready && ((x[k] >> 42) & 3) == kLbIncl);
+      const uint64_t waiting = __ballot(j >= 0 && !ready);
+      const uint32_t stop = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;   // nearest inclusive predecessor
+      const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);       // lanes 0..stop
+      if (waiting & need) { retry = true; continue; }
+      uint64_t v = (lane <= stop && j >= 0) ? (x[k] & kLbValueMask) : 0;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
+        v += ((uint64_t)hi << 32) | lo;
+      }
+      sum += v;
+      if (stop < 64 || top - 64 * k - 63 <= 0) done = true;
+    }
+    if (retry) {
       if (++spins > kSpinLimit) { if (lane == 0) atomicOr(&a.status[1], kErrLookback); break; }
       __builtin_amdgcn_s_sleep(1);
-      continue;
+      continue;   // the whole round again (its granules may have moved on)
     }
-    uint64_t v = (lane <= stop && j >= 0) ? (x & kLbValueMask) : 0;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
-      v += ((uint64_t)hi << 32) | lo;
-    }
-    excl += v;
-    if (stop < 64) break;
-    top -= 64;
+    excl += sum;
+    if (done) break;
+    top -= 64 * kLbDepth;
   }
   if (lane == 0) lb_store(lb + chunk, lb_pack(a.lb_tag, kLbIncl, excl + agg));
   return excl;
@@ -794,10 +810,10 @@ int fused_blocks_per_cu(uint32_t fast_g, uint32_t unroll) {
 
 // ------------------------------------------------------------------ scan
 // Exclusive scan of the per-publish counts in offsets[0, npub) into
-// offsets[0, npub] (offsets[npub] = total) in ONE launch: tiles of 2,048
+// offsets[0, npub] (offsets[npub] = total) in ONE launch: tiles of 4,096
 // taken by ticket, chained by the same decoupled look-back as the fused
 // kernel.  Slot npub is never read (no memset before the COUNT pass).
-constexpr uint32_t kScanItems = 8, kScanBlock = 256, kScanTile = kScanItems * kScanBlock;
+constexpr uint32_t kScanItems = 16, kScanBlock = 256, kScanTile = kScanItems * kScanBlock;
 
 __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
   __shared__ uint64_t part[kScanBlock];

@@ -551,7 +551,13 @@ def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None, part: s
       hit  (d < n_dev): S_p = 26 (20 trie_match + 2 match/4 + 4 fold), R_p = 65
       miss (d >= n_dev): S_p = 17 (13 + 1 + 3),                       R_p = 64
     part: "all" = B_p; "lookup" = 8(L_p+1) + 16 S_p (the walk, COUNT kernel);
-    "emit" = 32 R_p (record read + write, EMIT kernel).
+    "emit" = 32 R_p (record read + write, EMIT kernel);
+    "emit_compulsory" = the bytes EMIT cannot avoid moving through HBM:
+    16 R_p written + 40 B per publish read (32-B key cache, its offset) +
+    16 B per DISTINCT record of the batch (the 64 shared wildcard records
+    once, each hit publish's own device record).  32 R_p charges a 16-B HBM
+    read for every emission although 64 of a publish's 65 records are the
+    same L2-resident list, so it can exceed what any kernel moves.
     """
     hi = w.n_pubs if hi is None else hi
     d = w.pw[4 * lo + 1:4 * hi:4] - 18
@@ -561,4 +567,8 @@ def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None, part: s
     emit_hit, emit_miss = 32 * (w.notes["n_wild"] + 1), 32 * w.notes["n_wild"]
     look = n_hit * look_hit + n_miss * look_miss
     emit = n_hit * emit_hit + n_miss * emit_miss
+    if part == "emit_compulsory":
+        distinct = int(np.unique(d[d < w.notes["n_dev"]]).size) + w.notes["n_wild"]
+        writes = 16 * (n_hit * (w.notes["n_wild"] + 1) + n_miss * w.notes["n_wild"])
+        return writes + 40 * (hi - lo) + 16 * distinct
     return {"all": look + emit, "lookup": look, "emit": emit}[part]
