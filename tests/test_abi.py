@@ -1,4 +1,4 @@
-"""CPU checks of the C ABI boundary (include/vmqg.h): the library loads,
+"""CPU checks of the C ABI boundary (include/vmqg.h, include/vmqr.h): the library loads,
 exports every declared entry point, its structs have the header's layout,
 and a host-only context fails loudly on match calls (no CPU fallback)."""
 import ctypes
@@ -13,18 +13,21 @@ from vernemq_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "vmqg.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "vmqr.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*[\w\s\*]+?\b(vmqg_\w+)\s*\(", src, flags=re.M)))
+    out = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        out |= set(re.findall(r"^\s*[\w\s\*]+?\b(vmq[gr]_\w+)\s*\(", src, flags=re.M))
+    return sorted(out)
 
 
 def test_every_declared_symbol_is_exported():
     L = _lib.lib()
     decl = declared_functions()
-    assert len(decl) >= 18
+    assert len(decl) >= 30
     missing = [f for f in decl if not hasattr(L, f)]
     assert not missing, missing
     bound = {name for name, _, _ in _lib.SIGNATURES}
@@ -47,6 +50,30 @@ def test_struct_layouts_match_header(tmp_path):
     assert got == want
     from vernemq_amd.reg_view import EMIT_DTYPE, OP_DTYPE, PUB_DTYPE
     assert (OP_DTYPE.itemsize, PUB_DTYPE.itemsize, EMIT_DTYPE.itemsize) == (got[1], got[2], got[3])
+
+
+def test_retain_struct_layouts_match_header(tmp_path):
+    prog = tmp_path / "szr.c"
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "vmqr.h"\n'
+                    'int main(void){printf("%zu %zu %zu %zu\\n", sizeof(vmqr_config), sizeof(vmqr_op),'
+                    ' sizeof(vmqr_stats_t), offsetof(vmqr_op, msg));return 0;}\n')
+    exe = tmp_path / "szr"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(prog),
+                    "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [ctypes.sizeof(_lib.RConfig), ctypes.sizeof(_lib.ROp), ctypes.sizeof(_lib.RStats),
+                   _lib.ROp.msg.offset]
+    from vernemq_amd.retain import ROP_DTYPE
+    assert ROP_DTYPE.itemsize == got[1]
+
+
+def test_host_only_retain_context_refuses_to_match():
+    from vernemq_amd.retain import RetainGpuSrv
+    r = RetainGpuSrv(device=-1)
+    r.insert("", (b"a",), "m")
+    with pytest.raises(_lib.VmqgError) as ei:
+        r.match_fold_batch([("", (b"#",))])
+    assert ei.value.rc == _lib.E_DEVICE
 
 
 def test_host_only_context_refuses_to_match():

@@ -1,0 +1,216 @@
+"""Retained-message store (vmq_retain_srv, include/vmqr.h): the CPU oracle
+against the reference's golden vectors, the host engine's table against the
+oracle (no GPU), and — marked gpu — the HIP match_fold path against the
+oracle, bit-exact as sets of (topic, payload) per filter."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import retain_oracle as RO
+from tests import scenarios as S
+
+RETAIN = S.load("retain.json")["scenarios"]
+PINNED = [s for s in RETAIN if s["pinned"]]
+
+
+def _t(s):
+    return S.topic(s)
+
+
+class OracleDriver:
+    """The oracle with payload ids <-> payload strings."""
+
+    def __init__(self):
+        self.o = RO.RetainOracle()
+        self.payloads = []
+
+    def insert(self, mp, topic, payload):
+        self.payloads.append((topic, payload))
+        self.o.apply([("insert", mp, topic, len(self.payloads) - 1)])
+
+    def delete(self, mp, topic):
+        self.o.apply([("delete", mp, topic)])
+
+    def fold_batch(self, filters):
+        return [sorted(self.payloads[i] for i in ids) for ids in self.o.match_batch(filters)]
+
+
+class ProductDriver:
+    def __init__(self, device=0):
+        from vernemq_amd.retain import RetainGpuSrv
+        self.r = RetainGpuSrv(device=device)
+
+    def insert(self, mp, topic, payload):
+        self.r.insert(mp, topic, payload)
+
+    def delete(self, mp, topic):
+        self.r.delete(mp, topic)
+
+    def fold_batch(self, filters):
+        return [sorted(x) for x in self.r.match_fold_batch(filters)]
+
+
+def run_retain_scenario(scen, drv):
+    for i, st in enumerate(scen["steps"]):
+        if "insert" in st:
+            mp, t, p = st["insert"]
+            drv.insert(mp, _t(t), p)
+        elif "delete" in st:
+            mp, t = st["delete"]
+            drv.delete(mp, _t(t))
+        else:
+            mp, f = st["fold"]
+            got = drv.fold_batch([(mp, _t(f))])[0]
+            want = sorted((_t(t), p) for t, p in st["expect"])
+            assert got == want, "%s step %d (%s): got %r want %r" % (scen["name"], i, f, got, want)
+
+
+# ------------------------------------------------------------------ CPU
+@pytest.mark.parametrize("scen", RETAIN, ids=[s["name"] for s in RETAIN])
+def test_oracle_retain_golden(scen):
+    run_retain_scenario(scen, OracleDriver())
+
+
+def test_pinned_fixtures_cover_the_reference_tests():
+    assert len(PINNED) >= 28 and {s["name"] for s in PINNED} >= {
+        "retain_qos0_test", "retain_wildcard_test", "retain_qos0_clear_test", "retain_qos1_qos0_test"}
+
+
+def test_oracle_topic_match_and_has_wildcard():
+    # vmq_topic:match/2 clauses (vmq_topic.erl:53-65) and has_wildcard/1 (vmq_retain_srv.erl:239-242)
+    assert RO.topic_match(_t("a/b"), _t("a/#")) and RO.topic_match(_t("a"), _t("a/#"))
+    assert not RO.topic_match(_t("a"), _t("a/+")) and RO.topic_match(_t("a/"), _t("a/+"))
+    assert RO.topic_match(_t("$SYS/x"), _t("#")) and not RO.topic_match(_t("a/x"), _t("a/#/x"))
+    assert RO.has_wildcard(_t("a/+/b")) and RO.has_wildcard(_t("#")) and not RO.has_wildcard(_t("#/a"))
+    assert not RO.has_wildcard(_t("a/b"))
+
+
+def random_store(seed, n_topics=400, n_ops=900, n_filters=300, mps=("", "m1", "m2")):
+    """Random retained topics (4 words/level, 1-4 levels, empty words and
+    '$' topics included), inserts / replaces / deletes, and filters of every
+    shape (exact, '+', '#', '#' not last, unknown words)."""
+    rnd = random.Random(seed)
+    vocab = [b"a", b"b", b"c", b"", b"$SYS"]
+    topics = list({tuple(rnd.choice(vocab[:4] if k else vocab) for k in range(rnd.randint(1, 4)))
+                   for _ in range(n_topics)})
+    ops = []
+    for i in range(n_ops):
+        mp, t = rnd.choice(mps), rnd.choice(topics)
+        if rnd.random() < 0.75:
+            ops.append(("insert", mp, t, "p%d" % i))
+        else:
+            ops.append(("delete", mp, t))
+    filters = []
+    for _ in range(n_filters):
+        L = rnd.randint(1, 5)
+        f = [rnd.choice([b"a", b"b", b"c", b"", b"+", b"$SYS", b"zz"]) for _ in range(L)]
+        r = rnd.random()
+        if r < 0.3:
+            f[-1] = b"#"
+        elif r < 0.35:
+            f.insert(0, b"#")
+        filters.append((rnd.choice(mps + ("nope",)), tuple(f)))
+    return ops, filters
+
+
+def test_host_engine_table_matches_oracle():
+    """The product's host tables (device=-1, vmqr_dump) hold exactly the
+    oracle's ?RETAIN_CACHE after a random op stream."""
+    from vernemq_amd.retain import RetainGpuSrv
+    ops, _ = random_store(7)
+    r = RetainGpuSrv(device=-1)
+    o = OracleDriver()
+    for k in range(0, len(ops), 37):
+        batch = ops[k:k + 37]
+        r.apply(batch)
+        for op in batch:
+            if op[0] == "insert":
+                o.insert(op[1], op[2], op[3])
+            else:
+                o.delete(op[1], op[2])
+    live = {}
+    for op in ops:
+        if op[0] == "insert":
+            live[(op[1], op[2])] = op[3]
+        else:
+            live.pop((op[1], op[2]), None)
+    assert r.stats()[0] == len(live) == o.o.size()
+    dump = r.dump().splitlines()
+    assert len(dump) == len(live)
+    got = {}
+    for line in dump:
+        key, msg = line.rsplit(" -> msg#", 1)
+        mp_id, words = key.split(" ", 1)
+        mp = r.mountpoints.terms[int(mp_id[3:])]
+        t = tuple(w.encode() for w in words[1:-1].split(","))   # topics have >= 1 word: "[]" is [<<>>]
+        got[(mp, t)] = r._msgs[int(msg)][1]
+    assert got == live
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("scen", RETAIN, ids=[s["name"] for s in RETAIN])
+def test_retain_golden_on_gpu(scen):
+    run_retain_scenario(scen, ProductDriver())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_retain_random_parity(seed):
+    ops, filters = random_store(seed)
+    prod, orc = ProductDriver(), OracleDriver()
+    for k in range(0, len(ops), 150):
+        batch = ops[k:k + 150]
+        prod.r.apply(batch)
+        for op in batch:
+            if op[0] == "insert":
+                orc.insert(op[1], op[2], op[3])
+            else:
+                orc.delete(op[1], op[2])
+        got, want = prod.fold_batch(filters), orc.fold_batch(filters)
+        bad = [i for i in range(len(filters)) if got[i] != want[i]]
+        assert not bad, (seed, k, filters[bad[0]], got[bad[0]][:5], want[bad[0]][:5])
+
+
+@pytest.mark.gpu
+def test_retain_large_lists_span_many_chunks():
+    """One MP list of 20,050 rows (20 chunks of 1,024; the 20,000 site
+    inserts overwrite 50 keys) and a partition of 20,000: '#', '+/...' and
+    literal-first filters spread over the chip; sets equal the oracle's."""
+    prod, orc = ProductDriver(), OracleDriver()
+    ops = []
+    for i in range(20_000):
+        ops.append(("insert", "", (b"dev", b"%d" % i, b"status"), "s%d" % i))
+        ops.append(("insert", "", (b"site%d" % (i % 50), b"temp"), "t%d" % i))
+    prod.r.apply(ops)
+    for op in ops:
+        orc.insert(op[1], op[2], op[3])
+    filters = [("", (b"#",)), ("", (b"dev", b"+", b"status")), ("", (b"+", b"temp")), ("", (b"dev", b"#")),
+               ("", (b"dev", b"77", b"status")), ("", (b"+", b"+", b"+")), ("", (b"site7", b"#"))] * 3
+    got, want = prod.fold_batch(filters), orc.fold_batch(filters)
+    assert [len(g) for g in got] == [len(w) for w in want]
+    assert got == want
+    assert len(got[0]) == 20_050
+
+
+@pytest.mark.gpu
+def test_retain_device_entry_and_empty_batch():
+    import torch
+    prod = ProductDriver()
+    prod.r.apply([("insert", "", (b"a", b"%d" % i), i) for i in range(3000)])
+    recs, offs = prod.r.match_arrays(*prod.r.prepare([]))
+    assert len(recs) == 0 and list(offs) == [0]
+    arr, words = prod.r.prepare([("", (b"a", b"+")), ("", (b"a", b"7")), ("", (b"b", b"#"))])
+    ref_ids, ref_offs = prod.r.match_arrays(arr, words, out_cap=8)   # grows internally
+    assert list(ref_offs) == [0, 3000, 3001, 3001]
+    dev = torch.device("cuda:0")
+    d_f = torch.from_numpy(arr.view(np.uint32).copy()).to(dev)
+    d_w = torch.from_numpy(words.astype(np.int32)).to(dev)
+    d_o = torch.zeros(4096, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(4, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream()
+    prod.r.match_device(d_f.data_ptr(), 3, d_w.data_ptr(), d_o.data_ptr(), 4096, d_offs.data_ptr(), s.cuda_stream)
+    assert prod.r.match_status(s.cuda_stream) == 0
+    assert d_offs.cpu().tolist() == [0, 3000, 3001, 3001]
+    assert sorted(d_o.cpu().numpy()[:3001].tolist()) == sorted(ref_ids.tolist())

@@ -1,4 +1,4 @@
-"""ctypes binding of libvmqgpu (include/vmqg.h) and its in-tree build.
+"""ctypes binding of libvmqgpu (include/vmqg.h, include/vmqr.h) and its in-tree build.
 
 The library is the product: there is no Python or CPU fallback for matching.
 If ``libvmqgpu.so`` is missing, :func:`lib` raises ``ImportError`` (call
@@ -14,10 +14,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "libvmqgpu.so")
 HEADER = os.path.join(ROOT, "include", "vmqg.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "vmqr.h")]
 SOURCES = [os.path.join(HERE, "csrc", f) for f in
-           ("vmqg_engine.cpp", "vmqg_abi.cpp", "vmqg_kernels.hip")]
+           ("vmqg_engine.cpp", "vmqg_abi.cpp", "vmqg_kernels.hip",
+            "vmqr_engine.cpp", "vmqr_abi.cpp", "vmqr_kernels.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in
-                  ("vmqg_common.h", "vmqg_engine.h", "vmqg_kernels.h")] + [HEADER]
+                  ("vmqg_common.h", "vmqg_engine.h", "vmqg_kernels.h", "vmqg_lookback.h",
+                   "vmqr_engine.h")] + HEADERS
 
 # ---- status codes / constants (vmqg.h)
 OK, E_INVAL, E_OVERFLOW, E_NOMEM, E_DEVICE, E_FRONTIER, E_LIMIT, E_STATE = 0, -1, -2, -3, -4, -5, -6, -7
@@ -69,7 +72,22 @@ class Stats(ctypes.Structure):
                  "deferred_tier1", "deferred_tier2")]
 
 
-# (name, restype, argtypes) for every entry point declared in include/vmqg.h
+class RConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("max_mountpoints", ctypes.c_uint32), ("hint_topics", ctypes.c_uint64)]
+
+
+class ROp(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("kind", "mountpoint", "word_off", "nwords", "msg", "reserved")]
+
+
+class RStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("retained", "device_bytes", "partitions", "epoch", "rebuilds", "words")]
+
+
+ROP_INSERT, ROP_DELETE = 1, 2
+
+
+# (name, restype, argtypes) for every entry point declared in include/vmqg.h and include/vmqr.h
 _P = ctypes.c_void_p
 _U32, _U64, _SZ = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 SIGNATURES = [
@@ -94,6 +112,19 @@ SIGNATURES = [
     ("vmqg_last_patches", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64),
                                          ctypes.POINTER(ctypes.c_int)]),
     ("vmqg_apply_patches_device", ctypes.c_int, [_P, _P, _U64, _P]),
+    # retained-message matcher (include/vmqr.h)
+    ("vmqr_create", _P, [ctypes.POINTER(RConfig), ctypes.POINTER(ctypes.c_int)]),
+    ("vmqr_destroy", None, [_P]),
+    ("vmqr_intern_words", ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
+    ("vmqr_apply", ctypes.c_int, [_P, _P, _SZ, _P, _SZ]),
+    ("vmqr_match_batch", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
+    ("vmqr_match_device", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),
+    ("vmqr_match_status", ctypes.c_int, [_P, _P]),
+    ("vmqr_stats", ctypes.c_int, [_P, ctypes.POINTER(RStats)]),
+    ("vmqr_dump", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_SZ)]),
+    ("vmqr_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
+    ("vmqr_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
 ]
 
 _lib = None
