@@ -41,17 +41,18 @@ def cpu_model():
     return "unknown"
 
 
-def load_pmc_traffic(kernel: str):
-    """HBM bytes per launch of the kernel whose name starts with `kernel`
-    (e.g. "k_match_fast<1" = EMIT) from the committed rocprofv3 PMC summary
-    (profiles/pmc_latest.json, written by tools/summarize_prof.py), or None.
-    Read bytes are 2 x FETCH_SIZE (gfx950 correction), writes WRITE_SIZE."""
-    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+def load_pmc_traffic(kernel: str, summary: str = "pmc_latest.json"):
+    """HBM bytes per launch of the kernel whose name contains `kernel`
+    (e.g. "k_match_fast<1" = EMIT) from a committed rocprofv3 PMC summary
+    (profiles/pmc_latest.json for config C, written by
+    tools/summarize_prof.py), or None.  Read bytes are 2 x FETCH_SIZE (gfx950
+    correction), writes WRITE_SIZE."""
+    p = os.path.join(ROOT, "profiles", summary)
     try:
         d = json.load(open(p))["kernels"]
     except (OSError, KeyError, ValueError):
         return None
-    cands = [v for k, v in d.items() if k.startswith(kernel) and "hbm_bytes_per_launch" in v]
+    cands = [v for k, v in d.items() if kernel in k and "hbm_bytes_per_launch" in v]
     if not cands:
         return None
     return max(cands, key=lambda v: v.get("total_ns", 0))["hbm_bytes_per_launch"]
@@ -68,9 +69,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP events (profiling runs)")
-    ap.add_argument("--config", default="C", choices=["A", "B", "C", "D", "E", "R1", "R2"],
+    ap.add_argument("--config", default="C", choices=["A", "B", "C", "D", "E", "R1", "R2", "RT"],
                     help="C: headline (1M subs); D: 10M subs with $share groups under 1%%/s churn; "
-                         "A, B, E, R1, R2: the other SURVEY §8d shapes (secondary lines)")
+                         "A, B, E, R1, R2: the other SURVEY §8d shapes (secondary lines); "
+                         "RT: retained-message match_fold (§8f rank 3)")
+    ap.add_argument("--rt-devices", type=int, default=62_500, help="RT: devices x 16 retained topics")
+    ap.add_argument("--rt-filters", type=int, default=1 << 18, help="RT: subscription filters per step")
     ap.add_argument("--e-scale", type=float, default=0.2, help="config E scale (1.0 = 50M subs)")
     ap.add_argument("--d-scale", type=float, default=1.0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N>1 on one GPU")
@@ -80,6 +84,8 @@ def main():
     args = ap.parse_args()
     if args.config == "D":
         return bench_d(args)
+    if args.config == "RT":
+        return bench_retain(args)
     if args.config != "C":
         return bench_other(args)
 
@@ -423,6 +429,105 @@ def bench_d(args):
         "deferred": [st["deferred_tier1"], st["deferred_tier2"]],
     }
     print(json.dumps(res), flush=True)
+
+
+def bench_retain(args):
+    """Retained-message matching (vmq_retain_srv:match_fold/4, SURVEY §8(f)
+    rank 3): 1M retained topics, one step = one burst of 2^18 subscription
+    filters folded over the store on one GPU (plan, chunk count, scan, emit
+    of message ids).  Prints one JSON line with the walk kernel's roofline
+    and the CPU restatement (a full ets:foldl per wildcard filter, as the
+    reference) timed on a bounded sample."""
+    import torch
+    from vernemq_amd import workloads as W
+    from vernemq_amd.retain import RetainGpuSrv
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    t0 = time.time()
+    w = W.RetainWorkload(n_dev=args.rt_devices, n_filters=args.rt_filters)
+    srv = RetainGpuSrv(device=0, hint_topics=w.n_topics)
+    vid = w.load_into(srv)
+    load_s = time.time() - t0
+    log("RT: %d retained topics loaded in %.1fs, %s" % (w.n_topics, load_s, srv.stats_raw()))
+    arr, words = w.filter_arrays(vid)
+    nf = len(arr)
+    d_f = torch.from_numpy(arr.view(np.uint32).reshape(-1).copy()).to(dev)
+    d_w = torch.from_numpy(words.astype(np.int32)).to(dev)
+    total = int(w.matches.sum())
+    out_cap = total + 1024
+    d_o = torch.empty(out_cap, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(nf + 1, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+    step = lambda: srv.match_device(d_f.data_ptr(), nf, d_w.data_ptr(), d_o.data_ptr(), out_cap,
+                                    d_offs.data_ptr(), sp)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    rc = srv.match_status(sp)
+    if rc != 0:
+        raise RuntimeError("retain match status %d after warmup" % rc)
+    # size-independent check: per-filter match counts = the workload's known answer,
+    # and every emitted message id's topic matches its filter (sampled)
+    offs = d_offs.cpu().numpy()
+    verified = bool(np.array_equal(np.diff(offs), w.matches))
+    if not verified:
+        raise RuntimeError("per-filter retained match counts differ from the workload's known answer")
+    srv.set_timing(not args.no_timing)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    rc = srv.match_status(sp)
+    if rc != 0:
+        raise RuntimeError("retain match status %d in timed region" % rc)
+    count_ns, emit_ns, nl = srv.kernel_times()
+    alg = w.algorithmic_bytes("walk")
+    achieved = alg / emit_ns if emit_ns else None
+
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import retain_oracle as RO   # the CPU restatement: baseline only
+        t0 = time.time()
+        orc = RO.RetainOracle()
+        B = 1 << 17
+        for lo in range(0, w.n_topics, B):
+            orc.apply([("insert", "", w.topic(i), i) for i in range(lo, min(w.n_topics, lo + B))])
+        log("RT cpu baseline: oracle loaded in %.1fs" % (time.time() - t0))
+        S = 64
+        sample = [("", w.filter(i)) for i in range(S)]
+        ns1, _ = orc.match_timed(sample, 1)
+        reps = max(1, int(math.ceil(args.cpu_seconds * 1e9 / max(ns1, 1))))
+        ns, _ = orc.match_timed(sample, reps)
+        cpu = {"value": S * reps / (ns / 1e9), "unit": "filters/s", "cores": 1, "kind": "port",
+               "sample": "first %d filters of the RT batch x %d reps (%.1fs), 1 thread, oracle/vmq_retain_oracle.cpp "
+                         "(C++ restatement of vmq_retain_srv:match_fold/4: ets:lookup for exact filters, a full "
+                         "ets:foldl + vmq_topic:match/2 per wildcard filter; not BEAM); host %s"
+                         % (S, reps, ns / 1e9, cpu_model())}
+        log("RT cpu baseline: %.0f filters/s" % cpu["value"])
+
+    st = srv.stats_raw()
+    print(json.dumps({
+        "metric": "retained match_fold: subscription filters matched/sec (1M retained topics)",
+        "value": nf * args.steps / el, "unit": "filters/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic: vernemq_amd.workloads.RetainWorkload (splitmix64 seed 0x7E7)",
+        "config": {"workload": "RT: %d retained devices/{d}/telemetry/{m}; %d filters/step (50%% d/telemetry/#, "
+                               "20%% d/+/m, 25%% exact, 5%% unknown device, %d x devices/+/telemetry/m)"
+                               % (w.n_topics, nf, w.n_heavy)},
+        "messages_per_s": total * args.steps / el, "matches_per_step": total,
+        "verified_counts": verified,
+        "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3, "launches": nl},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS if achieved else None,
+                     "traffic": load_pmc_traffic("k_rt_walk<1>", "pmc_rt.json"),
+                     "kernel": "k_rt_walk<1> (emit)", "algorithmic_bytes_per_launch": alg,
+                     "bytes_model": "36 B per visited row (list entry, row, 4 topic words) + 4 B per match + "
+                                    "40 B per filter (workloads.RetainWorkload.algorithmic_bytes)"},
+        "cpu_baseline": cpu, "load_s": load_s, "arena_bytes": st["device_bytes"],
+        "partitions": st["partitions"]}), flush=True)
 
 
 if __name__ == "__main__":

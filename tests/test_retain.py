@@ -187,7 +187,9 @@ def test_retain_large_lists_span_many_chunks():
     for op in ops:
         orc.insert(op[1], op[2], op[3])
     filters = [("", (b"#",)), ("", (b"dev", b"+", b"status")), ("", (b"+", b"temp")), ("", (b"dev", b"#")),
-               ("", (b"dev", b"77", b"status")), ("", (b"+", b"+", b"+")), ("", (b"site7", b"#"))] * 3
+               ("", (b"dev", b"77", b"status")), ("", (b"+", b"+", b"+")), ("", (b"site7", b"#")),
+               ("", (b"dev", b"77", b"#")), ("", (b"dev", b"78", b"+")), ("", (b"site7", b"temp", b"#")),
+               ("", (b"dev", b"nope", b"#"))] * 3
     got, want = prod.fold_batch(filters), orc.fold_batch(filters)
     assert [len(g) for g in got] == [len(w) for w in want]
     assert got == want

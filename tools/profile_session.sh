@@ -5,7 +5,7 @@
 # selects the workload (default: the headline config C).
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${OUT:-gpurun_out/prof}
 mkdir -p $OUT
 B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}"
 echo "== kernel trace"

@@ -84,8 +84,9 @@ RLayout RetainEngine::plan_layout(uint32_t scale) const {
   for (auto& m : mplists) if (!m.rows.empty()) lists += std::max<uint64_t>(4, next_pow2(m.rows.size()));
   L.rows_cap = std::max<uint64_t>({4096, rows.size() * 2, cfg.hint_topics}) * scale;
   L.rwords_cap = std::max<uint64_t>(16384, words * 2 + cfg.hint_topics * 8) * scale;
-  L.lists_cap = std::max<uint64_t>(16384, lists * 2 + cfg.hint_topics * 4) * scale;
-  L.ptab_buckets = next_pow2(std::max<uint64_t>(1024, parts.size())) * scale;   // <= 1/4 load per bucket slot
+  L.lists_cap = std::max<uint64_t>(16384, lists * 2 + cfg.hint_topics * 8) * scale;
+  // slot load <= 1/8 after a re-layout, <= 1/4 before the next (place_part)
+  L.ptab_buckets = next_pow2(std::max<uint64_t>({1024, parts.size() * 4, cfg.hint_topics})) * scale;
   L.exact_slots = next_pow2(std::max<uint64_t>({4096, rows.size() * 2 + 1024, cfg.hint_topics * 2})) * scale;
   uint64_t o = 0;
   L.rows_off = o;   o = align256(o + L.rows_cap * sizeof(RRow));
@@ -112,23 +113,21 @@ void RetainEngine::rebuild() {
     bool ok = true;
     for (auto& r : rows) { r.words_off = kNone; r.xslot = ~0ull; }
     for (uint32_t r = 0; ok && r < rows.size(); r++) ok = write_row(r) && (!rows[r].live || place_exact(r));
-    for (uint32_t p = 0; ok && p < parts.size(); p++) {
-      RList& l = parts[p];
+    auto lay_list = [&](RList& l) {
       l.cap = std::max<uint64_t>(4, next_pow2(l.rows.size()));
-      if (lists_top + l.cap > lay.lists_cap) { ok = false; break; }
+      if (lists_top + l.cap > lay.lists_cap) return false;
       l.off = lists_top; lists_top += l.cap;
       std::copy(l.rows.begin(), l.rows.end(), region<uint32_t>(lay.lists_off) + l.off);
+      return true;
+    };
+    for (uint32_t p = 0; ok && p < parts.size(); p++) {
       part_slot[p] = ~0ull;
-      ok = place_part(p);
+      ok = lay_list(parts[p]) && place_part(p);
     }
     for (uint32_t m = 0; ok && m < mplists.size(); m++) {
       RList& l = mplists[m];
       if (l.rows.empty()) { l.off = 0; l.cap = 0; continue; }
-      l.cap = std::max<uint64_t>(4, next_pow2(l.rows.size()));
-      if (lists_top + l.cap > lay.lists_cap) { ok = false; break; }
-      l.off = lists_top; lists_top += l.cap;
-      std::copy(l.rows.begin(), l.rows.end(), region<uint32_t>(lay.lists_off) + l.off);
-      ok = write_list_head(false, m);
+      ok = lay_list(l) && write_list_head(0, m);
     }
     if (ok) break;
   }
@@ -173,22 +172,22 @@ bool RetainEngine::place_part(uint32_t p) {
   if ((uint64_t)(p + 1) * 4 > lay.ptab_buckets * kPSlotsPerBucket) return false;   // keep the load <= 1/4
   PSlot* tab = region<PSlot>(lay.ptab_off);
   const uint64_t mask = lay.ptab_buckets - 1;
-  for (uint64_t b = vmqg::mix64(((uint64_t)part_mp[p] << 32) | part_w0[p]) & mask;; b = (b + 1) & mask) {
+  for (uint64_t b = part_hash(part_mp[p], part_w0[p], part_w1[p]) & mask;; b = (b + 1) & mask) {
     for (uint32_t j = 0; j < kPSlotsPerBucket; j++) {
       const uint64_t si = b * kPSlotsPerBucket + j;
       if (tab[si].mp == kEmpty) {
         part_slot[p] = si;
-        return write_list_head(true, p);
+        return write_list_head(1, p);
       }
     }
   }
 }
 
-bool RetainEngine::write_list_head(bool part, uint32_t id) {
-  if (part) {
+bool RetainEngine::write_list_head(int level, uint32_t id) {
+  if (level) {
     const RList& l = parts[id];
     PSlot& s = region<PSlot>(lay.ptab_off)[part_slot[id]];
-    s = PSlot{part_mp[id], part_w0[id], (uint32_t)l.off, (uint32_t)l.rows.size()};
+    s = PSlot{part_mp[id], part_w0[id], part_w1[id], (uint32_t)l.off, (uint32_t)l.rows.size(), {0, 0, 0}};
     touch(lay.ptab_off + part_slot[id] * sizeof(PSlot), sizeof(PSlot));
   } else {
     const RList& l = mplists[id];
@@ -198,10 +197,13 @@ bool RetainEngine::write_list_head(bool part, uint32_t id) {
   return true;
 }
 
-// Append `row` (relocating the list when it is full); returns false when
-// the list pool is exhausted (the caller re-lays the arena out).
-bool RetainEngine::list_push(RList& l, uint32_t row, uint32_t& pos, bool part, uint32_t id) {
-  pos = (uint32_t)l.rows.size();
+// Append `row` to list `id` of `level` (relocating the list when it is
+// full); returns false when the list pool is exhausted (the caller re-lays
+// the arena out).
+bool RetainEngine::list_push(int level, uint32_t id, uint32_t row) {
+  RList& l = list_of(level, id);
+  const uint32_t pos = (uint32_t)l.rows.size();
+  rows[row].pos[level] = pos;
   l.rows.push_back(row);
   uint32_t* pool = region<uint32_t>(lay.lists_off);
   if (l.rows.size() > l.cap) {
@@ -215,21 +217,24 @@ bool RetainEngine::list_push(RList& l, uint32_t row, uint32_t& pos, bool part, u
     pool[l.off + pos] = row;
     touch(lay.lists_off + (l.off + pos) * 4, 4);
   }
-  return write_list_head(part, id);
+  return write_list_head(level, id);
 }
 
-// Swap-remove of position `pos` (order inside a list is free: ets:foldl
-// order is unspecified).
-void RetainEngine::list_remove(RList& l, uint32_t pos, bool part, uint32_t id) {
+// Swap-remove of `row` from list `id` of `level` (order inside a list is
+// free: ets:foldl order is unspecified).
+void RetainEngine::list_remove(int level, uint32_t id, uint32_t row) {
+  RList& l = list_of(level, id);
+  const uint32_t pos = rows[row].pos[level];
   const uint32_t last = l.rows.back();
   l.rows.pop_back();
   if (pos < l.rows.size()) {
     l.rows[pos] = last;
-    if (part) rows[last].pos_p = pos; else rows[last].pos_m = pos;
+    rows[last].pos[level] = pos;
     region<uint32_t>(lay.lists_off)[l.off + pos] = last;
     touch(lay.lists_off + (l.off + pos) * 4, 4);
   }
-  write_list_head(part, id);
+  rows[row].pos[level] = kNone;
+  write_list_head(level, id);
 }
 
 uint32_t RetainEngine::find_row(uint32_t mp, const uint32_t* w, uint32_t L) const {
@@ -239,14 +244,18 @@ uint32_t RetainEngine::find_row(uint32_t mp, const uint32_t* w, uint32_t L) cons
   });
 }
 
-uint32_t RetainEngine::part_of(uint32_t mp, uint32_t w0) {
-  const uint64_t k = ((uint64_t)mp << 32) | w0;
-  const uint32_t f = part_index.find(k);
+// Level-1 partition {MP, w0} (parent == kNone) or level-2 {MP, w0, w1}
+// under level-1 partition `parent`.
+uint32_t RetainEngine::part_of(uint32_t mp, uint32_t w0, uint32_t parent, uint32_t w1) {
+  FlatIndex& ix = parent == kNone ? part1_index : part2_index;
+  const uint64_t k = parent == kNone ? ((uint64_t)mp << 32) | w0 : ((uint64_t)parent << 32) | w1;
+  const uint32_t f = ix.find(k);
   if (f != FlatIndex::kVoid) return f;
   const uint32_t p = (uint32_t)parts.size();
   parts.emplace_back();
-  part_mp.push_back(mp); part_w0.push_back(w0); part_slot.push_back(~0ull);
-  part_index.insert(k, p);
+  part_mp.push_back(mp); part_w0.push_back(w0); part_w1.push_back(parent == kNone ? kNone : w1);
+  part_slot.push_back(~0ull);
+  ix.insert(k, p);
   return p;
 }
 
@@ -261,19 +270,24 @@ void RetainEngine::insert(uint32_t mp, const uint32_t* w, uint32_t L, uint32_t m
     if (r == FlatIndex::kVoid) {
       r = (uint32_t)rows.size();
       rows.emplace_back();
-      rows[r].mp = mp;
-      rows[r].words.assign(w, w + L);
+      RRowInfo& N = rows[r];
+      N.mp = mp;
+      N.words.assign(w, w + L);
+      N.part[0] = mp;
+      N.part[1] = part_of(mp, w[0], kNone, 0);
+      if (L >= 2) N.part[2] = part_of(mp, w[0], N.part[1], w[1]);
       key_index.insert(retain_fp(mp, w, L), r);
     }
     RRowInfo& R = rows[r];
     R.msg = msg;
     R.live = true;
     n_live++;
-    if (R.part == kNone) R.part = part_of(mp, w[0]);
-    const bool fresh = part_slot[R.part] == ~0ull;
-    if (fresh) ok = place_part(R.part);
-    ok = list_push(parts[R.part], r, R.pos_p, true, R.part) && ok;
-    ok = list_push(mplists[mp], r, rows[r].pos_m, false, mp) && ok;
+    for (int lv = 0; lv < 3; lv++) {
+      const uint32_t id = R.part[lv];
+      if (id == kNone) continue;
+      if (lv && part_slot[id] == ~0ull) ok = place_part(id) && ok;
+      ok = list_push(lv, id, r) && ok;
+    }
     ok = ok && write_row(r) && place_exact(r);
   }
   if (!ok) full_image = true;   // capacity: apply() re-lays out
@@ -286,10 +300,9 @@ void RetainEngine::erase(uint32_t mp, const uint32_t* w, uint32_t L) {
   RRowInfo& R = rows[r];
   R.live = false;
   n_live--;
-  list_remove(parts[R.part], R.pos_p, true, R.part);
-  list_remove(mplists[mp], rows[r].pos_m, false, mp);
-  rows[r].pos_p = rows[r].pos_m = kNone;
-  if (rows[r].xslot != ~0ull) place_exact(r);   // tombstone
+  for (int lv = 0; lv < 3; lv++)
+    if (R.part[lv] != kNone) list_remove(lv, R.part[lv], r);
+  if (R.xslot != ~0ull) place_exact(r);   // tombstone
 }
 
 int RetainEngine::apply(const vmqr_op* ops, size_t n, const uint32_t* words, size_t nwords) {

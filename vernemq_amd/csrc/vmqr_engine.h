@@ -8,11 +8,13 @@
 // Device arena (one allocation, regions 256-B aligned):
 //   rows   : RRow per retained key {msg, nwords, words_off, mp}
 //   rwords : u32 pool of the keys' topic words
-//   lists  : u32 pool of row ids: one list per partition {MP, first word}
-//            and one per MP (all rows of the MP, for filters whose first
-//            word is '+' or that are exactly '#')
-//   ptab   : open-addressed {MP, first word} -> partition list, 4 slots per
-//            64-B bucket
+//   lists  : u32 pool of row ids: per MP (level 0: all its rows), per
+//            {MP, w0} (level 1) and per {MP, w0, w1} (level 2) — a row sits
+//            in the lists of its MP and of its first one and two words.  A
+//            filter scans the list of its literal prefix (up to 2 words):
+//            rows outside it fail vmq_topic:match/2 anyway (vmq_topic.erl:55-65)
+//   ptab   : open-addressed {MP, level, w0, w1} -> list, 2 slots per 64-B
+//            bucket
 //   mpl    : per MP its list {off, count}
 //   exact  : open-addressed fingerprint of (MP, words) -> row, for filters
 //            without a wildcard (ets:lookup, :93-98)
@@ -34,11 +36,15 @@ using vmqg::FlatIndex;
 using vmqg::Patch;
 
 struct alignas(16) RRow { uint32_t msg, nwords, words_off, mp; };
-struct alignas(16) PSlot { uint32_t mp, w0, off, count; };        // mp == kEmpty: free
+// partition slot: level 1 {MP, w0, kNone}, level 2 {MP, w0, w1}; mp == kEmpty: free
+struct alignas(32) PSlot { uint32_t mp, w0, w1, off, count, pad[3]; };
 struct alignas(16) XSlot { uint64_t fp; uint32_t row, state; };    // state 0 free, 1 live, 2 deleted
 struct alignas(8) MpList { uint32_t off, count; };
-static_assert(sizeof(RRow) == 16 && sizeof(PSlot) == 16 && sizeof(XSlot) == 16 && sizeof(MpList) == 8, "");
-constexpr uint32_t kPSlotsPerBucket = 4;
+static_assert(sizeof(RRow) == 16 && sizeof(PSlot) == 32 && sizeof(XSlot) == 16 && sizeof(MpList) == 8, "");
+constexpr uint32_t kPSlotsPerBucket = 2;
+VMQG_HD uint64_t part_hash(uint32_t mp, uint32_t w0, uint32_t w1) {
+  return vmqg::mix64(vmqg::mix64(((uint64_t)mp << 32) | w0) ^ w1);
+}
 constexpr uint32_t kXLive = 1, kXTomb = 2;
 
 struct RLayout {
@@ -72,9 +78,10 @@ hipError_t launch_retain_match(const RArgs& a, uint32_t grid, hipStream_t st, hi
 uint64_t retain_fp(uint32_t mp, const uint32_t* w, uint32_t L);
 
 struct RRowInfo {
-  uint32_t mp = 0, msg = 0, part = vmqg::kNone;
+  uint32_t mp = 0, msg = 0;
+  uint32_t part[3] = {vmqg::kNone, vmqg::kNone, vmqg::kNone};   // [0] = MP, [1], [2] partitions (kNone: L < 2)
   std::vector<uint32_t> words;
-  uint32_t pos_p = vmqg::kNone, pos_m = vmqg::kNone;   // positions in its partition / MP list
+  uint32_t pos[3] = {vmqg::kNone, vmqg::kNone, vmqg::kNone};    // positions in those lists
   uint64_t xslot = ~0ull;
   uint32_t words_off = vmqg::kNone;
   bool live = false;
@@ -96,10 +103,11 @@ struct RetainEngine {
   std::vector<RRowInfo> rows;
   FlatIndex key_index;                 // hash(mp, words) -> row (verified)
   uint64_t n_live = 0;
-  // partitions {MP, first word}
-  FlatIndex part_index;                // mp << 32 | w0 -> partition
+  // partitions {MP, w0} (level 1) and {MP, w0, w1} (level 2)
+  FlatIndex part1_index;               // mp << 32 | w0 -> partition
+  FlatIndex part2_index;               // level-1 partition << 32 | w1 -> partition
   std::vector<RList> parts;
-  std::vector<uint32_t> part_mp, part_w0;
+  std::vector<uint32_t> part_mp, part_w0, part_w1;   // w1 = kNone at level 1
   std::vector<uint64_t> part_slot;
   std::vector<RList> mplists;          // per MP
   // mirror
@@ -144,12 +152,14 @@ struct RetainEngine {
   void insert(uint32_t mp, const uint32_t* w, uint32_t L, uint32_t msg);
   void erase(uint32_t mp, const uint32_t* w, uint32_t L);
   uint32_t find_row(uint32_t mp, const uint32_t* w, uint32_t L) const;
-  uint32_t part_of(uint32_t mp, uint32_t w0);
+  uint32_t part_of(uint32_t mp, uint32_t w0, uint32_t parent, uint32_t w1);
   template <class T> T* region(uint64_t off) { return reinterpret_cast<T*>(reinterpret_cast<uint8_t*>(mirror.data()) + off); }
   void touch(uint64_t off, uint64_t bytes);
-  bool list_push(RList& l, uint32_t row, uint32_t& pos, bool part, uint32_t id);
-  void list_remove(RList& l, uint32_t pos, bool part, uint32_t id);
-  bool write_list_head(bool part, uint32_t id);
+  // level 0: the MP list `id`; 1, 2: partition `id`
+  bool list_push(int level, uint32_t id, uint32_t row);
+  void list_remove(int level, uint32_t id, uint32_t row);
+  bool write_list_head(int level, uint32_t id);
+  RList& list_of(int level, uint32_t id) { return level ? parts[id] : mplists[id]; }
   bool write_row(uint32_t r);
   bool place_exact(uint32_t r);
   bool place_part(uint32_t p);

@@ -3,10 +3,11 @@
 //
 // The reference answers a wildcard filter with a full ets:foldl over the
 // retained table, testing every entry with vmq_topic:match/2.  Here the same
-// test runs on the rows of ONE list: the filter's partition {MP, first word}
-// when its first word is literal, else (first word '+', or exactly '#') the
-// MP's list — every other row of the table fails the test anyway (other MP,
-// or a different first word, vmq_topic.erl:55-65).  Lists are cut into
+// test runs on the rows of ONE list: the filter's partition {MP, w0, w1}
+// when its first two words are literal, {MP, w0} when only the first is,
+// else (first word '+', or exactly '#') the MP's list — every other row of
+// the table fails the test anyway (other MP, or different leading words,
+// vmq_topic.erl:55-65).  Lists are cut into
 // chunks of `chunk_rows` rows so that one huge list spreads over the chip:
 //   k_rt_plan   one thread per filter: has_wildcard/1 (:239-242); the exact
 //               ets:lookup (:93-98) as a fingerprint probe + word compare;
@@ -85,17 +86,25 @@ __global__ __launch_bounds__(256) void k_rt_plan(RArgs a) {
         }
         chunks = cnt;
       } else {
-        if (w[0] == kPlus || (L == 1 && w[0] == kHash)) {
+        bool unknown = false;   // a literal word no retained topic holds: nothing can match (:55-57)
+        for (uint32_t i = 0; i < L && !unknown; i++) unknown = w[i] == vmqg::kUnknownWord;
+        if (unknown) {
+          cnt = 0;
+        } else if (w[0] == kPlus || (L == 1 && w[0] == kHash)) {
           const MpList m = a.mpl[F.mountpoint];
           off = m.off; cnt = m.count;
         } else {
-          const uint64_t key_b = vmqg::mix64(((uint64_t)F.mountpoint << 32) | w[0]);
-          for (uint64_t b = key_b & a.ptab_mask, n = 0; n <= a.ptab_mask; b = (b + 1) & a.ptab_mask, n++) {
+          // literal prefix of one or two words: the rows whose first words
+          // are those (a literal filter word must equal the topic's,
+          // vmq_topic.erl:55-57; '#' after two literals still needs them)
+          const uint32_t w1 = L >= 2 && w[1] != kPlus && w[1] != kHash ? w[1] : kNone;
+          for (uint64_t b = part_hash(F.mountpoint, w[0], w1) & a.ptab_mask, n = 0; n <= a.ptab_mask;
+               b = (b + 1) & a.ptab_mask, n++) {
             bool done = false;
             for (uint32_t j = 0; j < kPSlotsPerBucket; j++) {
               const PSlot s = a.ptab[b * kPSlotsPerBucket + j];
               if (s.mp == kEmpty) { done = true; break; }
-              if (s.mp == F.mountpoint && s.w0 == w[0]) { off = s.off; cnt = s.count; done = true; break; }
+              if (s.mp == F.mountpoint && s.w0 == w[0] && s.w1 == w1) { off = s.off; cnt = s.count; done = true; break; }
             }
             if (done) break;
           }

@@ -572,3 +572,117 @@ def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None, part: s
         writes = 16 * (n_hit * (w.notes["n_wild"] + 1) + n_miss * w.notes["n_wild"])
         return writes + 40 * (hi - lo) + 16 * distinct
     return {"all": look + emit, "lookup": look, "emit": emit}[part]
+
+
+class RetainWorkload:
+    """Retained-store workload RT: the retained
+    messages of config C's device fleet and a burst of subscriptions folding
+    over them (vmq_reg:deliver_retained/5 -> vmq_retain_srv:match_fold/4).
+
+    Store: ``devices/{d}/telemetry/{m}`` for d < n_dev, m < 16 (one retained
+    message per topic, message id = row).  Filters (splitmix64 seed 0x7E7):
+      50 % ``devices/{d}/telemetry/#``   -> 16 messages
+      20 % ``devices/{d}/+/{m}``         -> 1
+      25 % ``devices/{d}/telemetry/{m}`` -> 1 (exact ets:lookup)
+       5 % ``devices/{d'}/telemetry/#`` with d' >= n_dev (no retained topic) -> 0
+      plus ``n_heavy`` x ``devices/+/telemetry/{m}`` -> n_dev each (a scan of
+      the whole ``devices`` partition).
+    Columns: word strings in ``vocab``; topics/filters as (n, 4) index arrays.
+    """
+
+    def __init__(self, n_dev: int = 62_500, n_filters: int = 1 << 18, n_heavy: int = 16, seed: int = 0x7E7):
+        self.n_dev, self.n_filters, self.n_heavy = n_dev, n_filters, n_heavy
+        self.n_topics = 16 * n_dev
+        self.vocab = [b"devices", b"telemetry", b"+", b"#"] + [b"m%d" % m for m in range(16)] + \
+                     [b"%d" % d for d in range(n_dev)]
+        self.V_DEV, self.V_TEL, self.V_PLUS, self.V_HASH, self.V_M0, self.V_D0 = 0, 1, 2, 3, 4, 20
+        i = np.arange(self.n_topics, dtype=np.int64)
+        self.topics = np.stack([np.zeros_like(i), self.V_D0 + i // 16, np.full_like(i, self.V_TEL),
+                                self.V_M0 + i % 16], axis=1)
+        r = SplitMix(seed)
+        n_reg = n_filters - n_heavy
+        kind = r.ints(n_reg, 100)
+        d = r.ints(n_reg, n_dev)
+        m = r.ints(n_reg, 16)
+        f = np.empty((n_reg, 4), dtype=np.int64)
+        f[:, 0] = self.V_DEV
+        f[:, 1] = self.V_D0 + d
+        f[:, 2] = self.V_TEL
+        f[:, 3] = self.V_M0 + m
+        wild = kind < 50
+        f[wild, 3] = self.V_HASH
+        plus = (kind >= 50) & (kind < 70)
+        f[plus, 2] = self.V_PLUS
+        unk = kind >= 95
+        f[unk, 1] = -1 - d[unk]            # a device id no retained topic has (word "x{d}")
+        f[unk, 3] = self.V_HASH
+        heavy = np.empty((n_heavy, 4), dtype=np.int64)
+        heavy[:, 0], heavy[:, 1], heavy[:, 2] = self.V_DEV, self.V_PLUS, self.V_TEL
+        heavy[:, 3] = self.V_M0 + np.arange(n_heavy) % 16
+        # heavy filters spread through the batch
+        pos = np.linspace(0, n_filters - 1, n_heavy).astype(np.int64) if n_heavy else np.zeros(0, np.int64)
+        is_heavy = np.zeros(n_filters, dtype=bool)
+        is_heavy[pos] = True
+        self.filters = np.empty((n_filters, 4), dtype=np.int64)
+        self.filters[is_heavy] = heavy
+        self.filters[~is_heavy] = f
+        per = np.where(wild, 16, np.where(unk, 0, 1))
+        self.matches = np.empty(n_filters, dtype=np.int64)
+        self.matches[is_heavy] = n_dev
+        self.matches[~is_heavy] = per
+        # rows each filter's list holds (what the walk visits): level-2 list
+        # {devices, d} = 16 rows; '+' second word -> level-1 {devices} = all;
+        # exact -> 1 row (the plan's probe); unknown word -> none
+        self.rows_visited = np.empty(n_filters, dtype=np.int64)
+        self.rows_visited[is_heavy] = self.n_topics
+        self.rows_visited[~is_heavy] = np.where(wild, 16, np.where(plus, 16, np.where(unk, 0, 1)))
+        self.exact = np.zeros(n_filters, dtype=bool)
+        self.exact[~is_heavy] = (kind >= 70) & (kind < 95)
+
+    def word(self, v: int) -> bytes:
+        return self.vocab[v] if v >= 0 else b"x%d" % (-1 - v)
+
+    def topic(self, i: int):
+        return tuple(self.word(int(v)) for v in self.topics[i])
+
+    def filter(self, i: int):
+        return tuple(self.word(int(v)) for v in self.filters[i])
+
+    def load_into(self, srv, batch: int = 1 << 20):
+        """Bulk insert/3 of every retained topic (message id = row)."""
+        from .retain import ROP_DTYPE
+        vid = srv.intern_words(self.vocab, create=True).astype(np.int64)
+        for lo in range(0, self.n_topics, batch):
+            hi = min(self.n_topics, lo + batch)
+            n = hi - lo
+            ops = np.zeros(n, dtype=ROP_DTYPE)
+            ops["kind"] = _lib.ROP_INSERT
+            ops["word_off"] = 4 * np.arange(n)
+            ops["nwords"] = 4
+            ops["msg"] = np.arange(lo, hi)
+            srv.apply_op_arrays(ops, vid[self.topics[lo:hi]].reshape(-1).astype(np.uint32))
+        return vid
+
+    def filter_arrays(self, vid: np.ndarray):
+        """(PUB_DTYPE filters, word ids): unknown device words -> WORD_UNKNOWN."""
+        from .reg_view import PUB_DTYPE
+        n = self.n_filters
+        arr = np.zeros(n, dtype=PUB_DTYPE)
+        arr["word_off"] = 4 * np.arange(n)
+        arr["nwords"] = 4
+        f = self.filters
+        words = np.where(f >= 0, vid[np.maximum(f, 0)], np.int64(_lib.WORD_UNKNOWN)).astype(np.uint32)
+        return arr, words.reshape(-1)
+
+    def algorithmic_bytes(self, part: str = "walk") -> int:
+        """Bytes one match batch must move, per the walk over each filter's
+        list: per visited row its 4-B list entry + 16-B row + 16-B topic
+        words; per filter its 16-B descriptor + 16-B words + 8-B offset; per
+        match one 4-B message id written.  part "walk": the count/emit walk
+        (one pass); "batch": plan + both passes."""
+        rows = int(self.rows_visited.sum())
+        per_filter = 16 + 16 + 8
+        walk = 36 * rows + 4 * int(self.matches.sum()) + per_filter * self.n_filters
+        if part == "walk":
+            return walk
+        return walk + 36 * rows + per_filter * self.n_filters
