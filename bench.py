@@ -75,6 +75,7 @@ def main():
                          "RT: retained-message match_fold (§8f rank 3)")
     ap.add_argument("--rt-devices", type=int, default=62_500, help="RT: devices x 16 retained topics")
     ap.add_argument("--rt-filters", type=int, default=1 << 18, help="RT: subscription filters per step")
+    ap.add_argument("--rt-heavy", type=int, default=16, help="RT: devices/+/telemetry/{m} filters per step")
     ap.add_argument("--e-scale", type=float, default=0.2, help="config E scale (1.0 = 50M subs)")
     ap.add_argument("--d-scale", type=float, default=1.0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N>1 on one GPU")
@@ -444,7 +445,7 @@ def bench_retain(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     t0 = time.time()
-    w = W.RetainWorkload(n_dev=args.rt_devices, n_filters=args.rt_filters)
+    w = W.RetainWorkload(n_dev=args.rt_devices, n_filters=args.rt_filters, n_heavy=args.rt_heavy)
     srv = RetainGpuSrv(device=0, hint_topics=w.n_topics)
     vid = w.load_into(srv)
     load_s = time.time() - t0
@@ -519,11 +520,11 @@ def bench_retain(args):
                                % (w.n_topics, nf, w.n_heavy)},
         "messages_per_s": total * args.steps / el, "matches_per_step": total,
         "verified_counts": verified,
-        "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3, "launches": nl},
+        "kernel_us": {"plan_scan": count_ns / 1e3, "walk": emit_ns / 1e3, "launches": nl},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS if achieved else None,
-                     "traffic": load_pmc_traffic("k_rt_walk<1>", "pmc_rt.json"),
-                     "kernel": "k_rt_walk<1> (emit)", "algorithmic_bytes_per_launch": alg,
+                     "traffic": load_pmc_traffic("k_rt_walk", "pmc_rt.json"),
+                     "kernel": "k_rt_walk (one-pass walk + emit)", "algorithmic_bytes_per_launch": alg,
                      "bytes_model": "36 B per visited row (list entry, row, 4 topic words) + 4 B per match + "
                                     "40 B per filter (workloads.RetainWorkload.algorithmic_bytes)"},
         "cpu_baseline": cpu, "load_s": load_s, "arena_bytes": st["device_bytes"],

@@ -103,7 +103,13 @@ int vmqr_stats(vmqr_ctx* ctx, vmqr_stats_t* out);
  * entry, sorted.  Owned by the context until its next call. */
 int vmqr_dump(vmqr_ctx* ctx, const char** text, size_t* len);
 
-/* Average duration (ns) of the per-chunk match kernels of the timed calls. */
+/* Tuning knob (results unchanged): "walk_rows_hint" = rows of the flattened
+ * walk the first look-back allocation covers (grown on demand: a batch that
+ * walks more reports VMQG_E_FRONTIER once and succeeds when run again). */
+int vmqr_set_option(vmqr_ctx* ctx, const char* name, int64_t value);
+
+/* Average duration (ns) of the timed calls' kernels: count_ns = plan + filter
+ * scan, emit_ns = the one-pass walk. */
 int vmqr_set_timing(vmqr_ctx* ctx, int enable);
 int vmqr_kernel_times(vmqr_ctx* ctx, double* count_ns, double* emit_ns, uint64_t* launches);
 

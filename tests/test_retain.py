@@ -216,3 +216,54 @@ def test_retain_device_entry_and_empty_batch():
     assert prod.r.match_status(s.cuda_stream) == 0
     assert d_offs.cpu().tolist() == [0, 3000, 3001, 3001]
     assert sorted(d_o.cpu().numpy()[:3001].tolist()) == sorted(ref_ids.tolist())
+
+
+@pytest.mark.gpu
+def test_retain_empty_runs_and_tile_growth():
+    """Runs of > 64 filters without rows (unknown words, missing keys)
+    between filters with rows, a batch where no filter has a row, trailing
+    empty filters, and a batch walking more rows than the first look-back
+    allocation covers (walk_rows_hint = 1,024: vmqr_match_batch reruns after
+    VMQG_E_FRONTIER; the device entry point reports it once, then succeeds)."""
+    import torch
+    prod, orc = ProductDriver(), OracleDriver()
+    ops = [("insert", "", (b"k", b"%d" % (i % 700), b"v%d" % (i // 700)), "m%d" % i) for i in range(7_000)]
+    prod.r.apply(ops)
+    for op in ops:
+        orc.insert(op[1], op[2], op[3])
+    empty = [("", (b"zz%d" % i, b"#")) for i in range(150)] + [("", (b"k", b"nope", b"+"))] * 70
+    full = [("", (b"k", b"+", b"v3")), ("", (b"k", b"5", b"#")), ("", (b"+", b"+", b"+"))]
+    batches = [empty, empty + full + empty, full[:1] + empty + full[1:] + empty * 2, empty[:3]]
+    for filters in batches:
+        got, want = prod.fold_batch(filters), orc.fold_batch(filters)
+        assert got == want
+    prod.r.set_option("walk_rows_hint", 1024)
+    prod2 = ProductDriver()
+    prod2.r.set_option("walk_rows_hint", 1024)
+    prod2.r.apply(ops)
+    filters = full * 40     # 40 x (700 + 10 + 7,000) rows: far more than the first allocation
+    assert prod2.fold_batch(filters) == orc.fold_batch(filters)
+    prod3 = ProductDriver()
+    prod3.r.set_option("walk_rows_hint", 1024)
+    prod3.r.apply(ops)
+    arr, words = prod3.r.prepare(filters)
+    dev = torch.device("cuda:0")
+    d_f = torch.from_numpy(arr.view(np.uint32).copy()).to(dev)
+    d_w = torch.from_numpy(words.astype(np.int32)).to(dev)
+    cap = 40 * (700 + 10 + 7000) + 1024
+    d_o = torch.zeros(cap, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(len(filters) + 1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream()
+    call = lambda: prod3.r.match_device(d_f.data_ptr(), len(filters), d_w.data_ptr(), d_o.data_ptr(), cap,
+                                        d_offs.data_ptr(), s.cuda_stream)
+    from vernemq_amd import _lib
+    call()
+    assert prod3.r.match_status(s.cuda_stream) == _lib.E_FRONTIER
+    call()
+    assert prod3.r.match_status(s.cuda_stream) == 0
+    want = orc.o.match_batch(filters)
+    offs = d_offs.cpu().numpy()
+    assert list(np.diff(offs)) == [len(x) for x in want]
+    got = d_o.cpu().numpy()
+    for i in range(len(filters)):
+        assert sorted(prod3.r._msgs[j][1] for j in got[offs[i]:offs[i + 1]]) == sorted(orc.payloads[j][1] for j in want[i])

@@ -122,6 +122,7 @@ SIGNATURES = [
     ("vmqr_match_status", ctypes.c_int, [_P, _P]),
     ("vmqr_stats", ctypes.c_int, [_P, ctypes.POINTER(RStats)]),
     ("vmqr_dump", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_SZ)]),
+    ("vmqr_set_option", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int64]),
     ("vmqr_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
     ("vmqr_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),

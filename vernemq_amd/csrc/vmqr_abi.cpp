@@ -89,8 +89,8 @@ int vmqr_match_status(vmqr_ctx* ctx, void* stream) {
   GUARD_END
 }
 
-// Host buffers: copy in, match, copy out; the chunk table grows and the
-// batch reruns when a batch needs more chunk slots than allocated.
+// Host buffers: copy in, match, copy out; the look-back tiles grow and the
+// batch reruns when a batch walks more rows than they cover.
 int vmqr_match_batch(vmqr_ctx* ctx, const vmqg_pub* filters, size_t n, const uint32_t* words, size_t nwords,
                      uint32_t* out, size_t out_cap, size_t* out_n, uint64_t* offsets) {
   if (!ctx || !offsets || (n && !filters) || (nwords && !words) || (out_cap && !out)) return VMQG_E_INVAL;
@@ -117,16 +117,7 @@ int vmqr_match_batch(vmqr_ctx* ctx, const vmqg_pub* filters, size_t n, const uin
     if (rc) return rc;
     rc = e.match_status(st);
     if (rc != VMQG_E_FRONTIER || attempt > 0) break;
-    // chunk slots: size them from the device's count and run again
-    uint64_t need = 0;
-    if (hipMemcpy(&need, e.d_plan + 2 * e.plan_cap + n, 8, hipMemcpyDeviceToHost) != hipSuccess) return VMQG_E_DEVICE;
-    hipFree(e.d_ccount);
-    e.d_ccount = nullptr;
-    e.ccount_cap = 0;
-    uint64_t c = 1;
-    while (c < need + 2) c <<= 1;
-    if (hipMalloc(&e.d_ccount, c * 8) != hipSuccess) return VMQG_E_NOMEM;
-    e.ccount_cap = c;
+    // match_status grew the look-back tiles for this batch: run it again
   }
   if (hipMemcpyAsync(offsets, e.d_offs, (n + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
@@ -159,6 +150,15 @@ int vmqr_dump(vmqr_ctx* ctx, const char** text, size_t* len) {
   *len = ctx->e.dump_text.size();
   return VMQG_OK;
   GUARD_END
+}
+
+int vmqr_set_option(vmqr_ctx* ctx, const char* name, int64_t value) {
+  if (!ctx || !name) return VMQG_E_INVAL;
+  if (!strcmp(name, "walk_rows_hint") && value >= 1) {
+    ctx->e.walk_rows_hint = (uint64_t)value;
+    return VMQG_OK;
+  }
+  return VMQG_E_INVAL;
 }
 
 int vmqr_set_timing(vmqr_ctx* ctx, int enable) {

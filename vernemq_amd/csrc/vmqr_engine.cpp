@@ -24,7 +24,7 @@ RetainEngine::~RetainEngine() {
   for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (ev_match_done) hipEventDestroy(ev_match_done);
-  hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_plan); hipFree(d_ccount); hipFree(d_lookback);
+  hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_tickets); hipFree(d_plan); hipFree(d_lookback);
   hipFree(d_f); hipFree(d_w); hipFree(d_o); hipFree(d_offs);
   if (h_patch) hipHostFree(h_patch);
   if (stream) hipStreamDestroy(stream);
@@ -46,8 +46,11 @@ int RetainEngine::init(const vmqr_config& c) {
     if (hipEventCreateWithFlags(&ev_match_done, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
     has_device = true;
     if (hipMalloc(&d_status, 64) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_tickets, 8 * kTicketStride * 4) != hipSuccess) return VMQG_E_NOMEM;
     if (hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cu_count < 1)
       cu_count = 256;
+    // the walk's grid is what fits on the chip at once (every block resident)
+    walk_grid = std::max(8, cu_count * walk_blocks_per_cu());
     return upload();
   }
   return VMQG_OK;
@@ -399,23 +402,12 @@ int RetainEngine::match_device(const vmqg_pub* d_filters, uint32_t nf, const uin
     plan_cap = next_pow2(nf + 1);
     if (hipMalloc(&d_plan, plan_cap * 3 * sizeof(uint64_t)) != hipSuccess) { plan_cap = 0; return VMQG_E_NOMEM; }
   }
-  const uint64_t want_chunks = std::max<uint64_t>(1u << 16, 4ull * nf);
-  if (want_chunks + 1 > ccount_cap) {
-    if (d_ccount) { hipStreamSynchronize(st); hipFree(d_ccount); }
-    d_ccount = nullptr;
-    ccount_cap = next_pow2(want_chunks + 1);
-    if (hipMalloc(&d_ccount, ccount_cap * sizeof(uint64_t)) != hipSuccess) { ccount_cap = 0; return VMQG_E_NOMEM; }
-  }
-  const uint64_t granules = std::max<uint64_t>((nf + 2) / 4096 + 1, ccount_cap / 4096 + 1);
-  if (granules > lookback_cap) {
-    if (d_lookback) { hipStreamSynchronize(st); hipFree(d_lookback); }
-    d_lookback = nullptr;
-    lookback_cap = next_pow2(std::max<uint64_t>(granules, 1024));
-    if (hipMalloc(&d_lookback, lookback_cap * 8) != hipSuccess) { lookback_cap = 0; return VMQG_E_NOMEM; }
-    if (hipMemsetAsync(d_lookback, 0, lookback_cap * 8, st) != hipSuccess) return VMQG_E_DEVICE;
-    lb_tag = 0;
-  }
-  lb_tag += 2;   // two scans per call, one tag each
+  // look-back granules: the filter scan's tiles and the walk's tiles (the
+  // walk's row count is only known on the device: a batch needing more
+  // reports VMQG_E_FRONTIER and vmqr_match_batch grows and reruns)
+  if (int rc = grow_tiles(std::max<uint64_t>(walk_rows_hint, (uint64_t)nf * 64), st)) return rc;
+  last_nf = nf;
+  lb_tag += 2;   // two look-back passes per call, one tag each
   if (lb_tag + 1 >= (1u << 20)) {
     if (hipMemsetAsync(d_lookback, 0, lookback_cap * 8, st) != hipSuccess) return VMQG_E_DEVICE;
     lb_tag = 2;
@@ -430,17 +422,29 @@ int RetainEngine::match_device(const vmqg_pub* d_filters, uint32_t nf, const uin
   a.max_mp = (uint32_t)lay.max_mp;
   a.exact = reinterpret_cast<const XSlot*>(d_arena + lay.exact_off);
   a.exact_mask = lay.exact_slots - 1;
-  a.filters = d_filters; a.words = d_words; a.nf = nf; a.chunk_rows = chunk_rows;
-  a.plan = d_plan; a.fchunks = d_plan + 2 * plan_cap;
-  a.ccount = d_ccount; a.chunk_cap = ccount_cap - 1;
+  a.filters = d_filters; a.words = d_words; a.nf = nf;
+  a.plan = d_plan; a.rpfx = d_plan + 2 * plan_cap;
   a.out = d_out; a.out_cap = out_cap; a.offsets = d_offsets;
-  a.status = d_status; a.lookback = d_lookback; a.lb_tag = lb_tag;
+  a.status = d_status; a.lookback = d_lookback; a.lb_tag = lb_tag; a.tile_cap = lookback_cap;
+  a.tickets = d_tickets;
+  if (hipMemsetAsync(d_tickets, 0, 8 * kTicketStride * 4, st) != hipSuccess) return VMQG_E_DEVICE;
   hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
   if (timing) for (auto& x : e) hipEventCreate(&x);
-  const uint32_t grid = (uint32_t)cu_count * 8;
-  if (launch_retain_match(a, grid, st, e[0], e[1], e[2], e[3]) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_retain_match(a, (uint32_t)walk_grid, st, e[0], e[1], e[2], e[3]) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) { t_count.push_back({e[0], e[1]}); t_emit.push_back({e[2], e[3]}); }
   if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
+  return VMQG_OK;
+}
+
+int RetainEngine::grow_tiles(uint64_t rows, hipStream_t st) {
+  const uint64_t want = std::max<uint64_t>(rows / kTileRows + 2, (plan_cap + 4095) / 4096 + 2);
+  if (want <= lookback_cap) return VMQG_OK;
+  if (d_lookback) { hipStreamSynchronize(st); hipFree(d_lookback); }
+  d_lookback = nullptr;
+  lookback_cap = next_pow2(want);
+  if (hipMalloc(&d_lookback, lookback_cap * 8) != hipSuccess) { lookback_cap = 0; return VMQG_E_NOMEM; }
+  if (hipMemsetAsync(d_lookback, 0, lookback_cap * 8, st) != hipSuccess) return VMQG_E_DEVICE;
+  lb_tag = 2;
   return VMQG_OK;
 }
 
@@ -452,7 +456,14 @@ int RetainEngine::match_status(hipStream_t st) {
   if (hipMemcpyAsync(h, d_status, 32, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipMemsetAsync(d_status, 0, 32, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (h[1] & 32u) return VMQG_E_FRONTIER;   // chunk slots exhausted: retry after growth
+  if (h[1] & 32u) {
+    // look-back tiles exhausted: size them from the batch's row count, so
+    // that the same batch succeeds when it is run again
+    uint64_t need = 0;
+    if (hipMemcpy(&need, d_plan + 2 * plan_cap + last_nf, 8, hipMemcpyDeviceToHost) != hipSuccess) return VMQG_E_DEVICE;
+    if (int rc = grow_tiles(need, st)) return rc;
+    return VMQG_E_FRONTIER;
+  }
   if (h[1] & 4u) return VMQG_E_OVERFLOW;
   if (h[1]) return VMQG_E_DEVICE;
   return VMQG_OK;

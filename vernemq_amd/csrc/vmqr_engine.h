@@ -57,21 +57,24 @@ static_assert(sizeof(RLayout) == 256, "");
 constexpr uint64_t kRLayoutMagic = 0x31726D7176ull;   // "vmqr1"
 
 // Launch interface (vmqr_kernels.hip).
+constexpr uint32_t kTileRows = 1024;   // rows of the flattened walk per look-back tile
 struct RArgs {
   const RRow* rows; const uint32_t* rwords; const uint32_t* lists;
   const PSlot* ptab; uint64_t ptab_mask;          // bucket mask
   const MpList* mpl; uint32_t max_mp, pad0;
   const XSlot* exact; uint64_t exact_mask;        // slot mask
-  const vmqg_pub* filters; const uint32_t* words; uint32_t nf, chunk_rows;
+  const vmqg_pub* filters; const uint32_t* words; uint32_t nf, pad1;
   uint64_t* plan;        // nf x 2: {list off | row, count | kind << 62}
-  uint64_t* fchunks;     // nf + 1: chunks per filter -> exclusive prefix (scan)
-  uint64_t* ccount;      // per chunk: matches -> exclusive output prefix (scan); [total chunks] = total
+  uint64_t* rpfx;        // nf + 1: rows per filter -> exclusive prefix (scan); [nf] = rows of the batch
   uint32_t* out; uint64_t out_cap;
   uint64_t* offsets;     // nf + 1
-  uint32_t* status;      // [1] error bits, [3]/[4] scan tickets
-  uint64_t* lookback; uint32_t lb_tag, pad1;
-  uint64_t chunk_cap;    // entries of ccount - 1
+  uint32_t* status;      // [1] error bits, [3] scan ticket, [4] walk ticket
+  uint64_t* lookback; uint32_t lb_tag, pad2;
+  uint64_t tile_cap;     // look-back granules: the walk's tiles must fit
+  uint32_t* tickets;     // walk tickets: kClasses counters, kTicketStride apart (zeroed per call)
 };
+constexpr uint32_t kTicketStride = 64;   // u32: 256 B between the counters
+int walk_blocks_per_cu();   // resident blocks of the walk kernel per CU (the walk grid)
 hipError_t launch_retain_match(const RArgs& a, uint32_t grid, hipStream_t st, hipEvent_t e_count0,
                                hipEvent_t e_count1, hipEvent_t e_emit0, hipEvent_t e_emit1);
 
@@ -124,14 +127,16 @@ struct RetainEngine {
   Patch* h_patch = nullptr; uint64_t h_patch_cap = 0;
   Patch* d_patch = nullptr; uint64_t d_patch_cap = 0;
   uint32_t* d_status = nullptr;
+  uint32_t* d_tickets = nullptr;
+  int walk_grid = 0;
   uint64_t* d_plan = nullptr; uint64_t plan_cap = 0;       // filters
-  uint64_t* d_ccount = nullptr; uint64_t ccount_cap = 0;   // chunks
+  uint64_t walk_rows_hint = 1ull << 26;   // rows the first look-back allocation covers (option)
+  uint32_t last_nf = 0;                    // filters of the last match_device call
   uint64_t* d_lookback = nullptr; uint64_t lookback_cap = 0; uint32_t lb_tag = 0;
   void* d_f = nullptr; uint64_t d_f_cap = 0;   // host-buffer staging
   void* d_w = nullptr; uint64_t d_w_cap = 0;
   void* d_o = nullptr; uint64_t d_o_cap = 0;
   void* d_offs = nullptr; uint64_t d_offs_cap = 0;
-  uint32_t chunk_rows = 1024;
   int cu_count = 256;
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_emit;
@@ -145,6 +150,7 @@ struct RetainEngine {
   int match_device(const vmqg_pub* d_filters, uint32_t nf, const uint32_t* d_words, uint32_t* d_out,
                    uint64_t out_cap, uint64_t* d_offsets, hipStream_t st);
   int match_status(hipStream_t st);
+  int grow_tiles(uint64_t rows, hipStream_t st);   // look-back granules for a walk over `rows`
   void collect_times();
   std::string dump();
 

@@ -7,21 +7,23 @@
 // when its first two words are literal, {MP, w0} when only the first is,
 // else (first word '+', or exactly '#') the MP's list — every other row of
 // the table fails the test anyway (other MP, or different leading words,
-// vmq_topic.erl:55-65).  Lists are cut into
-// chunks of `chunk_rows` rows so that one huge list spreads over the chip:
+// vmq_topic.erl:55-65).  The rows of all filters' lists form one flat,
+// filter-major row space (filter f owns rows [rpfx[f], rpfx[f+1])):
 //   k_rt_plan   one thread per filter: has_wildcard/1 (:239-242); the exact
 //               ets:lookup (:93-98) as a fingerprint probe + word compare;
-//               else the list, its length and its chunk count;
-//   scan        chunk counts -> first chunk of each filter (one launch);
-//   k_rt_count  one wave per chunk: 64 rows per step, one row per lane,
-//               vmq_topic:match/2 against the filter words staged in LDS;
-//               matches per chunk;
-//   scan        chunk matches -> output offsets (one launch, device-side n);
-//   k_rt_emit   the same walk writing the matching rows' message ids,
-//               ballot + mbcnt compacted, contiguous per chunk; and the
-//               per-filter offsets.
-// Bound: HBM / L2 reads of 16-B rows and their words; no MFMA (integer
-// compares only).
+//               else the list and its length;
+//   scan        rows per filter -> rpfx (one launch, decoupled look-back);
+//   k_rt_walk   one wave per 1,024-row tile, tiles taken in ticket order:
+//               64 rows per step, one row per lane, each lane's filter found
+//               in an LDS window of rpfx; vmq_topic:match/2 of the row's
+//               topic against the filter; hits (message ids) compacted in
+//               LDS with ballot + mbcnt; the tile's output base from a
+//               decoupled look-back over the tiles before it; then one
+//               contiguous store of the tile's hits and the offsets of the
+//               filters whose rows start in the tile.  One pass: no count
+//               pass, no second scan.
+// Bound: HBM / L2 reads of 16-B rows, their words and the 4-B list entries;
+// no MFMA (integer compares only).
 #include <hip/hip_runtime.h>
 
 #include "vmqr_engine.h"
@@ -35,9 +37,8 @@ using vmqg::kNone;
 using vmqg::kPlus;
 
 constexpr int kW = 4;                 // waves per 256-thread block
-constexpr uint32_t kFW = 64;          // filter words staged in LDS per wave
 constexpr uint64_t kKindExact = 1ull << 62, kKindList = 2ull << 62, kCountMask = (1ull << 62) - 1;
-constexpr uint32_t kErrChunks = 32u;  // status[1]: the batch needs more chunk slots than allocated
+constexpr uint32_t kErrChunks = 32u;  // status[1]: the batch walks more tiles than look-back granules
 constexpr uint32_t kErrOut = 4u;      // status[1]: output overflow (VMQG_E_OVERFLOW)
 
 __host__ __device__ inline uint64_t fp_of(uint32_t mp, const uint32_t* w, uint32_t L) {
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(256) void k_rt_plan(RArgs a) {
     const vmqg_pub F = a.filters[f];
     const uint32_t* w = a.words + F.word_off;
     const uint32_t L = F.nwords;
-    uint64_t off = 0, cnt = 0, kind = kKindList, chunks = 0;
+    uint64_t off = 0, cnt = 0, kind = kKindList;
     if (L > 0 && F.mountpoint < a.max_mp) {
       bool wild = w[L - 1] == kHash;   // has_wildcard/1: '#' as the last word ...
       for (uint32_t i = 0; i < L && !wild; i++) wild = w[i] == kPlus;   // ... or '+' anywhere
@@ -84,7 +85,6 @@ __global__ __launch_bounds__(256) void k_rt_plan(RArgs a) {
           for (uint32_t k = 0; eq && k < L; k++) eq = a.rwords[r.words_off + k] == w[k];
           if (eq) { off = x.row; cnt = 1; break; }
         }
-        chunks = cnt;
       } else {
         bool unknown = false;   // a literal word no retained topic holds: nothing can match (:55-57)
         for (uint32_t i = 0; i < L && !unknown; i++) unknown = w[i] == vmqg::kUnknownWord;
@@ -109,12 +109,11 @@ __global__ __launch_bounds__(256) void k_rt_plan(RArgs a) {
             if (done) break;
           }
         }
-        chunks = (cnt + a.chunk_rows - 1) / a.chunk_rows;
       }
     }
     a.plan[2 * (uint64_t)f] = off;
     a.plan[2 * (uint64_t)f + 1] = cnt | kind;
-    a.fchunks[f] = chunks;
+    a.rpfx[f] = cnt;   // rows the walk visits for this filter
   }
 }
 
@@ -165,107 +164,226 @@ __global__ __launch_bounds__(256) void k_rt_scan(uint64_t* v, uint64_t n_host, c
   }
 }
 
-// ------------------------------------------------------ count / emit pass
-// Chunk c of the batch -> its filter (last f with fchunks[f] <= c) and its
-// row range; the filter's words staged in the wave's LDS slice.
-struct ChunkWork {
-  uint32_t f, L, mp;
-  uint64_t kind, off, lo, hi;
-  const uint32_t* fw;   // filter words (LDS, or global for > kFW words)
-};
+// ------------------------------------------------------------- walk pass
+constexpr uint32_t kGroups = kTileRows / 64;    // 64-row steps per tile
+constexpr uint32_t kWin = 64;                   // rpfx window (filters) per step
+constexpr uint32_t kU = 4;                      // 64-row steps in flight per lane
+constexpr uint32_t kClasses = 8;                // ticket counters (block classes)
+constexpr uint32_t kPre = 4;                    // topic / filter words preloaded per row
+static_assert(kGroups % kU == 0, "");
 
-__device__ __forceinline__ ChunkWork chunk_work(const RArgs& a, uint64_t c, uint32_t* lds_fw) {
-  uint32_t lo = 0, hi = a.nf;   // fchunks[lo] <= c < fchunks[hi]
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (a.fchunks[mid] <= c) lo = mid; else hi = mid;
+// vmq_topic:match/2 as topic_match, with the first kPre words of both
+// already in registers (the rest read from memory).
+__device__ __forceinline__ bool topic_match_pre(const uint32_t (&tw)[kPre], const uint32_t (&fw)[kPre],
+                                                const uint32_t* t, uint32_t nt, const uint32_t* f, uint32_t nf) {
+  bool done = false, res = false;
+#pragma unroll
+  for (uint32_t k = 0; k < kPre; k++) {   // constant indices, results by value: the words stay in registers
+    const uint32_t tk = tw[k], fk = fw[k];
+    const bool end = k == nt && k == nf;
+    const bool step = k < nt && k < nf && (tk == fk || fk == kPlus);
+    if (!done && !step) res = end || (k + 1 == nf && fk == kHash);
+    done = done || !step;
   }
-  ChunkWork k;
-  k.f = lo;
-  const vmqg_pub F = a.filters[lo];
-  k.L = F.nwords;
-  k.mp = F.mountpoint;
-  const uint64_t pc = a.plan[2 * (uint64_t)lo + 1];
-  k.kind = pc & ~kCountMask;
-  k.off = a.plan[2 * (uint64_t)lo];
-  const uint64_t cnt = pc & kCountMask;
-  const uint64_t kth = c - a.fchunks[lo];
-  k.lo = kth * a.chunk_rows;
-  k.hi = k.lo + a.chunk_rows < cnt ? k.lo + a.chunk_rows : cnt;
-  const uint32_t* w = a.words + F.word_off;
+  if (done) return res;
+  for (uint32_t i = kPre;;) {
+    if (i == nt && i == nf) return true;
+    const uint32_t fi = i < nf ? f[i] : 0u;
+    if (i < nt && i < nf && (t[i] == fi || fi == kPlus)) { i++; continue; }
+    return i + 1 == nf && fi == kHash;
+  }
+}
+
+// Last filter f in [lo, hi) with rpfx[f] <= x (rpfx[lo] <= x < rpfx[hi]),
+// 64-ary search by the whole wave: each round probes 64 evenly spaced
+// entries with one load per lane.
+__device__ __forceinline__ uint32_t wave_search(const uint64_t* rpfx, uint32_t lo, uint32_t hi, uint64_t x) {
   const uint32_t lane = __lane_id();
-  if (k.L <= kFW) {
-    if (lane < k.L) lds_fw[lane] = w[lane];
-    __builtin_amdgcn_wave_barrier();
-    k.fw = lds_fw;
-  } else {
-    k.fw = w;
+  while (hi - lo > 1) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint32_t p = lo + lane * step;
+    const bool le = p < hi && rpfx[p] <= x;
+    const uint64_t m = __ballot(le);                      // lanes 0..k* (monotone)
+    const uint32_t k = 63 - __builtin_clzll(m);           // lane 0 always qualifies
+    lo = lo + k * step;
+    hi = lo + step < hi ? lo + step : hi;
   }
-  return k;
+  return lo;
 }
 
-// Row i of the chunk matches?  Exact chunks hold the looked-up row (already
-// verified by the plan); list chunks test vmq_topic:match/2 on the row.
-__device__ __forceinline__ bool row_hits(const RArgs& a, const ChunkWork& k, uint64_t i, uint32_t& msg) {
-  const uint32_t id = k.kind == kKindExact ? (uint32_t)k.off : a.lists[k.off + i];
-  const RRow r = a.rows[id];
-  msg = r.msg;
-  if (k.kind == kKindExact) return true;
-  return r.mp == k.mp && topic_match(a.rwords + r.words_off, r.nwords, k.fw, k.L);
-}
-
-template <int MODE>
 __global__ __launch_bounds__(256) void k_rt_walk(RArgs a) {
-  __shared__ uint32_t fw[kW][kFW];
+  __shared__ uint32_t s_hits[kW][kTileRows];     // message ids of the tile's hits, in row order
+  __shared__ uint64_t s_mask[kW][kGroups];       // hit mask per 64-row step
+  __shared__ uint64_t s_win[kW][kWin + 1];       // rpfx[f0 .. f0 + 64]
+  __shared__ uint32_t s_round;
   const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
-  const uint64_t total = a.fchunks[a.nf];
-  if (MODE == 0 && blockIdx.x == 0 && threadIdx.x == 0 && total > a.chunk_cap) atomicOr(&a.status[1], kErrChunks);
-  const uint64_t ntot = total < a.chunk_cap ? total : a.chunk_cap;
-  if (MODE == 1) {
-    // per-filter offsets: first output of the filter's first chunk
-    const uint64_t grand = a.ccount[ntot];
-    if (grand > a.out_cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&a.status[1], kErrOut);
-    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f <= a.nf; f += (uint64_t)gridDim.x * blockDim.x) {
-      const uint64_t fc = a.fchunks[f];
-      a.offsets[f] = a.ccount[fc < ntot ? fc : ntot];
-    }
-    if (grand > a.out_cap || total > a.chunk_cap) return;
+  const uint64_t R = a.rpfx[a.nf];                // rows of the batch
+  const uint64_t ntiles = (R + kTileRows - 1) / kTileRows;
+  if (ntiles > a.tile_cap) {                      // granules exhausted: the host grows them and reruns
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&a.status[1], kErrChunks);
+    return;
   }
-  for (uint64_t c = (uint64_t)blockIdx.x * kW + wv; c < ntot; c += (uint64_t)gridDim.x * kW) {
-    const ChunkWork k = chunk_work(a, c, fw[wv]);
-    uint64_t run = MODE == 1 ? a.ccount[c] : 0;
-    for (uint64_t i0 = k.lo; i0 < k.hi; i0 += 64) {
-      const uint64_t i = i0 + lane;
-      uint32_t msg = 0;
-      const bool hit = i < k.hi && row_hits(a, k, i, msg);
-      const uint64_t m = __ballot(hit);
-      if (MODE == 1 && hit) a.out[run + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = msg;
-      run += (uint64_t)__popcll(m);
+  if (ntiles == 0) {                              // no filter has a row: every offset is 0
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f <= a.nf; f += (uint64_t)gridDim.x * blockDim.x)
+      a.offsets[f] = 0;
+    return;
+  }
+  uint32_t* hits = s_hits[wv];
+  uint64_t* mask = s_mask[wv];
+  uint64_t* win = s_win[wv];
+  // Tiles by ticket, one atomic per block and round: class c = blockIdx % 8
+  // (one XCD each under round-robin dispatch) owns tiles c, c + 8, ...;
+  // round r of a class-c block gives its wave w tile (4r + w) * 8 + c.
+  // Look-back waits only on lower tiles, and the lowest tile in progress
+  // never waits on an untaken one: its class's blocks hold lower rounds.
+  const uint32_t cls = blockIdx.x % kClasses;
+  for (;;) {
+    if (threadIdx.x == 0) s_round = atomicAdd(a.tickets + cls * kTicketStride, 1u);
+    __syncthreads();
+    const uint32_t round = s_round;
+    if (((uint64_t)round * kW) * kClasses + cls >= ntiles) break;   // uniform in the block
+    const uint64_t tile64 = ((uint64_t)round * kW + wv) * kClasses + cls;
+    if (tile64 < ntiles) {
+    const uint32_t tile = (uint32_t)tile64;
+    const uint64_t base = (uint64_t)tile * kTileRows;
+    const uint64_t end = base + kTileRows < R ? base + kTileRows : R;
+    uint32_t f0 = wave_search(a.rpfx, 0, a.nf, base);   // filter of the tile's first row
+    uint32_t nh = 0;                                     // hits so far in the tile
+    // kU steps of 64 rows at a time: each lane has kU rows in flight, every
+    // load of one row independent of the others'
+    for (uint32_t g = 0; g < kGroups; g += kU) {
+      const uint64_t g0 = base + (uint64_t)g * 64;
+      if (g0 >= end) {
+        if (lane == 0) for (uint32_t h = g; h < kGroups; h++) mask[h] = 0;
+        break;
+      }
+      // window of filter starts around these rows
+      const uint32_t wf = f0 + lane;
+      win[lane] = wf <= a.nf ? a.rpfx[wf] : ~0ull;
+      if (lane == 0) win[kWin] = f0 + kWin <= a.nf ? a.rpfx[f0 + kWin] : ~0ull;
+      __builtin_amdgcn_wave_barrier();
+      uint32_t f[kU], id[kU];
+      uint64_t pc[kU];
+      bool ok[kU];
+#pragma clang loop unroll(full)
+      for (uint32_t u = 0; u < kU; u++) {
+        const uint64_t gi = g0 + u * 64 + lane;
+        ok[u] = gi < end;
+        f[u] = f0;
+        if (!ok[u]) continue;
+        uint64_t start;
+        if (win[kWin] <= gi) {
+          // more than 64 filter starts before this row (runs of empty
+          // filters): search the rest of rpfx
+          uint32_t lo = f0 + kWin, hi = a.nf;
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.rpfx[mid] <= gi) lo = mid; else hi = mid;
+          }
+          f[u] = lo;
+          start = a.rpfx[lo];
+        } else {
+          uint32_t lo = 0, hi = kWin;   // win[lo] <= gi < win[hi]
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (win[mid] <= gi) lo = mid; else hi = mid;
+          }
+          f[u] = f0 + lo;
+          start = win[lo];
+        }
+        pc[u] = a.plan[2 * (uint64_t)f[u] + 1];
+        const uint64_t off = a.plan[2 * (uint64_t)f[u]];
+        id[u] = (pc[u] & ~kCountMask) == kKindExact ? (uint32_t)off : a.lists[off + (gi - start)];
+      }
+      RRow r[kU];
+      vmqg_pub F[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; u++) {
+        if (!ok[u]) continue;
+        r[u] = a.rows[id[u]];
+        F[u] = a.filters[f[u]];
+      }
+      // the first kPre words of topic and filter in registers
+      uint32_t tw[kU][kPre], fw[kU][kPre];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; u++) {
+#pragma unroll
+        for (uint32_t k = 0; k < kPre; k++) {
+          tw[u][k] = ok[u] && k < r[u].nwords ? a.rwords[r[u].words_off + k] : 0u;
+          fw[u][k] = ok[u] && k < F[u].nwords ? a.words[F[u].word_off + k] : 0u;
+        }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; u++) {
+        bool hit = false;
+        if (ok[u]) {
+          hit = (pc[u] & ~kCountMask) == kKindExact ||   // the plan already verified the key
+                (r[u].mp == F[u].mountpoint &&
+                 topic_match_pre(tw[u], fw[u], a.rwords + r[u].words_off, r[u].nwords, a.words + F[u].word_off,
+                                 F[u].nwords));
+        }
+        const uint64_t m = __ballot(hit);
+        if (hit)
+          hits[nh + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+              r[u].msg;
+        if (lane == 0) mask[g + u] = m;
+        nh += (uint32_t)__popcll(m);
+      }
+      // the next rows start at the filter of the last row (lanes past the
+      // end kept f0, and the loop ends with them)
+      f0 = __builtin_amdgcn_readlane(f[kU - 1], 63);
+      __builtin_amdgcn_wave_barrier();
     }
-    if (MODE == 0 && lane == 0) a.ccount[c] = run;
     __builtin_amdgcn_wave_barrier();
+    const uint64_t pre = vmqg::lookback(a.lookback, a.lb_tag + 1, a.status, tile, nh);
+    const uint64_t total = pre + nh;
+    if (total > a.out_cap) {
+      if (lane == 0) atomicOr(&a.status[1], kErrOut);
+    } else {
+      for (uint32_t i = lane; i < nh; i += 64) a.out[pre + i] = hits[i];
+    }
+    // offsets of the filters whose rows start in this tile (the last tile
+    // also takes the ones starting at R: trailing empty filters and [nf])
+    const bool last = tile + 1 == ntiles;
+    // first candidate: the filter holding row base - 1 (its start is < base)
+    for (uint32_t fb = base ? wave_search(a.rpfx, 0, a.nf, base - 1) : 0;; fb += 64) {
+      const uint32_t ff = fb + lane;
+      const uint64_t p = ff <= a.nf ? a.rpfx[ff] : ~0ull;
+      const bool mine = p >= base && (p < base + kTileRows || (last && p == R)) && ff <= a.nf;
+      if (mine) {
+        const uint64_t rel = p - base;
+        const uint32_t gq = (uint32_t)(rel >> 6);
+        uint64_t c = 0;
+        for (uint32_t h = 0; h < gq && h < kGroups; h++) c += (uint64_t)__popcll(mask[h]);
+        if (gq < kGroups) c += (uint64_t)__popcll(mask[gq] & ((1ull << (rel & 63)) - 1));
+        a.offsets[ff] = pre + c;
+      }
+      const uint64_t beyond = __ballot(ff > a.nf || (p >= base + kTileRows && !(last && p == R)));
+      if (beyond) break;   // rpfx is monotone: the tile's filters are done
+    }
+    }
+    __syncthreads();   // s_round is rewritten next round
   }
 }
 
 // ---------------------------------------------------------------- launch
+int walk_blocks_per_cu() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rt_walk, 256, 0) != hipSuccess || nb < 1) nb = 1;
+  return nb;
+}
+
 hipError_t launch_retain_match(const RArgs& a, uint32_t grid, hipStream_t st, hipEvent_t ec0, hipEvent_t ec1,
                                hipEvent_t ee0, hipEvent_t ee1) {
+  if (ec0) hipEventRecord(ec0, st);
   const uint32_t gp = (a.nf + 255) / 256;
   k_rt_plan<<<gp < 2048 ? gp : 2048, 256, 0, st>>>(a);
-  uint32_t gs = (uint32_t)((a.nf + 1 + kST) / kST);
-  k_rt_scan<<<gs < 2048 ? gs : 2048, kSB, 0, st>>>(a.fchunks, a.nf, nullptr, a.status + 3, a.lookback, a.lb_tag,
+  const uint32_t gs = (uint32_t)((a.nf + 1 + kST) / kST);
+  k_rt_scan<<<gs < 2048 ? gs : 2048, kSB, 0, st>>>(a.rpfx, a.nf, nullptr, a.status + 3, a.lookback, a.lb_tag,
                                                    a.status);
-  if (ec0) hipEventRecord(ec0, st);
-  k_rt_walk<0><<<grid, 256, 0, st>>>(a);
   if (ec1) hipEventRecord(ec1, st);
-  // chunk totals: the count is device-side (fchunks[nf]); the ticket loop
-  // stops at the real tile count, the grid only bounds the parallelism
-  gs = (uint32_t)((a.chunk_cap + 1 + kST) / kST);
-  k_rt_scan<<<gs < 1024 ? gs : 1024, kSB, 0, st>>>(a.ccount, a.chunk_cap, a.fchunks + a.nf, a.status + 4, a.lookback,
-                                                   a.lb_tag + 1, a.status);
   if (ee0) hipEventRecord(ee0, st);
-  k_rt_walk<1><<<grid, 256, 0, st>>>(a);
+  k_rt_walk<<<grid, 256, 0, st>>>(a);
   if (ee1) hipEventRecord(ee1, st);
   return hipGetLastError();
 }

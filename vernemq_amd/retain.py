@@ -195,6 +195,11 @@ class RetainGpuSrv:
         _lib.check(self._L.vmqr_dump(self._h, ctypes.byref(p), ctypes.byref(n)), "vmqr_dump")
         return ctypes.string_at(p, n.value).decode("latin-1")
 
+    def set_option(self, name: str, value: int):
+        """Tuning knob (vmqr_set_option): "walk_rows_hint" = rows the first
+        look-back allocation of the walk covers (results unchanged)."""
+        _lib.check(self._L.vmqr_set_option(self._h, name.encode(), int(value)), "vmqr_set_option")
+
     def set_timing(self, on: bool):
         _lib.check(self._L.vmqr_set_timing(self._h, 1 if on else 0), "vmqr_set_timing")
 
