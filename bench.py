@@ -525,7 +525,7 @@ def bench_retain(args):
                      "frac": achieved / PEAK_HBM_GBS if achieved else None,
                      "traffic": load_pmc_traffic("k_rt_walk", "pmc_rt.json"),
                      "kernel": "k_rt_walk (one-pass walk + emit)", "algorithmic_bytes_per_launch": alg,
-                     "bytes_model": "36 B per visited row (list entry, row, 4 topic words) + 4 B per match + "
+                     "bytes_model": "32 B per visited candidate (its list entry) + 4 B per match + "
                                     "40 B per filter (workloads.RetainWorkload.algorithmic_bytes)"},
         "cpu_baseline": cpu, "load_s": load_s, "arena_bytes": st["device_bytes"],
         "partitions": st["partitions"]}), flush=True)

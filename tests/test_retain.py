@@ -267,3 +267,34 @@ def test_retain_empty_runs_and_tile_growth():
     got = d_o.cpu().numpy()
     for i in range(len(filters)):
         assert sorted(prod3.r._msgs[j][1] for j in got[offs[i]:offs[i + 1]]) == sorted(orc.payloads[j][1] for j in want[i])
+
+
+@pytest.mark.gpu
+def test_retain_position_lists_and_long_topics():
+    """Filters whose only literals sit after a '+' (position lists), at the
+    last indexed position (15) and beyond it (>= 16: the MP list), on
+    20-word topics, under inserts and deletes."""
+    prod, orc = ProductDriver(), OracleDriver()
+    rnd = random.Random(5)
+    ops = []
+    for i in range(3000):
+        t = tuple(rnd.choice([b"a", b"b", b"c"]) for _ in range(rnd.choice([3, 16, 17, 20])))
+        ops.append(("insert", "", t, "p%d" % i) if rnd.random() < 0.8 else ("delete", "", t))
+    for k in range(0, len(ops), 500):
+        prod.r.apply(ops[k:k + 500])
+        for op in ops[k:k + 500]:
+            if op[0] == "insert":
+                orc.insert(op[1], op[2], op[3])
+            else:
+                orc.delete(op[1], op[2])
+    filters = []
+    for L in (3, 16, 17, 20):
+        for lit in (1, L - 2, L - 1):
+            f = [b"+"] * L
+            f[lit] = b"b"
+            filters.append(("", tuple(f)))
+            filters.append(("", tuple(f[:lit + 1]) + (b"#",)))
+    filters += [("", (b"+", b"c", b"#")), ("", (b"a", b"+", b"a", b"#")), ("", (b"#",))]
+    got, want = prod.fold_batch(filters), orc.fold_batch(filters)
+    assert [len(g) for g in got] == [len(w) for w in want]
+    assert got == want

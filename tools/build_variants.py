@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Compile libvmqgpu.so variants for A/B runs (tools/rt_ab.sh): the same
+sources and flags as vernemq_amd._lib.build plus -D knobs, into build/ab/."""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from vernemq_amd import _lib  # noqa: E402
+
+VARIANTS = {
+    "default": [],
+    "u1": ["-DVMQR_U=1"],
+    "u4": ["-DVMQR_U=4"],
+    "t512": ["-DVMQR_TILE_ROWS=512"],
+    "t2048": ["-DVMQR_TILE_ROWS=2048"],
+}
+
+
+def build(name, flags):
+    out = os.path.join(ROOT, "build", "ab", "lib_%s.so" % name)
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-value", "-Wno-unused-result"] + flags + ["-o", out] + _lib.SOURCES
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    return name, r.returncode, r.stderr[-2000:]
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(VARIANTS)
+    os.makedirs(os.path.join(ROOT, "build", "ab"), exist_ok=True)
+    with ThreadPoolExecutor(4) as ex:
+        for name, rc, err in ex.map(lambda n: build(n, VARIANTS[n]), names):
+            print(name, "ok" if rc == 0 else "FAILED\n" + err)

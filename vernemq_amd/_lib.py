@@ -170,10 +170,11 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError("libvmqgpu.so not built (%s); run vernemq_amd._lib.build()" % LIB_PATH)
+    path = os.environ.get("VMQG_LIB_PATH", LIB_PATH)   # A/B runs of kernel variants (tools/)
+    if not os.path.exists(path):
+        raise ImportError("libvmqgpu.so not built (%s); run vernemq_amd._lib.build()" % path)
     _share_torch_hip_runtime()
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
         f = getattr(L, name)
         f.restype = res

@@ -34,8 +34,15 @@ __device__ __forceinline__ uint64_t lb_load(uint64_t* p) {
 // with an inclusive prefix ends the walk, the aggregates of the ones in
 // between are summed.  A round is retried while a granule it needs is not
 // yet posted (tag of an earlier call).
-constexpr int kLbDepth = 4;
+#ifndef VMQG_LB_DEPTH
+#define VMQG_LB_DEPTH 4
+#endif
+constexpr int kLbDepth = VMQG_LB_DEPTH;
 
+// kSleep: s_sleep between rounds that found a granule not yet posted —
+// longer for callers with many waves spinning at once (their loads slow the
+// waves still working).
+template <int kSleep = 1>
 __device__ inline uint64_t lookback(uint64_t* lb, uint32_t tag, uint32_t* status, uint32_t chunk, uint64_t agg) {
   const uint32_t lane = __lane_id();
   if (chunk == 0) {
@@ -75,7 +82,7 @@ __device__ inline uint64_t lookback(uint64_t* lb, uint32_t tag, uint32_t* status
     }
     if (retry) {
       if (++spins > kSpinLimit) { if (lane == 0) atomicOr(&status[1], kErrLookback); break; }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(kSleep);
       continue;   // the whole round again (its granules may have moved on)
     }
     excl += sum;

@@ -94,7 +94,7 @@ RLayout RetainEngine::plan_layout(uint32_t scale) const {
   uint64_t o = 0;
   L.rows_off = o;   o = align256(o + L.rows_cap * sizeof(RRow));
   L.rwords_off = o; o = align256(o + L.rwords_cap * 4);
-  L.lists_off = o;  o = align256(o + L.lists_cap * 4);
+  L.lists_off = o;  o = align256(o + L.lists_cap * sizeof(LEnt));
   L.ptab_off = o;   o = align256(o + L.ptab_buckets * kPSlotsPerBucket * sizeof(PSlot));
   L.mpl_off = o;    o = align256(o + L.max_mp * sizeof(MpList));
   L.exact_off = o;  o = align256(o + L.exact_slots * sizeof(XSlot));
@@ -120,7 +120,8 @@ void RetainEngine::rebuild() {
       l.cap = std::max<uint64_t>(4, next_pow2(l.rows.size()));
       if (lists_top + l.cap > lay.lists_cap) return false;
       l.off = lists_top; lists_top += l.cap;
-      std::copy(l.rows.begin(), l.rows.end(), region<uint32_t>(lay.lists_off) + l.off);
+      LEnt* pool = region<LEnt>(lay.lists_off) + l.off;
+      for (size_t i = 0; i < l.rows.size(); i++) pool[i] = entry_of(l.rows[i]);
       return true;
     };
     for (uint32_t p = 0; ok && p < parts.size(); p++) {
@@ -130,7 +131,7 @@ void RetainEngine::rebuild() {
     for (uint32_t m = 0; ok && m < mplists.size(); m++) {
       RList& l = mplists[m];
       if (l.rows.empty()) { l.off = 0; l.cap = 0; continue; }
-      ok = lay_list(l) && write_list_head(0, m);
+      ok = lay_list(l) && write_list_head(false, m);
     }
     if (ok) break;
   }
@@ -150,6 +151,20 @@ bool RetainEngine::write_row(uint32_t r) {
   *(region<RRow>(lay.rows_off) + r) = RRow{R.msg, (uint32_t)R.words.size(), R.words_off, R.mp};
   touch(lay.rows_off + (uint64_t)r * sizeof(RRow), sizeof(RRow));
   return true;
+}
+
+LEnt RetainEngine::entry_of(uint32_t r) const {
+  const RRowInfo& R = rows[r];
+  LEnt e{r, R.msg, (uint32_t)R.words.size(), R.words_off, {0, 0, 0, 0}};
+  for (uint32_t k = 0; k < kLWords && k < R.words.size(); k++) e.w[k] = R.words[k];
+  return e;
+}
+
+void RetainEngine::put_entry(uint64_t slot, uint32_t r) {
+  // after a capacity miss in this batch the arena is laid out anew anyway
+  if (full_image || slot >= lay.lists_cap) return;
+  region<LEnt>(lay.lists_off)[slot] = entry_of(r);
+  touch(lay.lists_off + slot * sizeof(LEnt), sizeof(LEnt));
 }
 
 // Exact slot of a live row (a revived row reuses its slot; tombstones are
@@ -175,22 +190,23 @@ bool RetainEngine::place_part(uint32_t p) {
   if ((uint64_t)(p + 1) * 4 > lay.ptab_buckets * kPSlotsPerBucket) return false;   // keep the load <= 1/4
   PSlot* tab = region<PSlot>(lay.ptab_off);
   const uint64_t mask = lay.ptab_buckets - 1;
-  for (uint64_t b = part_hash(part_mp[p], part_w0[p], part_w1[p]) & mask;; b = (b + 1) & mask) {
+  for (uint64_t b = part_hash(part_mp[p], part_a[p], part_b[p], part_kind[p]) & mask;; b = (b + 1) & mask) {
     for (uint32_t j = 0; j < kPSlotsPerBucket; j++) {
       const uint64_t si = b * kPSlotsPerBucket + j;
       if (tab[si].mp == kEmpty) {
         part_slot[p] = si;
-        return write_list_head(1, p);
+        return write_list_head(true, p);
       }
     }
   }
 }
 
-bool RetainEngine::write_list_head(int level, uint32_t id) {
-  if (level) {
+bool RetainEngine::write_list_head(bool part, uint32_t id) {
+  if (part) {
+    if (part_slot[id] == ~0ull) return false;   // no table slot (capacity): the caller re-lays out
     const RList& l = parts[id];
     PSlot& s = region<PSlot>(lay.ptab_off)[part_slot[id]];
-    s = PSlot{part_mp[id], part_w0[id], part_w1[id], (uint32_t)l.off, (uint32_t)l.rows.size(), {0, 0, 0}};
+    s = PSlot{part_mp[id], part_a[id], part_b[id], part_kind[id], (uint32_t)l.off, (uint32_t)l.rows.size(), {0, 0}};
     touch(lay.ptab_off + part_slot[id] * sizeof(PSlot), sizeof(PSlot));
   } else {
     const RList& l = mplists[id];
@@ -200,44 +216,53 @@ bool RetainEngine::write_list_head(int level, uint32_t id) {
   return true;
 }
 
-// Append `row` to list `id` of `level` (relocating the list when it is
-// full); returns false when the list pool is exhausted (the caller re-lays
-// the arena out).
-bool RetainEngine::list_push(int level, uint32_t id, uint32_t row) {
-  RList& l = list_of(level, id);
+// Append `row` to one of its lists (relocating the list when it is full);
+// returns false when the list pool is exhausted (the caller re-lays the
+// arena out).
+bool RetainEngine::list_push(uint32_t row, int which) {
+  RRowInfo& R = rows[row];
+  const bool part = which >= 0;
+  const uint32_t id = part ? R.part[which] : R.mp;
+  RList& l = part ? parts[id] : mplists[id];
   const uint32_t pos = (uint32_t)l.rows.size();
-  rows[row].pos[level] = pos;
+  (part ? R.ppos[which] : R.mpos) = pos;
   l.rows.push_back(row);
-  uint32_t* pool = region<uint32_t>(lay.lists_off);
   if (l.rows.size() > l.cap) {
     const uint64_t cap = std::max<uint64_t>(4, next_pow2(l.rows.size()));
     if (lists_top + cap > lay.lists_cap) return false;
     lists_garbage += l.cap;
     l.off = lists_top; l.cap = cap; lists_top += cap;
-    std::copy(l.rows.begin(), l.rows.end(), pool + l.off);
-    touch(lay.lists_off + l.off * 4, l.rows.size() * 4);
+    for (size_t i = 0; i < l.rows.size(); i++) put_entry(l.off + i, l.rows[i]);
   } else {
-    pool[l.off + pos] = row;
-    touch(lay.lists_off + (l.off + pos) * 4, 4);
+    put_entry(l.off + pos, row);
   }
-  return write_list_head(level, id);
+  return write_list_head(part, id);
 }
 
-// Swap-remove of `row` from list `id` of `level` (order inside a list is
-// free: ets:foldl order is unspecified).
-void RetainEngine::list_remove(int level, uint32_t id, uint32_t row) {
-  RList& l = list_of(level, id);
-  const uint32_t pos = rows[row].pos[level];
+// Swap-remove of `row` from one of its lists (order inside a list is free:
+// ets:foldl order is unspecified).  The row moved into the hole finds its
+// own slot for the list by the list id (a row is in a list at most once).
+void RetainEngine::list_remove(uint32_t row, int which) {
+  RRowInfo& R = rows[row];
+  const bool part = which >= 0;
+  const uint32_t id = part ? R.part[which] : R.mp;
+  RList& l = part ? parts[id] : mplists[id];
+  uint32_t& mine = part ? R.ppos[which] : R.mpos;
+  const uint32_t pos = mine;
   const uint32_t last = l.rows.back();
   l.rows.pop_back();
   if (pos < l.rows.size()) {
     l.rows[pos] = last;
-    rows[last].pos[level] = pos;
-    region<uint32_t>(lay.lists_off)[l.off + pos] = last;
-    touch(lay.lists_off + (l.off + pos) * 4, 4);
+    RRowInfo& M = rows[last];
+    if (part) {
+      for (size_t j = 0; j < M.part.size(); j++) if (M.part[j] == id) { M.ppos[j] = pos; break; }
+    } else {
+      M.mpos = pos;
+    }
+    put_entry(l.off + pos, last);
   }
-  rows[row].pos[level] = kNone;
-  write_list_head(level, id);
+  mine = kNone;
+  write_list_head(part, id);
 }
 
 uint32_t RetainEngine::find_row(uint32_t mp, const uint32_t* w, uint32_t L) const {
@@ -247,18 +272,18 @@ uint32_t RetainEngine::find_row(uint32_t mp, const uint32_t* w, uint32_t L) cons
   });
 }
 
-// Level-1 partition {MP, w0} (parent == kNone) or level-2 {MP, w0, w1}
-// under level-1 partition `parent`.
-uint32_t RetainEngine::part_of(uint32_t mp, uint32_t w0, uint32_t parent, uint32_t w1) {
-  FlatIndex& ix = parent == kNone ? part1_index : part2_index;
-  const uint64_t k = parent == kNone ? ((uint64_t)mp << 32) | w0 : ((uint64_t)parent << 32) | w1;
-  const uint32_t f = ix.find(k);
+// The list {MP, kind, a, b}: kPair {MP, w0, w1}, kPos {MP, word, position}.
+uint32_t RetainEngine::part_of(uint32_t mp, uint32_t a, uint32_t b, uint32_t kind) {
+  const uint64_t h = part_hash(mp, a, b, kind);
+  const uint32_t f = part_index.find(h, [&](uint32_t p) {
+    return part_mp[p] == mp && part_a[p] == a && part_b[p] == b && part_kind[p] == kind;
+  });
   if (f != FlatIndex::kVoid) return f;
   const uint32_t p = (uint32_t)parts.size();
   parts.emplace_back();
-  part_mp.push_back(mp); part_w0.push_back(w0); part_w1.push_back(parent == kNone ? kNone : w1);
+  part_mp.push_back(mp); part_a.push_back(a); part_b.push_back(b); part_kind.push_back(kind);
   part_slot.push_back(~0ull);
-  ix.insert(k, p);
+  part_index.insert(h, p);
   return p;
 }
 
@@ -267,8 +292,12 @@ void RetainEngine::insert(uint32_t mp, const uint32_t* w, uint32_t L, uint32_t m
   uint32_t r = find_row(mp, w, L);
   bool ok = true;
   if (r != FlatIndex::kVoid && rows[r].live) {
-    rows[r].msg = msg;
+    RRowInfo& R = rows[r];
+    R.msg = msg;
     ok = write_row(r);
+    // the list entries carry the msg
+    for (size_t j = 0; j < R.part.size(); j++) put_entry(parts[R.part[j]].off + R.ppos[j], r);
+    put_entry(mplists[R.mp].off + R.mpos, r);
   } else {
     if (r == FlatIndex::kVoid) {
       r = (uint32_t)rows.size();
@@ -276,22 +305,23 @@ void RetainEngine::insert(uint32_t mp, const uint32_t* w, uint32_t L, uint32_t m
       RRowInfo& N = rows[r];
       N.mp = mp;
       N.words.assign(w, w + L);
-      N.part[0] = mp;
-      N.part[1] = part_of(mp, w[0], kNone, 0);
-      if (L >= 2) N.part[2] = part_of(mp, w[0], N.part[1], w[1]);
+      if (L >= 2) N.part.push_back(part_of(mp, w[0], w[1], kPair));
+      for (uint32_t k = 0; k < L && k < kMaxPos; k++) N.part.push_back(part_of(mp, w[k], k, kPos));
+      N.ppos.assign(N.part.size(), kNone);
       key_index.insert(retain_fp(mp, w, L), r);
     }
     RRowInfo& R = rows[r];
     R.msg = msg;
     R.live = true;
     n_live++;
-    for (int lv = 0; lv < 3; lv++) {
-      const uint32_t id = R.part[lv];
-      if (id == kNone) continue;
-      if (lv && part_slot[id] == ~0ull) ok = place_part(id) && ok;
-      ok = list_push(lv, id, r) && ok;
+    ok = write_row(r);   // first: the list entries copy its words offset
+    for (size_t j = 0; j < R.part.size(); j++) {
+      const uint32_t id = R.part[j];
+      if (part_slot[id] == ~0ull) ok = place_part(id) && ok;
+      ok = list_push(r, (int)j) && ok;
     }
-    ok = ok && write_row(r) && place_exact(r);
+    ok = list_push(r, -1) && ok;
+    ok = ok && place_exact(r);
   }
   if (!ok) full_image = true;   // capacity: apply() re-lays out
 }
@@ -303,8 +333,8 @@ void RetainEngine::erase(uint32_t mp, const uint32_t* w, uint32_t L) {
   RRowInfo& R = rows[r];
   R.live = false;
   n_live--;
-  for (int lv = 0; lv < 3; lv++)
-    if (R.part[lv] != kNone) list_remove(lv, R.part[lv], r);
+  for (size_t j = 0; j < R.part.size(); j++) list_remove(r, (int)j);
+  list_remove(r, -1);
   if (R.xslot != ~0ull) place_exact(r);   // tombstone
 }
 
@@ -415,7 +445,7 @@ int RetainEngine::match_device(const vmqg_pub* d_filters, uint32_t nf, const uin
   RArgs a{};
   a.rows = reinterpret_cast<const RRow*>(d_arena + lay.rows_off);
   a.rwords = reinterpret_cast<const uint32_t*>(d_arena + lay.rwords_off);
-  a.lists = reinterpret_cast<const uint32_t*>(d_arena + lay.lists_off);
+  a.lists = reinterpret_cast<const LEnt*>(d_arena + lay.lists_off);
   a.ptab = reinterpret_cast<const PSlot*>(d_arena + lay.ptab_off);
   a.ptab_mask = lay.ptab_buckets - 1;
   a.mpl = reinterpret_cast<const MpList*>(d_arena + lay.mpl_off);

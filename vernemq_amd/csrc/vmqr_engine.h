@@ -8,13 +8,14 @@
 // Device arena (one allocation, regions 256-B aligned):
 //   rows   : RRow per retained key {msg, nwords, words_off, mp}
 //   rwords : u32 pool of the keys' topic words
-//   lists  : u32 pool of row ids: per MP (level 0: all its rows), per
-//            {MP, w0} (level 1) and per {MP, w0, w1} (level 2) — a row sits
-//            in the lists of its MP and of its first one and two words.  A
-//            filter scans the list of its literal prefix (up to 2 words):
-//            rows outside it fail vmq_topic:match/2 anyway (vmq_topic.erl:55-65)
-//   ptab   : open-addressed {MP, level, w0, w1} -> list, 2 slots per 64-B
-//            bucket
+//   lists  : pool of 32-B entries (row id, msg, the topic's first words):
+//            per MP (all its rows); per {MP, k, w}
+//            (position list: rows whose word k is w, k < kMaxPos) and per
+//            {MP, w0, w1} (pair list: rows whose first two words are those).
+//            A wildcard filter scans the shortest list one of its literal
+//            words selects: a row outside it fails vmq_topic:match/2 anyway
+//            (a literal filter word must equal the topic's, vmq_topic.erl:55-57)
+//   ptab   : open-addressed {MP, kind, a, b} -> list, 2 slots per 64-B bucket
 //   mpl    : per MP its list {off, count}
 //   exact  : open-addressed fingerprint of (MP, words) -> row, for filters
 //            without a wildcard (ets:lookup, :93-98)
@@ -36,14 +37,22 @@ using vmqg::FlatIndex;
 using vmqg::Patch;
 
 struct alignas(16) RRow { uint32_t msg, nwords, words_off, mp; };
-// partition slot: level 1 {MP, w0, kNone}, level 2 {MP, w0, w1}; mp == kEmpty: free
-struct alignas(32) PSlot { uint32_t mp, w0, w1, off, count, pad[3]; };
+// list entry: a copy of the row the walk tests, so that one coalesced 32-B
+// load per candidate suffices whatever the list order (words past the
+// first kLWords are read from rwords)
+constexpr uint32_t kLWords = 4;
+struct alignas(16) LEnt { uint32_t row, msg, nwords, words_off, w[kLWords]; };
+// list slot: kind kPair {MP, w0, w1} or kPos {MP, word, position}; mp == kEmpty: free
+struct alignas(32) PSlot { uint32_t mp, a, b, kind, off, count, pad[2]; };
+constexpr uint32_t kPair = 1, kPos = 2;
+constexpr uint32_t kMaxPos = 16;   // word positions with a position list
 struct alignas(16) XSlot { uint64_t fp; uint32_t row, state; };    // state 0 free, 1 live, 2 deleted
 struct alignas(8) MpList { uint32_t off, count; };
+static_assert(sizeof(LEnt) == 32, "");
 static_assert(sizeof(RRow) == 16 && sizeof(PSlot) == 32 && sizeof(XSlot) == 16 && sizeof(MpList) == 8, "");
 constexpr uint32_t kPSlotsPerBucket = 2;
-VMQG_HD uint64_t part_hash(uint32_t mp, uint32_t w0, uint32_t w1) {
-  return vmqg::mix64(vmqg::mix64(((uint64_t)mp << 32) | w0) ^ w1);
+VMQG_HD uint64_t part_hash(uint32_t mp, uint32_t a, uint32_t b, uint32_t kind) {
+  return vmqg::mix64(vmqg::mix64(((uint64_t)mp << 32) | a) ^ (((uint64_t)kind << 32) | b));
 }
 constexpr uint32_t kXLive = 1, kXTomb = 2;
 
@@ -57,9 +66,12 @@ static_assert(sizeof(RLayout) == 256, "");
 constexpr uint64_t kRLayoutMagic = 0x31726D7176ull;   // "vmqr1"
 
 // Launch interface (vmqr_kernels.hip).
-constexpr uint32_t kTileRows = 1024;   // rows of the flattened walk per look-back tile
+#ifndef VMQR_TILE_ROWS
+#define VMQR_TILE_ROWS 1024
+#endif
+constexpr uint32_t kTileRows = VMQR_TILE_ROWS;   // rows of the flattened walk per look-back tile
 struct RArgs {
-  const RRow* rows; const uint32_t* rwords; const uint32_t* lists;
+  const RRow* rows; const uint32_t* rwords; const LEnt* lists;
   const PSlot* ptab; uint64_t ptab_mask;          // bucket mask
   const MpList* mpl; uint32_t max_mp, pad0;
   const XSlot* exact; uint64_t exact_mask;        // slot mask
@@ -82,9 +94,10 @@ uint64_t retain_fp(uint32_t mp, const uint32_t* w, uint32_t L);
 
 struct RRowInfo {
   uint32_t mp = 0, msg = 0;
-  uint32_t part[3] = {vmqg::kNone, vmqg::kNone, vmqg::kNone};   // [0] = MP, [1], [2] partitions (kNone: L < 2)
   std::vector<uint32_t> words;
-  uint32_t pos[3] = {vmqg::kNone, vmqg::kNone, vmqg::kNone};    // positions in those lists
+  std::vector<uint32_t> part;        // its lists besides the MP list (pair, then positions)
+  std::vector<uint32_t> ppos;        // its position in each (kNone while not live)
+  uint32_t mpos = vmqg::kNone;       // position in the MP list
   uint64_t xslot = ~0ull;
   uint32_t words_off = vmqg::kNone;
   bool live = false;
@@ -106,11 +119,10 @@ struct RetainEngine {
   std::vector<RRowInfo> rows;
   FlatIndex key_index;                 // hash(mp, words) -> row (verified)
   uint64_t n_live = 0;
-  // partitions {MP, w0} (level 1) and {MP, w0, w1} (level 2)
-  FlatIndex part1_index;               // mp << 32 | w0 -> partition
-  FlatIndex part2_index;               // level-1 partition << 32 | w1 -> partition
+  // pair and position lists
+  FlatIndex part_index;                // part_hash -> list (verified)
   std::vector<RList> parts;
-  std::vector<uint32_t> part_mp, part_w0, part_w1;   // w1 = kNone at level 1
+  std::vector<uint32_t> part_mp, part_a, part_b, part_kind;
   std::vector<uint64_t> part_slot;
   std::vector<RList> mplists;          // per MP
   // mirror
@@ -158,15 +170,16 @@ struct RetainEngine {
   void insert(uint32_t mp, const uint32_t* w, uint32_t L, uint32_t msg);
   void erase(uint32_t mp, const uint32_t* w, uint32_t L);
   uint32_t find_row(uint32_t mp, const uint32_t* w, uint32_t L) const;
-  uint32_t part_of(uint32_t mp, uint32_t w0, uint32_t parent, uint32_t w1);
+  uint32_t part_of(uint32_t mp, uint32_t a, uint32_t b, uint32_t kind);
   template <class T> T* region(uint64_t off) { return reinterpret_cast<T*>(reinterpret_cast<uint8_t*>(mirror.data()) + off); }
   void touch(uint64_t off, uint64_t bytes);
-  // level 0: the MP list `id`; 1, 2: partition `id`
-  bool list_push(int level, uint32_t id, uint32_t row);
-  void list_remove(int level, uint32_t id, uint32_t row);
-  bool write_list_head(int level, uint32_t id);
-  RList& list_of(int level, uint32_t id) { return level ? parts[id] : mplists[id]; }
+  // which = -1: the row's MP list; else its list R.part[which]
+  bool list_push(uint32_t row, int which);
+  void list_remove(uint32_t row, int which);
+  bool write_list_head(bool part, uint32_t id);
   bool write_row(uint32_t r);
+  LEnt entry_of(uint32_t r) const;
+  void put_entry(uint64_t slot, uint32_t r);
   bool place_exact(uint32_t r);
   bool place_part(uint32_t p);
   RLayout plan_layout(uint32_t scale) const;

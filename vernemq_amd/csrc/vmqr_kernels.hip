@@ -3,20 +3,22 @@
 //
 // The reference answers a wildcard filter with a full ets:foldl over the
 // retained table, testing every entry with vmq_topic:match/2.  Here the same
-// test runs on the rows of ONE list: the filter's partition {MP, w0, w1}
-// when its first two words are literal, {MP, w0} when only the first is,
-// else (first word '+', or exactly '#') the MP's list — every other row of
-// the table fails the test anyway (other MP, or different leading words,
+// test runs on the rows of ONE list: the shortest of the lists the filter's
+// literal words select — {MP, w0, w1} for two literal leading words, or
+// {MP, w_k, k} for a literal word at position k — else the MP's list (a
+// filter of '+' and '#' only).  Every other row fails the test anyway (other
+// MP, or a different word where the filter has a literal,
 // vmq_topic.erl:55-65).  The rows of all filters' lists form one flat,
 // filter-major row space (filter f owns rows [rpfx[f], rpfx[f+1])):
 //   k_rt_plan   one thread per filter: has_wildcard/1 (:239-242); the exact
 //               ets:lookup (:93-98) as a fingerprint probe + word compare;
-//               else the list and its length;
+//               else the shortest selecting list and its length;
 //   scan        rows per filter -> rpfx (one launch, decoupled look-back);
 //   k_rt_walk   one wave per 1,024-row tile, tiles taken in ticket order:
 //               64 rows per step, one row per lane, each lane's filter found
 //               in an LDS window of rpfx; vmq_topic:match/2 of the row's
-//               topic against the filter; hits (message ids) compacted in
+//               topic (its 32-B list entry carries the first words) against
+//               the filter; hits (message ids) compacted in
 //               LDS with ballot + mbcnt; the tile's output base from a
 //               decoupled look-back over the tiles before it; then one
 //               contiguous store of the tile's hits and the offsets of the
@@ -90,23 +92,35 @@ __global__ __launch_bounds__(256) void k_rt_plan(RArgs a) {
         for (uint32_t i = 0; i < L && !unknown; i++) unknown = w[i] == vmqg::kUnknownWord;
         if (unknown) {
           cnt = 0;
-        } else if (w[0] == kPlus || (L == 1 && w[0] == kHash)) {
+        } else {
+          // the shortest list a literal word selects: {MP, w0, w1}, or
+          // {MP, w_k, k} for a literal at position k; else the MP list
+          // (first word '+' and no other literal, or exactly '#')
           const MpList m = a.mpl[F.mountpoint];
           off = m.off; cnt = m.count;
-        } else {
-          // literal prefix of one or two words: the rows whose first words
-          // are those (a literal filter word must equal the topic's,
-          // vmq_topic.erl:55-57; '#' after two literals still needs them)
-          const uint32_t w1 = L >= 2 && w[1] != kPlus && w[1] != kHash ? w[1] : kNone;
-          for (uint64_t b = part_hash(F.mountpoint, w[0], w1) & a.ptab_mask, n = 0; n <= a.ptab_mask;
-               b = (b + 1) & a.ptab_mask, n++) {
-            bool done = false;
-            for (uint32_t j = 0; j < kPSlotsPerBucket; j++) {
-              const PSlot s = a.ptab[b * kPSlotsPerBucket + j];
-              if (s.mp == kEmpty) { done = true; break; }
-              if (s.mp == F.mountpoint && s.w0 == w[0] && s.w1 == w1) { off = s.off; cnt = s.count; done = true; break; }
+          const uint32_t np = L < kMaxPos ? L : kMaxPos;
+          for (uint32_t k = 0; k <= np; k++) {
+            uint32_t ka, kb, kk;
+            if (k == 0) {   // the pair list
+              if (L < 2 || w[0] == kPlus || w[0] == kHash || w[1] == kPlus || w[1] == kHash) continue;
+              ka = w[0]; kb = w[1]; kk = kPair;
+            } else {
+              ka = w[k - 1]; kb = k - 1; kk = kPos;
+              if (ka == kPlus || ka == kHash) continue;
             }
-            if (done) break;
+            uint64_t o = 0, c = 0;   // a missing list: no retained topic has that word there
+            for (uint64_t b = part_hash(F.mountpoint, ka, kb, kk) & a.ptab_mask, n = 0; n <= a.ptab_mask;
+                 b = (b + 1) & a.ptab_mask, n++) {
+              bool done = false;
+              for (uint32_t j = 0; j < kPSlotsPerBucket; j++) {
+                const PSlot s = a.ptab[b * kPSlotsPerBucket + j];
+                if (s.mp == kEmpty) { done = true; break; }
+                if (s.mp == F.mountpoint && s.a == ka && s.b == kb && s.kind == kk) { o = s.off; c = s.count; done = true; break; }
+              }
+              if (done) break;
+            }
+            if (c < cnt) { off = o; cnt = c; }
+            if (cnt == 0) break;
           }
         }
       }
@@ -167,9 +181,12 @@ __global__ __launch_bounds__(256) void k_rt_scan(uint64_t* v, uint64_t n_host, c
 // ------------------------------------------------------------- walk pass
 constexpr uint32_t kGroups = kTileRows / 64;    // 64-row steps per tile
 constexpr uint32_t kWin = 64;                   // rpfx window (filters) per step
-constexpr uint32_t kU = 4;                      // 64-row steps in flight per lane
+#ifndef VMQR_U
+#define VMQR_U 4
+#endif
+constexpr uint32_t kU = VMQR_U;                 // 64-row steps in flight per lane
 constexpr uint32_t kClasses = 8;                // ticket counters (block classes)
-constexpr uint32_t kPre = 4;                    // topic / filter words preloaded per row
+constexpr uint32_t kPre = kLWords;              // topic / filter words in registers per row
 static_assert(kGroups % kU == 0, "");
 
 // vmq_topic:match/2 as topic_match, with the first kPre words of both
@@ -262,8 +279,8 @@ __global__ __launch_bounds__(256) void k_rt_walk(RArgs a) {
       win[lane] = wf <= a.nf ? a.rpfx[wf] : ~0ull;
       if (lane == 0) win[kWin] = f0 + kWin <= a.nf ? a.rpfx[f0 + kWin] : ~0ull;
       __builtin_amdgcn_wave_barrier();
-      uint32_t f[kU], id[kU];
-      uint64_t pc[kU];
+      uint32_t f[kU];
+      uint64_t pc[kU], off[kU];
       bool ok[kU];
 #pragma clang loop unroll(full)
       for (uint32_t u = 0; u < kU; u++) {
@@ -292,40 +309,43 @@ __global__ __launch_bounds__(256) void k_rt_walk(RArgs a) {
           start = win[lo];
         }
         pc[u] = a.plan[2 * (uint64_t)f[u] + 1];
-        const uint64_t off = a.plan[2 * (uint64_t)f[u]];
-        id[u] = (pc[u] & ~kCountMask) == kKindExact ? (uint32_t)off : a.lists[off + (gi - start)];
+        off[u] = a.plan[2 * (uint64_t)f[u]] + (gi - start);   // list slot (exact: the row)
       }
-      RRow r[kU];
+      // one 32-B list entry per candidate (exact filters: the looked-up row)
+      LEnt e[kU];
       vmqg_pub F[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
         if (!ok[u]) continue;
-        r[u] = a.rows[id[u]];
-        F[u] = a.filters[f[u]];
+        if ((pc[u] & ~kCountMask) == kKindExact) {
+          e[u].msg = a.rows[(uint32_t)off[u]].msg;
+        } else {
+          e[u] = a.lists[off[u]];
+          F[u] = a.filters[f[u]];
+        }
       }
-      // the first kPre words of topic and filter in registers
-      uint32_t tw[kU][kPre], fw[kU][kPre];
+      // the filter's first kPre words in registers (the topic's are in the entry)
+      uint32_t fw[kU][kPre];
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
+        const bool list = ok[u] && (pc[u] & ~kCountMask) != kKindExact;
 #pragma unroll
-        for (uint32_t k = 0; k < kPre; k++) {
-          tw[u][k] = ok[u] && k < r[u].nwords ? a.rwords[r[u].words_off + k] : 0u;
-          fw[u][k] = ok[u] && k < F[u].nwords ? a.words[F[u].word_off + k] : 0u;
-        }
+        for (uint32_t k = 0; k < kPre; k++) fw[u][k] = list && k < F[u].nwords ? a.words[F[u].word_off + k] : 0u;
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; u++) {
         bool hit = false;
         if (ok[u]) {
-          hit = (pc[u] & ~kCountMask) == kKindExact ||   // the plan already verified the key
-                (r[u].mp == F[u].mountpoint &&
-                 topic_match_pre(tw[u], fw[u], a.rwords + r[u].words_off, r[u].nwords, a.words + F[u].word_off,
-                                 F[u].nwords));
+          // the plan already verified an exact filter's key; list rows all
+          // belong to the filter's MP
+          hit = (pc[u] & ~kCountMask) == kKindExact ||
+                topic_match_pre(e[u].w, fw[u], a.rwords + e[u].words_off, e[u].nwords, a.words + F[u].word_off,
+                                F[u].nwords);
         }
         const uint64_t m = __ballot(hit);
         if (hit)
           hits[nh + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-              r[u].msg;
+              e[u].msg;
         if (lane == 0) mask[g + u] = m;
         nh += (uint32_t)__popcll(m);
       }
@@ -335,7 +355,11 @@ __global__ __launch_bounds__(256) void k_rt_walk(RArgs a) {
       __builtin_amdgcn_wave_barrier();
     }
     __builtin_amdgcn_wave_barrier();
-    const uint64_t pre = vmqg::lookback(a.lookback, a.lb_tag + 1, a.status, tile, nh);
+#ifdef VMQR_DIAG_SKIP_LOOKBACK   // A/B diagnostics only (tools/rt_ab.sh): wrong offsets
+    const uint64_t pre = 0;
+#else
+    const uint64_t pre = vmqg::lookback<32>(a.lookback, a.lb_tag + 1, a.status, tile, nh);
+#endif
     const uint64_t total = pre + nh;
     if (total > a.out_cap) {
       if (lane == 0) atomicOr(&a.status[1], kErrOut);

@@ -585,8 +585,9 @@ class RetainWorkload:
       20 % ``devices/{d}/+/{m}``         -> 1
       25 % ``devices/{d}/telemetry/{m}`` -> 1 (exact ets:lookup)
        5 % ``devices/{d'}/telemetry/#`` with d' >= n_dev (no retained topic) -> 0
-      plus ``n_heavy`` x ``devices/+/telemetry/{m}`` -> n_dev each (a scan of
-      the whole ``devices`` partition).
+      plus ``n_heavy`` x ``devices/+/telemetry/{m}`` -> n_dev each (the
+      reference scans the whole table for it; the product walks the position
+      list {m, 3}).
     Columns: word strings in ``vocab``; topics/filters as (n, 4) index arrays.
     """
 
@@ -630,11 +631,12 @@ class RetainWorkload:
         self.matches = np.empty(n_filters, dtype=np.int64)
         self.matches[is_heavy] = n_dev
         self.matches[~is_heavy] = per
-        # rows each filter's list holds (what the walk visits): level-2 list
-        # {devices, d} = 16 rows; '+' second word -> level-1 {devices} = all;
-        # exact -> 1 row (the plan's probe); unknown word -> none
+        # rows of the list each filter walks (the shortest its literal words
+        # select): pair list {devices, d} = 16 rows; devices/+/telemetry/{m}
+        # -> position list {m, 3} = n_dev rows; exact -> 1 row (the plan's
+        # probe); unknown word -> none
         self.rows_visited = np.empty(n_filters, dtype=np.int64)
-        self.rows_visited[is_heavy] = self.n_topics
+        self.rows_visited[is_heavy] = n_dev
         self.rows_visited[~is_heavy] = np.where(wild, 16, np.where(plus, 16, np.where(unk, 0, 1)))
         self.exact = np.zeros(n_filters, dtype=bool)
         self.exact[~is_heavy] = (kind >= 70) & (kind < 95)
@@ -676,13 +678,14 @@ class RetainWorkload:
 
     def algorithmic_bytes(self, part: str = "walk") -> int:
         """Bytes one match batch must move, per the walk over each filter's
-        list: per visited row its 4-B list entry + 16-B row + 16-B topic
-        words; per filter its 16-B descriptor + 16-B words + 8-B offset; per
-        match one 4-B message id written.  part "walk": the count/emit walk
-        (one pass); "batch": plan + both passes."""
+        list: per visited candidate its 32-B list entry (row id, message id,
+        length, the topic's first 4 words); per filter its 16-B descriptor +
+        16-B words + 8-B offset; per match one 4-B message id written.
+        part "walk": the one-pass walk kernel; "batch": plus the plan (per
+        filter its descriptor and words again, the plan entry and row count
+        written: 56 B)."""
         rows = int(self.rows_visited.sum())
-        per_filter = 16 + 16 + 8
-        walk = 36 * rows + 4 * int(self.matches.sum()) + per_filter * self.n_filters
+        walk = 32 * rows + 4 * int(self.matches.sum()) + 40 * self.n_filters
         if part == "walk":
             return walk
-        return walk + 36 * rows + per_filter * self.n_filters
+        return walk + 56 * self.n_filters
