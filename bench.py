@@ -69,10 +69,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP events (profiling runs)")
-    ap.add_argument("--config", default="C", choices=["A", "B", "C", "D", "E", "R1", "R2", "RT"],
+    ap.add_argument("--config", default="C", choices=["A", "B", "C", "D", "E", "R1", "R2", "RT", "AC"],
                     help="C: headline (1M subs); D: 10M subs with $share groups under 1%%/s churn; "
                          "A, B, E, R1, R2: the other SURVEY §8d shapes (secondary lines); "
-                         "RT: retained-message match_fold (§8f rank 3)")
+                         "RT: retained-message match_fold (§8f rank 3); AC: vmq_acl checks (§8f rank 4)")
+    ap.add_argument("--ac-requests", type=int, default=1 << 20, help="AC: ACL checks per step")
     ap.add_argument("--rt-devices", type=int, default=62_500, help="RT: devices x 16 retained topics")
     ap.add_argument("--rt-filters", type=int, default=1 << 18, help="RT: subscription filters per step")
     ap.add_argument("--rt-heavy", type=int, default=16, help="RT: devices/+/telemetry/{m} filters per step")
@@ -87,6 +88,8 @@ def main():
         return bench_d(args)
     if args.config == "RT":
         return bench_retain(args)
+    if args.config == "AC":
+        return bench_acl(args)
     if args.config != "C":
         return bench_other(args)
 
@@ -529,6 +532,91 @@ def bench_retain(args):
                                     "40 B per filter (workloads.RetainWorkload.algorithmic_bytes)"},
         "cpu_baseline": cpu, "load_s": load_s, "arena_bytes": st["device_bytes"],
         "partitions": st["partitions"]}), flush=True)
+
+
+def bench_acl(args):
+    """ACL checks (vmq_acl:check/4 via auth_on_publish / auth_on_subscribe,
+    SURVEY §8(f) rank 4): 2^20 checks per step of config C's device fleet
+    against an ACL of 64 `all` rules, 15,625 users x 4 rules and 8 patterns
+    (vernemq_amd.workloads.AclWorkload).  Prints one JSON line with the
+    check kernel's roofline and the CPU restatement timed on a sample."""
+    import torch
+    from vernemq_amd import workloads as W
+    from vernemq_amd.acl import AclGpu
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    t0 = time.time()
+    w = W.AclWorkload(n_reqs=args.ac_requests)
+    acl = AclGpu(device=0)
+    lines = w.lines()
+    acl.load_from_list(lines)
+    reqs, words = w.arrays(acl)
+    load_s = time.time() - t0
+    log("AC: ACL of %d lines loaded in %.1fs, %s" % (len(lines), load_s, acl.stats_raw()))
+    n = len(reqs)
+    d_r = torch.from_numpy(reqs.view(np.uint32).reshape(-1).copy()).to(dev)
+    d_w = torch.from_numpy(words.astype(np.int32)).to(dev)
+    d_o = torch.zeros(n, dtype=torch.uint8, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+    step = lambda: acl.check_device(d_r.data_ptr(), n, d_w.data_ptr(), d_o.data_ptr(), sp)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    rc = acl.check_status(sp)
+    if rc != 0:
+        raise RuntimeError("acl check status %d after warmup" % rc)
+    verified = bool(np.array_equal(d_o.cpu().numpy(), w.expect))   # the workload's known answer
+    if not verified:
+        raise RuntimeError("ACL verdicts differ from the workload's known answer")
+    acl.set_timing(not args.no_timing)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    rc = acl.check_status(sp)
+    if rc != 0:
+        raise RuntimeError("acl check status %d in timed region" % rc)
+    check_ns, nl = acl.kernel_times()
+    alg = w.algorithmic_bytes()
+    achieved = alg / check_ns if check_ns else None
+
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import acl_oracle as AO   # the CPU restatement: baseline only
+        orc = AO.AclOracle()
+        orc.load_from_list(lines)
+        S = 20_000
+        sample = [w.request(i) for i in range(S)]
+        ns1, _ = orc.check_timed(sample, 1)
+        reps = max(1, int(math.ceil(args.cpu_seconds * 1e9 / max(ns1, 1))))
+        ns, _ = orc.check_timed(sample, reps)
+        cpu = {"value": S * reps / (ns / 1e9), "unit": "checks/s", "cores": 1, "kind": "port",
+               "sample": "first %d requests of the AC batch x %d reps (%.1fs), 1 thread, oracle/vmq_acl_oracle.cpp "
+                         "(C++ restatement of vmq_acl:check/4: all -> user -> pattern lists, vmq_topic:match/2 per "
+                         "rule; not BEAM); host %s" % (S, reps, ns / 1e9, cpu_model())}
+        log("AC cpu baseline: %.0f checks/s" % cpu["value"])
+
+    st = acl.stats_raw()
+    print(json.dumps({
+        "metric": "ACL checks/sec (vmq_acl auth_on_publish / auth_on_subscribe)",
+        "value": n * args.steps / el, "unit": "checks/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic: vernemq_amd.workloads.AclWorkload (splitmix64 seed 0xAC)",
+        "config": {"workload": "AC: %d checks/step (80%% allowed publishes via pattern %%c, 10%% denied, 5%% "
+                               "subscribes, 5%% user-table publishes); ACL %d rules, %d users"
+                               % (n, st["rules"], st["users"])},
+        "verified_counts": verified,
+        "kernel_us": {"check": check_ns / 1e3, "launches": nl},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS if achieved else None,
+                     "traffic": load_pmc_traffic("k_acl_check", "pmc_ac.json"),
+                     "kernel": "k_acl_check", "algorithmic_bytes_per_launch": alg,
+                     "bytes_model": "24-B request + 16-B topic words read, 1-B verdict written per check "
+                                    "(the rule tables are L2-resident; workloads.AclWorkload.algorithmic_bytes)"},
+        "cpu_baseline": cpu, "load_s": load_s, "arena_bytes": st["device_bytes"]}), flush=True)
 
 
 if __name__ == "__main__":

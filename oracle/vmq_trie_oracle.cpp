@@ -34,7 +34,11 @@
 #include <unordered_map>
 #include <vector>
 
+#include "vmq_topic_oracle.h"
+
 namespace {
+
+using namespace vmq_topic_oracle;   // validate_topic/2 and friends
 
 using Words = std::vector<std::string>;
 
@@ -99,63 +103,6 @@ bool contains_wildcard(const Words& t) {
     if (t[i] == "#" && i + 1 == t.size()) return true;
   }
   return false;
-}
-
-// validate_topic/2  vmq_topic.erl:82-133.  Error codes mirror the atoms.
-enum { V_OK = 0, V_EMPTY = 1, V_TOO_LONG = 2, V_PLUS_PUB = 3, V_HASH_PUB = 4,
-       V_PLUS_WORD = 5, V_HASH_WORD = 6, V_BAD_SHARED = 7 };
-
-int validate_publish(const std::string& topic, Words& out) {
-  // validate_publish_topic/3  vmq_topic.erl:97-112
-  size_t seg = 0;
-  out.clear();
-  for (;;) {
-    std::string rest = topic.substr(seg);
-    if (rest.compare(0, 2, "+/") == 0 || rest == "+") return V_PLUS_PUB;  // :97-98
-    if (rest == "#") return V_HASH_PUB;                                     // :99
-    size_t L = 0;
-    for (;;) {                                                              // :100-111
-      if (L < rest.size() && rest[L] == '/') { out.push_back(rest.substr(0, L)); seg += L + 1; break; }
-      if (L == rest.size()) { out.push_back(rest); return V_OK; }
-      if (rest[L] == '+') return V_PLUS_WORD;
-      if (rest[L] == '#') return V_HASH_WORD;
-      L++;
-    }
-  }
-}
-
-int validate_shared(const Words& t) {
-  // validate_shared_subscription/1  vmq_topic.erl:131-133
-  if (!t.empty() && t[0] == "$share") return t.size() >= 3 ? V_OK : V_BAD_SHARED;
-  return V_OK;
-}
-
-int validate_subscribe(const std::string& topic, Words& out) {
-  // validate_subscribe_topic/3  vmq_topic.erl:114-129
-  size_t seg = 0;
-  out.clear();
-  for (;;) {
-    std::string rest = topic.substr(seg);
-    if (rest.compare(0, 2, "+/") == 0) { out.push_back("+"); seg += 2; continue; }  // :114
-    if (rest == "+" || rest == "#") { out.push_back(rest); return validate_shared(out); }  // :115-116
-    size_t L = 0;
-    bool next = false;
-    for (;;) {
-      if (L < rest.size() && rest[L] == '/') { out.push_back(rest.substr(0, L)); seg += L + 1; next = true; break; }
-      if (L == rest.size()) { out.push_back(rest); return validate_shared(out); }
-      if (rest[L] == '+') return V_PLUS_WORD;
-      if (rest[L] == '#') return V_HASH_WORD;
-      L++;
-    }
-    if (!next) break;
-  }
-  return V_OK;
-}
-
-int validate_topic(int type, const std::string& topic, Words& out) {
-  if (topic.empty()) return V_EMPTY;                 // vmq_topic.erl:82-83
-  if (topic.size() > 65536) return V_TOO_LONG;       // :84-85 (MAX_LEN :45)
-  return type == 0 ? validate_publish(topic, out) : validate_subscribe(topic, out);
 }
 
 // match/2  vmq_topic.erl:53-65 (naive filter matcher, used as a cross-check)

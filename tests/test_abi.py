@@ -1,4 +1,4 @@
-"""CPU checks of the C ABI boundary (include/vmqg.h, include/vmqr.h): the library loads,
+"""CPU checks of the C ABI boundary (include/vmqg.h, vmqr.h, vmqa.h): the library loads,
 exports every declared entry point, its structs have the header's layout,
 and a host-only context fails loudly on match calls (no CPU fallback)."""
 import ctypes
@@ -13,14 +13,14 @@ from vernemq_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "vmqg.h")
-HEADERS = [HEADER, os.path.join(ROOT, "include", "vmqr.h")]
+HEADERS = [HEADER, os.path.join(ROOT, "include", "vmqr.h"), os.path.join(ROOT, "include", "vmqa.h")]
 
 
 def declared_functions():
     out = set()
     for h in HEADERS:
         src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
-        out |= set(re.findall(r"^\s*[\w\s\*]+?\b(vmq[gr]_\w+)\s*\(", src, flags=re.M))
+        out |= set(re.findall(r"^\s*[\w\s\*]+?\b(vmq[gra]_\w+)\s*\(", src, flags=re.M))
     return sorted(out)
 
 
@@ -50,6 +50,36 @@ def test_struct_layouts_match_header(tmp_path):
     assert got == want
     from vernemq_amd.reg_view import EMIT_DTYPE, OP_DTYPE, PUB_DTYPE
     assert (OP_DTYPE.itemsize, PUB_DTYPE.itemsize, EMIT_DTYPE.itemsize) == (got[1], got[2], got[3])
+
+
+def test_acl_struct_layouts_match_header(tmp_path):
+    prog = tmp_path / "sza.c"
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "vmqa.h"\n'
+                    'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(vmqa_config), sizeof(vmqa_rule),'
+                    ' sizeof(vmqa_req), sizeof(vmqa_stats_t), offsetof(vmqa_req, nwords));return 0;}\n')
+    exe = tmp_path / "sza"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(prog),
+                    "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    from vernemq_amd.acl import REQ_DTYPE, RULE_DTYPE
+    assert got == [ctypes.sizeof(_lib.AConfig), RULE_DTYPE.itemsize, REQ_DTYPE.itemsize, ctypes.sizeof(_lib.AStats),
+                   REQ_DTYPE.fields["nwords"][1]]
+
+
+def test_acl_host_context_refuses_checks():
+    """device = -1: tables only; a check fails loudly (no CPU fallback)."""
+    cfg = _lib.AConfig()
+    cfg.device = -1
+    err = ctypes.c_int(0)
+    L = _lib.lib()
+    h = L.vmqa_create(ctypes.byref(cfg), ctypes.byref(err))
+    assert h and err.value == 0
+    req = np.zeros(6, dtype=np.uint32)
+    req[0], req[5] = 2, 1
+    words = np.zeros(1, dtype=np.uint32)
+    out = np.zeros(1, dtype=np.uint8)
+    assert L.vmqa_check_batch(h, req.ctypes.data, 1, words.ctypes.data, 1, out.ctypes.data) == _lib.E_DEVICE
+    L.vmqa_destroy(h)
 
 
 def test_retain_struct_layouts_match_header(tmp_path):

@@ -14,13 +14,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "libvmqgpu.so")
 HEADER = os.path.join(ROOT, "include", "vmqg.h")
-HEADERS = [HEADER, os.path.join(ROOT, "include", "vmqr.h")]
+HEADERS = [HEADER, os.path.join(ROOT, "include", "vmqr.h"), os.path.join(ROOT, "include", "vmqa.h")]
 SOURCES = [os.path.join(HERE, "csrc", f) for f in
            ("vmqg_engine.cpp", "vmqg_abi.cpp", "vmqg_kernels.hip",
-            "vmqr_engine.cpp", "vmqr_abi.cpp", "vmqr_kernels.hip")]
+            "vmqr_engine.cpp", "vmqr_abi.cpp", "vmqr_kernels.hip",
+            "vmqa_engine.cpp", "vmqa_abi.cpp", "vmqa_kernels.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in
                   ("vmqg_common.h", "vmqg_engine.h", "vmqg_kernels.h", "vmqg_lookback.h",
-                   "vmqr_engine.h")] + HEADERS
+                   "vmqr_engine.h", "vmqa_engine.h")] + HEADERS
 
 # ---- status codes / constants (vmqg.h)
 OK, E_INVAL, E_OVERFLOW, E_NOMEM, E_DEVICE, E_FRONTIER, E_LIMIT, E_STATE = 0, -1, -2, -3, -4, -5, -6, -7
@@ -87,7 +88,22 @@ class RStats(ctypes.Structure):
 ROP_INSERT, ROP_DELETE = 1, 2
 
 
-# (name, restype, argtypes) for every entry point declared in include/vmqg.h and include/vmqr.h
+class AConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+
+
+class AStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("rules", "users", "device_bytes", "loads", "words")]
+
+
+# vmqa.h constants
+A_READ, A_WRITE = 1, 2
+A_TABLE_ALL, A_TABLE_USER, A_TABLE_PATTERN = 0, 1, 2
+A_WORD_USER, A_WORD_CLIENT, A_WORD_MOUNTPOINT = 3, 4, 5
+A_NO_USER, A_EPHEMERAL = 0xFFFFFFFE, 0x80000000
+
+
+# (name, restype, argtypes) for every entry point declared in include/vmqg.h, vmqr.h and vmqa.h
 _P = ctypes.c_void_p
 _U32, _U64, _SZ = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 SIGNATURES = [
@@ -123,6 +139,17 @@ SIGNATURES = [
     ("vmqr_stats", ctypes.c_int, [_P, ctypes.POINTER(RStats)]),
     ("vmqr_dump", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_SZ)]),
     ("vmqr_set_option", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int64]),
+    # ACL checker (include/vmqa.h)
+    ("vmqa_create", _P, [ctypes.POINTER(AConfig), ctypes.POINTER(ctypes.c_int)]),
+    ("vmqa_destroy", None, [_P]),
+    ("vmqa_intern_words", ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
+    ("vmqa_load", ctypes.c_int, [_P, _P, _SZ, _P, _SZ]),
+    ("vmqa_check_batch", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P]),
+    ("vmqa_check_device", ctypes.c_int, [_P, _P, _U32, _P, _P, _P]),
+    ("vmqa_check_status", ctypes.c_int, [_P, _P]),
+    ("vmqa_stats", ctypes.c_int, [_P, ctypes.POINTER(AStats)]),
+    ("vmqa_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
+    ("vmqa_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
     ("vmqr_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
     ("vmqr_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),

@@ -689,3 +689,90 @@ class RetainWorkload:
         if part == "walk":
             return walk
         return walk + 56 * self.n_filters
+
+
+class AclWorkload:
+    """ACL-check workload AC: config C's device
+    fleet publishing through vmq_acl's auth_on_publish / auth_on_subscribe
+    (apps/vmq_acl/src/vmq_acl.erl:78-93).
+
+    ACL (``lines()``): 32 ``topic read sys/{k}/#`` + 32 ``topic write
+    public/{k}/+`` (the `all` tables, never matching a device topic);
+    ``n_users`` users ``u{k}`` with ``topic write devices/{4k+j}/cmd/#``
+    (j < 4); patterns ``pattern write devices/%c/telemetry/+``, ``pattern
+    read devices/%c/cmd/#``, ``pattern write %m/%u/#`` and 5 ``pattern write
+    tenants/%m/%c/x{j}``.
+    Requests (splitmix64 seed 0xAC), client id = the device id string d,
+    user ``u{d // 4}``:
+      80 % write devices/{d}/telemetry/{m}          -> allowed (pattern %c)
+      10 % write devices/{d}/telemetry/{m}, client d+1 -> denied (every list walked)
+       5 % read  devices/{d}/cmd/#                  -> allowed (pattern read %c)
+       5 % write devices/{d}/cmd/x                  -> allowed (user table)
+    """
+
+    def __init__(self, n_dev: int = 62_500, n_reqs: int = 1 << 20, seed: int = 0xAC):
+        self.n_dev, self.n_reqs = n_dev, n_reqs
+        self.n_users = (n_dev + 3) // 4
+        r = SplitMix(seed)
+        kind = r.ints(n_reqs, 100)
+        self.d = r.ints(n_reqs, n_dev)
+        self.m = r.ints(n_reqs, 16)
+        self.kind = np.where(kind < 80, 0, np.where(kind < 90, 1, np.where(kind < 95, 2, 3)))
+        self.expect = (self.kind != 1).astype(np.uint8)
+
+    def lines(self):
+        out = [b"# workload AC\n"]
+        out += [b"topic read sys/%d/#\n" % k for k in range(32)]
+        out += [b"topic write public/%d/+\n" % k for k in range(32)]
+        for k in range(self.n_users):
+            out.append(b"user u%d\n" % k)
+            out += [b"topic write devices/%d/cmd/#\n" % (4 * k + j) for j in range(4)]
+        out += [b"pattern write devices/%c/telemetry/+\n", b"pattern read devices/%c/cmd/#\n",
+                b"pattern write %m/%u/#\n"]
+        out += [b"pattern write tenants/%%m/%%c/x%d\n" % j for j in range(5)]
+        return out
+
+    def vocab(self):
+        return [b"devices", b"telemetry", b"cmd", b"x", b"#", b""] + [b"m%d" % m for m in range(16)] + \
+               [b"%d" % d for d in range(self.n_dev + 1)] + [b"u%d" % k for k in range(self.n_users)]
+
+    def request(self, i: int):
+        """Request i as (type, topic words, user, mountpoint, client id)."""
+        d, m, k = int(self.d[i]), int(self.m[i]), int(self.kind[i])
+        user = b"u%d" % (d // 4)
+        if k in (0, 1):
+            return ("write", (b"devices", b"%d" % d, b"telemetry", b"m%d" % m), user, "",
+                    b"%d" % (d + k))
+        if k == 2:
+            return ("read", (b"devices", b"%d" % d, b"cmd", b"#"), user, "", b"%d" % d)
+        return ("write", (b"devices", b"%d" % d, b"cmd", b"x"), user, "", b"%d" % d)
+
+    def arrays(self, acl):
+        """(REQ_DTYPE requests, word ids) for the whole batch, vectorised;
+        `acl` interns the vocabulary (real words of the workload)."""
+        from .acl import REQ_DTYPE
+        v = self.vocab()
+        ids = acl.intern_words(v, create=True).astype(np.int64)
+        DEV, TEL, CMD, X, HASH, EMPTY = ids[:6]
+        M0 = 6
+        D0 = M0 + 16
+        U0 = D0 + self.n_dev + 1
+        n = self.n_reqs
+        reqs = np.zeros(n, dtype=REQ_DTYPE)
+        reqs["type"] = np.where(self.kind == 2, _lib.A_READ, _lib.A_WRITE)
+        reqs["user"] = ids[U0 + self.d // 4]
+        reqs["client"] = ids[D0 + self.d + (self.kind == 1)]
+        reqs["mountpoint"] = EMPTY
+        reqs["word_off"] = 4 * np.arange(n)
+        reqs["nwords"] = 4
+        w = np.empty((n, 4), dtype=np.int64)
+        w[:, 0] = DEV
+        w[:, 1] = ids[D0 + self.d]
+        w[:, 2] = np.where(self.kind >= 2, CMD, TEL)
+        w[:, 3] = np.where(self.kind == 2, HASH, np.where(self.kind == 3, X, ids[M0 + self.m]))
+        return reqs, w.reshape(-1).astype(np.uint32)
+
+    def algorithmic_bytes(self) -> int:
+        """Per request its 24-B descriptor, 16-B topic words read and a 1-B
+        verdict written (the rules are an L2-resident table shared by all)."""
+        return 41 * self.n_reqs
