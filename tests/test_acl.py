@@ -175,3 +175,26 @@ def test_acl_random_parity(seed):
         got, want = prod.check_batch(reqs), orc.check_batch(reqs)
         bad = [i for i in range(len(reqs)) if got[i] != want[i]]
         assert not bad, (seed, k, reqs[bad[0]], got[bad[0]], want[bad[0]])
+
+
+@pytest.mark.gpu
+def test_acl_large_tables_skip_lds_staging():
+    """All / pattern tables past the 48-KiB LDS budget (the kernel reads them
+    from global memory) and a 2,000-rule user: verdicts equal the oracle's."""
+    lines = ["topic read r/%d/+/x\n" % k for k in range(3000)] + ["topic write w/%d/#\n" % k for k in range(2000)]
+    lines += ["pattern read p/%%c/%d\n" % k for k in range(500)] + ["user big\n"]
+    lines += ["topic b/%d/+\n" % k for k in range(2000)]
+    prod, orc = ProductDriver(), OracleDriver()
+    assert prod.load(lines) and orc.load(lines)
+    st = prod.a.stats_raw()
+    assert st["rules"] == 3000 + 2000 + 500 + 4000
+    rnd = random.Random(3)
+    reqs = []
+    for _ in range(3000):
+        k = rnd.randrange(3500)
+        reqs.append(rnd.choice([("read", (b"r", b"%d" % k, b"q", b"x"), None, "", b"c"),
+                                ("write", (b"w", b"%d" % k, b"z"), b"big", "", b"c"),
+                                ("read", (b"p", b"c%d" % (k % 3), b"%d" % k), None, "", b"c%d" % (k % 2)),
+                                ("read", (b"b", b"%d" % k, b"y"), rnd.choice([b"big", b"small"]), "", b"c")]))
+    got, want = prod.check_batch(reqs), orc.check_batch(reqs)
+    assert got == want and 0 < sum(got) < len(got)

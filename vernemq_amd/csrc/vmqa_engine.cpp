@@ -89,28 +89,42 @@ int AclEngine::load(const vmqa_rule* rules, size_t n, const uint32_t* words, siz
     else if (table == VMQA_TABLE_PATTERN) fixed[2 + type].push_back(id);
     else per_user[{std::get<2>(k), type}].push_back(id);
   }
+  // the fixed lists, packed: per rule {nwords, word index}, then the words
+  std::vector<uint32_t> fx;
+  uint32_t nfixed = 0;
+  for (auto& f : fixed) nfixed += (uint32_t)f.size();
+  fx.resize(2 * (size_t)nfixed);
+  uint32_t ri = 0;
+  std::vector<AList> fheads(4);
+  for (int h = 0; h < 4; h++) {
+    fheads[h] = AList{ri, (uint32_t)fixed[h].size()};
+    for (uint32_t id : fixed[h]) {
+      fx[2 * ri] = rl[id].nwords;
+      fx[2 * ri + 1] = (uint32_t)fx.size();
+      fx.insert(fx.end(), rw.begin() + rl[id].words_off, rw.begin() + rl[id].words_off + rl[id].nwords);
+      ri++;
+    }
+  }
   uint64_t nlist = 0;
-  for (auto& f : fixed) nlist += f.size();
   for (auto& u : per_user) nlist += u.second.size();
   users_slots = next_pow2(std::max<uint64_t>(64, per_user.size() * 4));   // load <= 1/4
   uint64_t o = 0;
   rules_off = o;  o = align256(o + std::max<size_t>(1, rl.size()) * sizeof(ARule));
   rwords_off = o; o = align256(o + std::max<size_t>(1, rw.size()) * 4);
   lists_off = o;  o = align256(o + std::max<uint64_t>(1, nlist) * 4);
+  fixed_off = o;  o = align256(o + std::max<size_t>(1, fx.size()) * 4);
   heads_off = o;  o = align256(o + 4 * sizeof(AList));
   users_off = o;  o = align256(o + users_slots * sizeof(USlot));
+  fixed_words = fx.size();
   image.assign(o, 0);
   memcpy(image.data() + rules_off, rl.data(), rl.size() * sizeof(ARule));
   memcpy(image.data() + rwords_off, rw.data(), rw.size() * 4);
+  memcpy(image.data() + fixed_off, fx.data(), fx.size() * 4);
+  memcpy(image.data() + heads_off, fheads.data(), 4 * sizeof(AList));
   uint32_t* lists = reinterpret_cast<uint32_t*>(image.data() + lists_off);
-  AList* heads = reinterpret_cast<AList*>(image.data() + heads_off);
   USlot* slots = reinterpret_cast<USlot*>(image.data() + users_off);
   for (uint64_t i = 0; i < users_slots; i++) slots[i] = USlot{kEmpty, 0, 0, 0};
   uint32_t top = 0;
-  for (int h = 0; h < 4; h++) {
-    heads[h] = AList{top, (uint32_t)fixed[h].size()};
-    for (uint32_t id : fixed[h]) lists[top++] = id;
-  }
   std::set<uint32_t> users;
   for (auto& u : per_user) {
     const uint64_t mask = users_slots - 1;
@@ -156,6 +170,8 @@ int AclEngine::check_device(const vmqa_req* d_reqs, uint32_t n, const uint32_t* 
   a.rwords = reinterpret_cast<const uint32_t*>(d_arena + rwords_off);
   a.lists = reinterpret_cast<const uint32_t*>(d_arena + lists_off);
   a.heads = reinterpret_cast<const AList*>(d_arena + heads_off);
+  a.fixed = reinterpret_cast<const uint32_t*>(d_arena + fixed_off);
+  a.fixed_words = (uint32_t)fixed_words;
   a.users = reinterpret_cast<const USlot*>(d_arena + users_off);
   a.users_mask = users_slots - 1;
   a.reqs = d_reqs; a.words = d_words; a.n = n; a.out = d_out; a.status = d_status;

@@ -7,7 +7,10 @@
 //   rwords : u32 pool of the rows' topic words
 //   lists  : u32 row ids: all-read, all-write, pattern-read, pattern-write,
 //            then one list per {user, type}
-//   heads  : 4 x AList {off, count} for the all / pattern lists
+//   fixed  : the all / pattern rules of both types packed for LDS staging:
+//            per rule {nwords, word index into `fixed`}, then their words
+//   heads  : 4 x AList {off, count} (rule indexes into `fixed`) for the
+//            all-read, all-write, pattern-read, pattern-write lists
 //   users  : open-addressed {user, type} -> AList (16-B slots), for
 //            check_user_acl's ets:match on {{User, '$1'}, '_'} (:194-197)
 #pragma once
@@ -36,11 +39,13 @@ VMQG_HD uint64_t user_hash(uint32_t user, uint32_t type) {
 struct AArgs {
   const ARule* rules; const uint32_t* rwords; const uint32_t* lists;
   const AList* heads;                  // [0] all-read [1] all-write [2] pattern-read [3] pattern-write
+  const uint32_t* fixed; uint32_t fixed_words, pad1;   // the lists heads[] index (see above)
   const USlot* users; uint64_t users_mask;
   const vmqa_req* reqs; const uint32_t* words; uint32_t n, pad0;
   uint8_t* out;
   uint32_t* status;                    // [1] error bits
 };
+constexpr uint32_t kFixedLdsWords = 12288;   // 48 KiB: the fixed lists are staged in LDS up to this size
 hipError_t launch_acl_check(const AArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
 
 struct AclEngine {
@@ -52,6 +57,7 @@ struct AclEngine {
   // the image (host copy) and its layout
   std::vector<uint8_t> image;
   uint64_t rules_off = 0, rwords_off = 0, lists_off = 0, heads_off = 0, users_off = 0, users_slots = 0;
+  uint64_t fixed_off = 0, fixed_words = 0;
   uint64_t n_rules = 0, n_users = 0, loads = 0;
   // device
   hipStream_t stream = nullptr;
