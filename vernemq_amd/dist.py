@@ -140,10 +140,14 @@ def apply_patches_host(image: np.ndarray, patches: np.ndarray):
 
 
 def hip_memcpy_d2d(dst: int, src: int, n: int):
-    """Device-to-device copy through the process's (torch's) HIP runtime."""
+    """Device-to-device copy through the process's one HIP runtime: the
+    hipMemcpy libvmqgpu itself resolves (its DT_NEEDED libamdhip64.so.7,
+    torch's copy once torch is imported) — never a second runtime loaded by
+    a bare "libamdhip64.so"."""
     import ctypes
-    lib = ctypes.CDLL("libamdhip64.so")
-    lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    rc = lib.hipMemcpy(dst, src, n, 3)
+    hip_memcpy = _lib.lib().hipMemcpy   # dlsym through libvmqgpu's dependencies
+    hip_memcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip_memcpy.restype = ctypes.c_int
+    rc = hip_memcpy(dst, src, n, 3)
     if rc != 0:
         raise _lib.VmqgError(_lib.E_DEVICE, "hipMemcpy D2D (%d)" % rc)
