@@ -48,7 +48,8 @@ constexpr uint32_t kNodeEmits = kNodeRec | kNodeTopic | kNodeFilter;
 // child flags cached in EdgeSlot.flags
 constexpr uint32_t kHasHash = 1u;   // the child has a '#' edge
 constexpr uint32_t kHasPlus = 2u;   // the child has a '+' edge
-constexpr uint32_t kHasAll = kHasHash | kHasPlus;
+constexpr uint32_t kHasWord = 4u;   // the child has an edge of a literal word
+constexpr uint32_t kHasAll = kHasHash | kHasPlus | kHasWord;
 
 struct alignas(16) EdgeSlot { uint32_t parent, word, child, flags; };
 // meta = flags | nkeys << 8; nkeys == 1: {off0, cnt0} inline; nkeys >= 2: key = keylist offset

@@ -166,8 +166,9 @@ void Engine::touch(uint64_t off, uint64_t bytes) {
   }
 }
 
-// `node` gained or lost a '#' / '+' edge: refresh the child flags cached in
-// its incoming slot (they let the walk skip probes that must miss).
+// `node` gained or lost a '#' / '+' edge or its first / last literal edge:
+// refresh the child flags cached in its incoming slot (they let the walk
+// skip probes that must miss).
 void Engine::refresh_incoming_flags(uint32_t node) {
   const PathInfo& P = paths[node];
   if (P.parent == kNone || P.in_slot == ~0ull) return;   // roots are always probed for both
@@ -199,6 +200,9 @@ void Engine::edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
         if (word == kHash || word == kPlus) {
           paths[parent].eflags |= word == kHash ? kHasHash : kHasPlus;
           refresh_incoming_flags(parent);
+        } else if (paths[parent].nlit++ == 0) {
+          paths[parent].eflags |= kHasWord;
+          refresh_incoming_flags(parent);
         }
         return;
       }
@@ -216,6 +220,9 @@ void Engine::edge_erase(uint32_t parent, uint32_t word, uint32_t child) {
   touch(lay.edge_off + si * sizeof(EdgeSlot), sizeof(EdgeSlot));
   if (word == kHash || word == kPlus) {
     paths[parent].eflags &= ~(word == kHash ? kHasHash : kHasPlus);
+    refresh_incoming_flags(parent);
+  } else if (--paths[parent].nlit == 0) {
+    paths[parent].eflags &= ~kHasWord;
     refresh_incoming_flags(parent);
   }
 }
@@ -286,7 +293,7 @@ void Engine::rebuild(uint64_t extra_edges, bool compact) {
     full_image = true;
     exact_live = exact_tomb = 0;
     rec_top = rec_garbage = kl_top = kl_garbage = xw_top = xw_garbage = 0;
-    for (auto& p : paths) p.in_slot = ~0ull;
+    for (auto& p : paths) { p.in_slot = ~0ull; p.nlit = 0; p.eflags &= ~kHasWord; }   // re-counted below
     for (auto& e : live) edge_insert(e.parent, e.word, e.child);
     for (auto& k : keys) { k.off = 0; k.cap = 0; k.dirty_pos.clear(); }
     for (auto& t : topics) { t.slot = ~0ull; t.words_off = kNone; }

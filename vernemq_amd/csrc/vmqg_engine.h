@@ -73,7 +73,8 @@ class FlatIndex {
 struct PathInfo {
   uint32_t parent, word, mp, depth;
   uint64_t in_slot = ~0ull;         // edge-table slot of the edge (parent, word) -> this path, if present
-  uint8_t eflags = 0;               // this path's own '#' / '+' edges present (kHasHash | kHasPlus)
+  uint8_t eflags = 0;               // this path's own '#' / '+' / literal edges present (kHas*)
+  uint32_t nlit = 0;                // its live literal-word edges (kHasWord while > 0)
   uint32_t topic_id = kNone;        // (MP, path words) term, once known
   uint32_t kl_off = 0, kl_cap = 0;  // keylist range owned by this path
   uint8_t rec = 0, topic_set = 0;   // vmq_trie_node record / its topic field
