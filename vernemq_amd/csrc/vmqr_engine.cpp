@@ -423,9 +423,12 @@ int RetainEngine::match_device(const vmqg_pub* d_filters, uint32_t nf, const uin
   hipSetDevice(device);
   if (!st) st = stream;
   // match_fold must not read tables a pending patch upload is writing: the
-  // context's stream is synchronised at the end of every apply
-  if (hipMemsetAsync(d_status, 0, 32, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (nf == 0) return hipMemsetAsync(d_offsets, 0, 8, st) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
+  // context's stream is synchronised at the end of every apply.  The status
+  // words and the walk tickets are zeroed by k_rt_plan (no memset launches).
+  if (nf == 0) {
+    if (hipMemsetAsync(d_status, 0, 32, st) != hipSuccess) return VMQG_E_DEVICE;
+    return hipMemsetAsync(d_offsets, 0, 8, st) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
+  }
   if (nf + 1 > plan_cap) {
     if (d_plan) { hipStreamSynchronize(st); hipFree(d_plan); }
     d_plan = nullptr;
@@ -457,7 +460,6 @@ int RetainEngine::match_device(const vmqg_pub* d_filters, uint32_t nf, const uin
   a.out = d_out; a.out_cap = out_cap; a.offsets = d_offsets;
   a.status = d_status; a.lookback = d_lookback; a.lb_tag = lb_tag; a.tile_cap = lookback_cap;
   a.tickets = d_tickets;
-  if (hipMemsetAsync(d_tickets, 0, 8 * kTicketStride * 4, st) != hipSuccess) return VMQG_E_DEVICE;
   hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
   if (timing) for (auto& x : e) hipEventCreate(&x);
   if (launch_retain_match(a, (uint32_t)walk_grid, st, e[0], e[1], e[2], e[3]) != hipSuccess) return VMQG_E_DEVICE;

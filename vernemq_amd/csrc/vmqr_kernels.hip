@@ -39,6 +39,7 @@ using vmqg::kNone;
 using vmqg::kPlus;
 
 constexpr int kW = 4;                 // waves per 256-thread block
+constexpr uint64_t kShortList = 64;   // plan: a list this short ends the search for a shorter one
 constexpr uint64_t kKindExact = 1ull << 62, kKindList = 2ull << 62, kCountMask = (1ull << 62) - 1;
 constexpr uint32_t kErrChunks = 32u;  // status[1]: the batch walks more tiles than look-back granules
 constexpr uint32_t kErrOut = 4u;      // status[1]: output overflow (VMQG_E_OVERFLOW)
@@ -66,6 +67,12 @@ __device__ __forceinline__ bool topic_match(const uint32_t* t, uint32_t nt, cons
 
 // ------------------------------------------------------------------ plan
 __global__ __launch_bounds__(256) void k_rt_plan(RArgs a) {
+  // this call's status words and walk tickets start at zero (read only by
+  // the kernels after this one on the stream)
+  if (blockIdx.x == 0 && threadIdx.x < 8) {
+    a.status[threadIdx.x] = 0;
+    a.tickets[threadIdx.x * kTicketStride] = 0;
+  }
   for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f < a.nf; f += gridDim.x * blockDim.x) {
     const vmqg_pub F = a.filters[f];
     const uint32_t* w = a.words + F.word_off;
@@ -120,7 +127,7 @@ __global__ __launch_bounds__(256) void k_rt_plan(RArgs a) {
               if (done) break;
             }
             if (c < cnt) { off = o; cnt = c; }
-            if (cnt == 0) break;
+            if (cnt <= kShortList) break;   // one walk step: no further probe can pay for itself
           }
         }
       }
