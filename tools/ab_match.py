@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Interleaved A/B of match-kernel tuning options (fast_g, nt_stores, fused,
-unroll, lean_emit) on one device, one process
+unroll) on one device, one process
 (cdna_hip_programming.md §5.4 rule 24): config C is loaded once, each round
 runs every variant for `steps` steps; medians of the per-variant step time
 and of the COUNT / EMIT kernel times are printed as JSON."""
@@ -25,7 +25,6 @@ def main():
     ap.add_argument("--nt", default="1")
     ap.add_argument("--fused", default="0,1")
     ap.add_argument("--unroll", default="4")
-    ap.add_argument("--lean", default="0")
     ap.add_argument("--config", default="C", choices=["C", "D"])
     ap.add_argument("--n-dev", type=int, default=1_000_000)
     args = ap.parse_args()
@@ -54,8 +53,7 @@ def main():
     variants = list(itertools.product([int(x) for x in args.fast_g.split(",")],
                                       [int(x) for x in args.nt.split(",")],
                                       [int(x) for x in args.fused.split(",")],
-                                      [int(x) for x in args.unroll.split(",")],
-                                      [int(x) for x in args.lean.split(",")]))
+                                      [int(x) for x in args.unroll.split(",")]))
     res = {str(vv): {"step_us": [], "count_us": [], "emit_us": []} for vv in variants}
     ref = None
     for rnd in range(args.rounds):
@@ -64,7 +62,6 @@ def main():
             v.set_option("nt_stores", vv[1])
             v.set_option("fused", vv[2])
             v.set_option("unroll", vv[3])
-            v.set_option("lean_emit", vv[4])
             v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap,
                            d_offs.data_ptr(), sp)
             torch.cuda.synchronize()
@@ -89,7 +86,7 @@ def main():
             r["count_us"].append(c / 1e3)
             r["emit_us"].append(e / 1e3)
     out = {k: {m: statistics.median(x) for m, x in d.items()} for k, d in res.items()}
-    print(json.dumps({"variants": "(fast_g, nt_stores, fused, unroll, lean_emit)", "config": args.config, "median": out, "rounds": args.rounds}, indent=1))
+    print(json.dumps({"variants": "(fast_g, nt_stores, fused, unroll)", "config": args.config, "median": out, "rounds": args.rounds}, indent=1))
 
 
 if __name__ == "__main__":

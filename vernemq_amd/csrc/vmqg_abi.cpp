@@ -198,8 +198,6 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
     e.opt_fast_g = (uint32_t)value;
   } else if (n == "nt_stores") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptNtStores) : (e.opt_flags & ~vmqg::kOptNtStores);
-  } else if (n == "lean_emit") {
-    e.opt_flags = value ? (e.opt_flags | vmqg::kOptLeanEmit) : (e.opt_flags & ~vmqg::kOptLeanEmit);
   } else if (n == "fused") {
     e.opt_fused = value != 0;
   } else if (n == "unroll") {

@@ -33,8 +33,6 @@ struct MatchArgs {
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
-constexpr uint32_t kOptLeanEmit = 2u;   // tier-0 EMIT without walk code: key-cached publishes only,
-                                        // COUNT hands the re-walk ones (> 2 keys) to tier 1
 
 // mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave path (grid a.o_waves / 4)
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st);

@@ -369,10 +369,6 @@ __device__ bool count_publish(const MatchArgs& a, uint32_t p, const Scratch& s, 
     const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
     kc[0] = make_uint4(m.total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
     kc[1] = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
-  } else if (TIER == 0 && (a.opts & kOptLeanEmit)) {
-    // the lean EMIT has no walk: tier 1 emits it (z = 1: already counted)
-    kc[0] = make_uint4(m.total, kRewalk, 1, 0);
-    defer_or_fail<0>(a, p);
   } else {
     kc[0] = make_uint4(m.total, kRewalk, 0, 0);
   }
@@ -491,72 +487,6 @@ __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
   }
 }
 
-// Lean EMIT (kOptLeanEmit): one publish per lane, 64 consecutive publishes
-// per wave, straight from the key cache — no walk code, so few registers and
-// more waves in flight for the record stores.  Publishes marked kRewalk
-// (overflowed, or > 2 keys) are skipped: tier 1 writes their ranges.
-struct LeanMeta { uint32_t rel, crel, k0, c0, k1, ksum, rm_lo, rm_hi; };
-
-template <bool NT>
-__global__ __launch_bounds__(256) void k_emit_lean(MatchArgs a) {
-  constexpr int U = 4;
-  __shared__ LeanMeta lm[kWaves][64];
-  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
-  const uint64_t stride = (uint64_t)gridDim.x * kWaves * 64;
-  for (uint64_t base = ((uint64_t)blockIdx.x * kWaves + wv) * 64; base < a.npub; base += stride) {
-    const uint64_t p = base + lane;
-    const bool valid = p < a.npub;
-    uint4 h = make_uint4(0, kRewalk, 0, 0), k = make_uint4(0, 0, 0, 0);
-    uint64_t ob = 0, oe = 0;
-    if (valid) {
-      const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + p * 2;
-      h = kc[0];
-      k = kc[1];
-      ob = a.offsets[p];
-      oe = a.offsets[p + 1];
-    }
-    bool ok = valid && h.y != kRewalk;
-    if (ok && oe > a.out_cap) { atomicOr(&a.status[1], kErrOverflow); ok = false; }
-    if (ok && oe - ob != h.x) { atomicOr(&a.status[1], kErrMismatch); ok = false; }
-    const uint32_t span = ok ? h.x : 0u;
-    const uint32_t incl = wave_incl_scan32(span);
-    const uint32_t Tok = __shfl(incl, 63, 64);
-    const uint64_t wbase = __shfl(ob, 0, 64);   // offsets[base]
-    lm[wv][lane] = LeanMeta{(uint32_t)(ob - wbase), incl - span, k.x, k.y, k.z, k.y + k.w, h.z, h.w};
-    wave_sync();
-    uint32_t j = 0;
-    for (uint32_t r0 = lane; r0 < Tok; r0 += 64 * U) {
-      uint4 v[U];
-      uint64_t dst[U];
-      bool w[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t r = r0 + 64 * u;
-        w[u] = r < Tok;
-        if (w[u]) {
-          while (j + 1 < 64 && lm[wv][j + 1].crel <= r) j++;
-          const LeanMeta m = lm[wv][j];
-          const uint32_t rr = r - m.crel;
-          if (rr < m.c0) {
-            v[u] = *reinterpret_cast<const uint4*>(a.records + m.k0 + rr);
-          } else if (rr < m.ksum) {
-            v[u] = *reinterpret_cast<const uint4*>(a.records + m.k1 + (rr - m.c0));
-          } else {   // the remote nodes of the mask, in node order (fold_/5 :78-84)
-            uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
-            for (uint32_t q = rr - m.ksum; q > 0; q--) rm &= rm - 1;
-            v[u] = make_uint4((VMQG_EMIT_REMOTE << 24) | (uint32_t)__builtin_ctzll(rm), kNone, kNone, kNone);
-          }
-          dst[u] = wbase + m.rel + rr;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++)
-        if (w[u]) store_rec<NT>(a.out, dst[u], v[u]);
-    }
-    wave_sync();
-  }
-}
-
 // Tier 1: one publish per wave from the deferred list; LDS lists, then the
 // wave's global scratch.
 template <int MODE, bool NT>
@@ -578,8 +508,6 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
   for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
     const uint32_t p = a.deferred[d];
     if (MODE == 0) {
-      const uint4 h0 = reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2];
-      if (h0.y == kRewalk && h0.z == 1) continue;   // counted by tier 0, handed over for EMIT only
       if (!count_publish<64, 1>(a, p, s, g)) {
         if (__lane_id() == 0) atomicAdd(&a.status[2], 1u);
         count_publish<64, 2>(a, p, so, g);
@@ -886,13 +814,7 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) 
     if (mode == 0) k_match_fast<0, GG, false><<<g, 256, 0, st>>>(a);        \
     else if (nt) k_match_fast<1, GG, true><<<g, 256, 0, st>>>(a);           \
     else k_match_fast<1, GG, false><<<g, 256, 0, st>>>(a);
-    if (mode == 1 && (a.opts & kOptLeanEmit)) {
-      uint32_t gl = div_up(a.npub, kWaves * 64);
-      if (gl > cap) gl = cap;
-      if (gl < 1) gl = 1;
-      if (nt) k_emit_lean<true><<<gl, 256, 0, st>>>(a);
-      else k_emit_lean<false><<<gl, 256, 0, st>>>(a);
-    } else if (G == 2) { VMQG_FAST(2) }
+    if (G == 2) { VMQG_FAST(2) }
     else if (G == 4) { VMQG_FAST(4) }
     else { VMQG_FAST(8) }
 #undef VMQG_FAST
