@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline: the box's host share")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP events (profiling runs)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end figure")
     ap.add_argument("--config", default="C", choices=["A", "B", "C", "D", "E", "R1", "R2", "RT", "AC"],
                     help="C: headline (1M subs); D: 10M subs with $share groups under 1%%/s churn; "
                          "A, B, E, R1, R2: the other SURVEY §8d shapes (secondary lines); "
@@ -188,6 +189,43 @@ def main():
     count_ns, emit_ns, nlaunch = view.kernel_times() if not args.no_timing else (0.0, 0.0, 0)
     emissions = int(d_offs[-1].item())
 
+    # SURVEY §8(d) end-to-end figure (never `value`): publishes from pinned
+    # host memory, match, offsets + every record back to pinned host memory,
+    # on the same stream; rank 0 at N = 1 only
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        h_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).pin_memory()
+        h_words = torch.from_numpy(words.astype(np.int32)).pin_memory()
+        h_offs = torch.empty(npub + 1, dtype=torch.int64).pin_memory()
+        h_out = torch.empty(emissions * 4, dtype=torch.int32).pin_memory()
+        cur = torch.cuda.current_stream()
+
+        def e2e_step():
+            d_pubs.copy_(h_pubs, non_blocking=True)
+            d_words.copy_(h_words, non_blocking=True)
+            step()
+            h_offs.copy_(d_offs, non_blocking=True)
+            h_out.copy_(d_out[: emissions * 4], non_blocking=True)
+
+        e2e_step()
+        cur.synchronize()
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            e2e_step()
+        cur.synchronize()
+        el_e2e = (time.perf_counter() - t0) / reps
+        if view.match_status(sp) != 0 or int(h_offs[-1]) != emissions:
+            raise RuntimeError("end-to-end pass differs from the device-resident one")
+        pcie = h_pubs.numel() * 4 + h_words.numel() * 4 + h_offs.numel() * 8 + emissions * 16
+        e2e = {"publishes_per_s": npub / el_e2e, "ms_per_batch": el_e2e * 1e3, "pcie_bytes_per_batch": pcie,
+               "pcie_GBps": pcie / el_e2e / 1e9,
+               "note": "H2D publishes + words, match, D2H offsets + all %d records (pinned host buffers), "
+                       "same stream; bounded by PCIe, not by the kernels" % emissions}
+        log("end-to-end: %.3g publishes/s (%.2f ms per batch, %.1f GB/s over PCIe)"
+            % (e2e["publishes_per_s"], e2e["ms_per_batch"], e2e["pcie_GBps"]))
+        del h_out
+
     # max over ranks of the timed region; all-gather the per-GPU match counts
     t_max = elapsed
     total_emit = emissions * args.steps
@@ -276,6 +314,7 @@ def main():
                              "note": "SURVEY 8(d) B_p = 8(L+1) + 16 S_p + 32 R_p; charges an HBM read per emission "
                                      "of the cache-resident fan-out list, so it can exceed the HBM peak"},
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
             "load_s": load_s,
         }
         print(json.dumps(res), flush=True)

@@ -12,10 +12,8 @@ from vernemq_amd import _lib  # noqa: E402
 
 VARIANTS = {
     "default": [],
-    "u1": ["-DVMQR_U=1"],
-    "u4": ["-DVMQR_U=4"],
-    "t512": ["-DVMQR_TILE_ROWS=512"],
-    "t2048": ["-DVMQR_TILE_ROWS=2048"],
+    "emit_u2": ["-DVMQG_EMIT_U=2"],
+    "emit_u8": ["-DVMQG_EMIT_U=8"],
 }
 
 

@@ -31,6 +31,9 @@
 namespace vmqg {
 
 constexpr int kWaves = 4;          // waves per 256-thread block
+#ifndef VMQG_EMIT_U
+#define VMQG_EMIT_U 8              // records in flight per lane in the tier-0 EMIT copy (A/B: 2, 4, 8)
+#endif
 // fast-tier LDS lists per group, sized so a block stays near 28 KiB
 template <int G> struct FastCaps { static constexpr uint32_t S = 8 * G, C = 4 * G, K = 4 * G; };
 constexpr uint32_t kRewalk = 0xFFFFFFFFu;   // key cache: EMIT must re-walk
@@ -481,7 +484,7 @@ __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
     if (MODE == 0) {
       if (g.gidx < n) count_publish<G, 0>(a, base + g.gidx, s, g);
     } else {
-      emit_wave<G, GPW, NT, 4>(a, base, n, s, nullptr, g, gm[wv], ky[wv * GPW], KC);
+      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, nullptr, g, gm[wv], ky[wv * GPW], KC);
     }
     wave_sync();
   }
