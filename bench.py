@@ -71,10 +71,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP events (profiling runs)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end figure")
-    ap.add_argument("--config", default="C", choices=["A", "B", "C", "D", "E", "R1", "R2", "RT", "AC"],
+    ap.add_argument("--config", default="C", choices=["A", "B", "C", "D", "E", "R1", "R2", "RT", "AC", "SS"],
                     help="C: headline (1M subs); D: 10M subs with $share groups under 1%%/s churn; "
                          "A, B, E, R1, R2: the other SURVEY §8d shapes (secondary lines); "
-                         "RT: retained-message match_fold (§8f rank 3); AC: vmq_acl checks (§8f rank 4)")
+                         "RT: retained-message match_fold (§8f rank 3); AC: vmq_acl checks (§8f rank 4); "
+                         "SS: $share dispatch on config D's match output (§8f rank 4)")
     ap.add_argument("--ac-requests", type=int, default=1 << 20, help="AC: ACL checks per step")
     ap.add_argument("--rt-devices", type=int, default=62_500, help="RT: devices x 16 retained topics")
     ap.add_argument("--rt-filters", type=int, default=1 << 18, help="RT: subscription filters per step")
@@ -92,6 +93,8 @@ def main():
         return bench_retain(args)
     if args.config == "AC":
         return bench_acl(args)
+    if args.config == "SS":
+        return bench_shared(args)
     if args.config != "C":
         return bench_other(args)
 
@@ -666,6 +669,134 @@ def bench_acl(args):
                      "bytes_model": "24-B request + 16-B topic words read, 1-B verdict written per check "
                                     "(the rule tables are L2-resident; workloads.AclWorkload.algorithmic_bytes)"},
         "cpu_baseline": cpu, "load_s": load_s, "arena_bytes": st["device_bytes"]}), flush=True)
+
+
+def bench_shared(args):
+    """Shared-subscription dispatch (vmq_shared_subscriptions:publish/3,
+    SURVEY §8(f) rank 4) on config D's match output: the 2^20-publish batch
+    is matched once on the device (untimed; its records stay in HBM), then
+    each step dispatches the whole batch with the default prefer_local policy
+    (every $share group of every publish gets its member; queue states: 3/4
+    online, 1/8 offline, 1/16 draining, 1/16 no queue).  Prints one JSON line
+    with the dispatch kernels' roofline and the CPU restatement on a sample."""
+    import torch
+    from vernemq_amd import workloads as W
+    from vernemq_amd.reg_view import RegGpuView
+    from vernemq_amd.shared import SharedGpu
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    t0 = time.time()
+    w = W.config_d(scale=args.d_scale, n_pubs=args.batch)
+    n_live = w.notes["n_live"]
+    view = RegGpuView(node=w.self_node, device=0, nodes=w.nodes,
+                      hints={"edges": 4 * n_live // 5, "paths": 4 * n_live // 5, "keys": n_live,
+                             "records": n_live * 11 // 10, "exact": n_live})
+    w.load_into(view, n=n_live)
+    load_s = time.time() - t0
+    log("SS: config D (%d live subs) loaded in %.1fs" % (n_live, load_s))
+    pubs, words = w.publish_arrays(view)
+    npub = len(pubs)
+    d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    d_offs = torch.zeros(npub + 1, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+    out_cap = 1024
+    d_out = torch.empty(4, dtype=torch.int32, device=dev)
+    for _ in range(2):   # first pass sizes the output
+        view.match_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_out.data_ptr(), out_cap,
+                          d_offs.data_ptr(), sp)
+        torch.cuda.synchronize()
+        need = int(d_offs[-1].item())
+        rc = view.match_status(sp)
+        if need <= out_cap and rc == 0:
+            break
+        out_cap = need + 1024
+        d_out = torch.empty(out_cap * 4, dtype=torch.int32, device=dev)
+    total = int(d_offs[-1].item())
+    sel = SharedGpu(device=0, local_node=0)
+    n_sub = len(w.clients)
+    st = np.ones(n_sub, dtype=np.uint8)
+    u = W.SplitMix(0x55).ints(n_sub, 16)
+    st[u >= 12] = 2   # offline
+    st[u == 14] = 3   # draining
+    st[u == 15] = 0   # no queue
+    ids = np.array([view.subscribers.ids[c] for c in w.clients], dtype=np.uint32)
+    sel.set_state_ids(ids, st)
+    d_ch = torch.empty(total, dtype=torch.uint8, device=dev)
+    d_f = torch.empty(npub, dtype=torch.int32, device=dev)
+    step = lambda k: sel.select_device(d_out.data_ptr(), d_offs.data_ptr(), npub, "prefer_local", 0x55, k * npub,
+                                       d_ch.data_ptr(), d_f.data_ptr(), sp)
+    n_warm = max(1, args.warmup)
+    for k in range(n_warm):
+        step(k)
+    torch.cuda.synchronize()
+    if sel.select_status(sp) != 0:
+        raise RuntimeError("select status after warmup")
+    # parity on a sample of the batch against the CPU restatement
+    from oracle import shared_oracle as SO   # checker (and CPU baseline) only
+    offs_h = d_offs.cpu().numpy().astype(np.uint64)
+    S = min(npub, 65536)
+    recs_s = d_out[: int(offs_h[S]) * 4].cpu().numpy().view(np.uint32).reshape(-1, 4)
+    full_states = np.ones(int(ids.max()) + 1, np.uint8)
+    full_states[ids] = st
+    k_last = n_warm - 1
+    want_c, want_f = SO.select(recs_s, offs_h[: S + 1], "prefer_local", 0x55, k_last * npub, full_states, 0)
+    got_c = d_ch[: int(offs_h[S])].cpu().numpy()
+    got_f = d_f[:S].cpu().numpy().astype(np.uint32)
+    verified = bool(np.array_equal(got_c, want_c) and np.array_equal(got_f, want_f))
+    if not verified:
+        raise RuntimeError("dispatch differs from the CPU restatement on the sample")
+    n_group = int((recs_s[:, 0] >> 24 == 2).sum())
+    sel.set_timing(not args.no_timing)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(n_warm + k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if sel.select_status(sp) != 0:
+        raise RuntimeError("select status in timed region")
+    sel_ns, nl, deferred = sel.kernel_times()
+    alg = total * 17 + npub * 12   # per record: 16-B read + 1-B chosen; per publish: offsets + failed
+    achieved = alg / sel_ns if sel_ns else None
+    chosen_n = int(d_ch.sum().item())
+
+    cpu = None
+    if not args.no_cpu_baseline:
+        thr = {}
+        for threads in (1, args.cpu_threads):
+            s1 = SO.select_timed(recs_s, offs_h[: S + 1], "prefer_local", 0x55, full_states, 0, 1, threads)
+            reps = max(1, int(math.ceil(args.cpu_seconds / max(s1, 1e-6))))
+            sec = SO.select_timed(recs_s, offs_h[: S + 1], "prefer_local", 0x55, full_states, 0, reps, threads)
+            thr[threads] = (S * reps / sec, reps, sec)
+        v, reps, sec = thr[args.cpu_threads]
+        cpu = {"value": v, "unit": "publishes/s", "cores": args.cpu_threads, "kind": "port",
+               "single_thread_value": thr[1][0],
+               "sample": "first %d publishes of the SS batch (%d records) x %d reps (%.1fs) on %d threads "
+                         "(1 thread: %.3g publishes/s), oracle/vmq_shared_oracle.cpp (C++ restatement of "
+                         "add_to_subscriber_group + vmq_shared_subscriptions:publish/3: group map, "
+                         "filter_subscribers, keyed sort, publish_online / publish_any; not BEAM); host %s"
+                         % (S, len(recs_s), reps, sec, args.cpu_threads, thr[1][0], cpu_model())}
+        log("SS cpu baseline: %.0f publishes/s (%d threads), %.0f (1 thread)" % (v, args.cpu_threads, thr[1][0]))
+
+    print(json.dumps({
+        "metric": "shared-subscription dispatches/sec (publishes through vmq_shared_subscriptions:publish/3)",
+        "value": npub * args.steps / el, "unit": "publishes/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic: SURVEY.md §8(d) config D generator (splitmix64 seed 0xD), scale %g" % args.d_scale,
+        "config": {"workload": "SS: config D match output, %d publishes / %d records per step (%d $share records "
+                               "in the first %d publishes), policy prefer_local" % (npub, total, n_group, S)},
+        "verified_sample": verified, "records_per_step": total, "chosen_per_step": chosen_n,
+        "kernel_us": {"select": sel_ns / 1e3, "launches": nl, "tier2_publishes": deferred},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS if achieved else None,
+                     "traffic": load_pmc_traffic("k_select_wave", "pmc_ss.json"),
+                     "kernel": "k_select_wave + k_select_block",
+                     "algorithmic_bytes_per_launch": alg,
+                     "bytes_model": "16-B record read + 1-B chosen written per record, 8-B offset + 4-B failed "
+                                    "per publish (queue states are L2-resident)"},
+        "cpu_baseline": cpu, "load_s": load_s}), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,4 +1,4 @@
-"""CPU checks of the C ABI boundary (include/vmqg.h, vmqr.h, vmqa.h): the library loads,
+"""CPU checks of the C ABI boundary (include/vmqg.h, vmqr.h, vmqa.h, vmqs.h): the library loads,
 exports every declared entry point, its structs have the header's layout,
 and a host-only context fails loudly on match calls (no CPU fallback)."""
 import ctypes
@@ -13,14 +13,14 @@ from vernemq_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "vmqg.h")
-HEADERS = [HEADER, os.path.join(ROOT, "include", "vmqr.h"), os.path.join(ROOT, "include", "vmqa.h")]
+HEADERS = [HEADER] + [os.path.join(ROOT, "include", h) for h in ("vmqr.h", "vmqa.h", "vmqs.h")]
 
 
 def declared_functions():
     out = set()
     for h in HEADERS:
         src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
-        out |= set(re.findall(r"^\s*[\w\s\*]+?\b(vmq[gra]_\w+)\s*\(", src, flags=re.M))
+        out |= set(re.findall(r"^\s*[\w\s\*]+?\b(vmq[gras]_\w+)\s*\(", src, flags=re.M))
     return sorted(out)
 
 
@@ -64,6 +64,36 @@ def test_acl_struct_layouts_match_header(tmp_path):
     from vernemq_amd.acl import REQ_DTYPE, RULE_DTYPE
     assert got == [ctypes.sizeof(_lib.AConfig), RULE_DTYPE.itemsize, REQ_DTYPE.itemsize, ctypes.sizeof(_lib.AStats),
                    REQ_DTYPE.fields["nwords"][1]]
+
+
+def test_shared_struct_layouts_match_header(tmp_path):
+    prog = tmp_path / "szs.c"
+    prog.write_text('#include <stdio.h>\n#include "vmqs.h"\n'
+                    'int main(void){printf("%zu %u %u %u\\n", sizeof(vmqs_config), VMQS_POLICY_LOCAL_ONLY,'
+                    ' VMQS_DRAINING, VMQS_MAX_SEGMENT);return 0;}\n')
+    exe = tmp_path / "szs"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(prog),
+                    "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [ctypes.sizeof(_lib.SConfig), _lib.S_LOCAL_ONLY, _lib.S_DRAINING, _lib.S_MAX_SEGMENT]
+
+
+def test_shared_key_matches_oracle():
+    """vmqs_key (the element order of a shared group) is host-callable and
+    equals the oracle's restatement of it bit for bit."""
+    from oracle import shared_oracle as SO
+    L = _lib.lib()
+    for seed, q, p in [(0, 0, 0), (1, 2, 3), (0xDEADBEEF, 1 << 40, (1 << 24) - 1), (7, 12345, 4095)]:
+        k = L.vmqs_key(seed, q, p)
+        assert k == SO.sel_key(seed, q, p)
+        assert k & 0xFFFFFF == p
+
+
+def test_shared_context_needs_a_device():
+    err = ctypes.c_int(0)
+    cfg = _lib.SConfig(device=-1, local_node=0)
+    assert _lib.lib().vmqs_create(ctypes.byref(cfg), ctypes.byref(err)) is None
+    assert err.value == _lib.E_DEVICE
 
 
 def test_acl_host_context_refuses_checks():

@@ -14,14 +14,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "libvmqgpu.so")
 HEADER = os.path.join(ROOT, "include", "vmqg.h")
-HEADERS = [HEADER, os.path.join(ROOT, "include", "vmqr.h"), os.path.join(ROOT, "include", "vmqa.h")]
+HEADERS = [HEADER, os.path.join(ROOT, "include", "vmqr.h"), os.path.join(ROOT, "include", "vmqa.h"),
+           os.path.join(ROOT, "include", "vmqs.h")]
 SOURCES = [os.path.join(HERE, "csrc", f) for f in
            ("vmqg_engine.cpp", "vmqg_abi.cpp", "vmqg_kernels.hip",
             "vmqr_engine.cpp", "vmqr_abi.cpp", "vmqr_kernels.hip",
-            "vmqa_engine.cpp", "vmqa_abi.cpp", "vmqa_kernels.hip")]
+            "vmqa_engine.cpp", "vmqa_abi.cpp", "vmqa_kernels.hip",
+            "vmqs_abi.cpp", "vmqs_kernels.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in
                   ("vmqg_common.h", "vmqg_engine.h", "vmqg_kernels.h", "vmqg_lookback.h",
-                   "vmqr_engine.h", "vmqa_engine.h")] + HEADERS
+                   "vmqr_engine.h", "vmqa_engine.h", "vmqs_engine.h")] + HEADERS
 
 # ---- status codes / constants (vmqg.h)
 OK, E_INVAL, E_OVERFLOW, E_NOMEM, E_DEVICE, E_FRONTIER, E_LIMIT, E_STATE = 0, -1, -2, -3, -4, -5, -6, -7
@@ -101,6 +103,14 @@ A_READ, A_WRITE = 1, 2
 A_TABLE_ALL, A_TABLE_USER, A_TABLE_PATTERN = 0, 1, 2
 A_WORD_USER, A_WORD_CLIENT, A_WORD_MOUNTPOINT = 3, 4, 5
 A_NO_USER, A_EPHEMERAL = 0xFFFFFFFE, 0x80000000
+# vmqs.h constants
+S_RANDOM, S_PREFER_LOCAL, S_LOCAL_ONLY = 0, 1, 2
+S_NOT_FOUND, S_ONLINE, S_OFFLINE, S_DRAINING = 0, 1, 2, 3
+S_MAX_SEGMENT = 1 << 24
+
+
+class SConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("local_node", ctypes.c_uint32)]
 
 
 # (name, restype, argtypes) for every entry point declared in include/vmqg.h, vmqr.h and vmqa.h
@@ -150,6 +160,17 @@ SIGNATURES = [
     ("vmqa_stats", ctypes.c_int, [_P, ctypes.POINTER(AStats)]),
     ("vmqa_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
     ("vmqa_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
+    # shared-subscription dispatcher (include/vmqs.h)
+    ("vmqs_create", _P, [ctypes.POINTER(SConfig), ctypes.POINTER(ctypes.c_int)]),
+    ("vmqs_destroy", None, [_P]),
+    ("vmqs_set_states", ctypes.c_int, [_P, _P, _P, _SZ]),
+    ("vmqs_select_batch", ctypes.c_int, [_P, _P, _P, _SZ, _U32, _U64, _U64, _P, _P]),
+    ("vmqs_select_device", ctypes.c_int, [_P, _P, _P, _U32, _U32, _U64, _U64, _P, _P, _P]),
+    ("vmqs_select_status", ctypes.c_int, [_P, _P]),
+    ("vmqs_key", _U64, [_U64, _U64, _U32]),
+    ("vmqs_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
+    ("vmqs_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64),
+                                         ctypes.POINTER(_U64)]),
     ("vmqr_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
     ("vmqr_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
