@@ -14,6 +14,8 @@ VARIANTS = {
     "default": [],
     "emit_u2": ["-DVMQG_EMIT_U=2"],
     "emit_u8": ["-DVMQG_EMIT_U=8"],
+    "ss_u2": ["-DVMQS_UNROLL=2"],
+    "ss_narrow": ["-DVMQS_WIDE_CHOSEN=0"],
 }
 
 

@@ -22,7 +22,7 @@
 // Layout of the work: keys order by (40 random bits, position), so "minimum
 // key" and "maximum key" are single 64-bit LDS atomicMin / atomicMax per
 // element; a group's slot holds {group, flags, min online key, max offline
-// key}.  Tier 1: one wave per publish, 64-slot table and a 4096-bit bitmap
+// key} (tier 1 keeps local / all pairs, see below).  Tier 1: one wave per publish, 64-slot table and a 4096-bit bitmap
 // of winners in LDS, so every chosen[] byte is written exactly once, in
 // order.  Tier 2 (long segments, many groups): one workgroup per publish.
 // Integer work only, no MFMA; HBM-bound on the 16-B record reads.
@@ -87,12 +87,80 @@ __device__ __forceinline__ void offer(const SArgs& a, GSlot* t, uint32_t mask, c
 
 __device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
 
-// ---- tier 1: one wavefront per publish --------------------------------------
+// ---- tier 1: one wavefront per publish, one read of the segment ----------------
+// prefer_local's eligible set depends on whether the group has a local member,
+// which is only known after the whole segment was seen; rather than reading the
+// records twice, each slot keeps the extremes over the local members and over
+// all members, and pass 3 picks the pair the policy selects.
 constexpr uint32_t kWaves = 4;
 constexpr uint32_t kBitWords = kWaveMax / 32;
+#ifndef VMQS_UNROLL
+#define VMQS_UNROLL 4
+#endif
+constexpr uint32_t kUnroll = VMQS_UNROLL;   // records in flight per lane (A/B: tools/build_variants.py)
+constexpr uint32_t kFOnL = 8u, kFOffL = 16u;
+
+struct alignas(8) WSlot { uint32_t group, flags; unsigned long long on_l, on_a, off_l, off_a; };
+static_assert(sizeof(WSlot) == 40, "");
+
+__device__ __forceinline__ uint32_t wslot_claim(WSlot* t, uint32_t mask, uint32_t g) {
+  uint32_t h = gslot_home(g, mask);
+  for (uint32_t n = 0; n <= mask; n++, h = (h + 1) & mask) {
+    const uint32_t cur = atomicCAS(&t[h].group, kEmpty, g);
+    if (cur == kEmpty || cur == g) return h;
+  }
+  return kEmpty;
+}
+
+// One kind-B element at position p: claim its group's slot and offer its key.
+// Returns false when the slot table is full.
+__device__ __forceinline__ bool offer1(const SArgs& a, WSlot* t, uint32_t mask, const Record& r, uint32_t s,
+                                       uint64_t q, uint32_t p) {
+  const uint32_t h = wslot_claim(t, mask, r.group);
+  if (h == kEmpty) return false;
+  const bool local = node_of(r) == a.local_node;
+  if (local) atomicOr(&t[h].flags, kFLocal);
+  if (s == VMQS_NOT_FOUND) return true;
+  const unsigned long long k = sel_key(a.seed, q, p);
+  if (s == VMQS_ONLINE) {
+    atomicMin(&t[h].on_a, k);
+    if (local) atomicMin(&t[h].on_l, k);
+    atomicOr(&t[h].flags, local ? (kFOn | kFOnL) : kFOn);
+  } else {
+    atomicMax(&t[h].off_a, k);
+    if (local) atomicMax(&t[h].off_l, k);
+    atomicOr(&t[h].flags, local ? (kFOff | kFOffL) : kFOff);
+  }
+  return true;
+}
+
+#ifndef VMQS_WIDE_CHOSEN
+#define VMQS_WIDE_CHOSEN 1
+#endif
+
+// Writes chosen[0..n) of one segment: bit p of `win` (all zero when win is
+// null).  Wide form: byte head up to 4-B alignment, then one dword of four
+// chosen bytes per lane, then the byte tail.
+__device__ __forceinline__ void write_chosen(uint8_t* ch, uint32_t n, const uint32_t* win, uint32_t lane) {
+#define VMQS_BIT(p) (win ? (win[(p) >> 5] >> ((p) & 31)) & 1u : 0u)
+#if VMQS_WIDE_CHOSEN
+  const uint32_t head = min(n, (uint32_t)((4u - ((uint32_t)(uintptr_t)ch & 3u)) & 3u));
+  if (lane < head) ch[lane] = (uint8_t)VMQS_BIT(lane);
+  const uint32_t nw = (n - head) >> 2;
+  uint32_t* cw = reinterpret_cast<uint32_t*>(ch + head);
+  for (uint32_t k = lane; k < nw; k += 64) {
+    const uint32_t p = head + 4 * k;
+    cw[k] = VMQS_BIT(p) | VMQS_BIT(p + 1) << 8 | VMQS_BIT(p + 2) << 16 | VMQS_BIT(p + 3) << 24;
+  }
+  for (uint32_t p = head + 4 * nw + lane; p < n; p += 64) ch[p] = (uint8_t)VMQS_BIT(p);
+#else
+  for (uint32_t p = lane; p < n; p += 64) ch[p] = (uint8_t)VMQS_BIT(p);
+#endif
+#undef VMQS_BIT
+}
 
 __global__ __launch_bounds__(256) void k_select_wave(SArgs a) {
-  __shared__ GSlot tab[kWaves][kWaveGroups];
+  __shared__ WSlot tab[kWaves][kWaveGroups];
   __shared__ uint32_t win[kWaves][kBitWords];
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t i = blockIdx.x * kWaves + w;
@@ -103,50 +171,95 @@ __global__ __launch_bounds__(256) void k_select_wave(SArgs a) {
     if (lane == 0) a.defer[atomicAdd(&a.status[0], 1u)] = i;
     return;
   }
-  GSlot* t = tab[w];
+  WSlot* t = tab[w];
   const uint32_t mask = kWaveGroups - 1;
   const Record* rec = a.emits + s0;
   uint8_t* ch = a.chosen + s0;
-  for (uint32_t k = lane; k < kWaveGroups; k += 64) t[k] = GSlot{kEmpty, 0u, ~0ull, 0ull};
+  for (uint32_t k = lane; k < kWaveGroups; k += 64) t[k] = WSlot{kEmpty, 0u, ~0ull, ~0ull, 0ull, 0ull};
+  for (uint32_t k = lane; k < kBitWords; k += 64) win[w][k] = 0;
   lds_fence();
   __builtin_amdgcn_wave_barrier();
-  // pass 1: the groups of the segment and whether each has a local member
+  // pass 1: groups, local flags and keys in one read of the segment
+  const uint64_t q = a.pub_seq + i;
   bool any = false, ovf = false;
-  for (uint32_t p = lane; p < n; p += 64) {
-    const Record r = rec[p];
-    if (kind_of(r) != VMQG_EMIT_GROUP) continue;
-    any = true;
-    const uint32_t h = gslot_claim(t, mask, r.group);
-    if (h == kEmpty) { ovf = true; continue; }
-    if (node_of(r) == a.local_node) atomicOr(&t[h].flags, kFLocal);
+  for (uint32_t base = 0; base < n; base += 64 * kUnroll) {
+    Record r[kUnroll];
+#pragma unroll
+    for (uint32_t j = 0; j < kUnroll; j++) {
+      const uint32_t p = base + j * 64 + lane;
+      if (p < n) r[j] = rec[p];
+      else r[j].kind_node = 0;
+    }
+    // queue states of the members, all loads in flight before any is used
+    uint32_t sv[kUnroll];
+#pragma unroll
+    for (uint32_t j = 0; j < kUnroll; j++)
+      sv[j] = kind_of(r[j]) == VMQG_EMIT_GROUP ? state_of(a, r[j].subscriber) : (uint32_t)VMQS_NOT_FOUND;
+#pragma unroll
+    for (uint32_t j = 0; j < kUnroll; j++) {
+      const bool isb = kind_of(r[j]) == VMQG_EMIT_GROUP;
+      const uint64_t mb = __ballot(isb);
+      if (!mb) continue;
+      any = true;
+      const uint32_t lead = __builtin_ctzll(mb);
+      const uint32_t g0 = __shfl(r[j].group, lead);
+      if (__ballot(isb && r[j].group != g0)) {   // mixed groups: per-lane atomics
+        if (isb && !offer1(a, t, mask, r[j], sv[j], q, base + j * 64 + lane)) ovf = true;
+        continue;
+      }
+      // One group in this instruction (members of a group are emitted
+      // contiguously): reduce across the wave, then one lane updates the slot,
+      // instead of 64 serialised LDS atomics on one address.
+      const bool local = isb && node_of(r[j]) == a.local_node;
+      const uint32_t st = sv[j];
+      const unsigned long long k = sel_key(a.seed, q, base + j * 64 + lane);
+      const bool on = st == VMQS_ONLINE, off = st == VMQS_OFFLINE || st == VMQS_DRAINING;
+      unsigned long long on_a = on ? k : ~0ull, on_l = on && local ? k : ~0ull;
+      unsigned long long off_a = off ? k : 0ull, off_l = off && local ? k : 0ull;
+      for (int o = 32; o > 0; o >>= 1) {
+        on_a = min(on_a, __shfl_xor(on_a, o));
+        on_l = min(on_l, __shfl_xor(on_l, o));
+        off_a = max(off_a, __shfl_xor(off_a, o));
+        off_l = max(off_l, __shfl_xor(off_l, o));
+      }
+      const uint32_t fl = (__ballot(local) ? kFLocal : 0u) | (__ballot(on) ? kFOn : 0u) |
+                          (__ballot(on && local) ? kFOnL : 0u) | (__ballot(off) ? kFOff : 0u) |
+                          (__ballot(off && local) ? kFOffL : 0u);
+      if (lane == lead) {
+        const uint32_t h = wslot_claim(t, mask, g0);
+        if (h == kEmpty) {
+          ovf = true;
+        } else {
+          if (fl) atomicOr(&t[h].flags, fl);
+          if (fl & kFOn) atomicMin(&t[h].on_a, on_a);
+          if (fl & kFOnL) atomicMin(&t[h].on_l, on_l);
+          if (fl & kFOff) atomicMax(&t[h].off_a, off_a);
+          if (fl & kFOffL) atomicMax(&t[h].off_l, off_l);
+        }
+      }
+    }
   }
   if (__ballot(ovf)) {
     if (lane == 0) a.defer[atomicAdd(&a.status[0], 1u)] = i;
     return;
   }
   if (!__ballot(any)) {   // no shared member: nothing chosen
-    for (uint32_t p = lane; p < n; p += 64) ch[p] = 0;
+    write_chosen(ch, n, nullptr, lane);
     if (lane == 0 && a.failed) a.failed[i] = 0;
     return;
-  }
-  for (uint32_t k = lane; k < kBitWords; k += 64) win[w][k] = 0;
-  lds_fence();
-  __builtin_amdgcn_wave_barrier();
-  // pass 2: filter, key, offer
-  const uint64_t q = a.pub_seq + i;
-  for (uint32_t p = lane; p < n; p += 64) {
-    const Record r = rec[p];
-    if (kind_of(r) == VMQG_EMIT_GROUP) offer(a, t, mask, r, q, p);
   }
   lds_fence();
   __builtin_amdgcn_wave_barrier();
   // pass 3: one winner per group (online first, else publish_any's pick)
   uint32_t nf = 0;
   for (uint32_t k = lane; k < kWaveGroups; k += 64) {
-    const GSlot s = t[k];
+    const WSlot s = t[k];
     if (s.group == kEmpty) continue;
-    if (s.flags & (kFOn | kFOff)) {
-      const uint32_t p = (uint32_t)((s.flags & kFOn ? s.on : s.off) & 0xFFFFFFu);
+    const bool loc = a.policy == VMQS_POLICY_LOCAL_ONLY ||
+                     (a.policy == VMQS_POLICY_PREFER_LOCAL && (s.flags & kFLocal));
+    const bool on = s.flags & (loc ? kFOnL : kFOn), off = s.flags & (loc ? kFOffL : kFOff);
+    if (on || off) {
+      const uint32_t p = (uint32_t)((on ? (loc ? s.on_l : s.on_a) : (loc ? s.off_l : s.off_a)) & 0xFFFFFFu);
       atomicOr(&win[w][p >> 5], 1u << (p & 31));
     } else {
       nf++;
@@ -155,7 +268,7 @@ __global__ __launch_bounds__(256) void k_select_wave(SArgs a) {
   lds_fence();
   __builtin_amdgcn_wave_barrier();
   // pass 4: every chosen byte once
-  for (uint32_t p = lane; p < n; p += 64) ch[p] = (win[w][p >> 5] >> (p & 31)) & 1u;
+  write_chosen(ch, n, win[w], lane);
   for (int o = 32; o > 0; o >>= 1) nf += __shfl_xor(nf, o);
   if (lane == 0 && a.failed) a.failed[i] = nf;
 }
