@@ -15,7 +15,8 @@ VARIANTS = {
     "emit_u2": ["-DVMQG_EMIT_U=2"],
     "emit_u8": ["-DVMQG_EMIT_U=8"],
     "ss_u2": ["-DVMQS_UNROLL=2"],
-    "ss_narrow": ["-DVMQS_WIDE_CHOSEN=0"],
+    "ss_wpe1": ["-DVMQS_WAVES_PER_EU=1"],
+    "ss_wpe8_u8": ["-DVMQS_UNROLL=8"],
 }
 
 

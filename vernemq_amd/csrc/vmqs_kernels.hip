@@ -159,7 +159,13 @@ __device__ __forceinline__ void write_chosen(uint8_t* ch, uint32_t n, const uint
 #undef VMQS_BIT
 }
 
-__global__ __launch_bounds__(256) void k_select_wave(SArgs a) {
+#ifndef VMQS_WAVES_PER_EU
+#define VMQS_WAVES_PER_EU 8
+#endif
+// 8 waves per SIMD: the kernel is latency-bound, so residency (bytes in
+// flight) matters more than the registers the unrolled loop would take.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VMQS_WAVES_PER_EU, 8)))
+void k_select_wave(SArgs a) {
   __shared__ WSlot tab[kWaves][kWaveGroups];
   __shared__ uint32_t win[kWaves][kBitWords];
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
