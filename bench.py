@@ -46,11 +46,19 @@ def load_pmc_traffic(kernel: str, summary: str = "pmc_latest.json"):
     (e.g. "k_match_fast<1" = EMIT) from a committed rocprofv3 PMC summary
     (profiles/pmc_latest.json for config C, written by
     tools/summarize_prof.py), or None.  Read bytes are 2 x FETCH_SIZE (gfx950
-    correction), writes WRITE_SIZE."""
+    correction), writes WRITE_SIZE.  The summary must have been taken on the
+    library loaded now (same vmqg_build_id): a profile of other kernels is
+    not evidence for these, so a mismatch reports None."""
+    from vernemq_amd import _lib
     p = os.path.join(ROOT, "profiles", summary)
     try:
-        d = json.load(open(p))["kernels"]
+        doc = json.load(open(p))
+        d = doc["kernels"]
     except (OSError, KeyError, ValueError):
+        return None
+    if doc.get("build_id") != _lib.build_id():
+        log("PMC summary %s is of build %s, loaded library is %s: traffic not reported"
+            % (summary, doc.get("build_id"), _lib.build_id()))
         return None
     cands = [v for k, v in d.items() if kernel in k and "hbm_bytes_per_launch" in v]
     if not cands:
@@ -114,6 +122,7 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
+    from vernemq_amd import _lib
     from vernemq_amd import workloads as W
     from vernemq_amd.reg_view import RegGpuView
 
@@ -228,6 +237,55 @@ def main():
         log("end-to-end: %.3g publishes/s (%.2f ms per batch, %.1f GB/s over PCIe)"
             % (e2e["publishes_per_s"], e2e["ms_per_batch"], e2e["pcie_GBps"]))
         del h_out
+        # range mode (vmqg_match_ranges_device): one 8-B {record off, count}
+        # per non-empty key + {node, 0} per remote node come back instead of
+        # the records; the host walks them over its own record table
+        # (vmqg_records), as the NIF does before calling FoldFun
+        rng_cap = 4 * npub
+        d_rng = torch.empty(rng_cap * 2, dtype=torch.int32, device=dev)
+        d_roffs = torch.zeros(npub + 1, dtype=torch.int64, device=dev)
+        view.match_ranges_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_rng.data_ptr(), rng_cap,
+                                 d_roffs.data_ptr(), sp)
+        if view.match_status(sp) != 0:
+            raise RuntimeError("range-mode match status")
+        n_rng = int(d_roffs[-1].item())
+        h_roffs = torch.empty(npub + 1, dtype=torch.int64).pin_memory()
+        h_rng = torch.empty(n_rng * 2, dtype=torch.int32).pin_memory()
+
+        def e2e_ranges():
+            d_pubs.copy_(h_pubs, non_blocking=True)
+            d_words.copy_(h_words, non_blocking=True)
+            view.match_ranges_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_rng.data_ptr(), rng_cap,
+                                     d_roffs.data_ptr(), sp)
+            h_roffs.copy_(d_roffs, non_blocking=True)
+            h_rng.copy_(d_rng[: n_rng * 2], non_blocking=True)
+
+        e2e_ranges()
+        cur.synchronize()
+        reps = 20
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            e2e_ranges()
+        cur.synchronize()
+        el_r = (time.perf_counter() - t0) / reps
+        if view.match_status(sp) != 0 or int(h_roffs[-1]) != n_rng:
+            raise RuntimeError("range-mode end-to-end pass failed")
+        # the ranges expand to exactly the records of the device-resident pass
+        rng_np = h_rng.numpy().view(np.uint32).reshape(-1, 2)
+        want_cnt = np.diff(d_offs.cpu().numpy())
+        got_cnt = np.zeros(npub, dtype=np.int64)
+        per = np.where(rng_np[:, 1] > 0, rng_np[:, 1], 1).astype(np.int64)
+        np.add.at(got_cnt, np.repeat(np.arange(npub), np.diff(h_roffs.numpy())), per)
+        if not np.array_equal(got_cnt, want_cnt):
+            raise RuntimeError("range-mode entries do not expand to the record-mode counts")
+        pcie_r = h_pubs.numel() * 4 + h_words.numel() * 4 + h_roffs.numel() * 8 + n_rng * 8
+        e2e["ranges"] = {"publishes_per_s": npub / el_r, "ms_per_batch": el_r * 1e3, "pcie_bytes_per_batch": pcie_r,
+                         "pcie_GBps": pcie_r / el_r / 1e9, "entries_per_batch": n_rng,
+                         "note": "vmqg_match_ranges_device: H2D publishes + words, match, D2H offsets + %d "
+                                 "{record off, count} / {node, 0} entries (pinned host buffers, same stream); "
+                                 "records are read on the host from vmqg_records" % n_rng}
+        log("end-to-end (ranges): %.3g publishes/s (%.2f ms per batch, %d entries)"
+            % (npub / el_r, el_r * 1e3, n_rng))
 
     # max over ranks of the timed region; all-gather the per-GPU match counts
     t_max = elapsed
@@ -319,6 +377,7 @@ def main():
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "load_s": load_s,
+            "build_id": _lib.build_id(),
         }
         print(json.dumps(res), flush=True)
     if dist:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VMQG_ABI_VERSION 1
+#define VMQG_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------- */
 #define VMQG_OK 0
@@ -42,7 +42,8 @@ extern "C" {
 #define VMQG_E_OVERFLOW (-2)  /* output buffer too small: *out_n = required    */
 #define VMQG_E_NOMEM (-3)     /* host or device allocation failed             */
 #define VMQG_E_DEVICE (-4)    /* no device / HIP runtime error                */
-#define VMQG_E_FRONTIER (-5)  /* a publish exceeded the device scratch limits */
+#define VMQG_E_FRONTIER (-5)  /* a publish exceeded the device scratch (internal; vmqg_match_batch /
+                                 vmqg_match_ranges retry with a larger stack) */
 #define VMQG_E_LIMIT (-6)     /* a configured limit (nodes, mountpoints, ids)  */
 #define VMQG_E_STATE (-7)     /* call not valid for this context kind          */
 
@@ -53,7 +54,8 @@ extern "C" {
 #define VMQG_WORD_UNKNOWN 0xFFFFFFFFu  /* publish word never seen in a filter */
 #define VMQG_NONE 0xFFFFFFFFu
 
-#define VMQG_MAX_NODES 64u      /* cluster nodes addressable in a remote mask  */
+#define VMQG_MAX_NODES 4096u    /* cluster nodes (vmq_trie_remote_subs / node lists are unbounded in
+                                   the reference; 4,096 is this library's node-id space)            */
 
 /* ---- configuration --------------------------------------------------- */
 #define VMQG_CFG_REPLICA 1u     /* no host engine: device tables arrive as
@@ -62,7 +64,7 @@ extern "C" {
 typedef struct vmqg_config {
   int32_t device;            /* HIP device ordinal; -1 = host engine only     */
   uint32_t local_node;       /* node id that plays node() (< max_nodes)       */
-  uint32_t max_nodes;        /* <= VMQG_MAX_NODES                             */
+  uint32_t max_nodes;        /* <= VMQG_MAX_NODES (0 = VMQG_MAX_NODES)        */
   uint32_t max_mountpoints;  /* mountpoint ids are dense in [0, max)          */
   uint32_t flags;            /* VMQG_CFG_*                                    */
   uint32_t reserved;
@@ -127,14 +129,24 @@ typedef struct vmqg_stats_s {
   uint64_t rebuilds;        /* full device-image rebuilds                   */
   uint64_t paths;           /* interned trie paths (host)                   */
   uint64_t words;           /* interned words                               */
-  uint64_t deferred_tier1;  /* publishes of the last checked match batch that  */
-  uint64_t deferred_tier2;  /* overflowed the fast / the mid LDS lists         */
+  uint64_t deferred_tier1;  /* publishes of the last checked match batch walked */
+  uint64_t deferred_tier2;  /* by a whole wave (LDS stack) / with a global stack */
+  uint64_t ops_applied;     /* vmqg_apply_ops: ops applied so far               */
+  uint64_t apply_host_ns;   /*   host time inside vmqg_apply_ops (never waits on */
+                            /*   queued matches)                                 */
+  uint64_t patch_bytes;     /*   patch bytes shipped to the device               */
+  uint64_t image_bytes;     /*   full-image bytes shipped (re-layouts)           */
+  uint64_t max_depth;       /* deepest trie path (levels)                       */
 } vmqg_stats_t;
 
 /* ---- lifecycle ------------------------------------------------------- */
 typedef struct vmqg_ctx vmqg_ctx;
 
 int vmqg_abi_version(void);
+
+/* "vmqg-build:<16 hex>": sha256 of the sources and flags the library was
+ * compiled from (profiles/ summaries carry it; bench.py compares them). */
+const char* vmqg_build_id(void);
 
 /* Creates a context.  With cfg->device >= 0 the device arena is allocated on
  * that HIP device; device = -1 gives a host-engine-only context (tables are
@@ -190,10 +202,43 @@ int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub,
                       const uint32_t* d_words, vmqg_emit* d_out, uint64_t out_cap,
                       uint64_t* d_offsets, void* stream);
 
-/* Synchronises `stream` and returns the latched status of the previous
- * vmqg_match_device calls (VMQG_OK, VMQG_E_OVERFLOW, VMQG_E_FRONTIER),
- * clearing it. */
+/* Synchronises `stream` and returns the status latched by every
+ * vmqg_match_device / vmqg_match_ranges_device call since the previous
+ * vmqg_match_status (VMQG_OK, VMQG_E_OVERFLOW, VMQG_E_FRONTIER,
+ * VMQG_E_DEVICE), then clears it: an error of any call in a pipelined
+ * sequence is reported, not only the last call's. */
 int vmqg_match_status(vmqg_ctx* ctx, void* stream);
+
+/* ---- range mode ------------------------------------------------------ */
+/* Range-mode matching returns, instead of copies of the records, one 8-byte
+ * entry per non-empty subscriber-list key (`lookup_subs/1`,
+ * vmq_reg_trie.erl:87-94) and per remote node: count > 0 — the records
+ * [off, off + count) of the context's record table (vmqg_records); count ==
+ * 0 — the remote node `off` (kind C, once per publish as fold_/5 :78-84).
+ * Expanding the ranges in order gives the same emission multiset as
+ * vmqg_match_batch; a publish with 65 emissions in config C is 2 entries.
+ *   Replaces: vmq_reg_trie:fold/4 (:59-98) for a batch, FoldFun-side expansion. */
+typedef struct vmqg_range {
+  uint32_t off;    /* record index, or node id when count == 0 */
+  uint32_t count;
+} vmqg_range;
+
+/* Host-buffer range match: offsets[0..npub] = exclusive prefix of the
+ * per-publish entry counts; VMQG_E_OVERFLOW with *out_n = total when
+ * out_cap is too small.  Synchronous. */
+int vmqg_match_ranges(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const uint32_t* words,
+                      size_t nwords, vmqg_range* out, size_t out_cap, size_t* out_n,
+                      uint64_t* offsets);
+
+/* Device-buffer range match (as vmqg_match_device). */
+int vmqg_match_ranges_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub,
+                             const uint32_t* d_words, vmqg_range* d_out, uint64_t out_cap,
+                             uint64_t* d_offsets, void* stream);
+
+/* Host view of the record table the ranges index (the host mirror of the
+ * device arena's records, byte-identical at the last vmqg_apply_ops).  Valid
+ * until the next vmqg_apply_ops on the context; primary contexts only. */
+int vmqg_records(vmqg_ctx* ctx, const vmqg_emit** recs, uint64_t* n);
 
 /* ---- introspection --------------------------------------------------- */
 int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out);
@@ -204,11 +249,8 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out);
 int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
 
 /* Tuning knobs of the match kernels (no effect on results):
- *   "fast_g"    2 | 4 | 8  lanes per publish in the fast tier (default 2)
- *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
- *   "fused"     0 | 1      1: one-pass kernel (walk, count, look-back offsets,
- *                          emit in one launch); 0 (default): COUNT / scan / EMIT
- *   "unroll"    4 | 8      records in flight per lane in the copy (default 4) */
+ *   "fast_g"    2 | 4      lanes per publish in the fast tier (default 2)
+ *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the dominant match kernel over the last
@@ -234,6 +276,11 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
  * (records of 24 bytes) valid until the next apply; *full_image = 1 when the
  * apply re-laid out the arena (replicas must reload the full image instead). */
 int vmqg_last_patches(vmqg_ctx* ctx, const void** host_ptr, uint64_t* bytes, int* full_image);
+
+/* Replica side: adopt the fields of the primary's layout that change without
+ * a re-layout (the trie depth that sizes the wave tier's stack); every
+ * region must match the replica's (else VMQG_E_STATE: reload the image). */
+int vmqg_replica_sync_layout(vmqg_ctx* ctx, const uint8_t* layout);
 
 /* Replica side: apply patch records already in device memory on `stream`. */
 int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t bytes, void* stream);

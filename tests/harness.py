@@ -20,20 +20,32 @@ def canon(entry):
 
 
 class ProductDriver:
-    """RegGpuView with the oracle's test interface.  device=-1: host engine only."""
+    """RegGpuView with the oracle's test interface.  device=-1: host engine only.
+    mode "records": vmqg_match_batch (16-B FoldFun records); "ranges":
+    vmqg_match_ranges, expanded on the host against vmqg_records."""
 
-    def __init__(self, node: str, device: int = 0, **kw):
+    def __init__(self, node: str, device: int = 0, mode: str = "records", **kw):
         from vernemq_amd.reg_view import RegGpuView
         self.view = RegGpuView(node=node, device=device, **kw)
+        self.mode = mode
 
     def apply(self, events):
         self.view.handle_events(events)
 
     def fold(self, mp, topic):
-        return [canon(e) for e in self.view.fold_batch([(mp, tuple(topic))])[0]]
+        return self.fold_batch([(mp, tuple(topic))])[0]
+
+    def match_arrays(self, pubs, words):
+        if self.mode == "ranges":
+            rng, offs = self.view.match_ranges(pubs, words)
+            return self.view.expand_ranges(rng, offs)
+        return self.view.match_arrays(pubs, words)
 
     def fold_batch(self, pubs):
-        return [[canon(e) for e in em] for em in self.view.fold_batch(pubs)]
+        v = self.view
+        arr, words = v.prepare([(mp, t if isinstance(t, (bytes, bytearray)) else tuple(t)) for mp, t in pubs])
+        recs, offs = self.match_arrays(arr, words)
+        return [[canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1]))] for i in range(len(arr))]
 
 
 def _esc(s) -> str:

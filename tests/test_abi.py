@@ -32,24 +32,27 @@ def test_every_declared_symbol_is_exported():
     assert not missing, missing
     bound = {name for name, _, _ in _lib.SIGNATURES}
     assert set(decl) == bound, set(decl) ^ bound
-    assert L.vmqg_abi_version() == 1
+    assert L.vmqg_abi_version() == 2
 
 
 def test_struct_layouts_match_header(tmp_path):
     prog = tmp_path / "sz.c"
     prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "vmqg.h"\n'
-                    'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(vmqg_config),'
+                    'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %u\\n", sizeof(vmqg_config),'
                     ' sizeof(vmqg_op), sizeof(vmqg_pub), sizeof(vmqg_emit), sizeof(vmqg_stats_t),'
-                    ' offsetof(vmqg_config, hint_edges), offsetof(vmqg_op, subinfo));return 0;}\n')
+                    ' offsetof(vmqg_config, hint_edges), offsetof(vmqg_op, subinfo), sizeof(vmqg_range),'
+                    ' VMQG_MAX_NODES);return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(prog),
                     "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.Op), ctypes.sizeof(_lib.Pub), ctypes.sizeof(_lib.Emit),
-            ctypes.sizeof(_lib.Stats), _lib.Config.hint_edges.offset, _lib.Op.subinfo.offset]
+            ctypes.sizeof(_lib.Stats), _lib.Config.hint_edges.offset, _lib.Op.subinfo.offset,
+            ctypes.sizeof(_lib.Range), _lib.MAX_NODES]
     assert got == want
-    from vernemq_amd.reg_view import EMIT_DTYPE, OP_DTYPE, PUB_DTYPE
-    assert (OP_DTYPE.itemsize, PUB_DTYPE.itemsize, EMIT_DTYPE.itemsize) == (got[1], got[2], got[3])
+    from vernemq_amd.reg_view import EMIT_DTYPE, OP_DTYPE, PUB_DTYPE, RANGE_DTYPE
+    assert (OP_DTYPE.itemsize, PUB_DTYPE.itemsize, EMIT_DTYPE.itemsize, RANGE_DTYPE.itemsize) == \
+        (got[1], got[2], got[3], got[7])
 
 
 def test_acl_struct_layouts_match_header(tmp_path):
@@ -143,6 +146,12 @@ def test_host_only_context_refuses_to_match():
     with pytest.raises(_lib.VmqgError) as ei:
         v.fold_batch([("", (b"a",))])
     assert ei.value.rc == _lib.E_DEVICE
+    with pytest.raises(_lib.VmqgError) as ei:
+        v.match_ranges(*v.prepare([("", (b"a",))]))
+    assert ei.value.rc == _lib.E_DEVICE
+    # the record table the ranges index is the host mirror
+    recs = v.records()
+    assert len(recs) > 0 and (recs["kind_node"] >> 24 == _lib.EMIT_LOCAL).sum() == 1
 
 
 def test_create_rejects_bad_config():
@@ -152,6 +161,9 @@ def test_create_rejects_bad_config():
     cfg.local_node = 70
     cfg.max_nodes = 64
     err = ctypes.c_int(0)
+    assert not L.vmqg_create(ctypes.byref(cfg), ctypes.byref(err))
+    assert err.value == _lib.E_LIMIT
+    cfg.local_node, cfg.max_nodes = 0, _lib.MAX_NODES + 1
     assert not L.vmqg_create(ctypes.byref(cfg), ctypes.byref(err))
     assert err.value == _lib.E_LIMIT
     assert not L.vmqg_create(None, ctypes.byref(err))

@@ -4,8 +4,6 @@ Bar: bit-exact — for every publish the sorted multiset of FoldFun entries
 equals vmq_reg_trie:fold/4's (restated by the oracle).  Sizes the oracle
 finishes in seconds are compared publish-for-publish; the full config C is
 checked by size-independent properties plus an oracle sample."""
-import ctypes
-
 import numpy as np
 import pytest
 
@@ -20,15 +18,13 @@ SCEN_FILES = ["pattern_matching.json", "upgrade.json", "overlapping_subscription
               "dollar_topics.json", "shared_subscriptions.json", "quirks.json"]
 
 
-# Both match pipelines of libvmqgpu: the one-pass kernel (default) and the
-# COUNT / scan / EMIT passes (vmqg_set_option "fused").
-PIPELINES = [pytest.param(1, id="fused"), pytest.param(0, id="passes")]
+# Both output modes of libvmqgpu: 16-B FoldFun records (vmqg_match_batch)
+# and key ranges expanded on the host (vmqg_match_ranges + vmqg_records).
+MODES = ["records", "ranges"]
 
 
-def _driver(node, fused=1, **kw):
-    d = H.ProductDriver(node, device=0, **kw)
-    d.view.set_option("fused", fused)
-    return d
+def _driver(node, mode="records", **kw):
+    return H.ProductDriver(node, device=0, mode=mode, **kw)
 
 
 def _scen():
@@ -45,10 +41,10 @@ def test_native_library_is_the_in_tree_build():
     assert v.stats_raw()["device_bytes"] > 0
 
 
-@pytest.mark.parametrize("fused", PIPELINES)
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("scen", list(_scen()))
-def test_golden_scenarios_on_gpu(scen, fused):
-    S.run_scenario(scen, lambda node: _driver(node, fused))
+def test_golden_scenarios_on_gpu(scen, mode):
+    S.run_scenario(scen, lambda node: _driver(node, mode))
 
 
 def _compare_batches(prod, orc, pubs, ctx=""):
@@ -58,11 +54,11 @@ def _compare_batches(prod, orc, pubs, ctx=""):
         assert sorted(g) == sorted(w), "%s publish %r: got %r want %r" % (ctx, pubs[i], sorted(g)[:8], sorted(w)[:8])
 
 
-@pytest.mark.parametrize("fused", PIPELINES)
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("seed", range(4))
-def test_random_churn_fold_parity(seed, fused):
+def test_random_churn_fold_parity(seed, mode):
     wl = H.ChurnWorkload(seed, n_clients=60)
-    prod = _driver(wl.self_node, fused)
+    prod = _driver(wl.self_node, mode)
     orc = O.TrieOracle(wl.self_node)
     for step in range(20):
         evs = [wl.event() for _ in range(25)]
@@ -71,10 +67,9 @@ def test_random_churn_fold_parity(seed, fused):
         _compare_batches(prod, orc, wl.publishes(200), "seed %d batch %d" % (seed, step))
 
 
-def _load_both(w, with_oracle=True, fused=1):
+def _load_both(w, with_oracle=True):
     from vernemq_amd.reg_view import RegGpuView
     v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
-    v.set_option("fused", fused)
     w.load_into(v)
     orc = None
     if with_oracle:
@@ -82,21 +77,28 @@ def _load_both(w, with_oracle=True, fused=1):
     return v, orc
 
 
-def _gpu_canon(v, w, lo, hi):
+def _match(v, pubs, words, mode="records", **kw):
+    if mode == "ranges":
+        rng, offs = v.match_ranges(pubs, words)
+        return v.expand_ranges(rng, offs)
+    return v.match_arrays(pubs, words, **kw)
+
+
+def _gpu_canon(v, w, lo, hi, mode="records"):
     pubs, words = w.publish_arrays(v, lo, hi)
-    recs, offs = v.match_arrays(pubs, words)
+    recs, offs = _match(v, pubs, words, mode)
     return [sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
             for i in range(hi - lo)]
 
 
-@pytest.mark.parametrize("fused", PIPELINES)
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("cfg", ["A", "B"])
-def test_config_full_parity(cfg, fused):
+def test_config_full_parity(cfg, mode):
     from vernemq_amd import workloads as W
     w = W.CONFIGS[cfg]()
-    v, orc = _load_both(w, fused=fused)
+    v, orc = _load_both(w)
     n = w.n_pubs
-    got = _gpu_canon(v, w, 0, n)
+    got = _gpu_canon(v, w, 0, n, mode)
     want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in range(n)])
     bad = [i for i in range(n) if got[i] != sorted(want[i])]
     assert not bad, "config %s: %d/%d publishes differ, first %r: got %r want %r" % (
@@ -145,6 +147,17 @@ def test_config_c_full_size():
     got = _gpu_canon(vs, ws, 0, ws.n_pubs)
     want = orc.fold_batch([("", b"pub", ws.pub_topic(i)) for i in range(ws.n_pubs)])
     assert all(g == sorted(x) for g, x in zip(got, want))
+    # range mode on the full batch: 2 entries per hit publish (the wildcard
+    # list + the device's own key), 1 per miss; expands to the same records
+    rng, roffs = v.match_ranges(pubs, words, out_cap=2 * w.n_pubs)
+    assert np.array_equal(np.diff(roffs.astype(np.int64)), np.where(hit, 2, 1))
+    assert np.all(rng["count"] > 0)
+    erec, eoffs = v.expand_ranges(rng, roffs)
+    assert np.array_equal(eoffs, offs)
+    for idx in np.linspace(0, len(counts) - 1, 500).astype(np.int64):
+        a = np.sort(erec["subscriber"][offs[idx]:offs[idx + 1]])
+        b = np.sort(recs["subscriber"][offs[idx]:offs[idx + 1]])
+        assert np.array_equal(a, b), idx
 
 
 def test_r1_r2_bench_shapes():
@@ -168,16 +181,17 @@ def test_r1_r2_bench_shapes():
     assert st["subs_objects"] == 0 and st["fanout_objects"] == 0
 
 
-@pytest.mark.parametrize("fused", PIPELINES)
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("levels,tier", [(7, 1), (10, 2)])
-def test_wide_frontier_deferred_tiers(levels, tier, fused):
+def test_wide_frontier_deferred_tiers(levels, tier, mode):
     """2^levels filters over {x, +} at every level: the frontier / candidate
-    lists overflow the fast tier's LDS lists (levels 7: the mid tier takes
-    them) or also the mid tier's (levels 10: global-memory scratch).  The
-    one-pass kernel has one such path: a whole wave with global scratch."""
+    lists overflow the fast tier's LDS lists, so a whole wave walks the
+    publish, streaming candidates and keys through bounded LDS buffers;
+    levels 7: its frontier stack fits LDS (tier 1); levels 10: the stack
+    moves to global memory (tier 2)."""
     import itertools
     node = "n@h"
-    prod = _driver(node, fused)
+    prod = _driver(node, mode)
     orc = O.TrieOracle(node)
     subs = []
     for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=levels)):
@@ -191,14 +205,90 @@ def test_wide_frontier_deferred_tiers(levels, tier, fused):
     _compare_batches(prod, orc, pubs, "wide%d" % levels)
     st = prod.view.stats_raw()
     assert st["deferred_tier1"] >= 1
-    assert (st["deferred_tier2"] >= 1) == (tier == 2 and not fused)
+    assert (st["deferred_tier2"] >= 1) == (tier == 2)
     assert len(prod.fold(*pubs[0])) > 64
 
 
-@pytest.mark.parametrize("fused", PIPELINES)
-def test_long_topics(fused):
+def test_frontier_2_16_is_answered():
+    """A 2^16-wide frontier (16 levels of {x, +}: 65,536 filters all matching
+    x^16) — vmq_reg_trie's trie_match/4 (:358-383) always answers; so must
+    the product (the wave tier streams its candidates, the stack is sized
+    from the trie depth)."""
+    import itertools
     node = "n@h"
-    prod = _driver(node, fused)
+    prod = _driver(node)
+    orc = O.TrieOracle(node)
+    subs = [("updated", ("", b"s%d" % i), None, [(node, True, [(combo, i % 3)])])
+            for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=16))]
+    for lo in range(0, len(subs), 8192):
+        prod.apply(subs[lo:lo + 8192])
+        orc.apply(subs[lo:lo + 8192])
+    pubs = [("", (b"x",) * 16), ("", (b"x", b"y") * 8), ("", (b"y",) * 16), ("", (b"x",) * 15)]
+    _compare_batches(prod, orc, pubs, "2^16")
+    assert len(prod.fold(*pubs[0])) == 1 << 16
+    assert prod.view.stats_raw()["deferred_tier2"] >= 1
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_cluster_of_100_nodes(mode):
+    """Remote subscriptions from 100 nodes (ids beyond the 64-bit inline
+    masks): get_remote_subscribers/2 and the wildcard node lists
+    (vmq_reg_trie.erl:503-520, :78-84) — each remote node once per publish,
+    in any mix of exact and wildcard matches."""
+    import random
+    r = random.Random(100)
+    nodes = ["n%d@h" % i for i in range(100)]
+    node = nodes[0]
+    prod = _driver(node, mode, nodes=nodes)
+    orc = O.TrieOracle(node)
+    filters = [(b"a", b"b"), (b"a", b"+"), (b"a", b"#"), (b"+", b"b"), (b"#",), (b"a", b"b", b"c"),
+               (b"x", b"y"), (b"$share", b"g", b"a", b"+")]
+    evs = []
+    for i in range(400):
+        n = r.choice(nodes)
+        evs.append(("updated", ("", b"c%d" % i), None, [(n, True, [(r.choice(filters), r.randint(0, 2))])]))
+    prod.apply(evs)
+    orc.apply(evs)
+    pubs = [("", t) for t in [(b"a", b"b"), (b"a", b"q"), (b"z", b"b"), (b"a", b"b", b"c"), (b"x", b"y"),
+                              (b"q",), (b"$SYS", b"b")]]
+    _compare_batches(prod, orc, pubs, "100 nodes")
+    got = prod.fold("", (b"a", b"b"))
+    remotes = [e for e in got if e[0] == "C"]
+    assert len(remotes) == len(set(remotes)) > 64
+    # deletes shrink the node lists again
+    dels = [("deleted", ev[1], ev[3]) for ev in evs[::2]]
+    prod.apply(dels)
+    orc.apply(dels)
+    _compare_batches(prod, orc, pubs, "100 nodes after deletes")
+
+
+def test_match_status_errors_are_sticky():
+    """An overflow in one of several pipelined vmqg_match_device calls is
+    still reported by the vmqg_match_status after the last one."""
+    import torch
+    prod = _driver("n@h")
+    v = prod.view
+    v.handle_events([("updated", ("", b"c%d" % i), None, [("n@h", True, [((b"t",), 0)])]) for i in range(100)])
+    pubs, words = v.prepare([("", (b"t",))] * 4)
+    dev = torch.device("cuda:0")
+    d_pubs = torch.from_numpy(pubs.view(np.uint32).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    d_out = torch.zeros(400 * 4, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(5, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+    v.match_device(d_pubs.data_ptr(), 4, d_words.data_ptr(), d_out.data_ptr(), 10, d_offs.data_ptr(), sp)   # overflows
+    v.match_device(d_pubs.data_ptr(), 4, d_words.data_ptr(), d_out.data_ptr(), 400, d_offs.data_ptr(), sp)  # clean
+    from vernemq_amd import _lib
+    assert v.match_status(sp) == _lib.E_OVERFLOW
+    v.match_device(d_pubs.data_ptr(), 4, d_words.data_ptr(), d_out.data_ptr(), 400, d_offs.data_ptr(), sp)
+    assert v.match_status(sp) == 0
+    assert int(d_offs[-1].item()) == 400
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_long_topics(mode):
+    node = "n@h"
+    prod = _driver(node, mode)
     orc = O.TrieOracle(node)
     long_t = tuple(b"w%d" % (i % 7) for i in range(150))
     evs = [("updated", ("", b"a"), None, [(node, True, [(long_t, 1), (long_t[:80] + (b"#",), 0),
@@ -223,9 +313,8 @@ def test_mountpoints_are_disjoint_roots():
     _compare_batches(prod, orc, pubs, "mp")
 
 
-@pytest.mark.parametrize("fused", PIPELINES)
-def test_empty_batch_and_output_growth(fused):
-    prod = _driver("n@h", fused)
+def test_empty_batch_and_output_growth():
+    prod = _driver("n@h")
     v = prod.view
     v.handle_events([("updated", ("", b"c%d" % i), None, [("n@h", True, [((b"t",), 0)])]) for i in range(5000)])
     recs, offs = v.match_arrays(*v.prepare([]))
@@ -264,6 +353,7 @@ def test_replica_follows_primary_by_image_and_patches():
     """A replica context fed the primary's arena image and then its patch
     stream answers identically (the RCCL broadcast payloads, minus RCCL)."""
     import torch
+    from vernemq_amd import dist as vd
     wl = H.ChurnWorkload(7, n_clients=50)
     prim = H.ProductDriver(wl.self_node, device=0)
     from vernemq_amd.reg_view import RegGpuView
@@ -273,9 +363,7 @@ def test_replica_follows_primary_by_image_and_patches():
     # D2D copy of the primary arena into a torch buffer (the RCCL broadcast
     # buffer in bench.py), then into the replica
     img = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
-    lib = ctypes.CDLL("libamdhip64.so")
-    lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    assert lib.hipMemcpy(img.data_ptr(), ptr, nbytes, 3) == 0
+    vd.hip_memcpy_d2d(img.data_ptr(), ptr, nbytes)
     rep.replica_load(lay, img.data_ptr())
     torch.cuda.synchronize()
     for step in range(10):
@@ -284,10 +372,11 @@ def test_replica_follows_primary_by_image_and_patches():
         if full:
             ptr, nbytes, lay = prim.view.arena()
             img = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
-            assert lib.hipMemcpy(img.data_ptr(), ptr, nbytes, 3) == 0
+            vd.hip_memcpy_d2d(img.data_ptr(), ptr, nbytes)
             rep.replica_load(lay, img.data_ptr())
         elif data:
             buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda:0")
+            rep.replica_sync_layout(prim.view.arena()[2])
             rep.apply_patches_device(buf.data_ptr(), len(data))
         torch.cuda.synchronize()
         pubs = wl.publishes(100)
@@ -331,8 +420,8 @@ def _config_d_expected_counts(w, live, pubs_lo, pubs_hi):
     return np.array(out, dtype=np.int64)
 
 
-@pytest.mark.parametrize("fused", PIPELINES)
-def test_config_d_churn_parity(fused):
+@pytest.mark.parametrize("mode", MODES)
+def test_config_d_churn_parity(mode):
     """Config D at 1/20 scale (500k subs incl. $share groups over 4 nodes):
     after every churn batch, all publishes match the known answer and a
     sample matches the oracle publish for publish."""
@@ -340,7 +429,6 @@ def test_config_d_churn_parity(fused):
     from vernemq_amd.reg_view import RegGpuView
     w = W.config_d(scale=0.05, n_pubs=20_000)
     v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
-    v.set_option("fused", fused)
     ids = w.load_into(v, n=w.notes["n_live"])
     orc = feed.load_prefix(w, w.notes["n_live"])
     ch = W.Churn(w)
@@ -351,7 +439,7 @@ def test_config_d_churn_parity(fused):
             ops, wds = ch.ops(ids, dels, adds)
             v.apply_op_arrays(ops, wds)
             orc.apply(ch.events(dels, adds))
-        recs, offs = v.match_arrays(pubs, words)
+        recs, offs = _match(v, pubs, words, mode)
         counts = np.diff(offs.astype(np.int64))
         assert np.array_equal(counts, _config_d_expected_counts(w, ch.live, 0, w.n_pubs)), step
         sample = list(range(0, w.n_pubs, 40))
@@ -360,14 +448,14 @@ def test_config_d_churn_parity(fused):
         assert all(g == sorted(x) for g, x in zip(got, want)), step
 
 
-@pytest.mark.parametrize("fused", PIPELINES)
-def test_config_e_multitenant_parity(fused):
+@pytest.mark.parametrize("mode", MODES)
+def test_config_e_multitenant_parity(mode):
     """Config E shape at 1/500 scale (100k subs over 1,000 Zipf-sized
     mountpoints, 12-level topics, hot-topic skew): every publish vs the oracle."""
     from vernemq_amd import workloads as W
     w = W.config_e(scale=0.002, n_pubs=8192)
-    v, orc = _load_both(w, fused=fused)
-    got = _gpu_canon(v, w, 0, w.n_pubs)
+    v, orc = _load_both(w)
+    got = _gpu_canon(v, w, 0, w.n_pubs, mode)
     want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in range(w.n_pubs)])
     bad = [i for i in range(w.n_pubs) if got[i] != sorted(want[i])]
     assert not bad, (len(bad), w.pub_topic(bad[0]))

@@ -10,6 +10,8 @@ usage: summarize_prof.py <stats_dir> <fetch_dir> <write_dir> <out_json> [tag] [l
   §HBM): FETCH_SIZE reads half of a wide coalesced read stream, so the
   corrected read bytes are 2 x FETCH_SIZE; WRITE_SIZE is exact for 16-B/lane
   streaming stores.  Both raw and corrected numbers are kept;
+* the build id of the profiled libvmqgpu.so (vmqg_build_id), which bench.py
+  requires to equal the loaded library's before it reports `traffic`;
 * optional passes: L2 hit rate TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum),
   LDS bank conflicts SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (cycles).
 """
@@ -86,7 +88,12 @@ def main():
             ent["lds_bank_conflict_frac"] = bank[name] / ldsact[name]
             ent["lds_bank_conflict_cycles"] = bank[name]
         kernels[short] = ent
-    json.dump({"tag": tag, "kernels": kernels,
+    build_id = os.environ.get("BUILD_ID")
+    if not build_id:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from vernemq_amd import _lib
+        build_id = _lib.build_id()
+    json.dump({"tag": tag, "build_id": build_id, "kernels": kernels,
                "notes": "rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE, --pmc WRITE_SIZE, "
                         "--pmc TCC_HIT_sum TCC_MISS_sum and --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE runs "
                         "of the same bench command; read bytes = 2 x FETCH_SIZE (gfx950 correction)"},

@@ -7,6 +7,7 @@ If ``libvmqgpu.so`` is missing, :func:`lib` raises ``ImportError`` (call
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import subprocess
 
@@ -37,7 +38,7 @@ PUB_DOLLAR = 1
 EMIT_LOCAL, EMIT_GROUP, EMIT_REMOTE = 1, 2, 3
 CFG_REPLICA = 1
 LAYOUT_BYTES = 256
-MAX_NODES = 64
+MAX_NODES = 4096
 
 
 class VmqgError(RuntimeError):
@@ -68,11 +69,16 @@ class Emit(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in ("kind_node", "group", "subscriber", "subinfo")]
 
 
+class Range(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("off", "count")]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("subs", "device_bytes", "trie_edges", "trie_nodes", "trie_topics", "subs_objects",
                  "fanout_objects", "remote_keys", "epoch", "rebuilds", "paths", "words",
-                 "deferred_tier1", "deferred_tier2")]
+                 "deferred_tier1", "deferred_tier2", "ops_applied", "apply_host_ns", "patch_bytes",
+                 "image_bytes", "max_depth")]
 
 
 class RConfig(ctypes.Structure):
@@ -118,6 +124,7 @@ _P = ctypes.c_void_p
 _U32, _U64, _SZ = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 SIGNATURES = [
     ("vmqg_abi_version", ctypes.c_int, []),
+    ("vmqg_build_id", ctypes.c_char_p, []),
     ("vmqg_create", _P, [ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_int)]),
     ("vmqg_destroy", None, [_P]),
     ("vmqg_intern_words", ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
@@ -126,6 +133,10 @@ SIGNATURES = [
     ("vmqg_match_batch", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
     ("vmqg_match_device", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),
     ("vmqg_match_status", ctypes.c_int, [_P, _P]),
+    ("vmqg_match_ranges", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
+    ("vmqg_match_ranges_device", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),
+    ("vmqg_records", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
+    ("vmqg_replica_sync_layout", ctypes.c_int, [_P, _P]),
     ("vmqg_stats", ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
     ("vmqg_dump", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_SZ)]),
     ("vmqg_set_option", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int64]),
@@ -179,11 +190,33 @@ SIGNATURES = [
 _lib = None
 
 
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+         "-Wall", "-Wno-unused-value", "-Wno-unused-result"]
+
+
+def source_id() -> str:
+    """Build id of the current sources: sha256 over every source and header
+    the library is compiled from, plus the compile flags (16 hex digits).
+    Embedded in the library (vmqg_build_id), recorded in every profile
+    summary, and compared by bench.py before a PMC figure is reported."""
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for p in sorted(DEPS):
+        h.update(os.path.relpath(p, ROOT).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def _stale() -> bool:
     if not os.path.exists(LIB_PATH):
         return True
-    t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(s) > t for s in DEPS if os.path.exists(s))
+    with open(LIB_PATH, "rb") as f:
+        return ("vmqg-build:" + source_id()).encode() not in f.read()
+
+
+def build_id() -> str:
+    """Build id embedded in the loaded library."""
+    return lib().vmqg_build_id().decode().split(":", 1)[-1]
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -191,9 +224,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-value", "-Wno-unused-result",
-           "-o", LIB_PATH + ".tmp"] + SOURCES
+    cmd = [hipcc] + FLAGS + ['-DVMQG_BUILD_ID="vmqg-build:%s"' % source_id(),
+                             "-o", LIB_PATH + ".tmp"] + SOURCES
     r = subprocess.run(cmd, capture_output=not verbose, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed:\n%s" % (r.stderr if not verbose else ""))

@@ -1,5 +1,6 @@
 // extern "C" boundary of libvmqgpu (include/vmqg.h).  No C++ exception and
 // no torch type crosses it; every entry point maps onto the Engine.
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <new>
@@ -25,6 +26,11 @@ struct vmqg_ctx {
 extern "C" {
 
 int vmqg_abi_version(void) { return VMQG_ABI_VERSION; }
+
+#ifndef VMQG_BUILD_ID
+#define VMQG_BUILD_ID "vmqg-build:unknown"
+#endif
+const char* vmqg_build_id(void) { return VMQG_BUILD_ID; }
 
 vmqg_ctx* vmqg_create(const vmqg_config* cfg, int* err) {
   int rc = VMQG_OK;
@@ -105,12 +111,13 @@ static int grow(void** p, uint64_t* cap, uint64_t need) {
   return VMQG_OK;
 }
 
-int vmqg_match_batch(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const uint32_t* words, size_t nwords,
-                     vmqg_emit* out, size_t out_cap, size_t* out_n, uint64_t* offsets) {
-  if (!ctx || !offsets || (npub && !pubs) || (nwords && !words) || (out_cap && !out)) return VMQG_E_INVAL;
-  if (npub > 0xFFFFFFF0u) return VMQG_E_LIMIT;
-  GUARD_BEGIN
-  Engine& e = ctx->e;
+// Host-buffer match in records (esz 16) or range (esz 8) mode: stage the
+// batch, match on the context stream, copy offsets (and, when they fit, the
+// entries) back.  A tier-2 stack overflow (never expected: the stack is
+// sized from the trie depth) is retried with a 4x larger stack, so a
+// publish the reference answers is never refused.
+static int match_host(Engine& e, const vmqg_pub* pubs, size_t npub, const uint32_t* words, size_t nwords,
+                      void* out, size_t esz, size_t out_cap, size_t* out_n, uint64_t* offsets) {
   if (!e.has_device) return VMQG_E_DEVICE;
   for (size_t i = 0; i < npub; i++)
     if (pubs[i].nwords == 0 || (uint64_t)pubs[i].word_off + pubs[i].nwords > nwords) return VMQG_E_INVAL;
@@ -119,26 +126,47 @@ int vmqg_match_batch(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const uin
   if ((rc = grow(&e.d_pubs, &e.d_pubs_cap, (npub + 1) * sizeof(vmqg_pub)))) return rc;
   if ((rc = grow(&e.d_words, &e.d_words_cap, (nwords + 1) * sizeof(uint32_t)))) return rc;
   if ((rc = grow(&e.d_offs, &e.d_offs_cap, (npub + 1) * sizeof(uint64_t)))) return rc;
-  if ((rc = grow(&e.d_out, &e.d_out_cap, (out_cap + 1) * sizeof(vmqg_emit)))) return rc;
+  if ((rc = grow(&e.d_out, &e.d_out_cap, (out_cap + 1) * esz))) return rc;
   hipStream_t st = e.stream;
   if (npub && hipMemcpyAsync(e.d_pubs, pubs, npub * sizeof(vmqg_pub), hipMemcpyHostToDevice, st) != hipSuccess)
     return VMQG_E_DEVICE;
   if (nwords && hipMemcpyAsync(e.d_words, words, nwords * 4, hipMemcpyHostToDevice, st) != hipSuccess)
     return VMQG_E_DEVICE;
-  rc = e.match_device(static_cast<const vmqg_pub*>(e.d_pubs), (uint32_t)npub,
-                      static_cast<const uint32_t*>(e.d_words), static_cast<vmqg::Record*>(e.d_out), out_cap,
-                      static_cast<uint64_t*>(e.d_offs), st);
-  if (rc) return rc;
-  if (hipMemcpyAsync(offsets, e.d_offs, (npub + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st) != hipSuccess)
-    return VMQG_E_DEVICE;
-  rc = e.match_status(st);
+  for (int attempt = 0;; attempt++) {
+    vmqg::Record* rec = esz == sizeof(vmqg_emit) ? static_cast<vmqg::Record*>(e.d_out) : nullptr;
+    vmqg_range* rng = esz == sizeof(vmqg_range) ? static_cast<vmqg_range*>(e.d_out) : nullptr;
+    rc = e.match_device(static_cast<const vmqg_pub*>(e.d_pubs), (uint32_t)npub, static_cast<const uint32_t*>(e.d_words),
+                        rec, rec ? out_cap : 0, rng, rng ? out_cap : 0, static_cast<uint64_t*>(e.d_offs), st);
+    if (rc) return rc;
+    if (hipMemcpyAsync(offsets, e.d_offs, (npub + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st) != hipSuccess)
+      return VMQG_E_DEVICE;
+    rc = e.match_status(st);
+    if (rc != VMQG_E_FRONTIER || attempt >= 6) break;
+    e.o_cap_floor = std::max<uint64_t>(e.o_cap_floor, (uint64_t)e.o_cap * 4);
+  }
   const uint64_t total = offsets[npub];
   if (out_n) *out_n = total;
   if (rc == VMQG_E_OVERFLOW || total > out_cap) return VMQG_E_OVERFLOW;
   if (rc) return rc;
-  if (total && hipMemcpy(out, e.d_out, total * sizeof(vmqg_emit), hipMemcpyDeviceToHost) != hipSuccess)
-    return VMQG_E_DEVICE;
+  if (total && hipMemcpy(out, e.d_out, total * esz, hipMemcpyDeviceToHost) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
+}
+
+int vmqg_match_batch(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const uint32_t* words, size_t nwords,
+                     vmqg_emit* out, size_t out_cap, size_t* out_n, uint64_t* offsets) {
+  if (!ctx || !offsets || (npub && !pubs) || (nwords && !words) || (out_cap && !out)) return VMQG_E_INVAL;
+  if (npub > 0xFFFFFFF0u) return VMQG_E_LIMIT;
+  GUARD_BEGIN
+  return match_host(ctx->e, pubs, npub, words, nwords, out, sizeof(vmqg_emit), out_cap, out_n, offsets);
+  GUARD_END
+}
+
+int vmqg_match_ranges(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const uint32_t* words, size_t nwords,
+                      vmqg_range* out, size_t out_cap, size_t* out_n, uint64_t* offsets) {
+  if (!ctx || !offsets || (npub && !pubs) || (nwords && !words) || (out_cap && !out)) return VMQG_E_INVAL;
+  if (npub > 0xFFFFFFF0u) return VMQG_E_LIMIT;
+  GUARD_BEGIN
+  return match_host(ctx->e, pubs, npub, words, nwords, out, sizeof(vmqg_range), out_cap, out_n, offsets);
   GUARD_END
 }
 
@@ -146,9 +174,29 @@ int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, cons
                       vmqg_emit* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream) {
   if (!ctx || !d_offsets || (npub && (!d_pubs || !d_words))) return VMQG_E_INVAL;
   GUARD_BEGIN
-  return ctx->e.match_device(d_pubs, npub, d_words, reinterpret_cast<vmqg::Record*>(d_out), out_cap, d_offsets,
+  return ctx->e.match_device(d_pubs, npub, d_words, reinterpret_cast<vmqg::Record*>(d_out), out_cap, nullptr, 0,
+                             d_offsets, static_cast<hipStream_t>(stream));
+  GUARD_END
+}
+
+int vmqg_match_ranges_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words,
+                             vmqg_range* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream) {
+  if (!ctx || !d_offsets || (npub && (!d_pubs || !d_words)) || (out_cap && !d_out)) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  // a non-null range buffer selects range mode even at out_cap 0
+  static vmqg_range dummy;
+  return ctx->e.match_device(d_pubs, npub, d_words, nullptr, 0, d_out ? d_out : &dummy, out_cap, d_offsets,
                              static_cast<hipStream_t>(stream));
   GUARD_END
+}
+
+int vmqg_records(vmqg_ctx* ctx, const vmqg_emit** recs, uint64_t* n) {
+  if (!ctx || !recs || !n) return VMQG_E_INVAL;
+  Engine& e = ctx->e;
+  if (e.replica) return VMQG_E_STATE;
+  *recs = reinterpret_cast<const vmqg_emit*>(e.region<uint8_t>(e.lay.rec_off));
+  *n = e.lay.rec_cap;
+  return VMQG_OK;
 }
 
 int vmqg_match_status(vmqg_ctx* ctx, void* stream) {
@@ -175,6 +223,11 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->words = e.word_text.size();
   out->deferred_tier1 = e.last_deferred[0];
   out->deferred_tier2 = e.last_deferred[1];
+  out->ops_applied = e.ops_applied;
+  out->apply_host_ns = e.apply_host_ns;
+  out->patch_bytes = e.patch_bytes;
+  out->image_bytes = e.image_bytes;
+  out->max_depth = e.stack_depth();
   return VMQG_OK;
 }
 
@@ -194,15 +247,10 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   Engine& e = ctx->e;
   const std::string n(name);
   if (n == "fast_g") {
-    if (value != 2 && value != 4 && value != 8) return VMQG_E_INVAL;
+    if (value != 2 && value != 4) return VMQG_E_INVAL;
     e.opt_fast_g = (uint32_t)value;
   } else if (n == "nt_stores") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptNtStores) : (e.opt_flags & ~vmqg::kOptNtStores);
-  } else if (n == "fused") {
-    e.opt_fused = value != 0;
-  } else if (n == "unroll") {
-    if (value != 4 && value != 8) return VMQG_E_INVAL;
-    e.opt_unroll = (uint32_t)value;
   } else {
     return VMQG_E_INVAL;
   }
@@ -276,6 +324,21 @@ int vmqg_last_patches(vmqg_ctx* ctx, const void** host_ptr, uint64_t* bytes, int
   *host_ptr = ctx->e.last_patches.data();
   *bytes = ctx->e.last_patches.size() * sizeof(vmqg::Patch);
   if (full_image) *full_image = ctx->e.last_full ? 1 : 0;
+  return VMQG_OK;
+}
+
+int vmqg_replica_sync_layout(vmqg_ctx* ctx, const uint8_t* layout) {
+  if (!ctx || !layout) return VMQG_E_INVAL;
+  Engine& e = ctx->e;
+  if (!e.replica) return VMQG_E_STATE;
+  vmqg::Layout L;
+  memcpy(&L, layout, sizeof(L));
+  if (L.magic != vmqg::kLayoutMagic) return VMQG_E_INVAL;
+  // every region must be where the replica's image has it
+  vmqg::Layout a = L, b = e.lay;
+  a.max_depth = b.max_depth = 0;
+  if (memcmp(&a, &b, sizeof(a)) != 0) return VMQG_E_STATE;
+  e.lay.max_depth = L.max_depth;
   return VMQG_OK;
 }
 

@@ -43,6 +43,7 @@ constexpr uint32_t kNodeRec = 1u;       // vmq_trie_node record exists
 constexpr uint32_t kNodeTopic = 2u;     // ... and its `topic` field is set
 constexpr uint32_t kNodeFilter = 4u;    // vmq_trie_topic entry exists for the path
 constexpr uint32_t kNodeDollarSkip = 8u;  // path is [#] or starts with + (:285-288)
+constexpr uint32_t kNodeHigh = 16u;       // remote nodes >= 64 listed at {hi_off, hi_cnt} (keylist pool)
 constexpr uint32_t kNodeEmits = kNodeRec | kNodeTopic | kNodeFilter;
 
 // child flags cached in EdgeSlot.flags
@@ -52,10 +53,14 @@ constexpr uint32_t kHasWord = 4u;   // the child has an edge of a literal word
 constexpr uint32_t kHasAll = kHasHash | kHasPlus | kHasWord;
 
 struct alignas(16) EdgeSlot { uint32_t parent, word, child, flags; };
-// meta = flags | nkeys << 8; nkeys == 1: {off0, cnt0} inline; nkeys >= 2: key = keylist offset
-struct alignas(16) NodeRec { uint32_t meta, key, rmask_lo, rmask_hi, off0, cnt0, pad0, pad1; };
+// meta = flags | nkeys << 8; nkeys == 1: {off0, cnt0} inline; nkeys >= 2: key = keylist offset.
+// rmask: remote nodes < 64; nodes >= 64 (kNodeHigh) are listed in the keylist pool at hi_off.
+struct alignas(16) NodeRec { uint32_t meta, key, rmask_lo, rmask_hi, off0, cnt0, hi_off, hi_cnt; };
 struct alignas(8) KeyDesc { uint32_t off, count; };
 struct alignas(16) Record { uint32_t kind_node, group, subscriber, subinfo; };
+// ExactSlot.nwords bit: remote nodes >= 64 follow the words in exwords
+// ({count, node ids}); the slot's rmask holds the nodes < 64.
+constexpr uint32_t kExactHigh = 0x40000000u;
 struct alignas(16) ExactSlot {
   uint64_t fp;
   uint32_t nwords, words_off;   // nwords == kEmpty / kTomb marks free slots; exwords[words_off] = MP
@@ -66,6 +71,8 @@ static_assert(sizeof(EdgeSlot) == 16 && sizeof(NodeRec) == 32 && sizeof(Record) 
 static_assert(sizeof(ExactSlot) == 32 && sizeof(KeyDesc) == 8, "");
 
 constexpr uint32_t kEdgeSlotsPerBucket = 4;
+constexpr uint32_t kMaxNodes = 4096;        // VMQG_MAX_NODES: one 64-bit bitset word per lane
+constexpr uint32_t kLowNodes = 64;          // nodes held in the inline 64-bit masks
 constexpr uint32_t kExactSlotsPerBucket = 2;
 
 // Arena layout.  Fixed-size POD: it is what a replica needs to read an image
@@ -83,7 +90,8 @@ struct Layout {
   uint64_t exwords_cap;      // u32 entries
   uint64_t max_mountpoints;
   uint64_t local_node;
-  uint64_t pad[14];
+  uint64_t max_depth;        // deepest trie path (sizes the wave tier's global stack)
+  uint64_t pad[13];
 };
 static_assert(sizeof(Layout) == 256, "layout must be 256 bytes");
 constexpr uint64_t kLayoutMagic = 0x31676D7176ull;  // "vmqg1"

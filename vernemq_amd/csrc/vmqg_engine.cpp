@@ -5,6 +5,7 @@
 #include "vmqg_engine.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 namespace vmqg {
@@ -23,11 +24,15 @@ Engine::~Engine() {
     for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (ev_match_done) hipEventDestroy(ev_match_done);
-    hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_deferred);
+    for (Stage& sg : stage) {
+      if (sg.ev) hipEventDestroy(sg.ev);
+      if (sg.h) hipHostFree(sg.h);
+      hipFree(sg.d);
+    }
+    hipFree(d_arena); hipFree(d_status); hipFree(d_deferred);
     hipFree(d_keycache);
-    hipFree(d_lookback); hipFree(d_ostack); hipFree(d_ocand); hipFree(d_okeys);
+    hipFree(d_lookback); hipFree(d_ostack);
     hipFree(d_pubs); hipFree(d_words); hipFree(d_offs); hipFree(d_out);
-    if (h_patch_stage) hipHostFree(h_patch_stage);
     if (stream) hipStreamDestroy(stream);
   }
 }
@@ -37,6 +42,7 @@ int Engine::init(const vmqg_config& c) {
   if (cfg.max_nodes == 0) cfg.max_nodes = VMQG_MAX_NODES;
   if (cfg.max_mountpoints == 0) cfg.max_mountpoints = 1024;
   if (cfg.max_nodes > VMQG_MAX_NODES || cfg.local_node >= cfg.max_nodes) return VMQG_E_LIMIT;
+  static_assert(VMQG_MAX_NODES == kMaxNodes, "the wave tier's node set is kMaxNodes bits");
   if (cfg.max_mountpoints > (1u << 24)) return VMQG_E_LIMIT;
   replica = (cfg.flags & VMQG_CFG_REPLICA) != 0;
   // reserved words
@@ -57,7 +63,9 @@ int Engine::init(const vmqg_config& c) {
     if (hipEventCreateWithFlags(&ev_match_done, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
     has_device = true;
     if (hipMalloc(&d_status, 64) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_deferred, sizeof(uint32_t) * deferred_cap) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMemset(d_status, 0, 64) != hipSuccess) return VMQG_E_DEVICE;
+    for (Stage& sg : stage)
+      if (hipEventCreateWithFlags(&sg.ev, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
     if (hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cu_count < 1)
       cu_count = 256;
     if (!replica) {
@@ -92,6 +100,7 @@ uint32_t Engine::path_child(uint32_t parent, uint32_t word, bool create) {
   // MQTT-4.7.2-1 filters: exactly [#], or starting with + (vmq_reg_trie.erl:285-288)
   pi.first_plus = pi.depth == 1 ? (word == kPlus) : paths[parent].first_plus;
   pi.dollar_skip = pi.first_plus || (pi.depth == 1 && word == kHash);
+  if (pi.depth > max_depth) max_depth = pi.depth;
   paths.push_back(std::move(pi));
   path_index.insert(k, id);
   return id;
@@ -232,12 +241,23 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) c
   L.magic = kLayoutMagic;
   L.max_mountpoints = cfg.max_mountpoints;
   L.local_node = cfg.local_node;
+  L.max_depth = max_depth;
   uint64_t recs = 0, kl = 0, xw = 0, ex = 0;
   for (auto& k : keys) recs += next_pow2(k.vals.size() ? k.vals.size() : 1);
-  for (auto& p : paths) if (p.filter && p.nodes.size() >= 2) kl += next_pow2(p.nodes.size());
+  for (auto& p : paths) {
+    if (!p.filter) continue;
+    if (p.nodes.size() >= 2) kl += next_pow2(p.nodes.size());
+    uint64_t nh = 0;
+    for (auto& e : p.nodes) nh += e.first.group == kNone && e.first.node >= kLowNodes;
+    if (nh) kl += next_pow2(nh);
+  }
   for (auto& t : topics) {
     const bool has = t.exact_ok && ((t.local_key != kNone && !keys[t.local_key].vals.empty()) || !t.remote.empty());
-    if (has) { ex++; xw += t.words.size() + 1; }
+    if (!has) continue;
+    ex++;
+    uint64_t nh = 0;
+    for (auto& r : t.remote) nh += r.first >= kLowNodes;
+    xw += t.words.size() + 1 + (nh ? nh + 1 : 0);
   }
   const uint64_t edges_need = edge_live + extra_edges;
   const uint64_t edge_slots = next_pow2(std::max<uint64_t>(4096, std::max<uint64_t>(edges_need * 2, cfg.hint_edges * 2)));
@@ -296,8 +316,8 @@ void Engine::rebuild(uint64_t extra_edges, bool compact) {
     for (auto& p : paths) { p.in_slot = ~0ull; p.nlit = 0; p.eflags &= ~kHasWord; }   // re-counted below
     for (auto& e : live) edge_insert(e.parent, e.word, e.child);
     for (auto& k : keys) { k.off = 0; k.cap = 0; k.dirty_pos.clear(); }
-    for (auto& t : topics) { t.slot = ~0ull; t.words_off = kNone; }
-    for (auto& p : paths) { p.kl_off = 0; p.kl_cap = 0; }
+    for (auto& t : topics) { t.slot = ~0ull; t.words_off = kNone; t.xw_len = 0; }
+    for (auto& p : paths) { p.kl_off = 0; p.kl_cap = 0; p.hn_off = 0; p.hn_cap = 0; }
     bool ok = true;
     for (uint32_t k = 0; ok && k < keys.size(); k++) ok = write_key(k);
     for (uint32_t p = 0; ok && p < paths.size(); p++) ok = write_path(p);
@@ -346,7 +366,7 @@ bool Engine::write_path(uint32_t p) {
   if (P.rec && P.topic_set) flags |= kNodeTopic;
   if (P.filter) flags |= kNodeFilter;
   if (P.dollar_skip) flags |= kNodeDollarSkip;
-  std::vector<uint32_t> ks;
+  std::vector<uint32_t> ks, high;
   uint64_t rmask = 0;
   if (P.filter) {
     // match_/3 (:301-303): one candidate per node-list entry; a key that does
@@ -358,10 +378,19 @@ bool Engine::write_path(uint32_t p) {
       } else if (e.first.node == cfg.local_node) {                                     // :73-77
         const uint32_t k = local_key(P.topic_id, false);
         if (k != kNone) ks.push_back(k);
-      } else {
+      } else if (e.first.node < kLowNodes) {
         rmask |= 1ull << e.first.node;                                                 // :78-84
+      } else {
+        high.push_back(e.first.node);
       }
     }
+  }
+  if (!high.empty()) {
+    std::sort(high.begin(), high.end());
+    if (!write_high_list(P.hn_off, P.hn_cap, high)) return false;
+    flags |= kNodeHigh;
+    r.hi_off = P.hn_off;
+    r.hi_cnt = (uint32_t)high.size();
   }
   if (ks.size() == 1) {
     r.key = ks[0];
@@ -382,7 +411,7 @@ bool Engine::write_path(uint32_t p) {
       if (kl[i] != ks[i]) { kl[i] = ks[i]; touch(lay.keylist_off + (P.kl_off + i) * 4, 4); }
     }
   }
-  r.meta = flags | ((uint32_t)ks.size() << 8);
+  r.meta = flags | ((uint32_t)std::min<size_t>(ks.size(), 0xFFFFFF) << 8);
   r.rmask_lo = (uint32_t)rmask; r.rmask_hi = (uint32_t)(rmask >> 32);
   *(region<NodeRec>(lay.node_off) + p) = r;
   touch(lay.node_off + (uint64_t)p * sizeof(NodeRec), sizeof(NodeRec));
@@ -395,6 +424,27 @@ uint64_t Engine::exact_fp(const TopicInfo& t) const {
   return fp_final(s, t.mp, (uint32_t)t.words.size());
 }
 
+// A remote-node list (nodes >= 64, sorted) in the keylist pool, in place
+// when its range has room, else at a fresh range (the old one is garbage).
+bool Engine::write_high_list(uint32_t& off, uint32_t& cap, const std::vector<uint32_t>& nodes) {
+  if (nodes.size() > cap) {
+    const uint64_t c = next_pow2(nodes.size());
+    if (kl_top + c > lay.keylist_cap) return false;
+    kl_garbage += cap;
+    off = (uint32_t)kl_top;
+    cap = (uint32_t)c;
+    kl_top += c;
+  }
+  uint32_t* kl = region<uint32_t>(lay.keylist_off) + off;
+  for (size_t i = 0; i < nodes.size(); i++) {
+    if (kl[i] != nodes[i]) { kl[i] = nodes[i]; touch(lay.keylist_off + (uint64_t)(off + i) * 4, 4); }
+  }
+  return true;
+}
+
+// The exact-table slot of one (MP, Topic): the `{Topic, node()}` candidate
+// (its local key's records) and vmq_trie_remote_subs (remote nodes: < 64 in
+// the slot's mask, the others listed after the words in exwords).
 bool Engine::write_topic(uint32_t ti) {
   TopicInfo& t = topics[ti];
   const bool local = t.local_key != kNone && !keys[t.local_key].vals.empty();
@@ -406,23 +456,42 @@ bool Engine::write_topic(uint32_t ti) {
       s.nwords = kTomb;
       touch(lay.exact_off + t.slot * sizeof(ExactSlot), sizeof(ExactSlot));
       t.slot = ~0ull;
-      xw_garbage += t.words.size() + 1;
+      xw_garbage += t.xw_len;
       t.words_off = kNone;
+      t.xw_len = 0;
       exact_live--; exact_tomb++;
     }
     return true;
   }
   uint64_t rmask = 0;
-  for (auto& r : t.remote) rmask |= 1ull << r.first;
-  if (t.slot == ~0ull) {
-    if ((exact_live + exact_tomb + 1) * 10 > lay.exact_buckets * kExactSlotsPerBucket * 7) return false;
-    if (xw_top + t.words.size() + 1 > lay.exwords_cap) return false;
+  std::vector<uint32_t> high;
+  for (auto& r : t.remote) {
+    if (r.first < kLowNodes) rmask |= 1ull << r.first;
+    else high.push_back(r.first);
+  }
+  std::sort(high.begin(), high.end());
+  const uint32_t L = (uint32_t)t.words.size();
+  const uint32_t need = 1 + L + (high.empty() ? 0 : 1 + (uint32_t)high.size());
+  if (t.slot == ~0ull && (exact_live + exact_tomb + 1) * 10 > lay.exact_buckets * kExactSlotsPerBucket * 7)
+    return false;
+  if (t.slot == ~0ull || need > t.xw_len) {   // (re)place MP + words [+ the high list]
+    if (xw_top + need > lay.exwords_cap) return false;
+    xw_garbage += t.xw_len;
     t.words_off = (uint32_t)xw_top;
+    t.xw_len = need;
     uint32_t* xw = region<uint32_t>(lay.exwords_off) + xw_top;
     xw[0] = t.mp;
-    memcpy(xw + 1, t.words.data(), t.words.size() * 4);
-    touch(lay.exwords_off + xw_top * 4, (t.words.size() + 1) * 4);
-    xw_top += t.words.size() + 1;
+    memcpy(xw + 1, t.words.data(), L * 4);
+    touch(lay.exwords_off + xw_top * 4, (uint64_t)(1 + L) * 4);
+    xw_top += need;
+  }
+  if (!high.empty()) {
+    uint32_t* hl = region<uint32_t>(lay.exwords_off) + t.words_off + 1 + L;
+    hl[0] = (uint32_t)high.size();
+    memcpy(hl + 1, high.data(), high.size() * 4);
+    touch(lay.exwords_off + ((uint64_t)t.words_off + 1 + L) * 4, (1 + high.size()) * 4);
+  }
+  if (t.slot == ~0ull) {
     const uint64_t fp = exact_fp(t);
     const uint64_t mask = lay.exact_buckets - 1;
     uint64_t b = fp & mask;
@@ -437,14 +506,14 @@ bool Engine::write_topic(uint32_t ti) {
         exact_live++;
         t.slot = found;
         tab[found].fp = fp;
-        tab[found].nwords = (uint32_t)t.words.size();
-        tab[found].words_off = t.words_off;
         break;
       }
       b = (b + 1) & mask;
     }
   }
   ExactSlot& s = tab[t.slot];
+  s.nwords = L | (high.empty() ? 0u : kExactHigh);
+  s.words_off = t.words_off;
   s.off = local ? (uint32_t)keys[t.local_key].off : 0;
   s.count = local ? (uint32_t)keys[t.local_key].vals.size() : 0;
   s.rmask = rmask;
@@ -667,6 +736,7 @@ void Engine::handle_delete(const vmqg_op& op, const uint32_t* w) {
 
 int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords) {
   if (replica) return VMQG_E_STATE;
+  const auto t0 = std::chrono::steady_clock::now();
   // validate the whole batch before touching state
   uint64_t add_words = 0;
   for (size_t i = 0; i < n; i++) {
@@ -698,11 +768,22 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
   for (uint32_t p : dirty_paths) paths[p].dirty = 0;
   for (uint32_t t : dirty_topics) topics[t].dirty = 0;
   dirty_keys.clear(); dirty_paths.clear(); dirty_topics.clear();
+  lay.max_depth = max_depth;   // replicas size their stacks from the layout
   epoch++;
-  return upload();
+  ops_applied += n;
+  const int rc = upload();
+  apply_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                       std::chrono::steady_clock::now() - t0).count();
+  return rc;
 }
 
 // --------------------------------------------------------------- device
+// Ships the pending changes: a patch batch (the 16-B dirty chunks), or the
+// whole image after a re-layout.  Patches are staged in a ring of pinned
+// buffers and applied by k_apply_patches on the context stream after
+// everything queued before (matches included); the call does not wait for
+// them.  A full image is copied synchronously (re-layouts are rare and the
+// arena may be reallocated).
 int Engine::upload() {
   last_patches.clear();
   if (!full_image && dirty_chunks.size() * sizeof(Patch) > lay.total_bytes / 2) {
@@ -723,60 +804,72 @@ int Engine::upload() {
       dirty_bits[c >> 6] = 0;
     }
     dirty_chunks.clear();
+    patch_bytes += last_patches.size() * sizeof(Patch);
+  } else {
+    image_bytes += lay.total_bytes;
   }
   if (!has_device) { full_image = false; return VMQG_OK; }
   hipSetDevice(device);
-  // tables must not change under a match still reading them
+  // tables must not change under a match still reading them (matches on
+  // caller streams are ordered through ev_match_done)
   if (hipStreamWaitEvent(stream, ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
   if (full_image) {
+    if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
+    if (hipEventSynchronize(ev_match_done) != hipSuccess) return VMQG_E_DEVICE;
     if (d_arena_bytes < lay.total_bytes) {
-      if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
-      if (hipEventSynchronize(ev_match_done) != hipSuccess) return VMQG_E_DEVICE;
       if (d_arena) hipFree(d_arena);
       d_arena = nullptr; d_arena_bytes = 0;
       if (hipMalloc(&d_arena, lay.total_bytes) != hipSuccess) return VMQG_E_NOMEM;
       d_arena_bytes = lay.total_bytes;
     }
-    if (hipMemcpyAsync(d_arena, mirror.data(), lay.total_bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
+    if (hipMemcpy(d_arena, mirror.data(), lay.total_bytes, hipMemcpyHostToDevice) != hipSuccess)
       return VMQG_E_DEVICE;
-    if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
     full_image = false;
     std::fill(dirty_bits.begin(), dirty_bits.end(), 0);
     return VMQG_OK;
   }
   const uint64_t np = last_patches.size();
   if (np == 0) return VMQG_OK;
-  if (h_patch_cap < np) {
-    if (h_patch_stage) hipHostFree(h_patch_stage);
-    h_patch_stage = nullptr;
-    h_patch_cap = next_pow2(np);
-    if (hipHostMalloc(&h_patch_stage, h_patch_cap * sizeof(Patch)) != hipSuccess) { h_patch_cap = 0; return VMQG_E_NOMEM; }
+  Stage& sg = stage[stage_next];
+  stage_next = (stage_next + 1) % kStage;
+  if (sg.used && hipEventSynchronize(sg.ev) != hipSuccess) return VMQG_E_DEVICE;   // its batch has landed
+  if (sg.cap < np) {
+    if (sg.h) hipHostFree(sg.h);
+    hipFree(sg.d);
+    sg.h = nullptr; sg.d = nullptr; sg.cap = 0;
+    const uint64_t cap = next_pow2(np);
+    if (hipHostMalloc(&sg.h, cap * sizeof(Patch)) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&sg.d, cap * sizeof(Patch)) != hipSuccess) return VMQG_E_NOMEM;
+    sg.cap = cap;
   }
-  if (d_patch_cap < np) {
-    if (d_patch) hipFree(d_patch);
-    d_patch = nullptr;
-    d_patch_cap = next_pow2(np);
-    if (hipMalloc(&d_patch, d_patch_cap * sizeof(Patch)) != hipSuccess) { d_patch_cap = 0; return VMQG_E_NOMEM; }
-  }
-  memcpy(h_patch_stage, last_patches.data(), np * sizeof(Patch));
-  if (hipMemcpyAsync(d_patch, h_patch_stage, np * sizeof(Patch), hipMemcpyHostToDevice, stream) != hipSuccess)
+  memcpy(sg.h, last_patches.data(), np * sizeof(Patch));
+  if (hipMemcpyAsync(sg.d, sg.h, np * sizeof(Patch), hipMemcpyHostToDevice, stream) != hipSuccess)
     return VMQG_E_DEVICE;
-  if (launch_patches(d_arena, d_patch, np, stream) != hipSuccess) return VMQG_E_DEVICE;
-  if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_patches(d_arena, sg.d, np, stream) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipEventRecord(sg.ev, stream) != hipSuccess) return VMQG_E_DEVICE;
+  sg.used = true;
+  // later matches on other streams must see the patches
+  if (hipEventRecord(ev_match_done, stream) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
 
-int Engine::ensure_match_scratch(uint64_t npub) {
-  if (npub > keycache_cap) {
-    if (d_keycache) hipFree(d_keycache);
-    d_keycache = nullptr;
-    keycache_cap = next_pow2(npub);
-    if (hipMalloc(&d_keycache, keycache_cap * 32) != hipSuccess) { keycache_cap = 0; return VMQG_E_NOMEM; }
+int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
+  if (npub > keycache_cap || 2 * npub > deferred_cap) {
+    if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
+    hipFree(d_keycache);
+    hipFree(d_deferred);
+    d_keycache = nullptr; d_deferred = nullptr;
+    keycache_cap = deferred_cap = 0;
+    const uint64_t cap = next_pow2(std::max<uint64_t>(npub, 1024));
+    if (hipMalloc(&d_keycache, cap * 32) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_deferred, 2 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
+    keycache_cap = cap;
+    deferred_cap = 2 * cap;
   }
   return VMQG_OK;
 }
 
-// Look-back granules for `granules` tiles / chunks; advances the call's tag.
+// Look-back granules for `granules` scan tiles; advances the call's tag.
 int Engine::ensure_lookback(uint64_t granules, hipStream_t st) {
   if (granules > lookback_cap) {
     if (d_lookback) { hipStreamSynchronize(st); hipFree(d_lookback); }
@@ -793,21 +886,27 @@ int Engine::ensure_lookback(uint64_t granules, hipStream_t st) {
   return VMQG_OK;
 }
 
-// Global scratch (o_cap stack / candidate / key entries) for `waves` waves.
-int Engine::ensure_wave_scratch(uint32_t waves, hipStream_t st) {
-  if (o_waves >= waves) return VMQG_OK;
-  if (d_ostack) { hipStreamSynchronize(st); hipFree(d_ostack); hipFree(d_ocand); hipFree(d_okeys); }
-  d_ostack = nullptr; d_ocand = nullptr; d_okeys = nullptr; o_waves = 0;
-  const uint64_t n = (uint64_t)waves * o_cap;
-  if (hipMalloc(&d_ostack, n * sizeof(uint2)) != hipSuccess || hipMalloc(&d_ocand, n * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&d_okeys, n * sizeof(uint2)) != hipSuccess)
-    return VMQG_E_NOMEM;
-  o_waves = waves;
+// Wave tiers: tier 1 fills the chip from LDS; tier 2 has a global stack of
+// o_cap entries per wave.  A wave pops <= 64 entries and pushes <= 2 per
+// entry, one depth further, so its stack holds < 64 entries per trie level
+// plus one step's pushes: 64 (depth + 4) entries cannot overflow.
+int Engine::ensure_wave_scratch(hipStream_t st) {
+  if (w1_waves == 0) w1_waves = (uint32_t)std::max(1, wave_blocks_per_cu()) * (uint32_t)cu_count * 4;
+  const uint64_t need = std::max<uint64_t>({1024, 64ull * (stack_depth() + 4), o_cap_floor});
+  if (need > (1ull << 31)) return VMQG_E_LIMIT;
+  if (o_cap >= need && d_ostack) return VMQG_OK;
+  // at most 256 MiB of stacks, at least 64 waves
+  uint64_t waves = (256ull << 20) / (need * sizeof(uint2));
+  waves = std::max<uint64_t>(64, std::min<uint64_t>(1024, waves)) & ~3ull;
+  if (d_ostack) { hipStreamSynchronize(st); hipFree(d_ostack); }
+  d_ostack = nullptr; o_waves = 0; o_cap = 0;
+  if (hipMalloc(&d_ostack, waves * need * sizeof(uint2)) != hipSuccess) return VMQG_E_NOMEM;
+  o_cap = (uint32_t)need;
+  o_waves = (uint32_t)waves;
   return VMQG_OK;
 }
 
-MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, Record* out,
-                           uint64_t out_cap, uint64_t* offs) const {
+MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, uint64_t* offs) const {
   MatchArgs a{};
   a.edges = reinterpret_cast<const EdgeSlot*>(d_arena + lay.edge_off);
   a.edge_mask = lay.edge_buckets - 1;
@@ -823,67 +922,55 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.max_mp = (uint32_t)lay.max_mountpoints;
   a.local_node = (uint32_t)lay.local_node;
   a.pubs = pubs; a.words = words; a.npub = npub;
-  a.offsets = offs; a.out = out; a.out_cap = out_cap;
+  a.offsets = offs;
   a.keycache = d_keycache;
   a.status = d_status; a.deferred = d_deferred;
-  a.deferred_cap = deferred_cap;
   a.fast_g = opt_fast_g; a.opts = opt_flags;
   a.lookback = d_lookback; a.lb_tag = lb_tag;
-  a.nchunks = (uint32_t)(((uint64_t)npub + fused_chunk(opt_fast_g) - 1) / fused_chunk(opt_fast_g));
-  a.o_stack = d_ostack; a.o_cand = d_ocand; a.o_keys = d_okeys;
-  a.o_cap = o_cap; a.o_waves = o_waves;
+  a.w1_waves = w1_waves;
+  a.o_stack = d_ostack; a.o_cap = o_cap; a.o_waves = o_waves;
   return a;
 }
 
 int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t* d_words_, Record* d_out_,
-                         uint64_t out_cap, uint64_t* d_offsets, hipStream_t st) {
+                         uint64_t out_cap, vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets,
+                         hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   if (!d_arena) return VMQG_E_STATE;
   hipSetDevice(device);
   if (!st) st = stream;
-  if (hipMemsetAsync(d_status, 0, 16, st) != hipSuccess) return VMQG_E_DEVICE;
+  // patches / images queued on the context stream land before this match
+  if (st != stream && hipStreamWaitEvent(st, ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
   if (npub == 0) return hipMemsetAsync(d_offsets, 0, 8, st) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
   int rc;
-  if (opt_fused) {
-    // one launch: walk + count + look-back offsets + emit (k_match_fused)
-    const uint32_t CH = fused_chunk(opt_fast_g);
-    const uint32_t nchunks = (uint32_t)(((uint64_t)npub + CH - 1) / CH);
-    const uint32_t per_cu = (uint32_t)std::max(1, fused_blocks_per_cu(opt_fast_g, opt_unroll));
-    if ((rc = ensure_lookback(nchunks, st)) || (rc = ensure_wave_scratch(per_cu * cu_count * 4, st))) return rc;
-    const MatchArgs a = args_for(d_pubs_, npub, d_words_, d_out_, out_cap, d_offsets);
-    const uint32_t grid = std::min<uint32_t>(nchunks, per_cu * cu_count);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (timing) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
-    if (launch_fused(a, grid, opt_unroll, st) != hipSuccess) return VMQG_E_DEVICE;
-    if (timing) { hipEventRecord(e1, st); t_emit.push_back({e0, e1}); t_count.push_back({nullptr, nullptr}); }
-    if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
-    return VMQG_OK;
-  }
-  // COUNT (fast groups, then the wave path for what they deferred), one-launch
-  // scan of the counts, EMIT (same two tiers)
-  const uint32_t per_cu = (uint32_t)std::max(1, wave_blocks_per_cu());
-  if ((rc = ensure_match_scratch(npub)) || (rc = ensure_lookback(scan_tiles(npub), st)) ||
-      (rc = ensure_wave_scratch(per_cu * cu_count * 4, st)))
+  if ((rc = ensure_match_scratch(npub, st)) || (rc = ensure_lookback(scan_tiles(npub), st)) ||
+      (rc = ensure_wave_scratch(st)))
     return rc;
-  MatchArgs a = args_for(d_pubs_, npub, d_words_, d_out_, out_cap, d_offsets);
-  a.o_waves = per_cu * cu_count * 4;   // the wave kernel's grid
+  MatchArgs a = args_for(d_pubs_, npub, d_words_, d_offsets);
+  a.out = d_out_; a.out_cap = out_cap;
+  a.out_rng = d_rng; a.rng_cap = rng_cap;
+  if (launch_reset(d_status, st) != hipSuccess) return VMQG_E_DEVICE;
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
   if (timing) {
     hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2); hipEventCreate(&e3);
     hipEventRecord(e0, st);
   }
+  // COUNT: fast groups, then the wave tiers for what they deferred
   if (launch_match(a, 0, 0, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) hipEventRecord(e1, st);
-  if (launch_match(a, 0, 1, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 0, 1, st) != hipSuccess || launch_match(a, 0, 2, st) != hipSuccess) return VMQG_E_DEVICE;
   if (launch_scan(a, st) != hipSuccess) return VMQG_E_DEVICE;
+  // EMIT: same tiers
   if (timing) hipEventRecord(e2, st);
   if (launch_match(a, 1, 0, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) { hipEventRecord(e3, st); t_count.push_back({e0, e1}); t_emit.push_back({e2, e3}); }
-  if (launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 1, 1, st) != hipSuccess || launch_match(a, 1, 2, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
 
+// Status words: [0] tier-1 publishes, [1] tier-2 publishes of the last call,
+// [3] error bits latched since the previous vmqg_match_status.
 int Engine::match_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
@@ -892,11 +979,13 @@ int Engine::match_status(hipStream_t st) {
   if (hipMemcpyAsync(h, d_status, 16, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipMemsetAsync(d_status, 0, 16, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
   last_deferred[0] = h[0];
-  last_deferred[1] = h[2];
-  if (h[1] & (2u | 1u)) return VMQG_E_FRONTIER;
-  if (h[1] & 4u) return VMQG_E_OVERFLOW;
-  if (h[1] & (8u | 16u)) return VMQG_E_DEVICE;   // count mismatch, look-back timeout
+  last_deferred[1] = h[1];
+  const uint32_t err = h[3];
+  if (err & 2u) return VMQG_E_FRONTIER;
+  if (err & 4u) return VMQG_E_OVERFLOW;
+  if (err & (8u | 16u)) return VMQG_E_DEVICE;   // count mismatch, look-back timeout
   return VMQG_OK;
 }
 
@@ -906,10 +995,10 @@ void Engine::collect_times() {
   for (size_t i = 0; i < t_count.size(); i++) {
     float a = 0, b = 0;
     hipEventSynchronize(t_emit[i].second);
-    if (t_count[i].first) hipEventElapsedTime(&a, t_count[i].first, t_count[i].second);   // null: fused call
+    hipEventElapsedTime(&a, t_count[i].first, t_count[i].second);
     hipEventElapsedTime(&b, t_emit[i].first, t_emit[i].second);
     sum_count_ns += a * 1e6; sum_emit_ns += b * 1e6; n_timed++;
-    if (t_count[i].first) { hipEventDestroy(t_count[i].first); hipEventDestroy(t_count[i].second); }
+    hipEventDestroy(t_count[i].first); hipEventDestroy(t_count[i].second);
     hipEventDestroy(t_emit[i].first); hipEventDestroy(t_emit[i].second);
   }
   t_count.clear(); t_emit.clear();

@@ -77,6 +77,7 @@ struct PathInfo {
   uint32_t nlit = 0;                // its live literal-word edges (kHasWord while > 0)
   uint32_t topic_id = kNone;        // (MP, path words) term, once known
   uint32_t kl_off = 0, kl_cap = 0;  // keylist range owned by this path
+  uint32_t hn_off = 0, hn_cap = 0;  // keylist range of its remote nodes >= 64
   uint8_t rec = 0, topic_set = 0;   // vmq_trie_node record / its topic field
   uint8_t filter = 0;               // vmq_trie_topic entry exists
   uint8_t dollar_skip = 0, first_plus = 0, dirty = 0;
@@ -117,6 +118,7 @@ struct TopicInfo {
   std::vector<std::pair<uint32_t, int64_t>> remote;
   uint64_t slot = ~0ull;
   uint32_t words_off = kNone;
+  uint32_t xw_len = 0;              // exwords entries owned: MP, words, [count, remote nodes >= 64]
 };
 
 struct Engine {
@@ -147,17 +149,25 @@ struct Engine {
   uint64_t rec_top = 0, rec_garbage = 0, kl_top = 0, kl_garbage = 0, xw_top = 0, xw_garbage = 0;
   bool full_image = false;          // the pending upload is a whole image
   uint64_t epoch = 0, rebuilds = 0;
+  uint32_t max_depth = 0;           // deepest path interned (sizes the wave tier's stack)
   std::vector<Patch> last_patches;
   bool last_full = false;
+  // apply accounting (vmqg_stats): host work only, separate from device waits
+  uint64_t ops_applied = 0, apply_host_ns = 0, patch_bytes = 0, image_bytes = 0;
 
   // ---- device
   int device = -1;
   hipStream_t stream = nullptr;
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
-  Patch* h_patch_stage = nullptr; uint64_t h_patch_cap = 0;
-  Patch* d_patch = nullptr; uint64_t d_patch_cap = 0;
-  uint32_t* d_status = nullptr; uint32_t* d_deferred = nullptr;
-  uint32_t deferred_cap = 1u << 20;
+  // patch staging ring: pinned host + device buffers, each reusable once its
+  // event (recorded after the patch kernel) has fired, so vmqg_apply_ops
+  // never waits for matches still queued on the stream
+  static constexpr int kStage = 4;
+  struct Stage { Patch* h = nullptr; Patch* d = nullptr; uint64_t cap = 0; hipEvent_t ev = nullptr; bool used = false; };
+  Stage stage[kStage];
+  int stage_next = 0;
+  uint32_t* d_status = nullptr;
+  uint32_t* d_deferred = nullptr; uint64_t deferred_cap = 0;   // 2 x publishes
   void* d_keycache = nullptr; uint64_t keycache_cap = 0;   // publishes
   // host-buffer match staging
   void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
@@ -167,11 +177,11 @@ struct Engine {
   hipEvent_t ev_match_done = nullptr;
   bool timing = false;
   uint32_t opt_fast_g = 2, opt_flags = kOptNtStores;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
-  uint32_t opt_fused = 0, opt_unroll = 4;              // one-pass kernel (A/B: slower, off); its copy unroll
-  // look-back granules (tagged per call), global scratch of the wave path
+  // look-back granules (tagged per call), global stack of the tier-2 wave path
   uint64_t* d_lookback = nullptr; uint64_t lookback_cap = 0; uint32_t lb_tag = 0;
-  uint2* d_ostack = nullptr; uint32_t* d_ocand = nullptr; uint2* d_okeys = nullptr;
-  uint32_t o_cap = 4096, o_waves = 0;
+  uint2* d_ostack = nullptr; uint64_t ostack_bytes = 0;
+  uint32_t o_cap = 0, o_waves = 0, w1_waves = 0;
+  uint64_t o_cap_floor = 0;         // raised by vmqg_match_batch if a tier-2 stack ever overflowed
   int cu_count = 0;
   uint32_t last_deferred[2] = {0, 0};   // tier-1 / tier-2 publishes of the last checked batch
   std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_emit;
@@ -211,6 +221,7 @@ struct Engine {
   void edge_insert(uint32_t parent, uint32_t word, uint32_t child);
   void edge_erase(uint32_t parent, uint32_t word, uint32_t child);
   void refresh_incoming_flags(uint32_t node);
+  bool write_high_list(uint32_t& off, uint32_t& cap, const std::vector<uint32_t>& nodes);
   Layout plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) const;
   void rebuild(uint64_t extra_edges, bool compact = false);
   bool flush_incremental();
@@ -221,13 +232,14 @@ struct Engine {
 
   // device
   int upload();
-  int ensure_match_scratch(uint64_t npub);
+  int ensure_match_scratch(uint64_t npub, hipStream_t st);
   int ensure_lookback(uint64_t granules, hipStream_t st);
-  int ensure_wave_scratch(uint32_t waves, hipStream_t st);
-  MatchArgs args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, Record* out, uint64_t out_cap,
-                     uint64_t* offs) const;
+  int ensure_wave_scratch(hipStream_t st);
+  MatchArgs args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, uint64_t* offs) const;
+  // out_rng == null: records mode into out; else range mode into out_rng
   int match_device(const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words, Record* d_out,
-                   uint64_t out_cap, uint64_t* d_offsets, hipStream_t st);
+                   uint64_t out_cap, vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets, hipStream_t st);
+  uint32_t stack_depth() const { return (uint32_t)std::max<uint64_t>(max_depth, lay.max_depth); }
   int match_status(hipStream_t st);
   void collect_times();
 

@@ -1,27 +1,38 @@
 // HIP kernels for gfx950 (MI355X): the publish -> matched-subscriber path of
 // vmq_reg_trie:fold/4 (apps/vmq_server/src/vmq_reg_trie.erl:59-98).
 //
-// Work unit: a GROUP of G lanes owns one publish (G = 8 on the fast path, so
-// a 64-lane wavefront keeps 8 publishes in flight; G = 64 on the slow path).
-// The group walks the trie in chunks: up to G frontier entries {path, depth}
-// are popped from the group's LDS stack, one per lane, and each active lane
-// issues its three edge probes ('#', the publish word, '+') as independent
-// 64-B bucket loads before resolving any of them — the ets:lookup calls of
-// trie_match/4 and 'trie_match_#'/2 (:358-383), many frontier nodes and many
-// publishes per memory round trip.  '#' children and end-of-topic nodes are
-// compacted (ballot + mbcnt) into an LDS candidate list; their node records
-// (match/4, :283-303) give the subscriber-list keys, compacted into an LDS
-// key list.  The exact-topic probe (the `{Topic, node()}` candidate and
-// get_remote_subscribers/2, :62, :514-520) is a fingerprint lookup computed
-// group-parallel.  Remote nodes are OR-ed into a 64-bit mask: exactly the
-// `Remotes` dedupe of fold_/5 (:78-84).
+// Fast tier — work unit: a GROUP of G lanes (G = 2 by default, 4 as an
+// option) owns one publish, so a 64-lane wavefront keeps 64 / G publishes in
+// flight.  The group walks the trie in chunks: up to G frontier entries
+// {path, depth} are popped from the group's LDS stack, one per lane, and each
+// active lane issues its three edge probes ('#', the publish word, '+') as
+// independent 64-B bucket loads before resolving any of them — the
+// ets:lookup calls of trie_match/4 and 'trie_match_#'/2 (:358-383), many
+// frontier nodes and many publishes per memory round trip.  '#' children and
+// end-of-topic nodes are compacted (ballot + mbcnt) into an LDS candidate
+// list; their node records (match/4, :283-303) give the subscriber-list
+// keys, compacted into an LDS key list.  The exact-topic probe (the
+// `{Topic, node()}` candidate and get_remote_subscribers/2, :62, :514-520) is
+// a fingerprint lookup computed group-parallel.  Remote nodes < 64 are OR-ed
+// into a 64-bit mask: exactly the `Remotes` dedupe of fold_/5 (:78-84).
+// The group lists are interleaved across the block's groups with an XOR
+// swizzle, so groups at the same list depth hit distinct LDS banks.
 //
-// Passes per batch: COUNT (walk; per-publish emission count, plus a 32-B key
-// cache {total, nk, remote mask, <=2 x (record off, count)}), a device scan
-// (counts -> offsets), EMIT (records from the key cache; re-walk only for
-// publishes with > 2 keys), writing the 16-B records (lookup_subs + fold__,
-// :87-98) group-contiguously.  Publishes that overflow the LDS lists go to
-// the SLOW instantiation (G = 64, scratch in global memory).
+// Wave tier — a publish whose lists overflow the fast tier's, or that meets
+// a remote node >= 64, is deferred to one whole wave that walks it with
+// bounded LDS buffers, flushing candidates into keys and keys into output
+// (or into a count) as they fill: only its frontier stack needs room, and
+// that is bounded by the trie depth (tier 2: the stack in global memory,
+// sized by the host from the deepest path).  Remote nodes go to a 4,096-bit
+// set (one 64-bit word per lane at the end).  No publish is refused.
+//
+// Passes per batch: COUNT (fast tier: per-publish count + a 32-B key cache
+// {total, nk, remote mask, <= 2 x (record off, count)}; then the wave tiers
+// for what it deferred), a one-launch scan (counts -> offsets), EMIT (fast
+// tier from the key cache, re-walk only for publishes with > 2 keys; then the
+// wave tiers).  Output is either the 16-B records (lookup_subs + fold__,
+// :87-98) or, in range mode, one 8-B {record off, count} per non-empty
+// subscriber-list key plus {node, 0} per remote node.
 #include <hip/hip_runtime.h>
 
 #include "vmqg_common.h"
@@ -32,11 +43,17 @@ namespace vmqg {
 
 constexpr int kWaves = 4;          // waves per 256-thread block
 #ifndef VMQG_EMIT_U
-#define VMQG_EMIT_U 8              // records in flight per lane in the tier-0 EMIT copy (A/B: 2, 4, 8)
+#define VMQG_EMIT_U 8              // records in flight per lane in the fast EMIT copy (A/B: 2, 4, 8)
 #endif
 // fast-tier LDS lists per group, sized so a block stays near 28 KiB
 template <int G> struct FastCaps { static constexpr uint32_t S = 8 * G, C = 4 * G, K = 4 * G; };
 constexpr uint32_t kRewalk = 0xFFFFFFFFu;   // key cache: EMIT must re-walk
+constexpr uint32_t kDeferred = 0xFFFFFFFEu; // key cache: the wave tier owns the publish
+
+// status words (d_status): per-call counters are reset by the host before
+// each match call, the error word only by vmqg_match_status (sticky).
+enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStErr = 3 };
+enum : uint32_t { kErrFrontier = 2u, kErrOverflow = 4u, kErrMismatch = 8u };   // kErrLookback = 16 (lookback.h)
 
 __device__ __forceinline__ uint32_t prefix_bits(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -80,9 +97,24 @@ struct Group {
     }
     return v;
   }
+  __device__ uint32_t max32(uint32_t v) const {
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) { const uint32_t t = __shfl_xor(v, o, G); v = t > v ? t : v; }
+    return v;
+  }
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= (uint32_t)o) v += t;
+  }
+  return v;
+}
 
 // ---------------------------------------------------------------- probes
 struct Bucket { uint4 s0, s1, s2, s3; };
@@ -129,35 +161,114 @@ __device__ __forceinline__ void probe(const EdgeSlot* t, uint64_t mask, uint64_t
 constexpr uint32_t kDepthMask = 0x0FFFFFFFu;   // frontier entry: {path, depth | child flags << 28}
 constexpr uint32_t kUnresolved = 0xFFFFFFFFu;  // key list entry still holds a key id
 
-struct Scratch {
-  uint2* stack;    // {path, depth}
-  uint32_t* cand;  // path ids
-  uint2* keys;     // key id, then {record off, cumulative start}
-  uint32_t scap, ccap, kcap;
-};
+// One step of trie_match/4 + 'trie_match_#'/2 (vmq_reg_trie.erl:358-383) for
+// up to G frontier entries, one per lane: the three edge probes, issued
+// before any is resolved.  The node's cached edge flags (`fl`) skip '#' / '+'
+// / literal probes that must miss.
+struct StepOut { uint32_t hc, wc, pc, wf, pf; bool at_end; };
 
-enum : uint32_t { kErrDeferFull = 1u, kErrFrontier = 2u, kErrOverflow = 4u, kErrMismatch = 8u };
+template <int G>
+__device__ __forceinline__ StepOut probe_step(const MatchArgs& a, const Group<G>& g, bool act, uint32_t node,
+                                              uint32_t d, uint32_t fl, uint32_t L, const uint32_t* w,
+                                              uint32_t wreg) {
+  const bool at_end = act && d == L;
+  const uint32_t wsh = g.bcast(wreg, d % G);   // all group lanes take part
+  uint32_t wd = kUnknownWord;
+  if (act && !at_end) wd = d < (uint32_t)G ? wsh : w[d];
+  const bool do_h = act && (fl & kHasHash);
+  const bool do_w = act && !at_end && (fl & kHasWord) && wd != kPlus && wd != kHash && wd != kUnknownWord;
+  const bool do_p = act && !at_end && (fl & kHasPlus);
+  const uint64_t bh = edge_hash(node, kHash) & a.edge_mask;
+  const uint64_t bw = edge_hash(node, wd) & a.edge_mask;
+  const uint64_t bp = edge_hash(node, kPlus) & a.edge_mask;
+  Bucket Bh{}, Bw{}, Bp{};
+  if (do_h) Bh = load_bucket(a.edges, bh);
+  if (do_w) Bw = load_bucket(a.edges, bw);
+  if (do_p) Bp = load_bucket(a.edges, bp);
+  StepOut o{kNone, kNone, kNone, 0, 0, at_end};
+  uint32_t hf = 0;
+  if (do_h) probe(a.edges, a.edge_mask, bh, Bh, node, kHash, o.hc, hf);
+  if (do_w) probe(a.edges, a.edge_mask, bw, Bw, node, wd, o.wc, o.wf);
+  if (do_p) probe(a.edges, a.edge_mask, bp, Bp, node, kPlus, o.pc, o.pf);
+  return o;
+}
+
+// Exact-topic fingerprint of the publish, computed by the G lanes of a group.
+template <int G>
+__device__ __forceinline__ uint64_t publish_fp(const vmqg_pub& pub, const uint32_t* w, uint32_t wreg,
+                                               const Group<G>& g) {
+  const uint32_t L = pub.nwords;
+  uint64_t part = 0;
+  for (uint32_t i = g.lane; i < L; i += G) part += fp_word(i < (uint32_t)G ? wreg : w[i], i);
+  return fp_final(g.sum64(part), pub.mountpoint, L);
+}
+
+// The exact slot of (MP, Topic), or null: fingerprint probe, then the stored
+// MP and words compared group-parallel.
+template <int G>
+__device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, const uint32_t* w, uint32_t wreg,
+                                       const Group<G>& g) {
+  const uint32_t L = pub.nwords;
+  const uint64_t fp = publish_fp<G>(pub, w, wreg, g);
+  uint64_t b = fp & a.exact_mask;
+  for (uint64_t iter = 0; iter <= a.exact_mask; iter++) {
+    const ExactSlot* bk = a.exact + b * kExactSlotsPerBucket;
+    bool seen_empty = false;
+    for (uint32_t j = 0; j < kExactSlotsPerBucket; j++) {
+      const ExactSlot& e = bk[j];
+      const uint32_t nw = e.nwords;
+      if (nw == kEmpty) { seen_empty = true; break; }
+      if (e.fp != fp || (nw & ~kExactHigh) != L) continue;
+      const uint32_t* xw = a.exwords + e.words_off;
+      bool diff = g.lane == 0 && xw[0] != pub.mountpoint;
+      for (uint32_t i = g.lane; i < L; i += G) diff |= xw[1 + i] != (i < (uint32_t)G ? wreg : w[i]);
+      if (g.ballot(diff) == 0) return &e;
+    }
+    if (seen_empty) break;
+    b = (b + 1) & a.exact_mask;
+  }
+  return nullptr;
+}
+
+// ============================================================== fast tier
+// A group's three lists live in LDS interleaved over the block's SLOTS
+// groups: entry i of group `slot` sits at i * SLOTS + (slot ^ swz(i)), the
+// XOR moving the G consecutive entries a group touches at once onto
+// different banks, so neither the G lanes of a group nor groups at the same
+// depth conflict (SLOTS is a multiple of 32).
+template <int G>
+struct FastScratch {
+  static constexpr uint32_t GPW = 64 / G, SLOTS = kWaves * GPW;
+  static constexpr uint32_t SH = G == 2 ? 4 : G == 4 ? 3 : 2;   // 32 / G = 1 << SH
+  static constexpr uint32_t SC = FastCaps<G>::S, CC = FastCaps<G>::C, KC = FastCaps<G>::K;
+  uint2* stack; uint32_t* cand; uint2* keys;
+  uint32_t slot;
+  __device__ uint32_t at(uint32_t i) const { return i * SLOTS + (slot ^ ((i & (G - 1)) << SH)); }
+  __device__ uint2& st(uint32_t i) const { return stack[at(i)]; }
+  __device__ uint32_t& cd(uint32_t i) const { return cand[at(i)]; }
+  __device__ uint2& ky(uint32_t i) const { return keys[at(i)]; }
+};
 
 // Per-publish result of the walk: keys[0..nk) hold {record off, cum start}.
 struct Matched {
-  uint32_t nk, ksum, total;
+  uint32_t nk, nkr, ksum, total_rec;   // keys, non-empty keys, records, record-mode total
   uint64_t rmask;
-  bool overflow;
+  bool overflow;                        // the lists overflowed or a node >= 64: the wave tier takes it
 };
 
-// ----------------------------------------------------- walk + resolution
 template <int G>
-__device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const Scratch& s, const Group<G>& g) {
+__device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const FastScratch<G>& s,
+                                const Group<G>& g) {
   const uint32_t L = pub.nwords;
   const uint32_t* w = a.words + pub.word_off;
   const bool dollar = (pub.flags & VMQG_PUB_DOLLAR) != 0;
   const bool mp_ok = pub.mountpoint < a.max_mp && L > 0;
   // lane i of the group keeps word i (i < G); deeper words come from memory
   const uint32_t wreg = g.lane < L ? w[g.lane] : kUnknownWord;
-  Matched m{0, 0, 0, 0, false};
+  Matched m{0, 0, 0, 0, 0, false};
   uint32_t nc = 0, sp = 0;
   if (mp_ok) {
-    if (g.lane == 0) s.stack[0] = make_uint2(pub.mountpoint, kHasAll << 28);   // {MP, root}: probe all
+    if (g.lane == 0) s.st(0) = make_uint2(pub.mountpoint, kHasAll << 28);   // {MP, root}: probe all
     sp = 1;
   }
   wave_sync();
@@ -168,41 +279,22 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
     const uint32_t base = sp - k;
     const bool act = g.lane < k;
     uint32_t node = 0, d = 0, fl = 0;
-    if (act) { const uint2 e = s.stack[base + g.lane]; node = e.x; d = e.y & kDepthMask; fl = e.y >> 28; }
+    if (act) { const uint2 e = s.st(base + g.lane); node = e.x; d = e.y & kDepthMask; fl = e.y >> 28; }
     sp = base;
     wave_sync();
-    const bool at_end = act && d == L;
-    const uint32_t wsh = g.bcast(wreg, d % G);   // all group lanes take part
-    uint32_t wd = kUnknownWord;
-    if (act && !at_end) wd = d < (uint32_t)G ? wsh : w[d];
-    // the node's cached edge flags skip '#' / '+' probes that must miss
-    const bool do_h = act && (fl & kHasHash);
-    const bool do_w = act && !at_end && (fl & kHasWord) && wd != kPlus && wd != kHash && wd != kUnknownWord;
-    const bool do_p = act && !at_end && (fl & kHasPlus);
-    const uint64_t bh = edge_hash(node, kHash) & a.edge_mask;
-    const uint64_t bw = edge_hash(node, wd) & a.edge_mask;
-    const uint64_t bp = edge_hash(node, kPlus) & a.edge_mask;
-    Bucket Bh{}, Bw{}, Bp{};
-    if (do_h) Bh = load_bucket(a.edges, bh);
-    if (do_w) Bw = load_bucket(a.edges, bw);
-    if (do_p) Bp = load_bucket(a.edges, bp);
-    uint32_t hc = kNone, wc = kNone, pc = kNone, hf = 0, wf = 0, pf = 0;
-    if (do_h) probe(a.edges, a.edge_mask, bh, Bh, node, kHash, hc, hf);
-    if (do_w) probe(a.edges, a.edge_mask, bw, Bw, node, wd, wc, wf);
-    if (do_p) probe(a.edges, a.edge_mask, bp, Bp, node, kPlus, pc, pf);
-
+    const StepOut o = probe_step<G>(a, g, act, node, d, fl, L, w, wreg);
     // candidates: the '#' child (:377-383) and, with no words left, the node itself (:361-363)
-    const uint64_t m_hc = g.ballot(hc != kNone), m_end = g.ballot(at_end);
+    const uint64_t m_hc = g.ballot(o.hc != kNone), m_end = g.ballot(o.at_end);
     const uint32_t n_hc = (uint32_t)__popcll(m_hc), n_new_c = n_hc + (uint32_t)__popcll(m_end);
     // frontier: the W and '+' children (:364-375)
-    const uint64_t m_wc = g.ballot(wc != kNone), m_pc = g.ballot(pc != kNone);
+    const uint64_t m_wc = g.ballot(o.wc != kNone), m_pc = g.ballot(o.pc != kNone);
     const uint32_t n_pc = (uint32_t)__popcll(m_pc), n_new_s = n_pc + (uint32_t)__popcll(m_wc);
-    if (nc + n_new_c > s.ccap || sp + n_new_s > s.scap) { m.overflow = true; break; }
-    if (hc != kNone) s.cand[nc + prefix_bits(m_hc)] = hc;
-    if (at_end) s.cand[nc + n_hc + prefix_bits(m_end)] = node;
+    if (nc + n_new_c > s.CC || sp + n_new_s > s.SC) { m.overflow = true; break; }
+    if (o.hc != kNone) s.cd(nc + prefix_bits(m_hc)) = o.hc;
+    if (o.at_end) s.cd(nc + n_hc + prefix_bits(m_end)) = node;
     nc += n_new_c;
-    if (pc != kNone) s.stack[sp + prefix_bits(m_pc)] = make_uint2(pc, (d + 1) | (pf << 28));
-    if (wc != kNone) s.stack[sp + n_pc + prefix_bits(m_wc)] = make_uint2(wc, (d + 1) | (wf << 28));
+    if (o.pc != kNone) s.st(sp + prefix_bits(m_pc)) = make_uint2(o.pc, (d + 1) | (o.pf << 28));
+    if (o.wc != kNone) s.st(sp + n_pc + prefix_bits(m_wc)) = make_uint2(o.wc, (d + 1) | (o.wf << 28));
     sp += n_new_s;
     wave_sync();
   }
@@ -214,28 +306,30 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
     for (uint32_t c0 = 0; c0 < nc; c0 += G) {
       const uint32_t ci = c0 + g.lane;
       uint32_t nkeys = 0, key = kNone, off0 = 0, cnt0 = 0;
+      bool high = false;
       if (ci < nc) {
-        const uint32_t path = s.cand[ci];
+        const uint32_t path = s.cd(ci);
         if (path < a.node_cap) {
           const uint4 r = *reinterpret_cast<const uint4*>(a.nodes + path);
           const uint2 r2 = *reinterpret_cast<const uint2*>(&a.nodes[path].off0);
           const bool valid = (r.x & kNodeEmits) == kNodeEmits &&
                              !(dollar && (r.x & kNodeDollarSkip));   // MQTT-4.7.2-1 (:285-288)
           if (valid) {
-            nkeys = r.x >> 8;
+            nkeys = (r.x >> 8) & 0xFFFFFFu;
             key = r.y;
             off0 = r2.x;
             cnt0 = r2.y;
             rmask |= ((uint64_t)r.w << 32) | r.z;
+            high = (r.x & kNodeHigh) != 0;
           }
         }
       }
       const uint32_t incl = g.incl_scan(nkeys);
       const uint32_t tot = g.last(incl);
-      if (nk + tot > s.kcap) { m.overflow = true; break; }
+      if (nk + tot > s.KC || g.ballot(high) != 0) { m.overflow = true; break; }
       const uint32_t at = nk + incl - nkeys;
-      if (nkeys == 1) s.keys[at] = make_uint2(off0, cnt0);   // resolved inline
-      else for (uint32_t j = 0; j < nkeys; j++) s.keys[at + j] = make_uint2(a.keylist[key + j], kUnresolved);
+      if (nkeys == 1) s.ky(at) = make_uint2(off0, cnt0);   // resolved inline
+      else for (uint32_t j = 0; j < nkeys; j++) s.ky(at + j) = make_uint2(a.keylist[key + j], kUnresolved);
       nk += tot;
     }
   }
@@ -243,72 +337,70 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const S
 
   // ---- the exact candidate {Topic, node()} and remote exact subscribers (:62, :514-520)
   if (!m.overflow && mp_ok) {
-    uint64_t part = 0;
-    for (uint32_t i = g.lane; i < L; i += G) part += fp_word(i < (uint32_t)G ? wreg : w[i], i);
-    const uint64_t fp = fp_final(g.sum64(part), pub.mountpoint, L);
-    uint64_t b = fp & a.exact_mask;
-    for (uint64_t iter = 0; iter <= a.exact_mask; iter++) {
-      const ExactSlot* bk = a.exact + b * kExactSlotsPerBucket;
-      bool seen_empty = false, found = false;
-      for (uint32_t j = 0; j < kExactSlotsPerBucket && !found; j++) {
-        const ExactSlot e = bk[j];
-        if (e.nwords == kEmpty) { seen_empty = true; break; }
-        if (e.fp != fp || e.nwords != L) continue;
-        // exactness: the stored MP and words, compared group-parallel
-        const uint32_t* xw = a.exwords + e.words_off;
-        bool diff = g.lane == 0 && xw[0] != pub.mountpoint;
-        for (uint32_t i = g.lane; i < L; i += G) diff |= xw[1 + i] != (i < (uint32_t)G ? wreg : w[i]);
-        if (g.ballot(diff) != 0) continue;
-        found = true;
-        rmask |= e.rmask;
-        if (e.count != 0) {
-          if (nk + 1 > s.kcap) m.overflow = true;
-          else { if (g.lane == 0) s.keys[nk] = make_uint2(e.off, e.count); nk += 1; }
-        }
+    const ExactSlot* e = find_exact<G>(a, pub, w, wreg, g);
+    if (e) {
+      const uint4 q = *reinterpret_cast<const uint4*>(&e->off);   // {off, count, rmask lo, hi}
+      rmask |= ((uint64_t)q.w << 32) | q.z;
+      if (e->nwords & kExactHigh) m.overflow = true;
+      else if (q.y != 0) {
+        if (nk + 1 > s.KC) m.overflow = true;
+        else { if (g.lane == 0) s.ky(nk) = make_uint2(q.x, q.y); nk += 1; }
       }
-      if (found || seen_empty) break;
-      b = (b + 1) & a.exact_mask;
     }
   }
   wave_sync();
-  m.rmask = g.or64(rmask) & ~(1ull << a.local_node);
+  m.rmask = g.or64(rmask);
+  if (a.local_node < kLowNodes) m.rmask &= ~(1ull << a.local_node);
   if (m.overflow) return m;
 
   // ---- record ranges per key: lookup_subs/1 (:87-94)
-  uint32_t ksum = 0;
+  uint32_t ksum = 0, nkr = 0;
   for (uint32_t k0 = 0; k0 < nk; k0 += G) {
     const uint32_t ki = k0 + g.lane;
     uint32_t cnt = 0, off = 0;
     if (ki < nk) {
-      const uint2 e = s.keys[ki];
+      const uint2 e = s.ky(ki);
       if (e.y != kUnresolved) { off = e.x; cnt = e.y; }
       else if (e.x < a.key_cap) { const uint2 kd = *reinterpret_cast<const uint2*>(a.keydesc + e.x); off = kd.x; cnt = kd.y; }
     }
     const uint32_t incl = g.incl_scan(cnt);
+    nkr += (uint32_t)__popcll(g.ballot(cnt != 0));
     wave_sync();
-    if (ki < nk) s.keys[ki] = make_uint2(off, ksum + incl - cnt);
+    if (ki < nk) s.ky(ki) = make_uint2(off, ksum + incl - cnt);
     ksum += g.last(incl);
   }
   wave_sync();
   m.nk = nk;
+  m.nkr = nkr;
   m.ksum = ksum;
-  m.total = ksum + (uint32_t)__popcll(m.rmask);
+  m.total_rec = ksum + (uint32_t)__popcll(m.rmask);
   return m;
 }
 
-// r-th emission of a publish whose keys are {off, cum start} in `keys`.
-__device__ __forceinline__ uint4 emission(const MatchArgs& a, const uint2* keys, uint32_t nk, uint32_t ksum,
+// Output entries of a publish: records (OUT 0) or ranges (OUT 1).
+template <int OUT>
+__device__ __forceinline__ uint32_t out_total(const Matched& m) {
+  return OUT ? m.nkr + (uint32_t)__popcll(m.rmask) : m.total_rec;
+}
+
+// j-th set bit of m (j < popcount(m))
+__device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t j) {
+  for (; j > 0; j--) m &= m - 1;
+  return (uint32_t)__builtin_ctzll(m);
+}
+
+// r-th emission of a publish whose keys are {off, cum start} in `ks`.
+template <class Keys>
+__device__ __forceinline__ uint4 emission(const MatchArgs& a, const Keys& ks, uint32_t nk, uint32_t ksum,
                                           uint64_t rmask, uint32_t r) {
   if (r < ksum) {
     uint32_t lo = 0, hi = nk;   // last key whose cumulative start <= r
-    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (keys[mid].y <= r) lo = mid; else hi = mid; }
-    const uint2 kk = keys[lo];
+    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (ks(mid).y <= r) lo = mid; else hi = mid; }
+    const uint2 kk = ks(lo);
     return *reinterpret_cast<const uint4*>(a.records + kk.x + (r - kk.y));
   }
   // j-th remote node of the mask, in node order (fold_/5 :78-84)
-  uint64_t m = rmask;
-  for (uint32_t j = r - ksum; j > 0; j--) m &= m - 1;
-  return make_uint4((VMQG_EMIT_REMOTE << 24) | (uint32_t)__builtin_ctzll(m), kNone, kNone, kNone);
+  return make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rmask, r - ksum), kNone, kNone, kNone);
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -323,106 +415,90 @@ __device__ __forceinline__ void store_rec(Record* out, uint64_t i, uint4 v) {
   }
 }
 
-// Tiers: 0 = fast (G = fast_g lanes per publish, small LDS lists); 1 = wave
-// (G = 64, one publish per wave, publishes deferred by tier 0): 256-entry LDS
-// lists first, the wave's global scratch (o_cap entries) when those overflow.
-template <int TIER>
-__device__ __forceinline__ void defer_or_fail(const MatchArgs& a, uint32_t p) {
-  if (TIER == 0) {
-    const uint32_t idx = atomicAdd(&a.status[0], 1u);
-    if (idx < a.deferred_cap) a.deferred[idx] = p;
-    else atomicOr(&a.status[1], kErrDeferFull);
-  } else {
-    atomicOr(&a.status[1], kErrFrontier);
-  }
-}
-
-__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
-  const uint32_t lane = __lane_id();
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= (uint32_t)o) v += t;
-  }
-  return v;
+__device__ __forceinline__ void store_range(vmqg_range* out, uint64_t i, uint32_t off, uint32_t count) {
+  *reinterpret_cast<uint2*>(out + i) = make_uint2(off, count);
 }
 
 // ------------------------------------------------------------ COUNT pass
-// Returns false when the walk overflowed `s`.  Tier 0 defers the publish;
-// tier 1 returns to its caller, which retries with global scratch (tier 2
-// role: an overflow there is a frontier error).
-template <int G, int TIER>
-__device__ bool count_publish(const MatchArgs& a, uint32_t p, const Scratch& s, const Group<G>& g) {
+template <int G, int OUT>
+__device__ void count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g) {
   const vmqg_pub pub = a.pubs[p];
   const Matched m = walk_publish<G>(a, pub, s, g);
-  if (m.overflow && TIER == 1) return false;
-  if (g.lane != 0) return !m.overflow;
+  if (g.lane != 0) return;
   uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
-  if (m.overflow) {
-    defer_or_fail<TIER>(a, p);
+  if (m.overflow) {   // the wave tier counts it (and writes offsets[p])
+    const uint32_t idx = atomicAdd(&a.status[kStDeferred], 1u);
+    a.deferred[idx] = p;   // the list holds npub entries
     a.offsets[p] = 0;
-    kc[0] = make_uint4(0, kRewalk, 0, 0);
-    return false;
+    kc[0] = make_uint4(0, kDeferred, 0, 0);
+    return;
   }
-  a.offsets[p] = m.total;
+  const uint32_t total = out_total<OUT>(m);
+  a.offsets[p] = total;
   // key cache: total, nk, remote mask, up to two {record off, count}
   if (m.nk <= 2) {
-    const uint2 k0 = m.nk > 0 ? s.keys[0] : make_uint2(0, 0);
-    const uint2 k1 = m.nk > 1 ? s.keys[1] : make_uint2(0, m.ksum);
+    const uint2 k0 = m.nk > 0 ? s.ky(0) : make_uint2(0, 0);
+    const uint2 k1 = m.nk > 1 ? s.ky(1) : make_uint2(0, m.ksum);
     const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
-    kc[0] = make_uint4(m.total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
+    kc[0] = make_uint4(total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
     kc[1] = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
   } else {
-    kc[0] = make_uint4(m.total, kRewalk, 0, 0);
+    kc[0] = make_uint4(total, kRewalk, 0, 0);
   }
-  return true;
 }
 
 // ------------------------------------------------------------- EMIT pass
 // Per-group result of the resolve step, staged in LDS for the wave copy.
 struct GroupMeta {
-  uint32_t rel, span, nk, ksum;   // output start relative to the wave's first publish, length
+  uint32_t rel, span, nk, ksum;      // output start relative to the wave's first publish, length
   uint32_t rm_lo, rm_hi, ok, crel;   // crel: start among the wave's copied (ok) records
 };
 
-// EMIT for the GPW consecutive publishes [first, first + n) of one wave.
-// Resolve (key cache or re-walk) is per group; the copy is wave-wide over
-// the wave's output range minus the ranges of publishes a later tier
-// writes, so every store instruction writes up to 64 x 16 B = 1 KiB
-// contiguous.  `s2` (tier 1): global scratch for a re-walk that overflows `s`.
+// Resolve publish first + gidx of a wave: from the key cache, or by a
+// re-walk (> 2 keys).  Leaves the keys {off, cum start} in the group's LDS
+// key list.  ok = false: the wave tier writes it (or an error is latched).
+template <int G, int OUT>
+__device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
+                        uint32_t& nk, uint32_t& ksum, uint64_t& rmask, uint64_t& obase, uint64_t& oend) {
+  const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+  const uint4 h = kc[0];
+  obase = a.offsets[p];
+  oend = a.offsets[p + 1];
+  uint32_t total;
+  if (h.y == kDeferred) return false;   // written by the wave tier
+  if (h.y == kRewalk) {
+    const Matched m = walk_publish<G>(a, a.pubs[p], s, g);
+    if (m.overflow) return false;   // written by the wave tier
+    total = out_total<OUT>(m); nk = m.nk; ksum = m.ksum; rmask = m.rmask;
+  } else {
+    total = h.x; nk = h.y; rmask = ((uint64_t)h.w << 32) | h.z;
+    const uint4 k = kc[1];
+    ksum = k.y + k.w;
+    if (g.lane == 0) {
+      s.ky(0) = make_uint2(k.x, 0u);
+      s.ky(1) = make_uint2(k.z, k.y);
+    }
+    wave_sync();
+  }
+  const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
+  if (oend > cap) { if (g.lane == 0) atomicOr(&a.status[kStErr], kErrOverflow); return false; }
+  if (oend - obase != total) { if (g.lane == 0) atomicOr(&a.status[kStErr], kErrMismatch); return false; }
+  return true;
+}
+
+// Records mode: EMIT for the GPW consecutive publishes [first, first + n)
+// of one wave.  Resolve is per group; the copy is wave-wide over the wave's
+// output range minus the ranges of publishes the wave tier writes, so every
+// store instruction writes up to 64 x 16 B = 1 KiB contiguous.
 template <int G, int GPW, bool NT, int U>
-__device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const Scratch& s, const Scratch* s2,
-                          const Group<G>& g, GroupMeta* gm, const uint2* keys_wave, uint32_t kstride) {
+__device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const FastScratch<G>& s,
+                          const Group<G>& g, GroupMeta* gm, uint32_t slot0) {
   const uint32_t p = first + g.gidx;
   const bool valid = g.gidx < n;
-  uint32_t total = 0, nk = 0, ksum = 0;
+  uint32_t nk = 0, ksum = 0;
   uint64_t rmask = 0, obase = 0, oend = 0;
-  bool ok = valid;
-  if (valid) {
-    const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
-    const uint4 h = kc[0];
-    obase = a.offsets[p];
-    oend = a.offsets[p + 1];
-    if (h.y == kRewalk) {
-      Matched m = walk_publish<G>(a, a.pubs[p], s, g);
-      if (m.overflow && s2) {
-        m = walk_publish<G>(a, a.pubs[p], *s2, g);
-        keys_wave = s2->keys;   // G == 64: one publish per wave
-      }
-      if (m.overflow) ok = false;   // written by the next tier (or a latched frontier error)
-      else { total = m.total; nk = m.nk; ksum = m.ksum; rmask = m.rmask; }
-    } else {
-      total = h.x; nk = h.y < 2 ? h.y : 2; rmask = ((uint64_t)h.w << 32) | h.z;
-      const uint4 k = kc[1];
-      ksum = k.y + k.w;
-      if (g.lane == 0) {
-        s.keys[0] = make_uint2(k.x, 0u);
-        s.keys[1] = make_uint2(k.z, k.y);
-      }
-    }
-    if (ok && oend > a.out_cap) { if (g.lane == 0) atomicOr(&a.status[1], kErrOverflow); ok = false; }
-    if (ok && oend - obase != total) { if (g.lane == 0) atomicOr(&a.status[1], kErrMismatch); ok = false; }
-  }
+  bool ok = false;
+  if (valid) ok = resolve<G, 0>(a, p, s, g, nk, ksum, rmask, obase, oend);
   const uint64_t wbase = a.offsets[first];
   if (g.lane == 0)
     gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : 0u, ok ? (uint32_t)(oend - obase) : 0u,
@@ -430,16 +506,11 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
   wave_sync();
   // compact the copied ranges: crel = exclusive scan of the ok spans
   const uint32_t lane = __lane_id();
-  uint32_t Tok;
-  if (GPW == 1) {
-    Tok = gm[0].span;
-  } else {
-    const uint32_t sp = lane < (uint32_t)GPW ? gm[lane].span : 0u;
-    const uint32_t incl = wave_incl_scan32(sp);
-    if (lane < (uint32_t)GPW) gm[lane].crel = incl - sp;
-    Tok = __shfl(incl, GPW - 1, 64);
-    wave_sync();
-  }
+  const uint32_t sp = lane < (uint32_t)GPW ? gm[lane].span : 0u;
+  const uint32_t incl = wave_incl_scan32(sp);
+  if (lane < (uint32_t)GPW) gm[lane].crel = incl - sp;
+  const uint32_t Tok = __shfl(incl, GPW - 1, 64);
+  wave_sync();
   // U records per lane in flight: all loads issued before the stores
   uint32_t j = 0;
   for (uint32_t r0 = lane; r0 < Tok; r0 += 64 * U) {
@@ -454,7 +525,9 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
         while (j + 1 < (uint32_t)GPW && gm[j + 1].crel <= r) j++;
         const GroupMeta m = gm[j];
         const uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
-        v[u] = emission(a, keys_wave + (uint64_t)j * kstride, m.nk, m.ksum, rm, r - m.crel);
+        FastScratch<G> sj = s;
+        sj.slot = slot0 + j;
+        v[u] = emission(a, [&](uint32_t i) -> uint2 { return sj.ky(i); }, m.nk, m.ksum, rm, r - m.crel);
         dst[u] = wbase + m.rel + (r - m.crel);
       }
     }
@@ -465,283 +538,304 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
   wave_sync();
 }
 
+// Range mode: each group writes its publish's non-empty keys as
+// {record off, count}, then its remote nodes as {node, 0}.
+template <int G>
+__device__ void emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g) {
+  uint32_t nk = 0, ksum = 0;
+  uint64_t rmask = 0, obase = 0, oend = 0;
+  if (!resolve<G, 1>(a, p, s, g, nk, ksum, rmask, obase, oend)) return;
+  uint32_t pos = 0;
+  for (uint32_t k0 = 0; k0 < nk; k0 += G) {
+    const uint32_t ki = k0 + g.lane;
+    uint32_t off = 0, cnt = 0;
+    if (ki < nk) {
+      const uint2 e = s.ky(ki);
+      const uint32_t next = ki + 1 < nk ? s.ky(ki + 1).y : ksum;
+      off = e.x;
+      cnt = next - e.y;
+    }
+    const uint64_t mb = g.ballot(cnt != 0);
+    if (cnt != 0) store_range(a.out_rng, obase + pos + prefix_bits(mb), off, cnt);   // mb: this group's lanes only
+    pos += (uint32_t)__popcll(mb);
+  }
+  const uint32_t nrem = (uint32_t)__popcll(rmask);
+  for (uint32_t j = g.lane; j < nrem; j += G) store_range(a.out_rng, obase + pos + j, select_bit(rmask, j), 0u);
+}
+
 // --------------------------------------------------------------- kernels
-template <int MODE, int G, bool NT>
+template <int MODE, int OUT, int G, bool NT>
 __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
-  constexpr int GPW = 64 / G;   // groups (publishes) per wave
-  constexpr uint32_t SC = FastCaps<G>::S, CC = FastCaps<G>::C, KC = FastCaps<G>::K;
-  __shared__ uint2 st[kWaves * GPW][SC];
-  __shared__ uint32_t cd[kWaves * GPW][CC];
-  __shared__ uint2 ky[kWaves * GPW][KC];
+  using FS = FastScratch<G>;
+  constexpr int GPW = FS::GPW;
+  __shared__ uint2 st[FS::SC * FS::SLOTS];
+  __shared__ uint32_t cd[FS::CC * FS::SLOTS];
+  __shared__ uint2 ky[FS::KC * FS::SLOTS];
   __shared__ GroupMeta gm[kWaves][GPW];
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t slot = wv * GPW + g.gidx;
-  const Scratch s{st[slot], cd[slot], ky[slot], SC, CC, KC};
+  const FS s{st, cd, ky, wv * GPW + g.gidx};
   const uint32_t stride = gridDim.x * kWaves * GPW;
   for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
     if (MODE == 0) {
-      if (g.gidx < n) count_publish<G, 0>(a, base + g.gidx, s, g);
+      if (g.gidx < n) count_publish<G, OUT>(a, base + g.gidx, s, g);
+    } else if (OUT == 0) {
+      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
     } else {
-      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, nullptr, g, gm[wv], ky[wv * GPW], KC);
+      if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g);
     }
     wave_sync();
   }
 }
 
-// Tier 1: one publish per wave from the deferred list; LDS lists, then the
-// wave's global scratch.
-template <int MODE, bool NT>
-__global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
-  constexpr uint32_t kMidCap = 256;
-  __shared__ uint2 st[kWaves][kMidCap];
-  __shared__ uint32_t cd[kWaves][kMidCap];
-  __shared__ uint2 ky[kWaves][kMidCap];
-  __shared__ GroupMeta gm[kWaves][1];
-  const Group<64> g;
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
-  const Scratch s{st[wv], cd[wv], ky[wv], kMidCap, kMidCap, kMidCap};
-  const Scratch so{a.o_stack + gw * a.o_cap, a.o_cand + gw * a.o_cap, a.o_keys + gw * a.o_cap,
-                   a.o_cap, a.o_cap, a.o_cap};
-  uint32_t n = a.status[0];
-  if (n > a.deferred_cap) n = a.deferred_cap;
-  const uint32_t nwaves = gridDim.x * kWaves;
-  for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
-    const uint32_t p = a.deferred[d];
-    if (MODE == 0) {
-      if (!count_publish<64, 1>(a, p, s, g)) {
-        if (__lane_id() == 0) atomicAdd(&a.status[2], 1u);
-        count_publish<64, 2>(a, p, so, g);
-      }
-    } else {
-      emit_wave<64, 1, NT, 8>(a, p, 1, s, &so, g, gm[wv], s.keys, 0);
-    }
-    wave_sync();
-  }
-}
+// ============================================================== wave tier
+constexpr uint32_t kWStack = 256, kWCand = 256, kWKeys = 256, kHiWords = kMaxNodes / 32;
 
-// ------------------------------------------------------ fused single pass
-// k_match_fused: one launch does what COUNT + scan + EMIT do above.  A block
-// takes chunks of CH = 4 * (64 / G) consecutive publishes by ticket (so a
-// chunk's predecessors are always owned by running blocks) and for each:
-//   1. walks every publish with G lanes (fast LDS lists, as COUNT);
-//   2. publishes that overflow the fast lists are walked again by a whole
-//      wave with global scratch (o_stack / o_cand / o_keys) — their count;
-//   3. scans the chunk's counts (per wave, then across the 4 waves);
-//   4. gets the chunk's output base by decoupled look-back over the
-//      predecessors' 8-B {tag, flag, value} granules (agent-scope relaxed
-//      atomics: the granule is its own flag, cdna_hip_programming.md G16 R2);
-//   5. writes offsets[] for its publishes;
-//   6. copies the fast publishes' records wave-wide (contiguous, NT stores),
-//      skipping the ranges of the wave-path publishes;
-//   7. re-walks each wave-path publish with a whole wave and copies its
-//      records.
-// The walk of one chunk overlaps the record stores of the other blocks on
-// the CU, which a COUNT -> EMIT kernel boundary forbids.
-struct FusedMeta {               // per publish of the chunk
-  uint32_t rel, span, crel, ok;  // output start / length relative to the wave; start among ok records
-  uint32_t nk, ksum, rm_lo, rm_hi;
+struct WaveLds {
+  uint2 stack[kWStack];   // tier 1's frontier stack
+  uint32_t cand[kWCand];  // candidate paths awaiting resolution
+  uint2 keys[kWKeys];     // {record off, count}, then {record off, cum start}
+  uint32_t hb[kHiWords];  // remote-node set (4,096 bits)
 };
 
-// Wave path (G = 64, global scratch) of the fused kernel: a publish whose
-// frontier / candidate / key lists overflow the fast LDS lists.  Kept out of
-// line so the fast walk's register budget is not the sum of both paths.
-__device__ __noinline__ uint32_t wave_path_count(const MatchArgs& a, uint32_t p, const Scratch& so) {
-  const Group<64> g64;
-  const Matched mo = walk_publish<64>(a, a.pubs[p], so, g64);
-  return mo.overflow ? kNone : mo.total;
-}
+template <int MODE, int OUT, bool NT>
+struct WaveWalk {
+  const MatchArgs& a;
+  WaveLds& W;
+  uint2* stack;
+  uint32_t scap;
+  uint64_t obase;       // output position of the publish (MODE 1)
+  uint64_t run = 0;     // entries counted / written so far (wave-uniform)
+  uint32_t nc = 0, nk = 0;
+  uint64_t rm = 0;      // lane-partial remote mask (nodes < 64)
+  bool dollar = false;
 
-template <bool NT, int U>
-__device__ __noinline__ void wave_path_emit(const MatchArgs& a, uint32_t p, const Scratch& so, uint64_t ob,
-                                            uint32_t want) {
-  const Group<64> g64;
-  const uint32_t lane = __lane_id();
-  const Matched mo = walk_publish<64>(a, a.pubs[p], so, g64);
-  if (mo.overflow) return;   // latched by the count
-  if (mo.total != want) { if (lane == 0) atomicOr(&a.status[1], kErrMismatch); return; }
-  uint32_t kk = 0;
-  for (uint32_t r0 = lane; r0 < mo.total; r0 += 64 * U) {
-    uint4 v[U];
-    bool w[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t r = r0 + 64 * u;
-      w[u] = r < mo.total;
-      if (w[u]) {
-        if (r < mo.ksum) {
-          while (kk + 1 < mo.nk && so.keys[kk + 1].y <= r) kk++;
-          const uint2 kd = so.keys[kk];
-          v[u] = *reinterpret_cast<const uint4*>(a.records + kd.x + (r - kd.y));
-        } else {
-          v[u] = emission(a, so.keys, 1, mo.ksum, mo.rmask, r);
-        }
-      }
+  __device__ WaveWalk(const MatchArgs& a_, WaveLds& W_, uint2* st, uint32_t cap, uint64_t ob)
+      : a(a_), W(W_), stack(st), scap(cap), obase(ob) {}
+
+  __device__ void add_high(uint32_t off, uint32_t cnt) {   // remote nodes >= 64 into the set
+    for (uint32_t j = 0; j < cnt; j++) {
+      const uint32_t n = a.keylist[off + j];
+      if (n < kMaxNodes) atomicOr(&W.hb[n >> 5], 1u << (n & 31));
     }
-#pragma unroll
-    for (int u = 0; u < U; u++)
-      if (w[u]) store_rec<NT>(a.out, ob + r0 + 64 * u, v[u]);
   }
-}
 
-template <int G, bool NT, int U>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_match_fused(MatchArgs a) {
-  constexpr int GPW = 64 / G;                 // publishes per wave
-  constexpr uint32_t CH = kWaves * GPW;       // publishes per chunk
-  constexpr uint32_t SC = FastCaps<G>::S, CC = FastCaps<G>::C, KC = FastCaps<G>::K;
-  __shared__ uint2 st[CH][SC];
-  __shared__ uint32_t cd[CH][CC];
-  __shared__ uint2 ky[CH][KC];
-  __shared__ FusedMeta fm[CH];
-  __shared__ uint32_t tot[CH], ovl[CH];
-  __shared__ uint64_t wtot[kWaves];
-  __shared__ uint32_t s_chunk, s_novf;
-  __shared__ uint64_t s_base;
-  const Group<G> g;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = __lane_id();
-  const uint32_t slot = wv * GPW + g.gidx;
-  const Scratch s{st[slot], cd[slot], ky[slot], SC, CC, KC};
-  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
-  const Scratch so{a.o_stack + gw * a.o_cap, a.o_cand + gw * a.o_cap, a.o_keys + gw * a.o_cap,
-                   a.o_cap, a.o_cap, a.o_cap};
-  for (;;) {
-    if (threadIdx.x == 0) { s_chunk = atomicAdd(&a.status[3], 1u); s_novf = 0; }
-    __syncthreads();
-    const uint32_t chunk = s_chunk;
-    if (chunk >= a.nchunks) break;
-    const uint32_t base = chunk * CH;
-
-    // 1. fast walks (trie_match/4 + match/4 + lookup_subs/1 of every publish)
-    const uint32_t p = base + slot;
-    const bool have = p < a.npub;
-    Matched m{0, 0, 0, 0, false};
-    if (have) m = walk_publish<G>(a, a.pubs[p], s, g);
-    if (g.lane == 0) {
-      const bool ok = have && !m.overflow;
-      tot[slot] = ok ? m.total : 0;
-      fm[slot] = FusedMeta{0, 0, 0, ok ? 1u : 0u, m.nk == 0 ? 1u : m.nk, m.ksum, (uint32_t)m.rmask,
-                           (uint32_t)(m.rmask >> 32)};
-      if (have && m.overflow) ovl[atomicAdd(&s_novf, 1u)] = slot;
+  // the buffered keys -> count / records / ranges
+  __device__ void flush_keys() {
+    const uint32_t lane = __lane_id();
+    if (nk == 0) return;
+    if (MODE == 0 && OUT == 1) { run += nk; nk = 0; return; }
+    if (MODE == 1 && OUT == 1) {
+      for (uint32_t k = lane; k < nk; k += 64) store_range(a.out_rng, obase + run + k, W.keys[k].x, W.keys[k].y);
+      run += nk;
+      nk = 0;
+      wave_sync();
+      return;
     }
-    __syncthreads();
-
-    // 2. publishes that overflowed the fast lists: counted by whole waves
-    const uint32_t novf = s_novf;
-    for (uint32_t k = wv; k < novf; k += kWaves) {
-      const uint32_t j = ovl[k];
-      const uint32_t t = wave_path_count(a, base + j, so);
-      if (lane == 0) {
-        if (t == kNone) atomicOr(&a.status[1], kErrFrontier);
-        else tot[j] = t;
-      }
+    // records: cumulative starts
+    uint32_t tot = 0;
+    for (uint32_t k0 = 0; k0 < nk; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      const uint32_t c = k < nk ? W.keys[k].y : 0u;
+      const uint32_t incl = wave_incl_scan32(c);
+      wave_sync();
+      if (MODE == 1 && k < nk) W.keys[k].y = tot + incl - c;
+      tot += __shfl(incl, 63, 64);
     }
-    if (threadIdx.x == 0 && novf) atomicAdd(&a.status[0], novf);
-    __syncthreads();
-
-    // 3. offsets inside the chunk: per-wave scans of the counts and of the
-    //    fast publishes' counts, then the waves' totals
-    const uint32_t me = wv * GPW + lane;
-    const uint32_t cnt = lane < (uint32_t)GPW ? tot[me] : 0u;
-    const uint32_t cnt_ok = lane < (uint32_t)GPW && fm[me].ok ? cnt : 0u;
-    const uint32_t incl = wave_incl_scan32(cnt);
-    const uint32_t incl_ok = wave_incl_scan32(cnt_ok);
-    const uint32_t wsum = __shfl(incl, 63, 64), wsum_ok = __shfl(incl_ok, 63, 64);
-    if (lane < (uint32_t)GPW) { fm[me].rel = incl - cnt; fm[me].span = cnt; fm[me].crel = incl_ok - cnt_ok; }
-    if (lane == 0) wtot[wv] = wsum;
-    __syncthreads();
-    uint64_t wrel = 0, agg = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < (uint32_t)kWaves; w++) { if (w < wv) wrel += wtot[w]; agg += wtot[w]; }
-
-    // 4. chunk base: decoupled look-back
-    if (wv == 0) {
-      const uint64_t b = lookback(a.lookback, a.lb_tag, a.status, chunk, agg);
-      if (lane == 0) s_base = b;
-    }
-    __syncthreads();
-    const uint64_t cbase = s_base;
-    const bool fits = cbase + agg <= a.out_cap;
-    if (threadIdx.x == 0 && !fits) atomicOr(&a.status[1], kErrOverflow);
-
-    // 5. offsets (exclusive prefix; the batch's last publish also writes the total)
-    if (lane < (uint32_t)GPW) {
-      const uint32_t pp = base + me;
-      if (pp < a.npub) a.offsets[pp] = cbase + wrel + (incl - cnt);
-      if (pp + 1 == a.npub) a.offsets[a.npub] = cbase + agg;
-    }
-
-    // 6. fast publishes: one contiguous copy per wave, U records per lane in flight
-    if (fits) {
-      const uint64_t wbase = cbase + wrel;
-      const FusedMeta* wm = fm + wv * GPW;
-      uint32_t j = 0;
-      for (uint32_t r0 = lane; r0 < wsum_ok; r0 += 64 * U) {
+    wave_sync();
+    if (MODE == 1) {
+      constexpr int U = 8;
+      const uint32_t n = nk;
+      auto ks = [&](uint32_t i) -> uint2 { return W.keys[i]; };
+      for (uint32_t r0 = lane; r0 < tot; r0 += 64 * U) {
         uint4 v[U];
-        uint64_t dst[U];
-        bool w[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
           const uint32_t r = r0 + 64 * u;
-          w[u] = r < wsum_ok;
-          if (w[u]) {
-            while (j + 1 < (uint32_t)GPW && wm[j + 1].crel <= r) j++;
-            const FusedMeta mm = wm[j];
-            const uint64_t rm = ((uint64_t)mm.rm_hi << 32) | mm.rm_lo;
-            v[u] = emission(a, ky[wv * GPW + j], mm.nk, mm.ksum, rm, r - mm.crel);
-            dst[u] = wbase + mm.rel + (r - mm.crel);
-          }
+          if (r < tot) v[u] = emission(a, ks, n, tot, 0, r);
         }
 #pragma unroll
-        for (int u = 0; u < U; u++)
-          if (w[u]) store_rec<NT>(a.out, dst[u], v[u]);
+        for (int u = 0; u < U; u++) {
+          const uint32_t r = r0 + 64 * u;
+          if (r < tot) store_rec<NT>(a.out, obase + run + r, v[u]);
+        }
+      }
+      wave_sync();
+    }
+    run += tot;
+    nk = 0;
+  }
+
+  // the buffered candidates -> keys (match/4, match_/3 :283-303)
+  __device__ void flush_cands() {
+    const uint32_t lane = __lane_id();
+    for (uint32_t c0 = 0; c0 < nc; c0 += 64) {
+      const uint32_t ci = c0 + lane;
+      uint32_t nkeys = 0, key = kNone, off0 = 0, cnt0 = 0;
+      if (ci < nc) {
+        const uint32_t path = W.cand[ci];
+        if (path < a.node_cap) {
+          const NodeRec r = a.nodes[path];
+          const bool valid = (r.meta & kNodeEmits) == kNodeEmits && !(dollar && (r.meta & kNodeDollarSkip));
+          if (valid) {
+            nkeys = (r.meta >> 8) & 0xFFFFFFu;
+            key = r.key; off0 = r.off0; cnt0 = r.cnt0;
+            rm |= ((uint64_t)r.rmask_hi << 32) | r.rmask_lo;
+            if (r.meta & kNodeHigh) add_high(r.hi_off, r.hi_cnt);
+          }
+        }
+      }
+      const Group<64> g;
+      const uint32_t maxk = g.max32(nkeys);
+      for (uint32_t j = 0; j < maxk; j++) {
+        uint32_t off = 0, cnt = 0;
+        if (j < nkeys) {
+          if (nkeys == 1) { off = off0; cnt = cnt0; }
+          else {
+            const uint32_t kid = a.keylist[key + j];
+            if (kid < a.key_cap) { const KeyDesc kd = a.keydesc[kid]; off = kd.off; cnt = kd.count; }
+          }
+        }
+        const uint64_t mb = __ballot(cnt != 0);
+        const uint32_t nn = (uint32_t)__popcll(mb);
+        if (nk + nn > kWKeys) flush_keys();
+        if (cnt != 0) W.keys[nk + prefix_bits(mb)] = make_uint2(off, cnt);
+        nk += nn;
+        wave_sync();
       }
     }
-
-    // 7. wave-path publishes: re-walk, then a 64-lane copy in key order
-    for (uint32_t k = wv; fits && k < novf; k += kWaves) {
-      const uint32_t j = ovl[k];
-      uint64_t ob = cbase + fm[j].rel;   // + the totals of the waves before publish j's
-      for (uint32_t w = 0; w < j / GPW; w++) ob += wtot[w];
-      wave_path_emit<NT, U>(a, base + j, so, ob, tot[j]);
-    }
-    __syncthreads();   // LDS is reused by the next chunk
+    nc = 0;
+    wave_sync();
   }
-}
 
-uint32_t fused_chunk(uint32_t fast_g) { return kWaves * (64 / fast_g); }
+  // returns false when the frontier stack overflowed (tier 2 retries)
+  __device__ bool run_publish(uint32_t p) {
+    const Group<64> g;
+    const uint32_t lane = __lane_id();
+    const vmqg_pub pub = a.pubs[p];
+    const uint32_t L = pub.nwords;
+    const uint32_t* w = a.words + pub.word_off;
+    dollar = (pub.flags & VMQG_PUB_DOLLAR) != 0;
+    const bool mp_ok = pub.mountpoint < a.max_mp && L > 0;
+    const uint32_t wreg = lane < L ? w[lane] : kUnknownWord;
+    for (uint32_t i = lane; i < kHiWords; i += 64) W.hb[i] = 0;
+    uint32_t sp = 0;
+    if (mp_ok) { if (lane == 0) stack[0] = make_uint2(pub.mountpoint, kHasAll << 28); sp = 1; }
+    wave_sync();
+    while (sp > 0) {
+      const uint32_t k = sp < 64u ? sp : 64u;
+      const uint32_t base = sp - k;
+      const bool act = lane < k;
+      uint32_t node = 0, d = 0, fl = 0;
+      if (act) { const uint2 e = stack[base + lane]; node = e.x; d = e.y & kDepthMask; fl = e.y >> 28; }
+      sp = base;
+      wave_sync();
+      const StepOut o = probe_step<64>(a, g, act, node, d, fl, L, w, wreg);
+      const uint64_t m_hc = __ballot(o.hc != kNone), m_end = __ballot(o.at_end);
+      const uint32_t n_hc = (uint32_t)__popcll(m_hc), n_new_c = n_hc + (uint32_t)__popcll(m_end);
+      const uint64_t m_wc = __ballot(o.wc != kNone), m_pc = __ballot(o.pc != kNone);
+      const uint32_t n_pc = (uint32_t)__popcll(m_pc), n_new_s = n_pc + (uint32_t)__popcll(m_wc);
+      if (sp + n_new_s > scap) return false;
+      if (nc + n_new_c > kWCand) flush_cands();   // n_new_c <= 128 < kWCand
+      if (o.hc != kNone) W.cand[nc + prefix_bits(m_hc)] = o.hc;
+      if (o.at_end) W.cand[nc + n_hc + prefix_bits(m_end)] = node;
+      nc += n_new_c;
+      if (o.pc != kNone) stack[sp + prefix_bits(m_pc)] = make_uint2(o.pc, (d + 1) | (o.pf << 28));
+      if (o.wc != kNone) stack[sp + n_pc + prefix_bits(m_wc)] = make_uint2(o.wc, (d + 1) | (o.wf << 28));
+      sp += n_new_s;
+      wave_sync();
+    }
+    flush_cands();
+    if (mp_ok) {
+      const ExactSlot* e = find_exact<64>(a, pub, w, wreg, g);
+      if (e) {
+        const uint32_t nw = e->nwords;
+        rm |= e->rmask;
+        if (e->count != 0) {
+          if (nk + 1 > kWKeys) flush_keys();
+          if (lane == 0) W.keys[nk] = make_uint2(e->off, e->count);
+          nk += 1;
+        }
+        if (nw & kExactHigh) {   // {count, ids} after the MP and the words
+          const uint32_t* hl = a.exwords + e->words_off + 1 + L;
+          const uint32_t cnt = hl[0];
+          for (uint32_t j = lane; j < cnt; j += 64) {
+            const uint32_t n = hl[1 + j];
+            if (n < kMaxNodes) atomicOr(&W.hb[n >> 5], 1u << (n & 31));
+          }
+        }
+      }
+    }
+    wave_sync();
+    flush_keys();
+    // remote nodes in node order (fold_/5 :78-84): lane l owns nodes [64 l, 64 l + 64)
+    const uint64_t low = g.or64(rm);
+    wave_sync();
+    uint64_t word = ((uint64_t)W.hb[2 * lane + 1] << 32) | W.hb[2 * lane];
+    if (lane == 0) word |= low;
+    if (lane == (a.local_node >> 6)) word &= ~(1ull << (a.local_node & 63));
+    const uint32_t c = (uint32_t)__popcll(word);
+    const uint32_t incl = wave_incl_scan32(c);
+    if (MODE == 1) {
+      uint64_t pos = obase + run + incl - c;
+      while (word) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(word);
+        word &= word - 1;
+        const uint32_t node = lane * 64 + b;
+        if (OUT == 0) store_rec<NT>(a.out, pos, make_uint4((VMQG_EMIT_REMOTE << 24) | node, kNone, kNone, kNone));
+        else store_range(a.out_rng, pos, node, 0u);
+        pos++;
+      }
+    }
+    run += __shfl(incl, 63, 64);
+    wave_sync();
+    return true;
+  }
+};
 
-template <int GG, int U>
-static hipError_t launch_fused_g(const MatchArgs& a, uint32_t grid, bool nt, hipStream_t st) {
-  if (nt) k_match_fused<GG, true, U><<<grid, 256, 0, st>>>(a);
-  else k_match_fused<GG, false, U><<<grid, 256, 0, st>>>(a);
-  return hipGetLastError();
-}
-
-hipError_t launch_fused(const MatchArgs& a, uint32_t grid, uint32_t unroll, hipStream_t st) {
-  const bool nt = (a.opts & kOptNtStores) != 0;
-  if (grid < 1) grid = 1;
-  if (a.fast_g == 2) return unroll == 8 ? launch_fused_g<2, 8>(a, grid, nt, st) : launch_fused_g<2, 4>(a, grid, nt, st);
-  if (a.fast_g == 8) return unroll == 8 ? launch_fused_g<8, 8>(a, grid, nt, st) : launch_fused_g<8, 4>(a, grid, nt, st);
-  return unroll == 8 ? launch_fused_g<4, 8>(a, grid, nt, st) : launch_fused_g<4, 4>(a, grid, nt, st);
-}
-
-int fused_blocks_per_cu(uint32_t fast_g, uint32_t unroll) {
-  int n = 0;
-  const void* f;
-  if (fast_g == 2) f = unroll == 8 ? (const void*)k_match_fused<2, true, 8> : (const void*)k_match_fused<2, true, 4>;
-  else if (fast_g == 8) f = unroll == 8 ? (const void*)k_match_fused<8, true, 8> : (const void*)k_match_fused<8, true, 4>;
-  else f = unroll == 8 ? (const void*)k_match_fused<4, true, 8> : (const void*)k_match_fused<4, true, 4>;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) return 0;
-  return n;
+// Wave tiers: one publish per wave.  TIER 1 takes the fast tier's deferred
+// list with its stack in LDS; a stack overflow sends the publish to TIER 2
+// (stack in global scratch, o_cap entries per wave, sized from the trie
+// depth).  EMIT re-walks in the same order and checks the count.
+template <int MODE, int OUT, bool NT, int TIER>
+__global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
+  __shared__ WaveLds lds[kWaves];
+  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
+  uint2* stack = TIER == 1 ? lds[wv].stack : a.o_stack + gw * a.o_cap;
+  const uint32_t scap = TIER == 1 ? kWStack : a.o_cap;
+  const uint32_t* list = TIER == 1 ? a.deferred : a.deferred + a.npub;
+  const uint32_t n = a.status[TIER == 1 ? kStDeferred : kStTier2];   // written by earlier launches
+  const uint32_t nwaves = gridDim.x * kWaves;
+  for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
+    const uint32_t p = list[d];
+    if (MODE == 0) {
+      WaveWalk<0, OUT, NT> ww(a, lds[wv], stack, scap, 0);
+      if (ww.run_publish(p)) {
+        if (lane == 0) a.offsets[p] = ww.run;
+      } else if (lane == 0) {
+        if (TIER == 1) a.deferred[a.npub + atomicAdd(&a.status[kStTier2], 1u)] = p;
+        else atomicOr(&a.status[kStErr], kErrFrontier);
+      }
+    } else {
+      const uint64_t ob = a.offsets[p], oe = a.offsets[p + 1];
+      if (oe > (OUT ? a.rng_cap : a.out_cap)) {
+        if (lane == 0) atomicOr(&a.status[kStErr], kErrOverflow);
+      } else {
+        WaveWalk<1, OUT, NT> ww(a, lds[wv], stack, scap, ob);
+        if (ww.run_publish(p) && ww.run != oe - ob && lane == 0) atomicOr(&a.status[kStErr], kErrMismatch);
+      }
+    }
+    wave_sync();
+  }
 }
 
 // ------------------------------------------------------------------ scan
 // Exclusive scan of the per-publish counts in offsets[0, npub) into
 // offsets[0, npub] (offsets[npub] = total) in ONE launch: tiles of 4,096
-// taken by ticket, chained by the same decoupled look-back as the fused
-// kernel.  Slot npub is never read (no memset before the COUNT pass).
+// taken by ticket, chained by a decoupled look-back.  Slot npub is never
+// read (no memset before the COUNT pass).
 constexpr uint32_t kScanItems = 16, kScanBlock = 256, kScanTile = kScanItems * kScanBlock;
 
 __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
@@ -752,7 +846,7 @@ __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
   const uint32_t ntiles = (uint32_t)((n + kScanTile - 1) / kScanTile);
   uint64_t* v = a.offsets;
   for (;;) {
-    if (threadIdx.x == 0) s_tile = atomicAdd(&a.status[3], 1u);
+    if (threadIdx.x == 0) s_tile = atomicAdd(&a.status[kStTicket], 1u);
     __syncthreads();
     const uint32_t tile = s_tile;
     if (tile >= ntiles) break;
@@ -770,7 +864,7 @@ __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
       __syncthreads();
     }
     if (threadIdx.x < 64) {
-      const uint64_t b = lookback(a.lookback, a.lb_tag, a.status, tile, part[kScanBlock - 1]);
+      const uint64_t b = lookback(a.lookback, a.lb_tag, &a.status[kStErr], tile, part[kScanBlock - 1]);
       if (threadIdx.x == 0) s_base = b;
     }
     __syncthreads();
@@ -795,8 +889,19 @@ __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uin
   }
 }
 
+// Resets the per-call status counters (deferred lists, scan ticket); the
+// error word stays latched until vmqg_match_status reads it.
+__global__ void k_reset_status(uint32_t* status) {
+  if (threadIdx.x < 3) status[threadIdx.x] = 0;
+}
+
 // ---------------------------------------------------------------- launch
 static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+hipError_t launch_reset(uint32_t* status, hipStream_t st) {
+  k_reset_status<<<1, 64, 0, st>>>(status);
+  return hipGetLastError();
+}
 
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
   uint32_t g = scan_tiles(a.npub);
@@ -805,36 +910,52 @@ hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int MODE, int OUT>
+static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st) {
+  if (a.fast_g == 4) {
+    if (nt) k_match_fast<MODE, OUT, 4, true><<<g, 256, 0, st>>>(a);
+    else k_match_fast<MODE, OUT, 4, false><<<g, 256, 0, st>>>(a);
+  } else {
+    if (nt) k_match_fast<MODE, OUT, 2, true><<<g, 256, 0, st>>>(a);
+    else k_match_fast<MODE, OUT, 2, false><<<g, 256, 0, st>>>(a);
+  }
+}
+
+template <int MODE, int OUT, int TIER>
+static void launch_wave(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st) {
+  if (nt) k_match_wave<MODE, OUT, true, TIER><<<g, 256, 0, st>>>(a);
+  else k_match_wave<MODE, OUT, false, TIER><<<g, 256, 0, st>>>(a);
+}
+
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) {
   const bool nt = (a.opts & kOptNtStores) != 0;
+  const int out = a.out_rng ? 1 : 0;
   if (tier == 0) {
-    const uint32_t G = (a.fast_g == 2 || a.fast_g == 8) ? a.fast_g : 4;
+    const uint32_t G = a.fast_g == 4 ? 4 : 2;
     uint32_t g = div_up(a.npub, kWaves * (64 / G));
     const uint32_t cap = 256u * 8u;   // grid-stride beyond 8 blocks per CU
     if (g > cap) g = cap;
     if (g < 1) g = 1;
-#define VMQG_FAST(GG)                                                       \
-    if (mode == 0) k_match_fast<0, GG, false><<<g, 256, 0, st>>>(a);        \
-    else if (nt) k_match_fast<1, GG, true><<<g, 256, 0, st>>>(a);           \
-    else k_match_fast<1, GG, false><<<g, 256, 0, st>>>(a);
-    if (G == 2) { VMQG_FAST(2) }
-    else if (G == 4) { VMQG_FAST(4) }
-    else { VMQG_FAST(8) }
-#undef VMQG_FAST
+    if (mode == 0) { if (out) launch_fast<0, 1>(a, g, nt, st); else launch_fast<0, 0>(a, g, nt, st); }
+    else { if (out) launch_fast<1, 1>(a, g, nt, st); else launch_fast<1, 0>(a, g, nt, st); }
   } else {
     // reads its list length on the device (exits at once when empty); one
-    // wave per deferred publish, as many waves as have global scratch
-    const uint32_t g = a.o_waves / kWaves;
-    if (mode == 0) k_match_wave<0, false><<<g, 256, 0, st>>>(a);
-    else if (nt) k_match_wave<1, true><<<g, 256, 0, st>>>(a);
-    else k_match_wave<1, false><<<g, 256, 0, st>>>(a);
+    // wave per deferred publish
+    const uint32_t g = (tier == 1 ? a.w1_waves : a.o_waves) / kWaves;
+#define VMQG_WAVE(T)                                                              \
+    if (mode == 0) { if (out) launch_wave<0, 1, T>(a, g, nt, st); else launch_wave<0, 0, T>(a, g, nt, st); } \
+    else { if (out) launch_wave<1, 1, T>(a, g, nt, st); else launch_wave<1, 0, T>(a, g, nt, st); }
+    if (tier == 1) { VMQG_WAVE(1) } else { VMQG_WAVE(2) }
+#undef VMQG_WAVE
   }
   return hipGetLastError();
 }
 
 int wave_blocks_per_cu() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)k_match_wave<1, true>, 256, 0) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)k_match_wave<1, 0, true, 1>, 256, 0) !=
+      hipSuccess)
+    return 0;
   return n;
 }
 

@@ -1,5 +1,4 @@
-// Decoupled look-back shared by the one-launch scans and the fused match
-// kernel (vmqg_kernels.hip) and by the retained-store kernels
+// Decoupled look-back shared by the one-launch offset scan (vmqg_kernels.hip) and by the retained-store kernels
 // (vmqr_kernels.hip).  Each tile / chunk owns one 8-B granule
 // {tag:20, flag:2, value:42}; the granule is its own flag, written and read
 // with agent-scope relaxed atomics (cdna_hip_programming.md Guideline 16,
@@ -42,8 +41,10 @@ constexpr int kLbDepth = VMQG_LB_DEPTH;
 // kSleep: s_sleep between rounds that found a granule not yet posted —
 // longer for callers with many waves spinning at once (their loads slow the
 // waves still working).
+// `err`: the caller's error word (kErrLookback is OR-ed in when a round spins
+// past kSpinLimit).
 template <int kSleep = 1>
-__device__ inline uint64_t lookback(uint64_t* lb, uint32_t tag, uint32_t* status, uint32_t chunk, uint64_t agg) {
+__device__ inline uint64_t lookback(uint64_t* lb, uint32_t tag, uint32_t* err, uint32_t chunk, uint64_t agg) {
   const uint32_t lane = __lane_id();
   if (chunk == 0) {
     if (lane == 0) lb_store(lb, lb_pack(tag, kLbIncl, agg));
@@ -81,7 +82,7 @@ __device__ inline uint64_t lookback(uint64_t* lb, uint32_t tag, uint32_t* status
       if (stop < 64 || top - 64 * k - 63 <= 0) done = true;
     }
     if (retry) {
-      if (++spins > kSpinLimit) { if (lane == 0) atomicOr(&status[1], kErrLookback); break; }
+      if (++spins > kSpinLimit) { if (lane == 0) atomicOr(err, kErrLookback); break; }
       __builtin_amdgcn_s_sleep(kSleep);
       continue;   // the whole round again (its granules may have moved on)
     }

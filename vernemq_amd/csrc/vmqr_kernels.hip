@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void k_rt_scan(uint64_t* v, uint64_t n_host, c
       __syncthreads();
     }
     if (threadIdx.x < 64) {
-      const uint64_t b = vmqg::lookback(lb, tag, status, tile, part[kSB - 1]);
+      const uint64_t b = vmqg::lookback(lb, tag, status + 1, tile, part[kSB - 1]);
       if (threadIdx.x == 0) s_base = b;
     }
     __syncthreads();
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256) void k_rt_walk(RArgs a) {
 #ifdef VMQR_DIAG_SKIP_LOOKBACK   // A/B diagnostics only (tools/rt_ab.sh): wrong offsets
     const uint64_t pre = 0;
 #else
-    const uint64_t pre = vmqg::lookback<32>(a.lookback, a.lb_tag + 1, a.status, tile, nh);
+    const uint64_t pre = vmqg::lookback<32>(a.lookback, a.lb_tag + 1, a.status + 1, tile, nh);
 #endif
     const uint64_t total = pre + nh;
     if (total > a.out_cap) {

@@ -6,9 +6,10 @@ the tables and matches its own publish batches; the only collectives are
 
 * the device image broadcast when a replica starts or the primary re-lays
   its arena out (``ImageSync.full``),
-* the 24-B patch records of each delta batch (``ImageSync.delta``) —
-  rank 0 runs the host engine (``vmqg_apply_ops``), every rank applies the
-  same bytes, so all replicas stay byte-identical at each epoch,
+* the 24-B patch records of each delta batch (``ImageSync.delta``) plus the
+  256-B layout (its trie depth sizes the wave tier's stack) — rank 0 runs
+  the host engine (``vmqg_apply_ops``), every rank applies the same bytes, so
+  all replicas stay byte-identical at each epoch,
 * an all-gather of per-GPU counts (``gather_counts``).
 
 Nothing on the match data path is communicated.
@@ -25,25 +26,35 @@ def shard(n: int, rank: int, world: int):
     return n * rank // world, n * (rank + 1) // world
 
 
+def _comm_device(dist, device, group=None):
+    """Where collective buffers live: the GPU for nccl (RCCL over xGMI),
+    host memory for gloo (CPU tests, or a one-GPU rehearsal of N ranks)."""
+    import torch
+    if dist.get_backend(group) == "gloo":
+        return torch.device("cpu")
+    return device
+
+
 def _bcast_bytes(dist, data, src: int, device, group=None):
     """Broadcast a byte string (given on src) -> uint8 tensor on `device`."""
     import torch
-    n = torch.zeros(1, dtype=torch.int64, device=device)
+    cdev = _comm_device(dist, device, group)
+    n = torch.zeros(1, dtype=torch.int64, device=cdev)
     if dist.get_rank(group) == src:
         n[0] = len(data)
     dist.broadcast(n, src, group=group)
-    buf = torch.empty(int(n.item()), dtype=torch.uint8, device=device)
+    buf = torch.empty(int(n.item()), dtype=torch.uint8, device=cdev)
     if dist.get_rank(group) == src and len(data):
         buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
     if buf.numel():
         dist.broadcast(buf, src, group=group)
-    return buf
+    return buf.to(device)
 
 
 def gather_counts(dist, values, device, group=None):
     """All-gather a small int64 vector from every rank -> [world, k] array."""
     import torch
-    t = torch.as_tensor(np.asarray(values, dtype=np.int64), device=device)
+    t = torch.as_tensor(np.asarray(values, dtype=np.int64), device=_comm_device(dist, device, group))
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
     dist.all_gather(out, t, group=group)
     return np.stack([o.cpu().numpy() for o in out])
@@ -81,7 +92,8 @@ class ImageSync:
         else:
             ptr, nbytes, lay = 0, 0, b""
         lay_t = _bcast_bytes(d, lay, self.src, self.device, self.group)
-        n = torch.tensor([nbytes], dtype=torch.int64, device=self.device)
+        cdev = _comm_device(d, self.device, self.group)
+        n = torch.tensor([nbytes], dtype=torch.int64, device=cdev)
         d.broadcast(n, self.src, group=self.group)
         nbytes = int(n.item())
         img = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
@@ -92,7 +104,12 @@ class ImageSync:
                 img.copy_(torch.from_numpy(self.view.export_image()))
         if self._gpu():
             torch.cuda.synchronize(self.device)
-        d.broadcast(img, self.src, group=self.group)
+        if cdev.type == "cpu" and self._gpu():   # gloo rehearsal: stage through host memory
+            host = img.cpu()
+            d.broadcast(host, self.src, group=self.group)
+            img.copy_(host)
+        else:
+            d.broadcast(img, self.src, group=self.group)
         self.layout = bytes(lay_t.cpu().numpy())
         if not self.primary:
             if self._gpu():
@@ -107,21 +124,26 @@ class ImageSync:
         image when the batch re-laid the arena out)."""
         import torch
         d = self.dist
-        flag = torch.zeros(1, dtype=torch.int64, device=self.device)
-        data = b""
+        flag = torch.zeros(1, dtype=torch.int64, device=_comm_device(d, self.device, self.group))
+        data, lay = b"", b""
         if self.primary:
             data, full = self.view.last_patches()
             flag[0] = 1 if full else 0
+            lay = self.view.arena()[2]
         d.broadcast(flag, self.src, group=self.group)
         if int(flag.item()):
             self.full()
             return -1
+        lay_t = _bcast_bytes(d, lay, self.src, self.device, self.group)
         buf = _bcast_bytes(d, data, self.src, self.device, self.group)
-        if not self.primary and buf.numel():
+        if not self.primary:
+            self.layout = bytes(lay_t.cpu().numpy())
             if self._gpu():
-                self.view.apply_patches_device(buf.data_ptr(), buf.numel())
+                self.view.replica_sync_layout(self.layout)
+                if buf.numel():
+                    self.view.apply_patches_device(buf.data_ptr(), buf.numel())
                 torch.cuda.synchronize(self.device)
-            else:
+            elif buf.numel():
                 apply_patches_host(self.image, buf.numpy())
         return buf.numel() // 24
 

@@ -36,6 +36,7 @@ OP_DTYPE = np.dtype([(n, "<u4") for n in
                      ("kind", "mountpoint", "word_off", "nwords", "node", "subscriber", "subinfo", "reserved")])
 PUB_DTYPE = np.dtype([(n, "<u4") for n in ("mountpoint", "word_off", "nwords", "flags")])
 EMIT_DTYPE = np.dtype([(n, "<u4") for n in ("kind_node", "group", "subscriber", "subinfo")])
+RANGE_DTYPE = np.dtype([("off", "<u4"), ("count", "<u4")])
 
 
 def _subinfo_key(si):
@@ -220,6 +221,56 @@ class RegGpuView:
             _lib.check(rc, "vmqg_match_batch")
             return out[: n.value], offs
 
+    def match_ranges(self, pubs: np.ndarray, words: np.ndarray, out_cap: int | None = None):
+        """Range-mode match (vmqg_match_ranges) -> (RANGE_DTYPE entries,
+        uint64 offsets[n+1]).  count > 0: records [off, off + count) of
+        records(); count == 0: remote node `off`."""
+        pubs = np.ascontiguousarray(pubs, dtype=PUB_DTYPE)
+        words = np.ascontiguousarray(words, dtype=np.uint32)
+        offs = np.zeros(len(pubs) + 1, dtype=np.uint64)
+        cap = out_cap if out_cap is not None else max(1024, 2 * len(pubs))
+        while True:
+            out = np.zeros(cap, dtype=RANGE_DTYPE)
+            n = ctypes.c_size_t(0)
+            rc = self._L.vmqg_match_ranges(self._h, pubs.ctypes.data, len(pubs), words.ctypes.data, len(words),
+                                           out.ctypes.data, cap, ctypes.byref(n), offs.ctypes.data)
+            if rc == _lib.E_OVERFLOW and n.value > cap:
+                cap = int(n.value)
+                continue
+            _lib.check(rc, "vmqg_match_ranges")
+            return out[: n.value], offs
+
+    def records(self) -> np.ndarray:
+        """Host view (copy) of the record table that ranges index (vmqg_records)."""
+        p, n = ctypes.c_void_p(), ctypes.c_uint64()
+        _lib.check(self._L.vmqg_records(self._h, ctypes.byref(p), ctypes.byref(n)), "vmqg_records")
+        if not n.value:
+            return np.zeros(0, dtype=EMIT_DTYPE)
+        buf = (ctypes.c_uint8 * (n.value * 16)).from_address(p.value)
+        return np.frombuffer(buf, dtype=EMIT_DTYPE).copy()
+
+    def expand_ranges(self, rng: np.ndarray, offs: np.ndarray, recs: np.ndarray | None = None):
+        """Range entries -> (EMIT_DTYPE records, offsets): the FoldFun
+        arguments in the order the ranges give them (host-side expansion, as
+        the NIF does it)."""
+        recs = self.records() if recs is None else recs
+        cnt = rng["count"].astype(np.int64)
+        per = np.where(cnt > 0, cnt, 1)
+        starts = np.concatenate([[0], np.cumsum(per)])
+        out = np.zeros(int(starts[-1]), dtype=EMIT_DTYPE)
+        idx = np.repeat(rng["off"].astype(np.int64), per) + (np.arange(int(starts[-1])) - np.repeat(starts[:-1], per))
+        isrec = np.repeat(cnt > 0, per)
+        out[isrec] = recs[idx[isrec]]
+        rem = out[~isrec]
+        rem["kind_node"] = (_lib.EMIT_REMOTE << 24) | np.repeat(rng["off"], per)[~isrec]
+        rem["group"] = rem["subscriber"] = rem["subinfo"] = _lib.NONE
+        out[~isrec] = rem
+        n_ent = np.diff(offs.astype(np.int64))
+        sums = np.zeros(len(n_ent), dtype=np.int64)
+        np.add.at(sums, np.repeat(np.arange(len(n_ent)), n_ent), per)
+        eoffs = np.concatenate([[0], np.cumsum(sums)])
+        return out, eoffs.astype(np.uint64)
+
     def decode(self, rec) -> object:
         """One 16-B record -> the FoldFun entry term."""
         kind, node = int(rec["kind_node"]) >> 24, int(rec["kind_node"]) & 0xFFFFFF
@@ -252,7 +303,7 @@ class RegGpuView:
         return self._L.vmqg_match_status(self._h, stream or None)
 
     def set_option(self, name: str, value: int):
-        """Kernel tuning knob (vmqg_set_option): "fast_g" 2|4|8, "nt_stores" 0|1, "fused" 0|1, "unroll" 4|8."""
+        """Kernel tuning knob (vmqg_set_option): "fast_g" 2|4, "nt_stores" 0|1."""
         _lib.check(self._L.vmqg_set_option(self._h, name.encode(), int(value)), "vmqg_set_option")
 
     def set_timing(self, on: bool):
@@ -288,6 +339,15 @@ class RegGpuView:
                    "vmqg_last_patches")
         data = ctypes.string_at(p.value, b.value) if b.value else b""
         return data, bool(full.value)
+
+    def replica_sync_layout(self, layout: bytes):
+        lay = (ctypes.c_uint8 * _lib.LAYOUT_BYTES).from_buffer_copy(layout)
+        _lib.check(self._L.vmqg_replica_sync_layout(self._h, lay), "vmqg_replica_sync_layout")
+
+    def match_ranges_device(self, d_pubs: int, npub: int, d_words: int, d_out: int, out_cap: int, d_offsets: int,
+                            stream: int = 0):
+        _lib.check(self._L.vmqg_match_ranges_device(self._h, d_pubs, npub, d_words, d_out, out_cap, d_offsets,
+                                                    stream or None), "vmqg_match_ranges_device")
 
     def apply_patches_device(self, d_patches: int, nbytes: int, stream: int = 0):
         _lib.check(self._L.vmqg_apply_patches_device(self._h, d_patches, nbytes, stream or None),
