@@ -7,7 +7,9 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/prof}
 mkdir -p $OUT
-B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}"
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-}"
+export BUILD_ID=$(python3 -c "from vernemq_amd import _lib; print(_lib.build_id())")
+echo "build $BUILD_ID"
 echo "== kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- $B > $OUT/stats.log 2>&1 || { tail -20 $OUT/stats.log; exit 3; }
 tail -2 $OUT/stats.log
