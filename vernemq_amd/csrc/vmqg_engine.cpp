@@ -854,7 +854,7 @@ int Engine::upload() {
 }
 
 int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
-  if (npub > keycache_cap || 2 * npub > deferred_cap) {
+  if (npub > keycache_cap || npub > deferred_cap) {
     if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
     hipFree(d_keycache);
     hipFree(d_deferred);
@@ -862,9 +862,9 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     keycache_cap = deferred_cap = 0;
     const uint64_t cap = next_pow2(std::max<uint64_t>(npub, 1024));
     if (hipMalloc(&d_keycache, cap * 32) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_deferred, 2 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_deferred, cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
     keycache_cap = cap;
-    deferred_cap = 2 * cap;
+    deferred_cap = cap;
   }
   return VMQG_OK;
 }
@@ -886,18 +886,18 @@ int Engine::ensure_lookback(uint64_t granules, hipStream_t st) {
   return VMQG_OK;
 }
 
-// Wave tiers: tier 1 fills the chip from LDS; tier 2 has a global stack of
-// o_cap entries per wave.  A wave pops <= 64 entries and pushes <= 2 per
-// entry, one depth further, so its stack holds < 64 entries per trie level
-// plus one step's pushes: 64 (depth + 4) entries cannot overflow.
+// Wave tier: each wave has an LDS stack and a global one of o_cap entries.
+// A wave pops <= 64 entries and pushes <= 2 per entry, one depth further, so
+// its stack holds < 64 entries per trie level plus one step's pushes:
+// 64 (depth + 4) entries cannot overflow.
 int Engine::ensure_wave_scratch(hipStream_t st) {
-  if (w1_waves == 0) w1_waves = (uint32_t)std::max(1, wave_blocks_per_cu()) * (uint32_t)cu_count * 4;
   const uint64_t need = std::max<uint64_t>({1024, 64ull * (stack_depth() + 4), o_cap_floor});
   if (need > (1ull << 31)) return VMQG_E_LIMIT;
   if (o_cap >= need && d_ostack) return VMQG_OK;
-  // at most 256 MiB of stacks, at least 64 waves
+  // two 256-thread blocks per CU (8 waves) when the stacks fit 256 MiB, at
+  // least 64 waves for deep tries
   uint64_t waves = (256ull << 20) / (need * sizeof(uint2));
-  waves = std::max<uint64_t>(64, std::min<uint64_t>(1024, waves)) & ~3ull;
+  waves = std::max<uint64_t>(64, std::min<uint64_t>(8ull * (uint64_t)cu_count, waves)) & ~3ull;
   if (d_ostack) { hipStreamSynchronize(st); hipFree(d_ostack); }
   d_ostack = nullptr; o_waves = 0; o_cap = 0;
   if (hipMalloc(&d_ostack, waves * need * sizeof(uint2)) != hipSuccess) return VMQG_E_NOMEM;
@@ -924,10 +924,12 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.pubs = pubs; a.words = words; a.npub = npub;
   a.offsets = offs;
   a.keycache = d_keycache;
-  a.status = d_status; a.deferred = d_deferred;
+  a.status = d_status + 4 * (call_seq & 1);
+  a.status_next = d_status + 4 * ((call_seq + 1) & 1);
+  a.err = d_status + 8;
+  a.deferred = d_deferred;
   a.fast_g = opt_fast_g; a.opts = opt_flags;
   a.lookback = d_lookback; a.lb_tag = lb_tag;
-  a.w1_waves = w1_waves;
   a.o_stack = d_ostack; a.o_cap = o_cap; a.o_waves = o_waves;
   return a;
 }
@@ -949,40 +951,43 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   MatchArgs a = args_for(d_pubs_, npub, d_words_, d_offsets);
   a.out = d_out_; a.out_cap = out_cap;
   a.out_rng = d_rng; a.rng_cap = rng_cap;
-  if (launch_reset(d_status, st) != hipSuccess) return VMQG_E_DEVICE;
+  last_set = call_seq & 1;
+  call_seq++;
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
   if (timing) {
     hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2); hipEventCreate(&e3);
     hipEventRecord(e0, st);
   }
-  // COUNT: fast groups, then the wave tiers for what they deferred
+  // COUNT: fast groups, then the wave tier for what they deferred
   if (launch_match(a, 0, 0, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) hipEventRecord(e1, st);
-  if (launch_match(a, 0, 1, st) != hipSuccess || launch_match(a, 0, 2, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 0, 1, st) != hipSuccess) return VMQG_E_DEVICE;
   if (launch_scan(a, st) != hipSuccess) return VMQG_E_DEVICE;
   // EMIT: same tiers
   if (timing) hipEventRecord(e2, st);
   if (launch_match(a, 1, 0, st) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) { hipEventRecord(e3, st); t_count.push_back({e0, e1}); t_emit.push_back({e2, e3}); }
-  if (launch_match(a, 1, 1, st) != hipSuccess || launch_match(a, 1, 2, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
 
-// Status words: [0] tier-1 publishes, [1] tier-2 publishes of the last call,
-// [3] error bits latched since the previous vmqg_match_status.
+// Status words: two sets of per-call counters ([0] deferred publishes, [1]
+// of those walked with a global stack, [2] scan ticket) used by alternate
+// calls, and at [8] the error bits latched since the previous
+// vmqg_match_status.
 int Engine::match_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
   if (!st) st = stream;
-  uint32_t h[4] = {0, 0, 0, 0};
-  if (hipMemcpyAsync(h, d_status, 16, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
+  uint32_t h[12] = {0};
+  if (hipMemcpyAsync(h, d_status, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
-  if (hipMemsetAsync(d_status, 0, 16, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipMemsetAsync(d_status + 8, 0, 4, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
-  last_deferred[0] = h[0];
-  last_deferred[1] = h[1];
-  const uint32_t err = h[3];
+  last_deferred[0] = h[4 * last_set];
+  last_deferred[1] = h[4 * last_set + 1];
+  const uint32_t err = h[8];
   if (err & 2u) return VMQG_E_FRONTIER;
   if (err & 4u) return VMQG_E_OVERFLOW;
   if (err & (8u | 16u)) return VMQG_E_DEVICE;   // count mismatch, look-back timeout

@@ -167,7 +167,8 @@ struct Engine {
   Stage stage[kStage];
   int stage_next = 0;
   uint32_t* d_status = nullptr;
-  uint32_t* d_deferred = nullptr; uint64_t deferred_cap = 0;   // 2 x publishes
+  uint32_t* d_deferred = nullptr; uint64_t deferred_cap = 0;   // publishes
+  uint64_t call_seq = 0; uint32_t last_set = 0;                // status set of the next / last match call
   void* d_keycache = nullptr; uint64_t keycache_cap = 0;   // publishes
   // host-buffer match staging
   void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
@@ -180,7 +181,7 @@ struct Engine {
   // look-back granules (tagged per call), global stack of the tier-2 wave path
   uint64_t* d_lookback = nullptr; uint64_t lookback_cap = 0; uint32_t lb_tag = 0;
   uint2* d_ostack = nullptr; uint64_t ostack_bytes = 0;
-  uint32_t o_cap = 0, o_waves = 0, w1_waves = 0;
+  uint32_t o_cap = 0, o_waves = 0;
   uint64_t o_cap_floor = 0;         // raised by vmqg_match_batch if a tier-2 stack ever overflowed
   int cu_count = 0;
   uint32_t last_deferred[2] = {0, 0};   // tier-1 / tier-2 publishes of the last checked batch

@@ -21,27 +21,25 @@ struct MatchArgs {
   void* keycache;                                 // npub x 32 B (COUNT -> EMIT)
   Record* out; uint64_t out_cap;                  // records mode
   vmqg_range* out_rng; uint64_t rng_cap;          // range mode (out_rng != null)
-  uint32_t* status;                               // [0] tier-1 list length, [1] tier-2 list length,
-                                                  // [2] scan tile ticket, [3] error bits (sticky)
-  uint32_t* deferred;                             // 2 x npub: the tier-1 list, then the tier-2 list
+  uint32_t* status;                               // this call's counters: [0] deferred publishes,
+                                                  // [1] of those, walked with a global stack, [2] scan ticket
+  uint32_t* status_next;                          // the next call's counters (zeroed by this call)
+  uint32_t* err;                                  // error bits, sticky until vmqg_match_status
+  uint32_t* deferred;                             // npub: publishes the fast tier hands to the wave tier
   uint32_t fast_g, opts;                          // tuning: lanes per publish (2|4), kOpt* bits
   uint64_t* lookback;                             // per scan tile: {tag, flag, value} granule
-  uint32_t lb_tag, w1_waves;                      // this call's granule tag (never 0); tier-1 grid waves
-  uint2* o_stack;                                 // tier 2: global frontier stack, o_cap entries per wave
+  uint32_t lb_tag, pad1;                          // this call's granule tag (never 0)
+  uint2* o_stack;                                 // wave tier: global frontier stacks, o_cap entries per wave
   uint32_t o_cap, o_waves;
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
 
-// mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier with an LDS
-// stack (grid a.w1_waves / 4), 2 = wave tier with a global stack (a.o_waves / 4)
+// mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier (grid a.o_waves / 4)
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st);
 // counts in offsets[0, npub) -> exclusive offsets[0, npub] (one launch, look-back)
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st);
 uint32_t scan_tiles(uint64_t npub);
-int wave_blocks_per_cu();
-// zero the per-call status counters (the error word stays latched)
-hipError_t launch_reset(uint32_t* status, hipStream_t st);
 hipError_t launch_patches(uint8_t* arena, const void* d_patches, uint64_t n, hipStream_t st);
 
 }  // namespace vmqg

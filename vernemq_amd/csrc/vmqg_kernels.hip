@@ -50,9 +50,11 @@ template <int G> struct FastCaps { static constexpr uint32_t S = 8 * G, C = 4 * 
 constexpr uint32_t kRewalk = 0xFFFFFFFFu;   // key cache: EMIT must re-walk
 constexpr uint32_t kDeferred = 0xFFFFFFFEu; // key cache: the wave tier owns the publish
 
-// status words (d_status): per-call counters are reset by the host before
-// each match call, the error word only by vmqg_match_status (sticky).
-enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStErr = 3 };
+// Per-call status counters (a.status; two sets used by alternate calls: each
+// call's first kernel zeroes the set of the call after it, so no reset
+// launch is needed) and the sticky error word (a.err, cleared only by
+// vmqg_match_status).
+enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2 };
 enum : uint32_t { kErrFrontier = 2u, kErrOverflow = 4u, kErrMismatch = 8u };   // kErrLookback = 16 (lookback.h)
 
 __device__ __forceinline__ uint32_t prefix_bits(uint64_t m) {
@@ -481,8 +483,8 @@ __device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s,
     wave_sync();
   }
   const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
-  if (oend > cap) { if (g.lane == 0) atomicOr(&a.status[kStErr], kErrOverflow); return false; }
-  if (oend - obase != total) { if (g.lane == 0) atomicOr(&a.status[kStErr], kErrMismatch); return false; }
+  if (oend > cap) { if (g.lane == 0) atomicOr(a.err, kErrOverflow); return false; }
+  if (oend - obase != total) { if (g.lane == 0) atomicOr(a.err, kErrMismatch); return false; }
   return true;
 }
 
@@ -568,6 +570,7 @@ template <int MODE, int OUT, int G, bool NT>
 __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
   using FS = FastScratch<G>;
   constexpr int GPW = FS::GPW;
+  if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < 3) a.status_next[threadIdx.x] = 0;
   __shared__ uint2 st[FS::SC * FS::SLOTS];
   __shared__ uint32_t cd[FS::CC * FS::SLOTS];
   __shared__ uint2 ky[FS::KC * FS::SLOTS];
@@ -794,38 +797,43 @@ struct WaveWalk {
   }
 };
 
-// Wave tiers: one publish per wave.  TIER 1 takes the fast tier's deferred
-// list with its stack in LDS; a stack overflow sends the publish to TIER 2
-// (stack in global scratch, o_cap entries per wave, sized from the trie
-// depth).  EMIT re-walks in the same order and checks the count.
-template <int MODE, int OUT, bool NT, int TIER>
+// Wave tier: one publish per wave, from the fast tier's deferred list.  The
+// frontier stack is in LDS; a publish that outgrows it is walked again with
+// the wave's stack in global scratch (o_cap entries, sized from the trie
+// depth so it cannot overflow).  EMIT re-walks in the same order and checks
+// the count.
+template <int MODE, int OUT, bool NT>
 __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
   __shared__ WaveLds lds[kWaves];
   const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
-  uint2* stack = TIER == 1 ? lds[wv].stack : a.o_stack + gw * a.o_cap;
-  const uint32_t scap = TIER == 1 ? kWStack : a.o_cap;
-  const uint32_t* list = TIER == 1 ? a.deferred : a.deferred + a.npub;
-  const uint32_t n = a.status[TIER == 1 ? kStDeferred : kStTier2];   // written by earlier launches
+  uint2* gstack = a.o_stack + gw * a.o_cap;
+  const uint32_t n = a.status[kStDeferred];   // written by the fast tier's launch
   const uint32_t nwaves = gridDim.x * kWaves;
   for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
-    const uint32_t p = list[d];
-    if (MODE == 0) {
-      WaveWalk<0, OUT, NT> ww(a, lds[wv], stack, scap, 0);
-      if (ww.run_publish(p)) {
-        if (lane == 0) a.offsets[p] = ww.run;
-      } else if (lane == 0) {
-        if (TIER == 1) a.deferred[a.npub + atomicAdd(&a.status[kStTier2], 1u)] = p;
-        else atomicOr(&a.status[kStErr], kErrFrontier);
-      }
-    } else {
-      const uint64_t ob = a.offsets[p], oe = a.offsets[p + 1];
+    const uint32_t p = a.deferred[d];
+    uint64_t ob = 0, oe = 0;
+    if (MODE == 1) {
+      ob = a.offsets[p];
+      oe = a.offsets[p + 1];
       if (oe > (OUT ? a.rng_cap : a.out_cap)) {
-        if (lane == 0) atomicOr(&a.status[kStErr], kErrOverflow);
-      } else {
-        WaveWalk<1, OUT, NT> ww(a, lds[wv], stack, scap, ob);
-        if (ww.run_publish(p) && ww.run != oe - ob && lane == 0) atomicOr(&a.status[kStErr], kErrMismatch);
+        if (lane == 0) atomicOr(a.err, kErrOverflow);
+        continue;
       }
+    }
+    WaveWalk<MODE, OUT, NT> w1(a, lds[wv], lds[wv].stack, kWStack, ob);
+    bool ok = w1.run_publish(p);
+    uint64_t total = w1.run;
+    if (!ok) {
+      if (MODE == 0 && lane == 0) atomicAdd(&a.status[kStTier2], 1u);
+      WaveWalk<MODE, OUT, NT> w2(a, lds[wv], gstack, a.o_cap, ob);
+      ok = w2.run_publish(p);
+      total = w2.run;
+      if (!ok && lane == 0) atomicOr(a.err, kErrFrontier);
+    }
+    if (ok && lane == 0) {
+      if (MODE == 0) a.offsets[p] = total;
+      else if (total != oe - ob) atomicOr(a.err, kErrMismatch);
     }
     wave_sync();
   }
@@ -864,7 +872,7 @@ __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
       __syncthreads();
     }
     if (threadIdx.x < 64) {
-      const uint64_t b = lookback(a.lookback, a.lb_tag, &a.status[kStErr], tile, part[kScanBlock - 1]);
+      const uint64_t b = lookback(a.lookback, a.lb_tag, a.err, tile, part[kScanBlock - 1]);
       if (threadIdx.x == 0) s_base = b;
     }
     __syncthreads();
@@ -889,19 +897,8 @@ __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uin
   }
 }
 
-// Resets the per-call status counters (deferred lists, scan ticket); the
-// error word stays latched until vmqg_match_status reads it.
-__global__ void k_reset_status(uint32_t* status) {
-  if (threadIdx.x < 3) status[threadIdx.x] = 0;
-}
-
 // ---------------------------------------------------------------- launch
 static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
-
-hipError_t launch_reset(uint32_t* status, hipStream_t st) {
-  k_reset_status<<<1, 64, 0, st>>>(status);
-  return hipGetLastError();
-}
 
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
   uint32_t g = scan_tiles(a.npub);
@@ -921,10 +918,10 @@ static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st)
   }
 }
 
-template <int MODE, int OUT, int TIER>
+template <int MODE, int OUT>
 static void launch_wave(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st) {
-  if (nt) k_match_wave<MODE, OUT, true, TIER><<<g, 256, 0, st>>>(a);
-  else k_match_wave<MODE, OUT, false, TIER><<<g, 256, 0, st>>>(a);
+  if (nt) k_match_wave<MODE, OUT, true><<<g, 256, 0, st>>>(a);
+  else k_match_wave<MODE, OUT, false><<<g, 256, 0, st>>>(a);
 }
 
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) {
@@ -940,24 +937,14 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) 
     else { if (out) launch_fast<1, 1>(a, g, nt, st); else launch_fast<1, 0>(a, g, nt, st); }
   } else {
     // reads its list length on the device (exits at once when empty); one
-    // wave per deferred publish
-    const uint32_t g = (tier == 1 ? a.w1_waves : a.o_waves) / kWaves;
-#define VMQG_WAVE(T)                                                              \
-    if (mode == 0) { if (out) launch_wave<0, 1, T>(a, g, nt, st); else launch_wave<0, 0, T>(a, g, nt, st); } \
-    else { if (out) launch_wave<1, 1, T>(a, g, nt, st); else launch_wave<1, 0, T>(a, g, nt, st); }
-    if (tier == 1) { VMQG_WAVE(1) } else { VMQG_WAVE(2) }
-#undef VMQG_WAVE
+    // wave per deferred publish, each wave with its own global stack
+    const uint32_t g = a.o_waves / kWaves;
+    if (mode == 0) { if (out) launch_wave<0, 1>(a, g, nt, st); else launch_wave<0, 0>(a, g, nt, st); }
+    else { if (out) launch_wave<1, 1>(a, g, nt, st); else launch_wave<1, 0>(a, g, nt, st); }
   }
   return hipGetLastError();
 }
 
-int wave_blocks_per_cu() {
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)k_match_wave<1, 0, true, 1>, 256, 0) !=
-      hipSuccess)
-    return 0;
-  return n;
-}
 
 hipError_t launch_patches(uint8_t* arena, const void* d_patches, uint64_t n, hipStream_t st) {
   if (n == 0) return hipSuccess;
