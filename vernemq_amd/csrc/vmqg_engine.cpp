@@ -122,6 +122,32 @@ static uint64_t topic_hash(uint32_t mp, const uint32_t* w, uint32_t L) {
   return h;
 }
 
+// The (MP, Topic) term of an op: the $share prefix is not part of it.
+static inline void op_topic(const vmqg_op& op, const uint32_t*& w, uint32_t& L) {
+  L = op.nwords;
+  if (L >= 3 && w[0] == kShare) { w += 2; L -= 2; }
+}
+
+// apply_ops keeps the lookups of later ops in flight while it handles the
+// current one: stage 0 (8 ops ahead) prefetches the topic's index slot,
+// stage 1 (4 ahead) the topic record it names, stage 2 (2 ahead) the
+// topic's words and its local key.  The handlers then find them in cache.
+void Engine::prefetch_op(const vmqg_op& op, const uint32_t* w, int stage) {
+  uint32_t L;
+  op_topic(op, w, L);
+  const uint64_t h = topic_hash(op.mountpoint, w, L);
+  if (stage == 0) { topic_index.prefetch(h); return; }
+  const uint32_t t = topic_index.find(h);   // unverified: a prefetch hint only
+  if (t == FlatIndex::kVoid || t >= topics.size()) return;
+  const TopicInfo& T = topics[t];
+  if (stage == 1) { __builtin_prefetch(&T); return; }
+  __builtin_prefetch(T.words.data());
+  if (T.local_key != kNone) {
+    __builtin_prefetch(&keys[T.local_key]);
+    if (!keys[T.local_key].vals.empty()) __builtin_prefetch(keys[T.local_key].vals.data());
+  }
+}
+
 uint32_t Engine::topic_id(uint32_t mp, const uint32_t* w, uint32_t L, bool create) {
   const uint64_t h = topic_hash(mp, w, L);
   const uint32_t found = topic_index.find(h, [&](uint32_t id) {
@@ -366,7 +392,9 @@ bool Engine::write_path(uint32_t p) {
   if (P.rec && P.topic_set) flags |= kNodeTopic;
   if (P.filter) flags |= kNodeFilter;
   if (P.dollar_skip) flags |= kNodeDollarSkip;
-  std::vector<uint32_t> ks, high;
+  std::vector<uint32_t> ks;
+  std::vector<uint32_t>& high = scratch_u32;
+  high.clear();
   uint64_t rmask = 0;
   if (P.filter) {
     // match_/3 (:301-303): one candidate per node-list entry; a key that does
@@ -464,12 +492,13 @@ bool Engine::write_topic(uint32_t ti) {
     return true;
   }
   uint64_t rmask = 0;
-  std::vector<uint32_t> high;
+  std::vector<uint32_t>& high = scratch_u32;
+  high.clear();
   for (auto& r : t.remote) {
     if (r.first < kLowNodes) rmask |= 1ull << r.first;
     else high.push_back(r.first);
   }
-  std::sort(high.begin(), high.end());
+  if (high.size() > 1) std::sort(high.begin(), high.end());
   const uint32_t L = (uint32_t)t.words.size();
   const uint32_t need = 1 + L + (high.empty() ? 0 : 1 + (uint32_t)high.size());
   if (t.slot == ~0ull && (exact_live + exact_tomb + 1) * 10 > lay.exact_buckets * kExactSlotsPerBucket * 7)
@@ -524,6 +553,12 @@ bool Engine::write_topic(uint32_t ti) {
 bool Engine::flush_incremental() {
   // keys first (record ranges), then the paths and exact slots that inline them
   for (size_t i = 0; i < dirty_keys.size(); i++) {
+    if (i + 4 < dirty_keys.size()) __builtin_prefetch(&keys[dirty_keys[i + 4]]);
+    if (i + 2 < dirty_keys.size()) {
+      const KeyInfo& K = keys[dirty_keys[i + 2]];
+      __builtin_prefetch(&topics[K.topic_id]);
+      __builtin_prefetch(region<KeyDesc>(lay.keydesc_off) + dirty_keys[i + 2]);
+    }
     const uint32_t k = dirty_keys[i];
     if (!write_key(k)) return false;
     const TopicInfo& t = topics[keys[k].topic_id];
@@ -531,7 +566,16 @@ bool Engine::flush_incremental() {
     if (keys[k].group == kNone) mark_topic(keys[k].topic_id);
   }
   for (size_t i = 0; i < dirty_paths.size(); i++) if (!write_path(dirty_paths[i])) return false;
-  for (size_t i = 0; i < dirty_topics.size(); i++) if (!write_topic(dirty_topics[i])) return false;
+  const ExactSlot* tab = region<ExactSlot>(lay.exact_off);
+  for (size_t i = 0; i < dirty_topics.size(); i++) {
+    if (i + 4 < dirty_topics.size()) __builtin_prefetch(&topics[dirty_topics[i + 4]]);
+    if (i + 2 < dirty_topics.size()) {
+      const TopicInfo& T = topics[dirty_topics[i + 2]];
+      if (T.slot != ~0ull) __builtin_prefetch(&tab[T.slot]);
+      if (T.local_key != kNone) __builtin_prefetch(&keys[T.local_key]);
+    }
+    if (!write_topic(dirty_topics[i])) return false;
+  }
   return true;
 }
 
@@ -755,6 +799,9 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
   // the edge table must absorb every edge this batch could add
   if ((edge_live + edge_tomb + add_words) * 10 > lay.edge_buckets * kEdgeSlotsPerBucket * 7) rebuild(add_words);
   for (size_t i = 0; i < n; i++) {
+    if (i + 8 < n) prefetch_op(ops[i + 8], words + ops[i + 8].word_off, 0);
+    if (i + 4 < n) prefetch_op(ops[i + 4], words + ops[i + 4].word_off, 1);
+    if (i + 2 < n) prefetch_op(ops[i + 2], words + ops[i + 2].word_off, 2);
     const uint32_t* w = words + ops[i].word_off;
     if (ops[i].kind == VMQG_OP_ADD) handle_add(ops[i], w);
     else handle_delete(ops[i], w);
@@ -862,7 +909,7 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     keycache_cap = deferred_cap = 0;
     const uint64_t cap = next_pow2(std::max<uint64_t>(npub, 1024));
     if (hipMalloc(&d_keycache, cap * 32) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_deferred, cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_deferred, 2 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
     keycache_cap = cap;
     deferred_cap = cap;
   }

@@ -6,8 +6,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+
 #include <algorithm>
+#include <cstdlib>
 #include <memory>
+#include <new>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -16,6 +20,36 @@
 #include "vmqg_kernels.h"
 
 namespace vmqg {
+
+// Allocator for the engine's big tables (the arena mirror, the indexes, the
+// path / key / topic arrays): blocks of >= 4 MiB are 2-MiB aligned and
+// advised to transparent huge pages, so the random lookups of a delta batch
+// do not pay a page walk each.
+template <class T>
+struct HugeAlloc {
+  using value_type = T;
+  HugeAlloc() = default;
+  template <class U> HugeAlloc(const HugeAlloc<U>&) {}
+  T* allocate(size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes < (4u << 20)) {
+      void* p = ::operator new(bytes);
+      return static_cast<T*>(p);
+    }
+    const size_t huge = 2u << 20, rounded = (bytes + huge - 1) & ~(huge - 1);
+    void* p = std::aligned_alloc(huge, rounded);
+    if (!p) throw std::bad_alloc();
+    madvise(p, rounded, MADV_HUGEPAGE);
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t n) {
+    if (n * sizeof(T) < (4u << 20)) ::operator delete(p);
+    else std::free(p);
+  }
+  template <class U> bool operator==(const HugeAlloc<U>&) const { return true; }
+  template <class U> bool operator!=(const HugeAlloc<U>&) const { return false; }
+};
+template <class T> using HugeVec = std::vector<T, HugeAlloc<T>>;
 
 // NodeOrGroup of a vmq_trie_topic node list: Node | {Node, Group}
 struct Nog {
@@ -43,6 +77,10 @@ class FlatIndex {
     }
   }
   uint32_t find(uint64_t key) const { return find(key, [](uint32_t) { return true; }); }
+  // software prefetch of the slot `key` hashes to
+  void prefetch(uint64_t key) const {
+    if (!slots_.empty()) __builtin_prefetch(&slots_[mix64(key) & (slots_.size() - 1)]);
+  }
   void insert(uint64_t key, uint32_t val) {
     if ((n_ + 1) * 2 > slots_.size()) regrow(std::max<uint64_t>(1024, slots_.size() * 2));
     put(key, val);
@@ -61,12 +99,12 @@ class FlatIndex {
   void regrow(uint64_t want) {
     uint64_t cap = 1;
     while (cap < want) cap <<= 1;
-    std::vector<Slot> old;
+    HugeVec<Slot> old;
     old.swap(slots_);
     slots_.assign(cap, Slot{0, kVoid});
     for (const Slot& s : old) if (s.val != kVoid) put(s.key, s.val);
   }
-  std::vector<Slot> slots_;
+  HugeVec<Slot> slots_;
   uint64_t n_ = 0;
 };
 
@@ -131,18 +169,18 @@ struct Engine {
   std::vector<std::string> word_text;
 
   // ---- logical state
-  std::vector<PathInfo> paths;                              // ids [0, max_mp) are roots
+  HugeVec<PathInfo> paths;                              // ids [0, max_mp) are roots
   FlatIndex path_index;                                     // parent<<32|word -> path
-  std::vector<KeyInfo> keys;
+  HugeVec<KeyInfo> keys;
   FlatIndex group_key_index;                                // topic<<32|group -> key
-  std::vector<TopicInfo> topics;
+  HugeVec<TopicInfo> topics;
   FlatIndex topic_index;                                    // hash(mp, words) -> topic (verified)
   uint64_t n_trie_nodes = 0, n_trie_topics = 0, n_subs_objects = 0, n_fanout = 0, n_remote_keys = 0;
 
   // ---- mirror of the device arena
   Layout lay{};
-  std::vector<uint64_t> mirror;     // lay.total_bytes / 8 words
-  std::vector<uint64_t> dirty_bits; // one bit per 16-B chunk
+  HugeVec<uint64_t> mirror;         // lay.total_bytes / 8 words
+  HugeVec<uint64_t> dirty_bits;     // one bit per 16-B chunk
   std::vector<uint64_t> dirty_chunks;
   std::vector<uint32_t> dirty_paths, dirty_keys, dirty_topics;
   uint64_t edge_live = 0, edge_tomb = 0, exact_live = 0, exact_tomb = 0;
@@ -210,6 +248,8 @@ struct Engine {
   uint32_t path_child(uint32_t parent, uint32_t word, bool create);
   bool path_chain(uint32_t mp, const uint32_t* w, uint32_t L, bool create, std::vector<uint32_t>& chain);
   uint32_t topic_id(uint32_t mp, const uint32_t* w, uint32_t L, bool create);
+  void prefetch_op(const vmqg_op& op, const uint32_t* w, int stage);   // apply_ops software pipeline
+  std::vector<uint32_t> scratch_u32;                                 // write_path / write_topic lists
   uint32_t local_key(uint32_t tid, bool create);
   uint32_t group_key(uint32_t tid, uint32_t group, bool create);
   void mark_path(uint32_t p) { if (!paths[p].dirty) { paths[p].dirty = 1; dirty_paths.push_back(p); } }

@@ -22,10 +22,11 @@ struct MatchArgs {
   Record* out; uint64_t out_cap;                  // records mode
   vmqg_range* out_rng; uint64_t rng_cap;          // range mode (out_rng != null)
   uint32_t* status;                               // this call's counters: [0] deferred publishes,
-                                                  // [1] of those, walked with a global stack, [2] scan ticket
+                                                  // [1] of those, walked with a global stack, [2] scan ticket,
+                                                  // [3] publishes the records EMIT hands to the wave tier
   uint32_t* status_next;                          // the next call's counters (zeroed by this call)
   uint32_t* err;                                  // error bits, sticky until vmqg_match_status
-  uint32_t* deferred;                             // npub: publishes the fast tier hands to the wave tier
+  uint32_t* deferred;                             // 2 x npub: publishes deferred by COUNT, then by EMIT
   uint32_t fast_g, opts;                          // tuning: lanes per publish (2|4), kOpt* bits
   uint64_t* lookback;                             // per scan tile: {tag, flag, value} granule
   uint32_t lb_tag, pad1;                          // this call's granule tag (never 0)

@@ -54,7 +54,7 @@ constexpr uint32_t kDeferred = 0xFFFFFFFEu; // key cache: the wave tier owns the
 // call's first kernel zeroes the set of the call after it, so no reset
 // launch is needed) and the sticky error word (a.err, cleared only by
 // vmqg_match_status).
-enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2 };
+enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStRewalk = 3 };
 enum : uint32_t { kErrFrontier = 2u, kErrOverflow = 4u, kErrMismatch = 8u };   // kErrLookback = 16 (lookback.h)
 
 __device__ __forceinline__ uint32_t prefix_bits(uint64_t m) {
@@ -450,12 +450,6 @@ __device__ void count_publish(const MatchArgs& a, uint32_t p, const FastScratch<
 }
 
 // ------------------------------------------------------------- EMIT pass
-// Per-group result of the resolve step, staged in LDS for the wave copy.
-struct GroupMeta {
-  uint32_t rel, span, nk, ksum;      // output start relative to the wave's first publish, length
-  uint32_t rm_lo, rm_hi, ok, crel;   // crel: start among the wave's copied (ok) records
-};
-
 // Resolve publish first + gidx of a wave: from the key cache, or by a
 // re-walk (> 2 keys).  Leaves the keys {off, cum start} in the group's LDS
 // key list.  ok = false: the wave tier writes it (or an error is latched).
@@ -488,56 +482,76 @@ __device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s,
   return true;
 }
 
-// Records mode: EMIT for the GPW consecutive publishes [first, first + n)
-// of one wave.  Resolve is per group; the copy is wave-wide over the wave's
-// output range minus the ranges of publishes the wave tier writes, so every
-// store instruction writes up to 64 x 16 B = 1 KiB contiguous.
-template <int G, int GPW, bool NT, int U>
-__device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const FastScratch<G>& s,
-                          const Group<G>& g, GroupMeta* gm, uint32_t slot0) {
-  const uint32_t p = first + g.gidx;
-  const bool valid = g.gidx < n;
-  uint32_t nk = 0, ksum = 0;
-  uint64_t rmask = 0, obase = 0, oend = 0;
-  bool ok = false;
-  if (valid) ok = resolve<G, 0>(a, p, s, g, nk, ksum, rmask, obase, oend);
-  const uint64_t wbase = a.offsets[first];
-  if (g.lane == 0)
-    gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : 0u, ok ? (uint32_t)(oend - obase) : 0u,
-                           nk == 0 ? 1 : nk, ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), ok ? 1u : 0u, 0u};
-  wave_sync();
-  // compact the copied ranges: crel = exclusive scan of the ok spans
-  const uint32_t lane = __lane_id();
-  const uint32_t sp = lane < (uint32_t)GPW ? gm[lane].span : 0u;
-  const uint32_t incl = wave_incl_scan32(sp);
-  if (lane < (uint32_t)GPW) gm[lane].crel = incl - sp;
-  const uint32_t Tok = __shfl(incl, GPW - 1, 64);
-  wave_sync();
-  // U records per lane in flight: all loads issued before the stores
-  uint32_t j = 0;
-  for (uint32_t r0 = lane; r0 < Tok; r0 += 64 * U) {
-    uint4 v[U];
-    uint64_t dst[U];
-    bool w[U];
+// Records mode EMIT (no walk code: publishes whose key cache cannot serve
+// them — more than two keys, or deferred — are emitted by the wave tier).
+// A wave takes 64 R consecutive publishes, one per lane per round: key
+// cache + offsets -> an LDS table {rel, span, crel, off0, c0, off1, rmask};
+// then one copy over the wave's whole output range (minus the wave tier's
+// publishes), U records per lane in flight, 1 KiB per store instruction.
+// R rounds per copy keep the ragged tail of the copy short.
+struct EmitMeta { uint32_t rel, span, crel, off0, c0, off1, rm_lo, rm_hi; };
+
+template <bool NT, int U, int R>
+__global__ __launch_bounds__(256) void k_emit_records(MatchArgs a) {
+  constexpr uint32_t PW = 64 * R;   // publishes per wave and copy
+  __shared__ EmitMeta gm[kWaves][PW];
+  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
+  EmitMeta* M = gm[wv];
+  const uint32_t stride = gridDim.x * kWaves * PW;
+  for (uint32_t base = (blockIdx.x * kWaves + wv) * PW; base < a.npub; base += stride) {
+    const uint32_t n = a.npub - base < PW ? a.npub - base : PW;
+    const uint64_t wbase = a.offsets[base];
+    uint32_t tot = 0;
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t r = r0 + 64 * u;
-      w[u] = r < Tok;
-      if (w[u]) {
-        while (j + 1 < (uint32_t)GPW && gm[j + 1].crel <= r) j++;
-        const GroupMeta m = gm[j];
-        const uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
-        FastScratch<G> sj = s;
-        sj.slot = slot0 + j;
-        v[u] = emission(a, [&](uint32_t i) -> uint2 { return sj.ky(i); }, m.nk, m.ksum, rm, r - m.crel);
-        dst[u] = wbase + m.rel + (r - m.crel);
+    for (int rr = 0; rr < R; rr++) {
+      const uint32_t i = rr * 64 + lane;
+      EmitMeta e{0, 0, 0, 0, 0, 0, 0, 0};
+      if (i < n) {
+        const uint32_t p = base + i;
+        const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+        const uint4 h = kc[0];
+        const uint64_t ob = a.offsets[p], oe = a.offsets[p + 1];
+        e.rel = (uint32_t)(ob - wbase);
+        if (h.y == kRewalk) {
+          a.deferred[a.npub + atomicAdd(&a.status[kStRewalk], 1u)] = p;   // the wave tier emits it
+        } else if (h.y != kDeferred) {
+          const uint4 k = kc[1];
+          if (oe > a.out_cap) atomicOr(a.err, kErrOverflow);
+          else if (oe - ob != h.x) atomicOr(a.err, kErrMismatch);
+          else e = EmitMeta{e.rel, h.x, 0, k.x, k.y, k.z, h.z, h.w};
+        }
       }
+      const uint32_t incl = wave_incl_scan32(e.span);
+      e.crel = tot + incl - e.span;
+      tot += __shfl(incl, 63, 64);
+      if (i < n) M[i] = e;
     }
+    wave_sync();
+    uint32_t j = 0;
+    for (uint32_t r0 = lane; r0 < tot; r0 += 64 * U) {
+      uint4 v[U];
+      uint64_t dst[U];
 #pragma unroll
-    for (int u = 0; u < U; u++)
-      if (w[u]) store_rec<NT>(a.out, dst[u], v[u]);
+      for (int u = 0; u < U; u++) {
+        const uint32_t r = r0 + 64 * u;
+        if (r < tot) {
+          while (j + 1 < n && M[j + 1].crel <= r) j++;
+          const EmitMeta m = M[j];
+          const uint32_t q = r - m.crel;
+          const uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
+          const uint32_t ksum = m.span - (uint32_t)__popcll(rm);
+          if (q < m.c0) v[u] = *reinterpret_cast<const uint4*>(a.records + m.off0 + q);
+          else if (q < ksum) v[u] = *reinterpret_cast<const uint4*>(a.records + m.off1 + (q - m.c0));
+          else v[u] = make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rm, q - ksum), kNone, kNone, kNone);
+          dst[u] = wbase + m.rel + q;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (r0 + 64 * u < tot) store_rec<NT>(a.out, dst[u], v[u]);
+    }
+    wave_sync();
   }
-  wave_sync();
 }
 
 // Range mode: each group writes its publish's non-empty keys as
@@ -570,11 +584,11 @@ template <int MODE, int OUT, int G, bool NT>
 __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
   using FS = FastScratch<G>;
   constexpr int GPW = FS::GPW;
-  if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < 3) a.status_next[threadIdx.x] = 0;
+  if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < 4) a.status_next[threadIdx.x] = 0;
   __shared__ uint2 st[FS::SC * FS::SLOTS];
   __shared__ uint32_t cd[FS::CC * FS::SLOTS];
   __shared__ uint2 ky[FS::KC * FS::SLOTS];
-  __shared__ GroupMeta gm[kWaves][GPW];
+  static_assert(!(MODE == 1 && OUT == 0), "records-mode EMIT is k_emit_records");
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
@@ -583,8 +597,6 @@ __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
     if (MODE == 0) {
       if (g.gidx < n) count_publish<G, OUT>(a, base + g.gidx, s, g);
-    } else if (OUT == 0) {
-      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
     } else {
       if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g);
     }
@@ -808,10 +820,13 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
   const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
   uint2* gstack = a.o_stack + gw * a.o_cap;
-  const uint32_t n = a.status[kStDeferred];   // written by the fast tier's launch
+  // the fast tier's deferred list, and in EMIT the publishes its key cache
+  // could not serve (written by the fast tier's launches)
+  const uint32_t n1 = a.status[kStDeferred];
+  const uint32_t n = n1 + (MODE == 1 ? a.status[kStRewalk] : 0u);
   const uint32_t nwaves = gridDim.x * kWaves;
   for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
-    const uint32_t p = a.deferred[d];
+    const uint32_t p = d < n1 ? a.deferred[d] : a.deferred[a.npub + (d - n1)];
     uint64_t ob = 0, oe = 0;
     if (MODE == 1) {
       ob = a.offsets[p];
@@ -909,6 +924,7 @@ hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
 
 template <int MODE, int OUT>
 static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st) {
+  static_assert(!(MODE == 1 && OUT == 0), "records-mode EMIT is k_emit_records");
   if (a.fast_g == 4) {
     if (nt) k_match_fast<MODE, OUT, 4, true><<<g, 256, 0, st>>>(a);
     else k_match_fast<MODE, OUT, 4, false><<<g, 256, 0, st>>>(a);
@@ -934,7 +950,15 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) 
     if (g > cap) g = cap;
     if (g < 1) g = 1;
     if (mode == 0) { if (out) launch_fast<0, 1>(a, g, nt, st); else launch_fast<0, 0>(a, g, nt, st); }
-    else { if (out) launch_fast<1, 1>(a, g, nt, st); else launch_fast<1, 0>(a, g, nt, st); }
+    else if (out) launch_fast<1, 1>(a, g, nt, st);
+    else {
+      constexpr int R = 2;
+      uint32_t ge = div_up(a.npub, kWaves * 64 * R);
+      if (ge > cap) ge = cap;
+      if (ge < 1) ge = 1;
+      if (nt) k_emit_records<true, VMQG_EMIT_U, R><<<ge, 256, 0, st>>>(a);
+      else k_emit_records<false, VMQG_EMIT_U, R><<<ge, 256, 0, st>>>(a);
+    }
   } else {
     // reads its list length on the device (exits at once when empty); one
     // wave per deferred publish, each wave with its own global stack
