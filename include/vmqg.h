@@ -282,7 +282,9 @@ int vmqg_last_patches(vmqg_ctx* ctx, const void** host_ptr, uint64_t* bytes, int
  * region must match the replica's (else VMQG_E_STATE: reload the image). */
 int vmqg_replica_sync_layout(vmqg_ctx* ctx, const uint8_t* layout);
 
-/* Replica side: apply patch records already in device memory on `stream`. */
+/* Replica side: apply patch records already in device memory on `stream`
+ * (after every match already queued on the context; matches queued later, on
+ * any stream, see them).  Asynchronous. */
 int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t bytes, void* stream);
 
 #ifdef __cplusplus

@@ -313,8 +313,11 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
     e.d_arena_bytes = L.total_bytes;
   }
   e.lay = L;
+  // after the matches already queued, before the ones queued later
+  if (hipStreamWaitEvent(st, e.ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
   if (hipMemcpyAsync(e.d_arena, d_src, L.total_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return VMQG_E_DEVICE;
+  if (hipEventRecord(e.ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
   e.epoch++;
   return VMQG_OK;
 }
@@ -348,8 +351,12 @@ int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t byt
   if (!e.has_device || !e.d_arena) return VMQG_E_DEVICE;
   hipSetDevice(e.device);
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e.stream;
+  // tables change only after the matches queued before, and matches queued
+  // later (on any stream) see the patches
+  if (hipStreamWaitEvent(st, e.ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
   if (vmqg::launch_patches(e.d_arena, d_patches, bytes / sizeof(vmqg::Patch), st) != hipSuccess)
     return VMQG_E_DEVICE;
+  if (hipEventRecord(e.ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
   e.epoch++;
   return VMQG_OK;
 }

@@ -6,10 +6,11 @@ the tables and matches its own publish batches; the only collectives are
 
 * the device image broadcast when a replica starts or the primary re-lays
   its arena out (``ImageSync.full``),
-* the 24-B patch records of each delta batch (``ImageSync.delta``) plus the
-  256-B layout (its trie depth sizes the wave tier's stack) — rank 0 runs
-  the host engine (``vmqg_apply_ops``), every rank applies the same bytes, so
-  all replicas stay byte-identical at each epoch,
+* the 24-B patch records of each delta batch (``ImageSync.delta``) — rank 0
+  runs the host engine (``vmqg_apply_ops``), every rank applies the same
+  bytes, so all replicas stay byte-identical at each epoch; sizes and the
+  256-B layout (its trie depth sizes the wave tier's stack) go over a
+  host-side gloo group, so the delta path never waits on a GPU stream,
 * an all-gather of per-GPU counts (``gather_counts``).
 
 Nothing on the match data path is communicated.
@@ -35,22 +36,6 @@ def _comm_device(dist, device, group=None):
     return device
 
 
-def _bcast_bytes(dist, data, src: int, device, group=None):
-    """Broadcast a byte string (given on src) -> uint8 tensor on `device`."""
-    import torch
-    cdev = _comm_device(dist, device, group)
-    n = torch.zeros(1, dtype=torch.int64, device=cdev)
-    if dist.get_rank(group) == src:
-        n[0] = len(data)
-    dist.broadcast(n, src, group=group)
-    buf = torch.empty(int(n.item()), dtype=torch.uint8, device=cdev)
-    if dist.get_rank(group) == src and len(data):
-        buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
-    if buf.numel():
-        dist.broadcast(buf, src, group=group)
-    return buf.to(device)
-
-
 def gather_counts(dist, values, device, group=None):
     """All-gather a small int64 vector from every rank -> [world, k] array."""
     import torch
@@ -65,14 +50,22 @@ class ImageSync:
 
     GPU mode (`device` is a cuda device): replicas are RegGpuView contexts
     created with replica=True; images and patches land directly in their
-    device arenas.  Host mode (`device` is cpu, used by the gloo tests): the
-    replica side keeps a numpy image and applies patches itself, so the tests
-    can prove that the patch stream reproduces the primary's image bytes.
+    device arenas, stream-ordered behind the matches already queued (no
+    device synchronisation on the delta path).  The small control messages
+    (image / patch sizes, the full-image flag, the 256-B layout) travel over
+    a host-side gloo group, so no rank has to read a GPU tensor back to learn
+    a size; the payloads travel over `group` (RCCL over xGMI with nccl).
+    Host mode (`device` is cpu, used by the gloo tests): the replica side
+    keeps a numpy image and applies patches itself, so the tests can prove
+    that the patch stream reproduces the primary's image bytes.
     """
 
-    def __init__(self, dist, view, device, src: int = 0, group=None):
+    def __init__(self, dist, view, device, src: int = 0, group=None, ctrl_group=None):
         self.dist, self.view, self.device, self.src, self.group = dist, view, device, src, group
         self.rank = dist.get_rank(group)
+        if ctrl_group is None:
+            ctrl_group = group if dist.get_backend(group) == "gloo" else dist.new_group(backend="gloo")
+        self.ctrl = ctrl_group
         self.image = None     # host mode replica image
         self.layout = None
 
@@ -83,69 +76,95 @@ class ImageSync:
     def _gpu(self) -> bool:
         return getattr(self.device, "type", str(self.device)) != "cpu"
 
+    def _ctrl(self, values, layout: bytes = b""):
+        """Broadcast a few int64s and the layout bytes over the host group."""
+        import torch
+        t = torch.zeros(len(values) + 1 + 32, dtype=torch.int64)
+        if self.primary:
+            t[: len(values)] = torch.tensor(values, dtype=torch.int64)
+            t[len(values)] = len(layout)
+            if layout:
+                t[len(values) + 1:len(values) + 1 + len(layout) // 8] = torch.frombuffer(bytearray(layout),
+                                                                                     dtype=torch.int64)
+        self.dist.broadcast(t, self.src, group=self.ctrl)
+        vals = [int(x) for x in t[: len(values)]]
+        nl = int(t[len(values)])
+        lay = t[len(values) + 1:len(values) + 1 + nl // 8].numpy().tobytes() if nl else b""
+        return vals, lay
+
+    def _payload(self, nbytes: int, fill=None):
+        """A uint8 device tensor of nbytes broadcast from the primary
+        (`fill(tensor)` writes the primary's bytes)."""
+        import torch
+        cdev = _comm_device(self.dist, self.device, self.group)
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        if self.primary and fill is not None and nbytes:
+            fill(buf)
+        if not nbytes:
+            return buf
+        if cdev.type == "cpu" and self._gpu():   # gloo rehearsal: stage through host memory
+            host = buf.cpu()
+            self.dist.broadcast(host, self.src, group=self.group)
+            buf.copy_(host, non_blocking=True)
+        else:
+            self.dist.broadcast(buf, self.src, group=self.group)
+        return buf
+
     def full(self):
         """Broadcast the primary's whole image; replicas adopt it."""
         import torch
-        d = self.dist
         if self.primary:
             ptr, nbytes, lay = self.view.arena()
         else:
             ptr, nbytes, lay = 0, 0, b""
-        lay_t = _bcast_bytes(d, lay, self.src, self.device, self.group)
-        cdev = _comm_device(d, self.device, self.group)
-        n = torch.tensor([nbytes], dtype=torch.int64, device=cdev)
-        d.broadcast(n, self.src, group=self.group)
-        nbytes = int(n.item())
-        img = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-        if self.primary:
+        (nbytes,), lay = self._ctrl([nbytes], lay)
+        self.layout = lay
+
+        def fill(buf):
             if self._gpu():
-                hip_memcpy_d2d(img.data_ptr(), ptr, nbytes)
+                torch.cuda.synchronize(self.device)   # the primary's arena is up to date
+                hip_memcpy_d2d(buf.data_ptr(), ptr, nbytes)
             else:
-                img.copy_(torch.from_numpy(self.view.export_image()))
-        if self._gpu():
-            torch.cuda.synchronize(self.device)
-        if cdev.type == "cpu" and self._gpu():   # gloo rehearsal: stage through host memory
-            host = img.cpu()
-            d.broadcast(host, self.src, group=self.group)
-            img.copy_(host)
-        else:
-            d.broadcast(img, self.src, group=self.group)
-        self.layout = bytes(lay_t.cpu().numpy())
+                buf.copy_(torch.from_numpy(self.view.export_image()))
+
+        img = self._payload(nbytes, fill)
         if not self.primary:
             if self._gpu():
-                self.view.replica_load(self.layout, img.data_ptr())
-                torch.cuda.synchronize(self.device)
+                self.view.replica_load(self.layout, img.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+                torch.cuda.synchronize(self.device)   # img is released after the copy
             else:
                 self.image = img.numpy().copy()
         return nbytes
 
     def delta(self):
         """After the primary applied a batch: ship its patches (or the full
-        image when the batch re-laid the arena out)."""
+        image when the batch re-laid the arena out).  Returns the number of
+        patch records (-1: a full image was shipped)."""
         import torch
-        d = self.dist
-        flag = torch.zeros(1, dtype=torch.int64, device=_comm_device(d, self.device, self.group))
-        data, lay = b"", b""
+        data, full, lay = b"", 0, b""
         if self.primary:
-            data, full = self.view.last_patches()
-            flag[0] = 1 if full else 0
+            data, f = self.view.last_patches()
+            full = 1 if f else 0
             lay = self.view.arena()[2]
-        d.broadcast(flag, self.src, group=self.group)
-        if int(flag.item()):
+        (full, nbytes), lay = self._ctrl([full, len(data)], lay)
+        if full:
             self.full()
             return -1
-        lay_t = _bcast_bytes(d, lay, self.src, self.device, self.group)
-        buf = _bcast_bytes(d, data, self.src, self.device, self.group)
+
+        def fill(buf):
+            buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8), non_blocking=False)
+
+        buf = self._payload(nbytes, fill)
         if not self.primary:
-            self.layout = bytes(lay_t.cpu().numpy())
+            self.layout = lay
             if self._gpu():
-                self.view.replica_sync_layout(self.layout)
-                if buf.numel():
-                    self.view.apply_patches_device(buf.data_ptr(), buf.numel())
-                torch.cuda.synchronize(self.device)
-            elif buf.numel():
+                self.view.replica_sync_layout(lay)
+                if nbytes:
+                    self.view.apply_patches_device(buf.data_ptr(), nbytes,
+                                                   torch.cuda.current_stream(self.device).cuda_stream)
+            elif nbytes:
                 apply_patches_host(self.image, buf.numpy())
-        return buf.numel() // 24
+        return nbytes // 24
 
 
 PATCH_DTYPE = np.dtype([("off", "<u8"), ("data", "<u4", (4,))])
