@@ -448,102 +448,251 @@ def bench_other(args):
         "deferred": [st["deferred_tier1"], st["deferred_tier2"]]}), flush=True)
 
 
+def _dist_init(args):
+    """RANK / LOCAL_RANK / WORLD_SIZE from torch.distributed.run; nccl = RCCL."""
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.force_device >= 0:
+        local = args.force_device
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
+    return world, rank, local, dev, dist
+
+
 def bench_d(args):
     """Config D: 10M subscriptions (8M exact, 1M '+'/'#', 1M
     $share members on 4 nodes) under 1 %/s churn: 10 delta batches per second
-    of 10k ops (50/50 sub/unsub, host engine + device patches).  One step =
-    one churn period: the match batches (2^20 publishes each) that fit in
-    100 ms of GPU time are queued, then the period's delta batch is applied
-    (its host work overlaps the queued matches; the patches land after them,
-    stream-ordered).  Single GPU; prints one JSON line."""
+    of 10k ops (50/50 sub/unsub).  One step = one churn period: every rank
+    queues the match batches (2^20 publishes each) that fit in 100 ms of its
+    GPU time, then rank 0 applies the period's delta batch in the host
+    engine (vmqg_apply_ops: never waits for the queued matches; its patches
+    land after them, stream-ordered) and, at N > 1, broadcasts the patches to
+    every replica over RCCL (ImageSync.delta, sizes over a host gloo group).
+    At the end every rank matches one common sample batch: replica outputs
+    must equal rank 0's byte for byte, and the per-publish counts the known
+    answer of the live set (workloads.config_d_counts)."""
+    import hashlib
+
     import torch
+    world, rank, local, dev, dist = _dist_init(args)
+    from vernemq_amd import _lib
+    from vernemq_amd import dist as vd
     from vernemq_amd import workloads as W
     from vernemq_amd.reg_view import RegGpuView
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(0)
     t0 = time.time()
     w = W.config_d(scale=args.d_scale, n_pubs=args.batch)
     n_live = w.notes["n_live"]
-    view = RegGpuView(node=w.self_node, device=0, nodes=w.nodes,
-                      hints={"edges": 4 * n_live // 5, "paths": 4 * n_live // 5, "keys": n_live,
-                             "records": n_live * 11 // 10, "exact": n_live})
-    ids = w.load_into(view, n=n_live)
-    load_s = time.time() - t0
-    log("config D: %d live subs loaded in %.1fs, %s" % (n_live, load_s, view.stats_raw()))
+    load_s = 0.0
     ch = W.Churn(w)
-    pubs, words = w.publish_arrays(view)
+    if rank == 0:
+        view = RegGpuView(node=w.self_node, device=local, nodes=w.nodes,
+                          hints={"edges": 4 * n_live // 5, "paths": 4 * n_live // 5, "keys": n_live,
+                                 "records": n_live * 11 // 10, "exact": n_live})
+        ids = w.load_into(view, n=n_live)
+        load_s = time.time() - t0
+        log("config D: %d live subs loaded in %.1fs, %s" % (n_live, load_s, view.stats_raw()))
+        pwid = view.intern_words(w.pub_words, create=False).astype(np.int64)
+    else:
+        view = RegGpuView(node=w.self_node, device=local, replica=True)
+        pwid = np.zeros(len(w.pub_words), dtype=np.int64)
+    sync = None
+    if world > 1:
+        sync = vd.ImageSync(dist, view, dev)
+        nbytes = sync.full()
+        pw_t = torch.from_numpy(pwid).to(dev)
+        dist.broadcast(pw_t, 0)
+        pwid = pw_t.cpu().numpy()
+        log("rank %d: config D image %.1f MB replicated" % (rank, nbytes / 1e6))
+    pubs, words = w.publish_arrays_ids(pwid, np.array([0], dtype=np.uint32))
     npub = len(pubs)
+    pubs0 = pubs
+    if rank:   # every GPU its own batch of the same distribution
+        pubs = np.roll(pubs, rank * npub // world)
     d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
     d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
     d_offs = torch.zeros(npub + 1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream().cuda_stream
-    # size the output from a first count
-    recs, offs = None, None
-    out_cap = 8 * npub
+    out_cap = 1024
     d_out = torch.empty(out_cap * 4, dtype=torch.int32, device=dev)
 
     def match():
-        nonlocal out_cap, d_out
         view.match_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_out.data_ptr(), out_cap,
                           d_offs.data_ptr(), sp)
 
-    match()
+    match()   # sizes the output (the churn keeps the total within 20 %)
     torch.cuda.synchronize()
     need = int(d_offs[-1].item())
     view.match_status(sp)
     out_cap = int(need * 1.2) + 1024
     d_out = torch.empty(out_cap * 4, dtype=torch.int32, device=dev)
     batches = [ch.batch(args.churn_batch) for _ in range(args.warmup + args.steps)]
+    ops_of = (lambda k: ch.ops(ids, *batches[k])) if rank == 0 else None
+
+    def period(k, per_period, acc):
+        for _ in range(per_period):
+            match()                                   # queued on the GPU
+        if rank == 0:
+            ops, wds = ops_of(k)
+            ta = time.perf_counter()
+            view.apply_op_arrays(ops, wds)            # host engine; patches queued behind the matches
+            acc["apply"] += time.perf_counter() - ta
+        if sync is not None:
+            td = time.perf_counter()
+            acc["patches"] += max(0, sync.delta())
+            acc["delta"] += time.perf_counter() - td
+
+    acc = {"apply": 0.0, "delta": 0.0, "patches": 0}
     for k in range(args.warmup):
-        view.apply_op_arrays(*ch.ops(ids, *batches[k]))
-        match()
+        period(k, 1, acc)
     torch.cuda.synchronize()
     if view.match_status(sp) != 0:
         raise RuntimeError("match status after warmup")
-    # GPU time of one match batch -> match batches per 100 ms churn period
+    # GPU time of one match batch -> match batches per 100 ms churn period (rank 0 decides)
     t0 = time.perf_counter()
     for _ in range(5):
         match()
     torch.cuda.synchronize()
     t_match = (time.perf_counter() - t0) / 5
-    period = 1.0 / args.churn_rate_batches
-    per_period = max(1, int(period / t_match))
-    log("config D: match batch %.2f ms -> %d match batches per %.0f ms churn period" %
-        (t_match * 1e3, per_period, period * 1e3))
-    apply_s = 0.0
+    period_s = 1.0 / args.churn_rate_batches
+    pp = torch.tensor([max(1, int(period_s / t_match))], dtype=torch.int64, device=dev)
+    if dist:
+        dist.broadcast(pp, 0)
+    per_period = int(pp.item())
+    log("rank %d: match batch %.2f ms -> %d match batches per %.0f ms churn period"
+        % (rank, t_match * 1e3, per_period, period_s * 1e3))
+    st0 = view.stats_raw()
+    view.set_timing(True)
+    acc = {"apply": 0.0, "delta": 0.0, "patches": 0}
+    if dist:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
-        for _ in range(per_period):
-            match()                                   # queued on the GPU
-        ops, wds = ch.ops(ids, *batches[k])
-        ta = time.perf_counter()
-        view.apply_op_arrays(ops, wds)                # host engine overlaps the queued matches
-        apply_s += time.perf_counter() - ta
+        period(k, per_period, acc)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
     rc = view.match_status(sp)
     if rc != 0:
         raise RuntimeError("match status %d" % rc)
+    count_ns, emit_ns, _ = view.kernel_times()
+    st1 = view.stats_raw()
     emitted = int(d_offs[-1].item())
-    st = view.stats_raw()
-    res = {
-        "metric": "publishes/sec under churn (config D, 10M subs incl. $share, 1%/s deltas)",
-        "value": npub * args.steps * per_period / el, "unit": "publishes/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-        "data": "synthetic: SURVEY.md §8(d) config D generator (splitmix64 seed 0xD), scale %g" % args.d_scale,
-        "config": {"workload": "D: %d live subs, %d-op delta batch + %d publishes per step" %
-                               (n_live, args.churn_batch, npub)},
-        "deltas_per_s": args.churn_batch * args.steps / el,
-        "apply_ms_per_batch": apply_s * 1e3 / args.steps,
-        "match_batches_per_delta_batch": per_period,
-        "pairs_per_s": emitted * args.steps * per_period / el,
-        "emissions_per_match_batch": emitted, "load_s": load_s,
-        "arena_bytes": st["device_bytes"], "rebuilds": st["rebuilds"],
-        "deferred": [st["deferred_tier1"], st["deferred_tier2"]],
-    }
-    print(json.dumps(res), flush=True)
+    # parity: every rank matches rank 0's (unrolled) batch; replicas must
+    # equal the primary byte for byte, and all the live set's known answer
+    if rank:
+        d_pubs.copy_(torch.from_numpy(pubs0.view(np.uint32).reshape(-1).copy()))
+    match()
+    torch.cuda.synchronize()
+    if view.match_status(sp) != 0:
+        raise RuntimeError("match status (parity pass)")
+    offs_h = d_offs.cpu().numpy()
+    known = bool(np.array_equal(np.diff(offs_h), W.config_d_counts(w, ch.live)))
+    if not known:
+        raise RuntimeError("config D counts differ from the live set's known answer")
+    S = min(npub, 1 << 16)
+    h = hashlib.sha256(offs_h[: S + 1].tobytes() + d_out[: int(offs_h[S]) * 4].cpu().numpy().tobytes()).digest()
+    replicas_equal = True
+    if dist:
+        allh = vd.gather_counts(dist, np.frombuffer(h[:16], dtype=np.int64), dev)
+        replicas_equal = bool((allh == allh[0]).all())
+        if not replicas_equal:
+            raise RuntimeError("replica match output differs from the primary's")
+    t_max = el
+    if dist:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+    total_pubs = npub * args.steps * per_period * world
+
+    cpu = None
+    b_p = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import feed   # the CPU restatement: baseline (and lookup counts) only
+        t0 = time.time()
+        orc = feed.load_prefix(w, n_live)
+        log("D cpu baseline: oracle loaded %d subs in %.1fs" % (n_live, time.time() - t0))
+        CS = 2048
+        buf = feed.publish_bytes(w, 0, CS)
+        rates = {}
+        for th in (1, args.cpu_threads):
+            ns1, _ = orc.fold_timed(buf, 1, th)
+            reps = max(1, int(math.ceil(args.cpu_seconds * 1e9 / max(ns1, 1))))
+            ns, _ = orc.fold_timed(buf, reps, th)
+            rates[th] = (CS * reps / (ns / 1e9), reps, ns / 1e9)
+        _, counts = orc.fold_batch([("", b"p", w.pub_topic(i)) for i in range(256)], with_counts=True)
+        b_p = {"lookup": float(np.mean([8 * (c[2] + 1) + 16 * c[0] for c in counts])),
+               "emit": float(np.mean([32 * c[1] for c in counts]))}
+        cpu = {"value": rates[args.cpu_threads][0], "unit": "publishes/s", "cores": args.cpu_threads, "kind": "port",
+               "single_thread_value": rates[1][0],
+               "sample": "first %d publishes of the D batch x %d reps (%.1fs) on %d threads against the %d live "
+                         "subscriptions (1 thread: %.3g publishes/s), oracle/vmq_trie_oracle.cpp (C++ restatement "
+                         "of vmq_reg_trie fold/4; not BEAM); host %s"
+                         % (CS, rates[args.cpu_threads][1], rates[args.cpu_threads][2], args.cpu_threads, n_live,
+                            rates[1][0], cpu_model())}
+        log("D cpu baseline: %.0f publishes/s (%d threads), %.0f (1 thread)"
+            % (rates[args.cpu_threads][0], args.cpu_threads, rates[1][0]))
+
+    if rank == 0:
+        ops_n = st1["ops_applied"] - st0["ops_applied"]
+        host_ns = st1["apply_host_ns"] - st0["apply_host_ns"]
+        # dominant kernel: EMIT; SURVEY §8(d)'s R_p term, 16 B read + 16 B
+        # written per emission (D's records are mostly distinct: real reads)
+        alg_emit = 32 * emitted
+        achieved = alg_emit / emit_ns if emit_ns else None
+        res = {
+            "metric": "publishes/sec under churn (config D, 10M subs incl. $share, 1%/s deltas)",
+            "value": total_pubs / t_max, "unit": "publishes/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": t_max * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: SURVEY.md §8(d) config D generator (splitmix64 seed 0xD), scale %g" % args.d_scale,
+            "config": {"workload": "D: %d live subs, %d-op delta batch per period (%g periods/s) + %d match "
+                                   "batches of %d publishes per period per GPU"
+                                   % (n_live, args.churn_batch, args.churn_rate_batches, per_period, npub),
+                       "parallelism": "trie replicated, deltas broadcast as patches (RCCL), publishes sharded x%d"
+                                      % world},
+            "deltas_per_s": args.churn_batch * args.steps / t_max,
+            "delta_apply": {"host_ops_per_s": ops_n / (host_ns / 1e9) if host_ns else None,
+                            "host_ms_per_batch": host_ns / 1e6 / args.steps,
+                            "caller_ms_per_batch": acc["apply"] * 1e3 / args.steps,
+                            "patch_bytes_per_batch": (st1["patch_bytes"] - st0["patch_bytes"]) / args.steps,
+                            "full_images": int(st1["image_bytes"] > st0["image_bytes"]),
+                            "rebuilds": st1["rebuilds"] - st0["rebuilds"],
+                            "broadcast_ms_per_batch": acc["delta"] * 1e3 / args.steps if sync else None,
+                            "headroom_vs_100k_per_s": (ops_n / (host_ns / 1e9)) / 1e5 if host_ns else None},
+            "match_batches_per_delta_batch": per_period,
+            "pairs_per_s": emitted * args.steps * per_period * world / t_max,
+            "emissions_per_match_batch": emitted, "load_s": load_s,
+            "verified": {"known_answer": known, "replicas_equal": replicas_equal},
+            "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS if achieved else None,
+                         "traffic": load_pmc_traffic("k_emit_records", "pmc_d.json"),
+                         "kernel": "k_emit_records (EMIT)", "algorithmic_bytes_per_launch": alg_emit,
+                         "bytes_model": "SURVEY 8(d) 32 B per emission (16-B record read + 16-B written)"},
+            "survey_bytes_per_publish": b_p,
+            "count_kernel": {"us": count_ns / 1e3,
+                             "achieved": (b_p["lookup"] * npub / count_ns) if (b_p and count_ns) else None,
+                             "bytes_model": "8(L+1) + 16 S_p per publish, S_p from the oracle's lookup counters on "
+                                            "256 publishes"},
+            "cpu_baseline": cpu,
+            "arena_bytes": st1["device_bytes"],
+            "deferred": [st1["deferred_tier1"], st1["deferred_tier2"]],
+            "build_id": _lib.build_id(),
+        }
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
 
 def bench_retain(args):

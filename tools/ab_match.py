@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of match-kernel tuning options (fast_g, nt_stores, fused,
-unroll) on one device, one process
-(cdna_hip_programming.md §5.4 rule 24): config C is loaded once, each round
-runs every variant for `steps` steps; medians of the per-variant step time
-and of the COUNT / EMIT kernel times are printed as JSON."""
+"""Interleaved A/B of match-kernel options (vmqg_set_option) on one device,
+one process (cdna_hip_programming.md §5.4 rule 24): the workload is loaded
+once, each round runs every variant for `steps` steps; outputs are checked
+equal between variants (offsets exactly, records as a per-batch checksum:
+the order inside a publish may differ between variants); medians of the
+per-variant step time and the COUNT / fast-EMIT kernel times are printed as
+JSON.  usage: ab_match.py --config C --opt emit_lean=0,1 --opt fast_g=2,4"""
 import argparse
 import itertools
 import json
@@ -21,11 +23,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--fast-g", default="4,8")
-    ap.add_argument("--nt", default="1")
-    ap.add_argument("--fused", default="0,1")
-    ap.add_argument("--unroll", default="4")
+    ap.add_argument("--opt", action="append", default=[], help="name=v1,v2,...")
     ap.add_argument("--config", default="C", choices=["C", "D"])
+    ap.add_argument("--d-scale", type=float, default=1.0)
     ap.add_argument("--n-dev", type=int, default=1_000_000)
     args = ap.parse_args()
     import torch
@@ -37,7 +37,7 @@ def main():
         v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
         w.load_into(v)
     else:
-        w = W.config_d(n_pubs=1 << 20)
+        w = W.config_d(scale=args.d_scale, n_pubs=1 << 20)
         n_live = w.notes["n_live"]
         v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes,
                        hints={"edges": 4 * n_live // 5, "paths": 4 * n_live // 5, "keys": n_live,
@@ -50,18 +50,15 @@ def main():
     d_out = torch.empty(cap * 4, dtype=torch.int32, device=dev)
     d_offs = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream().cuda_stream
-    variants = list(itertools.product([int(x) for x in args.fast_g.split(",")],
-                                      [int(x) for x in args.nt.split(",")],
-                                      [int(x) for x in args.fused.split(",")],
-                                      [int(x) for x in args.unroll.split(",")]))
-    res = {str(vv): {"step_us": [], "count_us": [], "emit_us": []} for vv in variants}
+    names = [o.split("=")[0] for o in args.opt]
+    values = [[int(x) for x in o.split("=")[1].split(",")] for o in args.opt]
+    variants = list(itertools.product(*values))
+    res = {str(dict(zip(names, vv))): {"step_us": [], "count_us": [], "emit_us": []} for vv in variants}
     ref = None
     for rnd in range(args.rounds):
         for vv in variants:
-            v.set_option("fast_g", vv[0])
-            v.set_option("nt_stores", vv[1])
-            v.set_option("fused", vv[2])
-            v.set_option("unroll", vv[3])
+            for n, x in zip(names, vv):
+                v.set_option(n, x)
             v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap,
                            d_offs.data_ptr(), sp)
             torch.cuda.synchronize()
@@ -81,12 +78,12 @@ def main():
             dt = (time.perf_counter() - t0) / args.steps
             c, e, _ = v.kernel_times()
             v.set_timing(False)
-            r = res[str(vv)]
+            r = res[str(dict(zip(names, vv)))]
             r["step_us"].append(dt * 1e6)
             r["count_us"].append(c / 1e3)
             r["emit_us"].append(e / 1e3)
     out = {k: {m: statistics.median(x) for m, x in d.items()} for k, d in res.items()}
-    print(json.dumps({"variants": "(fast_g, nt_stores, fused, unroll)", "config": args.config, "median": out, "rounds": args.rounds}, indent=1))
+    print(json.dumps({"config": args.config, "median": out, "rounds": args.rounds, "steps": args.steps}))
 
 
 if __name__ == "__main__":

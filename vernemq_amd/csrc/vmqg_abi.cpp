@@ -251,6 +251,8 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
     e.opt_fast_g = (uint32_t)value;
   } else if (n == "nt_stores") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptNtStores) : (e.opt_flags & ~vmqg::kOptNtStores);
+  } else if (n == "emit_lean") {
+    e.opt_flags = value ? (e.opt_flags | vmqg::kOptLeanEmit) : (e.opt_flags & ~vmqg::kOptLeanEmit);
   } else {
     return VMQG_E_INVAL;
   }

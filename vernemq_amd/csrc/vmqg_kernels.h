@@ -35,6 +35,7 @@ struct MatchArgs {
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
+constexpr uint32_t kOptLeanEmit = 2u;   // records EMIT by k_emit_records (multi-key publishes to the wave tier)
 
 // mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier (grid a.o_waves / 4)
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st);

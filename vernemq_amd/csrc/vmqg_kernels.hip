@@ -450,6 +450,12 @@ __device__ void count_publish(const MatchArgs& a, uint32_t p, const FastScratch<
 }
 
 // ------------------------------------------------------------- EMIT pass
+// Per-group result of the resolve step, staged in LDS for the wave copy.
+struct GroupMeta {
+  uint32_t rel, span, nk, ksum;      // output start relative to the wave's first publish, length
+  uint32_t rm_lo, rm_hi, ok, crel;   // crel: start among the wave's copied (ok) records
+};
+
 // Resolve publish first + gidx of a wave: from the key cache, or by a
 // re-walk (> 2 keys).  Leaves the keys {off, cum start} in the group's LDS
 // key list.  ok = false: the wave tier writes it (or an error is latched).
@@ -482,7 +488,59 @@ __device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s,
   return true;
 }
 
-// Records mode EMIT (no walk code: publishes whose key cache cannot serve
+// Records mode: EMIT for the GPW consecutive publishes [first, first + n)
+// of one wave.  Resolve is per group; the copy is wave-wide over the wave's
+// output range minus the ranges of publishes the wave tier writes, so every
+// store instruction writes up to 64 x 16 B = 1 KiB contiguous.
+template <int G, int GPW, bool NT, int U>
+__device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const FastScratch<G>& s,
+                          const Group<G>& g, GroupMeta* gm, uint32_t slot0) {
+  const uint32_t p = first + g.gidx;
+  const bool valid = g.gidx < n;
+  uint32_t nk = 0, ksum = 0;
+  uint64_t rmask = 0, obase = 0, oend = 0;
+  bool ok = false;
+  if (valid) ok = resolve<G, 0>(a, p, s, g, nk, ksum, rmask, obase, oend);
+  const uint64_t wbase = a.offsets[first];
+  if (g.lane == 0)
+    gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : 0u, ok ? (uint32_t)(oend - obase) : 0u,
+                           nk == 0 ? 1 : nk, ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), ok ? 1u : 0u, 0u};
+  wave_sync();
+  // compact the copied ranges: crel = exclusive scan of the ok spans
+  const uint32_t lane = __lane_id();
+  const uint32_t sp = lane < (uint32_t)GPW ? gm[lane].span : 0u;
+  const uint32_t incl = wave_incl_scan32(sp);
+  if (lane < (uint32_t)GPW) gm[lane].crel = incl - sp;
+  const uint32_t Tok = __shfl(incl, GPW - 1, 64);
+  wave_sync();
+  // U records per lane in flight: all loads issued before the stores
+  uint32_t j = 0;
+  for (uint32_t r0 = lane; r0 < Tok; r0 += 64 * U) {
+    uint4 v[U];
+    uint64_t dst[U];
+    bool w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t r = r0 + 64 * u;
+      w[u] = r < Tok;
+      if (w[u]) {
+        while (j + 1 < (uint32_t)GPW && gm[j + 1].crel <= r) j++;
+        const GroupMeta m = gm[j];
+        const uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
+        FastScratch<G> sj = s;
+        sj.slot = slot0 + j;
+        v[u] = emission(a, [&](uint32_t i) -> uint2 { return sj.ky(i); }, m.nk, m.ksum, rm, r - m.crel);
+        dst[u] = wbase + m.rel + (r - m.crel);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (w[u]) store_rec<NT>(a.out, dst[u], v[u]);
+  }
+  wave_sync();
+}
+
+// Records mode EMIT, lean variant (option "emit_lean"; no walk code: publishes whose key cache cannot serve
 // them — more than two keys, or deferred — are emitted by the wave tier).
 // A wave takes 64 R consecutive publishes, one per lane per round: key
 // cache + offsets -> an LDS table {rel, span, crel, off0, c0, off1, rmask};
@@ -588,7 +646,7 @@ __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
   __shared__ uint2 st[FS::SC * FS::SLOTS];
   __shared__ uint32_t cd[FS::CC * FS::SLOTS];
   __shared__ uint2 ky[FS::KC * FS::SLOTS];
-  static_assert(!(MODE == 1 && OUT == 0), "records-mode EMIT is k_emit_records");
+  __shared__ GroupMeta gm[kWaves][MODE == 1 && OUT == 0 ? GPW : 1];
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
@@ -597,6 +655,8 @@ __global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
     if (MODE == 0) {
       if (g.gidx < n) count_publish<G, OUT>(a, base + g.gidx, s, g);
+    } else if (OUT == 0) {
+      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
     } else {
       if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g);
     }
@@ -924,7 +984,6 @@ hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
 
 template <int MODE, int OUT>
 static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st) {
-  static_assert(!(MODE == 1 && OUT == 0), "records-mode EMIT is k_emit_records");
   if (a.fast_g == 4) {
     if (nt) k_match_fast<MODE, OUT, 4, true><<<g, 256, 0, st>>>(a);
     else k_match_fast<MODE, OUT, 4, false><<<g, 256, 0, st>>>(a);
@@ -951,6 +1010,7 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) 
     if (g < 1) g = 1;
     if (mode == 0) { if (out) launch_fast<0, 1>(a, g, nt, st); else launch_fast<0, 0>(a, g, nt, st); }
     else if (out) launch_fast<1, 1>(a, g, nt, st);
+    else if (!(a.opts & kOptLeanEmit)) launch_fast<1, 0>(a, g, nt, st);
     else {
       constexpr int R = 2;
       uint32_t ge = div_up(a.npub, kWaves * 64 * R);

@@ -465,6 +465,53 @@ class Churn:
         return ev
 
 
+def config_d_counts(w: Workload, live: np.ndarray, lo: int = 0, hi: int | None = None) -> np.ndarray:
+    """Known answer (vectorised) for config D: emissions per publish [lo, hi)
+    given the live-subscription mask.  site/s/dev/d/state emits every live
+    exact subscriber of (s, d); site/s/x/alarm/z every live site/s/+/alarm/#
+    subscriber; jobs/q/x every live member of every group on q, once per
+    distinct node hosting a live member of the group (Q2, vmq_reg_trie.erl:
+    68-72, 301-303).  Used by bench.py as a size-independent check."""
+    hi = w.n_pubs if hi is None else hi
+    n_s, n_d, n_q = w.notes["n_s"], w.notes["n_d"], w.notes["n_q"]
+    s_base = 8
+    T = w.tw.reshape(-1, 5)
+    idx = np.flatnonzero(live)
+    rows = T[idx]
+    is_exact = (rows[:, 0] == 0) & (rows[:, 2] == 1)
+    is_alarm = (rows[:, 0] == 0) & (rows[:, 2] == 3)
+    is_jobs = rows[:, 0] == 6
+    ex = np.bincount((rows[is_exact, 1] - s_base) * n_d + (rows[is_exact, 3] - s_base), minlength=n_s * n_d)
+    al = np.bincount(rows[is_alarm, 1] - s_base, minlength=n_s)
+    g = rows[is_jobs, 1]
+    q = rows[is_jobs, 3] - s_base
+    nodes = w.sub_node[idx[is_jobs]]
+    g_min = int(g.min()) if len(g) else 0
+    G = (g - g_min) if len(g) else g
+    n_g = int(G.max()) + 1 if len(G) else 1
+    members = np.bincount(G, minlength=n_g)
+    node_seen = np.zeros((n_g, 4), dtype=bool)
+    node_seen[G, nodes] = True
+    distinct = node_seen.sum(axis=1)
+    g_q = np.zeros(n_g, dtype=np.int64)
+    g_q[G] = q
+    jobs = np.bincount(g_q, weights=members * distinct, minlength=n_q).astype(np.int64)
+    out = np.zeros(hi - lo, dtype=np.int64)
+    pn_base = 5
+    a = w.pw_off[lo:hi]
+    first = w.pw[a]
+    second = w.pw[a + 1] - pn_base
+    is_jobs_p = first == 4
+    third = np.where(is_jobs_p, 0, w.pw[np.minimum(a + 2, len(w.pw) - 1)])
+    is_state = ~is_jobs_p & (third == 1)
+    fourth = np.where(is_state, w.pw[np.minimum(a + 3, len(w.pw) - 1)] - pn_base, 0)
+    out[is_jobs_p] = jobs[second[is_jobs_p]]
+    out[is_state] = ex[second[is_state] * n_d + fourth[is_state]]
+    alarm_p = ~is_jobs_p & ~is_state
+    out[alarm_p] = al[second[alarm_p]]
+    return out
+
+
 def _zipf_cdf(n: int, s: float) -> np.ndarray:
     p = 1.0 / np.arange(1, n + 1, dtype=np.float64) ** s
     return np.cumsum(p / p.sum())
