@@ -1,0 +1,336 @@
+/*
+ * vmqg_nif.c — the erl_nif glue of vmq_reg_gpu_view (src/vmq_reg_gpu_view.erl)
+ * over libvmqgpu (include/vmqg.h).
+ *
+ * Only term <-> id conversion lives here; batching, matching with the
+ * overflow retry, the fold and the op batches are vmqg_batch.c (plain C,
+ * compiled and unit-tested in this repository: tests/test_nif_layer.py,
+ * tools/nif_harness.c).  This file is written against the documented
+ * erl_nif API (OTP 21+) and is NOT compiled here: the image has no OTP.
+ *
+ * Build (in apps/vmq_server, rebar3 port_specs or a Makefile):
+ *   cc -O2 -fPIC -shared -I$ERTS/include -I<repo>/include -I<repo>/integration/c_src \
+ *      vmqg_nif.c vmqg_batch.c -L<priv> -lvmqgpu -o priv/vmqg_nif.so
+ *
+ * Terms and their ids (one resource per view):
+ *   mountpoint (string)          -> vmqg mountpoint id    (interner `mps`)
+ *   node atom                    -> node id; node() is 0   (interner `nodes`)
+ *   SubscriberId {MP, ClientId}  -> subscriber id         (interner `subs`)
+ *   SubInfo (QoS | {QoS, Map})   -> subinfo id            (interner `infos`)
+ *   $share group binary          <- its word id           (`groups`, by word id)
+ * Terms are keyed by their external term format (enif_term_to_binary) and
+ * kept as copies in the resource's own environment, so building an entry is
+ * an enif_make_copy, never a decode.
+ */
+#include <erl_nif.h>
+#include <string.h>
+
+#include "vmqg.h"
+#include "vmqg_batch.h"
+
+typedef struct {
+  ErlNifEnv* env;                 /* owns the stored terms */
+  ERL_NIF_TERM* terms;
+  size_t n, cap;
+} term_store;
+
+typedef struct {
+  vmqg_ctx* ctx;
+  ErlNifMutex* lock;              /* fold callers vs. the initial load process */
+  vmqgb_interner *mps, *nodes, *subs, *infos;
+  term_store node_t, sub_t, info_t, group_t;   /* group_t indexed by word id */
+  vmqgb_batch batch;
+  vmqgb_ops ops;                  /* add_init accumulation */
+  uint32_t max_mountpoints;
+} vmqg_res;
+
+static ErlNifResourceType* RES;
+static ERL_NIF_TERM a_ok, a_error, a_invalid_topic, a_device, a_nomem, a_badarg, a_records, a_ranges;
+
+/* ------------------------------------------------------------ helpers */
+static int store_put(term_store* s, size_t id, ERL_NIF_TERM t) {
+  if (id >= s->cap) {
+    size_t c = s->cap ? s->cap * 2 : 1024;
+    while (c <= id) c *= 2;
+    ERL_NIF_TERM* nt = (ERL_NIF_TERM*)enif_realloc(s->terms, c * sizeof(ERL_NIF_TERM));
+    if (!nt) return 0;
+    s->terms = nt;
+    s->cap = c;
+  }
+  if (id >= s->n) s->n = id + 1;
+  s->terms[id] = enif_make_copy(s->env, t);
+  return 1;
+}
+
+/* id of a term (created on first sight), its copy stored under the id */
+static int term_id(vmqgb_interner* in, term_store* st, ErlNifEnv* env, ERL_NIF_TERM t, uint32_t* id) {
+  ErlNifBinary b;
+  if (!enif_term_to_binary(env, t, &b)) return 0;
+  const uint32_t before = vmqgb_count(in);
+  *id = vmqgb_intern(in, b.data, b.size);
+  enif_release_binary(&b);
+  if (*id == VMQG_NONE) return 0;
+  if (st && *id >= before) return store_put(st, *id, t);
+  return 1;
+}
+
+static ERL_NIF_TERM error_term(ErlNifEnv* env, int rc) {
+  ERL_NIF_TERM r = rc == VMQG_E_INVAL ? a_invalid_topic : rc == VMQG_E_NOMEM ? a_nomem
+                 : rc == VMQG_E_DEVICE ? a_device : a_badarg;
+  return enif_make_tuple2(env, a_error, r);
+}
+
+static void res_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  vmqg_res* r = (vmqg_res*)obj;
+  if (r->ctx) vmqg_destroy(r->ctx);
+  vmqgb_interner_free(r->mps); vmqgb_interner_free(r->nodes);
+  vmqgb_interner_free(r->subs); vmqgb_interner_free(r->infos);
+  term_store* ts[4] = {&r->node_t, &r->sub_t, &r->info_t, &r->group_t};
+  for (int i = 0; i < 4; i++) { if (ts[i]->env) enif_free_env(ts[i]->env); enif_free(ts[i]->terms); }
+  vmqgb_batch_free(&r->batch);
+  vmqgb_ops_free(&r->ops);
+  if (r->lock) enif_mutex_destroy(r->lock);
+}
+
+static vmqg_res* get_res(ErlNifEnv* env, ERL_NIF_TERM t) {
+  vmqg_res* r = NULL;
+  return enif_get_resource(env, t, RES, (void**)&r) ? r : NULL;
+}
+
+/* ------------------------------------------------------------- create/1 */
+/* create(#{device => D, local_node => node()}) -> {ok, Ctx} | {error, _}
+ * (vmq_reg_trie:init/1, vmq_reg_trie.erl:135-151) */
+static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  ERL_NIF_TERM v;
+  int device = 0;
+  if (enif_get_map_value(env, argv[0], enif_make_atom(env, "device"), &v)) enif_get_int(env, v, &device);
+  ERL_NIF_TERM local;
+  if (!enif_get_map_value(env, argv[0], enif_make_atom(env, "local_node"), &local)) return enif_make_badarg(env);
+  vmqg_res* r = (vmqg_res*)enif_alloc_resource(RES, sizeof(vmqg_res));
+  memset(r, 0, sizeof(*r));
+  r->lock = enif_mutex_create("vmqg_res");
+  r->mps = vmqgb_interner_new(); r->nodes = vmqgb_interner_new();
+  r->subs = vmqgb_interner_new(); r->infos = vmqgb_interner_new();
+  r->node_t.env = enif_alloc_env(); r->sub_t.env = enif_alloc_env();
+  r->info_t.env = enif_alloc_env(); r->group_t.env = enif_alloc_env();
+  vmqgb_batch_init(&r->batch, 4096);
+  vmqgb_ops_init(&r->ops);
+  r->max_mountpoints = 1024;
+  uint32_t id;
+  term_id(r->mps, NULL, env, enif_make_string(env, "", ERL_NIF_LATIN1), &id);   /* "" is mountpoint 0 */
+  term_id(r->nodes, &r->node_t, env, local, &id);                               /* node() is node 0 */
+  vmqg_config cfg;
+  memset(&cfg, 0, sizeof cfg);
+  cfg.device = device;
+  cfg.local_node = 0;
+  cfg.max_nodes = VMQG_MAX_NODES;
+  cfg.max_mountpoints = r->max_mountpoints;
+  int err = 0;
+  r->ctx = vmqg_create(&cfg, &err);
+  ERL_NIF_TERM ret = r->ctx ? enif_make_tuple2(env, a_ok, enif_make_resource(env, r)) : error_term(env, err);
+  enif_release_resource(r);
+  return ret;
+}
+
+/* ------------------------------------------------------------------ ops */
+/* One {Kind, Topic, SubInfo, Node} change of SubscriberId into r->ops. */
+static int add_change(ErlNifEnv* env, vmqg_res* r, uint32_t kind, ERL_NIF_TERM sid, ERL_NIF_TERM topic,
+                      ERL_NIF_TERM subinfo, ERL_NIF_TERM node) {
+  int arity;
+  const ERL_NIF_TERM* sid_el;
+  if (!enif_get_tuple(env, sid, &arity, &sid_el) || arity != 2) return VMQG_E_INVAL;
+  uint32_t mp, sub, info, nd;
+  if (!term_id(r->mps, NULL, env, sid_el[0], &mp) || mp >= r->max_mountpoints) return VMQG_E_LIMIT;
+  if (!term_id(r->subs, &r->sub_t, env, sid, &sub) || !term_id(r->infos, &r->info_t, env, subinfo, &info) ||
+      !term_id(r->nodes, &r->node_t, env, node, &nd))
+    return VMQG_E_NOMEM;
+  unsigned len;
+  if (!enif_get_list_length(env, topic, &len) || len == 0 || len > 65536) return VMQG_E_INVAL;
+  const uint8_t* wp[len];
+  size_t wl[len];
+  ERL_NIF_TERM group = 0, head, tail = topic;
+  for (unsigned i = 0; i < len; i++) {
+    ErlNifBinary b;
+    enif_get_list_cell(env, tail, &head, &tail);
+    if (!enif_inspect_binary(env, head, &b)) return VMQG_E_INVAL;
+    wp[i] = b.data;
+    wl[i] = b.size;
+    if (i == 1) group = head;
+  }
+  const size_t w0 = r->ops.nwords;
+  const int rc = vmqgb_ops_add(&r->ops, r->ctx, kind, mp, wp, wl, len, nd, sub, info);
+  if (rc) return rc;
+  /* $share/Group/...: remember the group binary under its word id (decoding kind-B entries) */
+  if (len >= 3 && r->ops.words[w0] == VMQG_WORD_SHARE) store_put(&r->group_t, r->ops.words[w0 + 1], group);
+  return 0;
+}
+
+/* apply(Ctx, SubscriberId, [{add | del, Topic, SubInfo, Node}]) -> ok | {error, _}
+ * (handle_event/2, vmq_reg_trie.erl:240-277) */
+static ERL_NIF_TERM nif_apply(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  if (!r) return enif_make_badarg(env);
+  enif_mutex_lock(r->lock);
+  vmqgb_ops_reset(&r->ops);
+  ERL_NIF_TERM head, tail = argv[2];
+  int rc = 0;
+  while (!rc && enif_get_list_cell(env, tail, &head, &tail)) {
+    int arity;
+    const ERL_NIF_TERM* el;
+    if (!enif_get_tuple(env, head, &arity, &el) || arity != 4) { rc = VMQG_E_INVAL; break; }
+    const uint32_t kind = enif_is_identical(el[0], enif_make_atom(env, "add")) ? VMQG_OP_ADD : VMQG_OP_DEL;
+    rc = add_change(env, r, kind, argv[1], el[1], el[2], el[3]);
+  }
+  if (!rc) rc = vmqgb_ops_apply(&r->ops, r->ctx, NULL);
+  enif_mutex_unlock(r->lock);
+  return rc ? error_term(env, rc) : a_ok;
+}
+
+/* add_init(Ctx, MP, Topic, SubscriberId, SubInfo, Node) -> ok: one
+ * initialize_trie/2 tuple (vmq_reg_trie.erl:305-316), applied in batches */
+static ERL_NIF_TERM nif_add_init(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  if (!r) return enif_make_badarg(env);
+  enif_mutex_lock(r->lock);
+  int rc = add_change(env, r, VMQG_OP_ADD, argv[3], argv[2], argv[4], argv[5]);
+  if (!rc && r->ops.n >= 65536) rc = vmqgb_ops_apply(&r->ops, r->ctx, NULL);
+  enif_mutex_unlock(r->lock);
+  return rc ? error_term(env, rc) : a_ok;
+}
+
+static ERL_NIF_TERM nif_flush_init(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  if (!r) return enif_make_badarg(env);
+  enif_mutex_lock(r->lock);
+  const int rc = r->ops.n ? vmqgb_ops_apply(&r->ops, r->ctx, NULL) : 0;
+  enif_mutex_unlock(r->lock);
+  return rc ? error_term(env, rc) : a_ok;
+}
+
+/* ---------------------------------------------------------------- match */
+typedef struct {
+  ErlNifEnv* env;
+  vmqg_res* r;
+  ERL_NIF_TERM* out;
+  size_t n;
+} fold_acc;
+
+/* FoldFun argument term of one entry (vmq_reg_trie.erl:68-98) */
+static int make_entry(void* accp, const vmqgb_entry* e) {
+  fold_acc* acc = (fold_acc*)accp;
+  vmqg_res* r = acc->r;
+  ErlNifEnv* env = acc->env;
+  ERL_NIF_TERM t;
+  if (e->kind == VMQG_EMIT_LOCAL) {          /* {SubscriberId, SubInfo} */
+    t = enif_make_tuple2(env, enif_make_copy(env, r->sub_t.terms[e->subscriber]),
+                         enif_make_copy(env, r->info_t.terms[e->subinfo]));
+  } else if (e->kind == VMQG_EMIT_GROUP) {   /* {Node, Group, SubscriberId, SubInfo} */
+    t = enif_make_tuple4(env, enif_make_copy(env, r->node_t.terms[e->node]),
+                         enif_make_copy(env, r->group_t.terms[e->group]),
+                         enif_make_copy(env, r->sub_t.terms[e->subscriber]),
+                         enif_make_copy(env, r->info_t.terms[e->subinfo]));
+  } else {                                   /* Node */
+    t = enif_make_copy(env, r->node_t.terms[e->node]);
+  }
+  acc->out[acc->n++] = t;
+  return 0;
+}
+
+/* match(Ctx, [{MP, TopicBin}], records | ranges) -> [{ok, Entries} | {error, Reason}]
+ * (fold/4 for a batch of callers, vmq_reg_trie.erl:59-98); dirty CPU */
+static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  unsigned n;
+  if (!r || !enif_get_list_length(env, argv[1], &n)) return enif_make_badarg(env);
+  const int ranges = enif_is_identical(argv[2], a_ranges);
+  enif_mutex_lock(r->lock);
+  vmqgb_batch* b = &r->batch;
+  vmqgb_batch_reset(b);
+  long* idx = (long*)enif_alloc((n ? n : 1) * sizeof(long));
+  ERL_NIF_TERM head, tail = argv[1];
+  for (unsigned i = 0; i < n; i++) {
+    int arity;
+    const ERL_NIF_TERM* el;
+    ErlNifBinary topic;
+    uint32_t mp;
+    enif_get_list_cell(env, tail, &head, &tail);
+    if (!enif_get_tuple(env, head, &arity, &el) || arity != 2 || !enif_inspect_iolist_as_binary(env, el[1], &topic)) {
+      idx[i] = VMQG_E_INVAL;
+      continue;
+    }
+    ErlNifBinary mpb;
+    if (!enif_term_to_binary(env, el[0], &mpb)) { idx[i] = VMQG_E_NOMEM; continue; }
+    const int known = vmqgb_lookup(r->mps, mpb.data, mpb.size, &mp) == 0;
+    enif_release_binary(&mpb);
+    /* an unknown mountpoint has no subscriptions: an id past every root matches nothing */
+    idx[i] = vmqgb_batch_add(b, r->ctx, known ? mp : r->max_mountpoints, topic.data, topic.size);
+  }
+  int rc = b->n ? (ranges ? vmqgb_match_ranges(b, r->ctx) : vmqgb_match(b, r->ctx)) : 0;
+  const vmqg_emit* recs = NULL;
+  uint64_t nrecs = 0;
+  if (!rc && ranges) rc = vmqg_records(r->ctx, &recs, &nrecs);
+  ERL_NIF_TERM* res = (ERL_NIF_TERM*)enif_alloc((n ? n : 1) * sizeof(ERL_NIF_TERM));
+  for (unsigned i = 0; i < n; i++) {
+    if (idx[i] < 0 || rc) { res[i] = error_term(env, idx[i] < 0 ? (int)idx[i] : rc); continue; }
+    size_t cnt = 0;
+    if (ranges) {
+      for (uint64_t k = b->offsets[idx[i]]; k < b->offsets[idx[i] + 1]; k++) cnt += b->rng[k].count ? b->rng[k].count : 1;
+    } else {
+      cnt = vmqgb_count_of(b, (size_t)idx[i]);
+    }
+    fold_acc acc = {env, r, (ERL_NIF_TERM*)enif_alloc((cnt ? cnt : 1) * sizeof(ERL_NIF_TERM)), 0};
+    if (ranges) vmqgb_fold_ranges(b, recs, nrecs, (size_t)idx[i], make_entry, &acc);
+    else vmqgb_fold(b, (size_t)idx[i], make_entry, &acc);
+    res[i] = enif_make_tuple2(env, a_ok, enif_make_list_from_array(env, acc.out, (unsigned)acc.n));
+    enif_free(acc.out);
+  }
+  enif_mutex_unlock(r->lock);
+  ERL_NIF_TERM list = enif_make_list_from_array(env, res, n);
+  enif_free(res);
+  enif_free(idx);
+  return list;
+}
+
+/* stats(Ctx) -> {NrOfSubs + NrOfRemoteSubs, DeviceBytes} (vmq_reg_trie.erl:101-112) */
+static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  if (!r) return enif_make_badarg(env);
+  vmqg_stats_t st;
+  enif_mutex_lock(r->lock);
+  const int rc = vmqg_stats(r->ctx, &st);
+  enif_mutex_unlock(r->lock);
+  if (rc) return error_term(env, rc);
+  return enif_make_tuple2(env, enif_make_uint64(env, st.subs), enif_make_uint64(env, st.device_bytes));
+}
+
+static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
+  (void)priv; (void)info;
+  RES = enif_open_resource_type(env, NULL, "vmqg_ctx", res_dtor, ERL_NIF_RT_CREATE, NULL);
+  a_ok = enif_make_atom(env, "ok");
+  a_error = enif_make_atom(env, "error");
+  a_invalid_topic = enif_make_atom(env, "invalid_topic");
+  a_device = enif_make_atom(env, "device");
+  a_nomem = enif_make_atom(env, "nomem");
+  a_badarg = enif_make_atom(env, "badarg");
+  a_records = enif_make_atom(env, "records");
+  a_ranges = enif_make_atom(env, "ranges");
+  return RES ? 0 : 1;
+}
+
+static ErlNifFunc funcs[] = {
+    {"create", 1, nif_create, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"apply", 3, nif_apply, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"add_init", 6, nif_add_init, 0},
+    {"flush_init", 1, nif_flush_init, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"match", 3, nif_match, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"stats", 1, nif_stats, 0},
+};
+
+ERL_NIF_INIT(vmqg_nif, funcs, load, NULL, NULL, NULL)

@@ -1,0 +1,173 @@
+%% vmq_reg_gpu_view — a vmq_reg_view backed by libvmqgpu (MI355X).
+%%
+%% Drop-in for vmq_reg_trie (apps/vmq_server/src/vmq_reg_trie.erl): same
+%% exports for the view behaviour (vmq_reg_view.erl:20-27) and the registry
+%% supervisor (vmq_reg_sup.erl:86-87, 128-129), same event source
+%% (vmq_reg:subscribe_subscriber_changes/0, vmq_reg.erl:618-619), same
+%% initial fold (vmq_reg:fold_subscriptions/2, vmq_reg_trie.erl:145-149) and
+%% the same event replay after `subscribers_loaded` (:198-205).
+%%
+%% What changes is where fold/4 is answered.  vmq_reg_trie walks ETS in the
+%% caller's process; here concurrent callers are collected into one batch
+%% and matched by one NIF call on a dirty scheduler (vmqg_nif:match/3), and
+%% each caller then runs its FoldFun over its own entries in its own
+%% process — FoldFun has side effects (vmq_queue:enqueue, cluster forward,
+%% vmq_reg.erl:327-353) and is called exactly as vmq_reg_trie calls it,
+%% FoldFun(Entry, SubscriberId, Acc) (vmq_reg_trie.erl:83, 97).  A caller
+%% blocks on its own call, so the order of one publisher's publishes is kept
+%% (vmq_in_order_delivery_SUITE).
+%%
+%% Install: reg_views = [vmq_reg_trie, vmq_reg_gpu_view] (shadow) or
+%% default_reg_view = vmq_reg_gpu_view (vmq_server.schema:115-137).  The NIF
+%% (c_src/vmqg_nif.c) and priv/libvmqgpu.so come from this repository.
+%%
+%% Not compiled in this repository's image (no OTP); its C core
+%% (c_src/vmqg_batch.c) is compiled and tested (tests/test_nif_layer.py,
+%% tools/nif_harness.c).
+-module(vmq_reg_gpu_view).
+-behaviour(gen_server).
+-behaviour(vmq_reg_view).
+
+-export([start_link/0,
+         fold/4,
+         stats/0]).
+
+%% gen_server callbacks
+-export([init/1,
+         handle_call/3,
+         handle_cast/2,
+         handle_info/2,
+         terminate/2,
+         code_change/3]).
+
+-define(SERVER, ?MODULE).
+%% a batch goes to the GPU when it holds this many publishes, or when the
+%% server's mailbox has no more fold requests queued behind it
+-define(MAX_BATCH, 4096).
+
+-record(state, {ctx,                    % vmqg_nif resource (vmqg_ctx + term tables)
+                event_handler,
+                status=init,
+                event_queue=queue:new(),
+                pending=[],             % [{From, MP, TopicBin}], newest first
+                npending=0}).
+
+%%%===================================================================
+%%% API
+%%%===================================================================
+start_link() ->
+    gen_server:start_link({local, ?SERVER}, ?MODULE, [], []).
+
+%% vmq_reg_view callback (vmq_reg_view.erl:20-25; called by vmq_reg:publish/5,
+%% vmq_reg.erl:260, and vmq_cluster_com:process/2, vmq_cluster_com.erl:156).
+fold({MP, _} = SubscriberId, Topic, FoldFun, Acc) when is_list(Topic) ->
+    TopicBin = iolist_to_binary(lists:join(<<"/">>, Topic)),
+    case gen_server:call(?SERVER, {match, MP, TopicBin}, infinity) of
+        {ok, Entries} ->
+            lists:foldl(fun(Entry, AccAcc) -> FoldFun(Entry, SubscriberId, AccAcc) end,
+                        Acc, Entries);
+        {error, Reason} ->
+            error({vmq_reg_gpu_view, Reason})
+    end.
+
+%% stats/0 as vmq_reg_trie:stats/0 (vmq_reg_trie.erl:101-112):
+%% {NrOfSubs + NrOfRemoteSubs, Memory}, memory being the device arena.
+stats() ->
+    case persistent_term:get({?MODULE, ctx}, undefined) of
+        undefined -> {0, 0};
+        Ctx -> vmqg_nif:stats(Ctx)
+    end.
+
+%%%===================================================================
+%%% gen_server callbacks
+%%%===================================================================
+init([]) ->
+    Device = application:get_env(vmq_server, gpu_reg_view_device, 0),
+    {ok, Ctx} = vmqg_nif:create(#{device => Device, local_node => node()}),
+    persistent_term:put({?MODULE, ctx}, Ctx),
+    Self = self(),
+    spawn_link(
+      fun() ->
+              %% initialize_trie/2 (vmq_reg_trie.erl:305-316), batched
+              ok = vmq_reg:fold_subscriptions(
+                     fun({MP, Topic, {SubscriberId, SubInfo, Node}}, ok) ->
+                             vmqg_nif:add_init(Ctx, MP, Topic, SubscriberId, SubInfo, Node)
+                     end, ok),
+              ok = vmqg_nif:flush_init(Ctx),
+              Self ! subscribers_loaded
+      end),
+    EventHandler = vmq_reg:subscribe_subscriber_changes(),
+    {ok, #state{ctx=Ctx, event_handler=EventHandler}}.
+
+handle_call({match, MP, TopicBin}, From, #state{pending=P, npending=N} = State) ->
+    State1 = State#state{pending=[{From, MP, TopicBin} | P], npending=N + 1},
+    case N + 1 >= ?MAX_BATCH of
+        true -> {noreply, flush(State1)};
+        false -> {noreply, State1, 0}   % timeout 0: flush once the mailbox is drained
+    end;
+handle_call({event, Event}, _From, State) ->
+    %% used only for testing/microbenchmarking, as vmq_reg_trie.erl:167-170
+    {reply, ok, handle_event(Event, State)};
+handle_call(_Request, _From, State) ->
+    {reply, ok, State}.
+
+handle_cast(_Msg, State) ->
+    {noreply, State}.
+
+handle_info(timeout, State) ->
+    {noreply, flush(State)};
+handle_info(subscribers_loaded, #state{event_queue=Q} = State) ->
+    State1 = lists:foldl(fun handle_event/2, State#state{status=ready}, queue:to_list(Q)),
+    {Subs, _} = stats(),
+    lager:info("loaded ~p subscriptions into ~p", [Subs, ?MODULE]),
+    {noreply, State1#state{event_queue=undefined}};
+handle_info(Event, #state{status=init, event_queue=Q} = State) ->
+    {noreply, State#state{event_queue=queue:in(Event, Q)}};
+handle_info(Event, State) ->
+    {noreply, handle_event(Event, State)}.
+
+terminate(_Reason, _State) ->
+    persistent_term:erase({?MODULE, ctx}),
+    ok.
+
+code_change(_OldVsn, State, _Extra) ->
+    {ok, State}.
+
+%%%===================================================================
+%%% Internal functions
+%%%===================================================================
+
+%% One NIF call for every queued fold request (dirty CPU scheduler: topic
+%% splitting + interning, the GPU match, term construction), then one reply
+%% per caller.  Publishes the reference rejects are rejected per caller.
+flush(#state{pending=[]} = State) ->
+    State;
+flush(#state{ctx=Ctx, pending=P} = State) ->
+    Batch = lists:reverse(P),
+    Results = vmqg_nif:match(Ctx, [{MP, T} || {_, MP, T} <- Batch], records),
+    lists:foreach(fun({{From, _, _}, Res}) -> gen_server:reply(From, Res) end,
+                  lists:zip(Batch, Results)),
+    State#state{pending=[], npending=0}.
+
+%% handle_event/2 (vmq_reg_trie.erl:240-251): the same diff, the same order
+%% (deletes, then adds); the NIF turns the changes into one vmqg_apply_ops.
+handle_event(Event, #state{ctx=Ctx, event_handler=Handler} = State) ->
+    case Handler(Event) of
+        {delete, SubscriberId, Subscriptions} ->
+            Removed = vmq_subscriber:get_changes(Subscriptions),
+            ok = vmqg_nif:apply(Ctx, SubscriberId, changes(del, Removed));
+        {update, SubscriberId, OldValue, NewValue} ->
+            {ToRemove, ToAdd} = vmq_subscriber:get_changes(OldValue, NewValue),
+            ok = vmqg_nif:apply(Ctx, SubscriberId, changes(del, ToRemove) ++ changes(add, ToAdd));
+        ignore ->
+            ok
+    end,
+    State.
+
+%% [{Node, [{Topic, SubInfo}]}] (vmq_subscriber:get_changes/1,2) in the
+%% order vmq_subscriber:fold/3 (vmq_subscriber.erl:184-196) visits it ->
+%% [{Kind, Topic, SubInfo, Node}]
+changes(Kind, Changes) ->
+    lists:reverse(
+      vmq_subscriber:fold(fun({Topic, SubInfo, Node}, Acc) -> [{Kind, Topic, SubInfo, Node} | Acc] end,
+                          [], Changes)).

@@ -1,0 +1,23 @@
+%% vmqg_nif — NIF stubs of c_src/vmqg_nif.c (libvmqgpu behind vmq_reg_gpu_view).
+-module(vmqg_nif).
+-export([create/1, apply/3, add_init/6, flush_init/1, match/3, stats/1]).
+-on_load(init/0).
+
+init() ->
+    Priv = case code:priv_dir(vmq_server) of
+               {error, _} -> "priv";
+               Dir -> Dir
+           end,
+    erlang:load_nif(filename:join(Priv, "vmqg_nif"), 0).
+
+%% #{device => integer(), local_node => node()} -> {ok, Ctx} | {error, term()}
+create(_Opts) -> erlang:nif_error(nif_not_loaded).
+%% Ctx, SubscriberId, [{add | del, Topic, SubInfo, Node}] -> ok | {error, term()}
+apply(_Ctx, _SubscriberId, _Changes) -> erlang:nif_error(nif_not_loaded).
+%% Ctx, MP, Topic, SubscriberId, SubInfo, Node -> ok | {error, term()}
+add_init(_Ctx, _MP, _Topic, _SubscriberId, _SubInfo, _Node) -> erlang:nif_error(nif_not_loaded).
+flush_init(_Ctx) -> erlang:nif_error(nif_not_loaded).
+%% Ctx, [{MP, TopicBin}], records | ranges -> [{ok, [Entry]} | {error, term()}]
+match(_Ctx, _Publishes, _Mode) -> erlang:nif_error(nif_not_loaded).
+%% Ctx -> {NrOfSubs, DeviceBytes}
+stats(_Ctx) -> erlang:nif_error(nif_not_loaded).

@@ -138,7 +138,7 @@ def _gpu_worker(rank, world, port, out_dir, seed):
         else:
             hdr = torch.zeros(2, dtype=torch.int64)
         dist.broadcast(hdr, 0)
-        a_t = torch.from_numpy(arr.view(np.uint32).copy()) if rank == 0 else \
+        a_t = torch.from_numpy(arr.view(np.uint32).view(np.int32).copy()) if rank == 0 else \
             torch.zeros(int(hdr[0]) * 4, dtype=torch.int32)
         w_t = torch.from_numpy(words.astype(np.int32)) if rank == 0 else torch.zeros(int(hdr[1]), dtype=torch.int32)
         dist.broadcast(a_t, 0)
