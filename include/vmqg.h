@@ -134,6 +134,7 @@ typedef struct vmqg_stats_s {
   uint64_t ops_applied;     /* vmqg_apply_ops: ops applied so far               */
   uint64_t apply_host_ns;   /*   host time inside vmqg_apply_ops (never waits on */
                             /*   queued matches)                                 */
+  uint64_t apply_upload_ns; /*   of which staging + enqueueing the patches       */
   uint64_t patch_bytes;     /*   patch bytes shipped to the device               */
   uint64_t image_bytes;     /*   full-image bytes shipped (re-layouts)           */
   uint64_t max_depth;       /* deepest trie path (levels)                       */
@@ -252,7 +253,8 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "fast_g"    2 | 4      lanes per publish in the fast tier (default 2)
  *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
  *   "emit_lean" 0 | 1      records EMIT without walk code, one publish per lane
- *                          (multi-key publishes go to the wave tier); default 0 */
+ *                          (multi-key publishes go to the wave tier); default 0
+ *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the dominant match kernel over the last

@@ -225,6 +225,7 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->deferred_tier2 = e.last_deferred[1];
   out->ops_applied = e.ops_applied;
   out->apply_host_ns = e.apply_host_ns;
+  out->apply_upload_ns = e.apply_upload_ns;
   out->patch_bytes = e.patch_bytes;
   out->image_bytes = e.image_bytes;
   out->max_depth = e.stack_depth();
@@ -251,6 +252,9 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
     e.opt_fast_g = (uint32_t)value;
   } else if (n == "nt_stores") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptNtStores) : (e.opt_flags & ~vmqg::kOptNtStores);
+  } else if (n == "count_bpc" || n == "emit_bpc") {
+    if (value < 0 || value > 32) return VMQG_E_INVAL;
+    (n == "count_bpc" ? e.opt_count_bpc : e.opt_emit_bpc) = (uint32_t)value;
   } else if (n == "emit_lean") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptLeanEmit) : (e.opt_flags & ~vmqg::kOptLeanEmit);
   } else {

@@ -290,11 +290,13 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) c
   L.edge_buckets = edge_slots / kEdgeSlotsPerBucket;
   L.node_cap = std::max<uint64_t>({4096, paths.size() + paths.size() / 2, cfg.hint_paths + cfg.max_mountpoints});
   L.key_cap = std::max<uint64_t>({4096, keys.size() + keys.size() / 2, cfg.hint_keys});
-  L.keylist_cap = std::max<uint64_t>(4096, kl * 2);
+  // keylists (multi-key filters, remote nodes >= 64) and exact-topic words:
+  // sized from the hints too, so a bulk load does not re-lay the arena out
+  L.keylist_cap = std::max<uint64_t>({4096, kl * 2, cfg.hint_keys / 16});
   L.rec_cap = std::max<uint64_t>({16384, recs * 2, cfg.hint_records * 2});
   const uint64_t exact_slots = next_pow2(std::max<uint64_t>(4096, std::max<uint64_t>(ex * 2 + 1024, cfg.hint_exact * 2)));
   L.exact_buckets = exact_slots / kExactSlotsPerBucket;
-  L.exwords_cap = std::max<uint64_t>(16384, xw * 2);
+  L.exwords_cap = std::max<uint64_t>({16384, xw * 2, cfg.hint_exact * 8});
   uint64_t o = 0;
   if (!compact && lay.total_bytes) {   // a growth re-layout never shrinks a region
     L.edge_buckets = std::max<uint64_t>(L.edge_buckets, lay.edge_buckets);
@@ -818,9 +820,11 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
   lay.max_depth = max_depth;   // replicas size their stacks from the layout
   epoch++;
   ops_applied += n;
+  const auto t1 = std::chrono::steady_clock::now();
   const int rc = upload();
-  apply_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                       std::chrono::steady_clock::now() - t0).count();
+  const auto t2 = std::chrono::steady_clock::now();
+  apply_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t0).count();
+  apply_upload_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
   return rc;
 }
 
@@ -976,6 +980,8 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.err = d_status + 8;
   a.deferred = d_deferred;
   a.fast_g = opt_fast_g; a.opts = opt_flags;
+  a.count_bpc = opt_count_bpc; a.emit_bpc = opt_emit_bpc;
+  a.cus = (uint32_t)cu_count;
   a.lookback = d_lookback; a.lb_tag = lb_tag;
   a.o_stack = d_ostack; a.o_cap = o_cap; a.o_waves = o_waves;
   return a;

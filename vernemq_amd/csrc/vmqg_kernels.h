@@ -28,6 +28,8 @@ struct MatchArgs {
   uint32_t* err;                                  // error bits, sticky until vmqg_match_status
   uint32_t* deferred;                             // 2 x npub: publishes deferred by COUNT, then by EMIT
   uint32_t fast_g, opts;                          // tuning: lanes per publish (2|4), kOpt* bits
+  uint32_t count_bpc, emit_bpc;                   // tuning: fast-tier grid cap in blocks per CU (0 = 8)
+  uint32_t cus, pad2;                             // compute units of the device
   uint64_t* lookback;                             // per scan tile: {tag, flag, value} granule
   uint32_t lb_tag, pad1;                          // this call's granule tag (never 0)
   uint2* o_stack;                                 // wave tier: global frontier stacks, o_cap entries per wave

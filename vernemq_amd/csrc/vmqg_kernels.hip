@@ -1005,7 +1005,9 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) 
   if (tier == 0) {
     const uint32_t G = a.fast_g == 4 ? 4 : 2;
     uint32_t g = div_up(a.npub, kWaves * (64 / G));
-    const uint32_t cap = 256u * 8u;   // grid-stride beyond 8 blocks per CU
+    // grid-stride beyond bpc blocks per CU (option count_bpc / emit_bpc; 8 default)
+    const uint32_t bpc = mode == 0 ? a.count_bpc : a.emit_bpc;
+    const uint32_t cap = (uint32_t)a.cus * (bpc ? bpc : 8u);
     if (g > cap) g = cap;
     if (g < 1) g = 1;
     if (mode == 0) { if (out) launch_fast<0, 1>(a, g, nt, st); else launch_fast<0, 0>(a, g, nt, st); }

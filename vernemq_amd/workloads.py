@@ -67,6 +67,7 @@ class Workload:
         self.tw_off = self.tw = None
         self.pub_words: list = []
         self.pub_mp = self.pw_off = self.pw = None
+        self.client_mp = None             # lean workloads: MP index per client (clients is None)
         self.notes = {}
 
     # ------------------------------------------------------------ helpers
@@ -92,16 +93,28 @@ class Workload:
     # ------------------------------------------------------------ product
     def bind(self, view):
         """Intern this workload's terms in `view`; returns the id maps
-        (word, node, mountpoint-of-client, subscriber, subinfo)."""
+        (word, node, mountpoint-of-client, subscriber, subinfo).  A lean
+        workload (clients is None: tens of millions of subscribers) uses
+        the client index itself as the opaque SubscriberId id and never
+        materialises the terms (its records are decoded with client_term)."""
         from .reg_view import _subinfo_key
         wid = view.intern_words(self.words, create=True).astype(np.uint32)
         node_id = np.array([view.nodes.get(n) for n in self.nodes], dtype=np.uint32)
         mp_id = np.array([view.mountpoints.get(m) for m in self.mps], dtype=np.uint32)
-        sid_id = np.array([view.subscribers.get(c) for c in self.clients], dtype=np.uint32)
         si_id = np.array([view.subinfos.get(s, _subinfo_key(s)) for s in self.subinfos], dtype=np.uint32)
+        if self.clients is None:
+            return {"wid": wid, "node": node_id, "client_mp": mp_id[self.client_mp],
+                    "sid": np.arange(len(self.client_mp), dtype=np.uint32), "si": si_id}
+        sid_id = np.array([view.subscribers.get(c) for c in self.clients], dtype=np.uint32)
         mp_index = {m: i for i, m in enumerate(self.mps)}
         client_mp = np.array([mp_index[c[0]] for c in self.clients], dtype=np.int64)
         return {"wid": wid, "node": node_id, "client_mp": mp_id[client_mp], "sid": sid_id, "si": si_id}
+
+    def client_term(self, i: int):
+        """SubscriberId term of client i (lean workloads: from client_mp)."""
+        if self.clients is not None:
+            return self.clients[i]
+        return (self.mps[int(self.client_mp[i])], b"c%d" % i)
 
     def op_arrays(self, ids, idx: np.ndarray, kind: int):
         """OP_DTYPE + word-id arrays for subscriptions `idx` (one op each)."""
@@ -518,12 +531,14 @@ def _zipf_cdf(n: int, s: float) -> np.ndarray:
 
 
 def config_e(scale: float = 1.0, seed: int = 0xE, n_pubs: int = 1 << 20, n_mps: int = 1000,
-             levels: int = 12, vocab: int = 64, n_hot: int = 1_000_000) -> Workload:
+             levels: int = 12, vocab: int = 64, n_hot: int = 1_000_000, lean: bool | None = None) -> Workload:
     """Config E (§8d) at `scale` (1.0 = 50M subscriptions): `n_mps`
     mountpoints t{n} with Zipf(1.0) sizes; topics of `levels` words from
     `vocab` words per level; 80 % exact, 15 % with 1-3 '+', 5 % truncated +
     '#'.  Publishes: Zipf(1.1) over `n_hot` hot topics (half instantiate a
-    random filter, half random), each in its filter's / a size-weighted MP."""
+    random filter, half random), each in its filter's / a size-weighted MP.
+    lean (default above 5M subscriptions): no per-client Python terms (see
+    Workload.bind), 16-bit word indexes."""
     r = SplitMix(seed)
     w = Workload("E")
     n = max(1000, int(50_000_000 * scale))
@@ -534,7 +549,9 @@ def config_e(scale: float = 1.0, seed: int = 0xE, n_pubs: int = 1 << 20, n_mps: 
     lvl = [[b"l%d_%d" % (k, j) for j in range(vocab)] for k in range(levels)]
     w.words = [b"+", b"#"] + [x for lv in lvl for x in lv]
     base = lambda k: 2 + k * vocab
-    T = np.empty((n, levels), dtype=np.int64)
+    if lean is None:
+        lean = n > 5_000_000
+    T = np.empty((n, levels), dtype=np.int16 if lean else np.int64)
     for k in range(levels):
         T[:, k] = base(k) + r.ints(n, vocab)
     u = r.unif(n)
@@ -555,7 +572,11 @@ def config_e(scale: float = 1.0, seed: int = 0xE, n_pubs: int = 1 << 20, n_mps: 
     w.subinfos = std_subinfos()
     w.sub_info = r.ints(n, len(w.subinfos))
     w.sub_node = np.zeros(n, dtype=np.int64)
-    w.clients = [(w.mps[m], b"c%d" % i) for i, m in enumerate(sub_mp)]
+    if lean:
+        w.clients = None
+        w.client_mp = sub_mp.astype(np.int32)
+    else:
+        w.clients = [(w.mps[m], b"c%d" % i) for i, m in enumerate(sub_mp)]
     w.sub_client = np.arange(n, dtype=np.int64)
     # hot topics: half instantiate a filter (same MP), half random (size-weighted MP)
     src = r.ints(n_hot, n)
