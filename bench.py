@@ -405,6 +405,7 @@ def bench_other(args):
     torch.cuda.set_device(0)
     t0 = time.time()
     if args.config == "E":
+        log("config E: generating %.0fM subscriptions" % (50 * args.e_scale))
         w = W.config_e(scale=args.e_scale, n_pubs=args.batch)
     elif args.config in ("R1", "R2"):
         w = W.CONFIGS[args.config](args.r_n)
@@ -416,7 +417,14 @@ def bench_other(args):
     view = RegGpuView(node=w.self_node, device=0, nodes=w.nodes, max_mountpoints=max(1024, len(w.mps) + 1),
                       hints=hints)
     t0 = time.time()
-    w.load_into(view)
+    last = [t0]
+
+    def progress(done, total):
+        if time.time() - last[0] > 20:
+            last[0] = time.time()
+            log("config %s: %d / %d subscriptions loaded (%.0fs)" % (args.config, done, total, time.time() - t0))
+
+    w.load_into(view, progress=progress)
     load_s = time.time() - t0
     st = view.stats_raw()
     log("config %s: %d subs generated in %.1fs, loaded in %.1fs (host engine %.1fs), %s"
@@ -754,7 +762,8 @@ def bench_d(args):
 
     if rank == 0:
         ops_n = st1["ops_applied"] - st0["ops_applied"]
-        host_ns = st1["apply_host_ns"] - st0["apply_host_ns"]
+        wait_ns = st1["apply_wait_ns"] - st0["apply_wait_ns"]
+        host_ns = st1["apply_host_ns"] - st0["apply_host_ns"] - wait_ns   # host work, without GPU back-pressure
         # dominant kernel: EMIT.  Its compulsory HBM bytes are at least the
         # 16 B written per emission (the records read are the 16 MB of $share
         # member lists and the exact keys' records, largely cache-resident);
@@ -776,7 +785,9 @@ def bench_d(args):
             "deltas_per_s": args.churn_batch * args.steps / t_max,
             "delta_apply": {"host_ops_per_s": ops_n / (host_ns / 1e9) if host_ns else None,
                             "host_ms_per_batch": host_ns / 1e6 / args.steps,
-                            "enqueue_ms_per_batch": (st1["apply_upload_ns"] - st0["apply_upload_ns"]) / 1e6 / args.steps,
+                            "enqueue_ms_per_batch": (st1["apply_upload_ns"] - st0["apply_upload_ns"] - wait_ns)
+                                                    / 1e6 / args.steps,
+                            "backpressure_ms_per_batch": wait_ns / 1e6 / args.steps,
                             "caller_ms_per_batch": acc["apply"] * 1e3 / args.steps,
                             "patch_bytes_per_batch": (st1["patch_bytes"] - st0["patch_bytes"]) / args.steps,
                             "full_images": int(st1["image_bytes"] > st0["image_bytes"]),
@@ -1115,6 +1126,8 @@ def bench_shared(args):
                      "frac": achieved / PEAK_HBM_GBS if achieved else None,
                      "traffic": load_pmc_traffic("k_select_wave", "pmc_ss.json"),
                      "kernel": "k_select_wave + k_select_block",
+                     "note": "byte-bound by HBM in principle (one read of the records); measured at ~36 % of peak "
+                             "it is limited by per-wave latency (load -> LDS claim -> reduction -> write phases)",
                      "algorithmic_bytes_per_launch": alg,
                      "bytes_model": "16-B record read + 1-B chosen written per record, 8-B offset + 4-B failed "
                                     "per publish (queue states are L2-resident)"},

@@ -132,9 +132,10 @@ typedef struct vmqg_stats_s {
   uint64_t deferred_tier1;  /* publishes of the last checked match batch walked */
   uint64_t deferred_tier2;  /* by a whole wave (LDS stack) / with a global stack */
   uint64_t ops_applied;     /* vmqg_apply_ops: ops applied so far               */
-  uint64_t apply_host_ns;   /*   host time inside vmqg_apply_ops (never waits on */
-                            /*   queued matches)                                 */
-  uint64_t apply_upload_ns; /*   of which staging + enqueueing the patches       */
+  uint64_t apply_host_ns;   /*   time inside vmqg_apply_ops, of which:           */
+  uint64_t apply_upload_ns; /*   staging + enqueueing the patches, of which:      */
+  uint64_t apply_wait_ns;   /*   waiting for a staging buffer (back-pressure:     */
+                            /*   the host ran 4 batches ahead of the GPU)        */
   uint64_t patch_bytes;     /*   patch bytes shipped to the device               */
   uint64_t image_bytes;     /*   full-image bytes shipped (re-layouts)           */
   uint64_t max_depth;       /* deepest trie path (levels)                       */
@@ -254,7 +255,8 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
  *   "emit_lean" 0 | 1      records EMIT without walk code, one publish per lane
  *                          (multi-key publishes go to the wave tier); default 0
- *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8) */
+ *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8;
+ *                          defaults 4 and 16) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the dominant match kernel over the last

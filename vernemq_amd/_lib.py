@@ -77,7 +77,7 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("subs", "device_bytes", "trie_edges", "trie_nodes", "trie_topics", "subs_objects",
                  "fanout_objects", "remote_keys", "epoch", "rebuilds", "paths", "words",
-                 "deferred_tier1", "deferred_tier2", "ops_applied", "apply_host_ns", "apply_upload_ns", "patch_bytes",
+                 "deferred_tier1", "deferred_tier2", "ops_applied", "apply_host_ns", "apply_upload_ns", "apply_wait_ns", "patch_bytes",
                  "image_bytes", "max_depth")]
 
 

@@ -226,6 +226,7 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->ops_applied = e.ops_applied;
   out->apply_host_ns = e.apply_host_ns;
   out->apply_upload_ns = e.apply_upload_ns;
+  out->apply_wait_ns = e.apply_wait_ns;
   out->patch_bytes = e.patch_bytes;
   out->image_bytes = e.image_bytes;
   out->max_depth = e.stack_depth();

@@ -883,7 +883,12 @@ int Engine::upload() {
   if (np == 0) return VMQG_OK;
   Stage& sg = stage[stage_next];
   stage_next = (stage_next + 1) % kStage;
-  if (sg.used && hipEventSynchronize(sg.ev) != hipSuccess) return VMQG_E_DEVICE;   // its batch has landed
+  if (sg.used) {   // its batch has landed: waits only when the host runs kStage batches ahead of the GPU
+    const auto w0 = std::chrono::steady_clock::now();
+    if (hipEventSynchronize(sg.ev) != hipSuccess) return VMQG_E_DEVICE;
+    apply_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                         std::chrono::steady_clock::now() - w0).count();
+  }
   if (sg.cap < np) {
     if (sg.h) hipHostFree(sg.h);
     hipFree(sg.d);

@@ -191,7 +191,8 @@ struct Engine {
   std::vector<Patch> last_patches;
   bool last_full = false;
   // apply accounting (vmqg_stats): host work only, separate from device waits
-  uint64_t ops_applied = 0, apply_host_ns = 0, apply_upload_ns = 0, patch_bytes = 0, image_bytes = 0;
+  uint64_t ops_applied = 0, apply_host_ns = 0, apply_upload_ns = 0, apply_wait_ns = 0, patch_bytes = 0,
+           image_bytes = 0;
 
   // ---- device
   int device = -1;
@@ -216,7 +217,7 @@ struct Engine {
   hipEvent_t ev_match_done = nullptr;
   bool timing = false;
   uint32_t opt_fast_g = 2, opt_flags = kOptNtStores;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
-  uint32_t opt_count_bpc = 0, opt_emit_bpc = 0;        // fast-tier grid caps (blocks per CU; 0 = 8)
+  uint32_t opt_count_bpc = 4, opt_emit_bpc = 16;       // fast-tier grid caps, blocks per CU (A/B-tuned)
   // look-back granules (tagged per call), global stack of the tier-2 wave path
   uint64_t* d_lookback = nullptr; uint64_t lookback_cap = 0; uint32_t lb_tag = 0;
   uint2* d_ostack = nullptr; uint64_t ostack_bytes = 0;

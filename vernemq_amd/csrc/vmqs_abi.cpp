@@ -13,6 +13,7 @@ SelEngine::~SelEngine() {
   hipSetDevice(device);
   if (stream) hipStreamSynchronize(stream);
   for (auto& e : t_sel) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
+  if (ev_sel) hipEventDestroy(ev_sel);
   hipFree(d_states); hipFree(d_status); hipFree(d_defer);
   hipFree(d_e); hipFree(d_o); hipFree(d_c); hipFree(d_f);
   if (stream) hipStreamDestroy(stream);
@@ -26,7 +27,9 @@ int SelEngine::init(const vmqs_config& c) {
   if (hipSetDevice(device) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VMQG_E_DEVICE;
   if (hipMalloc(&d_status, 64) != hipSuccess) return VMQG_E_NOMEM;
+  if (hipEventCreateWithFlags(&ev_sel, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
   if (hipMemsetAsync(d_status, 0, 64, stream) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipEventRecord(ev_sel, stream) != hipSuccess) return VMQG_E_DEVICE;
   return hipStreamSynchronize(stream) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
 }
 
@@ -41,6 +44,9 @@ int SelEngine::set_states(const uint32_t* subs, const uint8_t* st, size_t n) {
   if (top > h_states.size()) h_states.resize(top, (uint8_t)VMQS_ONLINE);
   for (size_t i = 0; i < n; i++) h_states[subs[i]] = st[i];
   hipSetDevice(device);
+  // selects still running on any stream read the old table: the copy (and a
+  // free of the old buffer) waits for the last one
+  if (hipStreamWaitEvent(stream, ev_sel, 0) != hipSuccess) return VMQG_E_DEVICE;
   if (top > states_cap) {
     uint64_t c = 4096;
     while (c < top) c <<= 1;
@@ -85,6 +91,7 @@ int SelEngine::select_device(const vmqg_emit* d_emits, const uint64_t* d_offsets
   if (timing) for (auto& x : e) hipEventCreate(&x);
   if (launch_select(a, st, e[0], e[1]) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) t_sel.push_back({e[0], e[1]});
+  if (hipEventRecord(ev_sel, st) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
 

@@ -25,7 +25,11 @@
 // key} (tier 1 keeps local / all pairs, see below).  Tier 1: one wave per publish, 64-slot table and a 4096-bit bitmap
 // of winners in LDS, so every chosen[] byte is written exactly once, in
 // order.  Tier 2 (long segments, many groups): one workgroup per publish.
-// Integer work only, no MFMA; HBM-bound on the 16-B record reads.
+// Integer work only, no MFMA.  The byte bound is one read of the 16-B
+// records (8.27 GB of HBM traffic per launch for 8.05 GB algorithmic on the
+// SS workload), but the kernel runs at ~36 % of the HBM peak: it is
+// latency-bound per wave (load -> LDS claim -> reduction -> bitmap ->
+// write), see DESIGN.md "Shared-subscription dispatch".
 #include <hip/hip_runtime.h>
 
 #include "vmqs_engine.h"

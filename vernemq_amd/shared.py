@@ -78,6 +78,8 @@ class SharedGpu:
         output).  Returns (chosen uint8 per record, failed uint32 per publish)."""
         recs = np.ascontiguousarray(records)
         offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if len(offs) == 0:
+            raise ValueError("offsets must hold npub + 1 entries (got an empty array)")
         npub = len(offs) - 1
         total = int(offs[-1]) if npub >= 0 else 0
         chosen = np.zeros(max(total, 1), dtype=np.uint8)

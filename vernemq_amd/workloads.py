@@ -138,14 +138,17 @@ class Workload:
         words = ids["wid"][self.tw[np.arange(total, dtype=np.int64) + rep]] if total else np.zeros(0, np.uint32)
         return ops, words
 
-    def load_into(self, view, batch: int = 1 << 20, n: int | None = None):
+    def load_into(self, view, batch: int = 1 << 20, n: int | None = None, progress=None):
         """Bulk initialize_trie of subscriptions [0, n) into a RegGpuView (op
-        arrays, no per-subscription Python).  Returns the id maps."""
+        arrays, no per-subscription Python).  Returns the id maps.
+        progress(done, n): called after every batch (long loads log)."""
         ids = self.bind(view)
         n = self.n_subs if n is None else n
         for lo in range(0, n, batch):
             ops, words = self.op_arrays(ids, np.arange(lo, min(n, lo + batch)), _lib.OP_ADD)
             view.apply_op_arrays(ops, words)
+            if progress is not None:
+                progress(min(n, lo + batch), n)
         return ids
 
     def publish_arrays(self, view, lo: int = 0, hi: int | None = None):
