@@ -12,6 +12,7 @@ from vernemq_amd import _lib  # noqa: E402
 
 VARIANTS = {
     "default": [],
+    "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "emit_u2": ["-DVMQG_EMIT_U=2"],
     "emit_u8": ["-DVMQG_EMIT_U=8"],
     "ss_u2": ["-DVMQS_UNROLL=2"],
@@ -22,8 +23,8 @@ VARIANTS = {
 
 def build(name, flags):
     out = os.path.join(ROOT, "build", "ab", "lib_%s.so" % name)
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-value", "-Wno-unused-result"] + flags + ["-o", out] + _lib.SOURCES
+    cmd = ["/opt/rocm/bin/hipcc"] + _lib.FLAGS + flags + ['-DVMQG_BUILD_ID="vmqg-build:%s+%s"' % (_lib.source_id(), name),
+                                                          "-o", out] + _lib.SOURCES
     r = subprocess.run(cmd, capture_output=True, text=True)
     return name, r.returncode, r.stderr[-2000:]
 

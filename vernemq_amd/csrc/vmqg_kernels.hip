@@ -453,7 +453,9 @@ __device__ void count_publish(const MatchArgs& a, uint32_t p, const FastScratch<
 // Per-group result of the resolve step, staged in LDS for the wave copy.
 struct GroupMeta {
   uint32_t rel, span, nk, ksum;      // output start relative to the wave's first publish, length
-  uint32_t rm_lo, rm_hi, ok, crel;   // crel: start among the wave's copied (ok) records
+  uint32_t rm_lo, rm_hi, crel, c0;   // crel: start among the wave's copied records
+  uint32_t off0, off1, pad0, pad1;   // nk <= 2 (key cache): key 0 = [off0, +c0), key 1 = [off1, +ksum-c0)
+  uint4 pre0, pre1;                  // a one-record key's record, loaded during the resolve
 };
 
 // Resolve publish first + gidx of a wave: from the key cache, or by a
@@ -502,10 +504,26 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
   bool ok = false;
   if (valid) ok = resolve<G, 0>(a, p, s, g, nk, ksum, rmask, obase, oend);
   const uint64_t wbase = a.offsets[first];
+  // key-cache groups (<= 2 keys) copy from {off0, c0, off1} directly; the
+  // record of a one-record key (a publish's own exact subscriber, say) is
+  // loaded now, by every group at once, instead of as a lone HBM miss in
+  // the middle of the copy
+  uint32_t off0 = 0, off1 = 0, c0 = 0;
+  uint4 pre = make_uint4(0, 0, 0, 0);
+  if (ok && nk <= 2) {
+    const uint2 k0 = s.ky(0), k1 = s.ky(1);
+    off0 = k0.x;
+    off1 = k1.x;
+    c0 = nk >= 2 ? k1.y : ksum;
+    if (g.lane == 0 && nk >= 1 && c0 == 1) pre = *reinterpret_cast<const uint4*>(a.records + off0);
+    if (g.lane == 1 && nk == 2 && ksum - c0 == 1) pre = *reinterpret_cast<const uint4*>(a.records + off1);
+  }
   if (g.lane == 0)
     gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : 0u, ok ? (uint32_t)(oend - obase) : 0u,
-                           nk == 0 ? 1 : nk, ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), ok ? 1u : 0u, 0u};
+                           nk == 0 ? 1 : nk, ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), 0u, c0,
+                           off0, off1, 0u, 0u, pre, make_uint4(0, 0, 0, 0)};
   wave_sync();
+  if (g.lane == 1) gm[g.gidx].pre1 = pre;
   // compact the copied ranges: crel = exclusive scan of the ok spans
   const uint32_t lane = __lane_id();
   const uint32_t sp = lane < (uint32_t)GPW ? gm[lane].span : 0u;
@@ -525,12 +543,20 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
       w[u] = r < Tok;
       if (w[u]) {
         while (j + 1 < (uint32_t)GPW && gm[j + 1].crel <= r) j++;
-        const GroupMeta m = gm[j];
+        const GroupMeta& m = gm[j];
+        const uint32_t q = r - m.crel;
+        const uint32_t mk = m.nk, ks = m.ksum, mc0 = m.c0;
         const uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
-        FastScratch<G> sj = s;
-        sj.slot = slot0 + j;
-        v[u] = emission(a, [&](uint32_t i) -> uint2 { return sj.ky(i); }, m.nk, m.ksum, rm, r - m.crel);
-        dst[u] = wbase + m.rel + (r - m.crel);
+        if (mk <= 2) {
+          if (q < mc0) v[u] = mc0 == 1 ? m.pre0 : *reinterpret_cast<const uint4*>(a.records + m.off0 + q);
+          else if (q < ks) v[u] = ks - mc0 == 1 ? m.pre1 : *reinterpret_cast<const uint4*>(a.records + m.off1 + (q - mc0));
+          else v[u] = make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rm, q - ks), kNone, kNone, kNone);
+        } else {   // re-walked: keys {off, cum start} in the group's LDS list
+          FastScratch<G> sj = s;
+          sj.slot = slot0 + j;
+          v[u] = emission(a, [&](uint32_t i) -> uint2 { return sj.ky(i); }, mk, ks, rm, q);
+        }
+        dst[u] = wbase + m.rel + q;
       }
     }
 #pragma unroll
@@ -639,7 +665,11 @@ __device__ void emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScra
 
 // --------------------------------------------------------------- kernels
 template <int MODE, int OUT, int G, bool NT>
-__global__ __launch_bounds__(256) void k_match_fast(MatchArgs a) {
+#ifndef VMQG_COUNT_WPE
+#define VMQG_COUNT_WPE 4   // COUNT waves per SIMD the register budget must allow (A/B: 4, 5)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? VMQG_COUNT_WPE : 4)))
+void k_match_fast(MatchArgs a) {
   using FS = FastScratch<G>;
   constexpr int GPW = FS::GPW;
   if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < 4) a.status_next[threadIdx.x] = 0;
