@@ -468,7 +468,9 @@ def bench_other(args):
     # oracle leg: parity on a sample, lookup counts (SURVEY B_p), CPU baseline
     cpu, parity, b_p = None, None, None
     if not args.no_cpu_baseline:
-        CS = min(2048, npub)
+        # bounded sample: <= 2,048 publishes and <= 4M emissions (R2's one
+        # publish emits every subscriber)
+        CS = int(max(1, min(2048, npub, np.searchsorted(offs_h, 4_000_000, side="right") - 1)))
         if w.clients is None:
             per_mp = np.bincount(w.client_mp, minlength=len(w.mps))
             small = per_mp <= 2_000_000
@@ -484,11 +486,12 @@ def bench_other(args):
         from oracle import feed   # the CPU restatement: checker, lookup counts and baseline only
         t0 = time.time()
         orc = O.TrieOracle(w.self_node)
-        B = 1 << 20
+        B = 1 << 18
         idx_all = np.arange(n) if subs_idx is None else subs_idx
         for lo in range(0, len(idx_all), B):
             orc.apply_raw(feed.init_bytes(w, idx=idx_all[lo:lo + B]))
-        log("oracle loaded %d subs in %.1fs" % (len(idx_all), time.time() - t0))
+            log("oracle: %d / %d subscriptions loaded (%.0fs)" % (min(len(idx_all), lo + B), len(idx_all),
+                                                                 time.time() - t0))
         want, counts = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in cand], with_counts=True)
         recs = d_out[: int(offs_h[-1]) * 4].cpu().numpy().view(np.uint32).reshape(-1, 4)
         infos = view.subinfos.terms
