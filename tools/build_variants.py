@@ -13,6 +13,7 @@ from vernemq_amd import _lib  # noqa: E402
 VARIANTS = {
     "default": [],
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
+    "nospill": ["-DVMQG_SPILL_KEYS=2"],
     "emit_u2": ["-DVMQG_EMIT_U=2"],
     "emit_u8": ["-DVMQG_EMIT_U=8"],
     "ss_u2": ["-DVMQS_UNROLL=2"],

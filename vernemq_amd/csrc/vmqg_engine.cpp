@@ -917,7 +917,8 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     d_keycache = nullptr; d_deferred = nullptr;
     keycache_cap = deferred_cap = 0;
     const uint64_t cap = next_pow2(std::max<uint64_t>(npub, 1024));
-    if (hipMalloc(&d_keycache, cap * 32) != hipSuccess) return VMQG_E_NOMEM;
+    // 32-B key cache + kSpillKeys x 8-B spilled keys per publish
+    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8)) != hipSuccess) return VMQG_E_NOMEM;
     if (hipMalloc(&d_deferred, 2 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
     keycache_cap = cap;
     deferred_cap = cap;
@@ -980,6 +981,7 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.pubs = pubs; a.words = words; a.npub = npub;
   a.offsets = offs;
   a.keycache = d_keycache;
+  a.keyspill = reinterpret_cast<uint2*>(static_cast<char*>(d_keycache) + keycache_cap * 32);
   a.status = d_status + 4 * (call_seq & 1);
   a.status_next = d_status + 4 * ((call_seq + 1) & 1);
   a.err = d_status + 8;

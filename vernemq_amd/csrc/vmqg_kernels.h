@@ -19,6 +19,7 @@ struct MatchArgs {
   const vmqg_pub* pubs; const uint32_t* words; uint32_t npub, pad0;
   uint64_t* offsets;                              // npub + 1
   void* keycache;                                 // npub x 32 B (COUNT -> EMIT)
+  uint2* keyspill;                                // npub x kSpillKeys {record off, cum start}: 3..8-key publishes
   Record* out; uint64_t out_cap;                  // records mode
   vmqg_range* out_rng; uint64_t rng_cap;          // range mode (out_rng != null)
   uint32_t* status;                               // this call's counters: [0] deferred publishes,

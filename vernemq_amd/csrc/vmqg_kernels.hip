@@ -48,6 +48,10 @@ constexpr int kWaves = 4;          // waves per 256-thread block
 // fast-tier LDS lists per group, sized so a block stays near 28 KiB
 template <int G> struct FastCaps { static constexpr uint32_t S = 8 * G, C = 4 * G, K = 4 * G; };
 constexpr uint32_t kRewalk = 0xFFFFFFFFu;   // key cache: EMIT must re-walk
+#ifndef VMQG_SPILL_KEYS
+#define VMQG_SPILL_KEYS 8                   // A/B: 2 = no spill (every publish with > 2 keys is re-walked)
+#endif
+constexpr uint32_t kSpillKeys = 8;          // spill slots per publish (more keys: re-walk)
 constexpr uint32_t kDeferred = 0xFFFFFFFEu; // key cache: the wave tier owns the publish
 
 // Per-call status counters (a.status; two sets used by alternate calls: each
@@ -426,6 +430,10 @@ template <int G, int OUT>
 __device__ void count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g) {
   const vmqg_pub pub = a.pubs[p];
   const Matched m = walk_publish<G>(a, pub, s, g);
+  // 3..8 keys: the group copies its key list to the publish's spill slots
+  const bool spill = !m.overflow && m.nk > 2 && m.nk <= VMQG_SPILL_KEYS;
+  if (spill)
+    for (uint32_t i = g.lane; i < m.nk; i += G) a.keyspill[(uint64_t)p * kSpillKeys + i] = s.ky(i);
   if (g.lane != 0) return;
   uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
   if (m.overflow) {   // the wave tier counts it (and writes offsets[p])
@@ -438,12 +446,16 @@ __device__ void count_publish(const MatchArgs& a, uint32_t p, const FastScratch<
   const uint32_t total = out_total<OUT>(m);
   a.offsets[p] = total;
   // key cache: total, nk, remote mask, up to two {record off, count}
+  // (3..8 keys: the keys in the spill slots, kc[1].y = their record total)
   if (m.nk <= 2) {
     const uint2 k0 = m.nk > 0 ? s.ky(0) : make_uint2(0, 0);
     const uint2 k1 = m.nk > 1 ? s.ky(1) : make_uint2(0, m.ksum);
     const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
     kc[0] = make_uint4(total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
     kc[1] = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
+  } else if (spill) {
+    kc[0] = make_uint4(total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
+    kc[1] = make_uint4(0, m.ksum, 0, 0);
   } else {
     kc[0] = make_uint4(total, kRewalk, 0, 0);
   }
@@ -459,7 +471,7 @@ struct GroupMeta {
 };
 
 // Resolve publish first + gidx of a wave: from the key cache, or by a
-// re-walk (> 2 keys).  Leaves the keys {off, cum start} in the group's LDS
+// re-walk (> 8 keys).  Leaves the keys {off, cum start} in the group's LDS
 // key list.  ok = false: the wave tier writes it (or an error is latched).
 template <int G, int OUT>
 __device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
@@ -478,7 +490,9 @@ __device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s,
     total = h.x; nk = h.y; rmask = ((uint64_t)h.w << 32) | h.z;
     const uint4 k = kc[1];
     ksum = k.y + k.w;
-    if (g.lane == 0) {
+    if (nk > 2) {   // spilled by COUNT: {off, cum start} as the walk left them
+      for (uint32_t i = g.lane; i < nk; i += G) s.ky(i) = a.keyspill[(uint64_t)p * kSpillKeys + i];
+    } else if (g.lane == 0) {
       s.ky(0) = make_uint2(k.x, 0u);
       s.ky(1) = make_uint2(k.z, k.y);
     }
@@ -596,7 +610,7 @@ __global__ __launch_bounds__(256) void k_emit_records(MatchArgs a) {
         const uint4 h = kc[0];
         const uint64_t ob = a.offsets[p], oe = a.offsets[p + 1];
         e.rel = (uint32_t)(ob - wbase);
-        if (h.y == kRewalk) {
+        if (h.y == kRewalk || (h.y > 2 && h.y != kDeferred)) {
           a.deferred[a.npub + atomicAdd(&a.status[kStRewalk], 1u)] = p;   // the wave tier emits it
         } else if (h.y != kDeferred) {
           const uint4 k = kc[1];
