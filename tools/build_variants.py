@@ -14,6 +14,7 @@ VARIANTS = {
     "default": [],
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "nospill": ["-DVMQG_SPILL_KEYS=2"],
+    "noalias": ["-DVMQG_HASH_ALIAS=0"],
     "emit_u2": ["-DVMQG_EMIT_U=2"],
     "emit_u8": ["-DVMQG_EMIT_U=8"],
     "ss_u2": ["-DVMQS_UNROLL=2"],

@@ -55,6 +55,9 @@ constexpr uint32_t kHasAll = kHasHash | kHasPlus | kHasWord;
 struct alignas(16) EdgeSlot { uint32_t parent, word, child, flags; };
 // meta = flags | nkeys << 8; nkeys == 1: {off0, cnt0} inline; nkeys >= 2: key = keylist offset.
 // rmask: remote nodes < 64; nodes >= 64 (kNodeHigh) are listed in the keylist pool at hi_off.
+// The node region holds 2 x node_cap records: [p] is path p's own, [node_cap + p]
+// a copy of the record of p's '#' child while the edge (p, '#') exists (else
+// empty), so a '#' candidate costs one record read and no edge probe.
 struct alignas(16) NodeRec { uint32_t meta, key, rmask_lo, rmask_hi, off0, cnt0, hi_off, hi_cnt; };
 struct alignas(8) KeyDesc { uint32_t off, count; };
 struct alignas(16) Record { uint32_t kind_node, group, subscriber, subinfo; };
@@ -82,7 +85,7 @@ struct Layout {
   uint64_t total_bytes;
   uint64_t edge_off, node_off, keydesc_off, keylist_off, rec_off, exact_off, exwords_off;
   uint64_t edge_buckets;     // power of two
-  uint64_t node_cap;         // path ids
+  uint64_t node_cap;         // path ids (the node region holds 2 x node_cap records)
   uint64_t key_cap;          // key ids
   uint64_t keylist_cap;      // u32 entries
   uint64_t rec_cap;          // records

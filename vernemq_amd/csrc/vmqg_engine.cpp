@@ -235,6 +235,7 @@ void Engine::edge_insert(uint32_t parent, uint32_t word, uint32_t child) {
         if (word == kHash || word == kPlus) {
           paths[parent].eflags |= word == kHash ? kHasHash : kHasPlus;
           refresh_incoming_flags(parent);
+          if (word == kHash) write_hash_alias(parent);
         } else if (paths[parent].nlit++ == 0) {
           paths[parent].eflags |= kHasWord;
           refresh_incoming_flags(parent);
@@ -256,6 +257,7 @@ void Engine::edge_erase(uint32_t parent, uint32_t word, uint32_t child) {
   if (word == kHash || word == kPlus) {
     paths[parent].eflags &= ~(word == kHash ? kHasHash : kHasPlus);
     refresh_incoming_flags(parent);
+    if (word == kHash) write_hash_alias(parent);
   } else if (--paths[parent].nlit == 0) {
     paths[parent].eflags &= ~kHasWord;
     refresh_incoming_flags(parent);
@@ -310,7 +312,7 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) c
   L.edge_buckets *= scale; L.node_cap *= scale; L.key_cap *= scale; L.keylist_cap *= scale;
   L.rec_cap *= scale; L.exact_buckets *= scale; L.exwords_cap *= scale;
   L.edge_off = o;    o = align256(o + L.edge_buckets * kEdgeSlotsPerBucket * sizeof(EdgeSlot));
-  L.node_off = o;    o = align256(o + L.node_cap * sizeof(NodeRec));
+  L.node_off = o;    o = align256(o + 2 * L.node_cap * sizeof(NodeRec));   // records, then '#'-child aliases
   L.keydesc_off = o; o = align256(o + L.key_cap * sizeof(KeyDesc));
   L.keylist_off = o; o = align256(o + L.keylist_cap * sizeof(uint32_t));
   L.rec_off = o;     o = align256(o + L.rec_cap * sizeof(Record));
@@ -445,7 +447,25 @@ bool Engine::write_path(uint32_t p) {
   r.rmask_lo = (uint32_t)rmask; r.rmask_hi = (uint32_t)(rmask >> 32);
   *(region<NodeRec>(lay.node_off) + p) = r;
   touch(lay.node_off + (uint64_t)p * sizeof(NodeRec), sizeof(NodeRec));
+  if (P.word == kHash && P.parent != kNone) write_hash_alias(P.parent);
   return true;
+}
+
+// Record slot node_cap + parent holds a copy of the record of parent's '#'
+// child while the edge (parent, '#') exists, else an empty record: the walk
+// reads it for a node whose cached flags say it has a '#' edge (and for the
+// roots, always) instead of probing the edge table first (a '#' path is a
+// leaf, so its record is all the walk needs of it).
+void Engine::write_hash_alias(uint32_t parent) {
+  if (parent >= lay.node_cap) return;
+  const uint32_t c = path_child(parent, kHash, false);
+  NodeRec r{0, kNone, 0, 0, 0, 0, 0, 0};
+  if (c != kNone && c < lay.node_cap && paths[c].in_slot != ~0ull) r = region<NodeRec>(lay.node_off)[c];
+  NodeRec* dst = region<NodeRec>(lay.node_off) + lay.node_cap + parent;
+  if (memcmp(dst, &r, sizeof(r)) != 0) {
+    *dst = r;
+    touch(lay.node_off + (lay.node_cap + parent) * sizeof(NodeRec), sizeof(NodeRec));
+  }
 }
 
 uint64_t Engine::exact_fp(const TopicInfo& t) const {

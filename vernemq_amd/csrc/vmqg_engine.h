@@ -270,6 +270,7 @@ struct Engine {
   bool flush_incremental();
   bool write_key(uint32_t k);
   bool write_path(uint32_t p);
+  void write_hash_alias(uint32_t parent);
   bool write_topic(uint32_t t);
   uint64_t exact_fp(const TopicInfo& t) const;
 

@@ -168,8 +168,8 @@ constexpr uint32_t kDepthMask = 0x0FFFFFFFu;   // frontier entry: {path, depth |
 constexpr uint32_t kUnresolved = 0xFFFFFFFFu;  // key list entry still holds a key id
 
 // One step of trie_match/4 + 'trie_match_#'/2 (vmq_reg_trie.erl:358-383) for
-// up to G frontier entries, one per lane: the three edge probes, issued
-// before any is resolved.  The node's cached edge flags (`fl`) skip '#' / '+'
+// up to G frontier entries, one per lane: the word and '+' edge probes,
+// issued before either is resolved; the '#' child is its aliased record.  The node's cached edge flags (`fl`) skip '#' / '+'
 // / literal probes that must miss.
 struct StepOut { uint32_t hc, wc, pc, wf, pf; bool at_end; };
 
@@ -184,16 +184,25 @@ __device__ __forceinline__ StepOut probe_step(const MatchArgs& a, const Group<G>
   const bool do_h = act && (fl & kHasHash);
   const bool do_w = act && !at_end && (fl & kHasWord) && wd != kPlus && wd != kHash && wd != kUnknownWord;
   const bool do_p = act && !at_end && (fl & kHasPlus);
-  const uint64_t bh = edge_hash(node, kHash) & a.edge_mask;
   const uint64_t bw = edge_hash(node, wd) & a.edge_mask;
   const uint64_t bp = edge_hash(node, kPlus) & a.edge_mask;
-  Bucket Bh{}, Bw{}, Bp{};
-  if (do_h) Bh = load_bucket(a.edges, bh);
+  Bucket Bw{}, Bp{};
   if (do_w) Bw = load_bucket(a.edges, bw);
   if (do_p) Bp = load_bucket(a.edges, bp);
+#ifndef VMQG_HASH_ALIAS
+#define VMQG_HASH_ALIAS 1   // A/B: 0 = probe the '#' edge and read the child's own record
+#endif
+#if VMQG_HASH_ALIAS
+  // the '#' child: no probe, its record is aliased at node_cap + node
+  StepOut o{do_h ? (uint32_t)(a.node_cap + node) : kNone, kNone, kNone, 0, 0, at_end};
+#else
+  const uint64_t bh = edge_hash(node, kHash) & a.edge_mask;
+  Bucket Bh{};
+  if (do_h) Bh = load_bucket(a.edges, bh);
   StepOut o{kNone, kNone, kNone, 0, 0, at_end};
   uint32_t hf = 0;
   if (do_h) probe(a.edges, a.edge_mask, bh, Bh, node, kHash, o.hc, hf);
+#endif
   if (do_w) probe(a.edges, a.edge_mask, bw, Bw, node, wd, o.wc, o.wf);
   if (do_p) probe(a.edges, a.edge_mask, bp, Bp, node, kPlus, o.pc, o.pf);
   return o;
@@ -315,7 +324,7 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
       bool high = false;
       if (ci < nc) {
         const uint32_t path = s.cd(ci);
-        if (path < a.node_cap) {
+        if (path < 2 * a.node_cap) {   // own records, then '#' aliases
           const uint4 r = *reinterpret_cast<const uint4*>(a.nodes + path);
           const uint2 r2 = *reinterpret_cast<const uint2*>(&a.nodes[path].off0);
           const bool valid = (r.x & kNodeEmits) == kNodeEmits &&
@@ -794,7 +803,7 @@ struct WaveWalk {
       uint32_t nkeys = 0, key = kNone, off0 = 0, cnt0 = 0;
       if (ci < nc) {
         const uint32_t path = W.cand[ci];
-        if (path < a.node_cap) {
+        if (path < 2 * a.node_cap) {   // own records, then '#' aliases
           const NodeRec r = a.nodes[path];
           const bool valid = (r.meta & kNodeEmits) == kNodeEmits && !(dollar && (r.meta & kNodeDollarSkip));
           if (valid) {
