@@ -364,11 +364,11 @@ def main():
             "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3, "launches": nlaunch},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
-                         "kernel": "k_match_fast<1,2,true> (EMIT)",
+                         "kernel": "k_match_fast<1,0,2,true> (EMIT)",
                          "algorithmic_bytes_per_launch": alg["emit_compulsory"],
                          "bytes_model": "16 B written per emission + 40 B read per publish + 16 B per distinct "
                                         "record (workloads.algorithmic_bytes_c emit_compulsory)"},
-            "count_kernel": {"kernel": "k_match_fast<0,2,false> (COUNT)", "us": count_ns / 1e3 if count_ns else None,
+            "count_kernel": {"kernel": "k_match_fast<0,0,2,true> (COUNT)", "us": count_ns / 1e3 if count_ns else None,
                              "lookup_bytes_model": alg["count"],
                              "achieved": alg["count"] / count_ns if count_ns else None},
             "survey_model": {"bytes_per_step": alg["all"], "achieved_per_step": alg["all"] / pipe_ns,
@@ -717,9 +717,24 @@ def bench_d(args):
     if view.match_status(sp) != 0:
         raise RuntimeError("match status (parity pass)")
     offs_h = d_offs.cpu().numpy()
-    known = bool(np.array_equal(np.diff(offs_h), W.config_d_counts(w, ch.live)))
+    want_counts = W.config_d_counts(w, ch.live)
+    known = bool(np.array_equal(np.diff(offs_h), want_counts))
+    images_equal = True
+    if dist:   # every replica's device arena must equal the primary's, region by region
+        regions = vd.arena_region_hashes(view, dev)
+        allr = vd.gather_counts(dist, np.array(regions, dtype=np.int64), dev)
+        images_equal = bool((allr == allr[0]).all())
+        if not images_equal:
+            log("rank %d: arena regions differing from rank 0: %s" % (rank, [
+                vd.REGION_NAMES[i] for i in range(len(regions)) if (allr[:, i] != allr[0, i]).any()]))
     if not known:
-        raise RuntimeError("config D counts differ from the live set's known answer")
+        bad = np.flatnonzero(np.diff(offs_h) != want_counts)
+        raise RuntimeError("rank %d: config D counts differ from the live set's known answer at %d of %d publishes "
+                           "(first %s: got %s, want %s); replica images equal: %s"
+                           % (rank, len(bad), npub, bad[:4].tolist(), np.diff(offs_h)[bad[:4]].tolist(),
+                              want_counts[bad[:4]].tolist(), images_equal))
+    if not images_equal:
+        raise RuntimeError("replica arena image differs from the primary's")
     S = min(npub, 1 << 16)
     h = hashlib.sha256(offs_h[: S + 1].tobytes() + d_out[: int(offs_h[S]) * 4].cpu().numpy().tobytes()).digest()
     replicas_equal = True
@@ -800,7 +815,7 @@ def bench_d(args):
             "match_batches_per_delta_batch": per_period,
             "pairs_per_s": emitted * args.steps * per_period * world / t_max,
             "emissions_per_match_batch": emitted, "load_s": load_s,
-            "verified": {"known_answer": known, "replicas_equal": replicas_equal},
+            "verified": {"known_answer": known, "replicas_equal": replicas_equal, "images_equal": images_equal},
             "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS if achieved else None,

@@ -196,8 +196,12 @@ int vmqg_match_batch(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const uin
                      uint64_t* offsets);
 
 /* Device-buffer match: every pointer is device memory of the context's
- * device; work is enqueued on `stream` (a hipStream_t, NULL = the context's
- * own stream) and the call returns without synchronising.  d_offsets needs
+ * device; work is enqueued on `stream` (a hipStream_t; NULL = the context's
+ * own stream, ordered after work already queued on the legacy default
+ * stream and before default-stream work queued later, so a caller on the
+ * default stream needs no extra synchronisation) and the call returns
+ * without synchronising.  Table changes (patches, images) queued on any
+ * stream land before the match.  d_offsets needs
  * npub + 1 entries.  Overflow / scratch errors are latched on the device and
  * reported by the next vmqg_match_status(). */
 int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub,

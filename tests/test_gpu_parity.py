@@ -349,6 +349,43 @@ def test_device_entry_point_with_torch_buffers():
     assert np.array_equal(out, ref)
 
 
+def test_null_stream_is_ordered_with_torch_default_stream():
+    """stream = NULL (torch's default stream handle) is ordered like default-
+    stream work: the match waits for inputs still being copied in behind a
+    long default-stream queue, and a default-stream read-back waits for the
+    match — no torch.cuda.synchronize() in between (vmqg_nullorder.h)."""
+    import torch
+    from vernemq_amd import workloads as W
+    w = W.config_b(n_subs=20_000, n_pubs=4096)
+    v, _ = _load_both(w, with_oracle=False)
+    pubs, words = w.publish_arrays(v)
+    ref_recs, ref_offs = v.match_arrays(pubs, words)
+    dev = torch.device("cuda:0")
+    assert torch.cuda.current_stream().cuda_stream == 0
+    h_pubs = torch.from_numpy(pubs.view(np.uint32).view(np.int32).copy()).pin_memory()
+    h_words = torch.from_numpy(words.astype(np.int32)).pin_memory()
+    d_pubs = torch.zeros(h_pubs.numel(), dtype=torch.int32, device=dev)   # all publishes on an empty mountpoint...
+    d_words = torch.zeros(h_words.numel(), dtype=torch.int32, device=dev)
+    cap = int(ref_offs[-1]) + 16
+    d_out = torch.zeros(cap * 4, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    for rep in range(3):
+        d_pubs.zero_()
+        d_offs.zero_()
+        x = torch.randn(4096, 4096, device=dev)
+        for _ in range(8):                      # tens of ms of default-stream work ahead of the copies
+            x = torch.tanh(x @ x)
+        d_pubs.copy_(h_pubs, non_blocking=True)   # ...until these land
+        d_words.copy_(h_words, non_blocking=True)
+        v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap, d_offs.data_ptr(), 0)
+        offs = d_offs.cpu().numpy().astype(np.uint64)     # default stream, no synchronize
+        assert np.array_equal(offs, ref_offs), rep
+        assert v.match_status(0) == 0
+    out = d_out.cpu().numpy().view(np.uint32).reshape(-1, 4)[: int(offs[-1])]
+    assert np.array_equal(out, ref_recs.view(np.uint32).reshape(-1, 4))
+
+
 def test_replica_follows_primary_by_image_and_patches():
     """A replica context fed the primary's arena image and then its patch
     stream answers identically (the RCCL broadcast payloads, minus RCCL)."""

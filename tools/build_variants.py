@@ -15,6 +15,8 @@ VARIANTS = {
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "nospill": ["-DVMQG_SPILL_KEYS=2"],
     "noalias": ["-DVMQG_HASH_ALIAS=0"],
+    "scan4": ["-DVMQG_SCAN_ITEMS=4"],
+    "scan8": ["-DVMQG_SCAN_ITEMS=8"],
     "emit_u2": ["-DVMQG_EMIT_U=2"],
     "emit_u8": ["-DVMQG_EMIT_U=8"],
     "ss_u2": ["-DVMQS_UNROLL=2"],

@@ -13,6 +13,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
 __device__ __forceinline__ uint32_t mix(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
@@ -52,7 +54,59 @@ __global__ __launch_bounds__(256) void k_probe(const uint4* tab, uint32_t nb, ui
   }
 }
 
-#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+// Probes of 64-B buckets on 128-B lines, each followed (F = 1) by a dependent
+// 16-B read of the line's other half (an edge slot's side payload): is the
+// follow-up an L2 hit or a second random access?
+template <int G, int F, int D>
+__global__ __launch_bounds__(256) void k_probe_line(const uint4* tab, uint32_t nl, uint32_t nchains, uint32_t* out) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t sub = threadIdx.x & (G - 1);
+  const uint32_t grp = tid / G, ngrp = gridDim.x * blockDim.x / G;
+  for (uint32_t c = grp; c < nchains; c += ngrp) {
+    uint32_t b = mix(c) % nl, acc = 0;
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+      uint4 v[4 / G];
+#pragma unroll
+      for (int k = 0; k < 4 / G; k++) v[k] = tab[(uint64_t)b * 8 + sub * (4 / G) + k];
+      uint32_t h = 0;
+#pragma unroll
+      for (int k = 0; k < 4 / G; k++) h ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+#pragma unroll
+      for (int s = 1; s < G; s <<= 1) h ^= __shfl_xor(h, s, 64);
+      if (F) {
+        const uint4 q = tab[(uint64_t)b * 8 + 4 + (h & 3)];
+        h += q.x ^ q.w;
+      }
+      acc += h;
+      b = mix(h + d) % nl;
+    }
+    if (sub == 0) out[c] = acc;
+  }
+}
+
+template <int G, int F, int D>
+static void run_line(const char* table, const uint4* tab, uint32_t nl, uint32_t nchains, uint32_t* out, int bpc, int cus) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  const int blocks = bpc * cus, reps = 20;
+  for (int w = 0; w < 3; w++) k_probe_line<G, F, D><<<blocks, 256>>>(tab, nl, nchains, out);
+  CK(hipEventRecord(a));
+  for (int r = 0; r < reps; r++) k_probe_line<G, F, D><<<blocks, 256>>>(tab, nl, nchains, out);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  const double us = ms * 1e3 / reps, probes = (double)nchains * D;
+  printf("{\"table\": \"%s\", \"kind\": \"64B of a 128B line%s\", \"G\": %d, \"depth\": %d, \"blocks_per_cu\": %d, "
+         "\"us_per_launch\": %.1f, \"Gprobes_per_s\": %.2f}\n",
+         table, F ? " + dependent 16B of its other half" : "", G, D, bpc, us, probes / (us * 1e-6) / 1e9);
+  fflush(stdout);
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+}
+
 
 template <int G, int C, int D>
 static void run(const char* table, const uint4* tab, uint32_t nb, uint32_t nchains, uint32_t* out, int bpc, int cus) {
@@ -99,6 +153,10 @@ int main() {
       run<4, 2, 4>(t.name, tab, nb, nchains, out, bpc, cus);
       run<1, 1, 4>(t.name, tab, nb, nchains, out, bpc, cus);
       run<2, 1, 1>(t.name, tab, nb, nchains * 4, out, bpc, cus);   // independent probes, same count
+      const uint32_t nl = (uint32_t)(t.bytes / 128);
+      run_line<2, 0, 4>(t.name, tab, nl, nchains, out, bpc, cus);
+      run_line<2, 1, 4>(t.name, tab, nl, nchains, out, bpc, cus);
+      run_line<2, 0, 8>(t.name, tab, nl, nchains, out, bpc, cus);
     }
     CK(hipFree(tab));
   }

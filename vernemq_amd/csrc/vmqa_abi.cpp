@@ -2,6 +2,7 @@
 #include <new>
 
 #include "vmqa_engine.h"
+#include "vmqg_nullorder.h"
 
 using vmqa::AclEngine;
 
@@ -76,6 +77,8 @@ int vmqa_check_device(vmqa_ctx* ctx, const vmqa_req* d_reqs, uint32_t n, const u
                       uint8_t* d_allowed, void* stream) {
   if (!ctx || (n && (!d_reqs || !d_words || !d_allowed))) return VMQG_E_INVAL;
   GUARD_BEGIN
+  hipSetDevice(ctx->e.device);
+  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
   return ctx->e.check_device(d_reqs, n, d_words, d_allowed, static_cast<hipStream_t>(stream));
   GUARD_END
 }

@@ -25,6 +25,7 @@ AclEngine::~AclEngine() {
   if (stream) hipStreamSynchronize(stream);
   for (auto& e : t_check) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (ev_done) hipEventDestroy(ev_done);
+  if (ev_null) hipEventDestroy(ev_null);
   hipFree(d_arena); hipFree(d_status); hipFree(d_r); hipFree(d_w); hipFree(d_o);
   if (stream) hipStreamDestroy(stream);
 }

@@ -62,6 +62,7 @@ struct AclEngine {
   // device
   hipStream_t stream = nullptr;
   hipEvent_t ev_done = nullptr;
+  hipEvent_t ev_null = nullptr;   // NullOrder (vmqg_nullorder.h)
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
   uint32_t* d_status = nullptr;
   void* d_r = nullptr; uint64_t d_r_cap = 0;   // host-buffer staging

@@ -5,6 +5,7 @@
 #include <string>
 #include <new>
 
+#include "vmqg_nullorder.h"
 #include "vmqg_engine.h"
 
 using vmqg::Engine;
@@ -174,6 +175,8 @@ int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, cons
                       vmqg_emit* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream) {
   if (!ctx || !d_offsets || (npub && (!d_pubs || !d_words))) return VMQG_E_INVAL;
   GUARD_BEGIN
+  hipSetDevice(ctx->e.device);
+  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
   return ctx->e.match_device(d_pubs, npub, d_words, reinterpret_cast<vmqg::Record*>(d_out), out_cap, nullptr, 0,
                              d_offsets, static_cast<hipStream_t>(stream));
   GUARD_END
@@ -185,6 +188,8 @@ int vmqg_match_ranges_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npu
   GUARD_BEGIN
   // a non-null range buffer selects range mode even at out_cap 0
   static vmqg_range dummy;
+  hipSetDevice(ctx->e.device);
+  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
   return ctx->e.match_device(d_pubs, npub, d_words, nullptr, 0, d_out ? d_out : &dummy, out_cap, d_offsets,
                              static_cast<hipStream_t>(stream));
   GUARD_END
@@ -312,6 +317,7 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
   if (L.magic != vmqg::kLayoutMagic) return VMQG_E_INVAL;
   hipSetDevice(e.device);
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e.stream;
+  vmqg::NullOrder order(stream, e.stream, e.ev_null);
   if (e.d_arena_bytes < L.total_bytes) {
     if (hipDeviceSynchronize() != hipSuccess) return VMQG_E_DEVICE;
     if (e.d_arena) hipFree(e.d_arena);
@@ -325,6 +331,7 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
   if (hipMemcpyAsync(e.d_arena, d_src, L.total_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return VMQG_E_DEVICE;
   if (hipEventRecord(e.ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
+  e.ev_stream = st;
   e.epoch++;
   return VMQG_OK;
 }
@@ -358,12 +365,14 @@ int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t byt
   if (!e.has_device || !e.d_arena) return VMQG_E_DEVICE;
   hipSetDevice(e.device);
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e.stream;
+  vmqg::NullOrder order(stream, e.stream, e.ev_null);
   // tables change only after the matches queued before, and matches queued
   // later (on any stream) see the patches
   if (hipStreamWaitEvent(st, e.ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
   if (vmqg::launch_patches(e.d_arena, d_patches, bytes / sizeof(vmqg::Patch), st) != hipSuccess)
     return VMQG_E_DEVICE;
   if (hipEventRecord(e.ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
+  e.ev_stream = st;
   e.epoch++;
   return VMQG_OK;
 }

@@ -24,6 +24,7 @@ Engine::~Engine() {
     for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (ev_match_done) hipEventDestroy(ev_match_done);
+    if (ev_null) hipEventDestroy(ev_null);
     for (Stage& sg : stage) {
       if (sg.ev) hipEventDestroy(sg.ev);
       if (sg.h) hipHostFree(sg.h);
@@ -926,6 +927,7 @@ int Engine::upload() {
   sg.used = true;
   // later matches on other streams must see the patches
   if (hipEventRecord(ev_match_done, stream) != hipSuccess) return VMQG_E_DEVICE;
+  ev_stream = stream;
   return VMQG_OK;
 }
 
@@ -1022,7 +1024,9 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   hipSetDevice(device);
   if (!st) st = stream;
   // patches / images queued on the context stream land before this match
-  if (st != stream && hipStreamWaitEvent(st, ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
+  // table changes (patches, images) land before this match: the primary's on
+  // the context stream, a replica's on whatever stream the caller gave
+  if (st != ev_stream && hipStreamWaitEvent(st, ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
   if (npub == 0) return hipMemsetAsync(d_offsets, 0, 8, st) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
   int rc;
   if ((rc = ensure_match_scratch(npub, st)) || (rc = ensure_lookback(scan_tiles(npub), st)) ||
@@ -1049,6 +1053,7 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   if (timing) { hipEventRecord(e3, st); t_count.push_back({e0, e1}); t_emit.push_back({e2, e3}); }
   if (launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
+  ev_stream = st;
   return VMQG_OK;
 }
 

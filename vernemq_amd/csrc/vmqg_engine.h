@@ -215,6 +215,8 @@ struct Engine {
   void* d_offs = nullptr; uint64_t d_offs_cap = 0;
   void* d_out = nullptr; uint64_t d_out_cap = 0;
   hipEvent_t ev_match_done = nullptr;
+  hipStream_t ev_stream = nullptr;   // the stream ev_match_done was last recorded on
+  hipEvent_t ev_null = nullptr;      // NullOrder (vmqg_nullorder.h)
   bool timing = false;
   uint32_t opt_fast_g = 2, opt_flags = kOptNtStores;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
   uint32_t opt_count_bpc = 4, opt_emit_bpc = 16;       // fast-tier grid caps, blocks per CU (A/B-tuned)

@@ -972,7 +972,10 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
 // offsets[0, npub] (offsets[npub] = total) in ONE launch: tiles of 4,096
 // taken by ticket, chained by a decoupled look-back.  Slot npub is never
 // read (no memset before the COUNT pass).
-constexpr uint32_t kScanItems = 16, kScanBlock = 256, kScanTile = kScanItems * kScanBlock;
+#ifndef VMQG_SCAN_ITEMS
+#define VMQG_SCAN_ITEMS 16   // counts per thread (A/B: 4, 8, 16)
+#endif
+constexpr uint32_t kScanItems = VMQG_SCAN_ITEMS, kScanBlock = 256, kScanTile = kScanItems * kScanBlock;
 
 __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
   __shared__ uint64_t part[kScanBlock];

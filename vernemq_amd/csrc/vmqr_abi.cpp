@@ -4,6 +4,7 @@
 #include <string>
 
 #include "vmqr_engine.h"
+#include "vmqg_nullorder.h"
 
 using vmqr::RetainEngine;
 
@@ -78,6 +79,8 @@ int vmqr_match_device(vmqr_ctx* ctx, const vmqg_pub* d_filters, uint32_t n, cons
                       uint32_t* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream) {
   if (!ctx || !d_offsets || (n && (!d_filters || !d_words))) return VMQG_E_INVAL;
   GUARD_BEGIN
+  hipSetDevice(ctx->e.device);
+  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
   return ctx->e.match_device(d_filters, n, d_words, d_out, out_cap, d_offsets, static_cast<hipStream_t>(stream));
   GUARD_END
 }

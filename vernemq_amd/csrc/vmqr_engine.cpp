@@ -24,6 +24,7 @@ RetainEngine::~RetainEngine() {
   for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (ev_match_done) hipEventDestroy(ev_match_done);
+  if (ev_null) hipEventDestroy(ev_null);
   hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_tickets); hipFree(d_plan); hipFree(d_lookback);
   hipFree(d_f); hipFree(d_w); hipFree(d_o); hipFree(d_offs);
   if (h_patch) hipHostFree(h_patch);

@@ -134,6 +134,7 @@ struct RetainEngine {
   uint64_t epoch = 0, rebuilds = 0;
   // device
   hipStream_t stream = nullptr;
+  hipEvent_t ev_null = nullptr;   // NullOrder (vmqg_nullorder.h)
   hipEvent_t ev_match_done = nullptr;
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
   Patch* h_patch = nullptr; uint64_t h_patch_cap = 0;

@@ -5,6 +5,7 @@
 #include <new>
 
 #include "vmqs_engine.h"
+#include "vmqg_nullorder.h"
 
 namespace vmqs {
 
@@ -14,6 +15,7 @@ SelEngine::~SelEngine() {
   if (stream) hipStreamSynchronize(stream);
   for (auto& e : t_sel) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (ev_sel) hipEventDestroy(ev_sel);
+  if (ev_null) hipEventDestroy(ev_null);
   hipFree(d_states); hipFree(d_status); hipFree(d_defer);
   hipFree(d_e); hipFree(d_o); hipFree(d_c); hipFree(d_f);
   if (stream) hipStreamDestroy(stream);
@@ -187,6 +189,8 @@ int vmqs_select_device(vmqs_ctx* ctx, const vmqg_emit* d_emits, const uint64_t* 
                        void* stream) {
   if (!ctx || (npub && (!d_emits || !d_offsets || !d_chosen))) return VMQG_E_INVAL;
   GUARD_BEGIN
+  hipSetDevice(ctx->e.device);
+  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
   return ctx->e.select_device(d_emits, d_offsets, npub, policy, seed, pub_seq, d_chosen, d_failed,
                               static_cast<hipStream_t>(stream));
   GUARD_END

@@ -54,6 +54,7 @@ struct SelEngine {
   uint8_t* d_states = nullptr; uint64_t n_states = 0, states_cap = 0;
   std::vector<uint8_t> h_states;   // host copy of the state table
   uint32_t* d_status = nullptr;
+  hipEvent_t ev_null = nullptr;   // NullOrder (vmqg_nullorder.h)
   hipEvent_t ev_sel = nullptr;     // after the last select (any stream): state-table updates wait on it
   uint32_t* d_defer = nullptr; uint64_t defer_cap = 0;
   void* d_e = nullptr; uint64_t d_e_cap = 0;   // host-buffer staging

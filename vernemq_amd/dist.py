@@ -68,6 +68,7 @@ class ImageSync:
         self.ctrl = ctrl_group
         self.image = None     # host mode replica image
         self.layout = None
+        self._stream = None   # GPU replicas: where images and patches land (see _side_stream)
 
     @property
     def primary(self) -> bool:
@@ -91,6 +92,20 @@ class ImageSync:
         nl = int(t[len(values)])
         lay = t[len(values) + 1:len(values) + 1 + nl // 8].numpy().tobytes() if nl else b""
         return vals, lay
+
+    def _side_stream(self, buf):
+        """A stream of its own for the library's image / patch copy, after
+        everything queued on torch's current stream (the payload's broadcast
+        or host staging).  Never pass torch's default stream through: its
+        handle is 0, which the library reads as "my context stream", a
+        different stream that would not wait for the payload.  `buf` stays
+        allocated until the side stream has used it."""
+        import torch
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(self.device)
+        self._stream.wait_stream(torch.cuda.current_stream(self.device))
+        buf.record_stream(self._stream)
+        return self._stream
 
     def _payload(self, nbytes: int, fill=None):
         """A uint8 device tensor of nbytes broadcast from the primary
@@ -130,7 +145,8 @@ class ImageSync:
         img = self._payload(nbytes, fill)
         if not self.primary:
             if self._gpu():
-                self.view.replica_load(self.layout, img.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+                st = self._side_stream(img)
+                self.view.replica_load(self.layout, img.data_ptr(), st.cuda_stream)
                 torch.cuda.synchronize(self.device)   # img is released after the copy
             else:
                 self.image = img.numpy().copy()
@@ -160,11 +176,30 @@ class ImageSync:
             if self._gpu():
                 self.view.replica_sync_layout(lay)
                 if nbytes:
-                    self.view.apply_patches_device(buf.data_ptr(), nbytes,
-                                                   torch.cuda.current_stream(self.device).cuda_stream)
+                    st = self._side_stream(buf)
+                    self.view.apply_patches_device(buf.data_ptr(), nbytes, st.cuda_stream)
             elif nbytes:
                 apply_patches_host(self.image, buf.numpy())
         return nbytes // 24
+
+
+REGION_NAMES = ("edges", "nodes", "keydesc", "keylist", "records", "exact", "exwords")
+
+
+def arena_region_hashes(view, device):
+    """64-bit hashes of the seven arena regions of a view's device image
+    (the layout's region offsets), to compare replicas with the primary."""
+    import hashlib
+
+    import torch
+    ptr, nbytes, lay = view.arena()
+    torch.cuda.synchronize(device)
+    img = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    hip_memcpy_d2d(img.data_ptr(), ptr, nbytes)
+    host = img.cpu().numpy()
+    offs = [int(x) for x in np.frombuffer(lay[16:72], dtype=np.uint64)] + [nbytes]
+    return [int.from_bytes(hashlib.sha256(host[offs[i]:offs[i + 1]].tobytes()).digest()[:8], "little", signed=True)
+            for i in range(len(REGION_NAMES))]
 
 
 PATCH_DTYPE = np.dtype([("off", "<u8"), ("data", "<u4", (4,))])
