@@ -257,8 +257,6 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
 /* Tuning knobs of the match kernels (no effect on results):
  *   "fast_g"    2 | 4      lanes per publish in the fast tier (default 2)
  *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
- *   "emit_lean" 0 | 1      records EMIT without walk code, one publish per lane
- *                          (multi-key publishes go to the wave tier); default 0
  *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8;
  *                          defaults 4 and 16) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);

@@ -5,7 +5,7 @@ once, each round runs every variant for `steps` steps; outputs are checked
 equal between variants (offsets exactly, records as a per-batch checksum:
 the order inside a publish may differ between variants); medians of the
 per-variant step time and the COUNT / fast-EMIT kernel times are printed as
-JSON.  usage: ab_match.py --config C --opt emit_lean=0,1 --opt fast_g=2,4"""
+JSON.  usage: ab_match.py --config C --opt nt_stores=0,1 --opt fast_g=2,4"""
 import argparse
 import itertools
 import json

@@ -261,8 +261,6 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   } else if (n == "count_bpc" || n == "emit_bpc") {
     if (value < 0 || value > 32) return VMQG_E_INVAL;
     (n == "count_bpc" ? e.opt_count_bpc : e.opt_emit_bpc) = (uint32_t)value;
-  } else if (n == "emit_lean") {
-    e.opt_flags = value ? (e.opt_flags | vmqg::kOptLeanEmit) : (e.opt_flags & ~vmqg::kOptLeanEmit);
   } else {
     return VMQG_E_INVAL;
   }

@@ -939,8 +939,9 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     d_keycache = nullptr; d_deferred = nullptr;
     keycache_cap = deferred_cap = 0;
     const uint64_t cap = next_pow2(std::max<uint64_t>(npub, 1024));
-    // 32-B key cache + kSpillKeys x 8-B spilled keys per publish
-    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8)) != hipSuccess) return VMQG_E_NOMEM;
+    // 32-B key cache + kSpillKeys x 8-B spilled keys per publish, then the
+    // chunk totals (one per 16 or 32 publishes, + 1)
+    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + (cap / 16 + 2) * 8) != hipSuccess) return VMQG_E_NOMEM;
     if (hipMalloc(&d_deferred, 2 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
     keycache_cap = cap;
     deferred_cap = cap;
@@ -1004,6 +1005,8 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.offsets = offs;
   a.keycache = d_keycache;
   a.keyspill = reinterpret_cast<uint2*>(static_cast<char*>(d_keycache) + keycache_cap * 32);
+  a.chunk = reinterpret_cast<uint64_t*>(static_cast<char*>(d_keycache) + keycache_cap * (32 + 8 * 8));
+  a.gpw = 64 / (opt_fast_g == 4 ? 4 : 2);
   a.status = d_status + 4 * (call_seq & 1);
   a.status_next = d_status + 4 * ((call_seq + 1) & 1);
   a.err = d_status + 8;
@@ -1029,7 +1032,7 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   if (st != ev_stream && hipStreamWaitEvent(st, ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
   if (npub == 0) return hipMemsetAsync(d_offsets, 0, 8, st) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
   int rc;
-  if ((rc = ensure_match_scratch(npub, st)) || (rc = ensure_lookback(scan_tiles(npub), st)) ||
+  if ((rc = ensure_match_scratch(npub, st)) || (rc = ensure_lookback(scan_tiles((npub + 15) / 16), st)) ||
       (rc = ensure_wave_scratch(st)))
     return rc;
   MatchArgs a = args_for(d_pubs_, npub, d_words_, d_offsets);

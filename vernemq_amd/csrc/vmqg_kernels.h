@@ -19,12 +19,14 @@ struct MatchArgs {
   const vmqg_pub* pubs; const uint32_t* words; uint32_t npub, pad0;
   uint64_t* offsets;                              // npub + 1
   void* keycache;                                 // npub x 32 B (COUNT -> EMIT)
+  uint64_t* chunk;                                // per chunk of gpw publishes: COUNT's total, then its output base
+  uint32_t gpw;                                   // publishes per chunk (64 / fast-tier lanes per publish)
   uint2* keyspill;                                // npub x kSpillKeys {record off, cum start}: 3..8-key publishes
   Record* out; uint64_t out_cap;                  // records mode
   vmqg_range* out_rng; uint64_t rng_cap;          // range mode (out_rng != null)
   uint32_t* status;                               // this call's counters: [0] deferred publishes,
                                                   // [1] of those, walked with a global stack, [2] scan ticket,
-                                                  // [3] publishes the records EMIT hands to the wave tier
+                                                  // [3] publishes EMIT hands to the wave tier (none today)
   uint32_t* status_next;                          // the next call's counters (zeroed by this call)
   uint32_t* err;                                  // error bits, sticky until vmqg_match_status
   uint32_t* deferred;                             // 2 x npub: publishes deferred by COUNT, then by EMIT
@@ -38,13 +40,12 @@ struct MatchArgs {
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
-constexpr uint32_t kOptLeanEmit = 2u;   // records EMIT by k_emit_records (multi-key publishes to the wave tier)
 
 // mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier (grid a.o_waves / 4)
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st);
 // counts in offsets[0, npub) -> exclusive offsets[0, npub] (one launch, look-back)
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st);
-uint32_t scan_tiles(uint64_t npub);
+uint32_t scan_tiles(uint64_t nchunks);   // look-back tiles of the chunk-total scan
 hipError_t launch_patches(uint8_t* arena, const void* d_patches, uint64_t n, hipStream_t st);
 
 }  // namespace vmqg

@@ -122,6 +122,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
   return v;
 }
 
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t t = __shfl_up(v, o, 64);
+    if (lane >= (uint32_t)o) v += t;
+  }
+  return v;
+}
+
 // ---------------------------------------------------------------- probes
 struct Bucket { uint4 s0, s1, s2, s3; };
 
@@ -435,22 +445,24 @@ __device__ __forceinline__ void store_range(vmqg_range* out, uint64_t i, uint32_
 }
 
 // ------------------------------------------------------------ COUNT pass
+// Returns the publish's count on the group's lane 0 (0 when deferred: the
+// wave tier adds it to the chunk total), 0 on the other lanes.
 template <int G, int OUT>
-__device__ void count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g) {
+__device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g) {
   const vmqg_pub pub = a.pubs[p];
   const Matched m = walk_publish<G>(a, pub, s, g);
   // 3..8 keys: the group copies its key list to the publish's spill slots
   const bool spill = !m.overflow && m.nk > 2 && m.nk <= VMQG_SPILL_KEYS;
   if (spill)
     for (uint32_t i = g.lane; i < m.nk; i += G) a.keyspill[(uint64_t)p * kSpillKeys + i] = s.ky(i);
-  if (g.lane != 0) return;
+  if (g.lane != 0) return 0;
   uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
   if (m.overflow) {   // the wave tier counts it (and writes offsets[p])
     const uint32_t idx = atomicAdd(&a.status[kStDeferred], 1u);
     a.deferred[idx] = p;   // the list holds npub entries
     a.offsets[p] = 0;
     kc[0] = make_uint4(0, kDeferred, 0, 0);
-    return;
+    return 0;
   }
   const uint32_t total = out_total<OUT>(m);
   a.offsets[p] = total;
@@ -468,6 +480,7 @@ __device__ void count_publish(const MatchArgs& a, uint32_t p, const FastScratch<
   } else {
     kc[0] = make_uint4(total, kRewalk, 0, 0);
   }
+  return total;
 }
 
 // ------------------------------------------------------------- EMIT pass
@@ -481,14 +494,13 @@ struct GroupMeta {
 
 // Resolve publish first + gidx of a wave: from the key cache, or by a
 // re-walk (> 8 keys).  Leaves the keys {off, cum start} in the group's LDS
-// key list.  ok = false: the wave tier writes it (or an error is latched).
+// key list; [obase, oend) is the publish's output range.  ok = false: the
+// wave tier writes it (or an error is latched).
 template <int G, int OUT>
 __device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
-                        uint32_t& nk, uint32_t& ksum, uint64_t& rmask, uint64_t& obase, uint64_t& oend) {
+                        uint32_t& nk, uint32_t& ksum, uint64_t& rmask, uint64_t obase, uint64_t oend) {
   const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
   const uint4 h = kc[0];
-  obase = a.offsets[p];
-  oend = a.offsets[p + 1];
   uint32_t total;
   if (h.y == kDeferred) return false;   // written by the wave tier
   if (h.y == kRewalk) {
@@ -513,6 +525,25 @@ __device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s,
   return true;
 }
 
+// Output ranges of the GPW publishes [first, first + n) of one chunk: the
+// chunk's base (the scanned chunk totals) plus the exclusive prefix of the
+// counts COUNT left in offsets[]; each group's lane 0 writes its publish's
+// final offset.  Returns the chunk base.
+template <int G, int GPW>
+__device__ __forceinline__ uint64_t chunk_offsets(const MatchArgs& a, uint32_t first, uint32_t n, const Group<G>& g,
+                                                  uint64_t& obase, uint64_t& oend) {
+  const uint32_t p = first + g.gidx;
+  const bool valid = g.gidx < n;
+  const uint64_t wbase = a.chunk[first / GPW];
+  const uint64_t cnt = valid ? a.offsets[p] : 0;
+  const uint64_t incl = wave_incl_scan64(g.lane == 0 ? cnt : 0);
+  const uint64_t excl = __shfl(incl - (g.lane == 0 ? cnt : 0), __lane_id() & ~(uint32_t)(G - 1), 64);
+  obase = wbase + excl;
+  oend = obase + cnt;
+  if (valid && g.lane == 0) a.offsets[p] = obase;
+  return wbase;
+}
+
 // Records mode: EMIT for the GPW consecutive publishes [first, first + n)
 // of one wave.  Resolve is per group; the copy is wave-wide over the wave's
 // output range minus the ranges of publishes the wave tier writes, so every
@@ -522,11 +553,12 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
                           const Group<G>& g, GroupMeta* gm, uint32_t slot0) {
   const uint32_t p = first + g.gidx;
   const bool valid = g.gidx < n;
+  uint64_t obase, oend;
+  const uint64_t wbase = chunk_offsets<G, GPW>(a, first, n, g, obase, oend);
   uint32_t nk = 0, ksum = 0;
-  uint64_t rmask = 0, obase = 0, oend = 0;
+  uint64_t rmask = 0;
   bool ok = false;
   if (valid) ok = resolve<G, 0>(a, p, s, g, nk, ksum, rmask, obase, oend);
-  const uint64_t wbase = a.offsets[first];
   // key-cache groups (<= 2 keys) copy from {off0, c0, off1} directly; the
   // record of a one-record key (a publish's own exact subscriber, say) is
   // loaded now, by every group at once, instead of as a lone HBM miss in
@@ -589,84 +621,13 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
   wave_sync();
 }
 
-// Records mode EMIT, lean variant (option "emit_lean"; no walk code: publishes whose key cache cannot serve
-// them — more than two keys, or deferred — are emitted by the wave tier).
-// A wave takes 64 R consecutive publishes, one per lane per round: key
-// cache + offsets -> an LDS table {rel, span, crel, off0, c0, off1, rmask};
-// then one copy over the wave's whole output range (minus the wave tier's
-// publishes), U records per lane in flight, 1 KiB per store instruction.
-// R rounds per copy keep the ragged tail of the copy short.
-struct EmitMeta { uint32_t rel, span, crel, off0, c0, off1, rm_lo, rm_hi; };
-
-template <bool NT, int U, int R>
-__global__ __launch_bounds__(256) void k_emit_records(MatchArgs a) {
-  constexpr uint32_t PW = 64 * R;   // publishes per wave and copy
-  __shared__ EmitMeta gm[kWaves][PW];
-  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
-  EmitMeta* M = gm[wv];
-  const uint32_t stride = gridDim.x * kWaves * PW;
-  for (uint32_t base = (blockIdx.x * kWaves + wv) * PW; base < a.npub; base += stride) {
-    const uint32_t n = a.npub - base < PW ? a.npub - base : PW;
-    const uint64_t wbase = a.offsets[base];
-    uint32_t tot = 0;
-#pragma unroll
-    for (int rr = 0; rr < R; rr++) {
-      const uint32_t i = rr * 64 + lane;
-      EmitMeta e{0, 0, 0, 0, 0, 0, 0, 0};
-      if (i < n) {
-        const uint32_t p = base + i;
-        const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
-        const uint4 h = kc[0];
-        const uint64_t ob = a.offsets[p], oe = a.offsets[p + 1];
-        e.rel = (uint32_t)(ob - wbase);
-        if (h.y == kRewalk || (h.y > 2 && h.y != kDeferred)) {
-          a.deferred[a.npub + atomicAdd(&a.status[kStRewalk], 1u)] = p;   // the wave tier emits it
-        } else if (h.y != kDeferred) {
-          const uint4 k = kc[1];
-          if (oe > a.out_cap) atomicOr(a.err, kErrOverflow);
-          else if (oe - ob != h.x) atomicOr(a.err, kErrMismatch);
-          else e = EmitMeta{e.rel, h.x, 0, k.x, k.y, k.z, h.z, h.w};
-        }
-      }
-      const uint32_t incl = wave_incl_scan32(e.span);
-      e.crel = tot + incl - e.span;
-      tot += __shfl(incl, 63, 64);
-      if (i < n) M[i] = e;
-    }
-    wave_sync();
-    uint32_t j = 0;
-    for (uint32_t r0 = lane; r0 < tot; r0 += 64 * U) {
-      uint4 v[U];
-      uint64_t dst[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t r = r0 + 64 * u;
-        if (r < tot) {
-          while (j + 1 < n && M[j + 1].crel <= r) j++;
-          const EmitMeta m = M[j];
-          const uint32_t q = r - m.crel;
-          const uint64_t rm = ((uint64_t)m.rm_hi << 32) | m.rm_lo;
-          const uint32_t ksum = m.span - (uint32_t)__popcll(rm);
-          if (q < m.c0) v[u] = *reinterpret_cast<const uint4*>(a.records + m.off0 + q);
-          else if (q < ksum) v[u] = *reinterpret_cast<const uint4*>(a.records + m.off1 + (q - m.c0));
-          else v[u] = make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rm, q - ksum), kNone, kNone, kNone);
-          dst[u] = wbase + m.rel + q;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++)
-        if (r0 + 64 * u < tot) store_rec<NT>(a.out, dst[u], v[u]);
-    }
-    wave_sync();
-  }
-}
-
 // Range mode: each group writes its publish's non-empty keys as
 // {record off, count}, then its remote nodes as {node, 0}.
 template <int G>
-__device__ void emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g) {
+__device__ void emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
+                                  uint64_t obase, uint64_t oend) {
   uint32_t nk = 0, ksum = 0;
-  uint64_t rmask = 0, obase = 0, oend = 0;
+  uint64_t rmask = 0;
   if (!resolve<G, 1>(a, p, s, g, nk, ksum, rmask, obase, oend)) return;
   uint32_t pos = 0;
   for (uint32_t k0 = 0; k0 < nk; k0 += G) {
@@ -707,11 +668,17 @@ void k_match_fast(MatchArgs a) {
   for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
     if (MODE == 0) {
-      if (g.gidx < n) count_publish<G, OUT>(a, base + g.gidx, s, g);
+      uint64_t c = 0;
+      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g);
+      // the chunk's total (publishes the wave tier takes add theirs later)
+      const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
+      if (__lane_id() == 0) a.chunk[base / GPW] = tot;
     } else if (OUT == 0) {
       emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
     } else {
-      if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g);
+      uint64_t ob, oe;
+      chunk_offsets<G, GPW>(a, base, n, g, ob, oe);
+      if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
     }
     wave_sync();
   }
@@ -960,18 +927,24 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
       if (!ok && lane == 0) atomicOr(a.err, kErrFrontier);
     }
     if (ok && lane == 0) {
-      if (MODE == 0) a.offsets[p] = total;
-      else if (total != oe - ob) atomicOr(a.err, kErrMismatch);
+      if (MODE == 0) {
+        a.offsets[p] = total;
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)total);
+      } else if (total != oe - ob) {
+        atomicOr(a.err, kErrMismatch);
+      }
     }
     wave_sync();
   }
 }
 
 // ------------------------------------------------------------------ scan
-// Exclusive scan of the per-publish counts in offsets[0, npub) into
-// offsets[0, npub] (offsets[npub] = total) in ONE launch: tiles of 4,096
-// taken by ticket, chained by a decoupled look-back.  Slot npub is never
-// read (no memset before the COUNT pass).
+// Exclusive scan of the per-chunk totals COUNT wrote (one chunk = the GPW
+// publishes one wave takes) into chunk bases, in ONE launch: tiles taken by
+// ticket, chained by a decoupled look-back; writes offsets[npub] = the batch
+// total.  EMIT turns a chunk base and its publishes' counts into their
+// offsets, so the per-publish counts are read and written once, by EMIT,
+// instead of by a scan pass of their own.
 #ifndef VMQG_SCAN_ITEMS
 #define VMQG_SCAN_ITEMS 16   // counts per thread (A/B: 4, 8, 16)
 #endif
@@ -981,9 +954,10 @@ __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
   __shared__ uint64_t part[kScanBlock];
   __shared__ uint32_t s_tile;
   __shared__ uint64_t s_base;
-  const uint64_t n = (uint64_t)a.npub + 1;
+  const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
+  const uint64_t n = (uint64_t)nchunks + 1;
   const uint32_t ntiles = (uint32_t)((n + kScanTile - 1) / kScanTile);
-  uint64_t* v = a.offsets;
+  uint64_t* v = a.chunk;
   for (;;) {
     if (threadIdx.x == 0) s_tile = atomicAdd(&a.status[kStTicket], 1u);
     __syncthreads();
@@ -993,7 +967,7 @@ __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
     uint64_t x[kScanItems];
     uint64_t acc = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < kScanItems; i++) { x[i] = base + i < a.npub ? v[base + i] : 0; acc += x[i]; }
+    for (uint32_t i = 0; i < kScanItems; i++) { x[i] = base + i < nchunks ? v[base + i] : 0; acc += x[i]; }
     part[threadIdx.x] = acc;
     __syncthreads();
     for (uint32_t o = 1; o < kScanBlock; o <<= 1) {
@@ -1011,13 +985,14 @@ __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
 #pragma unroll
     for (uint32_t i = 0; i < kScanItems; i++) {
       if (base + i < n) v[base + i] = run;
+      if (base + i == nchunks) a.offsets[a.npub] = run;   // the batch total
       run += x[i];
     }
     __syncthreads();
   }
 }
 
-uint32_t scan_tiles(uint64_t npub) { return (uint32_t)((npub + 1 + kScanTile - 1) / kScanTile); }
+uint32_t scan_tiles(uint64_t nchunks) { return (uint32_t)((nchunks + 1 + kScanTile - 1) / kScanTile); }
 
 // ---------------------------------------------------------------- patches
 __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uint32_t* patches, uint64_t n) {
@@ -1032,7 +1007,7 @@ __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uin
 static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
-  uint32_t g = scan_tiles(a.npub);
+  uint32_t g = scan_tiles((a.npub + a.gpw - 1) / a.gpw);
   if (g > 2048) g = 2048;
   k_scan_offsets<<<g, kScanBlock, 0, st>>>(a);
   return hipGetLastError();
@@ -1068,15 +1043,7 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) 
     if (g < 1) g = 1;
     if (mode == 0) { if (out) launch_fast<0, 1>(a, g, nt, st); else launch_fast<0, 0>(a, g, nt, st); }
     else if (out) launch_fast<1, 1>(a, g, nt, st);
-    else if (!(a.opts & kOptLeanEmit)) launch_fast<1, 0>(a, g, nt, st);
-    else {
-      constexpr int R = 2;
-      uint32_t ge = div_up(a.npub, kWaves * 64 * R);
-      if (ge > cap) ge = cap;
-      if (ge < 1) ge = 1;
-      if (nt) k_emit_records<true, VMQG_EMIT_U, R><<<ge, 256, 0, st>>>(a);
-      else k_emit_records<false, VMQG_EMIT_U, R><<<ge, 256, 0, st>>>(a);
-    }
+    else launch_fast<1, 0>(a, g, nt, st);
   } else {
     // reads its list length on the device (exits at once when empty); one
     // wave per deferred publish, each wave with its own global stack
