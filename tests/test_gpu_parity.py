@@ -106,6 +106,25 @@ def test_config_full_parity(cfg, mode):
     assert sum(len(x) for x in got) > n // 10   # the workload does match
 
 
+def test_store_policies_write_the_same_records():
+    """Both EMIT store policies (vmqg_set_option "nt_stores": non-temporal,
+    the default, and plain) write the same bytes; the default is checked
+    against the oracle by every other test."""
+    from vernemq_amd import workloads as W
+    w = W.CONFIGS["B"]()
+    v, orc = _load_both(w)
+    pubs, words = w.publish_arrays(v, 0, w.n_pubs)
+    outs = []
+    for sp in (1, 0):
+        v.set_option("nt_stores", sp)
+        recs, offs = v.match_arrays(pubs, words)
+        outs.append((np.asarray(offs).copy(), np.asarray(recs).view(np.uint8).copy()))
+    v.set_option("nt_stores", 1)
+    assert np.array_equal(outs[1][0], outs[0][0]), "offsets differ under plain stores"
+    assert np.array_equal(outs[1][1], outs[0][1]), "records differ under plain stores"
+    assert int(outs[0][0][-1]) > w.n_pubs // 10
+
+
 def test_config_c_full_size():
     """Config C at full size (1,000,064 subs, 2^20 publishes): every publish
     devices/{d}/telemetry/{m} emits the 64 wildcard subscribers plus c{d}
