@@ -505,6 +505,52 @@ def test_config_d_churn_parity(mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("fast_g", [2, 4])
+def test_output_offsets_of_a_large_deferral_heavy_batch(mode, fast_g):
+    """Output offsets over 300,000 publishes (9,375 chunks of 32 publishes,
+    18,750 of 16) where every 23rd is h/x/y/z, which 31 filters match (more
+    keys than the fast lists hold: deferred to the wave tier all over the
+    batch, its count added to its chunk's total after COUNT), the others
+    n/{j} matched by a few filters: every publish's count must equal the
+    oracle's, and a sample its records."""
+    import itertools
+    node = "n@h"
+    prod = _driver(node, mode)
+    prod.view.set_option("fast_g", fast_g)
+    orc = O.TrieOracle(node)
+    evs = []
+    hot = (b"h", b"x", b"y", b"z")
+    filters = set()
+    for combo in itertools.product([0, 1], repeat=4):
+        t = tuple(b"+" if c else hot[i] for i, c in enumerate(combo))
+        filters.add(t)
+        for k in range(4):
+            filters.add(t[:k] + (b"#",))
+    for i, t in enumerate(sorted(filters)):
+        evs.append(("updated", ("", b"f%d" % i), None, [(node, True, [(t, i % 3)])]))
+    for j in range(0, 1000, 2):
+        evs.append(("updated", ("", b"n%d" % j), None, [(node, True, [((b"n", b"%d" % j), 1)])]))
+    prod.apply(evs)
+    orc.apply(evs)
+    topics = [("", (b"n", b"%d" % j)) for j in range(1000)] + [("", hot)]
+    want = orc.fold_batch([(mp, b"pub", t) for mp, t in topics])
+    assert len(want[-1]) == len(filters) > 16
+    v = prod.view
+    arr, words = v.prepare(topics)
+    n = 300_000
+    idx = np.arange(n) % 1000
+    idx[::23] = 1000
+    recs, offs = prod.match_arrays(arr[idx], words)
+    assert v.stats_raw()["deferred_tier1"] == len(idx[::23])
+    counts = np.diff(offs.astype(np.int64))
+    assert int(offs[0]) == 0
+    assert np.array_equal(counts, np.array([len(x) for x in want], dtype=np.int64)[idx])
+    for i in list(range(0, n, 1999)) + list(range(n - 40, n)):
+        got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
+        assert got == sorted(want[idx[i]]), i
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_config_e_multitenant_parity(mode):
     """Config E shape at 1/500 scale (100k subs over 1,000 Zipf-sized
     mountpoints, 12-level topics, hot-topic skew): every publish vs the oracle."""

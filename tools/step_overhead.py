@@ -3,7 +3,7 @@
 library's kernel timing events on and off, and over batch sizes 2^17..2^21
 (the intercept of a least-squares line through them is the per-call cost
 that does not scale with the batch: launches, their gaps, empty wave-tier
-launches, the scan).  Interleaved rounds, one process, one JSON line."""
+launches, the scan), and the host time per call to enqueue it.  Interleaved rounds, one process, one JSON line."""
 import json
 import os
 import statistics
@@ -33,6 +33,7 @@ def main():
     sizes = [1 << 17, 1 << 18, 1 << 19, 1 << 20, 1 << 21]
     variants = [(n, t) for n in sizes for t in (0, 1)]
     res = {str(x): [] for x in variants}
+    enq = {str(x): [] for x in variants}   # host time per call to enqueue (no sync)
     steps = 20
     for _ in range(5):
         for n, t in variants:
@@ -43,12 +44,14 @@ def main():
             t0 = time.perf_counter()
             for _ in range(steps):
                 v.match_device(d_pubs.data_ptr(), n, d_words.data_ptr(), d_out.data_ptr(), cap, d_offs.data_ptr(), sp)
+            t1 = time.perf_counter()
             torch.cuda.synchronize()
             res[str((n, t))].append((time.perf_counter() - t0) / steps * 1e6)
+            enq[str((n, t))].append((t1 - t0) / steps * 1e6)
             v.set_timing(False)
     assert v.match_status(sp) == 0
     med = {k: statistics.median(x) for k, x in res.items()}
-    out = {"config": "C", "step_us": med}
+    out = {"config": "C", "step_us": med, "host_enqueue_us": {k: statistics.median(x) for k, x in enq.items()}}
     for t in (0, 1):
         xs = np.array(sizes, dtype=float)
         ys = np.array([med[str((n, t))] for n in sizes])

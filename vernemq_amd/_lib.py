@@ -23,7 +23,8 @@ SOURCES = [os.path.join(HERE, "csrc", f) for f in
             "vmqa_engine.cpp", "vmqa_abi.cpp", "vmqa_kernels.hip",
             "vmqs_abi.cpp", "vmqs_kernels.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in
-                  ("vmqg_common.h", "vmqg_engine.h", "vmqg_kernels.h", "vmqg_lookback.h",
+                  ("vmqg_common.h", "vmqg_engine.h", "vmqg_kernels.h", "vmqg_lookback.h", "vmqg_chain.h",
+                   "vmqg_nullorder.h",
                    "vmqr_engine.h", "vmqa_engine.h", "vmqs_engine.h")] + HEADERS
 
 # ---- status codes / constants (vmqg.h)

@@ -1,6 +1,7 @@
 // ACL checker host engine (see vmqa_engine.h).  Citations are to
 // apps/vmq_acl/src/vmq_acl.erl unless noted.
 #include "vmqa_engine.h"
+#include "vmqg_chain.h"
 
 #include <algorithm>
 #include <cstring>
@@ -145,7 +146,7 @@ int AclEngine::upload() {
   if (!has_device) return VMQG_OK;
   hipSetDevice(device);
   // tables must not change under a check still reading them
-  if (hipStreamWaitEvent(stream, ev_done, 0) != hipSuccess) return VMQG_E_DEVICE;
+  if (vmqg::chain_order(ev_done, chk_stream, stream) != VMQG_OK) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
   if (d_arena_bytes < image.size()) {
     if (d_arena) hipFree(d_arena);
@@ -164,6 +165,7 @@ int AclEngine::check_device(const vmqa_req* d_reqs, uint32_t n, const uint32_t* 
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
   if (!st) st = stream;
+  if (vmqg::chain_order(ev_done, chk_stream, st) != VMQG_OK) return VMQG_E_DEVICE;
   if (hipMemsetAsync(d_status, 0, 32, st) != hipSuccess) return VMQG_E_DEVICE;
   if (n == 0) return VMQG_OK;
   AArgs a{};
@@ -180,7 +182,6 @@ int AclEngine::check_device(const vmqa_req* d_reqs, uint32_t n, const uint32_t* 
   if (timing) for (auto& x : e) hipEventCreate(&x);
   if (launch_acl_check(a, st, e[0], e[1]) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) t_check.push_back({e[0], e[1]});
-  if (hipEventRecord(ev_done, st) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
 

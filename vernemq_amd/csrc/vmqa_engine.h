@@ -61,7 +61,8 @@ struct AclEngine {
   uint64_t n_rules = 0, n_users = 0, loads = 0;
   // device
   hipStream_t stream = nullptr;
-  hipEvent_t ev_done = nullptr;
+  hipEvent_t ev_done = nullptr;        // uploads and checks chain across streams (vmqg_chain.h)
+  hipStream_t chk_stream = nullptr;
   hipEvent_t ev_null = nullptr;   // NullOrder (vmqg_nullorder.h)
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
   uint32_t* d_status = nullptr;

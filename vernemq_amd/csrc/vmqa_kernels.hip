@@ -14,6 +14,7 @@
 // the first 4 topic words sit in registers; a lane that has its verdict
 // idles until the wave's last lane has one.  Integer compares only, no MFMA; bound by the rule
 // and topic word loads (L2-resident tables).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "vmqa_engine.h"
@@ -117,14 +118,13 @@ __global__ __launch_bounds__(256) void k_acl_check(AArgs a) {
   if (live) a.out[r] = allowed ? 1 : 0;
 }
 
+// e0 / e1 (both or neither): recorded by the dispatch itself
 hipError_t launch_acl_check(const AArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-  if (e0) hipEventRecord(e0, st);
   const uint32_t g = (a.n + 255) / 256;
   if (a.fixed_words <= kFixedLdsWords)
-    k_acl_check<true><<<g, 256, (size_t)a.fixed_words * 4, st>>>(a);
+    hipExtLaunchKernelGGL(k_acl_check<true>, dim3(g), dim3(256), (uint32_t)a.fixed_words * 4, st, e0, e1, 0, a);
   else
-    k_acl_check<false><<<g, 256, 0, st>>>(a);
-  if (e1) hipEventRecord(e1, st);
+    hipExtLaunchKernelGGL(k_acl_check<false>, dim3(g), dim3(256), 0, st, e0, e1, 0, a);
   return hipGetLastError();
 }
 

@@ -325,11 +325,9 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
   }
   e.lay = L;
   // after the matches already queued, before the ones queued later
-  if (hipStreamWaitEvent(st, e.ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
+  if (e.order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
   if (hipMemcpyAsync(e.d_arena, d_src, L.total_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return VMQG_E_DEVICE;
-  if (hipEventRecord(e.ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
-  e.ev_stream = st;
   e.epoch++;
   return VMQG_OK;
 }
@@ -366,11 +364,9 @@ int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t byt
   vmqg::NullOrder order(stream, e.stream, e.ev_null);
   // tables change only after the matches queued before, and matches queued
   // later (on any stream) see the patches
-  if (hipStreamWaitEvent(st, e.ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
+  if (e.order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
   if (vmqg::launch_patches(e.d_arena, d_patches, bytes / sizeof(vmqg::Patch), st) != hipSuccess)
     return VMQG_E_DEVICE;
-  if (hipEventRecord(e.ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
-  e.ev_stream = st;
   e.epoch++;
   return VMQG_OK;
 }

@@ -1,0 +1,28 @@
+// One ordering chain across the streams a context's work is queued on.
+//
+// Table changes and matches (or selects, checks) must not overtake each
+// other, whichever caller streams they are queued on.  Instead of recording
+// an event after every call (a marker between two calls on one stream costs
+// the GPU ~27 us of idle time per call on MI355X,
+// profiles/step_overhead_r02_*), the context remembers the stream it queued
+// on last; work about to be queued on another stream first records `ev` on
+// that one and waits for it.  So an event is recorded only when the stream
+// changes, and the chain property holds: each piece of work is ordered
+// after everything queued before it on any stream.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/vmqg.h"
+
+namespace vmqg {
+
+inline int chain_order(hipEvent_t ev, hipStream_t& last, hipStream_t st) {
+  if (last && st != last) {
+    if (hipEventRecord(ev, last) != hipSuccess) return VMQG_E_DEVICE;
+    if (hipStreamWaitEvent(st, ev, 0) != hipSuccess) return VMQG_E_DEVICE;
+  }
+  last = st;
+  return VMQG_OK;
+}
+
+}  // namespace vmqg

@@ -2,6 +2,7 @@
 // the device-image mirror.  See vmqg_engine.h for the data model; every
 // state-machine function cites the Erlang clause it reproduces
 // (apps/vmq_server/src/vmq_reg_trie.erl unless noted).
+#include "vmqg_chain.h"
 #include "vmqg_engine.h"
 
 #include <algorithm>
@@ -882,12 +883,11 @@ int Engine::upload() {
   }
   if (!has_device) { full_image = false; return VMQG_OK; }
   hipSetDevice(device);
-  // tables must not change under a match still reading them (matches on
-  // caller streams are ordered through ev_match_done)
-  if (hipStreamWaitEvent(stream, ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
+  // tables must not change under a match still reading them (queued on any
+  // stream: order_on chains them)
+  if (order_on(stream) != VMQG_OK) return VMQG_E_DEVICE;
   if (full_image) {
     if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
-    if (hipEventSynchronize(ev_match_done) != hipSuccess) return VMQG_E_DEVICE;
     if (d_arena_bytes < lay.total_bytes) {
       if (d_arena) hipFree(d_arena);
       d_arena = nullptr; d_arena_bytes = 0;
@@ -925,11 +925,11 @@ int Engine::upload() {
   if (launch_patches(d_arena, sg.d, np, stream) != hipSuccess) return VMQG_E_DEVICE;
   if (hipEventRecord(sg.ev, stream) != hipSuccess) return VMQG_E_DEVICE;
   sg.used = true;
-  // later matches on other streams must see the patches
-  if (hipEventRecord(ev_match_done, stream) != hipSuccess) return VMQG_E_DEVICE;
-  ev_stream = stream;
   return VMQG_OK;
 }
+
+// Table changes and matches form one chain across streams (vmqg_chain.h).
+int Engine::order_on(hipStream_t st) { return chain_order(ev_match_done, ev_stream, st); }
 
 int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
   if (npub > keycache_cap || npub > deferred_cap) {
@@ -1026,10 +1026,9 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   if (!d_arena) return VMQG_E_STATE;
   hipSetDevice(device);
   if (!st) st = stream;
-  // patches / images queued on the context stream land before this match
   // table changes (patches, images) land before this match: the primary's on
   // the context stream, a replica's on whatever stream the caller gave
-  if (st != ev_stream && hipStreamWaitEvent(st, ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
+  if (order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
   if (npub == 0) return hipMemsetAsync(d_offsets, 0, 8, st) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
   int rc;
   if ((rc = ensure_match_scratch(npub, st)) || (rc = ensure_lookback(scan_tiles((npub + 15) / 16), st)) ||
@@ -1040,23 +1039,21 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   a.out_rng = d_rng; a.rng_cap = rng_cap;
   last_set = call_seq & 1;
   call_seq++;
+  // kernel timing (vmqg_set_timing): events written by the fast-tier
+  // dispatches themselves, so timing adds no marker packets between launches
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
   if (timing) {
     hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2); hipEventCreate(&e3);
-    hipEventRecord(e0, st);
+    t_count.push_back({e0, e1});
+    t_emit.push_back({e2, e3});
   }
   // COUNT: fast groups, then the wave tier for what they deferred
-  if (launch_match(a, 0, 0, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (timing) hipEventRecord(e1, st);
+  if (launch_match(a, 0, 0, st, e0, e1) != hipSuccess) return VMQG_E_DEVICE;
   if (launch_match(a, 0, 1, st) != hipSuccess) return VMQG_E_DEVICE;
   if (launch_scan(a, st) != hipSuccess) return VMQG_E_DEVICE;
   // EMIT: same tiers
-  if (timing) hipEventRecord(e2, st);
-  if (launch_match(a, 1, 0, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (timing) { hipEventRecord(e3, st); t_count.push_back({e0, e1}); t_emit.push_back({e2, e3}); }
+  if (launch_match(a, 1, 0, st, e2, e3) != hipSuccess) return VMQG_E_DEVICE;
   if (launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
-  ev_stream = st;
   return VMQG_OK;
 }
 

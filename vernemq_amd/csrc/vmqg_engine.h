@@ -214,8 +214,8 @@ struct Engine {
   void* d_words = nullptr; uint64_t d_words_cap = 0;
   void* d_offs = nullptr; uint64_t d_offs_cap = 0;
   void* d_out = nullptr; uint64_t d_out_cap = 0;
-  hipEvent_t ev_match_done = nullptr;
-  hipStream_t ev_stream = nullptr;   // the stream ev_match_done was last recorded on
+  hipEvent_t ev_match_done = nullptr;   // recorded by order_on when the stream changes
+  hipStream_t ev_stream = nullptr;      // the stream table changes / matches were last queued on
   hipEvent_t ev_null = nullptr;      // NullOrder (vmqg_nullorder.h)
   bool timing = false;
   uint32_t opt_fast_g = 2, opt_flags = kOptNtStores;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
@@ -278,6 +278,7 @@ struct Engine {
 
   // device
   int upload();
+  int order_on(hipStream_t st);
   int ensure_match_scratch(uint64_t npub, hipStream_t st);
   int ensure_lookback(uint64_t granules, hipStream_t st);
   int ensure_wave_scratch(hipStream_t st);

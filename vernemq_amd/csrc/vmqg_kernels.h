@@ -41,8 +41,11 @@ struct MatchArgs {
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
 
-// mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier (grid a.o_waves / 4)
-hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st);
+// mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier (grid a.o_waves / 4).
+// t0 / t1 (both or neither): timing events recorded by the kernel's own
+// dispatch (hipExtLaunchKernel), not by marker packets between launches.
+hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, hipEvent_t t0 = nullptr,
+                        hipEvent_t t1 = nullptr);
 // counts in offsets[0, npub) -> exclusive offsets[0, npub] (one launch, look-back)
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st);
 uint32_t scan_tiles(uint64_t nchunks);   // look-back tiles of the chunk-total scan

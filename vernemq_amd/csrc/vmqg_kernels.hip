@@ -33,6 +33,7 @@
 // wave tiers).  Output is either the 16-B records (lookup_subs + fold__,
 // :87-98) or, in range mode, one 8-B {record off, count} per non-empty
 // subscriber-list key plus {node, 0} per remote node.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "vmqg_common.h"
@@ -1013,14 +1014,20 @@ hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int MODE, int OUT, int G, bool NT>
+static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  if (t0) hipExtLaunchKernelGGL(k_match_fast<MODE, OUT, G, NT>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+  else k_match_fast<MODE, OUT, G, NT><<<g, 256, 0, st>>>(a);
+}
+
 template <int MODE, int OUT>
-static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st) {
+static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   if (a.fast_g == 4) {
-    if (nt) k_match_fast<MODE, OUT, 4, true><<<g, 256, 0, st>>>(a);
-    else k_match_fast<MODE, OUT, 4, false><<<g, 256, 0, st>>>(a);
+    if (nt) launch_fast_k<MODE, OUT, 4, true>(a, g, st, t0, t1);
+    else launch_fast_k<MODE, OUT, 4, false>(a, g, st, t0, t1);
   } else {
-    if (nt) k_match_fast<MODE, OUT, 2, true><<<g, 256, 0, st>>>(a);
-    else k_match_fast<MODE, OUT, 2, false><<<g, 256, 0, st>>>(a);
+    if (nt) launch_fast_k<MODE, OUT, 2, true>(a, g, st, t0, t1);
+    else launch_fast_k<MODE, OUT, 2, false>(a, g, st, t0, t1);
   }
 }
 
@@ -1030,7 +1037,7 @@ static void launch_wave(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st)
   else k_match_wave<MODE, OUT, false><<<g, 256, 0, st>>>(a);
 }
 
-hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) {
+hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   const bool nt = (a.opts & kOptNtStores) != 0;
   const int out = a.out_rng ? 1 : 0;
   if (tier == 0) {
@@ -1041,9 +1048,9 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st) 
     const uint32_t cap = (uint32_t)a.cus * (bpc ? bpc : 8u);
     if (g > cap) g = cap;
     if (g < 1) g = 1;
-    if (mode == 0) { if (out) launch_fast<0, 1>(a, g, nt, st); else launch_fast<0, 0>(a, g, nt, st); }
-    else if (out) launch_fast<1, 1>(a, g, nt, st);
-    else launch_fast<1, 0>(a, g, nt, st);
+    if (mode == 0) { if (out) launch_fast<0, 1>(a, g, nt, st, t0, t1); else launch_fast<0, 0>(a, g, nt, st, t0, t1); }
+    else if (out) launch_fast<1, 1>(a, g, nt, st, t0, t1);
+    else launch_fast<1, 0>(a, g, nt, st, t0, t1);
   } else {
     // reads its list length on the device (exits at once when empty); one
     // wave per deferred publish, each wave with its own global stack

@@ -1,6 +1,7 @@
 // Retained store host engine (see vmqr_engine.h).  Citations are to
 // apps/vmq_server/src/vmq_retain_srv.erl unless noted.
 #include "vmqr_engine.h"
+#include "vmqg_chain.h"
 
 #include <algorithm>
 #include <cstring>
@@ -21,8 +22,8 @@ RetainEngine::~RetainEngine() {
   if (!has_device) return;
   hipSetDevice(device);
   if (stream) hipStreamSynchronize(stream);
-  for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
-  for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
+  for (auto* v : {&t_count, &t_scan, &t_emit})
+    for (auto& e : *v) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (ev_match_done) hipEventDestroy(ev_match_done);
   if (ev_null) hipEventDestroy(ev_null);
   hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_tickets); hipFree(d_plan); hipFree(d_lookback);
@@ -380,7 +381,7 @@ int RetainEngine::upload() {
   if (!has_device) { full_image = false; return VMQG_OK; }
   hipSetDevice(device);
   // tables must not change under a match still reading them
-  if (hipStreamWaitEvent(stream, ev_match_done, 0) != hipSuccess) return VMQG_E_DEVICE;
+  if (order_on(stream) != VMQG_OK) return VMQG_E_DEVICE;
   if (full_image) {
     if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
     if (d_arena_bytes < lay.total_bytes) {
@@ -424,8 +425,10 @@ int RetainEngine::match_device(const vmqg_pub* d_filters, uint32_t nf, const uin
   hipSetDevice(device);
   if (!st) st = stream;
   // match_fold must not read tables a pending patch upload is writing: the
-  // context's stream is synchronised at the end of every apply.  The status
-  // words and the walk tickets are zeroed by k_rt_plan (no memset launches).
+  // context's stream is synchronised at the end of every apply; later
+  // applies wait for this match (order_on).  The status words and the walk
+  // tickets are zeroed by k_rt_plan (no memset launches).
+  if (order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
   if (nf == 0) {
     if (hipMemsetAsync(d_status, 0, 32, st) != hipSuccess) return VMQG_E_DEVICE;
     return hipMemsetAsync(d_offsets, 0, 8, st) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
@@ -461,13 +464,15 @@ int RetainEngine::match_device(const vmqg_pub* d_filters, uint32_t nf, const uin
   a.out = d_out; a.out_cap = out_cap; a.offsets = d_offsets;
   a.status = d_status; a.lookback = d_lookback; a.lb_tag = lb_tag; a.tile_cap = lookback_cap;
   a.tickets = d_tickets;
-  hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t e[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (timing) for (auto& x : e) hipEventCreate(&x);
-  if (launch_retain_match(a, (uint32_t)walk_grid, st, e[0], e[1], e[2], e[3]) != hipSuccess) return VMQG_E_DEVICE;
-  if (timing) { t_count.push_back({e[0], e[1]}); t_emit.push_back({e[2], e[3]}); }
-  if (hipEventRecord(ev_match_done, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_retain_match(a, (uint32_t)walk_grid, st, timing ? e : nullptr) != hipSuccess) return VMQG_E_DEVICE;
+  if (timing) { t_count.push_back({e[0], e[1]}); t_scan.push_back({e[2], e[3]}); t_emit.push_back({e[4], e[5]}); }
   return VMQG_OK;
 }
+
+// Patches and matches form one chain across streams (vmqg_chain.h).
+int RetainEngine::order_on(hipStream_t st) { return vmqg::chain_order(ev_match_done, ev_stream, st); }
 
 int RetainEngine::grow_tiles(uint64_t rows, hipStream_t st) {
   const uint64_t want = std::max<uint64_t>(rows / kTileRows + 2, (plan_cap + 4095) / 4096 + 2);
@@ -505,15 +510,15 @@ int RetainEngine::match_status(hipStream_t st) {
 void RetainEngine::collect_times() {
   if (!has_device) return;
   for (size_t i = 0; i < t_count.size(); i++) {
-    float a = 0, b = 0;
+    float a = 0, a2 = 0, b = 0;
     hipEventSynchronize(t_emit[i].second);
     hipEventElapsedTime(&a, t_count[i].first, t_count[i].second);
+    hipEventElapsedTime(&a2, t_scan[i].first, t_scan[i].second);
     hipEventElapsedTime(&b, t_emit[i].first, t_emit[i].second);
-    sum_count_ns += a * 1e6; sum_emit_ns += b * 1e6; n_timed++;
-    hipEventDestroy(t_count[i].first); hipEventDestroy(t_count[i].second);
-    hipEventDestroy(t_emit[i].first); hipEventDestroy(t_emit[i].second);
+    sum_count_ns += (a + a2) * 1e6; sum_emit_ns += b * 1e6; n_timed++;
+    for (auto* v : {&t_count, &t_scan, &t_emit}) { hipEventDestroy((*v)[i].first); hipEventDestroy((*v)[i].second); }
   }
-  t_count.clear(); t_emit.clear();
+  t_count.clear(); t_scan.clear(); t_emit.clear();
 }
 
 std::string RetainEngine::dump() {

@@ -87,8 +87,8 @@ struct RArgs {
 };
 constexpr uint32_t kTicketStride = 64;   // u32: 256 B between the counters
 int walk_blocks_per_cu();   // resident blocks of the walk kernel per CU (the walk grid)
-hipError_t launch_retain_match(const RArgs& a, uint32_t grid, hipStream_t st, hipEvent_t e_count0,
-                               hipEvent_t e_count1, hipEvent_t e_emit0, hipEvent_t e_emit1);
+// t: null, or {start, stop} events of the plan, the scan and the walk (6)
+hipError_t launch_retain_match(const RArgs& a, uint32_t grid, hipStream_t st, const hipEvent_t* t);
 
 uint64_t retain_fp(uint32_t mp, const uint32_t* w, uint32_t L);
 
@@ -135,7 +135,8 @@ struct RetainEngine {
   // device
   hipStream_t stream = nullptr;
   hipEvent_t ev_null = nullptr;   // NullOrder (vmqg_nullorder.h)
-  hipEvent_t ev_match_done = nullptr;
+  hipEvent_t ev_match_done = nullptr;   // recorded by order_on when the stream changes
+  hipStream_t ev_stream = nullptr;      // the stream patches / matches were last queued on
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
   Patch* h_patch = nullptr; uint64_t h_patch_cap = 0;
   Patch* d_patch = nullptr; uint64_t d_patch_cap = 0;
@@ -152,7 +153,7 @@ struct RetainEngine {
   void* d_offs = nullptr; uint64_t d_offs_cap = 0;
   int cu_count = 256;
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_emit;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_scan, t_emit;   // plan, scan, walk
   double sum_count_ns = 0, sum_emit_ns = 0; uint64_t n_timed = 0;
   std::string dump_text;
 
@@ -165,6 +166,7 @@ struct RetainEngine {
   int match_status(hipStream_t st);
   int grow_tiles(uint64_t rows, hipStream_t st);   // look-back granules for a walk over `rows`
   void collect_times();
+  int order_on(hipStream_t st);
   std::string dump();
 
  private:

@@ -26,6 +26,7 @@
 //               pass, no second scan.
 // Bound: HBM / L2 reads of 16-B rows, their words and the 4-B list entries;
 // no MFMA (integer compares only).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "vmqr_engine.h"
@@ -404,18 +405,23 @@ int walk_blocks_per_cu() {
   return nb;
 }
 
-hipError_t launch_retain_match(const RArgs& a, uint32_t grid, hipStream_t st, hipEvent_t ec0, hipEvent_t ec1,
-                               hipEvent_t ee0, hipEvent_t ee1) {
-  if (ec0) hipEventRecord(ec0, st);
+// t[0..6) (all or none): {start, stop} of the plan, the scan and the walk,
+// recorded by the dispatches themselves (hipExtLaunchKernel) rather than by
+// marker packets between the launches
+hipError_t launch_retain_match(const RArgs& a, uint32_t grid, hipStream_t st, const hipEvent_t* t) {
   const uint32_t gp = (a.nf + 255) / 256;
-  k_rt_plan<<<gp < 2048 ? gp : 2048, 256, 0, st>>>(a);
   const uint32_t gs = (uint32_t)((a.nf + 1 + kST) / kST);
-  k_rt_scan<<<gs < 2048 ? gs : 2048, kSB, 0, st>>>(a.rpfx, a.nf, nullptr, a.status + 3, a.lookback, a.lb_tag,
-                                                   a.status);
-  if (ec1) hipEventRecord(ec1, st);
-  if (ee0) hipEventRecord(ee0, st);
-  k_rt_walk<<<grid, 256, 0, st>>>(a);
-  if (ee1) hipEventRecord(ee1, st);
+  if (t) {
+    hipExtLaunchKernelGGL(k_rt_plan, dim3(gp < 2048 ? gp : 2048), dim3(256), 0, st, t[0], t[1], 0, a);
+    hipExtLaunchKernelGGL(k_rt_scan, dim3(gs < 2048 ? gs : 2048), dim3(kSB), 0, st, t[2], t[3], 0, a.rpfx,
+                          (uint64_t)a.nf, (const uint64_t*)nullptr, a.status + 3, a.lookback, a.lb_tag, a.status);
+    hipExtLaunchKernelGGL(k_rt_walk, dim3(grid), dim3(256), 0, st, t[4], t[5], 0, a);
+  } else {
+    k_rt_plan<<<gp < 2048 ? gp : 2048, 256, 0, st>>>(a);
+    k_rt_scan<<<gs < 2048 ? gs : 2048, kSB, 0, st>>>(a.rpfx, a.nf, nullptr, a.status + 3, a.lookback, a.lb_tag,
+                                                     a.status);
+    k_rt_walk<<<grid, 256, 0, st>>>(a);
+  }
   return hipGetLastError();
 }
 

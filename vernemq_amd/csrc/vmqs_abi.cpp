@@ -5,6 +5,7 @@
 #include <new>
 
 #include "vmqs_engine.h"
+#include "vmqg_chain.h"
 #include "vmqg_nullorder.h"
 
 namespace vmqs {
@@ -31,7 +32,6 @@ int SelEngine::init(const vmqs_config& c) {
   if (hipMalloc(&d_status, 64) != hipSuccess) return VMQG_E_NOMEM;
   if (hipEventCreateWithFlags(&ev_sel, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
   if (hipMemsetAsync(d_status, 0, 64, stream) != hipSuccess) return VMQG_E_DEVICE;
-  if (hipEventRecord(ev_sel, stream) != hipSuccess) return VMQG_E_DEVICE;
   return hipStreamSynchronize(stream) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
 }
 
@@ -47,8 +47,8 @@ int SelEngine::set_states(const uint32_t* subs, const uint8_t* st, size_t n) {
   for (size_t i = 0; i < n; i++) h_states[subs[i]] = st[i];
   hipSetDevice(device);
   // selects still running on any stream read the old table: the copy (and a
-  // free of the old buffer) waits for the last one
-  if (hipStreamWaitEvent(stream, ev_sel, 0) != hipSuccess) return VMQG_E_DEVICE;
+  // free of the old buffer) waits for them
+  if (vmqg::chain_order(ev_sel, sel_stream, stream) != VMQG_OK) return VMQG_E_DEVICE;
   if (top > states_cap) {
     uint64_t c = 4096;
     while (c < top) c <<= 1;
@@ -72,6 +72,7 @@ int SelEngine::select_device(const vmqg_emit* d_emits, const uint64_t* d_offsets
   if (policy > VMQS_POLICY_LOCAL_ONLY) return VMQG_E_INVAL;
   hipSetDevice(device);
   if (!st) st = stream;
+  if (vmqg::chain_order(ev_sel, sel_stream, st) != VMQG_OK) return VMQG_E_DEVICE;
   if (npub > defer_cap) {
     uint64_t c = 1024;
     while (c < npub) c <<= 1;
@@ -93,7 +94,6 @@ int SelEngine::select_device(const vmqg_emit* d_emits, const uint64_t* d_offsets
   if (timing) for (auto& x : e) hipEventCreate(&x);
   if (launch_select(a, st, e[0], e[1]) != hipSuccess) return VMQG_E_DEVICE;
   if (timing) t_sel.push_back({e[0], e[1]});
-  if (hipEventRecord(ev_sel, st) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
 

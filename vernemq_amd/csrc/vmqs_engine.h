@@ -55,7 +55,8 @@ struct SelEngine {
   std::vector<uint8_t> h_states;   // host copy of the state table
   uint32_t* d_status = nullptr;
   hipEvent_t ev_null = nullptr;   // NullOrder (vmqg_nullorder.h)
-  hipEvent_t ev_sel = nullptr;     // after the last select (any stream): state-table updates wait on it
+  hipEvent_t ev_sel = nullptr;     // state-table updates and selects chain across streams (vmqg_chain.h)
+  hipStream_t sel_stream = nullptr;
   uint32_t* d_defer = nullptr; uint64_t defer_cap = 0;
   void* d_e = nullptr; uint64_t d_e_cap = 0;   // host-buffer staging
   void* d_o = nullptr; uint64_t d_o_cap = 0;

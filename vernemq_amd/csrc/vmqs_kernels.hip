@@ -30,6 +30,7 @@
 // SS workload), but the kernel runs at ~36 % of the HBM peak: it is
 // latency-bound per wave (load -> LDS claim -> reduction -> bitmap ->
 // write), see DESIGN.md "Shared-subscription dispatch".
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "vmqs_engine.h"
@@ -334,13 +335,19 @@ __global__ __launch_bounds__(256) void k_select_block(SArgs a) {
   }
 }
 
+// e0 / e1: start of the wave tier, end of the block tier, recorded by the
+// dispatches themselves (no marker packets between launches)
 hipError_t launch_select(const SArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-  if (e0) hipEventRecord(e0, st);
-  if (a.npub) {
-    k_select_wave<<<(a.npub + kWaves - 1) / kWaves, 256, 0, st>>>(a);
+  const uint32_t g = (a.npub + kWaves - 1) / kWaves;
+  if (!a.npub) {
+    if (e0) { hipEventRecord(e0, st); hipEventRecord(e1, st); }
+  } else if (e0) {
+    hipExtLaunchKernelGGL(k_select_wave, dim3(g), dim3(256), 0, st, e0, (hipEvent_t) nullptr, 0, a);
+    hipExtLaunchKernelGGL(k_select_block, dim3(kBlockGrid), dim3(256), 0, st, (hipEvent_t) nullptr, e1, 0, a);
+  } else {
+    k_select_wave<<<g, 256, 0, st>>>(a);
     k_select_block<<<kBlockGrid, 256, 0, st>>>(a);
   }
-  if (e1) hipEventRecord(e1, st);
   return hipGetLastError();
 }
 
