@@ -79,10 +79,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP events (profiling runs)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end figure")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="C: time unpipelined vmqg_match_device calls only (default: vmqg_match_submit, each "
-                         "batch's COUNT mixed with the previous batch's EMIT; the unpipelined figure is reported "
-                         "beside it)")
     ap.add_argument("--config", default="C", choices=["A", "B", "C", "D", "E", "R1", "R2", "RT", "AC", "SS"],
                     help="C: headline (1M subs); D: 10M subs with $share groups under 1%%/s churn; "
                          "A, B, E, R1, R2: the other SURVEY §8d shapes (secondary lines); "
@@ -165,89 +161,45 @@ def main():
     d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
     d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
     out_cap = (w.notes["n_wild"] + 1) * npub
-    # two output sets: a pipelined batch's outputs stay untouched until the
-    # next submit has EMITted it (include/vmqg.h), so consecutive steps alternate
-    d_outs = [torch.empty(out_cap * 4, dtype=torch.int32, device=dev) for _ in range(2)]
-    d_offss = [torch.zeros(npub + 1, dtype=torch.int64, device=dev) for _ in range(2)]
-    d_out, d_offs = d_outs[0], d_offss[0]
+    d_out = torch.empty(out_cap * 4, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(npub + 1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
-    pipelined = not args.no_pipeline
-    nstep = [0]
 
     def step():
         view.match_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_out.data_ptr(), out_cap,
                           d_offs.data_ptr(), sp)
 
-    def submit():
-        k = nstep[0] & 1
-        nstep[0] += 1
-        view.match_submit(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_outs[k].data_ptr(), out_cap,
-                          d_offss[k].data_ptr(), sp)
-
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    rc = view.match_status(sp)
+    if rc != 0:
+        raise RuntimeError("match status %d after warmup" % rc)
     # size-independent parity check of the step's output (every publish: 64
     # wildcard subscribers + its own device subscriber when d < n_dev)
     d_idx = w.pw[1::4] - 18
     want = np.where(d_idx < args.n_dev, w.notes["n_wild"] + 1, w.notes["n_wild"])
+    got = np.diff(d_offs.cpu().numpy())
+    verified = bool(np.array_equal(got, want))
+    if not verified:
+        raise RuntimeError("per-publish emission counts differ from config C's known answer")
 
-    def verify(tag):
-        for o in (d_offss if pipelined else [d_offs]):
-            if not np.array_equal(np.diff(o.cpu().numpy()), want):
-                raise RuntimeError("%s: per-publish emission counts differ from config C's known answer" % tag)
-
-    def timed(fn, steps, pipe):
-        # `steps` whole batches: in the pipeline the first submit COUNTs
-        # alone and the final flush EMITs the last batch, both inside the
-        # timed region, so it holds every batch's COUNT and EMIT
-        view.set_timing(not args.no_timing)
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            fn()
-        if pipe:
-            view.match_flush()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        if dist:
-            dist.barrier()
-        rc = view.match_status(sp)
-        if rc != 0:
-            raise RuntimeError("match status %d in timed region" % rc)
-        return el
-
-    for _ in range(args.warmup):
-        (submit if pipelined else step)()
+    view.set_timing(not args.no_timing)
+    if dist:
+        dist.barrier()
     torch.cuda.synchronize()
-    rc = view.match_status(sp)   # (flushes a pending batch)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    rc = view.match_status(sp)
     if rc != 0:
-        raise RuntimeError("match status %d after warmup" % rc)
-    verify("warmup")
-    verified = True
-
-    unpiped = None
-    if pipelined:
-        # the unpipelined calls on the same batch, reported beside the value
-        for _ in range(max(1, args.warmup)):
-            step()
-        el_u = timed(step, args.steps, False)
-        count_ns, emit_ns, _ = view.kernel_times() if not args.no_timing else (0.0, 0.0, 0)
-        unpiped = {"publishes_per_s": npub * world / (el_u / args.steps), "ms_per_step": el_u * 1e3 / args.steps,
-                   "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3},
-                   "note": "vmqg_match_device per step: COUNT, wave tier, scan, EMIT, wave tier (5 launches); "
-                           "rank 0's clock"}
-        log("unpipelined: %.3g publishes/s (%.1f us per step)" % (npub / (el_u / args.steps), el_u * 1e6 / args.steps))
-        elapsed = timed(submit, args.steps, True)
-        verify("timed pipeline")
-        if args.no_timing:
-            mixed_ns, nlaunch = 0.0, 0
-        else:
-            mixed_ns, nlaunch, count_ns, emit_ns = view.pipeline_times()
-    else:
-        elapsed = timed(step, args.steps, False)
-        count_ns, emit_ns, nlaunch = view.kernel_times() if not args.no_timing else (0.0, 0.0, 0)
-        mixed_ns = 0.0
+        raise RuntimeError("match status %d in timed region" % rc)
+    count_ns, emit_ns, nlaunch = view.kernel_times() if not args.no_timing else (0.0, 0.0, 0)
     emissions = int(d_offs[-1].item())
 
     # SURVEY §8(d) end-to-end figure (never `value`): publishes from pinned
@@ -384,25 +336,8 @@ def main():
         # L2-resident fan-out list, so it can exceed what the chip moves.
         alg = {"count": W.algorithmic_bytes_c(w, part="lookup"), "emit": W.algorithmic_bytes_c(w, part="emit"),
                "all": W.algorithmic_bytes_c(w), "emit_compulsory": W.algorithmic_bytes_c(w, part="emit_compulsory")}
-        if pipelined:
-            # the pipeline's dominant kernel is the mixed launch: one batch's
-            # COUNT (SURVEY lookup bytes) + the previous batch's EMIT
-            # (compulsory bytes) per launch
-            kern = "k_match_mixed"
-            kname = "k_match_mixed<0,2,true> (COUNT of batch k + EMIT of batch k-1)"
-            alg_launch = alg["emit_compulsory"] + alg["count"]
-            kern_ns = mixed_ns
-            bytes_model = ("COUNT: 8(L+1) + 16 S_p per publish (SURVEY 8d lookups); EMIT: 16 B written per "
-                           "emission + 40 B read per publish + 16 B per distinct record (workloads."
-                           "algorithmic_bytes_c lookup + emit_compulsory)")
-        else:
-            kern = "k_match_fast<1"
-            kname = "k_match_fast<1,0,2,true> (EMIT)"
-            alg_launch = alg["emit_compulsory"]
-            kern_ns = emit_ns
-            bytes_model = ("16 B written per emission + 40 B read per publish + 16 B per distinct "
-                           "record (workloads.algorithmic_bytes_c emit_compulsory)")
-        achieved = alg_launch / kern_ns if kern_ns > 0 else None   # bytes/ns == GB/s
+        kern = "k_match_fast<1"
+        achieved = alg["emit_compulsory"] / emit_ns if emit_ns > 0 else None   # bytes/ns == GB/s
         traffic = load_pmc_traffic(kern)
         pipe_ns = t_max * 1e9 / args.steps
         res = {
@@ -426,16 +361,14 @@ def main():
             "pairs_per_s": total_emit / t_max,
             "emissions_per_step_per_gpu": emissions,
             "verified_counts": verified,
-            "pipelined": pipelined,
-            "kernel_us": {"mixed": mixed_ns / 1e3, "count": count_ns / 1e3, "emit": emit_ns / 1e3,
-                          "launches": nlaunch},
-            "unpipelined": unpiped,
+            "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3, "launches": nlaunch},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
-                         "kernel": kname, "algorithmic_bytes_per_launch": alg_launch, "bytes_model": bytes_model},
-            "count_kernel": {"kernel": "k_match_fast<0,0,2,true> (COUNT%s)" % (", unmixed: a pipeline's first batch"
-                                                                               if pipelined else ""),
-                             "us": count_ns / 1e3 if count_ns else None,
+                         "kernel": "k_match_fast<1,0,2,true> (EMIT)",
+                         "algorithmic_bytes_per_launch": alg["emit_compulsory"],
+                         "bytes_model": "16 B written per emission + 40 B read per publish + 16 B per distinct "
+                                        "record (workloads.algorithmic_bytes_c emit_compulsory)"},
+            "count_kernel": {"kernel": "k_match_fast<0,0,2,true> (COUNT)", "us": count_ns / 1e3 if count_ns else None,
                              "lookup_bytes_model": alg["count"],
                              "achieved": alg["count"] / count_ns if count_ns else None},
             "survey_model": {"bytes_per_step": alg["all"], "achieved_per_step": alg["all"] / pipe_ns,

@@ -246,31 +246,6 @@ int vmqg_match_ranges_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npu
  * until the next vmqg_apply_ops on the context; primary contexts only. */
 int vmqg_records(vmqg_ctx* ctx, const vmqg_emit** recs, uint64_t* n);
 
-/* ---- pipelined matching ---------------------------------------------- */
-/* A stream of device-buffer batches (the NIF batcher's steady state).  Each
- * match runs as COUNT (walk the trie, count each publish's emissions) then
- * EMIT (write them); the two are bound by different things — random 64-B
- * table probes vs streaming stores — so vmqg_match_submit runs this batch's
- * COUNT in the same kernel launches as the previous submitted batch's EMIT.
- * Results are those of vmqg_match_device, but a batch is complete, in the
- * order of the stream it was submitted on, only after the NEXT
- * vmqg_match_submit / vmqg_match_submit_ranges, vmqg_match_flush,
- * vmqg_match_status, or any call that changes tables or the match settings
- * (vmqg_apply_ops, vmqg_replica_load, vmqg_apply_patches_device,
- * vmqg_set_option) or matches unpipelined (vmqg_match_device, ...); each of
- * those EMITs the pending batch first, on its own stream.  The caller keeps
- * a submitted batch's buffers (publishes, words, output, offsets) alive and
- * unchanged until then.  A pending batch of the other output mode or on
- * another stream is flushed before the new one is counted.  Errors latch as
- * for vmqg_match_device.  vmqg_destroy discards a pending batch.
- *   Replaces: vmq_reg_trie:fold/4 (vmq_reg_trie.erl:59-98) for a stream of batches. */
-int vmqg_match_submit(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words,
-                      vmqg_emit* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream);
-int vmqg_match_submit_ranges(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words,
-                             vmqg_range* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream);
-/* EMITs the pending batch (no-op without one).  Asynchronous. */
-int vmqg_match_flush(vmqg_ctx* ctx);
-
 /* ---- introspection --------------------------------------------------- */
 int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out);
 
@@ -283,20 +258,13 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "fast_g"    2 | 4      lanes per publish in the fast tier (default 2)
  *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
  *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8;
- *                          defaults 4 and 16)
- *   "mixed_bpc" 0..32      pipelined fast tier: grid cap, blocks per CU (0 = 8, default 8) */
+ *                          defaults 4 and 16) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the dominant match kernel over the last
  * vmqg_match_device calls made with timing enabled (vmqg_set_timing). */
 int vmqg_set_timing(vmqg_ctx* ctx, int enable);
 int vmqg_kernel_times(vmqg_ctx* ctx, double* count_ns, double* emit_ns, uint64_t* launches);
-/* Pipelined calls: average duration (ns) of the mixed launch (one batch's
- * COUNT fast tier + the previous batch's EMIT fast tier) and how many were
- * timed; count_ns / emit_ns average the unmixed COUNT / EMIT launches (the
- * first batch of a pipeline, the flushed last one). */
-int vmqg_pipeline_times(vmqg_ctx* ctx, double* mixed_ns, uint64_t* mixed_launches, double* count_ns,
-                        double* emit_ns);
 
 /* ---- replication (one primary, N device replicas) --------------------- */
 /* Device arena of the context: pointer, byte size and the layout descriptor

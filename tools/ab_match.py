@@ -5,10 +5,7 @@ once, each round runs every variant for `steps` steps; outputs are checked
 equal between variants (offsets exactly, records as a per-batch checksum:
 the order inside a publish may differ between variants); medians of the
 per-variant step time and the COUNT / fast-EMIT kernel times are printed as
-JSON.  The pseudo-option pipe=0,1 compares vmqg_match_device with the
-pipelined vmqg_match_submit (two output sets, a flush inside the timed
-steps; mixed_us = the mixed launch).
-usage: ab_match.py --config C --opt nt_stores=0,1 --opt fast_g=2,4 --opt pipe=0,1"""
+JSON.  usage: ab_match.py --config C --opt nt_stores=0,1 --opt fast_g=2,4"""
 import argparse
 import itertools
 import json
@@ -52,23 +49,16 @@ def main():
     cap = 66 * len(pubs) if args.config == "C" else 520 * len(pubs)
     d_out = torch.empty(cap * 4, dtype=torch.int32, device=dev)
     d_offs = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
-    d_out2 = torch.empty(cap * 4, dtype=torch.int32, device=dev)
-    d_offs2 = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream().cuda_stream
     names = [o.split("=")[0] for o in args.opt]
     values = [[int(x) for x in o.split("=")[1].split(",")] for o in args.opt]
     variants = list(itertools.product(*values))
-    res = {str(dict(zip(names, vv))): {"step_us": [], "count_us": [], "emit_us": [], "mixed_us": []}
-           for vv in variants}
+    res = {str(dict(zip(names, vv))): {"step_us": [], "count_us": [], "emit_us": []} for vv in variants}
     ref = None
     for rnd in range(args.rounds):
         for vv in variants:
-            pipe = False
             for n, x in zip(names, vv):
-                if n == "pipe":
-                    pipe = bool(x)
-                else:
-                    v.set_option(n, x)
+                v.set_option(n, x)
             v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap,
                            d_offs.data_ptr(), sp)
             torch.cuda.synchronize()
@@ -81,31 +71,17 @@ def main():
             assert torch.equal(ref[1], digest[1]), ("record checksum differs", vv)
             v.set_timing(True)
             t0 = time.perf_counter()
-            for k in range(args.steps):
-                if pipe:
-                    o, f = (d_out, d_offs) if k % 2 == 0 else (d_out2, d_offs2)
-                    v.match_submit(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), o.data_ptr(), cap,
-                                   f.data_ptr(), sp)
-                else:
-                    v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap,
-                                   d_offs.data_ptr(), sp)
-            if pipe:
-                v.match_flush()
+            for _ in range(args.steps):
+                v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap,
+                               d_offs.data_ptr(), sp)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / args.steps
-            if pipe:
-                m, _, c, e = v.pipeline_times()
-                assert v.match_status(sp) == 0, vv
-                assert torch.equal(ref[0], d_offs) and torch.equal(ref[0], d_offs2), ("pipelined offsets", vv)
-            else:
-                c, e, _ = v.kernel_times()
-                m = 0.0
+            c, e, _ = v.kernel_times()
             v.set_timing(False)
             r = res[str(dict(zip(names, vv)))]
             r["step_us"].append(dt * 1e6)
             r["count_us"].append(c / 1e3)
             r["emit_us"].append(e / 1e3)
-            r["mixed_us"].append(m / 1e3)
     out = {k: {m: statistics.median(x) for m, x in d.items()} for k, d in res.items()}
     print(json.dumps({"config": args.config, "median": out, "rounds": args.rounds, "steps": args.steps}))
 

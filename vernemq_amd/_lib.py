@@ -136,11 +136,6 @@ SIGNATURES = [
     ("vmqg_match_status", ctypes.c_int, [_P, _P]),
     ("vmqg_match_ranges", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
     ("vmqg_match_ranges_device", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),
-    ("vmqg_match_submit", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),
-    ("vmqg_match_submit_ranges", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),
-    ("vmqg_match_flush", ctypes.c_int, [_P]),
-    ("vmqg_pipeline_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64),
-                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     ("vmqg_records", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
     ("vmqg_replica_sync_layout", ctypes.c_int, [_P, _P]),
     ("vmqg_stats", ctypes.c_int, [_P, ctypes.POINTER(Stats)]),

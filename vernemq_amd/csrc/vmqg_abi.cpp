@@ -195,37 +195,6 @@ int vmqg_match_ranges_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npu
   GUARD_END
 }
 
-int vmqg_match_submit(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words,
-                      vmqg_emit* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream) {
-  if (!ctx || !d_offsets || (npub && (!d_pubs || !d_words))) return VMQG_E_INVAL;
-  GUARD_BEGIN
-  hipSetDevice(ctx->e.device);
-  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
-  return ctx->e.submit(d_pubs, npub, d_words, reinterpret_cast<vmqg::Record*>(d_out), out_cap, nullptr, 0,
-                       d_offsets, static_cast<hipStream_t>(stream), stream == nullptr);
-  GUARD_END
-}
-
-int vmqg_match_submit_ranges(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words,
-                             vmqg_range* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream) {
-  if (!ctx || !d_offsets || (npub && (!d_pubs || !d_words)) || (out_cap && !d_out)) return VMQG_E_INVAL;
-  GUARD_BEGIN
-  static vmqg_range dummy;
-  hipSetDevice(ctx->e.device);
-  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
-  return ctx->e.submit(d_pubs, npub, d_words, nullptr, 0, d_out ? d_out : &dummy, out_cap, d_offsets,
-                       static_cast<hipStream_t>(stream), stream == nullptr);
-  GUARD_END
-}
-
-int vmqg_match_flush(vmqg_ctx* ctx) {
-  if (!ctx) return VMQG_E_INVAL;
-  if (!ctx->e.has_device) return VMQG_E_DEVICE;
-  GUARD_BEGIN
-  return ctx->e.flush_pending();
-  GUARD_END
-}
-
 int vmqg_records(vmqg_ctx* ctx, const vmqg_emit** recs, uint64_t* n) {
   if (!ctx || !recs || !n) return VMQG_E_INVAL;
   Engine& e = ctx->e;
@@ -284,8 +253,6 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   if (!ctx || !name) return VMQG_E_INVAL;
   Engine& e = ctx->e;
   const std::string n(name);
-  // a pending pipelined batch was counted with the old settings
-  if (e.has_device && e.flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
   if (n == "fast_g") {
     if (value != 2 && value != 4) return VMQG_E_INVAL;
     e.opt_fast_g = (uint32_t)value;
@@ -294,9 +261,6 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   } else if (n == "count_bpc" || n == "emit_bpc") {
     if (value < 0 || value > 32) return VMQG_E_INVAL;
     (n == "count_bpc" ? e.opt_count_bpc : e.opt_emit_bpc) = (uint32_t)value;
-  } else if (n == "mixed_bpc") {
-    if (value < 0 || value > 32) return VMQG_E_INVAL;
-    e.opt_mixed_bpc = (uint32_t)value;
   } else {
     return VMQG_E_INVAL;
   }
@@ -307,8 +271,8 @@ int vmqg_set_timing(vmqg_ctx* ctx, int enable) {
   if (!ctx) return VMQG_E_INVAL;
   ctx->e.collect_times();
   ctx->e.timing = enable != 0;
-  ctx->e.sum_count_ns = ctx->e.sum_emit_ns = ctx->e.sum_mixed_ns = 0;
-  ctx->e.n_count = ctx->e.n_emit = ctx->e.n_mixed = 0;
+  ctx->e.sum_count_ns = ctx->e.sum_emit_ns = 0;
+  ctx->e.n_timed = 0;
   return VMQG_OK;
 }
 
@@ -317,23 +281,9 @@ int vmqg_kernel_times(vmqg_ctx* ctx, double* count_ns, double* emit_ns, uint64_t
   GUARD_BEGIN
   Engine& e = ctx->e;
   e.collect_times();
-  if (count_ns) *count_ns = e.n_count ? e.sum_count_ns / e.n_count : 0;
-  if (emit_ns) *emit_ns = e.n_emit ? e.sum_emit_ns / e.n_emit : 0;
-  if (launches) *launches = std::max(e.n_count, e.n_emit);
-  return VMQG_OK;
-  GUARD_END
-}
-
-int vmqg_pipeline_times(vmqg_ctx* ctx, double* mixed_ns, uint64_t* mixed_launches, double* count_ns,
-                        double* emit_ns) {
-  if (!ctx) return VMQG_E_INVAL;
-  GUARD_BEGIN
-  Engine& e = ctx->e;
-  e.collect_times();
-  if (mixed_ns) *mixed_ns = e.n_mixed ? e.sum_mixed_ns / e.n_mixed : 0;
-  if (mixed_launches) *mixed_launches = e.n_mixed;
-  if (count_ns) *count_ns = e.n_count ? e.sum_count_ns / e.n_count : 0;
-  if (emit_ns) *emit_ns = e.n_emit ? e.sum_emit_ns / e.n_emit : 0;
+  if (count_ns) *count_ns = e.n_timed ? e.sum_count_ns / e.n_timed : 0;
+  if (emit_ns) *emit_ns = e.n_timed ? e.sum_emit_ns / e.n_timed : 0;
+  if (launches) *launches = e.n_timed;
   return VMQG_OK;
   GUARD_END
 }
@@ -367,7 +317,6 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e.stream;
   vmqg::NullOrder order(stream, e.stream, e.ev_null);
   if (e.d_arena_bytes < L.total_bytes) {
-    if (e.flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
     if (hipDeviceSynchronize() != hipSuccess) return VMQG_E_DEVICE;
     if (e.d_arena) hipFree(e.d_arena);
     e.d_arena = nullptr; e.d_arena_bytes = 0;
@@ -375,9 +324,7 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
     e.d_arena_bytes = L.total_bytes;
   }
   e.lay = L;
-  // after the matches already queued (a pending pipelined batch's EMIT
-  // included), before the ones queued later
-  if (e.flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
+  // after the matches already queued, before the ones queued later
   if (e.order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
   if (hipMemcpyAsync(e.d_arena, d_src, L.total_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return VMQG_E_DEVICE;
@@ -415,10 +362,8 @@ int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t byt
   hipSetDevice(e.device);
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e.stream;
   vmqg::NullOrder order(stream, e.stream, e.ev_null);
-  // tables change only after the matches queued before (a pending pipelined
-  // batch's EMIT included), and matches queued later (on any stream) see the
-  // patches
-  if (e.flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
+  // tables change only after the matches queued before, and matches queued
+  // later (on any stream) see the patches
   if (e.order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
   if (vmqg::launch_patches(e.d_arena, d_patches, bytes / sizeof(vmqg::Patch), st) != hipSuccess)
     return VMQG_E_DEVICE;

@@ -3,7 +3,6 @@
 // state-machine function cites the Erlang clause it reproduces
 // (apps/vmq_server/src/vmq_reg_trie.erl unless noted).
 #include "vmqg_chain.h"
-#include "vmqg_nullorder.h"
 #include "vmqg_engine.h"
 
 #include <algorithm>
@@ -25,7 +24,6 @@ Engine::~Engine() {
     if (stream) hipStreamSynchronize(stream);
     for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
-    for (auto& e : t_mixed) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (ev_match_done) hipEventDestroy(ev_match_done);
     if (ev_null) hipEventDestroy(ev_null);
     for (Stage& sg : stage) {
@@ -66,8 +64,8 @@ int Engine::init(const vmqg_config& c) {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VMQG_E_DEVICE;
     if (hipEventCreateWithFlags(&ev_match_done, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
     has_device = true;
-    if (hipMalloc(&d_status, 128) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMemset(d_status, 0, 128) != hipSuccess) return VMQG_E_DEVICE;
+    if (hipMalloc(&d_status, 64) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMemset(d_status, 0, 64) != hipSuccess) return VMQG_E_DEVICE;
     for (Stage& sg : stage)
       if (hipEventCreateWithFlags(&sg.ev, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
     if (hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cu_count < 1)
@@ -886,9 +884,7 @@ int Engine::upload() {
   if (!has_device) { full_image = false; return VMQG_OK; }
   hipSetDevice(device);
   // tables must not change under a match still reading them (queued on any
-  // stream: order_on chains them), nor between a pipelined batch's COUNT and
-  // its EMIT
-  if (flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
+  // stream: order_on chains them)
   if (order_on(stream) != VMQG_OK) return VMQG_E_DEVICE;
   if (full_image) {
     if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
@@ -935,14 +931,8 @@ int Engine::upload() {
 // Table changes and matches form one chain across streams (vmqg_chain.h).
 int Engine::order_on(hipStream_t st) { return chain_order(ev_match_done, ev_stream, st); }
 
-// Two sets of per-batch scratch (key cache, spill slots, chunk totals,
-// deferred lists), batch b using set b & 1: a pipelined batch's EMIT reads its
-// set while the next batch's COUNT fills the other.
-uint64_t Engine::scratch_set_bytes(uint64_t cap) { return cap * (32 + 8 * 8) + (cap / 16 + 2) * 8; }
-
 int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
   if (npub > keycache_cap || npub > deferred_cap) {
-    if (flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
     if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
     hipFree(d_keycache);
     hipFree(d_deferred);
@@ -951,8 +941,8 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     const uint64_t cap = next_pow2(std::max<uint64_t>(npub, 1024));
     // 32-B key cache + kSpillKeys x 8-B spilled keys per publish, then the
     // chunk totals (one per 16 or 32 publishes, + 1)
-    if (hipMalloc(&d_keycache, 2 * scratch_set_bytes(cap)) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_deferred, 2 * 2 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + (cap / 16 + 2) * 8) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_deferred, 2 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
     keycache_cap = cap;
     deferred_cap = cap;
   }
@@ -962,7 +952,6 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
 // Look-back granules for `granules` scan tiles; advances the call's tag.
 int Engine::ensure_lookback(uint64_t granules, hipStream_t st) {
   if (granules > lookback_cap) {
-    if (flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
     if (d_lookback) { hipStreamSynchronize(st); hipFree(d_lookback); }
     d_lookback = nullptr;
     lookback_cap = next_pow2(std::max<uint64_t>(granules, 1024));
@@ -985,7 +974,6 @@ int Engine::ensure_wave_scratch(hipStream_t st) {
   const uint64_t need = std::max<uint64_t>({1024, 64ull * (stack_depth() + 4), o_cap_floor});
   if (need > (1ull << 31)) return VMQG_E_LIMIT;
   if (o_cap >= need && d_ostack) return VMQG_OK;
-  if (flush_pending() != VMQG_OK) return VMQG_E_DEVICE;   // its wave tier uses the stacks
   // two 256-thread blocks per CU (8 waves) when the stacks fit 256 MiB, at
   // least 64 waves for deep tries
   uint64_t waves = (256ull << 20) / (need * sizeof(uint2));
@@ -998,8 +986,7 @@ int Engine::ensure_wave_scratch(hipStream_t st) {
   return VMQG_OK;
 }
 
-MatchArgs Engine::args_for(uint64_t seq, const vmqg_pub* pubs, uint32_t npub, const uint32_t* words,
-                           uint64_t* offs) const {
+MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, uint64_t* offs) const {
   MatchArgs a{};
   a.edges = reinterpret_cast<const EdgeSlot*>(d_arena + lay.edge_off);
   a.edge_mask = lay.edge_buckets - 1;
@@ -1016,18 +1003,17 @@ MatchArgs Engine::args_for(uint64_t seq, const vmqg_pub* pubs, uint32_t npub, co
   a.local_node = (uint32_t)lay.local_node;
   a.pubs = pubs; a.words = words; a.npub = npub;
   a.offsets = offs;
-  char* kc = static_cast<char*>(d_keycache) + (seq & 1) * scratch_set_bytes(keycache_cap);
-  a.keycache = kc;
-  a.keyspill = reinterpret_cast<uint2*>(kc + keycache_cap * 32);
-  a.chunk = reinterpret_cast<uint64_t*>(kc + keycache_cap * (32 + 8 * 8));
+  a.keycache = d_keycache;
+  a.keyspill = reinterpret_cast<uint2*>(static_cast<char*>(d_keycache) + keycache_cap * 32);
+  a.chunk = reinterpret_cast<uint64_t*>(static_cast<char*>(d_keycache) + keycache_cap * (32 + 8 * 8));
   a.gpw = 64 / (opt_fast_g == 4 ? 4 : 2);
-  a.status = d_status + kStatusWords * (seq % kStatusSets);
-  a.status_next = d_status + kStatusWords * ((seq + 1) % kStatusSets);
-  a.err = d_status + kStatusErr;
-  a.deferred = d_deferred + (seq & 1) * 2 * deferred_cap;
+  a.status = d_status + 4 * (call_seq & 1);
+  a.status_next = d_status + 4 * ((call_seq + 1) & 1);
+  a.err = d_status + 8;
+  a.deferred = d_deferred;
   a.fast_g = opt_fast_g; a.opts = opt_flags;
   a.count_bpc = opt_count_bpc; a.emit_bpc = opt_emit_bpc;
-  a.cus = (uint32_t)cu_count; a.mixed_bpc = opt_mixed_bpc;
+  a.cus = (uint32_t)cu_count;
   a.lookback = d_lookback; a.lb_tag = lb_tag;
   a.o_stack = d_ostack; a.o_cap = o_cap; a.o_waves = o_waves;
   return a;
@@ -1040,25 +1026,6 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   if (!d_arena) return VMQG_E_STATE;
   hipSetDevice(device);
   if (!st) st = stream;
-  if (flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
-  MatchArgs a;
-  int rc = count_batch(d_pubs_, npub, d_words_, d_out_, out_cap, d_rng, rng_cap, d_offsets, st, a);
-  if (rc || npub == 0) return rc;
-  // EMIT: fast groups, then the wave tier
-  hipEvent_t e2 = nullptr, e3 = nullptr;
-  if (timing) { hipEventCreate(&e2); hipEventCreate(&e3); t_emit.push_back({e2, e3}); }
-  if (launch_match(a, 1, 0, st, e2, e3) != hipSuccess) return VMQG_E_DEVICE;
-  if (launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
-  return VMQG_OK;
-}
-
-// Orders `st` after earlier work, sizes the scratch and queues batch
-// (call_seq)'s COUNT — fast tier, wave tier, scan — unless `pipelined`, when
-// the fast and wave tiers run mixed with the pending batch's EMIT.  Leaves the
-// batch's arguments in `a` (its EMIT is the caller's).
-int Engine::count_batch(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t* d_words_, Record* d_out_,
-                        uint64_t out_cap, vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets, hipStream_t st,
-                        MatchArgs& a, bool pipelined) {
   // table changes (patches, images) land before this match: the primary's on
   // the context stream, a replica's on whatever stream the caller gave
   if (order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
@@ -1067,86 +1034,45 @@ int Engine::count_batch(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t* 
   if ((rc = ensure_match_scratch(npub, st)) || (rc = ensure_lookback(scan_tiles((npub + 15) / 16), st)) ||
       (rc = ensure_wave_scratch(st)))
     return rc;
-  // the scratch may have been re-sized, flushing the pending batch
-  if (pipelined && !pend.on) pipelined = false;
-  a = args_for(call_seq, d_pubs_, npub, d_words_, d_offsets);
+  MatchArgs a = args_for(d_pubs_, npub, d_words_, d_offsets);
   a.out = d_out_; a.out_cap = out_cap;
   a.out_rng = d_rng; a.rng_cap = rng_cap;
-  last_set = (uint32_t)(call_seq % kStatusSets);
+  last_set = call_seq & 1;
   call_seq++;
   // kernel timing (vmqg_set_timing): events written by the fast-tier
   // dispatches themselves, so timing adds no marker packets between launches
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
   if (timing) {
-    hipEventCreate(&e0); hipEventCreate(&e1);
-    (pipelined ? t_mixed : t_count).push_back({e0, e1});
+    hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2); hipEventCreate(&e3);
+    t_count.push_back({e0, e1});
+    t_emit.push_back({e2, e3});
   }
-  if (pipelined) {
-    if (launch_mixed(a, pend.a, st, e0, e1) != hipSuccess) return VMQG_E_DEVICE;
-    if (launch_wave_mixed(a, pend.a, st) != hipSuccess) return VMQG_E_DEVICE;
-    pend.on = false;
-  } else {
-    if (launch_match(a, 0, 0, st, e0, e1) != hipSuccess) return VMQG_E_DEVICE;
-    if (launch_match(a, 0, 1, st) != hipSuccess) return VMQG_E_DEVICE;
-  }
+  // COUNT: fast groups, then the wave tier for what they deferred
+  if (launch_match(a, 0, 0, st, e0, e1) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 0, 1, st) != hipSuccess) return VMQG_E_DEVICE;
   if (launch_scan(a, st) != hipSuccess) return VMQG_E_DEVICE;
+  // EMIT: same tiers
+  if (launch_match(a, 1, 0, st, e2, e3) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
 
-// Pipelined match: this batch's COUNT runs in the same launches as the
-// pending batch's EMIT; this batch becomes the pending one.  A pending batch
-// of the other output mode or on another stream is flushed first.
-int Engine::submit(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t* d_words_, Record* d_out_,
-                   uint64_t out_cap, vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets, hipStream_t st,
-                   bool null_stream) {
-  if (!has_device) return VMQG_E_DEVICE;
-  if (!d_arena) return VMQG_E_STATE;
-  hipSetDevice(device);
-  if (!st) st = stream;
-  if (pend.on && (pend.st != st || (pend.a.out_rng != nullptr) != (d_rng != nullptr) || npub == 0))
-    if (flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
-  MatchArgs a;
-  const int rc = count_batch(d_pubs_, npub, d_words_, d_out_, out_cap, d_rng, rng_cap, d_offsets, st, a, pend.on);
-  if (rc || npub == 0) return rc;
-  pend.on = true;
-  pend.a = a;
-  pend.st = st;
-  pend.null_stream = null_stream;
-  return VMQG_OK;
-}
-
-// EMIT of the pending pipelined batch, on the stream it was submitted on.
-int Engine::flush_pending() {
-  if (!pend.on) return VMQG_OK;
-  pend.on = false;
-  hipSetDevice(device);
-  NullOrder order(pend.null_stream ? nullptr : pend.st, stream, ev_null);
-  if (order_on(pend.st) != VMQG_OK) return VMQG_E_DEVICE;
-  hipEvent_t e2 = nullptr, e3 = nullptr;
-  if (timing) { hipEventCreate(&e2); hipEventCreate(&e3); t_emit.push_back({e2, e3}); }
-  if (launch_match(pend.a, 1, 0, pend.st, e2, e3) != hipSuccess) return VMQG_E_DEVICE;
-  if (launch_match(pend.a, 1, 1, pend.st) != hipSuccess) return VMQG_E_DEVICE;
-  return VMQG_OK;
-}
-
-// Status words: kStatusSets sets of per-batch counters ([0] deferred
-// publishes, [1] of those walked with a global stack, [2] scan ticket, ...)
-// and, at kStatusErr, the error bits latched since the previous
-// vmqg_match_status.  A pending pipelined batch is EMITted first.
+// Status words: two sets of per-call counters ([0] deferred publishes, [1]
+// of those walked with a global stack, [2] scan ticket) used by alternate
+// calls, and at [8] the error bits latched since the previous
+// vmqg_match_status.
 int Engine::match_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
   if (!st) st = stream;
-  if (flush_pending() != VMQG_OK) return VMQG_E_DEVICE;
-  if (order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
-  uint32_t h[kStatusErr + 1] = {0};
+  uint32_t h[12] = {0};
   if (hipMemcpyAsync(h, d_status, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
-  if (hipMemsetAsync(d_status + kStatusErr, 0, 4, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipMemsetAsync(d_status + 8, 0, 4, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
-  last_deferred[0] = h[kStatusWords * last_set];
-  last_deferred[1] = h[kStatusWords * last_set + 1];
-  const uint32_t err = h[kStatusErr];
+  last_deferred[0] = h[4 * last_set];
+  last_deferred[1] = h[4 * last_set + 1];
+  const uint32_t err = h[8];
   if (err & 2u) return VMQG_E_FRONTIER;
   if (err & 4u) return VMQG_E_OVERFLOW;
   if (err & (8u | 16u)) return VMQG_E_DEVICE;   // count mismatch, look-back timeout
@@ -1156,19 +1082,16 @@ int Engine::match_status(hipStream_t st) {
 void Engine::collect_times() {
   if (!has_device) return;
   hipSetDevice(device);
-  auto drain = [](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double& sum, uint64_t& n) {
-    for (auto& e : v) {
-      float ms = 0;
-      hipEventSynchronize(e.second);
-      hipEventElapsedTime(&ms, e.first, e.second);
-      sum += ms * 1e6; n++;
-      hipEventDestroy(e.first); hipEventDestroy(e.second);
-    }
-    v.clear();
-  };
-  drain(t_count, sum_count_ns, n_count);
-  drain(t_emit, sum_emit_ns, n_emit);
-  drain(t_mixed, sum_mixed_ns, n_mixed);
+  for (size_t i = 0; i < t_count.size(); i++) {
+    float a = 0, b = 0;
+    hipEventSynchronize(t_emit[i].second);
+    hipEventElapsedTime(&a, t_count[i].first, t_count[i].second);
+    hipEventElapsedTime(&b, t_emit[i].first, t_emit[i].second);
+    sum_count_ns += a * 1e6; sum_emit_ns += b * 1e6; n_timed++;
+    hipEventDestroy(t_count[i].first); hipEventDestroy(t_count[i].second);
+    hipEventDestroy(t_emit[i].first); hipEventDestroy(t_emit[i].second);
+  }
+  t_count.clear(); t_emit.clear();
 }
 
 // ------------------------------------------------------------------ dump

@@ -220,9 +220,6 @@ struct Engine {
   bool timing = false;
   uint32_t opt_fast_g = 2, opt_flags = kOptNtStores;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
   uint32_t opt_count_bpc = 4, opt_emit_bpc = 16;       // fast-tier grid caps, blocks per CU (A/B-tuned)
-  uint32_t opt_mixed_bpc = 8;                          // pipelined fast tier: grid cap, blocks per CU
-  // the pipelined batch whose COUNT is queued and whose EMIT is not (vmqg_match_submit)
-  struct Pending { bool on = false; bool null_stream = false; MatchArgs a{}; hipStream_t st = nullptr; } pend;
   // look-back granules (tagged per call), global stack of the tier-2 wave path
   uint64_t* d_lookback = nullptr; uint64_t lookback_cap = 0; uint32_t lb_tag = 0;
   uint2* d_ostack = nullptr; uint64_t ostack_bytes = 0;
@@ -230,9 +227,8 @@ struct Engine {
   uint64_t o_cap_floor = 0;         // raised by vmqg_match_batch if a tier-2 stack ever overflowed
   int cu_count = 0;
   uint32_t last_deferred[2] = {0, 0};   // tier-1 / tier-2 publishes of the last checked batch
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_emit, t_mixed;
-  double sum_count_ns = 0, sum_emit_ns = 0, sum_mixed_ns = 0;
-  uint64_t n_count = 0, n_emit = 0, n_mixed = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_emit;
+  double sum_count_ns = 0, sum_emit_ns = 0; uint64_t n_timed = 0;
 
   std::string dump_text;
 
@@ -286,17 +282,10 @@ struct Engine {
   int ensure_match_scratch(uint64_t npub, hipStream_t st);
   int ensure_lookback(uint64_t granules, hipStream_t st);
   int ensure_wave_scratch(hipStream_t st);
-  static uint64_t scratch_set_bytes(uint64_t cap);
-  MatchArgs args_for(uint64_t seq, const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, uint64_t* offs) const;
+  MatchArgs args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, uint64_t* offs) const;
   // out_rng == null: records mode into out; else range mode into out_rng
   int match_device(const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words, Record* d_out,
                    uint64_t out_cap, vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets, hipStream_t st);
-  int count_batch(const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words, Record* d_out, uint64_t out_cap,
-                  vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets, hipStream_t st, MatchArgs& a,
-                  bool pipelined = false);
-  int submit(const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words, Record* d_out, uint64_t out_cap,
-             vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets, hipStream_t st, bool null_stream);
-  int flush_pending();
   uint32_t stack_depth() const { return (uint32_t)std::max<uint64_t>(max_depth, lay.max_depth); }
   int match_status(hipStream_t st);
   void collect_times();

@@ -24,15 +24,15 @@ struct MatchArgs {
   uint2* keyspill;                                // npub x kSpillKeys {record off, cum start}: 3..8-key publishes
   Record* out; uint64_t out_cap;                  // records mode
   vmqg_range* out_rng; uint64_t rng_cap;          // range mode (out_rng != null)
-  uint32_t* status;                               // this batch's counters (kStatusWords): [0] deferred publishes,
+  uint32_t* status;                               // this call's counters: [0] deferred publishes,
                                                   // [1] of those, walked with a global stack, [2] scan ticket,
                                                   // [3] publishes EMIT hands to the wave tier (none today)
-  uint32_t* status_next;                          // the next batch's counters (zeroed by this batch's COUNT)
+  uint32_t* status_next;                          // the next call's counters (zeroed by this call)
   uint32_t* err;                                  // error bits, sticky until vmqg_match_status
   uint32_t* deferred;                             // 2 x npub: publishes deferred by COUNT, then by EMIT
   uint32_t fast_g, opts;                          // tuning: lanes per publish (2|4), kOpt* bits
   uint32_t count_bpc, emit_bpc;                   // tuning: fast-tier grid cap in blocks per CU (0 = 8)
-  uint32_t cus, mixed_bpc;                        // compute units of the device; pipelined grid cap (0 = 8)
+  uint32_t cus, pad2;                             // compute units of the device
   uint64_t* lookback;                             // per scan tile: {tag, flag, value} granule
   uint32_t lb_tag, pad1;                          // this call's granule tag (never 0)
   uint2* o_stack;                                 // wave tier: global frontier stacks, o_cap entries per wave
@@ -40,21 +40,12 @@ struct MatchArgs {
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
-// Status counters: kStatusSets sets of kStatusWords, batch b using set b % 3
-// (its COUNT zeroes set (b + 1) % 3, while batch b - 1's EMIT, pipelined
-// behind it, still reads set (b - 1) % 3), then the sticky error word.
-constexpr uint32_t kStatusWords = 8, kStatusSets = 3, kStatusErr = kStatusWords * kStatusSets;
 
 // mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier (grid a.o_waves / 4).
 // t0 / t1 (both or neither): timing events recorded by the kernel's own
 // dispatch (hipExtLaunchKernel), not by marker packets between launches.
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, hipEvent_t t0 = nullptr,
                         hipEvent_t t1 = nullptr);
-// Pipelined match (vmqg_match_submit): batch c's COUNT fast tier together
-// with batch e's EMIT fast tier in one launch, then both wave tiers in one.
-hipError_t launch_mixed(const MatchArgs& c, const MatchArgs& e, hipStream_t st, hipEvent_t t0 = nullptr,
-                        hipEvent_t t1 = nullptr);
-hipError_t launch_wave_mixed(const MatchArgs& c, const MatchArgs& e, hipStream_t st);
 // counts in offsets[0, npub) -> exclusive offsets[0, npub] (one launch, look-back)
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st);
 uint32_t scan_tiles(uint64_t nchunks);   // look-back tiles of the chunk-total scan

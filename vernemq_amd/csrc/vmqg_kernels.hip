@@ -55,8 +55,8 @@ constexpr uint32_t kRewalk = 0xFFFFFFFFu;   // key cache: EMIT must re-walk
 constexpr uint32_t kSpillKeys = 8;          // spill slots per publish (more keys: re-walk)
 constexpr uint32_t kDeferred = 0xFFFFFFFEu; // key cache: the wave tier owns the publish
 
-// Per-batch status counters (a.status; kStatusSets sets used in turn: each
-// batch's first kernel zeroes the set of the batch after it, so no reset
+// Per-call status counters (a.status; two sets used by alternate calls: each
+// call's first kernel zeroes the set of the call after it, so no reset
 // launch is needed) and the sticky error word (a.err, cleared only by
 // vmqg_match_status).
 enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStRewalk = 3 };
@@ -649,34 +649,6 @@ __device__ void emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScra
 }
 
 // --------------------------------------------------------------- kernels
-// One chunk (the GPW publishes [base, base + GPW) of one wave) of COUNT
-// (MODE 0) or EMIT (MODE 1).
-template <int MODE, int OUT, int G, bool NT>
-__device__ __forceinline__ void fast_chunk(const MatchArgs& a, uint32_t base, const FastScratch<G>& s,
-                                           const Group<G>& g, GroupMeta* gm, uint32_t slot0) {
-  constexpr int GPW = FastScratch<G>::GPW;
-  const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
-  if (MODE == 0) {
-    uint64_t c = 0;
-    if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g);
-    // the chunk's total (publishes the wave tier takes add theirs later)
-    const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
-    if (__lane_id() == 0) a.chunk[base / GPW] = tot;
-  } else if (OUT == 0) {
-    emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm, slot0);
-  } else {
-    uint64_t ob, oe;
-    chunk_offsets<G, GPW>(a, base, n, g, ob, oe);
-    if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
-  }
-  wave_sync();
-}
-
-// the first kernel of a call zeroes the next call's counters
-__device__ __forceinline__ void zero_next_status(const MatchArgs& a) {
-  if (blockIdx.x == 0 && threadIdx.x < kStatusWords) a.status_next[threadIdx.x] = 0;
-}
-
 template <int MODE, int OUT, int G, bool NT>
 #ifndef VMQG_COUNT_WPE
 #define VMQG_COUNT_WPE 4   // COUNT waves per SIMD the register budget must allow (A/B: 4, 5)
@@ -685,7 +657,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ?
 void k_match_fast(MatchArgs a) {
   using FS = FastScratch<G>;
   constexpr int GPW = FS::GPW;
-  if (MODE == 0) zero_next_status(a);
+  if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < 4) a.status_next[threadIdx.x] = 0;
   __shared__ uint2 st[FS::SC * FS::SLOTS];
   __shared__ uint32_t cd[FS::CC * FS::SLOTS];
   __shared__ uint2 ky[FS::KC * FS::SLOTS];
@@ -694,40 +666,22 @@ void k_match_fast(MatchArgs a) {
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
   const uint32_t stride = gridDim.x * kWaves * GPW;
-  for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride)
-    fast_chunk<MODE, OUT, G, NT>(a, base, s, g, gm[wv], wv * GPW);
-}
-
-// Pipelined fast tier (vmqg_match_submit): one launch COUNTs batch c (this
-// call's) while it EMITs batch e (the previous call's, already counted and
-// scanned).  The two are independent, and their bounds differ — COUNT is
-// bound by random 64-B probes, EMIT by streaming stores — so sharing the
-// chip's waves overlaps them (profiles/overlap_ceiling_r02.jsonl: one mixed
-// launch takes 0.81-0.83 of the two back to back).  Work items are chunks
-// (one wave's GPW publishes) of one merged sequence that interleaves the two
-// batches' chunks in proportion; waves stride over it statically, so every
-// CU runs both kinds all the time (a shared ticket counter serialises the
-// waves: 7x slower in the microbenchmark, 1.23x the unmixed pair here).
-template <int OUT, int G, bool NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-void k_match_mixed(MatchArgs c, MatchArgs e) {
-  using FS = FastScratch<G>;
-  constexpr uint32_t GPW = FS::GPW;
-  zero_next_status(c);
-  __shared__ uint2 st[FS::SC * FS::SLOTS];
-  __shared__ uint32_t cd[FS::CC * FS::SLOTS];
-  __shared__ uint2 ky[FS::KC * FS::SLOTS];
-  __shared__ GroupMeta gm[kWaves][OUT == 0 ? GPW : 1];
-  const Group<G> g;
-  const uint32_t wv = threadIdx.x >> 6;
-  const FS s{st, cd, ky, wv * GPW + g.gidx};
-  const uint64_t nc = (c.npub + GPW - 1) / GPW, ne = (e.npub + GPW - 1) / GPW, T = nc + ne;
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  for (uint64_t t = (uint64_t)blockIdx.x * kWaves + wv; t < T; t += nwaves) {
-    // chunk t of the merge: EMIT chunks sit at the steps where t * ne / T advances
-    const uint64_t ei = t * ne / T;
-    if ((t + 1) * ne / T > ei) fast_chunk<1, OUT, G, NT>(e, (uint32_t)(ei * GPW), s, g, gm[wv], wv * GPW);
-    else fast_chunk<0, OUT, G, NT>(c, (uint32_t)((t - ei) * GPW), s, g, gm[wv], wv * GPW);
+  for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
+    const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
+    if (MODE == 0) {
+      uint64_t c = 0;
+      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g);
+      // the chunk's total (publishes the wave tier takes add theirs later)
+      const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
+      if (__lane_id() == 0) a.chunk[base / GPW] = tot;
+    } else if (OUT == 0) {
+      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
+    } else {
+      uint64_t ob, oe;
+      chunk_offsets<G, GPW>(a, base, n, g, ob, oe);
+      if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
+    }
+    wave_sync();
   }
 }
 
@@ -941,69 +895,47 @@ struct WaveWalk {
 // the wave's stack in global scratch (o_cap entries, sized from the trie
 // depth so it cannot overflow).  EMIT re-walks in the same order and checks
 // the count.
-// Item d of a wave-tier list: the fast tier's deferred publishes, and in EMIT
-// then the publishes its key cache could not serve.
-template <int MODE, int OUT, bool NT>
-__device__ void wave_item(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t d, uint32_t n1) {
-  const uint32_t lane = __lane_id();
-  const uint32_t p = d < n1 ? a.deferred[d] : a.deferred[a.npub + (d - n1)];
-  uint64_t ob = 0, oe = 0;
-  if (MODE == 1) {
-    ob = a.offsets[p];
-    oe = a.offsets[p + 1];
-    if (oe > (OUT ? a.rng_cap : a.out_cap)) {
-      if (lane == 0) atomicOr(a.err, kErrOverflow);
-      return;
-    }
-  }
-  WaveWalk<MODE, OUT, NT> w1(a, W, W.stack, kWStack, ob);
-  bool ok = w1.run_publish(p);
-  uint64_t total = w1.run;
-  if (!ok) {
-    if (MODE == 0 && lane == 0) atomicAdd(&a.status[kStTier2], 1u);
-    WaveWalk<MODE, OUT, NT> w2(a, W, gstack, a.o_cap, ob);
-    ok = w2.run_publish(p);
-    total = w2.run;
-    if (!ok && lane == 0) atomicOr(a.err, kErrFrontier);
-  }
-  if (ok && lane == 0) {
-    if (MODE == 0) {
-      a.offsets[p] = total;
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)total);
-    } else if (total != oe - ob) {
-      atomicOr(a.err, kErrMismatch);
-    }
-  }
-  wave_sync();
-}
-
 template <int MODE, int OUT, bool NT>
 __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
   __shared__ WaveLds lds[kWaves];
-  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
   uint2* gstack = a.o_stack + gw * a.o_cap;
-  // the lists were written by the fast tier's launches
+  // the fast tier's deferred list, and in EMIT the publishes its key cache
+  // could not serve (written by the fast tier's launches)
   const uint32_t n1 = a.status[kStDeferred];
   const uint32_t n = n1 + (MODE == 1 ? a.status[kStRewalk] : 0u);
   const uint32_t nwaves = gridDim.x * kWaves;
-  for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) wave_item<MODE, OUT, NT>(a, lds[wv], gstack, d, n1);
-}
-
-// Pipelined wave tier: batch c's COUNT items, then batch e's EMIT items, in
-// one launch (both lists are final: written by k_match_mixed).
-template <int OUT, bool NT>
-__global__ __launch_bounds__(256) void k_match_wave_mixed(MatchArgs c, MatchArgs e) {
-  __shared__ WaveLds lds[kWaves];
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
-  uint2* gstack = c.o_stack + gw * c.o_cap;
-  const uint32_t nc = c.status[kStDeferred];
-  const uint32_t ne1 = e.status[kStDeferred], ne = ne1 + e.status[kStRewalk];
-  const uint32_t nwaves = gridDim.x * kWaves;
-  for (uint32_t d = (uint32_t)gw; d < nc + ne; d += nwaves) {
-    if (d < nc) wave_item<0, OUT, NT>(c, lds[wv], gstack, d, nc);
-    else wave_item<1, OUT, NT>(e, lds[wv], gstack, d - nc, ne1);
+  for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
+    const uint32_t p = d < n1 ? a.deferred[d] : a.deferred[a.npub + (d - n1)];
+    uint64_t ob = 0, oe = 0;
+    if (MODE == 1) {
+      ob = a.offsets[p];
+      oe = a.offsets[p + 1];
+      if (oe > (OUT ? a.rng_cap : a.out_cap)) {
+        if (lane == 0) atomicOr(a.err, kErrOverflow);
+        continue;
+      }
+    }
+    WaveWalk<MODE, OUT, NT> w1(a, lds[wv], lds[wv].stack, kWStack, ob);
+    bool ok = w1.run_publish(p);
+    uint64_t total = w1.run;
+    if (!ok) {
+      if (MODE == 0 && lane == 0) atomicAdd(&a.status[kStTier2], 1u);
+      WaveWalk<MODE, OUT, NT> w2(a, lds[wv], gstack, a.o_cap, ob);
+      ok = w2.run_publish(p);
+      total = w2.run;
+      if (!ok && lane == 0) atomicOr(a.err, kErrFrontier);
+    }
+    if (ok && lane == 0) {
+      if (MODE == 0) {
+        a.offsets[p] = total;
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)total);
+      } else if (total != oe - ob) {
+        atomicOr(a.err, kErrMismatch);
+      }
+    }
+    wave_sync();
   }
 }
 
@@ -1129,39 +1061,6 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, 
   return hipGetLastError();
 }
 
-template <int OUT, int G, bool NT>
-static void launch_mixed_k(const MatchArgs& c, const MatchArgs& e, uint32_t g, hipStream_t st, hipEvent_t t0,
-                           hipEvent_t t1) {
-  if (t0) hipExtLaunchKernelGGL(k_match_mixed<OUT, G, NT>, dim3(g), dim3(256), 0, st, t0, t1, 0, c, e);
-  else k_match_mixed<OUT, G, NT><<<g, 256, 0, st>>>(c, e);
-}
-
-hipError_t launch_mixed(const MatchArgs& c, const MatchArgs& e, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
-  const bool nt = (c.opts & kOptNtStores) != 0;
-  const int out = c.out_rng ? 1 : 0;
-  const uint32_t G = c.fast_g == 4 ? 4 : 2, per = kWaves * (64 / G);
-  // waves stride over the merged chunks: the grid only has to fill the chip
-  uint32_t g = div_up(c.npub, per) + div_up(e.npub, per);
-  const uint32_t cap = (uint32_t)c.cus * (c.mixed_bpc ? c.mixed_bpc : 8u);
-  if (g > cap) g = cap;
-  if (g < 1) g = 1;
-  if (G == 4) {
-    if (out) { if (nt) launch_mixed_k<1, 4, true>(c, e, g, st, t0, t1); else launch_mixed_k<1, 4, false>(c, e, g, st, t0, t1); }
-    else { if (nt) launch_mixed_k<0, 4, true>(c, e, g, st, t0, t1); else launch_mixed_k<0, 4, false>(c, e, g, st, t0, t1); }
-  } else {
-    if (out) { if (nt) launch_mixed_k<1, 2, true>(c, e, g, st, t0, t1); else launch_mixed_k<1, 2, false>(c, e, g, st, t0, t1); }
-    else { if (nt) launch_mixed_k<0, 2, true>(c, e, g, st, t0, t1); else launch_mixed_k<0, 2, false>(c, e, g, st, t0, t1); }
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_wave_mixed(const MatchArgs& c, const MatchArgs& e, hipStream_t st) {
-  const bool nt = (c.opts & kOptNtStores) != 0;
-  const uint32_t g = c.o_waves / kWaves;
-  if (c.out_rng) { if (nt) k_match_wave_mixed<1, true><<<g, 256, 0, st>>>(c, e); else k_match_wave_mixed<1, false><<<g, 256, 0, st>>>(c, e); }
-  else { if (nt) k_match_wave_mixed<0, true><<<g, 256, 0, st>>>(c, e); else k_match_wave_mixed<0, false><<<g, 256, 0, st>>>(c, e); }
-  return hipGetLastError();
-}
 
 hipError_t launch_patches(uint8_t* arena, const void* d_patches, uint64_t n, hipStream_t st) {
   if (n == 0) return hipSuccess;

@@ -299,29 +299,6 @@ class RegGpuView:
         _lib.check(self._L.vmqg_match_device(self._h, d_pubs, npub, d_words, d_out, out_cap, d_offsets,
                                              stream or None), "vmqg_match_device")
 
-    def match_submit(self, d_pubs: int, npub: int, d_words: int, d_out: int, out_cap: int, d_offsets: int,
-                     stream: int = 0):
-        """Pipelined match (vmqg_match_submit): this batch's COUNT runs with the
-        previous submitted batch's EMIT; a batch is complete after the next
-        submit, match_flush() or match_status()."""
-        _lib.check(self._L.vmqg_match_submit(self._h, d_pubs, npub, d_words, d_out, out_cap, d_offsets,
-                                             stream or None), "vmqg_match_submit")
-
-    def match_submit_ranges(self, d_pubs: int, npub: int, d_words: int, d_out: int, out_cap: int, d_offsets: int,
-                            stream: int = 0):
-        _lib.check(self._L.vmqg_match_submit_ranges(self._h, d_pubs, npub, d_words, d_out, out_cap, d_offsets,
-                                                    stream or None), "vmqg_match_submit_ranges")
-
-    def match_flush(self):
-        _lib.check(self._L.vmqg_match_flush(self._h), "vmqg_match_flush")
-
-    def pipeline_times(self):
-        """(mixed launch ns, mixed launches, unmixed COUNT ns, unmixed EMIT ns)."""
-        m, n, c, e = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
-        _lib.check(self._L.vmqg_pipeline_times(self._h, ctypes.byref(m), ctypes.byref(n), ctypes.byref(c),
-                                               ctypes.byref(e)), "vmqg_pipeline_times")
-        return m.value, n.value, c.value, e.value
-
     def match_status(self, stream: int = 0) -> int:
         return self._L.vmqg_match_status(self._h, stream or None)
 
