@@ -110,8 +110,8 @@ int vmqa_check_batch(vmqa_ctx* ctx, const vmqa_req* reqs, size_t n, const uint32
                      uint8_t* allowed);
 
 /* Device-buffer form (pointers on the context's device, work on `stream`,
- * NULL = the context's stream ordered like default-stream work as in
- * vmqg_match_device; no synchronisation); errors latch for vmqa_check_status. */
+ * NULL = the legacy default stream as in vmqg_match_device; no
+ * synchronisation); errors latch for vmqa_check_status. */
 int vmqa_check_device(vmqa_ctx* ctx, const vmqa_req* d_reqs, uint32_t n, const uint32_t* d_words,
                       uint8_t* d_allowed, void* stream);
 int vmqa_check_status(vmqa_ctx* ctx, void* stream);

@@ -196,11 +196,10 @@ int vmqg_match_batch(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const uin
                      uint64_t* offsets);
 
 /* Device-buffer match: every pointer is device memory of the context's
- * device; work is enqueued on `stream` (a hipStream_t; NULL = the context's
- * own stream, ordered after work already queued on the legacy default
- * stream and before default-stream work queued later, so a caller on the
- * default stream needs no extra synchronisation) and the call returns
- * without synchronising.  Table changes (patches, images) queued on any
+ * device; work is enqueued on `stream` (a hipStream_t; NULL = the legacy
+ * default stream itself, hipStreamLegacy, so a caller on the default stream
+ * needs no extra synchronisation) and the call returns without
+ * synchronising.  Table changes (patches, images) queued on any
  * stream land before the match.  d_offsets needs
  * npub + 1 entries.  Overflow / scratch errors are latched on the device and
  * reported by the next vmqg_match_status(). */
@@ -208,7 +207,8 @@ int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub,
                       const uint32_t* d_words, vmqg_emit* d_out, uint64_t out_cap,
                       uint64_t* d_offsets, void* stream);
 
-/* Synchronises `stream` and returns the status latched by every
+/* Synchronises `stream` (NULL = the legacy default stream), after the
+ * match calls queued on any stream, and returns the status latched by every
  * vmqg_match_device / vmqg_match_ranges_device call since the previous
  * vmqg_match_status (VMQG_OK, VMQG_E_OVERFLOW, VMQG_E_FRONTIER,
  * VMQG_E_DEVICE), then clears it: an error of any call in a pipelined

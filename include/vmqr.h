@@ -92,8 +92,8 @@ int vmqr_match_batch(vmqr_ctx* ctx, const vmqg_pub* filters, size_t n, const uin
                      uint32_t* out, size_t out_cap, size_t* out_n, uint64_t* offsets);
 
 /* Device-buffer form (pointers on the context's device, work on `stream`,
- * NULL = the context's stream ordered like default-stream work as in
- * vmqg_match_device; no synchronisation); errors latch for vmqr_match_status. */
+ * NULL = the legacy default stream as in vmqg_match_device; no
+ * synchronisation); errors latch for vmqr_match_status. */
 int vmqr_match_device(vmqr_ctx* ctx, const vmqg_pub* d_filters, uint32_t n, const uint32_t* d_words,
                       uint32_t* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream);
 int vmqr_match_status(vmqr_ctx* ctx, void* stream);

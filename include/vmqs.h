@@ -88,8 +88,8 @@ int vmqs_select_batch(vmqs_ctx* ctx, const vmqg_emit* emits, const uint64_t* off
                       uint32_t policy, uint64_t seed, uint64_t pub_seq, uint8_t* chosen, uint32_t* failed);
 
 /* Device-buffer form: every pointer on the context's device, work on
- * `stream` (NULL = the context's stream, ordered like default-stream work:
- * see vmqg_match_device), no synchronisation.  d_failed may
+ * `stream` (NULL = the legacy default stream, see vmqg_match_device), no
+ * synchronisation.  d_failed may
  * be NULL.  A publish whose groups exceed the device tables or whose segment
  * exceeds VMQS_MAX_SEGMENT latches VMQG_E_LIMIT for vmqs_select_status. */
 int vmqs_select_device(vmqs_ctx* ctx, const vmqg_emit* d_emits, const uint64_t* d_offsets, uint32_t npub,

@@ -369,8 +369,8 @@ def test_device_entry_point_with_torch_buffers():
 
 
 def test_null_stream_is_ordered_with_torch_default_stream():
-    """stream = NULL (torch's default stream handle) is ordered like default-
-    stream work: the match waits for inputs still being copied in behind a
+    """stream = NULL (torch's default stream handle) runs on the legacy
+    default stream: the match waits for inputs still being copied in behind a
     long default-stream queue, and a default-stream read-back waits for the
     match — no torch.cuda.synchronize() in between (vmqg_nullorder.h)."""
     import torch

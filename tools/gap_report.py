@@ -1,13 +1,66 @@
 #!/usr/bin/env python3
-"""Print the last kernels of a rocprofv3 kernel trace with their durations
-and the idle gap before each.  usage: gap_report.py run_kernel_trace.csv [n]"""
+"""Per-step GPU timeline of bench.py config C from a rocprofv3 kernel trace:
+for the last `--steps` match calls (five launches each: COUNT fast tier,
+COUNT wave tier, scan, EMIT fast tier, EMIT wave tier), the median duration
+of every launch and of the idle gap before it (end of the previous kernel to
+start of this one).  usage: gap_report.py <kernel_trace.csv> [--steps N]"""
+import argparse
 import csv
-import sys
+import json
+import statistics
 
-rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
-prev = None
-for r in rows[-n:]:
-    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    print("%-44s dur %8.1f us  gap %7.1f us" % (r["Kernel_Name"][:44], (e - s) / 1e3, (s - prev) / 1e3 if prev else 0))
-    prev = e
+
+def short(name):
+    for k in ("k_match_fast<0", "k_match_fast<1", "k_match_wave<0", "k_match_wave<1", "k_scan_offsets"):
+        if k in name:
+            return k
+    return name.split("(")[0][-40:]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, default=10)
+    args = ap.parse_args()
+    rows = []
+    with open(args.trace) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
+    rows.sort()
+    match = [r for r in rows if r[2].startswith("k_match") or r[2] == "k_scan_offsets"]
+    seq = ["k_match_fast<0", "k_match_wave<0", "k_scan_offsets", "k_match_fast<1", "k_match_wave<1"]
+    # the last complete steps
+    steps = []
+    i = len(match) - len(seq)
+    while i >= 0 and len(steps) < args.steps:
+        if [m[2] for m in match[i:i + len(seq)]] == seq:
+            steps.append(match[i:i + len(seq)])
+            i -= len(seq)
+        else:
+            i -= 1
+    steps.reverse()
+    dur = {k: [] for k in seq}
+    gap = {k: [] for k in seq}
+    step_ns = []
+    for s_idx, st in enumerate(steps):
+        prev_end = None
+        if s_idx > 0:
+            prev_end = steps[s_idx - 1][-1][1]
+        for (t0, t1, k) in st:
+            dur[k].append(t1 - t0)
+            if prev_end is not None:
+                gap[k].append(t0 - prev_end)
+            prev_end = t1
+        if s_idx > 0:
+            step_ns.append(st[-1][1] - steps[s_idx - 1][-1][1])
+    med = lambda x: statistics.median(x) / 1e3 if x else None
+    out = {"steps": len(steps), "kernel_us": {k: med(v) for k, v in dur.items()},
+           "gap_before_us": {k: med(v) for k, v in gap.items()},
+           "step_us": med(step_ns),
+           "kernels_sum_us": sum(med(v) for v in dur.values()),
+           "gaps_sum_us": sum(med(v) for v in gap.values() if v)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

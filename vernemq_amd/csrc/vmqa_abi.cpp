@@ -78,15 +78,14 @@ int vmqa_check_device(vmqa_ctx* ctx, const vmqa_req* d_reqs, uint32_t n, const u
   if (!ctx || (n && (!d_reqs || !d_words || !d_allowed))) return VMQG_E_INVAL;
   GUARD_BEGIN
   hipSetDevice(ctx->e.device);
-  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
-  return ctx->e.check_device(d_reqs, n, d_words, d_allowed, static_cast<hipStream_t>(stream));
+  return ctx->e.check_device(d_reqs, n, d_words, d_allowed, vmqg::caller_stream(stream));
   GUARD_END
 }
 
 int vmqa_check_status(vmqa_ctx* ctx, void* stream) {
   if (!ctx) return VMQG_E_INVAL;
   GUARD_BEGIN
-  return ctx->e.check_status(static_cast<hipStream_t>(stream));
+  return ctx->e.check_status(vmqg::caller_stream(stream));
   GUARD_END
 }
 

@@ -26,7 +26,6 @@ AclEngine::~AclEngine() {
   if (stream) hipStreamSynchronize(stream);
   for (auto& e : t_check) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (ev_done) hipEventDestroy(ev_done);
-  if (ev_null) hipEventDestroy(ev_null);
   hipFree(d_arena); hipFree(d_status); hipFree(d_r); hipFree(d_w); hipFree(d_o);
   if (stream) hipStreamDestroy(stream);
 }
@@ -164,7 +163,6 @@ int AclEngine::check_device(const vmqa_req* d_reqs, uint32_t n, const uint32_t* 
                             hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
-  if (!st) st = stream;
   if (vmqg::chain_order(ev_done, chk_stream, st) != VMQG_OK) return VMQG_E_DEVICE;
   if (hipMemsetAsync(d_status, 0, 32, st) != hipSuccess) return VMQG_E_DEVICE;
   if (n == 0) return VMQG_OK;
@@ -188,7 +186,7 @@ int AclEngine::check_device(const vmqa_req* d_reqs, uint32_t n, const uint32_t* 
 int AclEngine::check_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
-  if (!st) st = stream;
+  if (vmqg::chain_order(ev_done, chk_stream, st) != VMQG_OK) return VMQG_E_DEVICE;
   uint32_t h[8] = {0};
   if (hipMemcpyAsync(h, d_status, 32, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/vmqa.h"
+#include "vmqg_chain.h"
 #include "vmqg_common.h"
 
 namespace vmqa {
@@ -62,8 +63,7 @@ struct AclEngine {
   // device
   hipStream_t stream = nullptr;
   hipEvent_t ev_done = nullptr;        // uploads and checks chain across streams (vmqg_chain.h)
-  hipStream_t chk_stream = nullptr;
-  hipEvent_t ev_null = nullptr;   // NullOrder (vmqg_nullorder.h)
+  hipStream_t chk_stream = vmqg::no_stream();
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
   uint32_t* d_status = nullptr;
   void* d_r = nullptr; uint64_t d_r_cap = 0;   // host-buffer staging

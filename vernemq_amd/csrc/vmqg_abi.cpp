@@ -176,9 +176,8 @@ int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, cons
   if (!ctx || !d_offsets || (npub && (!d_pubs || !d_words))) return VMQG_E_INVAL;
   GUARD_BEGIN
   hipSetDevice(ctx->e.device);
-  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
   return ctx->e.match_device(d_pubs, npub, d_words, reinterpret_cast<vmqg::Record*>(d_out), out_cap, nullptr, 0,
-                             d_offsets, static_cast<hipStream_t>(stream));
+                             d_offsets, vmqg::caller_stream(stream));
   GUARD_END
 }
 
@@ -189,9 +188,8 @@ int vmqg_match_ranges_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npu
   // a non-null range buffer selects range mode even at out_cap 0
   static vmqg_range dummy;
   hipSetDevice(ctx->e.device);
-  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
   return ctx->e.match_device(d_pubs, npub, d_words, nullptr, 0, d_out ? d_out : &dummy, out_cap, d_offsets,
-                             static_cast<hipStream_t>(stream));
+                             vmqg::caller_stream(stream));
   GUARD_END
 }
 
@@ -207,7 +205,7 @@ int vmqg_records(vmqg_ctx* ctx, const vmqg_emit** recs, uint64_t* n) {
 int vmqg_match_status(vmqg_ctx* ctx, void* stream) {
   if (!ctx) return VMQG_E_INVAL;
   GUARD_BEGIN
-  return ctx->e.match_status(static_cast<hipStream_t>(stream));
+  return ctx->e.match_status(vmqg::caller_stream(stream));
   GUARD_END
 }
 
@@ -314,8 +312,7 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
   memcpy(&L, layout, sizeof(L));
   if (L.magic != vmqg::kLayoutMagic) return VMQG_E_INVAL;
   hipSetDevice(e.device);
-  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e.stream;
-  vmqg::NullOrder order(stream, e.stream, e.ev_null);
+  hipStream_t st = vmqg::caller_stream(stream);
   if (e.d_arena_bytes < L.total_bytes) {
     if (hipDeviceSynchronize() != hipSuccess) return VMQG_E_DEVICE;
     if (e.d_arena) hipFree(e.d_arena);
@@ -360,8 +357,7 @@ int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t byt
   Engine& e = ctx->e;
   if (!e.has_device || !e.d_arena) return VMQG_E_DEVICE;
   hipSetDevice(e.device);
-  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e.stream;
-  vmqg::NullOrder order(stream, e.stream, e.ev_null);
+  hipStream_t st = vmqg::caller_stream(stream);
   // tables change only after the matches queued before, and matches queued
   // later (on any stream) see the patches
   if (e.order_on(st) != VMQG_OK) return VMQG_E_DEVICE;

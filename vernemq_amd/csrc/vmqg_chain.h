@@ -16,8 +16,11 @@
 
 namespace vmqg {
 
+// "no work queued yet" (NULL is a real stream: the legacy default stream)
+inline hipStream_t no_stream() { return reinterpret_cast<hipStream_t>(~uintptr_t(0)); }
+
 inline int chain_order(hipEvent_t ev, hipStream_t& last, hipStream_t st) {
-  if (last && st != last) {
+  if (last != no_stream() && st != last) {
     if (hipEventRecord(ev, last) != hipSuccess) return VMQG_E_DEVICE;
     if (hipStreamWaitEvent(st, ev, 0) != hipSuccess) return VMQG_E_DEVICE;
   }

@@ -25,7 +25,6 @@ Engine::~Engine() {
     for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
     if (ev_match_done) hipEventDestroy(ev_match_done);
-    if (ev_null) hipEventDestroy(ev_null);
     for (Stage& sg : stage) {
       if (sg.ev) hipEventDestroy(sg.ev);
       if (sg.h) hipHostFree(sg.h);
@@ -1025,7 +1024,6 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   if (!has_device) return VMQG_E_DEVICE;
   if (!d_arena) return VMQG_E_STATE;
   hipSetDevice(device);
-  if (!st) st = stream;
   // table changes (patches, images) land before this match: the primary's on
   // the context stream, a replica's on whatever stream the caller gave
   if (order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
@@ -1064,7 +1062,7 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
 int Engine::match_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
-  if (!st) st = stream;
+  if (order_on(st) != VMQG_OK) return VMQG_E_DEVICE;   // the matches queued on any stream
   uint32_t h[12] = {0};
   if (hipMemcpyAsync(h, d_status, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;

@@ -16,6 +16,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "vmqg_chain.h"
 #include "vmqg_common.h"
 #include "vmqg_kernels.h"
 
@@ -215,8 +216,7 @@ struct Engine {
   void* d_offs = nullptr; uint64_t d_offs_cap = 0;
   void* d_out = nullptr; uint64_t d_out_cap = 0;
   hipEvent_t ev_match_done = nullptr;   // recorded by order_on when the stream changes
-  hipStream_t ev_stream = nullptr;      // the stream table changes / matches were last queued on
-  hipEvent_t ev_null = nullptr;      // NullOrder (vmqg_nullorder.h)
+  hipStream_t ev_stream = vmqg::no_stream();      // the stream table changes / matches were last queued on
   bool timing = false;
   uint32_t opt_fast_g = 2, opt_flags = kOptNtStores;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
   uint32_t opt_count_bpc = 4, opt_emit_bpc = 16;       // fast-tier grid caps, blocks per CU (A/B-tuned)

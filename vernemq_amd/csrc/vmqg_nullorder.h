@@ -1,39 +1,22 @@
-// Ordering for device entry points called with stream = NULL.
+// The stream a device entry point runs on.
 //
-// The ABI reads a NULL `stream` as "the context's own stream" (include/*.h).
-// That stream is non-blocking, so by itself it would neither wait for work
-// the caller queued on the legacy default stream — whose handle is also NULL,
-// e.g. torch's default stream filling the inputs — nor make later default-
-// stream work (reading the outputs back) wait for it.  NullOrder, held for
-// the duration of such a call, orders the context stream after the default
-// stream on entry and the default stream after the context stream on exit,
-// so a NULL call behaves like default-stream work.  Calls with an explicit
-// stream are ordered by that stream alone.
+// The ABI reads a NULL `stream` as the legacy default stream (torch's default
+// stream handle is NULL too): the call's work is queued on that stream
+// itself (handle NULL), so it is ordered after the default-stream work
+// the caller queued before (e.g. the copies filling its inputs) and before
+// the default-stream work it queues after (reading the outputs back), with
+// no cross-stream handshake.  An earlier version ran NULL calls on the
+// context's own stream and tied it to the default stream with an event pair
+// per call: ~28 us of GPU idle time per call on MI355X
+// (profiles/gap_r02_context_stream.json vs gap_r02_legacy_stream.json).  Calls with an explicit stream run on it.
 #pragma once
 #include <hip/hip_runtime.h>
 
 namespace vmqg {
 
-struct NullOrder {
-  hipStream_t ctx;
-  hipEvent_t ev;
-  bool on;
-  NullOrder(void* caller_stream, hipStream_t ctx_stream, hipEvent_t& ev_slot)
-      : ctx(ctx_stream), ev(nullptr), on(caller_stream == nullptr && ctx_stream != nullptr) {
-    if (!on) return;
-    if (!ev_slot && hipEventCreateWithFlags(&ev_slot, hipEventDisableTiming) != hipSuccess) ev_slot = nullptr;
-    ev = ev_slot;
-    if (!ev) { on = false; return; }
-    hipEventRecord(ev, nullptr);
-    hipStreamWaitEvent(ctx, ev, 0);
-  }
-  ~NullOrder() {
-    if (!on) return;
-    hipEventRecord(ev, ctx);
-    hipStreamWaitEvent(nullptr, ev, 0);
-  }
-  NullOrder(const NullOrder&) = delete;
-  NullOrder& operator=(const NullOrder&) = delete;
-};
+// (Engines therefore never read a NULL stream as their own: internal work
+// names the context stream explicitly.  The hipStreamLegacy sentinel is not
+// used: hipEventRecord on it crashed the runtime.)
+inline hipStream_t caller_stream(const void* s) { return static_cast<hipStream_t>(const_cast<void*>(s)); }
 
 }  // namespace vmqg

@@ -80,15 +80,14 @@ int vmqr_match_device(vmqr_ctx* ctx, const vmqg_pub* d_filters, uint32_t n, cons
   if (!ctx || !d_offsets || (n && (!d_filters || !d_words))) return VMQG_E_INVAL;
   GUARD_BEGIN
   hipSetDevice(ctx->e.device);
-  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
-  return ctx->e.match_device(d_filters, n, d_words, d_out, out_cap, d_offsets, static_cast<hipStream_t>(stream));
+  return ctx->e.match_device(d_filters, n, d_words, d_out, out_cap, d_offsets, vmqg::caller_stream(stream));
   GUARD_END
 }
 
 int vmqr_match_status(vmqr_ctx* ctx, void* stream) {
   if (!ctx) return VMQG_E_INVAL;
   GUARD_BEGIN
-  return ctx->e.match_status(static_cast<hipStream_t>(stream));
+  return ctx->e.match_status(vmqg::caller_stream(stream));
   GUARD_END
 }
 

@@ -25,7 +25,6 @@ RetainEngine::~RetainEngine() {
   for (auto* v : {&t_count, &t_scan, &t_emit})
     for (auto& e : *v) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (ev_match_done) hipEventDestroy(ev_match_done);
-  if (ev_null) hipEventDestroy(ev_null);
   hipFree(d_arena); hipFree(d_patch); hipFree(d_status); hipFree(d_tickets); hipFree(d_plan); hipFree(d_lookback);
   hipFree(d_f); hipFree(d_w); hipFree(d_o); hipFree(d_offs);
   if (h_patch) hipHostFree(h_patch);
@@ -423,7 +422,6 @@ int RetainEngine::match_device(const vmqg_pub* d_filters, uint32_t nf, const uin
                                uint64_t out_cap, uint64_t* d_offsets, hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
-  if (!st) st = stream;
   // match_fold must not read tables a pending patch upload is writing: the
   // context's stream is synchronised at the end of every apply; later
   // applies wait for this match (order_on).  The status words and the walk
@@ -489,7 +487,7 @@ int RetainEngine::grow_tiles(uint64_t rows, hipStream_t st) {
 int RetainEngine::match_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
-  if (!st) st = stream;
+  if (order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
   uint32_t h[8] = {0};
   if (hipMemcpyAsync(h, d_status, 32, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/vmqr.h"
+#include "vmqg_chain.h"
 #include "vmqg_common.h"
 #include "vmqg_engine.h"
 
@@ -134,9 +135,8 @@ struct RetainEngine {
   uint64_t epoch = 0, rebuilds = 0;
   // device
   hipStream_t stream = nullptr;
-  hipEvent_t ev_null = nullptr;   // NullOrder (vmqg_nullorder.h)
   hipEvent_t ev_match_done = nullptr;   // recorded by order_on when the stream changes
-  hipStream_t ev_stream = nullptr;      // the stream patches / matches were last queued on
+  hipStream_t ev_stream = vmqg::no_stream();      // the stream patches / matches were last queued on
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
   Patch* h_patch = nullptr; uint64_t h_patch_cap = 0;
   Patch* d_patch = nullptr; uint64_t d_patch_cap = 0;

@@ -16,7 +16,6 @@ SelEngine::~SelEngine() {
   if (stream) hipStreamSynchronize(stream);
   for (auto& e : t_sel) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (ev_sel) hipEventDestroy(ev_sel);
-  if (ev_null) hipEventDestroy(ev_null);
   hipFree(d_states); hipFree(d_status); hipFree(d_defer);
   hipFree(d_e); hipFree(d_o); hipFree(d_c); hipFree(d_f);
   if (stream) hipStreamDestroy(stream);
@@ -71,7 +70,6 @@ int SelEngine::select_device(const vmqg_emit* d_emits, const uint64_t* d_offsets
                              hipStream_t st) {
   if (policy > VMQS_POLICY_LOCAL_ONLY) return VMQG_E_INVAL;
   hipSetDevice(device);
-  if (!st) st = stream;
   if (vmqg::chain_order(ev_sel, sel_stream, st) != VMQG_OK) return VMQG_E_DEVICE;
   if (npub > defer_cap) {
     uint64_t c = 1024;
@@ -99,7 +97,7 @@ int SelEngine::select_device(const vmqg_emit* d_emits, const uint64_t* d_offsets
 
 int SelEngine::select_status(hipStream_t st) {
   hipSetDevice(device);
-  if (!st) st = stream;
+  if (vmqg::chain_order(ev_sel, sel_stream, st) != VMQG_OK) return VMQG_E_DEVICE;
   uint32_t h[2] = {0, 0};
   if (hipMemcpyAsync(h, d_status, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
@@ -190,16 +188,15 @@ int vmqs_select_device(vmqs_ctx* ctx, const vmqg_emit* d_emits, const uint64_t* 
   if (!ctx || (npub && (!d_emits || !d_offsets || !d_chosen))) return VMQG_E_INVAL;
   GUARD_BEGIN
   hipSetDevice(ctx->e.device);
-  vmqg::NullOrder order(stream, ctx->e.stream, ctx->e.ev_null);
   return ctx->e.select_device(d_emits, d_offsets, npub, policy, seed, pub_seq, d_chosen, d_failed,
-                              static_cast<hipStream_t>(stream));
+                              vmqg::caller_stream(stream));
   GUARD_END
 }
 
 int vmqs_select_status(vmqs_ctx* ctx, void* stream) {
   if (!ctx) return VMQG_E_INVAL;
   GUARD_BEGIN
-  return ctx->e.select_status(static_cast<hipStream_t>(stream));
+  return ctx->e.select_status(vmqg::caller_stream(stream));
   GUARD_END
 }
 

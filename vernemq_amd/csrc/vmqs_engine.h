@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/vmqs.h"
+#include "vmqg_chain.h"
 #include "vmqg_common.h"
 
 namespace vmqs {
@@ -54,9 +55,8 @@ struct SelEngine {
   uint8_t* d_states = nullptr; uint64_t n_states = 0, states_cap = 0;
   std::vector<uint8_t> h_states;   // host copy of the state table
   uint32_t* d_status = nullptr;
-  hipEvent_t ev_null = nullptr;   // NullOrder (vmqg_nullorder.h)
   hipEvent_t ev_sel = nullptr;     // state-table updates and selects chain across streams (vmqg_chain.h)
-  hipStream_t sel_stream = nullptr;
+  hipStream_t sel_stream = vmqg::no_stream();
   uint32_t* d_defer = nullptr; uint64_t defer_cap = 0;
   void* d_e = nullptr; uint64_t d_e_cap = 0;   // host-buffer staging
   void* d_o = nullptr; uint64_t d_o_cap = 0;
