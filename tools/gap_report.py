@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-step GPU timeline of bench.py config C from a rocprofv3 kernel trace:
 for the last `--steps` match calls (five launches each: COUNT fast tier,
-COUNT wave tier, scan, EMIT fast tier, EMIT wave tier), the median duration
+scan (+ wave tiers), EMIT fast tier; older builds had separate wave-tier
+launches), the median duration
 of every launch and of the idle gap before it (end of the previous kernel to
 start of this one).  usage: gap_report.py <kernel_trace.csv> [--steps N]"""
 import argparse
@@ -28,17 +29,11 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     rows.sort()
     match = [r for r in rows if r[2].startswith("k_match") or r[2] == "k_scan_offsets"]
-    seq = ["k_match_fast<0", "k_match_wave<0", "k_scan_offsets", "k_match_fast<1", "k_match_wave<1"]
-    # the last complete steps
-    steps = []
-    i = len(match) - len(seq)
-    while i >= 0 and len(steps) < args.steps:
-        if [m[2] for m in match[i:i + len(seq)]] == seq:
-            steps.append(match[i:i + len(seq)])
-            i -= len(seq)
-        else:
-            i -= 1
-    steps.reverse()
+    # a step: the launches from one COUNT fast tier to the next
+    starts = [i for i, r in enumerate(match) if r[2] == "k_match_fast<0"]
+    steps = [match[a:b] for a, b in zip(starts, starts[1:])][-args.steps:]
+    seq = [k for (_, _, k) in steps[-1]]
+    steps = [st for st in steps if [k for (_, _, k) in st] == seq]
     dur = {k: [] for k in seq}
     gap = {k: [] for k in seq}
     step_ns = []
