@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--opt", action="append", default=[], help="name=v1,v2,...")
-    ap.add_argument("--config", default="C", choices=["C", "D"])
+    ap.add_argument("--config", default="C", choices=["C", "D", "E"])
+    ap.add_argument("--e-scale", type=float, default=0.2)
     ap.add_argument("--d-scale", type=float, default=1.0)
     ap.add_argument("--n-dev", type=int, default=1_000_000)
     args = ap.parse_args()
@@ -36,6 +37,13 @@ def main():
         w = W.config_c(n_dev=args.n_dev)
         v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
         w.load_into(v)
+    elif args.config == "E":
+        w = W.config_e(scale=args.e_scale)
+        n = w.n_subs
+        v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes, max_mountpoints=max(1024, len(w.mps) + 1),
+                       hints={"edges": 2 * n, "paths": 2 * n, "keys": n * 5 // 4, "records": n * 5 // 4,
+                              "exact": n * 5 // 4})
+        w.load_into(v)
     else:
         w = W.config_d(scale=args.d_scale, n_pubs=1 << 20)
         n_live = w.notes["n_live"]
@@ -46,7 +54,7 @@ def main():
     pubs, words = w.publish_arrays(v)
     d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
     d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
-    cap = 66 * len(pubs) if args.config == "C" else 520 * len(pubs)
+    cap = {"C": 66, "D": 520, "E": 400}[args.config] * len(pubs)
     d_out = torch.empty(cap * 4, dtype=torch.int32, device=dev)
     d_offs = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream().cuda_stream
