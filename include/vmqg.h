@@ -255,7 +255,8 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out);
 int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
 
 /* Tuning knobs of the match kernels (no effect on results):
- *   "fast_g"    2 | 4      lanes per publish in the fast tier (default 2)
+ *   "fast_g"    1 | 2 | 4  lanes per publish in the fast tier (default 1: one lane per
+ *                          publish in COUNT, two in EMIT over the same 64-publish chunks)
  *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
  *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8;
  *                          defaults 4 and 16) */

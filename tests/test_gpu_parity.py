@@ -505,7 +505,7 @@ def test_config_d_churn_parity(mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-@pytest.mark.parametrize("fast_g", [2, 4])
+@pytest.mark.parametrize("fast_g", [1, 2, 4])
 def test_output_offsets_of_a_large_deferral_heavy_batch(mode, fast_g):
     """Output offsets over 300,000 publishes (9,375 chunks of 32 publishes,
     18,750 of 16) where every 23rd is h/x/y/z, which 31 filters match (more

@@ -1005,7 +1005,7 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.keycache = d_keycache;
   a.keyspill = reinterpret_cast<uint2*>(static_cast<char*>(d_keycache) + keycache_cap * 32);
   a.chunk = reinterpret_cast<uint64_t*>(static_cast<char*>(d_keycache) + keycache_cap * (32 + 8 * 8));
-  a.gpw = 64 / (opt_fast_g == 4 ? 4 : 2);
+  a.gpw = 64 / (opt_fast_g == 4 ? 4 : opt_fast_g == 1 ? 1 : 2);   // publishes per chunk
   a.status = d_status + 4 * (call_seq & 1);
   a.status_next = d_status + 4 * ((call_seq + 1) & 1);
   a.err = d_status + 8;

@@ -265,7 +265,7 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
 template <int G>
 struct FastScratch {
   static constexpr uint32_t GPW = 64 / G, SLOTS = kWaves * GPW;
-  static constexpr uint32_t SH = G == 2 ? 4 : G == 4 ? 3 : 2;   // 32 / G = 1 << SH
+  static constexpr uint32_t SH = G == 1 ? 5 : G == 2 ? 4 : G == 4 ? 3 : 2;   // 32 / G = 1 << SH
   static constexpr uint32_t SC = FastCaps<G>::S, CC = FastCaps<G>::C, KC = FastCaps<G>::K;
   uint2* stack; uint32_t* cand; uint2* keys;
   uint32_t slot;
@@ -549,13 +549,16 @@ __device__ __forceinline__ uint64_t chunk_offsets(const MatchArgs& a, uint32_t f
 // of one wave.  Resolve is per group; the copy is wave-wide over the wave's
 // output range minus the ranges of publishes the wave tier writes, so every
 // store instruction writes up to 64 x 16 B = 1 KiB contiguous.
-template <int G, int GPW, bool NT, int U>
+template <int G, int GPW, bool NT, int U, bool PRE = false>
 __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const FastScratch<G>& s,
-                          const Group<G>& g, GroupMeta* gm, uint32_t slot0) {
+                          const Group<G>& g, GroupMeta* gm, uint32_t slot0, uint64_t pre_obase = 0,
+                          uint64_t pre_oend = 0, uint64_t pre_wbase = 0) {
   const uint32_t p = first + g.gidx;
   const bool valid = g.gidx < n;
-  uint64_t obase, oend;
-  const uint64_t wbase = chunk_offsets<G, GPW>(a, first, n, g, obase, oend);
+  uint64_t obase = pre_obase, oend = pre_oend;
+  // PRE: the positions come from the caller (a chunk of two waves' worth of
+  // publishes, chunk_positions64)
+  const uint64_t wbase = PRE ? pre_wbase : chunk_offsets<G, GPW>(a, first, n, g, obase, oend);
   uint32_t nk = 0, ksum = 0;
   uint64_t rmask = 0;
   bool ok = false;
@@ -649,7 +652,21 @@ __device__ void emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScra
 }
 
 // --------------------------------------------------------------- kernels
-template <int MODE, int OUT, int G, bool NT>
+// Positions of the publishes of a 64-publish chunk (the chunks of a one-lane
+// COUNT, fast_g 1): lane l reads publish first + l's count, the wave scans
+// them from the chunk's base and writes the final offsets; returns lane l's
+// position and count for the halves to pick up.
+__device__ __forceinline__ void chunk_positions64(const MatchArgs& a, uint32_t first, uint32_t nch, uint64_t& pos,
+                                                  uint64_t& cnt) {
+  const uint32_t lane = __lane_id();
+  const bool valid = lane < nch;
+  cnt = valid ? a.offsets[first + lane] : 0;
+  const uint64_t incl = wave_incl_scan64(cnt);
+  pos = a.chunk[first / 64] + incl - cnt;
+  if (valid) a.offsets[first + lane] = pos;
+}
+
+template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
 #ifndef VMQG_COUNT_WPE
 #define VMQG_COUNT_WPE 4   // COUNT waves per SIMD the register budget must allow (A/B: 4, 5)
 #endif
@@ -665,6 +682,32 @@ void k_match_fast(MatchArgs a) {
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
+  if constexpr (MODE == 1 && CH != GPW) {
+    // EMIT over the 64-publish chunks of a one-lane COUNT, as two halves of
+    // GPW = 32 publishes with two lanes per publish
+    static_assert(CH == 2 * GPW, "");
+    const uint32_t stride = gridDim.x * kWaves * CH;
+    for (uint32_t base = (blockIdx.x * kWaves + wv) * CH; base < a.npub; base += stride) {
+      const uint32_t nch = a.npub - base < (uint32_t)CH ? a.npub - base : (uint32_t)CH;
+      uint64_t pos, cnt;
+      chunk_positions64(a, base, nch, pos, cnt);
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t first = base + h * GPW;
+        if (nch <= h * GPW) break;
+        const uint32_t n = nch - h * GPW < (uint32_t)GPW ? nch - h * GPW : (uint32_t)GPW;
+        const uint32_t q = h * GPW + g.gidx;
+        const uint64_t ob = __shfl(pos, q, 64), oe = ob + __shfl(cnt, q, 64);
+        const uint64_t wb = __shfl(pos, h * GPW, 64);
+        if (OUT == 0) {
+          emit_wave<G, GPW, NT, VMQG_EMIT_U, true>(a, first, n, s, g, gm[wv], wv * GPW, ob, oe, wb);
+        } else if (g.gidx < n) {
+          emit_ranges_group<G>(a, first + g.gidx, s, g, ob, oe);
+        }
+        wave_sync();
+      }
+    }
+    return;
+  }
   const uint32_t stride = gridDim.x * kWaves * GPW;
   for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
@@ -1014,10 +1057,10 @@ hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int MODE, int OUT, int G, bool NT>
+template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
 static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
-  if (t0) hipExtLaunchKernelGGL(k_match_fast<MODE, OUT, G, NT>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
-  else k_match_fast<MODE, OUT, G, NT><<<g, 256, 0, st>>>(a);
+  if (t0) hipExtLaunchKernelGGL(k_match_fast<MODE, OUT, G, NT, CH>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+  else k_match_fast<MODE, OUT, G, NT, CH><<<g, 256, 0, st>>>(a);
 }
 
 template <int MODE, int OUT>
@@ -1025,6 +1068,14 @@ static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st,
   if (a.fast_g == 4) {
     if (nt) launch_fast_k<MODE, OUT, 4, true>(a, g, st, t0, t1);
     else launch_fast_k<MODE, OUT, 4, false>(a, g, st, t0, t1);
+  } else if (a.fast_g == 1) {   // one-lane COUNT; EMIT two lanes per publish over its 64-publish chunks
+    if (MODE == 0) {
+      if (nt) launch_fast_k<0, OUT, 1, true>(a, g, st, t0, t1);
+      else launch_fast_k<0, OUT, 1, false>(a, g, st, t0, t1);
+    } else {
+      if (nt) launch_fast_k<1, OUT, 2, true, 64>(a, g, st, t0, t1);
+      else launch_fast_k<1, OUT, 2, false, 64>(a, g, st, t0, t1);
+    }
   } else {
     if (nt) launch_fast_k<MODE, OUT, 2, true>(a, g, st, t0, t1);
     else launch_fast_k<MODE, OUT, 2, false>(a, g, st, t0, t1);
@@ -1041,7 +1092,8 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, 
   const bool nt = (a.opts & kOptNtStores) != 0;
   const int out = a.out_rng ? 1 : 0;
   if (tier == 0) {
-    const uint32_t G = a.fast_g == 4 ? 4 : 2;
+    // publishes per wave: 64 / lanes per publish (fast_g 1: 64 for both passes)
+    const uint32_t G = a.fast_g == 4 ? 4 : a.fast_g == 1 ? 1 : 2;
     uint32_t g = div_up(a.npub, kWaves * (64 / G));
     // grid-stride beyond bpc blocks per CU (option count_bpc / emit_bpc; 8 default)
     const uint32_t bpc = mode == 0 ? a.count_bpc : a.emit_bpc;

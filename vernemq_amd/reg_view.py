@@ -303,7 +303,7 @@ class RegGpuView:
         return self._L.vmqg_match_status(self._h, stream or None)
 
     def set_option(self, name: str, value: int):
-        """Kernel tuning knob (vmqg_set_option): "fast_g" 2|4, "nt_stores" 0|1, "count_bpc" / "emit_bpc"."""
+        """Kernel tuning knob (vmqg_set_option): "fast_g" 1|2|4, "nt_stores" 0|1, "count_bpc" / "emit_bpc"."""
         _lib.check(self._L.vmqg_set_option(self._h, name.encode(), int(value)), "vmqg_set_option")
 
     def set_timing(self, on: bool):
