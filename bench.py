@@ -89,6 +89,9 @@ def main():
     ap.add_argument("--rt-filters", type=int, default=1 << 18, help="RT: subscription filters per step")
     ap.add_argument("--rt-heavy", type=int, default=16, help="RT: devices/+/telemetry/{m} filters per step")
     ap.add_argument("--e-scale", type=float, default=1.0, help="config E scale (1.0 = 50M subs)")
+    ap.add_argument("--fast-g", type=int, default=None,
+                    help="vmqg option fast_g for the secondary configs (default: the library's 1; 2 for E, "
+                         "whose publishes match 5-8 keys: the one-lane COUNT defers them, profiles/ab_r02_count_one_lane_e.json)")
     ap.add_argument("--r-n", type=int, default=1_000_000, help="R1 / R2: N (the reference suite goes to 4,096,000)")
     ap.add_argument("--d-scale", type=float, default=1.0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N>1 on one GPU")
@@ -364,11 +367,11 @@ def main():
             "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3, "launches": nlaunch},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
-                         "kernel": "k_match_fast<1,0,2,true> (EMIT)",
+                         "kernel": "k_match_fast<1,0,2,true,64> (EMIT)",
                          "algorithmic_bytes_per_launch": alg["emit_compulsory"],
                          "bytes_model": "16 B written per emission + 40 B read per publish + 16 B per distinct "
                                         "record (workloads.algorithmic_bytes_c emit_compulsory)"},
-            "count_kernel": {"kernel": "k_match_fast<0,0,2,true> (COUNT)", "us": count_ns / 1e3 if count_ns else None,
+            "count_kernel": {"kernel": "k_match_fast<0,0,1,true,64> (COUNT)", "us": count_ns / 1e3 if count_ns else None,
                              "lookup_bytes_model": alg["count"],
                              "achieved": alg["count"] / count_ns if count_ns else None},
             "survey_model": {"bytes_per_step": alg["all"], "achieved_per_step": alg["all"] / pipe_ns,
@@ -426,6 +429,9 @@ def bench_other(args):
 
     w.load_into(view, progress=progress)
     load_s = time.time() - t0
+    fast_g = args.fast_g or (2 if args.config == "E" else None)
+    if fast_g:
+        view.set_option("fast_g", fast_g)
     st = view.stats_raw()
     log("config %s: %d subs generated in %.1fs, loaded in %.1fs (host engine %.1fs), %s"
         % (args.config, n, gen_s, load_s, st["apply_host_ns"] / 1e9, st))
@@ -554,7 +560,8 @@ def bench_other(args):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic: SURVEY.md §8(d) config %s generator" % args.config,
         "config": {"workload": "%s: %d subs, %d publishes per step%s"
-                               % (args.config, n, npub, ", %d mountpoints" % len(w.mps) if len(w.mps) > 1 else "")},
+                               % (args.config, n, npub, ", %d mountpoints" % len(w.mps) if len(w.mps) > 1 else ""),
+                   "fast_g": fast_g or 1},
         "pairs_per_s": em * args.steps / el, "emissions_per_step": em,
         "kernel_us": {"count": count_ns / 1e3, "emit": emit_ns / 1e3},
         "roofline": roof, "survey_bytes_per_publish": b_p, "oracle_sample": parity, "cpu_baseline": cpu,
@@ -820,7 +827,7 @@ def bench_d(args):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS if achieved else None,
                          "traffic": load_pmc_traffic("k_match_fast<1", "pmc_d.json"),
-                         "kernel": "k_match_fast<1,0,2,true> (EMIT)", "algorithmic_bytes_per_launch": alg_emit,
+                         "kernel": "k_match_fast<1,0,2,true,64> (EMIT)", "algorithmic_bytes_per_launch": alg_emit,
                          "bytes_model": "16 B written per emission (compulsory lower bound)",
                          "survey_model_achieved": 32 * emitted / emit_ns if emit_ns else None},
             "survey_bytes_per_publish": b_p,
