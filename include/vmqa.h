@@ -116,6 +116,14 @@ int vmqa_check_device(vmqa_ctx* ctx, const vmqa_req* d_reqs, uint32_t n, const u
                       uint8_t* d_allowed, void* stream);
 int vmqa_check_status(vmqa_ctx* ctx, void* stream);
 
+/* Streams: device calls take the caller's stream (NULL = the legacy default
+ * stream).  The context orders its work across streams by recording an event
+ * on the stream it last queued on when the next call comes on another one;
+ * so a stream passed to any entry point must stay alive until the next call
+ * on the context, or be released first with vmqa_release_stream (records that
+ * event now; no-op if the context's last work is not on it). */
+int vmqa_release_stream(vmqa_ctx* ctx, void* stream);
+
 int vmqa_stats(vmqa_ctx* ctx, vmqa_stats_t* out);
 
 /* Average duration (ns) of the check kernel over the timed calls. */

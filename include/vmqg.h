@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VMQG_ABI_VERSION 2
+#define VMQG_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------- */
 #define VMQG_OK 0
@@ -130,7 +130,7 @@ typedef struct vmqg_stats_s {
   uint64_t paths;           /* interned trie paths (host)                   */
   uint64_t words;           /* interned words                               */
   uint64_t deferred_tier1;  /* publishes of the last checked match batch walked */
-  uint64_t deferred_tier2;  /* by a whole wave (LDS stack) / with a global stack */
+  uint64_t deferred_tier2;  /* by a whole wave (LDS stack) / of those, again with a global stack */
   uint64_t ops_applied;     /* vmqg_apply_ops: ops applied so far               */
   uint64_t apply_host_ns;   /*   time inside vmqg_apply_ops, of which:           */
   uint64_t apply_upload_ns; /*   staging + enqueueing the patches, of which:      */
@@ -139,6 +139,14 @@ typedef struct vmqg_stats_s {
   uint64_t patch_bytes;     /*   patch bytes shipped to the device               */
   uint64_t image_bytes;     /*   full-image bytes shipped (re-layouts)           */
   uint64_t max_depth;       /* deepest trie path (levels)                       */
+  /* ABI 3: how the last checked match batch was served                        */
+  uint64_t many_key;        /* publishes with more keys than the fast tier's    */
+                            /* lists, expanded wave-wide by EMIT (no deferral)  */
+  uint64_t retried;         /* publishes the one-lane fast pass could not hold, */
+                            /* retried four lanes per publish (the rest of them */
+                            /* are the deferred_tier1 walks)                    */
+  uint64_t wave_entries;    /* entries (records or ranges) written by the EMIT  */
+                            /* wave-tier launch (deferred + many-key publishes) */
 } vmqg_stats_t;
 
 /* ---- lifecycle ------------------------------------------------------- */
@@ -215,6 +223,14 @@ int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub,
  * sequence is reported, not only the last call's. */
 int vmqg_match_status(vmqg_ctx* ctx, void* stream);
 
+/* Streams: device calls take the caller's stream (NULL = the legacy default
+ * stream).  The context orders its work across streams by recording an event
+ * on the stream it last queued on when the next call comes on another one;
+ * so a stream passed to any entry point must stay alive until the next call
+ * on the context, or be released first with vmqg_release_stream (records that
+ * event now; no-op if the context's last work is not on it). */
+int vmqg_release_stream(vmqg_ctx* ctx, void* stream);
+
 /* ---- range mode ------------------------------------------------------ */
 /* Range-mode matching returns, instead of copies of the records, one 8-byte
  * entry per non-empty subscriber-list key (`lookup_subs/1`,
@@ -246,6 +262,18 @@ int vmqg_match_ranges_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npu
  * until the next vmqg_apply_ops on the context; primary contexts only. */
 int vmqg_records(vmqg_ctx* ctx, const vmqg_emit** recs, uint64_t* n);
 
+/* Epoch-safe expansion (ABI 3).  vmqg_epoch: the table epoch a match queued
+ * now sees (the number of vmqg_apply_ops batches applied; a device match is
+ * stream-ordered after every apply made before it is queued, and before every
+ * apply made after).  vmqg_records_at: the record table for range results
+ * of `epoch` — VMQG_E_STATE when a later vmqg_apply_ops has rewritten a
+ * record slot or re-laid out the arena, so the ranges could index changed
+ * records (lookup_subs/1 never returns a stale list, vmq_reg_trie.erl:87-94):
+ * the caller matches again.  Appends to fresh slots are conservative
+ * refusals too. */
+int vmqg_epoch(vmqg_ctx* ctx, uint64_t* epoch);
+int vmqg_records_at(vmqg_ctx* ctx, uint64_t epoch, const vmqg_emit** recs, uint64_t* n);
+
 /* ---- introspection --------------------------------------------------- */
 int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out);
 
@@ -262,10 +290,15 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *                          defaults 4 and 16) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
-/* Average duration (ns) of the dominant match kernel over the last
- * vmqg_match_device calls made with timing enabled (vmqg_set_timing). */
+/* Average duration (ns) of the match kernels over the last
+ * vmqg_match_device calls made with timing enabled (vmqg_set_timing):
+ * vmqg_kernel_times gives the fast-tier COUNT and EMIT launches;
+ * vmqg_kernel_times_ex all five launches of a call, stage_ns[5] =
+ * {COUNT fast tier, COUNT wave tier, scan, EMIT fast tier, EMIT wave tier}. */
+#define VMQG_TIMED_STAGES 5
 int vmqg_set_timing(vmqg_ctx* ctx, int enable);
 int vmqg_kernel_times(vmqg_ctx* ctx, double* count_ns, double* emit_ns, uint64_t* launches);
+int vmqg_kernel_times_ex(vmqg_ctx* ctx, double* stage_ns, uint64_t* launches);
 
 /* ---- replication (one primary, N device replicas) --------------------- */
 /* Device arena of the context: pointer, byte size and the layout descriptor

@@ -98,6 +98,14 @@ int vmqr_match_device(vmqr_ctx* ctx, const vmqg_pub* d_filters, uint32_t n, cons
                       uint32_t* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream);
 int vmqr_match_status(vmqr_ctx* ctx, void* stream);
 
+/* Streams: device calls take the caller's stream (NULL = the legacy default
+ * stream).  The context orders its work across streams by recording an event
+ * on the stream it last queued on when the next call comes on another one;
+ * so a stream passed to any entry point must stay alive until the next call
+ * on the context, or be released first with vmqr_release_stream (records that
+ * event now; no-op if the context's last work is not on it). */
+int vmqr_release_stream(vmqr_ctx* ctx, void* stream);
+
 int vmqr_stats(vmqr_ctx* ctx, vmqr_stats_t* out);
 
 /* Canonical dump of ?RETAIN_CACHE: one line "mp#M [w,...] -> msg#N" per

@@ -97,6 +97,14 @@ int vmqs_select_device(vmqs_ctx* ctx, const vmqg_emit* d_emits, const uint64_t* 
                        void* stream);
 int vmqs_select_status(vmqs_ctx* ctx, void* stream);
 
+/* Streams: device calls take the caller's stream (NULL = the legacy default
+ * stream).  The context orders its work across streams by recording an event
+ * on the stream it last queued on when the next call comes on another one;
+ * so a stream passed to any entry point must stay alive until the next call
+ * on the context, or be released first with vmqs_release_stream (records that
+ * event now; no-op if the context's last work is not on it). */
+int vmqs_release_stream(vmqs_ctx* ctx, void* stream);
+
 /* The element key of the record at position p of publish number q (the
  * batch's pub_seq + its index): the 40 high bits of a splitmix64-style mix
  * of (seed, q, p), then p in the low 24 bits, so keys order by (random, p). */

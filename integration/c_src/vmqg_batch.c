@@ -2,8 +2,10 @@
  * vmqg_batch.c — see vmqg_batch.h.  Plain C99, no OTP, no HIP: only the
  * libvmqgpu C ABI.
  */
+#define _GNU_SOURCE   /* pthread_rwlockattr_setkind_np: writers are not starved by readers */
 #include "vmqg_batch.h"
 
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -199,6 +201,7 @@ int vmqgb_match(vmqgb_batch* b, vmqg_ctx* ctx) {
 
 int vmqgb_match_ranges(vmqgb_batch* b, vmqg_ctx* ctx) {
   if (ensure_offsets(b)) return VMQG_E_NOMEM;
+  if (vmqg_epoch(ctx, &b->epoch)) return VMQG_E_INVAL;
   if (!b->rng_cap && grow((void**)&b->rng, &b->rng_cap, b->n * 2 + 64, sizeof(vmqg_range))) return VMQG_E_NOMEM;
   for (;;) {
     size_t need = 0;
@@ -327,5 +330,62 @@ int vmqgb_ops_add_filter(vmqgb_ops* o, vmqg_ctx* ctx, uint32_t kind, uint32_t mo
 int vmqgb_ops_apply(vmqgb_ops* o, vmqg_ctx* ctx, uint64_t* epoch) {
   const int rc = vmqg_apply_ops(ctx, o->ops, o->n, o->words, o->nwords, epoch);
   if (rc == 0) vmqgb_ops_reset(o);
+  return rc;
+}
+
+/* ------------------------------------------------------------------ view */
+struct vmqgb_view {
+  vmqg_ctx* ctx;
+  pthread_rwlock_t tables;   /* readers: batchers; writers: applies */
+  pthread_mutex_t device;    /* one device call at a time */
+};
+
+vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx) {
+  vmqgb_view* v = (vmqgb_view*)calloc(1, sizeof(*v));
+  if (!v) return NULL;
+  v->ctx = ctx;
+  pthread_rwlockattr_t a;
+  pthread_rwlockattr_init(&a);
+  pthread_rwlockattr_setkind_np(&a, PTHREAD_RWLOCK_PREFER_WRITER_NONRECURSIVE_NP);
+  const int r1 = pthread_rwlock_init(&v->tables, &a);
+  pthread_rwlockattr_destroy(&a);
+  const int r2 = pthread_mutex_init(&v->device, NULL);
+  if (r1 || r2) { free(v); return NULL; }
+  return v;
+}
+
+void vmqgb_view_free(vmqgb_view* v) {
+  if (!v) return;
+  pthread_rwlock_destroy(&v->tables);
+  pthread_mutex_destroy(&v->device);
+  free(v);
+}
+
+vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v) { return v->ctx; }
+void vmqgb_view_read_begin(vmqgb_view* v) { pthread_rwlock_rdlock(&v->tables); }
+void vmqgb_view_read_end(vmqgb_view* v) { pthread_rwlock_unlock(&v->tables); }
+void vmqgb_view_write_begin(vmqgb_view* v) { pthread_rwlock_wrlock(&v->tables); }
+void vmqgb_view_write_end(vmqgb_view* v) { pthread_rwlock_unlock(&v->tables); }
+
+int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
+  if (b->n == 0) {   /* nothing to match: empty results */
+    if (ensure_offsets(b)) return VMQG_E_NOMEM;
+    b->offsets[0] = 0;
+    b->out_n = b->rng_n = 0;
+    if (recs) *recs = NULL;
+    if (nrecs) *nrecs = 0;
+    return 0;
+  }
+  pthread_mutex_lock(&v->device);
+  int rc = ranges ? vmqgb_match_ranges(b, v->ctx) : vmqgb_match(b, v->ctx);
+  pthread_mutex_unlock(&v->device);
+  if (!rc && ranges && recs && nrecs) rc = vmqg_records_at(v->ctx, b->epoch, recs, nrecs);
+  return rc;
+}
+
+int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
+  vmqgb_view_write_begin(v);
+  const int rc = vmqgb_ops_apply(o, v->ctx, epoch);
+  vmqgb_view_write_end(v);
   return rc;
 }

@@ -19,10 +19,19 @@
  *   - subscription ops: {Topic words, Node, SubscriberId, SubInfo} changes
  *     (deletes before adds, vmq_reg_trie.erl:245-248) -> vmqg_op batches.
  *
+ *   - the view: the locking protocol the NIF runs fold/4 callers under
+ *     (vmqgb_view_*), so that every batcher prepares its batch and folds its
+ *     results in parallel — as vmq_reg_trie:fold/4 runs in every caller's
+ *     process against read_concurrency tables (vmq_reg_trie.erl:59-66,
+ *     136-137) — and only the device call is serialised.
+ *
  * Threading: an interner or a batch is owned by one thread at a time.
  * vmqgb_batch_add only reads the context's dictionary (vmqg_prepare_publish),
  * so per-thread batches may be filled concurrently while no other call
  * modifies the context; vmqgb_batch_append merges them for one match call.
+ * vmqgb_view: readers (a batch's prepare, device call and fold) share the
+ * tables; a writer (vmqg_apply_ops, through vmqgb_view_apply) excludes them
+ * and is not starved by them; device calls take turns.
  */
 #ifndef VMQG_BATCH_H
 #define VMQG_BATCH_H
@@ -59,6 +68,7 @@ typedef struct vmqgb_batch {
   size_t out_cap, out_n;
   vmqg_range* rng;      /* range mode */
   size_t rng_cap, rng_n;
+  uint64_t epoch;       /* table epoch of the last match (vmqg_epoch): ranges index that epoch's records */
 } vmqgb_batch;
 
 int vmqgb_batch_init(vmqgb_batch* b, size_t cap_hint);
@@ -110,6 +120,26 @@ int vmqgb_ops_add(vmqgb_ops* o, vmqg_ctx* ctx, uint32_t kind, uint32_t mountpoin
 int vmqgb_ops_add_filter(vmqgb_ops* o, vmqg_ctx* ctx, uint32_t kind, uint32_t mountpoint, const uint8_t* filter,
                          size_t len, uint32_t node, uint32_t sub, uint32_t subinfo);
 int vmqgb_ops_apply(vmqgb_ops* o, vmqg_ctx* ctx, uint64_t* epoch);
+
+/* ---- the view: concurrent batchers over one context ------------------- */
+typedef struct vmqgb_view vmqgb_view;
+
+vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx);
+void vmqgb_view_free(vmqgb_view* v);   /* does not destroy the context */
+vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v);
+/* A batcher's critical section: read_begin, vmqgb_batch_add for each of its
+ * publishes, vmqgb_view_match, the fold, read_end.  Any number of batchers
+ * at once; vmqgb_view_match serialises only the device call. */
+void vmqgb_view_read_begin(vmqgb_view* v);
+void vmqgb_view_read_end(vmqgb_view* v);
+/* Under the read lock: vmqgb_match or vmqgb_match_ranges (ranges != 0) with
+ * the device to itself; in range mode also the record table of the match's
+ * epoch (vmqg_records_at) for vmqgb_fold_ranges. */
+int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs);
+/* Table changes (vmqg_apply_ops, the term tables of the caller): writers. */
+void vmqgb_view_write_begin(vmqgb_view* v);
+void vmqgb_view_write_end(vmqgb_view* v);
+int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);   /* write_begin, apply, write_end */
 
 #ifdef __cplusplus
 }

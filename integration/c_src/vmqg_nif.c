@@ -21,8 +21,19 @@
  * Terms are keyed by their external term format (enif_term_to_binary) and
  * kept as copies in the resource's own environment, so building an entry is
  * an enif_make_copy, never a decode.
+ *
+ * Concurrency (vmqgb_view, vmqg_batch.c): vmq_reg_gpu_view runs one batcher
+ * process per scheduler; each calls match/4 with its own batch resource, and
+ * those calls run in parallel on dirty CPU schedulers — preparing the
+ * publishes and building the result terms under the view's read lock, only
+ * the device call itself taking turns — as vmq_reg_trie:fold/4 runs in
+ * every caller's process (vmq_reg_trie.erl:59-66, read_concurrency tables
+ * :136-137).  apply/3, add_init/6 and flush_init/1 (the subscription changes
+ * and the term tables they intern) are writers.  Every NIF that can wait for
+ * a lock or the device is a dirty one.
  */
 #include <erl_nif.h>
+#include <stdint.h>
 #include <string.h>
 
 #include "vmqg.h"
@@ -36,15 +47,20 @@ typedef struct {
 
 typedef struct {
   vmqg_ctx* ctx;
-  ErlNifMutex* lock;              /* fold callers vs. the initial load process */
+  vmqgb_view* view;               /* batchers (readers) vs. table changes (writers) */
   vmqgb_interner *mps, *nodes, *subs, *infos;
   term_store node_t, sub_t, info_t, group_t;   /* group_t indexed by word id */
-  vmqgb_batch batch;
-  vmqgb_ops ops;                  /* add_init accumulation */
+  vmqgb_ops ops;                  /* apply/3 and add_init/6 accumulation (under the write lock) */
   uint32_t max_mountpoints;
 } vmqg_res;
 
+typedef struct {                  /* one batcher's batch (batch_new/1) */
+  vmqg_res* owner;                /* kept alive while the batch lives */
+  vmqgb_batch b;
+} vmqg_bres;
+
 static ErlNifResourceType* RES;
+static ErlNifResourceType* BRES;
 static ERL_NIF_TERM a_ok, a_error, a_invalid_topic, a_device, a_nomem, a_badarg, a_records, a_ranges;
 
 /* ------------------------------------------------------------ helpers */
@@ -88,9 +104,15 @@ static void res_dtor(ErlNifEnv* env, void* obj) {
   vmqgb_interner_free(r->subs); vmqgb_interner_free(r->infos);
   term_store* ts[4] = {&r->node_t, &r->sub_t, &r->info_t, &r->group_t};
   for (int i = 0; i < 4; i++) { if (ts[i]->env) enif_free_env(ts[i]->env); enif_free(ts[i]->terms); }
-  vmqgb_batch_free(&r->batch);
   vmqgb_ops_free(&r->ops);
-  if (r->lock) enif_mutex_destroy(r->lock);
+  vmqgb_view_free(r->view);
+}
+
+static void bres_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  vmqg_bres* br = (vmqg_bres*)obj;
+  vmqgb_batch_free(&br->b);
+  if (br->owner) enif_release_resource(br->owner);
 }
 
 static vmqg_res* get_res(ErlNifEnv* env, ERL_NIF_TERM t) {
@@ -110,12 +132,10 @@ static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   if (!enif_get_map_value(env, argv[0], enif_make_atom(env, "local_node"), &local)) return enif_make_badarg(env);
   vmqg_res* r = (vmqg_res*)enif_alloc_resource(RES, sizeof(vmqg_res));
   memset(r, 0, sizeof(*r));
-  r->lock = enif_mutex_create("vmqg_res");
   r->mps = vmqgb_interner_new(); r->nodes = vmqgb_interner_new();
   r->subs = vmqgb_interner_new(); r->infos = vmqgb_interner_new();
   r->node_t.env = enif_alloc_env(); r->sub_t.env = enif_alloc_env();
   r->info_t.env = enif_alloc_env(); r->group_t.env = enif_alloc_env();
-  vmqgb_batch_init(&r->batch, 4096);
   vmqgb_ops_init(&r->ops);
   r->max_mountpoints = 1024;
   uint32_t id;
@@ -129,7 +149,8 @@ static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   cfg.max_mountpoints = r->max_mountpoints;
   int err = 0;
   r->ctx = vmqg_create(&cfg, &err);
-  ERL_NIF_TERM ret = r->ctx ? enif_make_tuple2(env, a_ok, enif_make_resource(env, r)) : error_term(env, err);
+  if (r->ctx && !(r->view = vmqgb_view_new(r->ctx))) err = VMQG_E_NOMEM;
+  ERL_NIF_TERM ret = r->ctx && r->view ? enif_make_tuple2(env, a_ok, enif_make_resource(env, r)) : error_term(env, err);
   enif_release_resource(r);
   return ret;
 }
@@ -148,19 +169,25 @@ static int add_change(ErlNifEnv* env, vmqg_res* r, uint32_t kind, ERL_NIF_TERM s
     return VMQG_E_NOMEM;
   unsigned len;
   if (!enif_get_list_length(env, topic, &len) || len == 0 || len > 65536) return VMQG_E_INVAL;
-  const uint8_t* wp[len];
-  size_t wl[len];
+  /* word pointers on the heap: a topic of 65,535 bytes has ~32k levels,
+   * far more than a scheduler's stack holds */
+  const uint8_t** wp = (const uint8_t**)enif_alloc(len * sizeof(*wp));
+  size_t* wl = (size_t*)enif_alloc(len * sizeof(*wl));
+  if (!wp || !wl) { enif_free(wp); enif_free(wl); return VMQG_E_NOMEM; }
   ERL_NIF_TERM group = 0, head, tail = topic;
+  int rc = 0;
   for (unsigned i = 0; i < len; i++) {
     ErlNifBinary b;
     enif_get_list_cell(env, tail, &head, &tail);
-    if (!enif_inspect_binary(env, head, &b)) return VMQG_E_INVAL;
+    if (!enif_inspect_binary(env, head, &b)) { rc = VMQG_E_INVAL; break; }
     wp[i] = b.data;
     wl[i] = b.size;
     if (i == 1) group = head;
   }
   const size_t w0 = r->ops.nwords;
-  const int rc = vmqgb_ops_add(&r->ops, r->ctx, kind, mp, wp, wl, len, nd, sub, info);
+  if (!rc) rc = vmqgb_ops_add(&r->ops, r->ctx, kind, mp, wp, wl, len, nd, sub, info);
+  enif_free(wp);
+  enif_free(wl);
   if (rc) return rc;
   /* $share/Group/...: remember the group binary under its word id (decoding kind-B entries) */
   if (len >= 3 && r->ops.words[w0] == VMQG_WORD_SHARE) store_put(&r->group_t, r->ops.words[w0 + 1], group);
@@ -173,7 +200,8 @@ static ERL_NIF_TERM nif_apply(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   (void)argc;
   vmqg_res* r = get_res(env, argv[0]);
   if (!r) return enif_make_badarg(env);
-  enif_mutex_lock(r->lock);
+  vmqgb_view_write_begin(r->view);
+  if (r->ops.n) vmqgb_ops_apply(&r->ops, r->ctx, NULL);   /* pending add_init ops keep their order */
   vmqgb_ops_reset(&r->ops);
   ERL_NIF_TERM head, tail = argv[2];
   int rc = 0;
@@ -185,7 +213,8 @@ static ERL_NIF_TERM nif_apply(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     rc = add_change(env, r, kind, argv[1], el[1], el[2], el[3]);
   }
   if (!rc) rc = vmqgb_ops_apply(&r->ops, r->ctx, NULL);
-  enif_mutex_unlock(r->lock);
+  vmqgb_ops_reset(&r->ops);
+  vmqgb_view_write_end(r->view);
   return rc ? error_term(env, rc) : a_ok;
 }
 
@@ -195,10 +224,10 @@ static ERL_NIF_TERM nif_add_init(ErlNifEnv* env, int argc, const ERL_NIF_TERM ar
   (void)argc;
   vmqg_res* r = get_res(env, argv[0]);
   if (!r) return enif_make_badarg(env);
-  enif_mutex_lock(r->lock);
+  vmqgb_view_write_begin(r->view);
   int rc = add_change(env, r, VMQG_OP_ADD, argv[3], argv[2], argv[4], argv[5]);
   if (!rc && r->ops.n >= 65536) rc = vmqgb_ops_apply(&r->ops, r->ctx, NULL);
-  enif_mutex_unlock(r->lock);
+  vmqgb_view_write_end(r->view);
   return rc ? error_term(env, rc) : a_ok;
 }
 
@@ -206,9 +235,9 @@ static ERL_NIF_TERM nif_flush_init(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
   (void)argc;
   vmqg_res* r = get_res(env, argv[0]);
   if (!r) return enif_make_badarg(env);
-  enif_mutex_lock(r->lock);
+  vmqgb_view_write_begin(r->view);
   const int rc = r->ops.n ? vmqgb_ops_apply(&r->ops, r->ctx, NULL) : 0;
-  enif_mutex_unlock(r->lock);
+  vmqgb_view_write_end(r->view);
   return rc ? error_term(env, rc) : a_ok;
 }
 
@@ -241,19 +270,41 @@ static int make_entry(void* accp, const vmqgb_entry* e) {
   return 0;
 }
 
-/* match(Ctx, [{MP, TopicBin}], records | ranges) -> [{ok, Entries} | {error, Reason}]
- * (fold/4 for a batch of callers, vmq_reg_trie.erl:59-98); dirty CPU */
+/* batch_new(Ctx) -> {ok, Batch}: a batcher's own publish batch */
+static ERL_NIF_TERM nif_batch_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  if (!r) return enif_make_badarg(env);
+  vmqg_bres* br = (vmqg_bres*)enif_alloc_resource(BRES, sizeof(vmqg_bres));
+  memset(br, 0, sizeof(*br));
+  if (vmqgb_batch_init(&br->b, 4096)) { enif_release_resource(br); return error_term(env, VMQG_E_NOMEM); }
+  enif_keep_resource(r);
+  br->owner = r;
+  ERL_NIF_TERM t = enif_make_resource(env, br);
+  enif_release_resource(br);
+  return enif_make_tuple2(env, a_ok, t);
+}
+
+/* match(Ctx, Batch, [{MP, TopicBin}], records | ranges) -> [{ok, Entries} | {error, Reason}]
+ * (fold/4 for a batch of callers, vmq_reg_trie.erl:59-98); dirty CPU.
+ * Batchers run this concurrently: the tables are read-locked from the first
+ * publish prepared to the last term built; the device call takes turns. */
 static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   (void)argc;
   vmqg_res* r = get_res(env, argv[0]);
+  vmqg_bres* br = NULL;
   unsigned n;
-  if (!r || !enif_get_list_length(env, argv[1], &n)) return enif_make_badarg(env);
-  const int ranges = enif_is_identical(argv[2], a_ranges);
-  enif_mutex_lock(r->lock);
-  vmqgb_batch* b = &r->batch;
-  vmqgb_batch_reset(b);
+  if (!r || !enif_get_resource(env, argv[1], BRES, (void**)&br) || br->owner != r ||
+      !enif_get_list_length(env, argv[2], &n))
+    return enif_make_badarg(env);
+  const int ranges = enif_is_identical(argv[3], a_ranges);
+  vmqgb_batch* b = &br->b;
   long* idx = (long*)enif_alloc((n ? n : 1) * sizeof(long));
-  ERL_NIF_TERM head, tail = argv[1];
+  ERL_NIF_TERM* res = (ERL_NIF_TERM*)enif_alloc((n ? n : 1) * sizeof(ERL_NIF_TERM));
+  if (!idx || !res) { enif_free(idx); enif_free(res); return enif_make_badarg(env); }
+  vmqgb_view_read_begin(r->view);
+  vmqgb_batch_reset(b);
+  ERL_NIF_TERM head, tail = argv[2];
   for (unsigned i = 0; i < n; i++) {
     int arity;
     const ERL_NIF_TERM* el;
@@ -271,11 +322,9 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     /* an unknown mountpoint has no subscriptions: an id past every root matches nothing */
     idx[i] = vmqgb_batch_add(b, r->ctx, known ? mp : r->max_mountpoints, topic.data, topic.size);
   }
-  int rc = b->n ? (ranges ? vmqgb_match_ranges(b, r->ctx) : vmqgb_match(b, r->ctx)) : 0;
   const vmqg_emit* recs = NULL;
   uint64_t nrecs = 0;
-  if (!rc && ranges) rc = vmqg_records(r->ctx, &recs, &nrecs);
-  ERL_NIF_TERM* res = (ERL_NIF_TERM*)enif_alloc((n ? n : 1) * sizeof(ERL_NIF_TERM));
+  const int rc = vmqgb_view_match(r->view, b, ranges, &recs, &nrecs);
   for (unsigned i = 0; i < n; i++) {
     if (idx[i] < 0 || rc) { res[i] = error_term(env, idx[i] < 0 ? (int)idx[i] : rc); continue; }
     size_t cnt = 0;
@@ -285,12 +334,13 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
       cnt = vmqgb_count_of(b, (size_t)idx[i]);
     }
     fold_acc acc = {env, r, (ERL_NIF_TERM*)enif_alloc((cnt ? cnt : 1) * sizeof(ERL_NIF_TERM)), 0};
-    if (ranges) vmqgb_fold_ranges(b, recs, nrecs, (size_t)idx[i], make_entry, &acc);
-    else vmqgb_fold(b, (size_t)idx[i], make_entry, &acc);
-    res[i] = enif_make_tuple2(env, a_ok, enif_make_list_from_array(env, acc.out, (unsigned)acc.n));
+    const int frc = ranges ? vmqgb_fold_ranges(b, recs, nrecs, (size_t)idx[i], make_entry, &acc)
+                           : vmqgb_fold(b, (size_t)idx[i], make_entry, &acc);
+    /* a fold that stops early (a range beyond the table) is this publish's error, never a partial list */
+    res[i] = frc ? error_term(env, frc) : enif_make_tuple2(env, a_ok, enif_make_list_from_array(env, acc.out, (unsigned)acc.n));
     enif_free(acc.out);
   }
-  enif_mutex_unlock(r->lock);
+  vmqgb_view_read_end(r->view);
   ERL_NIF_TERM list = enif_make_list_from_array(env, res, n);
   enif_free(res);
   enif_free(idx);
@@ -303,9 +353,9 @@ static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   vmqg_res* r = get_res(env, argv[0]);
   if (!r) return enif_make_badarg(env);
   vmqg_stats_t st;
-  enif_mutex_lock(r->lock);
+  vmqgb_view_read_begin(r->view);   /* never the device lock: metrics polling does not wait for a match */
   const int rc = vmqg_stats(r->ctx, &st);
-  enif_mutex_unlock(r->lock);
+  vmqgb_view_read_end(r->view);
   if (rc) return error_term(env, rc);
   return enif_make_tuple2(env, enif_make_uint64(env, st.subs), enif_make_uint64(env, st.device_bytes));
 }
@@ -313,6 +363,7 @@ static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   (void)priv; (void)info;
   RES = enif_open_resource_type(env, NULL, "vmqg_ctx", res_dtor, ERL_NIF_RT_CREATE, NULL);
+  BRES = enif_open_resource_type(env, NULL, "vmqg_batch", bres_dtor, ERL_NIF_RT_CREATE, NULL);
   a_ok = enif_make_atom(env, "ok");
   a_error = enif_make_atom(env, "error");
   a_invalid_topic = enif_make_atom(env, "invalid_topic");
@@ -321,16 +372,19 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   a_badarg = enif_make_atom(env, "badarg");
   a_records = enif_make_atom(env, "records");
   a_ranges = enif_make_atom(env, "ranges");
-  return RES ? 0 : 1;
+  return RES && BRES ? 0 : 1;
 }
 
+/* every call that can wait for the table lock or the device runs on a dirty
+ * scheduler (add_init applies a 65,536-op batch: host engine + upload) */
 static ErlNifFunc funcs[] = {
     {"create", 1, nif_create, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"apply", 3, nif_apply, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"add_init", 6, nif_add_init, 0},
+    {"add_init", 6, nif_add_init, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"flush_init", 1, nif_flush_init, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"match", 3, nif_match, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"stats", 1, nif_stats, 0},
+    {"batch_new", 1, nif_batch_new, 0},
+    {"match", 4, nif_match, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"stats", 1, nif_stats, ERL_NIF_DIRTY_JOB_CPU_BOUND},
 };
 
 ERL_NIF_INIT(vmqg_nif, funcs, load, NULL, NULL, NULL)

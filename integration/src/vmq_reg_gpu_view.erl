@@ -8,22 +8,30 @@
 %% the same event replay after `subscribers_loaded` (:198-205).
 %%
 %% What changes is where fold/4 is answered.  vmq_reg_trie walks ETS in the
-%% caller's process; here concurrent callers are collected into one batch
-%% and matched by one NIF call on a dirty scheduler (vmqg_nif:match/3), and
-%% each caller then runs its FoldFun over its own entries in its own
-%% process — FoldFun has side effects (vmq_queue:enqueue, cluster forward,
-%% vmq_reg.erl:327-353) and is called exactly as vmq_reg_trie calls it,
-%% FoldFun(Entry, SubscriberId, Acc) (vmq_reg_trie.erl:83, 97).  A caller
-%% blocks on its own call, so the order of one publisher's publishes is kept
-%% (vmq_in_order_delivery_SUITE).
+%% caller's process, on every scheduler at once (read_concurrency tables,
+%% vmq_reg_trie.erl:136-137); here the callers on each scheduler are
+%% collected by that scheduler's batcher (vmq_reg_gpu_batcher, one per
+%% scheduler), each batcher matches its batch with one NIF call on a dirty
+%% scheduler (vmqg_nif:match/4) — the batchers' calls run in parallel, only
+%% the device call itself takes turns — and each caller then runs its
+%% FoldFun over its own entries in its own process — FoldFun has side
+%% effects (vmq_queue:enqueue, cluster forward, vmq_reg.erl:327-353) and is
+%% called exactly as vmq_reg_trie calls it, FoldFun(Entry, SubscriberId,
+%% Acc) (vmq_reg_trie.erl:83, 97).  A caller blocks on its own call, so the
+%% order of one publisher's publishes is kept (vmq_in_order_delivery_SUITE).
+%%
+%% This gen_server owns the view: the NIF resource, the batchers, the
+%% subscriber-change events (applied as writers: no match reads the tables
+%% while an apply changes them) and the initial load.  It never queues a
+%% fold request, so no event can delay one.
 %%
 %% Install: reg_views = [vmq_reg_trie, vmq_reg_gpu_view] (shadow) or
 %% default_reg_view = vmq_reg_gpu_view (vmq_server.schema:115-137).  The NIF
 %% (c_src/vmqg_nif.c) and priv/libvmqgpu.so come from this repository.
 %%
 %% Not compiled in this repository's image (no OTP); its C core
-%% (c_src/vmqg_batch.c) is compiled and tested (tests/test_nif_layer.py,
-%% tools/nif_harness.c).
+%% (c_src/vmqg_batch.c, the batchers' locking protocol included) is compiled
+%% and tested (tests/test_nif_layer.py, tools/nif_harness.c).
 -module(vmq_reg_gpu_view).
 -behaviour(gen_server).
 -behaviour(vmq_reg_view).
@@ -41,16 +49,12 @@
          code_change/3]).
 
 -define(SERVER, ?MODULE).
-%% a batch goes to the GPU when it holds this many publishes, or when the
-%% server's mailbox has no more fold requests queued behind it
--define(MAX_BATCH, 4096).
 
 -record(state, {ctx,                    % vmqg_nif resource (vmqg_ctx + term tables)
+                batchers,               % tuple of vmq_reg_gpu_batcher pids
                 event_handler,
                 status=init,
-                event_queue=queue:new(),
-                pending=[],             % [{From, MP, TopicBin}], newest first
-                npending=0}).
+                event_queue=queue:new()}).
 
 %%%===================================================================
 %%% API
@@ -62,7 +66,9 @@ start_link() ->
 %% vmq_reg.erl:260, and vmq_cluster_com:process/2, vmq_cluster_com.erl:156).
 fold({MP, _} = SubscriberId, Topic, FoldFun, Acc) when is_list(Topic) ->
     TopicBin = iolist_to_binary(lists:join(<<"/">>, Topic)),
-    case gen_server:call(?SERVER, {match, MP, TopicBin}, infinity) of
+    Batchers = persistent_term:get({?MODULE, batchers}),
+    Batcher = element(erlang:system_info(scheduler_id) rem tuple_size(Batchers) + 1, Batchers),
+    case gen_server:call(Batcher, {match, MP, TopicBin}, infinity) of
         {ok, Entries} ->
             lists:foldl(fun(Entry, AccAcc) -> FoldFun(Entry, SubscriberId, AccAcc) end,
                         Acc, Entries);
@@ -85,6 +91,12 @@ init([]) ->
     Device = application:get_env(vmq_server, gpu_reg_view_device, 0),
     {ok, Ctx} = vmqg_nif:create(#{device => Device, local_node => node()}),
     persistent_term:put({?MODULE, ctx}, Ctx),
+    %% fold/4 batchers, one per scheduler (linked: they die with the view)
+    Mode = application:get_env(vmq_server, gpu_reg_view_output, records),
+    Batchers = list_to_tuple(
+                 [begin {ok, Pid} = vmq_reg_gpu_batcher:start_link(Ctx, Mode), Pid end
+                  || _ <- lists:seq(1, erlang:system_info(schedulers))]),
+    persistent_term:put({?MODULE, batchers}, Batchers),
     Self = self(),
     spawn_link(
       fun() ->
@@ -97,14 +109,8 @@ init([]) ->
               Self ! subscribers_loaded
       end),
     EventHandler = vmq_reg:subscribe_subscriber_changes(),
-    {ok, #state{ctx=Ctx, event_handler=EventHandler}}.
+    {ok, #state{ctx=Ctx, batchers=Batchers, event_handler=EventHandler}}.
 
-handle_call({match, MP, TopicBin}, From, #state{pending=P, npending=N} = State) ->
-    State1 = State#state{pending=[{From, MP, TopicBin} | P], npending=N + 1},
-    case N + 1 >= ?MAX_BATCH of
-        true -> {noreply, flush(State1)};
-        false -> {noreply, State1, 0}   % timeout 0: flush once the mailbox is drained
-    end;
 handle_call({event, Event}, _From, State) ->
     %% used only for testing/microbenchmarking, as vmq_reg_trie.erl:167-170
     {reply, ok, handle_event(Event, State)};
@@ -114,8 +120,6 @@ handle_call(_Request, _From, State) ->
 handle_cast(_Msg, State) ->
     {noreply, State}.
 
-handle_info(timeout, State) ->
-    {noreply, flush(State)};
 handle_info(subscribers_loaded, #state{event_queue=Q} = State) ->
     State1 = lists:foldl(fun handle_event/2, State#state{status=ready}, queue:to_list(Q)),
     {Subs, _} = stats(),
@@ -127,6 +131,7 @@ handle_info(Event, State) ->
     {noreply, handle_event(Event, State)}.
 
 terminate(_Reason, _State) ->
+    persistent_term:erase({?MODULE, batchers}),
     persistent_term:erase({?MODULE, ctx}),
     ok.
 
@@ -136,18 +141,6 @@ code_change(_OldVsn, State, _Extra) ->
 %%%===================================================================
 %%% Internal functions
 %%%===================================================================
-
-%% One NIF call for every queued fold request (dirty CPU scheduler: topic
-%% splitting + interning, the GPU match, term construction), then one reply
-%% per caller.  Publishes the reference rejects are rejected per caller.
-flush(#state{pending=[]} = State) ->
-    State;
-flush(#state{ctx=Ctx, pending=P} = State) ->
-    Batch = lists:reverse(P),
-    Results = vmqg_nif:match(Ctx, [{MP, T} || {_, MP, T} <- Batch], records),
-    lists:foreach(fun({{From, _, _}, Res}) -> gen_server:reply(From, Res) end,
-                  lists:zip(Batch, Results)),
-    State#state{pending=[], npending=0}.
 
 %% handle_event/2 (vmq_reg_trie.erl:240-251): the same diff, the same order
 %% (deletes, then adds); the NIF turns the changes into one vmqg_apply_ops.

@@ -1,6 +1,6 @@
 %% vmqg_nif — NIF stubs of c_src/vmqg_nif.c (libvmqgpu behind vmq_reg_gpu_view).
 -module(vmqg_nif).
--export([create/1, apply/3, add_init/6, flush_init/1, match/3, stats/1]).
+-export([create/1, apply/3, add_init/6, flush_init/1, batch_new/1, match/4, stats/1]).
 -on_load(init/0).
 
 init() ->
@@ -17,7 +17,9 @@ apply(_Ctx, _SubscriberId, _Changes) -> erlang:nif_error(nif_not_loaded).
 %% Ctx, MP, Topic, SubscriberId, SubInfo, Node -> ok | {error, term()}
 add_init(_Ctx, _MP, _Topic, _SubscriberId, _SubInfo, _Node) -> erlang:nif_error(nif_not_loaded).
 flush_init(_Ctx) -> erlang:nif_error(nif_not_loaded).
-%% Ctx, [{MP, TopicBin}], records | ranges -> [{ok, [Entry]} | {error, term()}]
-match(_Ctx, _Publishes, _Mode) -> erlang:nif_error(nif_not_loaded).
+%% Ctx -> {ok, Batch}: a batcher's own publish batch
+batch_new(_Ctx) -> erlang:nif_error(nif_not_loaded).
+%% Ctx, Batch, [{MP, TopicBin}], records | ranges -> [{ok, [Entry]} | {error, term()}]
+match(_Ctx, _Batch, _Publishes, _Mode) -> erlang:nif_error(nif_not_loaded).
 %% Ctx -> {NrOfSubs, DeviceBytes}
 stats(_Ctx) -> erlang:nif_error(nif_not_loaded).

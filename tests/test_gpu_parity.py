@@ -551,14 +551,241 @@ def test_output_offsets_of_a_large_deferral_heavy_batch(mode, fast_g):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_config_e_multitenant_parity(mode):
+@pytest.mark.parametrize("fast_g", [1, 2])
+def test_config_e_multitenant_parity(mode, fast_g):
     """Config E shape at 1/500 scale (100k subs over 1,000 Zipf-sized
-    mountpoints, 12-level topics, hot-topic skew): every publish vs the oracle."""
+    mountpoints, 12-level topics, hot-topic skew): every publish vs the
+    oracle, under both fast-tier mappings."""
     from vernemq_amd import workloads as W
     w = W.config_e(scale=0.002, n_pubs=8192)
     v, orc = _load_both(w)
+    v.set_option("fast_g", fast_g)
     got = _gpu_canon(v, w, 0, w.n_pubs, mode)
     want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in range(w.n_pubs)])
     bad = [i for i in range(w.n_pubs) if got[i] != sorted(want[i])]
     assert not bad, (len(bad), w.pub_topic(bad[0]))
     assert sum(len(x) for x in got) > w.n_pubs // 4
+
+
+def _many_key_events(node):
+    """$share groups hosted on 8 nodes: one filter node carries one key per
+    {Node, Group} entry (vmq_reg_trie.erl:68-72, 290-303), so a publish meets
+    far more keys than the fast tier's lists hold while its frontier stays
+    small — the many-key mode (no deferral)."""
+    nodes = [node] + ["n%d@h" % k for k in range(1, 8)]
+    evs = []
+    sub = lambda cid, nd, t, q: ("updated", ("", cid), None, [(nd, True, [(t, q)])])
+    for g in range(12):   # jobs/+ : 12 groups x 16 members over the 8 nodes = 96 keys, 1,536 records
+        for m in range(16):
+            evs.append(sub(b"g%dm%d" % (g, m), nodes[m % 8], (b"$share", b"g%d" % g, b"jobs", b"+"), m % 3))
+    for m in range(8):    # '#' alias candidate with many keys, and a group of one member per node
+        evs.append(sub(b"h%d" % m, nodes[m], (b"$share", b"gh", b"jobs", b"#"), 1))
+    evs.append(sub(b"plain", node, (b"jobs", b"#"), 0))              # one local key
+    evs.append(sub(b"remote3", nodes[3], (b"jobs", b"+"), 0))        # a remote node in the mask
+    evs.append(sub(b"exact5", node, (b"jobs", b"x5"), 2))            # the exact key, in many-key mode
+    for m in range(8):    # k/+ : 8 keys, + the exact key k/x = 9 (overflows G=2's 8 at the exact probe)
+        evs.append(sub(b"k%d" % m, nodes[m], (b"$share", b"gk", b"k", b"+"), 0))
+    evs.append(sub(b"kx", node, (b"k", b"x"), 1))
+    for m in range(8):    # $SYS/+ (valid for $-topics) and +/x5 (skipped for them, MQTT-4.7.2-1)
+        evs.append(sub(b"s%d" % m, nodes[m], (b"$share", b"gs", b"$SYS", b"+"), 0))
+        evs.append(sub(b"d%d" % m, nodes[m], (b"$share", b"gd", b"+", b"x5"), 0))
+    for j in range(64):   # ordinary publishes: one exact subscriber each
+        evs.append(sub(b"o%d" % j, node, (b"o", b"%d" % j), 0))
+    return evs
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("fast_g", [1, 2, 4])
+def test_many_key_publishes_stay_in_the_fast_tier(mode, fast_g):
+    """Publishes matching $share groups on many nodes (up to 105 keys, 1,600
+    records each) are counted by the fast tier and written wave-wide by the
+    EMIT wave-tier launch — none deferred — and equal the oracle's, mixed
+    with ordinary publishes in one batch."""
+    node = "n0@h"
+    prod = _driver(node, mode, nodes=[node] + ["n%d@h" % k for k in range(1, 8)])
+    prod.view.set_option("fast_g", fast_g)
+    orc = O.TrieOracle(node)
+    evs = _many_key_events(node)
+    prod.apply(evs)
+    orc.apply(evs)
+    kinds = [("", (b"jobs", b"x%d" % j)) for j in range(8)] + [("", (b"k", b"x")), ("", (b"k", b"y")),
+             ("", (b"$SYS", b"x5")), ("", (b"$SYS", b"q")), ("", (b"jobs",))]
+    kinds += [("", (b"o", b"%d" % j)) for j in range(64)]
+    want = orc.fold_batch([(mp, b"pub", t) for mp, t in kinds])
+    assert max(len(x) for x in want) > 1500
+    v = prod.view
+    arr, words = v.prepare(kinds)
+    rs = np.random.RandomState(7)
+    idx = rs.randint(0, len(kinds), size=6000)
+    idx[:len(kinds)] = np.arange(len(kinds))
+    recs, offs = prod.match_arrays(arr[idx], words)
+    st = v.stats_raw()
+    assert st["deferred_tier1"] == 0, st
+    assert st["many_key"] > 0, st
+    counts = np.diff(offs.astype(np.int64))
+    assert np.array_equal(counts, np.array([len(x) for x in want], dtype=np.int64)[idx])
+    for i in list(range(len(kinds))) + list(range(len(kinds), len(idx), 97)):
+        got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
+        assert got == sorted(want[idx[i]]), (i, kinds[idx[i]])
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("fast_g", [1, 2, 4])
+def test_two_key_publishes_with_one_record_keys(mode, fast_g):
+    """Every two-key publish whose second (or first, or both) key holds
+    exactly one record: the EMIT resolve preloads one-record keys, per lane
+    of the group (the one-lane case included)."""
+    node = "n@h"
+    prod = _driver(node, mode)
+    prod.view.set_option("fast_g", fast_g)
+    orc = O.TrieOracle(node)
+    sub = lambda cid, t, q: ("updated", ("", cid), None, [(node, True, [(t, q)])])
+    evs = [sub(b"a%d" % i, (b"a", b"+"), i % 3) for i in range(40)]           # key 0: 40 records
+    evs += [sub(b"b0", (b"b", b"+"), 1)]                                      # key 0: 1 record
+    evs += [sub(b"c%d" % i, (b"c", b"+"), 0) for i in range(3)]               # key 0: 3 records
+    for j in range(50):
+        evs.append(sub(b"ax%d" % j, (b"a", b"%d" % j), 2))                    # key 1: 1 record
+        evs.append(sub(b"bx%d" % j, (b"b", b"%d" % j), 0))                    # key 1: 1 record
+        evs += [sub(b"cx%d_%d" % (j, i), (b"c", b"%d" % j), 1) for i in range(2)]   # key 1: 2 records
+    prod.apply(evs)
+    orc.apply(evs)
+    kinds = [("", (p, b"%d" % j)) for p in (b"a", b"b", b"c") for j in range(60)]
+    want = orc.fold_batch([(mp, b"pub", t) for mp, t in kinds])
+    v = prod.view
+    arr, words = v.prepare(kinds)
+    idx = np.random.RandomState(3).randint(0, len(kinds), size=20_000)
+    recs, offs = prod.match_arrays(arr[idx], words)
+    counts = np.diff(offs.astype(np.int64))
+    assert np.array_equal(counts, np.array([len(x) for x in want], dtype=np.int64)[idx])
+    for i in range(0, len(idx), 7):
+        got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
+        assert got == sorted(want[idx[i]]), (i, kinds[idx[i]])
+
+
+def test_range_results_are_epoch_safe():
+    """A range match queued before an apply that rewrites record slots cannot
+    be expanded against the post-apply table (vmqg_records_at refuses its
+    epoch); matched again, the ranges expand to the oracle's answer at the
+    new epoch, and a range result with no apply after it expands to the
+    oracle's answer at its own epoch (lookup_subs/1 never returns a stale
+    list, vmq_reg_trie.erl:87-94)."""
+    import torch
+    from vernemq_amd import _lib
+    node = "n@h"
+    prod = _driver(node)
+    v = prod.view
+    orc = O.TrieOracle(node)
+    sub = lambda cid, t, q: ("updated", ("", cid), None, [(node, True, [(t, q)])])
+    evs = [sub(b"w%d" % i, (b"a", b"+"), i % 3) for i in range(50)]
+    evs += [sub(b"x%d" % i, (b"a", b"%d" % (i % 5)), 1) for i in range(20)]
+    prod.apply(evs)
+    orc.apply(evs)
+    topics = [("", (b"a", b"%d" % j)) for j in range(8)]
+    arr, words = v.prepare(topics)
+    dev = torch.device("cuda:0")
+    d_pubs = torch.from_numpy(arr.view(np.uint32).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    cap = 1024
+    d_rng = torch.zeros(cap * 2, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(len(arr) + 1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+
+    def queue():
+        e = v.epoch()
+        v.match_ranges_device(d_pubs.data_ptr(), len(arr), d_words.data_ptr(), d_rng.data_ptr(), cap,
+                              d_offs.data_ptr(), s)
+        return e
+
+    def expand(e):
+        assert v.match_status(s) == 0
+        offs = d_offs.cpu().numpy().astype(np.uint64)
+        rng = d_rng.cpu().numpy().view(np.uint32).reshape(-1, 2)[: int(offs[-1])]
+        r = np.zeros(len(rng), dtype=[("off", "<u4"), ("count", "<u4")])
+        r["off"], r["count"] = rng[:, 0], rng[:, 1]
+        recs, eo = v.expand_ranges(r, offs, recs=v.records(epoch=e))
+        return [sorted(H.canon(v.decode(recs[j])) for j in range(int(eo[i]), int(eo[i + 1]))) for i in range(len(arr))]
+
+    def want():
+        return [sorted(x) for x in orc.fold_batch([(mp, b"pub", t) for mp, t in topics])]
+
+    e0 = queue()
+    assert expand(e0) == want()                     # no apply in between
+    e1 = queue()
+    dels = [("deleted", ("", b"w%d" % i), [(node, True, [((b"a", b"+"), i % 3)])]) for i in range(0, 50, 3)]
+    prod.apply(dels)                                # deletes move records into the freed slots
+    orc.apply(dels)
+    torch.cuda.synchronize()
+    with pytest.raises(_lib.VmqgError):
+        v.records(epoch=e1)
+    e2 = queue()
+    assert e2 > e1
+    assert expand(e2) == want()
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("fast_g", [1, 2, 4])
+def test_retry_tier_serves_one_lane_overflows(mode, fast_g):
+    """16 filters over {x, +} at 4 levels all match x/x/x/x: more candidates
+    than the one- and two-lane fast passes hold, so the COUNT wave-tier
+    launch retries the publish four lanes per publish (16 candidates, 17 keys
+    with the exact one: many-key mode) — no whole-wave walk — interleaved
+    with publishes the fast pass serves."""
+    import itertools
+    node = "n@h"
+    prod = _driver(node, mode)
+    prod.view.set_option("fast_g", fast_g)
+    orc = O.TrieOracle(node)
+    evs = []
+    for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=4)):
+        evs.append(("updated", ("", b"f%d" % i), None, [(node, True, [(combo, i % 3)])]))
+    evs.append(("updated", ("", b"ex"), None, [(node, True, [((b"x", b"x", b"x", b"x"), 1)])]))
+    evs += [("updated", ("", b"o%d" % j), None, [(node, True, [((b"o", b"%d" % j), 0)])]) for j in range(32)]
+    prod.apply(evs)
+    orc.apply(evs)
+    kinds = [("", (b"x",) * 4), ("", (b"x", b"y", b"x", b"y"))] + [("", (b"o", b"%d" % j)) for j in range(32)]
+    want = orc.fold_batch([(mp, b"pub", t) for mp, t in kinds])
+    assert len(want[0]) == 17
+    v = prod.view
+    arr, words = v.prepare(kinds)
+    idx = np.random.RandomState(5).randint(0, len(kinds), size=5000)
+    idx[:2] = [0, 1]
+    recs, offs = prod.match_arrays(arr[idx], words)
+    st = v.stats_raw()
+    assert st["deferred_tier1"] == 0, st
+    assert (st["retried"] > 0) == (fast_g != 4), st
+    counts = np.diff(offs.astype(np.int64))
+    assert np.array_equal(counts, np.array([len(x) for x in want], dtype=np.int64)[idx])
+    for i in range(0, len(idx), 3):
+        got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
+        assert got == sorted(want[idx[i]]), (i, kinds[idx[i]])
+
+
+def test_released_stream_can_be_destroyed():
+    """A caller stream released with vmqg_release_stream (the context's last
+    work was on it) may be destroyed: the next call on another stream waits
+    for the event recorded at release, not on the dead stream."""
+    import gc
+    import torch
+    from vernemq_amd import workloads as W
+    w = W.config_b(n_subs=20_000, n_pubs=4096)
+    v, _ = _load_both(w, with_oracle=False)
+    pubs, words = w.publish_arrays(v)
+    ref_recs, ref_offs = v.match_arrays(pubs, words)
+    dev = torch.device("cuda:0")
+    d_pubs = torch.from_numpy(pubs.view(np.uint32).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    cap = int(ref_offs[-1]) + 16
+    d_out = torch.zeros(cap * 4, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
+    for rep in range(3):
+        s = torch.cuda.Stream()
+        v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap, d_offs.data_ptr(),
+                       s.cuda_stream)
+        v.release_stream(s.cuda_stream)
+        s.synchronize()
+        del s
+        gc.collect()
+        d_offs.zero_()
+        v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap, d_offs.data_ptr(), 0)
+        assert v.match_status(0) == 0
+        assert np.array_equal(d_offs.cpu().numpy().astype(np.uint64), ref_offs), rep

@@ -90,3 +90,27 @@ def test_bulk_growth_rebuilds():
     orc.apply(evs)
     assert prod.view.stats_raw()["rebuilds"] >= 2
     _compare(prod, orc, "bulk")
+
+
+def test_record_epochs_refuse_stale_ranges():
+    """vmqg_epoch / vmqg_records_at on the host engine: an apply that rewrites
+    record slots makes the older epochs' record tables unavailable (range
+    results of those epochs must be matched again); an epoch with no
+    record-writing apply after it stays valid."""
+    from vernemq_amd import _lib
+    node = "n@h"
+    prod = H.ProductDriver(node, device=-1)
+    v = prod.view
+    sub = lambda cid, t, q: ("updated", ("", cid), None, [(node, True, [(t, q)])])
+    prod.apply([sub(b"w%d" % i, (b"a", b"+"), 1) for i in range(10)])
+    e1 = v.epoch()
+    assert len(v.records(epoch=e1)) > 0
+    with pytest.raises(_lib.VmqgError):
+        v.records(epoch=e1 + 1)                       # not yet applied
+    prod.apply([("deleted", ("", b"w3"), [(node, True, [((b"a", b"+"), 1)])])])
+    e2 = v.epoch()
+    assert e2 == e1 + 1
+    with pytest.raises(_lib.VmqgError):
+        v.records(epoch=e1)                           # a slot was rewritten
+    recs = v.records(epoch=e2)
+    assert len(recs) > 0

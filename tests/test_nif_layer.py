@@ -7,6 +7,8 @@ and the loud refusal to match without a device."""
 import os
 import subprocess
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -30,5 +32,104 @@ def test_nif_sources_are_present():
     nif = open(os.path.join(ROOT, "integration", "c_src", "vmqg_nif.c")).read()
     for needle in ("-behaviour(vmq_reg_view)", "fold(", "start_link()", "stats()", "subscribe_subscriber_changes"):
         assert needle in erl, needle
-    for needle in ("ERL_NIF_INIT", "vmqgb_match", "vmqgb_fold", "vmqgb_ops_apply", "ERL_NIF_DIRTY_JOB_CPU_BOUND"):
+    for needle in ("ERL_NIF_INIT", "vmqgb_view_match", "vmqgb_fold", "vmqgb_ops_apply", "ERL_NIF_DIRTY_JOB_CPU_BOUND"):
         assert needle in nif, needle
+
+
+def _nif_script(seed=11, n_subs=3000, n_pubs=2500):
+    """A subscription set (wildcards, $share groups on several nodes, remote
+    nodes incl. one >= 64, $-topics), publishes, and the script that drives
+    tools/bin/batch_gpu_check through it; plus the same changes as
+    subscriber-store events for the oracle."""
+    import random
+    r = random.Random(seed)
+    nodes = ["n0@h"] + ["n%d@h" % k for k in range(1, 6)] + ["n70@h"]
+    node_ids = list(range(6)) + [70]
+    words = [b"a", b"b", b"c", b"d"]
+
+    def rand_filter():
+        pre = (b"$share", r.choice([b"g1", b"g2", b"g3"])) if r.random() < 0.2 else ()
+        L = r.randint(1, 4)
+        t = [b"+" if r.random() < 0.25 else (b"#" if (i == L - 1 and r.random() < 0.15) else r.choice(words))
+             for i in range(L)]
+        if r.random() < 0.05:
+            t[0] = b"$SYS"
+        return pre + tuple(t)
+
+    subs = []
+    for k in range(n_subs):
+        ni = r.choice(range(len(nodes))) if r.random() < 0.3 else 0
+        subs.append((ni, k, r.randint(0, 2), rand_filter()))
+    pubs = []
+    for _ in range(n_pubs):
+        L = r.randint(1, 5)
+        t = [r.choice(words) for _ in range(L)]
+        if r.random() < 0.05:
+            t[0] = b"$SYS"
+        pubs.append(tuple(t))
+    lines = []
+    line = lambda c, s: "%s %d %d %d 0 %s" % (c, node_ids[s[0]], s[1], s[2], b"/".join(s[3]).decode())
+    lines += [line("S", s) for s in subs] + ["A"]
+    lines += ["P 0 %s" % b"/".join(t).decode() for t in pubs]
+    lines += ["M records 8 64", "M ranges 4 100"]
+    gone = subs[::3]
+    lines += [line("U", s) for s in gone] + ["A"]
+    lines += ["M records 16 37", "C ranges 8 50 300"]
+    sid = lambda k: ("", b"c%d" % k)
+    ev_add = [("updated", sid(k), None, [(nodes[ni], True, [(f, q)])]) for ni, k, q, f in subs]
+    ev_del = [("deleted", sid(k), [(nodes[ni], True, [(f, q)])]) for ni, k, q, f in gone]
+    return "\n".join(lines) + "\n", nodes, node_ids, pubs, ev_add, ev_del
+
+
+def _parse_blocks(text, nodes, node_ids):
+    from oracle import oracle as O
+    name = {nid: nodes[i] for i, nid in enumerate(node_ids)}
+    blocks, cur = [], None
+    for ln in text.splitlines():
+        if ln.startswith("M "):
+            cur = []
+            blocks.append(cur)
+            continue
+        f = ln.split(" ")
+        rc = int(f[1])
+        ents = []
+        for e in f[2:]:
+            kind, node, group, sub, info = e.split(",")
+            kind, node, sub, info = int(kind), int(node), int(sub), int(info)
+            if kind == 1:
+                ents.append(("A", ("", b"c%d" % sub), O.subinfo_repr(info)))
+            elif kind == 2:
+                ents.append(("B", name[node], group.encode(), ("", b"c%d" % sub), O.subinfo_repr(info)))
+            else:
+                ents.append(("C", name[node]))
+        cur.append((rc, sorted(ents)))
+    return blocks
+
+
+@pytest.mark.gpu
+def test_batch_layer_on_the_gpu_with_concurrent_batchers(tmp_path):
+    """vmqg_batch.c on the device, driven as vmqg_nif.c drives it: 4-16
+    batcher threads with their own batches under the view's locks (records
+    and ranges, overflow retries, the fold), then after deletes, and once
+    more while a writer applies changes between batches — every publish's
+    entries equal the oracle's."""
+    import subprocess
+    from oracle import oracle as O
+    exe = os.path.join(ROOT, "tools", "bin", "batch_gpu_check")
+    assert os.path.exists(exe), "tools/bin/batch_gpu_check not built (__graft_entry__.build())"
+    script, nodes, node_ids, pubs, ev_add, ev_del = _nif_script()
+    (tmp_path / "s.txt").write_text(script)
+    r = subprocess.run([exe, str(tmp_path / "s.txt"), str(tmp_path / "o.txt")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    blocks = _parse_blocks((tmp_path / "o.txt").read_text(), nodes, node_ids)
+    assert len(blocks) == 4 and all(len(b) == len(pubs) for b in blocks)
+    orc = O.TrieOracle(nodes[0])
+    orc.apply(ev_add)
+    want1 = [sorted(x) for x in orc.fold_batch([("", b"pub", t) for t in pubs])]
+    orc.apply(ev_del)
+    want2 = [sorted(x) for x in orc.fold_batch([("", b"pub", t) for t in pubs])]
+    assert sum(len(x) for x in want1) > len(pubs)
+    for bi, want in ((0, want1), (1, want1), (2, want2), (3, want2)):
+        bad = [i for i in range(len(pubs)) if blocks[bi][i] != (0, want[i])]
+        assert not bad, (bi, len(bad), pubs[bad[0]], blocks[bi][bad[0]][1][:5], want[bad[0]][:5])

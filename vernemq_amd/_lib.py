@@ -79,7 +79,7 @@ class Stats(ctypes.Structure):
                 ("subs", "device_bytes", "trie_edges", "trie_nodes", "trie_topics", "subs_objects",
                  "fanout_objects", "remote_keys", "epoch", "rebuilds", "paths", "words",
                  "deferred_tier1", "deferred_tier2", "ops_applied", "apply_host_ns", "apply_upload_ns", "apply_wait_ns", "patch_bytes",
-                 "image_bytes", "max_depth")]
+                 "image_bytes", "max_depth", "many_key", "retried", "wave_entries")]
 
 
 class RConfig(ctypes.Structure):
@@ -137,6 +137,12 @@ SIGNATURES = [
     ("vmqg_match_ranges", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
     ("vmqg_match_ranges_device", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),
     ("vmqg_records", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
+    ("vmqg_release_stream", ctypes.c_int, [_P, _P]),
+    ("vmqr_release_stream", ctypes.c_int, [_P, _P]),
+    ("vmqa_release_stream", ctypes.c_int, [_P, _P]),
+    ("vmqs_release_stream", ctypes.c_int, [_P, _P]),
+    ("vmqg_epoch", ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
+    ("vmqg_records_at", ctypes.c_int, [_P, _U64, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
     ("vmqg_replica_sync_layout", ctypes.c_int, [_P, _P]),
     ("vmqg_stats", ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
     ("vmqg_dump", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_SZ)]),
@@ -144,6 +150,7 @@ SIGNATURES = [
     ("vmqg_set_timing", ctypes.c_int, [_P, ctypes.c_int]),
     ("vmqg_kernel_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
+    ("vmqg_kernel_times_ex", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
     ("vmqg_arena", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64), _P]),
     ("vmqg_export_image", ctypes.c_int, [_P, _P, _U64]),
     ("vmqg_replica_load", ctypes.c_int, [_P, _P, _P, _P]),

@@ -2,6 +2,7 @@
 #include <new>
 
 #include "vmqa_engine.h"
+#include "vmqg_chain.h"
 #include "vmqg_nullorder.h"
 
 using vmqa::AclEngine;
@@ -80,6 +81,13 @@ int vmqa_check_device(vmqa_ctx* ctx, const vmqa_req* d_reqs, uint32_t n, const u
   hipSetDevice(ctx->e.device);
   return ctx->e.check_device(d_reqs, n, d_words, d_allowed, vmqg::caller_stream(stream));
   GUARD_END
+}
+
+int vmqa_release_stream(vmqa_ctx* ctx, void* stream) {
+  if (!ctx) return VMQG_E_INVAL;
+  if (!ctx->e.ev_done) return VMQG_OK;
+  hipSetDevice(ctx->e.device);
+  return vmqg::chain_release(ctx->e.ev_done, ctx->e.chk_stream, vmqg::caller_stream(stream));
 }
 
 int vmqa_check_status(vmqa_ctx* ctx, void* stream) {

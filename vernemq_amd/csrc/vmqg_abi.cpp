@@ -5,6 +5,7 @@
 #include <string>
 #include <new>
 
+#include "vmqg_chain.h"
 #include "vmqg_nullorder.h"
 #include "vmqg_engine.h"
 
@@ -202,6 +203,27 @@ int vmqg_records(vmqg_ctx* ctx, const vmqg_emit** recs, uint64_t* n) {
   return VMQG_OK;
 }
 
+int vmqg_epoch(vmqg_ctx* ctx, uint64_t* epoch) {
+  if (!ctx || !epoch) return VMQG_E_INVAL;
+  *epoch = ctx->e.epoch;
+  return VMQG_OK;
+}
+
+int vmqg_records_at(vmqg_ctx* ctx, uint64_t epoch, const vmqg_emit** recs, uint64_t* n) {
+  if (!ctx || !recs || !n) return VMQG_E_INVAL;
+  Engine& e = ctx->e;
+  if (e.replica) return VMQG_E_STATE;
+  if (epoch > e.epoch || e.rec_epoch > epoch) return VMQG_E_STATE;   // a later apply rewrote record slots
+  return vmqg_records(ctx, recs, n);
+}
+
+int vmqg_release_stream(vmqg_ctx* ctx, void* stream) {
+  if (!ctx) return VMQG_E_INVAL;
+  if (!ctx->e.has_device) return VMQG_OK;
+  hipSetDevice(ctx->e.device);
+  return vmqg::chain_release(ctx->e.ev_match_done, ctx->e.ev_stream, vmqg::caller_stream(stream));
+}
+
 int vmqg_match_status(vmqg_ctx* ctx, void* stream) {
   if (!ctx) return VMQG_E_INVAL;
   GUARD_BEGIN
@@ -233,6 +255,9 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->patch_bytes = e.patch_bytes;
   out->image_bytes = e.image_bytes;
   out->max_depth = e.stack_depth();
+  out->many_key = e.last_many;
+  out->retried = e.last_retried;
+  out->wave_entries = e.last_wave_entries;
   return VMQG_OK;
 }
 
@@ -269,7 +294,7 @@ int vmqg_set_timing(vmqg_ctx* ctx, int enable) {
   if (!ctx) return VMQG_E_INVAL;
   ctx->e.collect_times();
   ctx->e.timing = enable != 0;
-  ctx->e.sum_count_ns = ctx->e.sum_emit_ns = 0;
+  for (double& x : ctx->e.sum_stage_ns) x = 0;
   ctx->e.n_timed = 0;
   return VMQG_OK;
 }
@@ -279,8 +304,20 @@ int vmqg_kernel_times(vmqg_ctx* ctx, double* count_ns, double* emit_ns, uint64_t
   GUARD_BEGIN
   Engine& e = ctx->e;
   e.collect_times();
-  if (count_ns) *count_ns = e.n_timed ? e.sum_count_ns / e.n_timed : 0;
-  if (emit_ns) *emit_ns = e.n_timed ? e.sum_emit_ns / e.n_timed : 0;
+  if (count_ns) *count_ns = e.n_timed ? e.sum_stage_ns[0] / e.n_timed : 0;
+  if (emit_ns) *emit_ns = e.n_timed ? e.sum_stage_ns[3] / e.n_timed : 0;
+  if (launches) *launches = e.n_timed;
+  return VMQG_OK;
+  GUARD_END
+}
+
+int vmqg_kernel_times_ex(vmqg_ctx* ctx, double* stage_ns, uint64_t* launches) {
+  if (!ctx) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  Engine& e = ctx->e;
+  e.collect_times();
+  for (int k = 0; k < Engine::kTimedStages; k++)
+    if (stage_ns) stage_ns[k] = e.n_timed ? e.sum_stage_ns[k] / e.n_timed : 0;
   if (launches) *launches = e.n_timed;
   return VMQG_OK;
   GUARD_END

@@ -22,8 +22,7 @@ Engine::~Engine() {
   if (has_device) {
     hipSetDevice(device);
     if (stream) hipStreamSynchronize(stream);
-    for (auto& e : t_count) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
-    for (auto& e : t_emit) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
+    for (auto& ev : t_ev) for (auto e : ev) hipEventDestroy(e);
     if (ev_match_done) hipEventDestroy(ev_match_done);
     for (Stage& sg : stage) {
       if (sg.ev) hipEventDestroy(sg.ev);
@@ -63,8 +62,8 @@ int Engine::init(const vmqg_config& c) {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VMQG_E_DEVICE;
     if (hipEventCreateWithFlags(&ev_match_done, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
     has_device = true;
-    if (hipMalloc(&d_status, 64) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMemset(d_status, 0, 64) != hipSuccess) return VMQG_E_DEVICE;
+    if (hipMalloc(&d_status, kStatusBytes) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMemset(d_status, 0, kStatusBytes) != hipSuccess) return VMQG_E_DEVICE;
     for (Stage& sg : stage)
       if (hipEventCreateWithFlags(&sg.ev, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
     if (hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cu_count < 1)
@@ -868,7 +867,9 @@ int Engine::upload() {
   if (!full_image) {
     last_patches.reserve(dirty_chunks.size());
     const uint8_t* base = reinterpret_cast<const uint8_t*>(mirror.data());
+    const uint64_t rec_lo = lay.rec_off >> 4, rec_hi = (lay.rec_off + lay.rec_cap * sizeof(Record)) >> 4;
     for (uint64_t c : dirty_chunks) {
+      if (c >= rec_lo && c < rec_hi) rec_epoch = epoch;   // a record slot rewritten: older ranges are stale
       Patch p;
       p.off = c * 16;
       memcpy(p.data, base + p.off, 16);
@@ -879,6 +880,7 @@ int Engine::upload() {
     patch_bytes += last_patches.size() * sizeof(Patch);
   } else {
     image_bytes += lay.total_bytes;
+    rec_epoch = epoch;   // re-laid out: every record may have moved
   }
   if (!has_device) { full_image = false; return VMQG_OK; }
   hipSetDevice(device);
@@ -941,7 +943,7 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     // 32-B key cache + kSpillKeys x 8-B spilled keys per publish, then the
     // chunk totals (one per 16 or 32 publishes, + 1)
     if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + (cap / 16 + 2) * 8) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_deferred, 2 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMalloc(&d_deferred, 3 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;   // three lists
     keycache_cap = cap;
     deferred_cap = cap;
   }
@@ -1006,9 +1008,9 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.keyspill = reinterpret_cast<uint2*>(static_cast<char*>(d_keycache) + keycache_cap * 32);
   a.chunk = reinterpret_cast<uint64_t*>(static_cast<char*>(d_keycache) + keycache_cap * (32 + 8 * 8));
   a.gpw = 64 / (opt_fast_g == 4 ? 4 : opt_fast_g == 1 ? 1 : 2);   // publishes per chunk
-  a.status = d_status + 4 * (call_seq & 1);
-  a.status_next = d_status + 4 * ((call_seq + 1) & 1);
-  a.err = d_status + 8;
+  a.status = d_status + kStatusSet * (call_seq & 1);
+  a.status_next = d_status + kStatusSet * ((call_seq + 1) & 1);
+  a.err = d_status + 2 * kStatusSet;
   a.deferred = d_deferred;
   a.fast_g = opt_fast_g; a.opts = opt_flags;
   a.count_bpc = opt_count_bpc; a.emit_bpc = opt_emit_bpc;
@@ -1037,40 +1039,45 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   a.out_rng = d_rng; a.rng_cap = rng_cap;
   last_set = call_seq & 1;
   call_seq++;
-  // kernel timing (vmqg_set_timing): events written by the fast-tier
-  // dispatches themselves, so timing adds no marker packets between launches
-  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
+  // kernel timing (vmqg_set_timing): events written by each dispatch itself
+  // (hipExtLaunchKernel), so timing adds no marker packets between launches
+  std::array<hipEvent_t, 2 * kTimedStages> ev{};
   if (timing) {
-    hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2); hipEventCreate(&e3);
-    t_count.push_back({e0, e1});
-    t_emit.push_back({e2, e3});
+    for (auto& e : ev) hipEventCreate(&e);
+    t_ev.push_back(ev);
   }
   // COUNT: fast groups, then the wave tier for what they deferred
-  if (launch_match(a, 0, 0, st, e0, e1) != hipSuccess) return VMQG_E_DEVICE;
-  if (launch_match(a, 0, 1, st) != hipSuccess) return VMQG_E_DEVICE;
-  if (launch_scan(a, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 0, 0, st, ev[0], ev[1]) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 0, 1, st, ev[2], ev[3]) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_scan(a, st, ev[4], ev[5]) != hipSuccess) return VMQG_E_DEVICE;
   // EMIT: same tiers
-  if (launch_match(a, 1, 0, st, e2, e3) != hipSuccess) return VMQG_E_DEVICE;
-  if (launch_match(a, 1, 1, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 1, 0, st, ev[6], ev[7]) != hipSuccess) return VMQG_E_DEVICE;
+  if (launch_match(a, 1, 1, st, ev[8], ev[9]) != hipSuccess) return VMQG_E_DEVICE;
   return VMQG_OK;
 }
 
-// Status words: two sets of per-call counters ([0] deferred publishes, [1]
-// of those walked with a global stack, [2] scan ticket) used by alternate
-// calls, and at [8] the error bits latched since the previous
-// vmqg_match_status.
+// Status words: two sets of per-call counters (kStatusSet words each: [0]
+// publishes the fast pass deferred to the 4-lane retry, [1] whole-wave walks
+// with a global stack, [2] scan ticket, [3] whole-wave walks, [4] many-key
+// publishes, [5] fast-pass deferrals by a walk overflow, [6..7] entries the
+// EMIT wave-tier launch wrote) used by alternate calls, then the error bits
+// latched since the previous vmqg_match_status.
 int Engine::match_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
   if (order_on(st) != VMQG_OK) return VMQG_E_DEVICE;   // the matches queued on any stream
-  uint32_t h[12] = {0};
+  uint32_t h[2 * kStatusSet + 1] = {0};
   if (hipMemcpyAsync(h, d_status, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
-  if (hipMemsetAsync(d_status + 8, 0, 4, st) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipMemsetAsync(d_status + 2 * kStatusSet, 0, 4, st) != hipSuccess) return VMQG_E_DEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
-  last_deferred[0] = h[4 * last_set];
-  last_deferred[1] = h[4 * last_set + 1];
-  const uint32_t err = h[8];
+  const uint32_t* c = h + kStatusSet * last_set;
+  last_deferred[0] = c[3];
+  last_deferred[1] = c[1];
+  last_retried = c[0];
+  last_many = c[4];
+  last_wave_entries = (uint64_t)c[6] | ((uint64_t)c[7] << 32);
+  const uint32_t err = h[2 * kStatusSet];
   if (err & 2u) return VMQG_E_FRONTIER;
   if (err & 4u) return VMQG_E_OVERFLOW;
   if (err & (8u | 16u)) return VMQG_E_DEVICE;   // count mismatch, look-back timeout
@@ -1080,16 +1087,17 @@ int Engine::match_status(hipStream_t st) {
 void Engine::collect_times() {
   if (!has_device) return;
   hipSetDevice(device);
-  for (size_t i = 0; i < t_count.size(); i++) {
-    float a = 0, b = 0;
-    hipEventSynchronize(t_emit[i].second);
-    hipEventElapsedTime(&a, t_count[i].first, t_count[i].second);
-    hipEventElapsedTime(&b, t_emit[i].first, t_emit[i].second);
-    sum_count_ns += a * 1e6; sum_emit_ns += b * 1e6; n_timed++;
-    hipEventDestroy(t_count[i].first); hipEventDestroy(t_count[i].second);
-    hipEventDestroy(t_emit[i].first); hipEventDestroy(t_emit[i].second);
+  for (auto& ev : t_ev) {
+    hipEventSynchronize(ev[2 * kTimedStages - 1]);
+    for (int k = 0; k < kTimedStages; k++) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
+      sum_stage_ns[k] += ms * 1e6;
+    }
+    n_timed++;
+    for (auto e : ev) hipEventDestroy(e);
   }
-  t_count.clear(); t_emit.clear();
+  t_ev.clear();
 }
 
 // ------------------------------------------------------------------ dump

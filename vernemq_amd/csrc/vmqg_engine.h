@@ -9,6 +9,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <memory>
 #include <new>
@@ -226,9 +227,19 @@ struct Engine {
   uint32_t o_cap = 0, o_waves = 0;
   uint64_t o_cap_floor = 0;         // raised by vmqg_match_batch if a tier-2 stack ever overflowed
   int cu_count = 0;
-  uint32_t last_deferred[2] = {0, 0};   // tier-1 / tier-2 publishes of the last checked batch
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> t_count, t_emit;
-  double sum_count_ns = 0, sum_emit_ns = 0; uint64_t n_timed = 0;
+  uint32_t last_deferred[2] = {0, 0};   // whole-wave walks (LDS / global stack) of the last checked batch
+  uint32_t last_many = 0, last_retried = 0;    // ... many-key publishes / retried four lanes per publish
+  uint64_t last_wave_entries = 0;              // ... entries (records or ranges) the wave tier wrote
+  // epoch of the last apply that rewrote a record slot (or re-laid out the
+  // arena): range results of an older epoch index records that may have
+  // changed (vmqg_records_at refuses them)
+  uint64_t rec_epoch = 0;
+  // device status: two per-call counter sets of kStatusSet words, then the sticky error word
+  static constexpr uint32_t kStatusSet = 8, kStatusBytes = 128;
+  // per-launch timing: COUNT fast tier, COUNT wave tier, scan, EMIT fast tier, EMIT wave tier
+  static constexpr int kTimedStages = 5;
+  std::vector<std::array<hipEvent_t, 2 * kTimedStages>> t_ev;
+  double sum_stage_ns[kTimedStages] = {0, 0, 0, 0, 0}; uint64_t n_timed = 0;
 
   std::string dump_text;
 

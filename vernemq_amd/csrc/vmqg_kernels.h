@@ -47,7 +47,7 @@ constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted r
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, hipEvent_t t0 = nullptr,
                         hipEvent_t t1 = nullptr);
 // counts in offsets[0, npub) -> exclusive offsets[0, npub] (one launch, look-back)
-hipError_t launch_scan(const MatchArgs& a, hipStream_t st);
+hipError_t launch_scan(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 uint32_t scan_tiles(uint64_t nchunks);   // look-back tiles of the chunk-total scan
 hipError_t launch_patches(uint8_t* arena, const void* d_patches, uint64_t n, hipStream_t st);
 

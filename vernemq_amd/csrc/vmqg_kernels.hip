@@ -48,18 +48,24 @@ constexpr int kWaves = 4;          // waves per 256-thread block
 #endif
 // fast-tier LDS lists per group, sized so a block stays near 28 KiB
 template <int G> struct FastCaps { static constexpr uint32_t S = 8 * G, C = 4 * G, K = 4 * G; };
-constexpr uint32_t kRewalk = 0xFFFFFFFFu;   // key cache: EMIT must re-walk
 #ifndef VMQG_SPILL_KEYS
 #define VMQG_SPILL_KEYS 8                   // A/B: 2 = no spill (every publish with > 2 keys is re-walked)
 #endif
 constexpr uint32_t kSpillKeys = 8;          // spill slots per publish (more keys: re-walk)
 constexpr uint32_t kDeferred = 0xFFFFFFFEu; // key cache: the wave tier owns the publish
+constexpr uint32_t kMany = 0xFFFFFFFDu;     // key cache: more keys than the lists hold; EMIT expands the
+                                            // candidates COUNT left in the spill slots, wave-wide
 
 // Per-call status counters (a.status; two sets used by alternate calls: each
 // call's first kernel zeroes the set of the call after it, so no reset
 // launch is needed) and the sticky error word (a.err, cleared only by
 // vmqg_match_status).
-enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStRewalk = 3 };
+// Deferral lists (a.deferred, 3 x npub entries): [0, npub) publishes the
+// fast pass could not hold (retried four lanes per publish by the COUNT
+// wave-tier launch), [npub, 2 npub) many-key publishes (written by the EMIT
+// wave-tier launch), [2 npub, 3 npub) publishes walked by a whole wave.
+enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, kStMany = 4, kStWalkOvf = 5,
+                  kStWaveEnt = 6 /* u64: entries the EMIT wave-tier launch wrote */, kStWords = 8 };
 enum : uint32_t { kErrFrontier = 2u, kErrOverflow = 4u, kErrMismatch = 8u };   // kErrLookback = 16 (lookback.h)
 
 __device__ __forceinline__ uint32_t prefix_bits(uint64_t m) {
@@ -280,7 +286,26 @@ struct Matched {
   uint32_t nk, nkr, ksum, total_rec;   // keys, non-empty keys, records, record-mode total
   uint64_t rmask;
   bool overflow;                        // the lists overflowed or a node >= 64: the wave tier takes it
+  bool walk_ovf;                        // ... because the frontier or candidate list overflowed
+  bool many;                            // more keys than the key list holds: totals only (nk, keys unset);
+  uint32_t nc, ex_off, ex_cnt;          // the candidates stay in the LDS list, the exact key is {ex_off, ex_cnt}
 };
+
+// Records and non-empty keys of one multi-key candidate (its keylist ids ->
+// keydesc counts), for the many-key totals.
+__device__ __forceinline__ void sum_keys(const MatchArgs& a, uint32_t key, uint32_t n, uint32_t& sum, uint32_t& nkr) {
+#if VMQG_SUM_UNROLL
+#pragma unroll 4
+#else
+#pragma unroll 1
+#endif
+  for (uint32_t j = 0; j < n; j++) {
+    const uint32_t kid = a.keylist[key + j];
+    const uint32_t c = kid < a.key_cap ? a.keydesc[kid].count : 0u;
+    sum += c;
+    nkr += c != 0;
+  }
+}
 
 template <int G>
 __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const FastScratch<G>& s,
@@ -291,7 +316,7 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
   const bool mp_ok = pub.mountpoint < a.max_mp && L > 0;
   // lane i of the group keeps word i (i < G); deeper words come from memory
   const uint32_t wreg = g.lane < L ? w[g.lane] : kUnknownWord;
-  Matched m{0, 0, 0, 0, 0, false};
+  Matched m{0, 0, 0, 0, 0, false, false, false, 0, 0, 0};
   uint32_t nc = 0, sp = 0;
   if (mp_ok) {
     if (g.lane == 0) s.st(0) = make_uint2(pub.mountpoint, kHasAll << 28);   // {MP, root}: probe all
@@ -315,7 +340,7 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
     // frontier: the W and '+' children (:364-375)
     const uint64_t m_wc = g.ballot(o.wc != kNone), m_pc = g.ballot(o.pc != kNone);
     const uint32_t n_pc = (uint32_t)__popcll(m_pc), n_new_s = n_pc + (uint32_t)__popcll(m_wc);
-    if (nc + n_new_c > s.CC || sp + n_new_s > s.SC) { m.overflow = true; break; }
+    if (nc + n_new_c > s.CC || sp + n_new_s > s.SC) { m.overflow = m.walk_ovf = true; break; }
     if (o.hc != kNone) s.cd(nc + prefix_bits(m_hc)) = o.hc;
     if (o.at_end) s.cd(nc + n_hc + prefix_bits(m_end)) = node;
     nc += n_new_c;
@@ -326,8 +351,24 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
   }
 
   // ---- candidates -> subscriber-list keys: match/4, match_/3 (:283-303)
+  // Keys go to the LDS key list; a publish with more keys than it holds
+  // (a $share filter hosted on many nodes: one key per {Node, Group} entry,
+  // :68-72) switches to many-key mode: only its totals are kept here, and
+  // EMIT expands the candidates again, wave-wide.
   uint64_t rmask = 0;
   uint32_t nk = 0;
+  uint32_t msum = 0, mnkr = 0;   // many-key mode: this lane's records / non-empty keys
+  // into many-key mode: the keys listed so far become totals
+  auto to_many = [&]() {
+    m.many = true;
+    for (uint32_t i = g.lane; i < nk; i += G) {
+      const uint2 e = s.ky(i);
+      uint32_t c = e.y;
+      if (e.y == kUnresolved) c = e.x < a.key_cap ? a.keydesc[e.x].count : 0u;
+      msum += c;
+      mnkr += c != 0;
+    }
+  };
   if (!m.overflow) {
     for (uint32_t c0 = 0; c0 < nc; c0 += G) {
       const uint32_t ci = c0 + g.lane;
@@ -352,11 +393,20 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
       }
       const uint32_t incl = g.incl_scan(nkeys);
       const uint32_t tot = g.last(incl);
-      if (nk + tot > s.KC || g.ballot(high) != 0) { m.overflow = true; break; }
-      const uint32_t at = nk + incl - nkeys;
-      if (nkeys == 1) s.ky(at) = make_uint2(off0, cnt0);   // resolved inline
-      else for (uint32_t j = 0; j < nkeys; j++) s.ky(at + j) = make_uint2(a.keylist[key + j], kUnresolved);
+      if (g.ballot(high) != 0) { m.overflow = true; break; }
+      if (!m.many && nk + tot > s.KC) to_many();
+      if (!m.many) {
+        const uint32_t at = nk + incl - nkeys;
+        if (nkeys == 1) s.ky(at) = make_uint2(off0, cnt0);   // resolved inline
+        else for (uint32_t j = 0; j < nkeys; j++) s.ky(at + j) = make_uint2(a.keylist[key + j], kUnresolved);
+      } else if (nkeys == 1) {
+        msum += cnt0;
+        mnkr += cnt0 != 0;
+      } else if (nkeys > 1) {
+        sum_keys(a, key, nkeys, msum, mnkr);
+      }
       nk += tot;
+      wave_sync();
     }
   }
   wave_sync();
@@ -369,8 +419,15 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
       rmask |= ((uint64_t)q.w << 32) | q.z;
       if (e->nwords & kExactHigh) m.overflow = true;
       else if (q.y != 0) {
-        if (nk + 1 > s.KC) m.overflow = true;
-        else { if (g.lane == 0) s.ky(nk) = make_uint2(q.x, q.y); nk += 1; }
+        if (!m.many && nk + 1 > s.KC) to_many();
+        m.ex_off = q.x;
+        m.ex_cnt = q.y;
+        if (m.many) {
+          if (g.lane == 0) { msum += q.y; mnkr += 1; }
+        } else if (g.lane == 0) {
+          s.ky(nk) = make_uint2(q.x, q.y);
+        }
+        nk += 1;
       }
     }
   }
@@ -378,7 +435,16 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
   m.rmask = g.or64(rmask);
   if (a.local_node < kLowNodes) m.rmask &= ~(1ull << a.local_node);
   if (m.overflow) return m;
+  if (m.many) {   // totals only; the candidates stay in the LDS list for COUNT to spill
+    m.nc = nc;
+    m.nk = nk;
+    m.ksum = (uint32_t)g.sum64(msum);
+    m.nkr = (uint32_t)g.sum64(mnkr);
+    m.total_rec = m.ksum + (uint32_t)__popcll(m.rmask);
+    return m;
+  }
 
+  m.nc = nc;
   // ---- record ranges per key: lookup_subs/1 (:87-94)
   uint32_t ksum = 0, nkr = 0;
   for (uint32_t k0 = 0; k0 < nk; k0 += G) {
@@ -446,42 +512,70 @@ __device__ __forceinline__ void store_range(vmqg_range* out, uint64_t i, uint32_
 }
 
 // ------------------------------------------------------------ COUNT pass
-// Returns the publish's count on the group's lane 0 (0 when deferred: the
-// wave tier adds it to the chunk total), 0 on the other lanes.
-template <int G, int OUT>
-__device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g) {
+// Returns the publish's count on the group's lane 0 (0 when deferred: a
+// later tier adds it to the chunk total), 0 on the other lanes; `fl` (lane
+// 0) says how it was served: 0 fast tier, 1 many-key mode, 2 deferred by a
+// walk overflow, 3 deferred otherwise (remote nodes >= 64).  Deferred
+// publishes go to list RETRY ? 2 (whole-wave walks) : 0 (the 4-lane retry).
+template <int G, int OUT, bool RETRY = false>
+__device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
+                                  uint32_t& fl) {
   const vmqg_pub pub = a.pubs[p];
   const Matched m = walk_publish<G>(a, pub, s, g);
+  fl = 0;
+  // more keys than the spill slots hold: many-key mode too (EMIT expands the
+  // candidates wave-wide instead of walking again)
+  const bool many = !m.overflow && (m.many || m.nk > VMQG_SPILL_KEYS);
   // 3..8 keys: the group copies its key list to the publish's spill slots
-  const bool spill = !m.overflow && m.nk > 2 && m.nk <= VMQG_SPILL_KEYS;
+  const bool spill = !m.overflow && !many && m.nk > 2;
   if (spill)
     for (uint32_t i = g.lane; i < m.nk; i += G) a.keyspill[(uint64_t)p * kSpillKeys + i] = s.ky(i);
+  // many keys: the candidate paths (<= FastCaps::C <= 16 words) instead
+  if (many)
+    for (uint32_t i = g.lane; i < m.nc; i += G)
+      reinterpret_cast<uint32_t*>(a.keyspill)[(uint64_t)p * 2 * kSpillKeys + i] = s.cd(i);
   if (g.lane != 0) return 0;
   uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
-  if (m.overflow) {   // the wave tier counts it (and writes offsets[p])
-    const uint32_t idx = atomicAdd(&a.status[kStDeferred], 1u);
-    a.deferred[idx] = p;   // the list holds npub entries
+  if (m.overflow) {   // a later tier counts it (and writes offsets[p])
+    const uint32_t idx = atomicAdd(&a.status[RETRY ? kStWalked : kStDeferred], 1u);
+    a.deferred[(RETRY ? 2ull * a.npub : 0ull) + idx] = p;   // each list holds npub entries
     a.offsets[p] = 0;
     kc[0] = make_uint4(0, kDeferred, 0, 0);
+    fl = m.walk_ovf ? 2 : 3;
     return 0;
   }
   const uint32_t total = out_total<OUT>(m);
   a.offsets[p] = total;
   // key cache: total, nk, remote mask, up to two {record off, count}
-  // (3..8 keys: the keys in the spill slots, kc[1].y = their record total)
-  if (m.nk <= 2) {
+  // (3..8 keys: the keys in the spill slots, kc[1].y = their record total;
+  // many keys: kc[1] = {candidates, record total, the exact key's off, count})
+  if (many) {
+    kc[0] = make_uint4(total, kMany, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
+    kc[1] = make_uint4(m.nc, m.ksum, m.ex_off, m.ex_cnt);
+    fl = 1;
+  } else if (m.nk <= 2) {
     const uint2 k0 = m.nk > 0 ? s.ky(0) : make_uint2(0, 0);
     const uint2 k1 = m.nk > 1 ? s.ky(1) : make_uint2(0, m.ksum);
     const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
     kc[0] = make_uint4(total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
     kc[1] = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
-  } else if (spill) {
+  } else {
     kc[0] = make_uint4(total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
     kc[1] = make_uint4(0, m.ksum, 0, 0);
-  } else {
-    kc[0] = make_uint4(total, kRewalk, 0, 0);
   }
   return total;
+}
+
+// Appends the many-key publishes among a wave's groups (fl == 1 on a
+// group's lane 0) to EMIT's many-key list: one atomic per wave.
+template <int G>
+__device__ __forceinline__ void append_many(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t p) {
+  const uint64_t m_many = __ballot(g.lane == 0 && fl == 1);
+  if (!m_many) return;
+  uint32_t at = 0;
+  if (__lane_id() == 0) at = atomicAdd(&a.status[kStMany], (uint32_t)__popcll(m_many));
+  at = __shfl(at, 0, 64);
+  if (g.lane == 0 && fl == 1) a.deferred[a.npub + at + prefix_bits(m_many)] = p;
 }
 
 // ------------------------------------------------------------- EMIT pass
@@ -493,21 +587,23 @@ struct GroupMeta {
   uint4 pre0, pre1;                  // a one-record key's record, loaded during the resolve
 };
 
-// Resolve publish first + gidx of a wave: from the key cache, or by a
-// re-walk (> 8 keys).  Leaves the keys {off, cum start} in the group's LDS
-// key list; [obase, oend) is the publish's output range.  ok = false: the
-// wave tier writes it (or an error is latched).
+// Resolve publish first + gidx of a wave from the key cache (<= 2 keys) or
+// the spill slots (3..8 keys).  Leaves the keys {off, cum start} in the
+// group's LDS key list; [obase, oend) is the publish's output range.  Returns kResOk,
+// kResMany (many-key mode: written wave-wide by emit_many) or kResSkip (the
+// wave tier writes it, or an error is latched).
+enum : int { kResSkip = 0, kResOk = 1, kResMany = 2 };
+
 template <int G, int OUT>
-__device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
-                        uint32_t& nk, uint32_t& ksum, uint64_t& rmask, uint64_t obase, uint64_t oend) {
+__device__ int resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
+                       uint32_t& nk, uint32_t& ksum, uint64_t& rmask, uint64_t obase, uint64_t oend) {
   const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
   const uint4 h = kc[0];
   uint32_t total;
-  if (h.y == kDeferred) return false;   // written by the wave tier
-  if (h.y == kRewalk) {
-    const Matched m = walk_publish<G>(a, a.pubs[p], s, g);
-    if (m.overflow) return false;   // written by the wave tier
-    total = out_total<OUT>(m); nk = m.nk; ksum = m.ksum; rmask = m.rmask;
+  if (h.y == kDeferred) return kResSkip;   // written by the wave tier
+  const bool many = h.y == kMany;
+  if (many) {
+    total = h.x;
   } else {
     total = h.x; nk = h.y; rmask = ((uint64_t)h.w << 32) | h.z;
     const uint4 k = kc[1];
@@ -521,9 +617,101 @@ __device__ bool resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s,
     wave_sync();
   }
   const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
-  if (oend > cap) { if (g.lane == 0) atomicOr(a.err, kErrOverflow); return false; }
-  if (oend - obase != total) { if (g.lane == 0) atomicOr(a.err, kErrMismatch); return false; }
-  return true;
+  if (oend > cap) { if (g.lane == 0) atomicOr(a.err, kErrOverflow); return kResSkip; }
+  if (oend - obase != total) { if (g.lane == 0) atomicOr(a.err, kErrMismatch); return kResSkip; }
+  return many ? kResMany : kResOk;
+}
+
+// Many-key publish p (key cache kMany), written by the whole wave into
+// [ob, oe): its candidates' node records (match/4, match_/3 :283-303) give
+// the keys, 64 at a time (lookup_subs/1 :87-94), then the exact key, then the
+// remote nodes in node order (fold_/5 :78-84) — the order and totals COUNT
+// used.  Records mode copies each batch of keys' records with 64 lanes x U
+// in flight (the key of each record from a per-lane cursor over `kb`, a
+// 64-entry LDS buffer of {record off, cum start}).
+template <int OUT, bool NT, int U>
+__device__ void emit_many(const MatchArgs& a, uint32_t p, uint64_t ob, uint64_t oe, uint2* kb) {
+  const uint32_t lane = __lane_id();
+  const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+  const uint4 h = kc[0], k1 = kc[1];
+  const uint32_t nc = k1.x;
+  const uint64_t rmask = ((uint64_t)h.w << 32) | h.z;
+  const bool dollar = (a.pubs[p].flags & VMQG_PUB_DOLLAR) != 0;
+  // lane c < nc: candidate c; lane nc: the exact key
+  uint32_t nkeys = 0, key = 0, off0 = 0, cnt0 = 0;
+  if (lane < nc) {
+    const uint32_t path = reinterpret_cast<const uint32_t*>(a.keyspill)[(uint64_t)p * 2 * kSpillKeys + lane];
+    if (path < 2 * a.node_cap) {
+      const NodeRec r = a.nodes[path];
+      if ((r.meta & kNodeEmits) == kNodeEmits && !(dollar && (r.meta & kNodeDollarSkip))) {
+        nkeys = (r.meta >> 8) & 0xFFFFFFu;
+        key = r.key; off0 = r.off0; cnt0 = r.cnt0;
+      }
+    }
+  } else if (lane == nc && k1.w != 0) {
+    nkeys = 1; off0 = k1.z; cnt0 = k1.w;
+  }
+  const uint32_t kincl = wave_incl_scan32(nkeys);
+  const uint32_t K = __shfl(kincl, 63, 64);
+  const uint32_t kstart = kincl - nkeys;
+  uint64_t run = 0;
+  for (uint32_t k0 = 0; k0 < K; k0 += 64) {
+    const uint32_t ki = k0 + lane;
+    // the candidate owning key ki: the last c whose keys start at or before it
+    uint32_t c = 0;
+    for (uint32_t q = 1; q <= nc; q++) if (__shfl(kstart, q, 64) <= ki) c = q;
+    const uint32_t c_n = __shfl(nkeys, c, 64), c_key = __shfl(key, c, 64), c_ks = __shfl(kstart, c, 64);
+    const uint32_t c_off0 = __shfl(off0, c, 64), c_cnt0 = __shfl(cnt0, c, 64);
+    uint32_t off = 0, cnt = 0;
+    if (ki < K) {
+      if (c_n == 1) { off = c_off0; cnt = c_cnt0; }
+      else {
+        const uint32_t kid = a.keylist[c_key + (ki - c_ks)];
+        if (kid < a.key_cap) { const KeyDesc kd = a.keydesc[kid]; off = kd.off; cnt = kd.count; }
+      }
+    }
+    if (OUT == 1) {
+      const uint64_t mb = __ballot(cnt != 0);
+      if (cnt != 0 && ob + run + prefix_bits(mb) < oe) store_range(a.out_rng, ob + run + prefix_bits(mb), off, cnt);
+      run += (uint32_t)__popcll(mb);
+      continue;
+    }
+    const uint32_t incl = wave_incl_scan32(cnt);
+    const uint32_t tot = __shfl(incl, 63, 64);
+    const uint32_t nb = K - k0 < 64u ? K - k0 : 64u;
+    kb[lane] = make_uint2(off, incl - cnt);
+    wave_sync();
+    uint32_t j = 0;
+    for (uint32_t r0 = lane; r0 < tot; r0 += 64 * U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t r = r0 + 64 * u;
+        if (r < tot) {
+          while (j + 1 < nb && kb[j + 1].y <= r) j++;
+          const uint2 kk = kb[j];
+          v[u] = *reinterpret_cast<const uint4*>(a.records + kk.x + (r - kk.y));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t r = r0 + 64 * u;
+        if (r < tot && ob + run + r < oe) store_rec<NT>(a.out, ob + run + r, v[u]);
+      }
+    }
+    run += tot;
+    wave_sync();
+  }
+  // remote nodes < 64 (COUNT already dropped the local node)
+  const uint32_t nrem = (uint32_t)__popcll(rmask);
+  for (uint32_t j = lane; j < nrem; j += 64) {
+    const uint32_t node = select_bit(rmask, j);
+    if (ob + run + j >= oe) break;
+    if (OUT == 0) store_rec<NT>(a.out, ob + run + j, make_uint4((VMQG_EMIT_REMOTE << 24) | node, kNone, kNone, kNone));
+    else store_range(a.out_rng, ob + run + j, node, 0u);
+  }
+  run += nrem;
+  if (lane == 0 && run != oe - ob) atomicOr(a.err, kErrMismatch);
 }
 
 // Output ranges of the GPW publishes [first, first + n) of one chunk: the
@@ -561,28 +749,31 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
   const uint64_t wbase = PRE ? pre_wbase : chunk_offsets<G, GPW>(a, first, n, g, obase, oend);
   uint32_t nk = 0, ksum = 0;
   uint64_t rmask = 0;
-  bool ok = false;
-  if (valid) ok = resolve<G, 0>(a, p, s, g, nk, ksum, rmask, obase, oend);
+  int res = kResSkip;
+  if (valid) res = resolve<G, 0>(a, p, s, g, nk, ksum, rmask, obase, oend);
+  const bool ok = res == kResOk;   // many-key publishes: the EMIT wave-tier launch writes them
   // key-cache groups (<= 2 keys) copy from {off0, c0, off1} directly; the
   // record of a one-record key (a publish's own exact subscriber, say) is
   // loaded now, by every group at once, instead of as a lone HBM miss in
-  // the middle of the copy
+  // the middle of the copy (key 0's by lane 0, key 1's by lane 1, or by
+  // lane 0 too when a group is one lane)
+  constexpr uint32_t kPre1Lane = G > 1 ? 1u : 0u;
   uint32_t off0 = 0, off1 = 0, c0 = 0;
-  uint4 pre = make_uint4(0, 0, 0, 0);
+  uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = make_uint4(0, 0, 0, 0);
   if (ok && nk <= 2) {
     const uint2 k0 = s.ky(0), k1 = s.ky(1);
     off0 = k0.x;
     off1 = k1.x;
     c0 = nk >= 2 ? k1.y : ksum;
-    if (g.lane == 0 && nk >= 1 && c0 == 1) pre = *reinterpret_cast<const uint4*>(a.records + off0);
-    if (g.lane == 1 && nk == 2 && ksum - c0 == 1) pre = *reinterpret_cast<const uint4*>(a.records + off1);
+    if (g.lane == 0 && nk >= 1 && c0 == 1) pre0 = *reinterpret_cast<const uint4*>(a.records + off0);
+    if (g.lane == kPre1Lane && nk == 2 && ksum - c0 == 1) pre1 = *reinterpret_cast<const uint4*>(a.records + off1);
   }
   if (g.lane == 0)
     gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : 0u, ok ? (uint32_t)(oend - obase) : 0u,
                            nk == 0 ? 1 : nk, ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), 0u, c0,
-                           off0, off1, 0u, 0u, pre, make_uint4(0, 0, 0, 0)};
+                           off0, off1, 0u, 0u, pre0, make_uint4(0, 0, 0, 0)};
   wave_sync();
-  if (g.lane == 1) gm[g.gidx].pre1 = pre;
+  if (g.lane == kPre1Lane) gm[g.gidx].pre1 = pre1;
   // compact the copied ranges: crel = exclusive scan of the ok spans
   const uint32_t lane = __lane_id();
   const uint32_t sp = lane < (uint32_t)GPW ? gm[lane].span : 0u;
@@ -628,11 +819,12 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
 // Range mode: each group writes its publish's non-empty keys as
 // {record off, count}, then its remote nodes as {node, 0}.
 template <int G>
-__device__ void emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
-                                  uint64_t obase, uint64_t oend) {
+__device__ int emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
+                                 uint64_t obase, uint64_t oend) {
   uint32_t nk = 0, ksum = 0;
   uint64_t rmask = 0;
-  if (!resolve<G, 1>(a, p, s, g, nk, ksum, rmask, obase, oend)) return;
+  const int res = resolve<G, 1>(a, p, s, g, nk, ksum, rmask, obase, oend);
+  if (res != kResOk) return res;   // many-key publishes: the EMIT wave-tier launch
   uint32_t pos = 0;
   for (uint32_t k0 = 0; k0 < nk; k0 += G) {
     const uint32_t ki = k0 + g.lane;
@@ -649,6 +841,7 @@ __device__ void emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScra
   }
   const uint32_t nrem = (uint32_t)__popcll(rmask);
   for (uint32_t j = g.lane; j < nrem; j += G) store_range(a.out_rng, obase + pos + j, select_bit(rmask, j), 0u);
+  return res;
 }
 
 // --------------------------------------------------------------- kernels
@@ -668,13 +861,17 @@ __device__ __forceinline__ void chunk_positions64(const MatchArgs& a, uint32_t f
 
 template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
 #ifndef VMQG_COUNT_WPE
-#define VMQG_COUNT_WPE 4   // COUNT waves per SIMD the register budget must allow (A/B: 4, 5)
+#define VMQG_COUNT_WPE 4    // COUNT waves per SIMD the register budget must allow, 2+ lanes per publish (A/B: 4, 5)
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? VMQG_COUNT_WPE : 4)))
+#ifndef VMQG_COUNT_WPE1
+#define VMQG_COUNT_WPE1 5   // ... one lane per publish (96 VGPRs, no spills)
+#endif
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(MODE == 0 ? (G == 1 ? VMQG_COUNT_WPE1 : VMQG_COUNT_WPE) : 4)))
 void k_match_fast(MatchArgs a) {
   using FS = FastScratch<G>;
   constexpr int GPW = FS::GPW;
-  if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < 4) a.status_next[threadIdx.x] = 0;
+  if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < kStWords) a.status_next[threadIdx.x] = 0;
   __shared__ uint2 st[FS::SC * FS::SLOTS];
   __shared__ uint32_t cd[FS::CC * FS::SLOTS];
   __shared__ uint2 ky[FS::KC * FS::SLOTS];
@@ -713,10 +910,15 @@ void k_match_fast(MatchArgs a) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
     if (MODE == 0) {
       uint64_t c = 0;
-      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g);
+      uint32_t fl = 0;
+      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl);
       // the chunk's total (publishes the wave tier takes add theirs later)
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
+      // many-key publishes go to EMIT's wave-tier list, one atomic per wave and kind
+      append_many<G>(a, g, fl, base + g.gidx);
+      const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
+      if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
     } else if (OUT == 0) {
       emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
     } else {
@@ -933,52 +1135,112 @@ struct WaveWalk {
   }
 };
 
-// Wave tier: one publish per wave, from the fast tier's deferred list.  The
-// frontier stack is in LDS; a publish that outgrows it is walked again with
-// the wave's stack in global scratch (o_cap entries, sized from the trie
-// depth so it cannot overflow).  EMIT re-walks in the same order and checks
-// the count.
+// One publish walked by the whole wave: the frontier stack in LDS, and if it
+// outgrows it, walked again with the wave's stack in global scratch (o_cap
+// entries, sized from the trie depth so it cannot overflow).  COUNT writes
+// offsets[p] and adds to the chunk total; EMIT re-walks in the same order,
+// writes [ob, oe) and checks the count.
+template <int MODE, int OUT, bool NT>
+__device__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p, uint64_t ob, uint64_t oe) {
+  const uint32_t lane = __lane_id();
+  WaveWalk<MODE, OUT, NT> w1(a, W, W.stack, kWStack, ob);
+  bool ok = w1.run_publish(p);
+  uint64_t total = w1.run;
+  if (!ok) {
+    if (MODE == 0 && lane == 0) atomicAdd(&a.status[kStTier2], 1u);
+    WaveWalk<MODE, OUT, NT> w2(a, W, gstack, a.o_cap, ob);
+    ok = w2.run_publish(p);
+    total = w2.run;
+    if (!ok && lane == 0) atomicOr(a.err, kErrFrontier);
+  }
+  if (ok && lane == 0) {
+    if (MODE == 0) {
+      a.offsets[p] = total;
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)total);
+    } else if (total != oe - ob) {
+      atomicOr(a.err, kErrMismatch);
+    } else {
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWaveEnt), (unsigned long long)total);
+    }
+  }
+  wave_sync();
+}
+
+// Wave tiers, one launch after each fast pass (each reads its list lengths
+// on the device and exits at once when they are empty).
+//
+// COUNT: the publishes the fast pass deferred (list 0) are retried four
+// lanes per publish (16 per wave, lists 4x the one-lane pass's: a deep
+// multi-wildcard walk fits); a publish served there gets its key cache as in
+// the fast pass and its count added to its chunk's total.  What overflows
+// even those lists is walked by the whole wave at once (and listed for
+// EMIT: list 2).  With fast_g 4 the fast pass already had these lists: its
+// deferrals go straight to the whole-wave walk.
+//
+// EMIT: the whole-wave walks again (list 2), then the many-key publishes
+// (list 1), expanded from their candidates with no walk.
 template <int MODE, int OUT, bool NT>
 __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
   __shared__ WaveLds lds[kWaves];
   const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
-  uint2* gstack = a.o_stack + gw * a.o_cap;
-  // the fast tier's deferred list, and in EMIT the publishes its key cache
-  // could not serve (written by the fast tier's launches)
-  const uint32_t n1 = a.status[kStDeferred];
-  const uint32_t n = n1 + (MODE == 1 ? a.status[kStRewalk] : 0u);
   const uint32_t nwaves = gridDim.x * kWaves;
-  for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
-    const uint32_t p = d < n1 ? a.deferred[d] : a.deferred[a.npub + (d - n1)];
-    uint64_t ob = 0, oe = 0;
-    if (MODE == 1) {
-      ob = a.offsets[p];
-      oe = a.offsets[p + 1];
+  uint2* gstack = a.o_stack + gw * a.o_cap;
+  if constexpr (MODE == 0) {
+    using FS = FastScratch<4>;
+    constexpr uint32_t GPW = FS::GPW;
+    __shared__ uint2 st[FS::SC * FS::SLOTS];
+    __shared__ uint32_t cd[FS::CC * FS::SLOTS];
+    __shared__ uint2 ky[FS::KC * FS::SLOTS];
+    const Group<4> g;
+    const FS s{st, cd, ky, wv * GPW + g.gidx};
+    const bool retry = a.fast_g != 4;
+    const uint32_t nd = a.status[kStDeferred];
+    for (uint32_t base = (uint32_t)gw * GPW; base < nd; base += nwaves * GPW) {
+      const uint32_t i = base + g.gidx;
+      const bool valid = i < nd;
+      const uint32_t p = valid ? a.deferred[i] : 0u;
+      uint32_t fl = 2, c = 0;
+      if (retry && valid) {
+        c = count_publish<4, OUT, true>(a, p, s, g, fl);
+        if (g.lane == 0 && fl <= 1)
+          atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)c);
+      }
+      wave_sync();
+      if (retry) append_many<4>(a, g, fl, p);
+      // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
+      uint64_t ov = __ballot(valid && g.lane == 0 && fl >= 2);
+      if (!retry && ov) {   // list 2 for EMIT (the retry's count_publish listed its own)
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(&a.status[kStWalked], (uint32_t)__popcll(ov));
+        at = __shfl(at, 0, 64);
+        if (valid && g.lane == 0) a.deferred[2ull * a.npub + at + prefix_bits(ov)] = p;
+      }
+      while (ov) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(ov);
+        ov &= ov - 1;
+        wave_publish<0, OUT, NT>(a, lds[wv], gstack, __shfl(p, l, 64), 0, 0);
+      }
+    }
+    return;
+  } else {
+    const uint32_t n2 = a.status[kStWalked];
+    const uint32_t n = n2 + a.status[kStMany];
+    for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
+      const uint32_t p = d < n2 ? a.deferred[2ull * a.npub + d] : a.deferred[a.npub + (d - n2)];
+      const uint64_t ob = a.offsets[p], oe = a.offsets[p + 1];
       if (oe > (OUT ? a.rng_cap : a.out_cap)) {
         if (lane == 0) atomicOr(a.err, kErrOverflow);
         continue;
       }
-    }
-    WaveWalk<MODE, OUT, NT> w1(a, lds[wv], lds[wv].stack, kWStack, ob);
-    bool ok = w1.run_publish(p);
-    uint64_t total = w1.run;
-    if (!ok) {
-      if (MODE == 0 && lane == 0) atomicAdd(&a.status[kStTier2], 1u);
-      WaveWalk<MODE, OUT, NT> w2(a, lds[wv], gstack, a.o_cap, ob);
-      ok = w2.run_publish(p);
-      total = w2.run;
-      if (!ok && lane == 0) atomicOr(a.err, kErrFrontier);
-    }
-    if (ok && lane == 0) {
-      if (MODE == 0) {
-        a.offsets[p] = total;
-        atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)total);
-      } else if (total != oe - ob) {
-        atomicOr(a.err, kErrMismatch);
+      if (d >= n2) {   // counted by a fast tier: expand its candidates, no walk
+        emit_many<OUT, NT, 8>(a, p, ob, oe, lds[wv].keys);
+        if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWaveEnt), (unsigned long long)(oe - ob));
+        wave_sync();
+        continue;
       }
+      wave_publish<1, OUT, NT>(a, lds[wv], gstack, p, ob, oe);
     }
-    wave_sync();
   }
 }
 
@@ -1050,10 +1312,11 @@ __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uin
 // ---------------------------------------------------------------- launch
 static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-hipError_t launch_scan(const MatchArgs& a, hipStream_t st) {
+hipError_t launch_scan(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   uint32_t g = scan_tiles((a.npub + a.gpw - 1) / a.gpw);
   if (g > 2048) g = 2048;
-  k_scan_offsets<<<g, kScanBlock, 0, st>>>(a);
+  if (t0) hipExtLaunchKernelGGL(k_scan_offsets, dim3(g), dim3(kScanBlock), 0, st, t0, t1, 0, a);
+  else k_scan_offsets<<<g, kScanBlock, 0, st>>>(a);
   return hipGetLastError();
 }
 
@@ -1082,10 +1345,16 @@ static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st,
   }
 }
 
+template <int MODE, int OUT, bool NT>
+static void launch_wave_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  if (t0) hipExtLaunchKernelGGL(k_match_wave<MODE, OUT, NT>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+  else k_match_wave<MODE, OUT, NT><<<g, 256, 0, st>>>(a);
+}
+
 template <int MODE, int OUT>
-static void launch_wave(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st) {
-  if (nt) k_match_wave<MODE, OUT, true><<<g, 256, 0, st>>>(a);
-  else k_match_wave<MODE, OUT, false><<<g, 256, 0, st>>>(a);
+static void launch_wave(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  if (nt) launch_wave_k<MODE, OUT, true>(a, g, st, t0, t1);
+  else launch_wave_k<MODE, OUT, false>(a, g, st, t0, t1);
 }
 
 hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
@@ -1107,8 +1376,8 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, 
     // reads its list length on the device (exits at once when empty); one
     // wave per deferred publish, each wave with its own global stack
     const uint32_t g = a.o_waves / kWaves;
-    if (mode == 0) { if (out) launch_wave<0, 1>(a, g, nt, st); else launch_wave<0, 0>(a, g, nt, st); }
-    else { if (out) launch_wave<1, 1>(a, g, nt, st); else launch_wave<1, 0>(a, g, nt, st); }
+    if (mode == 0) { if (out) launch_wave<0, 1>(a, g, nt, st, t0, t1); else launch_wave<0, 0>(a, g, nt, st, t0, t1); }
+    else { if (out) launch_wave<1, 1>(a, g, nt, st, t0, t1); else launch_wave<1, 0>(a, g, nt, st, t0, t1); }
   }
   return hipGetLastError();
 }

@@ -4,6 +4,7 @@
 #include <string>
 
 #include "vmqr_engine.h"
+#include "vmqg_chain.h"
 #include "vmqg_nullorder.h"
 
 using vmqr::RetainEngine;
@@ -82,6 +83,13 @@ int vmqr_match_device(vmqr_ctx* ctx, const vmqg_pub* d_filters, uint32_t n, cons
   hipSetDevice(ctx->e.device);
   return ctx->e.match_device(d_filters, n, d_words, d_out, out_cap, d_offsets, vmqg::caller_stream(stream));
   GUARD_END
+}
+
+int vmqr_release_stream(vmqr_ctx* ctx, void* stream) {
+  if (!ctx) return VMQG_E_INVAL;
+  if (!ctx->e.ev_match_done) return VMQG_OK;
+  hipSetDevice(ctx->e.device);
+  return vmqg::chain_release(ctx->e.ev_match_done, ctx->e.ev_stream, vmqg::caller_stream(stream));
 }
 
 int vmqr_match_status(vmqr_ctx* ctx, void* stream) {

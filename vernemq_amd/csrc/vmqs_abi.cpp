@@ -193,6 +193,13 @@ int vmqs_select_device(vmqs_ctx* ctx, const vmqg_emit* d_emits, const uint64_t* 
   GUARD_END
 }
 
+int vmqs_release_stream(vmqs_ctx* ctx, void* stream) {
+  if (!ctx) return VMQG_E_INVAL;
+  if (!ctx->e.ev_sel) return VMQG_OK;
+  hipSetDevice(ctx->e.device);
+  return vmqg::chain_release(ctx->e.ev_sel, ctx->e.sel_stream, vmqg::caller_stream(stream));
+}
+
 int vmqs_select_status(vmqs_ctx* ctx, void* stream) {
   if (!ctx) return VMQG_E_INVAL;
   GUARD_BEGIN

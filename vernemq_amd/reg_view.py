@@ -240,10 +240,22 @@ class RegGpuView:
             _lib.check(rc, "vmqg_match_ranges")
             return out[: n.value], offs
 
-    def records(self) -> np.ndarray:
-        """Host view (copy) of the record table that ranges index (vmqg_records)."""
+    def epoch(self) -> int:
+        """The table epoch a match queued now sees (vmqg_epoch)."""
+        e = ctypes.c_uint64()
+        _lib.check(self._L.vmqg_epoch(self._h, ctypes.byref(e)), "vmqg_epoch")
+        return e.value
+
+    def records(self, epoch: int | None = None) -> np.ndarray:
+        """Host view (copy) of the record table that ranges index
+        (vmqg_records); with `epoch`, the table for range results of that
+        epoch (vmqg_records_at: raises VmqgError E_STATE when a later apply
+        rewrote record slots)."""
         p, n = ctypes.c_void_p(), ctypes.c_uint64()
-        _lib.check(self._L.vmqg_records(self._h, ctypes.byref(p), ctypes.byref(n)), "vmqg_records")
+        if epoch is None:
+            _lib.check(self._L.vmqg_records(self._h, ctypes.byref(p), ctypes.byref(n)), "vmqg_records")
+        else:
+            _lib.check(self._L.vmqg_records_at(self._h, epoch, ctypes.byref(p), ctypes.byref(n)), "vmqg_records_at")
         if not n.value:
             return np.zeros(0, dtype=EMIT_DTYPE)
         buf = (ctypes.c_uint8 * (n.value * 16)).from_address(p.value)
@@ -302,6 +314,10 @@ class RegGpuView:
     def match_status(self, stream: int = 0) -> int:
         return self._L.vmqg_match_status(self._h, stream or None)
 
+    def release_stream(self, stream: int):
+        """Before destroying a stream passed to this view (vmqg_release_stream)."""
+        _lib.check(self._L.vmqg_release_stream(self._h, stream or None), "vmqg_release_stream")
+
     def set_option(self, name: str, value: int):
         """Kernel tuning knob (vmqg_set_option): "fast_g" 1|2|4, "nt_stores" 0|1, "count_bpc" / "emit_bpc"."""
         _lib.check(self._L.vmqg_set_option(self._h, name.encode(), int(value)), "vmqg_set_option")
@@ -314,6 +330,17 @@ class RegGpuView:
         _lib.check(self._L.vmqg_kernel_times(self._h, ctypes.byref(c), ctypes.byref(e), ctypes.byref(n)),
                    "vmqg_kernel_times")
         return c.value, e.value, n.value
+
+    STAGES = ("count", "count_wave", "scan", "emit", "emit_wave")
+
+    def stage_times(self) -> dict:
+        """Average ns per launch of all five kernels of a match call
+        (vmqg_kernel_times_ex), keyed by STAGES, plus "launches"."""
+        ns, n = (ctypes.c_double * len(self.STAGES))(), ctypes.c_uint64()
+        _lib.check(self._L.vmqg_kernel_times_ex(self._h, ns, ctypes.byref(n)), "vmqg_kernel_times_ex")
+        out = {k: ns[i] for i, k in enumerate(self.STAGES)}
+        out["launches"] = n.value
+        return out
 
     # ------------------------------------------------------------ replication
     def arena(self):
