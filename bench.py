@@ -101,8 +101,7 @@ def main():
     ap.add_argument("--rt-heavy", type=int, default=16, help="RT: devices/+/telemetry/{m} filters per step")
     ap.add_argument("--e-scale", type=float, default=1.0, help="config E scale (1.0 = 50M subs)")
     ap.add_argument("--fast-g", type=int, default=None,
-                    help="vmqg option fast_g for the secondary configs (default: the library's 1; 2 for E, "
-                         "whose publishes match 5-8 keys: the one-lane COUNT defers them, profiles/ab_r02_count_one_lane_e.json)")
+                    help="vmqg option fast_g for the secondary configs (A/B only; default: the library's own, 1)")
     ap.add_argument("--r-n", type=int, default=1_000_000, help="R1 / R2: N (the reference suite goes to 4,096,000)")
     ap.add_argument("--d-scale", type=float, default=1.0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N>1 on one GPU")
@@ -379,7 +378,7 @@ def main():
             "verified_counts": verified,
             "kernel_us": stages,
             "served": {"deferred": served["deferred_tier1"], "retried": served["retried"], "many_key": served["many_key"],
-                       "wave_entries": served["wave_entries"]},
+                       "wave_entries": served["wave_entries"], "wide_entries": served["wide_entries"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
                          "kernel": "k_match_fast<1,0,2,true,64> (EMIT)",
@@ -444,7 +443,7 @@ def bench_other(args):
 
     w.load_into(view, progress=progress)
     load_s = time.time() - t0
-    fast_g = args.fast_g or (2 if args.config == "E" else None)
+    fast_g = args.fast_g
     if fast_g:
         view.set_option("fast_g", fast_g)
     st = view.stats_raw()
@@ -585,7 +584,7 @@ def bench_other(args):
         "arena_bytes": st["device_bytes"], "trie_edges": st["trie_edges"], "paths": st["paths"],
         "rebuilds": st["rebuilds"], "deferred": [st["deferred_tier1"], st["deferred_tier2"]],
         "served": {"deferred": st["deferred_tier1"], "retried": st["retried"],
-                   "many_key": st["many_key"], "wave_entries": st["wave_entries"]},
+                   "many_key": st["many_key"], "wave_entries": st["wave_entries"], "wide_entries": st["wide_entries"]},
         "build_id": _lib.build_id()}), flush=True)
 
 
@@ -808,20 +807,23 @@ def bench_d(args):
         ops_n = st1["ops_applied"] - st0["ops_applied"]
         wait_ns = st1["apply_wait_ns"] - st0["apply_wait_ns"]
         host_ns = st1["apply_host_ns"] - st0["apply_host_ns"] - wait_ns   # host work, without GPU back-pressure
-        # Each EMIT launch is charged only the records it writes: the fast
-        # tier writes every publish's records except those of the publishes
-        # the wave-tier launch writes (deferred ones and many-key $share
-        # publishes, counted on the device: stats wave_entries).  Compulsory
-        # HBM bytes = 16 B written per record (the records read are the 16 MB
-        # of $share member lists and the exact keys' records, largely
-        # cache-resident); SURVEY §8(d)'s 32 B per emission is reported
-        # beside it.  The roofline line is the longer of the two launches.
+        # Each EMIT launch is charged only the records it writes (counted on
+        # the device): the fast EMIT launch writes every publish's records —
+        # the ordinary ones in its chunk pass, the wide ones ($share groups
+        # on 4 nodes: 40 keys; alarm lists: 1,000 records) in its second,
+        # XCD-labelled phase (stats wide_entries) — except those of the
+        # whole-wave walks, which the wave-tier launch writes (stats
+        # wave_entries).  Compulsory HBM bytes = 16 B written per record (the
+        # records read are the 16 MB of $share member lists, the 16 MB of
+        # alarm lists and the exact keys' records, cache-resident when their
+        # publishes share an XCD); SURVEY §8(d)'s 32 B per emission is
+        # reported beside it.  The roofline line is the longer launch.
         wave_rec = int(st1["wave_entries"])
         fast_rec = emitted - wave_rec
         per_kernel = {
-            "emit": {"kernel": "k_match_fast<1,0,2,true,64> (EMIT fast tier)", "records": fast_rec,
-                     "bytes": 16 * fast_rec, "us": stages["emit"]},
-            "emit_wave": {"kernel": "k_match_wave<1,0,true> (EMIT wave tier: many-key + deferred publishes)",
+            "emit": {"kernel": "k_match_fast<1,0,2,true,64> (EMIT fast tier + wide phase)", "records": fast_rec,
+                     "wide_records": int(st1["wide_entries"]), "bytes": 16 * fast_rec, "us": stages["emit"]},
+            "emit_wave": {"kernel": "k_match_wave<1,0,true> (EMIT wave tier: whole-wave walks)",
                           "records": wave_rec, "bytes": 16 * wave_rec, "us": stages["emit_wave"]},
         }
         for v in per_kernel.values():
@@ -862,7 +864,7 @@ def bench_d(args):
             "verified": {"known_answer": known, "replicas_equal": replicas_equal, "images_equal": images_equal},
             "kernel_us": stages,
             "served": {"deferred": st1["deferred_tier1"], "retried": st1["retried"],
-                       "many_key": st1["many_key"], "wave_entries": wave_rec},
+                       "many_key": st1["many_key"], "wave_entries": wave_rec, "wide_entries": st1["wide_entries"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS if achieved else None,
                          "traffic": load_pmc_traffic("k_match_fast<1" if dom_key == "emit" else "k_match_wave<1",

@@ -140,13 +140,15 @@ typedef struct vmqg_stats_s {
   uint64_t image_bytes;     /*   full-image bytes shipped (re-layouts)           */
   uint64_t max_depth;       /* deepest trie path (levels)                       */
   /* ABI 3: how the last checked match batch was served                        */
-  uint64_t many_key;        /* publishes with more keys than the fast tier's    */
-                            /* lists, expanded wave-wide by EMIT (no deferral)  */
+  uint64_t many_key;        /* wide publishes: more keys than the fast tier's   */
+                            /* lists or >= 256 records, written wave-wide by    */
+                            /* the fast EMIT launch's second phase (no walk)    */
   uint64_t retried;         /* publishes the one-lane fast pass could not hold, */
                             /* retried four lanes per publish (the rest of them */
                             /* are the deferred_tier1 walks)                    */
   uint64_t wave_entries;    /* entries (records or ranges) written by the EMIT  */
-                            /* wave-tier launch (deferred + many-key publishes) */
+                            /* wave-tier launch (the whole-wave walks)          */
+  uint64_t wide_entries;    /* entries written by the wide phase                */
 } vmqg_stats_t;
 
 /* ---- lifecycle ------------------------------------------------------- */

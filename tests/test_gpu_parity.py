@@ -789,3 +789,39 @@ def test_released_stream_can_be_destroyed():
         v.match_device(d_pubs.data_ptr(), len(pubs), d_words.data_ptr(), d_out.data_ptr(), cap, d_offs.data_ptr(), 0)
         assert v.match_status(0) == 0
         assert np.array_equal(d_offs.cpu().numpy().astype(np.uint64), ref_offs), rep
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("fast_g", [1, 2])
+def test_wide_publishes_by_record_count(mode, fast_g):
+    """Publishes of one or two keys but hundreds of records (a/+ with 300
+    subscribers, plus an exact one) are wide: written wave-wide by the fast
+    EMIT launch's second phase from the wide list of their XCD label, in
+    batches that mix them with one-record publishes and with publishes of
+    several hundred records under other keys."""
+    node = "n@h"
+    prod = _driver(node, mode)
+    prod.view.set_option("fast_g", fast_g)
+    orc = O.TrieOracle(node)
+    sub = lambda cid, t, q: ("updated", ("", cid), None, [(node, True, [(t, q)])])
+    evs = [sub(b"a%d" % i, (b"a", b"+"), i % 3) for i in range(300)]
+    evs += [sub(b"b%d" % i, (b"b", b"#"), 1) for i in range(255)]              # just below the threshold
+    evs += [sub(b"c%d" % i, (b"c", b"+", b"x"), 2) for i in range(700)]
+    evs += [sub(b"ax%d" % j, (b"a", b"%d" % j), 0) for j in range(0, 40, 2)]
+    evs += [sub(b"o%d" % j, (b"o", b"%d" % j), 0) for j in range(40)]
+    prod.apply(evs)
+    orc.apply(evs)
+    kinds = [("", (p, b"%d" % j)) for p in (b"a", b"b", b"o") for j in range(40)] + \
+            [("", (b"c", b"%d" % j, b"x")) for j in range(8)]
+    want = orc.fold_batch([(mp, b"pub", t) for mp, t in kinds])
+    v = prod.view
+    arr, words = v.prepare(kinds)
+    idx = np.random.RandomState(9).randint(0, len(kinds), size=12_000)
+    recs, offs = prod.match_arrays(arr[idx], words)
+    st = v.stats_raw()
+    assert st["many_key"] > 0 and st["deferred_tier1"] == 0, st
+    counts = np.diff(offs.astype(np.int64))
+    assert np.array_equal(counts, np.array([len(x) for x in want], dtype=np.int64)[idx])
+    for i in range(0, len(idx), 5):
+        got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
+        assert got == sorted(want[idx[i]]), (i, kinds[idx[i]])

@@ -21,7 +21,7 @@ for step in "$@"; do
     cat $O/bench_C.json
     timeout -k 10 400 python3 bench.py --config D --no-cpu-baseline > $O/bench_D.json 2> $O/bench_D.err || { tail -20 $O/bench_D.err; exit 5; }
     cat $O/bench_D.json
-    timeout -k 10 500 python3 bench.py --config E --fast-g 1 --no-cpu-baseline > $O/bench_E.json 2> $O/bench_E.err || { tail -20 $O/bench_E.err; exit 6; }
+    timeout -k 10 500 python3 bench.py --config E --no-cpu-baseline > $O/bench_E.json 2> $O/bench_E.err || { tail -20 $O/bench_E.err; exit 6; }
     cat $O/bench_E.json ;;
   profc)
     TAG=${T}_C OUT=$O/profc bash tools/profile_session.sh > $O/profc.log 2>&1 || { tail -20 $O/profc.log; exit 7; }

@@ -258,6 +258,7 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->many_key = e.last_many;
   out->retried = e.last_retried;
   out->wave_entries = e.last_wave_entries;
+  out->wide_entries = e.last_wide_entries;
   return VMQG_OK;
 }
 

@@ -943,7 +943,8 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     // 32-B key cache + kSpillKeys x 8-B spilled keys per publish, then the
     // chunk totals (one per 16 or 32 publishes, + 1)
     if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + (cap / 16 + 2) * 8) != hipSuccess) return VMQG_E_NOMEM;
-    if (hipMalloc(&d_deferred, 3 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;   // three lists
+    // publish lists: retry, whole-wave walks, eight wide lists (vmqg_kernels.hip kLists)
+    if (hipMalloc(&d_deferred, 10 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
     keycache_cap = cap;
     deferred_cap = cap;
   }
@@ -1058,10 +1059,12 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
 
 // Status words: two sets of per-call counters (kStatusSet words each: [0]
 // publishes the fast pass deferred to the 4-lane retry, [1] whole-wave walks
-// with a global stack, [2] scan ticket, [3] whole-wave walks, [4] many-key
-// publishes, [5] fast-pass deferrals by a walk overflow, [6..7] entries the
-// EMIT wave-tier launch wrote) used by alternate calls, then the error bits
-// latched since the previous vmqg_match_status.
+// with a global stack, [2] scan ticket, [3] whole-wave walks, [4] wide
+// publishes, [5] fast-pass deferrals by a walk overflow, [6..7] entries
+// written by the EMIT wave tier, [8..15] wide publishes per XCD label,
+// [16..23] their tickets, [24..25] entries written by the wide phase) used by
+// alternate calls, then the error bits latched since the previous
+// vmqg_match_status.
 int Engine::match_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
   hipSetDevice(device);
@@ -1077,6 +1080,7 @@ int Engine::match_status(hipStream_t st) {
   last_retried = c[0];
   last_many = c[4];
   last_wave_entries = (uint64_t)c[6] | ((uint64_t)c[7] << 32);
+  last_wide_entries = (uint64_t)c[24] | ((uint64_t)c[25] << 32);
   const uint32_t err = h[2 * kStatusSet];
   if (err & 2u) return VMQG_E_FRONTIER;
   if (err & 4u) return VMQG_E_OVERFLOW;

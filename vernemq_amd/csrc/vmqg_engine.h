@@ -229,13 +229,14 @@ struct Engine {
   int cu_count = 0;
   uint32_t last_deferred[2] = {0, 0};   // whole-wave walks (LDS / global stack) of the last checked batch
   uint32_t last_many = 0, last_retried = 0;    // ... many-key publishes / retried four lanes per publish
-  uint64_t last_wave_entries = 0;              // ... entries (records or ranges) the wave tier wrote
+  uint64_t last_wave_entries = 0;              // ... entries (records or ranges) the EMIT wave tier wrote
+  uint64_t last_wide_entries = 0;              // ... entries the fast EMIT's wide phase wrote
   // epoch of the last apply that rewrote a record slot (or re-laid out the
   // arena): range results of an older epoch index records that may have
   // changed (vmqg_records_at refuses them)
   uint64_t rec_epoch = 0;
   // device status: two per-call counter sets of kStatusSet words, then the sticky error word
-  static constexpr uint32_t kStatusSet = 8, kStatusBytes = 128;
+  static constexpr uint32_t kStatusSet = 32, kStatusBytes = 512;
   // per-launch timing: COUNT fast tier, COUNT wave tier, scan, EMIT fast tier, EMIT wave tier
   static constexpr int kTimedStages = 5;
   std::vector<std::array<hipEvent_t, 2 * kTimedStages>> t_ev;

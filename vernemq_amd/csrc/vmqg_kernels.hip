@@ -60,12 +60,19 @@ constexpr uint32_t kMany = 0xFFFFFFFDu;     // key cache: more keys than the lis
 // call's first kernel zeroes the set of the call after it, so no reset
 // launch is needed) and the sticky error word (a.err, cleared only by
 // vmqg_match_status).
-// Deferral lists (a.deferred, 3 x npub entries): [0, npub) publishes the
+// Publish lists (a.deferred, kLists x npub entries): [0, npub) publishes the
 // fast pass could not hold (retried four lanes per publish by the COUNT
-// wave-tier launch), [npub, 2 npub) many-key publishes (written by the EMIT
-// wave-tier launch), [2 npub, 3 npub) publishes walked by a whole wave.
+// wave-tier launch), [npub, 2 npub) publishes walked by a whole wave, then
+// eight lists of wide publishes (many keys, or >= kWideRecords records),
+// one per XCD label, written wave-wide by the second phase of the fast EMIT.
+constexpr uint32_t kXcds = 8, kLists = 2 + kXcds;
 enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, kStMany = 4, kStWalkOvf = 5,
-                  kStWaveEnt = 6 /* u64: entries the EMIT wave-tier launch wrote */, kStWords = 8 };
+                  kStWaveEnt = 6 /* u64: entries written by the EMIT wave tier (whole-wave walks) */,
+                  kStWideCount = 8 /* [8, 16): per XCD label */, kStWideTicket = 16 /* [16, 24) */,
+                  kStWideEnt = 24 /* u64: entries written by the wide phase */, kStWords = 32 };
+#ifndef VMQG_WIDE_RECORDS
+#define VMQG_WIDE_RECORDS 256   // publishes with at least this many records are written by the wide phase
+#endif
 enum : uint32_t { kErrFrontier = 2u, kErrOverflow = 4u, kErrMismatch = 8u };   // kErrLookback = 16 (lookback.h)
 
 __device__ __forceinline__ uint32_t prefix_bits(uint64_t m) {
@@ -519,13 +526,17 @@ __device__ __forceinline__ void store_range(vmqg_range* out, uint64_t i, uint32_
 // publishes go to list RETRY ? 2 (whole-wave walks) : 0 (the 4-lane retry).
 template <int G, int OUT, bool RETRY = false>
 __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
-                                  uint32_t& fl) {
+                                  uint32_t& fl, uint32_t& xl) {
   const vmqg_pub pub = a.pubs[p];
   const Matched m = walk_publish<G>(a, pub, s, g);
   fl = 0;
-  // more keys than the spill slots hold: many-key mode too (EMIT expands the
-  // candidates wave-wide instead of walking again)
-  const bool many = !m.overflow && (m.many || m.nk > VMQG_SPILL_KEYS);
+  // wide publishes — more keys than the spill slots hold, or many records —
+  // are written by a whole wave in EMIT's second phase, expanded again from
+  // their candidates; their XCD label (a hash of the first candidate, else
+  // of the exact key) sends publishes of one key to one XCD, whose L2 then
+  // keeps the key's records for all of them
+  const bool many = !m.overflow && (m.many || m.nk > VMQG_SPILL_KEYS || m.ksum >= VMQG_WIDE_RECORDS);
+  xl = ((m.nc ? s.cd(0) : m.ex_off) * 0x9E3779B1u) >> 29;
   // 3..8 keys: the group copies its key list to the publish's spill slots
   const bool spill = !m.overflow && !many && m.nk > 2;
   if (spill)
@@ -538,7 +549,7 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
   uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
   if (m.overflow) {   // a later tier counts it (and writes offsets[p])
     const uint32_t idx = atomicAdd(&a.status[RETRY ? kStWalked : kStDeferred], 1u);
-    a.deferred[(RETRY ? 2ull * a.npub : 0ull) + idx] = p;   // each list holds npub entries
+    a.deferred[(RETRY ? (uint64_t)a.npub : 0ull) + idx] = p;   // each list holds npub entries
     a.offsets[p] = 0;
     kc[0] = make_uint4(0, kDeferred, 0, 0);
     fl = m.walk_ovf ? 2 : 3;
@@ -566,16 +577,22 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
   return total;
 }
 
-// Appends the many-key publishes among a wave's groups (fl == 1 on a
-// group's lane 0) to EMIT's many-key list: one atomic per wave.
+// Appends the wide publishes among a wave's groups (fl == 1 on a group's
+// lane 0) to the wide list of their XCD label: one atomic per wave and label.
 template <int G>
-__device__ __forceinline__ void append_many(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t p) {
-  const uint64_t m_many = __ballot(g.lane == 0 && fl == 1);
-  if (!m_many) return;
-  uint32_t at = 0;
-  if (__lane_id() == 0) at = atomicAdd(&a.status[kStMany], (uint32_t)__popcll(m_many));
-  at = __shfl(at, 0, 64);
-  if (g.lane == 0 && fl == 1) a.deferred[a.npub + at + prefix_bits(m_many)] = p;
+__device__ __forceinline__ void append_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t xl,
+                                            uint32_t p) {
+  const uint64_t m_all = __ballot(g.lane == 0 && fl == 1);
+  if (!m_all) return;
+  if (__lane_id() == 0) atomicAdd(&a.status[kStMany], (uint32_t)__popcll(m_all));
+  for (uint32_t x = 0; x < kXcds; x++) {
+    const uint64_t m_x = __ballot(g.lane == 0 && fl == 1 && xl == x);
+    if (!m_x) continue;
+    uint32_t at = 0;
+    if (__lane_id() == 0) at = atomicAdd(&a.status[kStWideCount + x], (uint32_t)__popcll(m_x));
+    at = __shfl(at, 0, 64);
+    if (g.lane == 0 && fl == 1 && xl == x) a.deferred[(uint64_t)(2 + x) * a.npub + at + prefix_bits(m_x)] = p;
+  }
 }
 
 // ------------------------------------------------------------- EMIT pass
@@ -844,6 +861,44 @@ __device__ int emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScrat
   return res;
 }
 
+// Second phase of the fast EMIT launch: the wide publishes, one whole wave
+// each, taken by ticket from the wide list of the block's XCD label
+// (blockIdx % 8: blocks b and b + 8 share an XCD under the dispatcher's
+// observed round-robin — a speed choice only), then from the other labels'
+// lists.  A publish's output position is its chunk's base (scanned) plus the
+// counts of the publishes before it in its chunk, read from the key cache
+// (COUNT and the wave tier leave every count there; offsets[] may still be
+// being rewritten into positions by the wave that owns the chunk).
+template <int OUT, bool NT>
+__device__ void emit_wide_phase(const MatchArgs& a, uint2* kb) {
+  const uint32_t lane = __lane_id();
+  const uint4* kc = reinterpret_cast<const uint4*>(a.keycache);
+  const uint32_t x0 = blockIdx.x % kXcds;
+  for (uint32_t k = 0; k < kXcds; k++) {
+    const uint32_t x = (x0 + k) % kXcds;
+    const uint32_t nm = a.status[kStWideCount + x];
+    for (;;) {
+      uint32_t t = 0;
+      if (lane == 0) t = atomicAdd(&a.status[kStWideTicket + x], 1u);
+      t = __shfl(t, 0, 64);
+      if (t >= nm) break;
+      const uint32_t p = a.deferred[(uint64_t)(2 + x) * a.npub + t];
+      const uint32_t c0 = p - p % a.gpw;
+      const uint32_t q = c0 + lane;
+      const uint64_t before = q < p ? kc[(uint64_t)q * 2].x : 0u;   // a.gpw <= 64
+      const uint64_t rel = __shfl(wave_incl_scan64(before), 63, 64);
+      const uint64_t ob = a.chunk[p / a.gpw] + rel, oe = ob + kc[(uint64_t)p * 2].x;
+      if (oe > (OUT ? a.rng_cap : a.out_cap)) {
+        if (lane == 0) atomicOr(a.err, kErrOverflow);
+        continue;
+      }
+      emit_many<OUT, NT, 8>(a, p, ob, oe, kb);
+      if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)(oe - ob));
+      wave_sync();
+    }
+  }
+}
+
 // --------------------------------------------------------------- kernels
 // Positions of the publishes of a 64-publish chunk (the chunks of a one-lane
 // COUNT, fast_g 1): lane l reads publish first + l's count, the wave scans
@@ -876,6 +931,7 @@ void k_match_fast(MatchArgs a) {
   __shared__ uint32_t cd[FS::CC * FS::SLOTS];
   __shared__ uint2 ky[FS::KC * FS::SLOTS];
   __shared__ GroupMeta gm[kWaves][MODE == 1 && OUT == 0 ? GPW : 1];
+  __shared__ uint2 kbuf[kWaves][MODE == 1 ? 64 : 1];   // emit_many's key buffer
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
@@ -903,6 +959,7 @@ void k_match_fast(MatchArgs a) {
         wave_sync();
       }
     }
+    emit_wide_phase<OUT, NT>(a, kbuf[wv]);
     return;
   }
   const uint32_t stride = gridDim.x * kWaves * GPW;
@@ -910,13 +967,13 @@ void k_match_fast(MatchArgs a) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
     if (MODE == 0) {
       uint64_t c = 0;
-      uint32_t fl = 0;
-      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl);
+      uint32_t fl = 0, xl = 0;
+      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl, xl);
       // the chunk's total (publishes the wave tier takes add theirs later)
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
-      // many-key publishes go to EMIT's wave-tier list, one atomic per wave and kind
-      append_many<G>(a, g, fl, base + g.gidx);
+      // wide publishes go to EMIT's second phase, one atomic per wave and label
+      append_wide<G>(a, g, fl, xl, base + g.gidx);
       const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
       if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
     } else if (OUT == 0) {
@@ -928,6 +985,7 @@ void k_match_fast(MatchArgs a) {
     }
     wave_sync();
   }
+  if (MODE == 1) emit_wide_phase<OUT, NT>(a, kbuf[wv]);
 }
 
 // ============================================================== wave tier
@@ -1156,6 +1214,8 @@ __device__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint
   if (ok && lane == 0) {
     if (MODE == 0) {
       a.offsets[p] = total;
+      // its count in the key cache too: EMIT's many-key phase reads every count from there
+      reinterpret_cast<uint4*>(a.keycache)[(uint64_t)p * 2] = make_uint4((uint32_t)total, kDeferred, 0, 0);
       atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)total);
     } else if (total != oe - ob) {
       atomicOr(a.err, kErrMismatch);
@@ -1174,11 +1234,11 @@ __device__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint
 // multi-wildcard walk fits); a publish served there gets its key cache as in
 // the fast pass and its count added to its chunk's total.  What overflows
 // even those lists is walked by the whole wave at once (and listed for
-// EMIT: list 2).  With fast_g 4 the fast pass already had these lists: its
+// EMIT: list 1).  With fast_g 4 the fast pass already had these lists: its
 // deferrals go straight to the whole-wave walk.
 //
-// EMIT: the whole-wave walks again (list 2), then the many-key publishes
-// (list 1), expanded from their candidates with no walk.
+// EMIT: the whole-wave walks again (list 1); the wide publishes were written
+// by the fast EMIT launch's second phase.
 template <int MODE, int OUT, bool NT>
 __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
   __shared__ WaveLds lds[kWaves];
@@ -1200,21 +1260,21 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
       const uint32_t i = base + g.gidx;
       const bool valid = i < nd;
       const uint32_t p = valid ? a.deferred[i] : 0u;
-      uint32_t fl = 2, c = 0;
+      uint32_t fl = 2, c = 0, xl = 0;
       if (retry && valid) {
-        c = count_publish<4, OUT, true>(a, p, s, g, fl);
+        c = count_publish<4, OUT, true>(a, p, s, g, fl, xl);
         if (g.lane == 0 && fl <= 1)
           atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)c);
       }
       wave_sync();
-      if (retry) append_many<4>(a, g, fl, p);
+      if (retry) append_wide<4>(a, g, fl, xl, p);
       // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
       uint64_t ov = __ballot(valid && g.lane == 0 && fl >= 2);
-      if (!retry && ov) {   // list 2 for EMIT (the retry's count_publish listed its own)
+      if (!retry && ov) {   // list 1 for EMIT (the retry's count_publish listed its own)
         uint32_t at = 0;
         if (lane == 0) at = atomicAdd(&a.status[kStWalked], (uint32_t)__popcll(ov));
         at = __shfl(at, 0, 64);
-        if (valid && g.lane == 0) a.deferred[2ull * a.npub + at + prefix_bits(ov)] = p;
+        if (valid && g.lane == 0) a.deferred[(uint64_t)a.npub + at + prefix_bits(ov)] = p;
       }
       while (ov) {
         const uint32_t l = (uint32_t)__builtin_ctzll(ov);
@@ -1224,19 +1284,12 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
     }
     return;
   } else {
-    const uint32_t n2 = a.status[kStWalked];
-    const uint32_t n = n2 + a.status[kStMany];
+    const uint32_t n = a.status[kStWalked];
     for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
-      const uint32_t p = d < n2 ? a.deferred[2ull * a.npub + d] : a.deferred[a.npub + (d - n2)];
+      const uint32_t p = a.deferred[(uint64_t)a.npub + d];
       const uint64_t ob = a.offsets[p], oe = a.offsets[p + 1];
       if (oe > (OUT ? a.rng_cap : a.out_cap)) {
         if (lane == 0) atomicOr(a.err, kErrOverflow);
-        continue;
-      }
-      if (d >= n2) {   // counted by a fast tier: expand its candidates, no walk
-        emit_many<OUT, NT, 8>(a, p, ob, oe, lds[wv].keys);
-        if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWaveEnt), (unsigned long long)(oe - ob));
-        wave_sync();
         continue;
       }
       wave_publish<1, OUT, NT>(a, lds[wv], gstack, p, ob, oe);
