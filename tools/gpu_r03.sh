@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 T=${1:-r03}; shift
 O=gpurun_out/$T
 mkdir -p $O
-PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+PYT="python -u -m pytest -x -v --durations=15 --timeout 300 --timeout-method thread"
 for step in "$@"; do
   case $step in
   tests)

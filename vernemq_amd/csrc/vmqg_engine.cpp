@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <unistd.h>
 #include <cstring>
 
 namespace vmqg {
@@ -1021,6 +1023,49 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   return a;
 }
 
+// VMQG_DEBUG_SYNC=<seconds>: wait for each launch of a match call and name
+// the one still running after that many seconds, then end the process (a
+// diagnosis aid for a launch that does not finish; off by default).
+static double debug_limit() {
+  static const double lim = [] { const char* e = getenv("VMQG_DEBUG_SYNC"); return e ? atof(e) : 0.0; }();
+  return lim;
+}
+static uint32_t* debug_words() {   // 8 progress words per wave, host memory the kernels write directly
+  static uint32_t* w = [] {
+    void* p = nullptr;
+    if (debug_limit() > 0 && hipHostMalloc(&p, (size_t)8 * 4 * 65536, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) p = nullptr;
+    return static_cast<uint32_t*>(p);
+  }();
+  return w;
+}
+static void debug_sync(hipStream_t st, const char* what) {
+  const double lim = debug_limit();
+  if (lim <= 0) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (hipStreamQuery(st) == hipErrorNotReady) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim) {
+      fprintf(stderr, "vmqg debug: %s still running after %.0f s\n", what, lim);
+      if (uint32_t* w = debug_words()) {
+        uint32_t hist[16] = {0};
+        int shown = 0;
+        for (uint32_t i = 0; i < 65536; i++) {
+          const volatile uint32_t* q = w + (size_t)i * 8;
+          hist[q[0] & 15]++;
+          if (q[0] != 0 && q[0] != 9 && shown < 40) {
+            shown++;
+            fprintf(stderr, "  wave %u: phase %u base %u ticket %u/%u p %u k0 %u K %u nc %u\n", i, q[0], q[1],
+                    q[2] & 15, q[2] >> 4, q[3], q[5], q[6], q[7]);
+          }
+        }
+        fprintf(stderr, "  phases: 0:%u 1:%u 2:%u 9:%u\n", hist[0], hist[1], hist[2], hist[9]);
+      }
+      fflush(stderr);
+      _exit(3);
+    }
+  }
+  fprintf(stderr, "vmqg debug: %s done\n", what);
+}
+
 int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t* d_words_, Record* d_out_,
                          uint64_t out_cap, vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets,
                          hipStream_t st) {
@@ -1036,6 +1081,7 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
       (rc = ensure_wave_scratch(st)))
     return rc;
   MatchArgs a = args_for(d_pubs_, npub, d_words_, d_offsets);
+  if ((a.dbg = debug_words())) memset(a.dbg, 0, (size_t)8 * 4 * 65536);
   a.out = d_out_; a.out_cap = out_cap;
   a.out_rng = d_rng; a.rng_cap = rng_cap;
   last_set = call_seq & 1;
@@ -1049,11 +1095,16 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   }
   // COUNT: fast groups, then the wave tier for what they deferred
   if (launch_match(a, 0, 0, st, ev[0], ev[1]) != hipSuccess) return VMQG_E_DEVICE;
+  debug_sync(st, "COUNT");
   if (launch_match(a, 0, 1, st, ev[2], ev[3]) != hipSuccess) return VMQG_E_DEVICE;
+  debug_sync(st, "COUNT wave tier");
   if (launch_scan(a, st, ev[4], ev[5]) != hipSuccess) return VMQG_E_DEVICE;
+  debug_sync(st, "scan");
   // EMIT: same tiers
   if (launch_match(a, 1, 0, st, ev[6], ev[7]) != hipSuccess) return VMQG_E_DEVICE;
+  debug_sync(st, "EMIT");
   if (launch_match(a, 1, 1, st, ev[8], ev[9]) != hipSuccess) return VMQG_E_DEVICE;
+  debug_sync(st, "EMIT wave tier");
   return VMQG_OK;
 }
 

@@ -37,6 +37,7 @@ struct MatchArgs {
   uint32_t lb_tag, pad1;                          // this call's granule tag (never 0)
   uint2* o_stack;                                 // wave tier: global frontier stacks, o_cap entries per wave
   uint32_t o_cap, o_waves;
+  uint32_t* dbg;                                  // VMQG_DEBUG_SYNC only: per-wave progress words in host memory
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records

@@ -66,6 +66,13 @@ constexpr uint32_t kMany = 0xFFFFFFFDu;     // key cache: more keys than the lis
 // eight lists of wide publishes (many keys, or >= kWideRecords records),
 // one per XCD label, written wave-wide by the second phase of the fast EMIT.
 constexpr uint32_t kXcds = 8, kLists = 2 + kXcds;
+// progress words of the calling wave (VMQG_DEBUG_SYNC diagnosis; a.dbg null otherwise)
+#define DBGW(slot, v)                                                                                        \
+  do {                                                                                                       \
+    if (a.dbg)                                                                                               \
+      __hip_atomic_store(a.dbg + ((uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 8 + (slot), (uint32_t)(v), \
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                                       \
+  } while (0)
 enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, kStMany = 4, kStWalkOvf = 5,
                   kStWaveEnt = 6 /* u64: entries written by the EMIT wave tier (whole-wave walks) */,
                   kStWideCount = 8 /* [8, 16): per XCD label */, kStWideTicket = 16 /* [16, 24) */,
@@ -125,6 +132,22 @@ struct Group {
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+// Wave-uniform values as the compiler sees them (scalar registers): loops
+// and branches on them are scalar branches, so no lane can leave a ticket
+// loop on its own.  (A ticket loop whose exit the compiler took for
+// divergent hung the wide phase: lane 0, the one taking the tickets, left
+// it while the other lanes kept reading ticket 0.)
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+// One ticket per wave, taken by its first active lane.
+__device__ __forceinline__ uint32_t wave_ticket(uint32_t* ctr) {
+  uint32_t t = 0;
+  if (__lane_id() == uni(__lane_id())) t = atomicAdd(ctr, 1u);
+  return uni(t);
+}
 
 __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
   const uint32_t lane = __lane_id();
@@ -672,6 +695,8 @@ __device__ void emit_many(const MatchArgs& a, uint32_t p, uint64_t ob, uint64_t 
   const uint32_t K = __shfl(kincl, 63, 64);
   const uint32_t kstart = kincl - nkeys;
   uint64_t run = 0;
+  DBGW(6, K);
+  DBGW(7, nc);
   for (uint32_t k0 = 0; k0 < K; k0 += 64) {
     const uint32_t ki = k0 + lane;
     // the candidate owning key ki: the last c whose keys start at or before it
@@ -876,18 +901,18 @@ __device__ void emit_wide_phase(const MatchArgs& a, uint2* kb) {
   const uint32_t x0 = blockIdx.x % kXcds;
   for (uint32_t k = 0; k < kXcds; k++) {
     const uint32_t x = (x0 + k) % kXcds;
-    const uint32_t nm = a.status[kStWideCount + x];
+    const uint32_t nm = uni(a.status[kStWideCount + x]);
     for (;;) {
-      uint32_t t = 0;
-      if (lane == 0) t = atomicAdd(&a.status[kStWideTicket + x], 1u);
-      t = __shfl(t, 0, 64);
+      const uint32_t t = wave_ticket(&a.status[kStWideTicket + x]);
+      DBGW(2, x | (t << 4));
       if (t >= nm) break;
-      const uint32_t p = a.deferred[(uint64_t)(2 + x) * a.npub + t];
+      const uint32_t p = uni(a.deferred[(uint64_t)(2 + x) * a.npub + t]);
+      DBGW(3, p);
       const uint32_t c0 = p - p % a.gpw;
       const uint32_t q = c0 + lane;
       const uint64_t before = q < p ? kc[(uint64_t)q * 2].x : 0u;   // a.gpw <= 64
       const uint64_t rel = __shfl(wave_incl_scan64(before), 63, 64);
-      const uint64_t ob = a.chunk[p / a.gpw] + rel, oe = ob + kc[(uint64_t)p * 2].x;
+      const uint64_t ob = uni64(a.chunk[p / a.gpw] + rel), oe = uni64(ob + kc[(uint64_t)p * 2].x);
       if (oe > (OUT ? a.rng_cap : a.out_cap)) {
         if (lane == 0) atomicOr(a.err, kErrOverflow);
         continue;
@@ -935,6 +960,7 @@ void k_match_fast(MatchArgs a) {
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
+  if (MODE == 1) DBGW(0, 1);
   if constexpr (MODE == 1 && CH != GPW) {
     // EMIT over the 64-publish chunks of a one-lane COUNT, as two halves of
     // GPW = 32 publishes with two lanes per publish
@@ -959,7 +985,9 @@ void k_match_fast(MatchArgs a) {
         wave_sync();
       }
     }
+    DBGW(0, 2);
     emit_wide_phase<OUT, NT>(a, kbuf[wv]);
+    DBGW(0, 9);
     return;
   }
   const uint32_t stride = gridDim.x * kWaves * GPW;
@@ -1255,7 +1283,7 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
     const Group<4> g;
     const FS s{st, cd, ky, wv * GPW + g.gidx};
     const bool retry = a.fast_g != 4;
-    const uint32_t nd = a.status[kStDeferred];
+    const uint32_t nd = uni(a.status[kStDeferred]);
     for (uint32_t base = (uint32_t)gw * GPW; base < nd; base += nwaves * GPW) {
       const uint32_t i = base + g.gidx;
       const bool valid = i < nd;
@@ -1284,10 +1312,10 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
     }
     return;
   } else {
-    const uint32_t n = a.status[kStWalked];
+    const uint32_t n = uni(a.status[kStWalked]);
     for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
-      const uint32_t p = a.deferred[(uint64_t)a.npub + d];
-      const uint64_t ob = a.offsets[p], oe = a.offsets[p + 1];
+      const uint32_t p = uni(a.deferred[(uint64_t)a.npub + d]);
+      const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
       if (oe > (OUT ? a.rng_cap : a.out_cap)) {
         if (lane == 0) atomicOr(a.err, kErrOverflow);
         continue;
