@@ -984,7 +984,12 @@ int Engine::ensure_wave_scratch(hipStream_t st) {
   waves = std::max<uint64_t>(64, std::min<uint64_t>(8ull * (uint64_t)cu_count, waves)) & ~3ull;
   if (d_ostack) { hipStreamSynchronize(st); hipFree(d_ostack); }
   d_ostack = nullptr; o_waves = 0; o_cap = 0;
-  if (hipMalloc(&d_ostack, waves * need * sizeof(uint2)) != hipSuccess) return VMQG_E_NOMEM;
+  // the stacks, then one bit per stack: borrowed by the fused phases (held
+  // only during one walk, so the bitmap is all zero between calls)
+  const uint64_t stack_bytes = waves * need * sizeof(uint2);
+  if (hipMalloc(&d_ostack, stack_bytes + (waves + 31) / 32 * 4) != hipSuccess) return VMQG_E_NOMEM;
+  o_slots = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(d_ostack) + stack_bytes);
+  if (hipMemsetAsync(o_slots, 0, (waves + 31) / 32 * 4, st) != hipSuccess) return VMQG_E_DEVICE;
   o_cap = (uint32_t)need;
   o_waves = (uint32_t)waves;
   return VMQG_OK;
@@ -1019,7 +1024,7 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.count_bpc = opt_count_bpc; a.emit_bpc = opt_emit_bpc;
   a.cus = (uint32_t)cu_count;
   a.lookback = d_lookback; a.lb_tag = lb_tag;
-  a.o_stack = d_ostack; a.o_cap = o_cap; a.o_waves = o_waves;
+  a.o_stack = d_ostack; a.o_cap = o_cap; a.o_waves = o_waves; a.o_slots = o_slots;
   return a;
 }
 
@@ -1094,16 +1099,33 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
     t_ev.push_back(ev);
   }
   // COUNT: fast groups, then the wave tier for what they deferred
+  // (fuse_scan: the scan launch takes COUNT's wave tier too)
   if (launch_match(a, 0, 0, st, ev[0], ev[1]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "COUNT");
-  if (launch_match(a, 0, 1, st, ev[2], ev[3]) != hipSuccess) return VMQG_E_DEVICE;
+  if (opt_flags & kOptFuseScan) {
+    if (timing) {   // stage 1 made no launch: no events (collect_times counts it 0)
+      hipEventDestroy(ev[2]); hipEventDestroy(ev[3]);
+      t_ev.back()[2] = t_ev.back()[3] = nullptr;
+    }
+  } else if (launch_match(a, 0, 1, st, ev[2], ev[3]) != hipSuccess) {
+    return VMQG_E_DEVICE;
+  }
   debug_sync(st, "COUNT wave tier");
   if (launch_scan(a, st, ev[4], ev[5]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "scan");
-  // EMIT: same tiers
+  // EMIT: the fast tier (+ the wide publishes, and in records mode the
+  // whole-wave walks too unless fuse_walk is off), then the wave tier
   if (launch_match(a, 1, 0, st, ev[6], ev[7]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "EMIT");
-  if (launch_match(a, 1, 1, st, ev[8], ev[9]) != hipSuccess) return VMQG_E_DEVICE;
+  const bool fused = !d_rng && (opt_flags & kOptFuseWalk);
+  if (fused) {
+    if (timing) {   // stage 4 made no launch: no events (collect_times counts it 0)
+      hipEventDestroy(ev[8]); hipEventDestroy(ev[9]);
+      t_ev.back()[8] = t_ev.back()[9] = nullptr;
+    }
+  } else if (launch_match(a, 1, 1, st, ev[8], ev[9]) != hipSuccess) {
+    return VMQG_E_DEVICE;
+  }
   debug_sync(st, "EMIT wave tier");
   return VMQG_OK;
 }
@@ -1143,14 +1165,14 @@ void Engine::collect_times() {
   if (!has_device) return;
   hipSetDevice(device);
   for (auto& ev : t_ev) {
-    hipEventSynchronize(ev[2 * kTimedStages - 1]);
+    hipEventSynchronize(ev[2 * kTimedStages - 1] ? ev[2 * kTimedStages - 1] : ev[2 * kTimedStages - 3]);
     for (int k = 0; k < kTimedStages; k++) {
       float ms = 0;
-      hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
+      if (ev[2 * k]) hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);   // null: the stage made no launch
       sum_stage_ns[k] += ms * 1e6;
     }
     n_timed++;
-    for (auto e : ev) hipEventDestroy(e);
+    for (auto e : ev) if (e) hipEventDestroy(e);
   }
   t_ev.clear();
 }

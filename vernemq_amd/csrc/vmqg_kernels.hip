@@ -76,7 +76,9 @@ constexpr uint32_t kXcds = 8, kLists = 2 + kXcds;
 enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, kStMany = 4, kStWalkOvf = 5,
                   kStWaveEnt = 6 /* u64: entries written by the EMIT wave tier (whole-wave walks) */,
                   kStWideCount = 8 /* [8, 16): per XCD label */, kStWideTicket = 16 /* [16, 24) */,
-                  kStWideEnt = 24 /* u64: entries written by the wide phase */, kStWords = 32 };
+                  kStWideEnt = 24 /* u64: entries written by the wide phase */,
+                  kStWalkTicket = 26 /* fused walked phase of the fast EMIT (kOptFuseWalk) */,
+                  kStDeferDone = 27 /* fused scan (kOptFuseScan): deferred items done */, kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
 #define VMQG_WIDE_RECORDS 256   // publishes with at least this many records are written by the wide phase
 #endif
@@ -298,10 +300,13 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
 // XOR moving the G consecutive entries a group touches at once onto
 // different banks, so neither the G lanes of a group nor groups at the same
 // depth conflict (SLOTS is a multiple of 32).
-template <int G>
+// SLOTS_ = GPW: one wave's groups only (the fused scan's per-wave slices).
+template <int G, uint32_t SLOTS_ = kWaves * (64 / G)>
 struct FastScratch {
-  static constexpr uint32_t GPW = 64 / G, SLOTS = kWaves * GPW;
-  static constexpr uint32_t SH = G == 1 ? 5 : G == 2 ? 4 : G == 4 ? 3 : 2;   // 32 / G = 1 << SH
+  static constexpr uint32_t GPW = 64 / G, SLOTS = SLOTS_;
+  // 32 / G = 1 << SH, or SLOTS / G when the lists hold one wave's groups
+  static constexpr uint32_t SH0 = G == 1 ? 5 : G == 2 ? 4 : G == 4 ? 3 : 2;
+  static constexpr uint32_t SH = (32u / G) <= SLOTS / G ? SH0 : (SLOTS / G == 4 ? 2 : SLOTS / G == 2 ? 1 : 0);
   static constexpr uint32_t SC = FastCaps<G>::S, CC = FastCaps<G>::C, KC = FastCaps<G>::K;
   uint2* stack; uint32_t* cand; uint2* keys;
   uint32_t slot;
@@ -337,8 +342,8 @@ __device__ __forceinline__ void sum_keys(const MatchArgs& a, uint32_t key, uint3
   }
 }
 
-template <int G>
-__device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const FastScratch<G>& s,
+template <int G, uint32_t SL>
+__device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const FastScratch<G, SL>& s,
                                 const Group<G>& g) {
   const uint32_t L = pub.nwords;
   const uint32_t* w = a.words + pub.word_off;
@@ -547,11 +552,11 @@ __device__ __forceinline__ void store_range(vmqg_range* out, uint64_t i, uint32_
 // 0) says how it was served: 0 fast tier, 1 many-key mode, 2 deferred by a
 // walk overflow, 3 deferred otherwise (remote nodes >= 64).  Deferred
 // publishes go to list RETRY ? 2 (whole-wave walks) : 0 (the 4-lane retry).
-template <int G, int OUT, bool RETRY = false>
-__device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, const Group<G>& g,
+template <int G, int OUT, bool RETRY = false, uint32_t SL = kWaves * (64 / G)>
+__device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G, SL>& s, const Group<G>& g,
                                   uint32_t& fl, uint32_t& xl) {
   const vmqg_pub pub = a.pubs[p];
-  const Matched m = walk_publish<G>(a, pub, s, g);
+  const Matched m = walk_publish<G, SL>(a, pub, s, g);
   fl = 0;
   // wide publishes — more keys than the spill slots hold, or many records —
   // are written by a whole wave in EMIT's second phase, expanded again from
@@ -894,10 +899,18 @@ __device__ int emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScrat
 // counts of the publishes before it in its chunk, read from the key cache
 // (COUNT and the wave tier leave every count there; offsets[] may still be
 // being rewritten into positions by the wave that owns the chunk).
+// Output range [ob, oe) of publish p from the counts in the key cache (wave-wide).
+__device__ __forceinline__ void keycache_position(const MatchArgs& a, uint32_t p, uint64_t& ob, uint64_t& oe) {
+  const uint4* kc = reinterpret_cast<const uint4*>(a.keycache);
+  const uint32_t q = p - p % a.gpw + __lane_id();
+  const uint64_t before = q < p ? kc[(uint64_t)q * 2].x : 0u;   // a.gpw <= 64
+  ob = uni64(a.chunk[p / a.gpw] + __shfl(wave_incl_scan64(before), 63, 64));
+  oe = uni64(ob + kc[(uint64_t)p * 2].x);
+}
+
 template <int OUT, bool NT>
 __device__ void emit_wide_phase(const MatchArgs& a, uint2* kb) {
   const uint32_t lane = __lane_id();
-  const uint4* kc = reinterpret_cast<const uint4*>(a.keycache);
   const uint32_t x0 = blockIdx.x % kXcds;
   for (uint32_t k = 0; k < kXcds; k++) {
     const uint32_t x = (x0 + k) % kXcds;
@@ -908,11 +921,8 @@ __device__ void emit_wide_phase(const MatchArgs& a, uint2* kb) {
       if (t >= nm) break;
       const uint32_t p = uni(a.deferred[(uint64_t)(2 + x) * a.npub + t]);
       DBGW(3, p);
-      const uint32_t c0 = p - p % a.gpw;
-      const uint32_t q = c0 + lane;
-      const uint64_t before = q < p ? kc[(uint64_t)q * 2].x : 0u;   // a.gpw <= 64
-      const uint64_t rel = __shfl(wave_incl_scan64(before), 63, 64);
-      const uint64_t ob = uni64(a.chunk[p / a.gpw] + rel), oe = uni64(ob + kc[(uint64_t)p * 2].x);
+      uint64_t ob, oe;
+      keycache_position(a, p, ob, oe);
       if (oe > (OUT ? a.rng_cap : a.out_cap)) {
         if (lane == 0) atomicOr(a.err, kErrOverflow);
         continue;
@@ -922,98 +932,6 @@ __device__ void emit_wide_phase(const MatchArgs& a, uint2* kb) {
       wave_sync();
     }
   }
-}
-
-// --------------------------------------------------------------- kernels
-// Positions of the publishes of a 64-publish chunk (the chunks of a one-lane
-// COUNT, fast_g 1): lane l reads publish first + l's count, the wave scans
-// them from the chunk's base and writes the final offsets; returns lane l's
-// position and count for the halves to pick up.
-__device__ __forceinline__ void chunk_positions64(const MatchArgs& a, uint32_t first, uint32_t nch, uint64_t& pos,
-                                                  uint64_t& cnt) {
-  const uint32_t lane = __lane_id();
-  const bool valid = lane < nch;
-  cnt = valid ? a.offsets[first + lane] : 0;
-  const uint64_t incl = wave_incl_scan64(cnt);
-  pos = a.chunk[first / 64] + incl - cnt;
-  if (valid) a.offsets[first + lane] = pos;
-}
-
-template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
-#ifndef VMQG_COUNT_WPE
-#define VMQG_COUNT_WPE 4    // COUNT waves per SIMD the register budget must allow, 2+ lanes per publish (A/B: 4, 5)
-#endif
-#ifndef VMQG_COUNT_WPE1
-#define VMQG_COUNT_WPE1 5   // ... one lane per publish (96 VGPRs, no spills)
-#endif
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(MODE == 0 ? (G == 1 ? VMQG_COUNT_WPE1 : VMQG_COUNT_WPE) : 4)))
-void k_match_fast(MatchArgs a) {
-  using FS = FastScratch<G>;
-  constexpr int GPW = FS::GPW;
-  if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < kStWords) a.status_next[threadIdx.x] = 0;
-  __shared__ uint2 st[FS::SC * FS::SLOTS];
-  __shared__ uint32_t cd[FS::CC * FS::SLOTS];
-  __shared__ uint2 ky[FS::KC * FS::SLOTS];
-  __shared__ GroupMeta gm[kWaves][MODE == 1 && OUT == 0 ? GPW : 1];
-  __shared__ uint2 kbuf[kWaves][MODE == 1 ? 64 : 1];   // emit_many's key buffer
-  const Group<G> g;
-  const uint32_t wv = threadIdx.x >> 6;
-  const FS s{st, cd, ky, wv * GPW + g.gidx};
-  if (MODE == 1) DBGW(0, 1);
-  if constexpr (MODE == 1 && CH != GPW) {
-    // EMIT over the 64-publish chunks of a one-lane COUNT, as two halves of
-    // GPW = 32 publishes with two lanes per publish
-    static_assert(CH == 2 * GPW, "");
-    const uint32_t stride = gridDim.x * kWaves * CH;
-    for (uint32_t base = (blockIdx.x * kWaves + wv) * CH; base < a.npub; base += stride) {
-      const uint32_t nch = a.npub - base < (uint32_t)CH ? a.npub - base : (uint32_t)CH;
-      uint64_t pos, cnt;
-      chunk_positions64(a, base, nch, pos, cnt);
-      for (uint32_t h = 0; h < 2; h++) {
-        const uint32_t first = base + h * GPW;
-        if (nch <= h * GPW) break;
-        const uint32_t n = nch - h * GPW < (uint32_t)GPW ? nch - h * GPW : (uint32_t)GPW;
-        const uint32_t q = h * GPW + g.gidx;
-        const uint64_t ob = __shfl(pos, q, 64), oe = ob + __shfl(cnt, q, 64);
-        const uint64_t wb = __shfl(pos, h * GPW, 64);
-        if (OUT == 0) {
-          emit_wave<G, GPW, NT, VMQG_EMIT_U, true>(a, first, n, s, g, gm[wv], wv * GPW, ob, oe, wb);
-        } else if (g.gidx < n) {
-          emit_ranges_group<G>(a, first + g.gidx, s, g, ob, oe);
-        }
-        wave_sync();
-      }
-    }
-    DBGW(0, 2);
-    emit_wide_phase<OUT, NT>(a, kbuf[wv]);
-    DBGW(0, 9);
-    return;
-  }
-  const uint32_t stride = gridDim.x * kWaves * GPW;
-  for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
-    const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
-    if (MODE == 0) {
-      uint64_t c = 0;
-      uint32_t fl = 0, xl = 0;
-      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl, xl);
-      // the chunk's total (publishes the wave tier takes add theirs later)
-      const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
-      if (__lane_id() == 0) a.chunk[base / GPW] = tot;
-      // wide publishes go to EMIT's second phase, one atomic per wave and label
-      append_wide<G>(a, g, fl, xl, base + g.gidx);
-      const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
-      if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
-    } else if (OUT == 0) {
-      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
-    } else {
-      uint64_t ob, oe;
-      chunk_offsets<G, GPW>(a, base, n, g, ob, oe);
-      if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
-    }
-    wave_sync();
-  }
-  if (MODE == 1) emit_wide_phase<OUT, NT>(a, kbuf[wv]);
 }
 
 // ============================================================== wave tier
@@ -1226,6 +1144,35 @@ struct WaveWalk {
 // entries, sized from the trie depth so it cannot overflow).  COUNT writes
 // offsets[p] and adds to the chunk total; EMIT re-walks in the same order,
 // writes [ob, oe) and checks the count.
+//
+// The fused phases (gstack null) borrow one of the o_waves global stacks for
+// the second walk: claimed from the bitmap a.o_slots, released after.  A
+// wave that finds every stack taken waits for one; a holder is in the middle
+// of a walk, which never waits on anything, so it always comes back.
+__device__ uint32_t claim_ostack(const MatchArgs& a) {
+  const uint32_t lane = __lane_id(), nw = (a.o_waves + 31) / 32;
+  uint32_t slot = kNone;
+  if (lane == 0) {
+    for (uint32_t spins = 0; slot == kNone; spins++) {
+      for (uint32_t i = 0; i < nw && slot == kNone; i++) {
+        const uint32_t valid = i + 1 < nw || a.o_waves % 32 == 0 ? ~0u : (1u << (a.o_waves % 32)) - 1;
+        uint32_t cur = __hip_atomic_load(a.o_slots + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (slot == kNone && (~cur & valid)) {
+          const uint32_t b = (uint32_t)__builtin_ctz(~cur & valid);
+          const uint32_t old = atomicOr(a.o_slots + i, 1u << b);
+          if (!(old & (1u << b))) slot = i * 32 + b;
+          cur = old | (1u << b);
+        }
+      }
+      if (slot == kNone) {
+        if (spins > (1u << 20)) break;   // none came back (never expected): the walk is refused loudly
+        __builtin_amdgcn_s_sleep(8);
+      }
+    }
+  }
+  return __shfl(slot, 0, 64);
+}
+
 template <int MODE, int OUT, bool NT>
 __device__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p, uint64_t ob, uint64_t oe) {
   const uint32_t lane = __lane_id();
@@ -1234,9 +1181,13 @@ __device__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint
   uint64_t total = w1.run;
   if (!ok) {
     if (MODE == 0 && lane == 0) atomicAdd(&a.status[kStTier2], 1u);
-    WaveWalk<MODE, OUT, NT> w2(a, W, gstack, a.o_cap, ob);
-    ok = w2.run_publish(p);
-    total = w2.run;
+    const uint32_t slot = gstack ? kNone : claim_ostack(a);
+    if (gstack || slot != kNone) {
+      WaveWalk<MODE, OUT, NT> w2(a, W, gstack ? gstack : a.o_stack + (uint64_t)slot * a.o_cap, a.o_cap, ob);
+      ok = w2.run_publish(p);
+      total = w2.run;
+    }
+    if (slot != kNone && lane == 0) atomicAnd(a.o_slots + slot / 32, ~(1u << (slot % 32)));
     if (!ok && lane == 0) atomicOr(a.err, kErrFrontier);
   }
   if (ok && lane == 0) {
@@ -1252,6 +1203,178 @@ __device__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint
     }
   }
   wave_sync();
+}
+
+// COUNT's deferred publishes [i0, i0 + 16) of list 0 (those < nd), one wave:
+// retried four lanes per publish (a publish served there gets its key cache
+// as in the fast pass and its count added to its chunk's total); what
+// overflows even those lists (or all, at fast_g 4, whose fast pass already
+// had them) is walked by the whole wave and listed for EMIT (list 1).
+template <int OUT, bool NT, uint32_t SL>
+__device__ void count_deferred_wave(const MatchArgs& a, const FastScratch<4, SL>& s, const Group<4>& g, WaveLds& W,
+                                    uint2* gstack, uint32_t i0, uint32_t nd) {
+  const uint32_t lane = __lane_id();
+  const bool retry = a.fast_g != 4;
+  const uint32_t i = i0 + g.gidx;
+  const bool valid = i < nd;
+  const uint32_t p = valid ? a.deferred[i] : 0u;
+  uint32_t fl = 2, c = 0, xl = 0;
+  if (retry && valid) {
+    c = count_publish<4, OUT, true, SL>(a, p, s, g, fl, xl);
+    if (g.lane == 0 && fl <= 1)
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)c);
+  }
+  wave_sync();
+  if (retry) append_wide<4>(a, g, fl, xl, p);
+  // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
+  uint64_t ov = __ballot(valid && g.lane == 0 && fl >= 2);
+  if (!retry && ov) {   // list 1 for EMIT (the retry's count_publish listed its own)
+    uint32_t at = 0;
+    if (lane == 0) at = atomicAdd(&a.status[kStWalked], (uint32_t)__popcll(ov));
+    at = __shfl(at, 0, 64);
+    if (valid && g.lane == 0) a.deferred[(uint64_t)a.npub + at + prefix_bits(ov)] = p;
+  }
+  while (ov) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(ov);
+    ov &= ov - 1;
+    wave_publish<0, OUT, NT>(a, W, gstack, __shfl(p, l, 64), 0, 0);
+  }
+}
+
+// Third phase of the fast EMIT launch (kOptFuseWalk): the publishes COUNT's
+// wave tier walked with a whole wave (list 1), walked again and written here
+// instead of by an EMIT wave-tier launch of their own, taken by ticket.  A
+// wave with no ticket left exits.
+template <int OUT, bool NT>
+__device__ __noinline__ void emit_walked_phase(const MatchArgs& a, WaveLds& W) {
+  const uint32_t lane = __lane_id();
+  const uint32_t n = uni(a.status[kStWalked]);
+  if (n == 0) return;
+  uint2* const gstack = nullptr;   // borrowed when a walk outgrows its LDS stack
+  for (;;) {
+    const uint32_t t = wave_ticket(&a.status[kStWalkTicket]);
+    if (t >= n) break;
+    const uint32_t p = uni(a.deferred[(uint64_t)a.npub + t]);
+    uint64_t ob, oe;
+    keycache_position(a, p, ob, oe);
+    if (oe > (OUT ? a.rng_cap : a.out_cap)) {
+      if (lane == 0) atomicOr(a.err, kErrOverflow);
+      continue;
+    }
+    wave_publish<1, OUT, NT>(a, W, gstack, p, ob, oe);
+  }
+}
+
+// --------------------------------------------------------------- kernels
+// Positions of the publishes of a 64-publish chunk (the chunks of a one-lane
+// COUNT, fast_g 1): lane l reads publish first + l's count, the wave scans
+// them from the chunk's base and writes the final offsets; returns lane l's
+// position and count for the halves to pick up.
+__device__ __forceinline__ void chunk_positions64(const MatchArgs& a, uint32_t first, uint32_t nch, uint64_t& pos,
+                                                  uint64_t& cnt) {
+  const uint32_t lane = __lane_id();
+  const bool valid = lane < nch;
+  cnt = valid ? a.offsets[first + lane] : 0;
+  const uint64_t incl = wave_incl_scan64(cnt);
+  pos = a.chunk[first / 64] + incl - cnt;
+  if (valid) a.offsets[first + lane] = pos;
+}
+
+template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
+#ifndef VMQG_COUNT_WPE
+#define VMQG_COUNT_WPE 4    // COUNT waves per SIMD the register budget must allow, 2+ lanes per publish (A/B: 4, 5)
+#endif
+#ifndef VMQG_COUNT_WPE1
+#define VMQG_COUNT_WPE1 5   // ... one lane per publish (96 VGPRs, no spills)
+#endif
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(MODE == 0 ? (G == 1 ? VMQG_COUNT_WPE1 : VMQG_COUNT_WPE) : 4)))
+void k_match_fast(MatchArgs a) {
+  using FS = FastScratch<G>;
+  constexpr int GPW = FS::GPW;
+  if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < kStWords) a.status_next[threadIdx.x] = 0;
+  // LDS: COUNT {stack, candidates, keys}; EMIT {GroupMeta, keys} for its
+  // chunk pass, the same bytes as the four waves' WaveLds for the walked
+  // phase (after a block barrier), plus emit_many's key buffers
+  constexpr uint32_t kGmN = MODE == 1 && OUT == 0 ? GPW : 1;
+  constexpr uint32_t kStB = MODE == 0 ? FS::SC * FS::SLOTS * 8 : 0, kCdB = MODE == 0 ? FS::CC * FS::SLOTS * 4 : 0;
+  constexpr uint32_t kGmB = MODE == 1 ? kWaves * kGmN * (uint32_t)sizeof(GroupMeta) : 0;
+  constexpr uint32_t kKyB = FS::KC * FS::SLOTS * 8;
+  constexpr uint32_t kChunkB = kGmB + kStB + kCdB + kKyB;
+  constexpr uint32_t kWalkB = MODE == 1 && OUT == 0 ? kWaves * (uint32_t)sizeof(WaveLds) : 0;
+  __shared__ uint4 pool[((kChunkB > kWalkB ? kChunkB : kWalkB) + 15) / 16];
+  __shared__ uint2 kbuf[kWaves][MODE == 1 ? 64 : 1];   // emit_many's key buffer
+  uint8_t* pb = reinterpret_cast<uint8_t*>(pool);
+  auto gm = reinterpret_cast<GroupMeta(*)[kGmN]>(pb);
+  uint2* st = reinterpret_cast<uint2*>(pb + kGmB);
+  uint32_t* cd = reinterpret_cast<uint32_t*>(pb + kGmB + kStB);
+  uint2* ky = reinterpret_cast<uint2*>(pb + kGmB + kStB + kCdB);
+  const Group<G> g;
+  const uint32_t wv = threadIdx.x >> 6;
+  const FS s{st, cd, ky, wv * GPW + g.gidx};
+  // EMIT's phases after the chunk pass: the wide publishes, then (fused) the walked ones
+  auto tail = [&]() {
+    DBGW(0, 2);
+    emit_wide_phase<OUT, NT>(a, kbuf[wv]);
+    if (OUT == 0 && (a.opts & kOptFuseWalk)) {   // records only: the range EMIT keeps 8 waves per SIMD
+      __syncthreads();   // every wave of the block is done with the chunk pass's LDS
+      DBGW(0, 3);
+      emit_walked_phase<OUT, NT>(a, reinterpret_cast<WaveLds*>(pb)[wv]);
+    }
+    DBGW(0, 9);
+  };
+  if (MODE == 1) DBGW(0, 1);
+  if constexpr (MODE == 1 && CH != GPW) {
+    // EMIT over the 64-publish chunks of a one-lane COUNT, as two halves of
+    // GPW = 32 publishes with two lanes per publish
+    static_assert(CH == 2 * GPW, "");
+    const uint32_t stride = gridDim.x * kWaves * CH;
+    for (uint32_t base = (blockIdx.x * kWaves + wv) * CH; base < a.npub; base += stride) {
+      const uint32_t nch = a.npub - base < (uint32_t)CH ? a.npub - base : (uint32_t)CH;
+      uint64_t pos, cnt;
+      chunk_positions64(a, base, nch, pos, cnt);
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t first = base + h * GPW;
+        if (nch <= h * GPW) break;
+        const uint32_t n = nch - h * GPW < (uint32_t)GPW ? nch - h * GPW : (uint32_t)GPW;
+        const uint32_t q = h * GPW + g.gidx;
+        const uint64_t ob = __shfl(pos, q, 64), oe = ob + __shfl(cnt, q, 64);
+        const uint64_t wb = __shfl(pos, h * GPW, 64);
+        if (OUT == 0) {
+          emit_wave<G, GPW, NT, VMQG_EMIT_U, true>(a, first, n, s, g, gm[wv], wv * GPW, ob, oe, wb);
+        } else if (g.gidx < n) {
+          emit_ranges_group<G>(a, first + g.gidx, s, g, ob, oe);
+        }
+        wave_sync();
+      }
+    }
+    tail();
+    return;
+  }
+  const uint32_t stride = gridDim.x * kWaves * GPW;
+  for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
+    const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
+    if (MODE == 0) {
+      uint64_t c = 0;
+      uint32_t fl = 0, xl = 0;
+      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl, xl);
+      // the chunk's total (publishes the wave tier takes add theirs later)
+      const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
+      if (__lane_id() == 0) a.chunk[base / GPW] = tot;
+      // wide publishes go to EMIT's second phase, one atomic per wave and label
+      append_wide<G>(a, g, fl, xl, base + g.gidx);
+      const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
+      if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
+    } else if (OUT == 0) {
+      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
+    } else {
+      uint64_t ob, oe;
+      chunk_offsets<G, GPW>(a, base, n, g, ob, oe);
+      if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
+    }
+    wave_sync();
+  }
+  if constexpr (MODE == 1) tail();
 }
 
 // Wave tiers, one launch after each fast pass (each reads its list lengths
@@ -1282,34 +1405,9 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
     __shared__ uint2 ky[FS::KC * FS::SLOTS];
     const Group<4> g;
     const FS s{st, cd, ky, wv * GPW + g.gidx};
-    const bool retry = a.fast_g != 4;
     const uint32_t nd = uni(a.status[kStDeferred]);
-    for (uint32_t base = (uint32_t)gw * GPW; base < nd; base += nwaves * GPW) {
-      const uint32_t i = base + g.gidx;
-      const bool valid = i < nd;
-      const uint32_t p = valid ? a.deferred[i] : 0u;
-      uint32_t fl = 2, c = 0, xl = 0;
-      if (retry && valid) {
-        c = count_publish<4, OUT, true>(a, p, s, g, fl, xl);
-        if (g.lane == 0 && fl <= 1)
-          atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)c);
-      }
-      wave_sync();
-      if (retry) append_wide<4>(a, g, fl, xl, p);
-      // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
-      uint64_t ov = __ballot(valid && g.lane == 0 && fl >= 2);
-      if (!retry && ov) {   // list 1 for EMIT (the retry's count_publish listed its own)
-        uint32_t at = 0;
-        if (lane == 0) at = atomicAdd(&a.status[kStWalked], (uint32_t)__popcll(ov));
-        at = __shfl(at, 0, 64);
-        if (valid && g.lane == 0) a.deferred[(uint64_t)a.npub + at + prefix_bits(ov)] = p;
-      }
-      while (ov) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(ov);
-        ov &= ov - 1;
-        wave_publish<0, OUT, NT>(a, lds[wv], gstack, __shfl(p, l, 64), 0, 0);
-      }
-    }
+    for (uint32_t base = (uint32_t)gw * GPW; base < nd; base += nwaves * GPW)
+      count_deferred_wave<OUT, NT>(a, s, g, lds[wv], gstack, base, nd);
     return;
   } else {
     const uint32_t n = uni(a.status[kStWalked]);
@@ -1379,6 +1477,96 @@ __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
   }
 }
 
+// COUNT's wave tier folded into the scan launch (kOptFuseScan): one ticket
+// counter hands out first the deferred publishes (items of 64, one block
+// each: 16 per wave, count_deferred_wave), then the scan tiles.  A tile
+// waits until every item is done (their counts go into the chunk totals it
+// scans).  That wait cannot block an item: every item ticket was taken
+// before any tile ticket, by a block that was running, and an item never
+// waits on anything (its walks borrow global stacks from holders that never
+// wait either).  Within a block all four waves take the same ticket, so every
+// block barrier is reached by all of them.
+template <int OUT, bool NT>
+__device__ __noinline__ void scan_item(const MatchArgs& a, uint8_t* slice, uint32_t i0, uint32_t nd) {
+  using FS = FastScratch<4, 16>;
+  const Group<4> g;
+  const FS s{reinterpret_cast<uint2*>(slice), reinterpret_cast<uint32_t*>(slice + FS::SC * FS::SLOTS * 8),
+             reinterpret_cast<uint2*>(slice + FS::SC * FS::SLOTS * 8 + FS::CC * FS::SLOTS * 4), g.gidx};
+  count_deferred_wave<OUT, NT>(a, s, g, *reinterpret_cast<WaveLds*>(slice), nullptr, i0, nd);
+}
+
+template <int OUT, bool NT>
+__global__ __launch_bounds__(256) void k_scan_fused(MatchArgs a) {
+  using FS = FastScratch<4, 16>;
+  constexpr uint32_t kListB = (FS::SC * 8 + FS::CC * 4 + FS::KC * 8) * FS::SLOTS;
+  constexpr uint32_t kSliceB = ((kListB > sizeof(WaveLds) ? kListB : (uint32_t)sizeof(WaveLds)) + 15) / 16 * 16;
+  __shared__ uint4 pool[kWaves * kSliceB / 16];
+  __shared__ uint64_t part[kScanBlock];
+  __shared__ uint32_t s_t;
+  __shared__ uint64_t s_base;
+  const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
+  const uint64_t n = (uint64_t)nchunks + 1;
+  const uint32_t ntiles = (uint32_t)((n + kScanTile - 1) / kScanTile);
+  const uint32_t nd = uni(a.status[kStDeferred]);
+  const uint32_t nitems = (nd + 63) / 64;
+  if (blockIdx.x >= nitems + ntiles) return;   // no ticket left for this block: no atomic either
+  uint8_t* slice = reinterpret_cast<uint8_t*>(pool) + (threadIdx.x >> 6) * kSliceB;
+  uint64_t* v = a.chunk;
+  for (;;) {
+    if (threadIdx.x == 0) s_t = atomicAdd(&a.status[kStTicket], 1u);
+    __syncthreads();
+    const uint32_t t = __builtin_amdgcn_readfirstlane(s_t);
+    __syncthreads();
+    if (t < nitems) {
+      scan_item<OUT, NT>(a, slice, t * 64 + (threadIdx.x >> 6) * 16, nd);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __threadfence();
+        atomicAdd(&a.status[kStDeferDone], 1u);
+      }
+      continue;
+    }
+    const uint32_t tile = t - nitems;
+    if (tile >= ntiles) break;
+    if (nitems) {
+      if (threadIdx.x == 0) {
+        for (uint32_t spins = 0;
+             __hip_atomic_load(&a.status[kStDeferDone], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < nitems;) {
+          if (++spins > kSpinLimit) { atomicOr(a.err, kErrLookback); break; }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __syncthreads();
+    }
+    const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint64_t x[kScanItems];
+    uint64_t acc = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kScanItems; i++) { x[i] = base + i < nchunks ? v[base + i] : 0; acc += x[i]; }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t o = 1; o < kScanBlock; o <<= 1) {
+      const uint64_t tt = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+      __syncthreads();
+      part[threadIdx.x] += tt;
+      __syncthreads();
+    }
+    if (threadIdx.x < 64) {
+      const uint64_t b = lookback(a.lookback, a.lb_tag, a.err, tile, part[kScanBlock - 1]);
+      if (threadIdx.x == 0) s_base = b;
+    }
+    __syncthreads();
+    uint64_t run = s_base + part[threadIdx.x] - acc;
+#pragma unroll
+    for (uint32_t i = 0; i < kScanItems; i++) {
+      if (base + i < n) v[base + i] = run;
+      if (base + i == nchunks) a.offsets[a.npub] = run;   // the batch total
+      run += x[i];
+    }
+    __syncthreads();
+  }
+}
+
 uint32_t scan_tiles(uint64_t nchunks) { return (uint32_t)((nchunks + 1 + kScanTile - 1) / kScanTile); }
 
 // ---------------------------------------------------------------- patches
@@ -1395,6 +1583,17 @@ static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b
 
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   uint32_t g = scan_tiles((a.npub + a.gpw - 1) / a.gpw);
+  if (a.opts & kOptFuseScan) {
+    // tiles plus deferred items (unknown here): blocks beyond what the
+    // device lists exit at once
+    g = std::max<uint32_t>(g, (uint32_t)a.cus * 2u);
+    const bool nt = (a.opts & kOptNtStores) != 0;
+    auto k = a.out_rng ? (nt ? k_scan_fused<1, true> : k_scan_fused<1, false>)
+                       : (nt ? k_scan_fused<0, true> : k_scan_fused<0, false>);
+    if (t0) hipExtLaunchKernelGGL(k, dim3(g), dim3(kScanBlock), 0, st, t0, t1, 0, a);
+    else k<<<g, kScanBlock, 0, st>>>(a);
+    return hipGetLastError();
+  }
   if (g > 2048) g = 2048;
   if (t0) hipExtLaunchKernelGGL(k_scan_offsets, dim3(g), dim3(kScanBlock), 0, st, t0, t1, 0, a);
   else k_scan_offsets<<<g, kScanBlock, 0, st>>>(a);
