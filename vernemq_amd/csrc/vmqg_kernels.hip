@@ -607,12 +607,13 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
 
 // Appends the wide publishes among a wave's groups (fl == 1 on a group's
 // lane 0) to the wide list of their XCD label: one atomic per wave and label.
-template <int G>
+template <int G, int OUT>
 __device__ __forceinline__ void append_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t xl,
                                             uint32_t p) {
   const uint64_t m_all = __ballot(g.lane == 0 && fl == 1);
   if (!m_all) return;
   if (__lane_id() == 0) atomicAdd(&a.status[kStMany], (uint32_t)__popcll(m_all));
+  if (OUT == 0 && (a.opts & kOptWideInline)) return;   // the records EMIT writes them where it finds them
   for (uint32_t x = 0; x < kXcds; x++) {
     const uint64_t m_x = __ballot(g.lane == 0 && fl == 1 && xl == x);
     if (!m_x) continue;
@@ -761,6 +762,26 @@ __device__ void emit_many(const MatchArgs& a, uint32_t p, uint64_t ob, uint64_t 
   if (lane == 0 && run != oe - ob) atomicOr(a.err, kErrMismatch);
 }
 
+// kOptWideInline: the wide publishes among a wave's groups (resolve gave
+// kResMany), written by the whole wave right after the group pass, one after
+// the other — no publish lists, no atomics.
+template <int OUT, bool NT, int G>
+__device__ __forceinline__ uint64_t emit_wide_inline(const MatchArgs& a, const Group<G>& g, uint32_t first, int res,
+                                                     uint64_t ob, uint64_t oe, uint2* kb) {
+  uint64_t mm = __ballot(g.lane == 0 && res == kResMany), written = 0;
+  while (mm) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(mm);
+    mm &= mm - 1;
+    const uint32_t p = first + l / G;
+    const uint64_t pob = uni64(((uint64_t)__shfl((uint32_t)(ob >> 32), l, 64) << 32) | __shfl((uint32_t)ob, l, 64));
+    const uint64_t poe = uni64(((uint64_t)__shfl((uint32_t)(oe >> 32), l, 64) << 32) | __shfl((uint32_t)oe, l, 64));
+    emit_many<OUT, NT, 8>(a, p, pob, poe, kb);
+    written += poe - pob;
+    wave_sync();
+  }
+  return written;
+}
+
 // Output ranges of the GPW publishes [first, first + n) of one chunk: the
 // chunk's base (the scanned chunk totals) plus the exclusive prefix of the
 // counts COUNT left in offsets[]; each group's lane 0 writes its publish's
@@ -784,10 +805,12 @@ __device__ __forceinline__ uint64_t chunk_offsets(const MatchArgs& a, uint32_t f
 // of one wave.  Resolve is per group; the copy is wave-wide over the wave's
 // output range minus the ranges of publishes the wave tier writes, so every
 // store instruction writes up to 64 x 16 B = 1 KiB contiguous.
+// Returns the group's resolve result (kResMany: a wide publish, written by
+// the caller) and its output range in [ob_out, oe_out).
 template <int G, int GPW, bool NT, int U, bool PRE = false>
-__device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const FastScratch<G>& s,
-                          const Group<G>& g, GroupMeta* gm, uint32_t slot0, uint64_t pre_obase = 0,
-                          uint64_t pre_oend = 0, uint64_t pre_wbase = 0) {
+__device__ int emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const FastScratch<G>& s,
+                         const Group<G>& g, GroupMeta* gm, uint32_t slot0, uint64_t& ob_out, uint64_t& oe_out,
+                         uint64_t pre_obase = 0, uint64_t pre_oend = 0, uint64_t pre_wbase = 0) {
   const uint32_t p = first + g.gidx;
   const bool valid = g.gidx < n;
   uint64_t obase = pre_obase, oend = pre_oend;
@@ -861,6 +884,9 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
       if (w[u]) store_rec<NT>(a.out, dst[u], v[u]);
   }
   wave_sync();
+  ob_out = obase;
+  oe_out = oend;
+  return res;
 }
 
 // Range mode: each group writes its publish's non-empty keys as
@@ -891,14 +917,6 @@ __device__ int emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScrat
   return res;
 }
 
-// Second phase of the fast EMIT launch: the wide publishes, one whole wave
-// each, taken by ticket from the wide list of the block's XCD label
-// (blockIdx % 8: blocks b and b + 8 share an XCD under the dispatcher's
-// observed round-robin — a speed choice only), then from the other labels'
-// lists.  A publish's output position is its chunk's base (scanned) plus the
-// counts of the publishes before it in its chunk, read from the key cache
-// (COUNT and the wave tier leave every count there; offsets[] may still be
-// being rewritten into positions by the wave that owns the chunk).
 // Output range [ob, oe) of publish p from the counts in the key cache (wave-wide).
 __device__ __forceinline__ void keycache_position(const MatchArgs& a, uint32_t p, uint64_t& ob, uint64_t& oe) {
   const uint4* kc = reinterpret_cast<const uint4*>(a.keycache);
@@ -908,30 +926,54 @@ __device__ __forceinline__ void keycache_position(const MatchArgs& a, uint32_t p
   oe = uni64(ob + kc[(uint64_t)p * 2].x);
 }
 
+// Second phase of the fast EMIT launch: the wide publishes, one whole wave
+// each, shared out statically — no ticket atomics (thousands of waves taking
+// tickets on a few counters at the end of the launch cost milliseconds).
+// Pass 1: the waves of XCD label x (blocks b with b % 8 == x: the
+// dispatcher's observed round-robin, a speed choice only) take list x's
+// first min(n_x, avg) entries, so publishes of one key share an L2; pass 2:
+// what longer lists hold beyond avg goes round-robin to every wave.  A
+// publish's output position is its chunk's base (scanned) plus the counts of
+// the publishes before it in its chunk, read from the key cache (offsets[]
+// may still be being rewritten into positions by the wave owning the chunk).
 template <int OUT, bool NT>
 __device__ void emit_wide_phase(const MatchArgs& a, uint2* kb) {
-  const uint32_t lane = __lane_id();
-  const uint32_t x0 = blockIdx.x % kXcds;
-  for (uint32_t k = 0; k < kXcds; k++) {
-    const uint32_t x = (x0 + k) % kXcds;
-    const uint32_t nm = uni(a.status[kStWideCount + x]);
-    for (;;) {
-      const uint32_t t = wave_ticket(&a.status[kStWideTicket + x]);
-      DBGW(2, x | (t << 4));
-      if (t >= nm) break;
-      const uint32_t p = uni(a.deferred[(uint64_t)(2 + x) * a.npub + t]);
-      DBGW(3, p);
-      uint64_t ob, oe;
-      keycache_position(a, p, ob, oe);
-      if (oe > (OUT ? a.rng_cap : a.out_cap)) {
-        if (lane == 0) atomicOr(a.err, kErrOverflow);
-        continue;
-      }
-      emit_many<OUT, NT, 8>(a, p, ob, oe, kb);
-      if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)(oe - ob));
-      wave_sync();
+  uint32_t n[kXcds], total = 0;
+#pragma unroll
+  for (uint32_t x = 0; x < kXcds; x++) { n[x] = uni(a.status[kStWideCount + x]); total += n[x]; }
+  if (total == 0) return;
+  const uint32_t avg = (total + kXcds - 1) / kXcds;
+  uint64_t written = 0;
+  auto one = [&](uint32_t x, uint32_t i) {
+    const uint32_t p = uni(a.deferred[(uint64_t)(2 + x) * a.npub + i]);
+    DBGW(3, p);
+    uint64_t ob, oe;
+    keycache_position(a, p, ob, oe);
+    if (oe > (OUT ? a.rng_cap : a.out_cap)) {
+      if (__lane_id() == 0) atomicOr(a.err, kErrOverflow);
+      return;
     }
+    emit_many<OUT, NT, 8>(a, p, ob, oe, kb);
+    written += oe - ob;
+    wave_sync();
+  };
+  const uint32_t wv = threadIdx.x >> 6;
+  // pass 1: the block's own label
+  const uint32_t x = blockIdx.x % kXcds;
+  const uint32_t wx = ((gridDim.x - x + kXcds - 1) / kXcds) * kWaves;   // waves of label x
+  const uint32_t m1 = n[x] < avg ? n[x] : avg;
+  for (uint32_t i = (blockIdx.x / kXcds) * kWaves + wv; i < m1; i += wx) one(x, i);
+  // pass 2: the overflow of longer lists, round-robin over every wave
+  const uint32_t W = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
+  uint32_t base = 0;
+  for (uint32_t y = 0; y < kXcds; y++) {
+    if (n[y] <= avg) continue;
+    const uint32_t len = n[y] - avg;
+    for (uint32_t j = (gw + W - base % W) % W; j < len; j += W) one(y, avg + j);
+    base += len;
   }
+  if (written && __lane_id() == 0)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)written);
 }
 
 // ============================================================== wave tier
@@ -1225,7 +1267,7 @@ __device__ void count_deferred_wave(const MatchArgs& a, const FastScratch<4, SL>
       atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)c);
   }
   wave_sync();
-  if (retry) append_wide<4>(a, g, fl, xl, p);
+  if (retry) append_wide<4, OUT>(a, g, fl, xl, p);
   // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
   uint64_t ov = __ballot(valid && g.lane == 0 && fl >= 2);
   if (!retry && ov) {   // list 1 for EMIT (the retry's count_publish listed its own)
@@ -1243,17 +1285,16 @@ __device__ void count_deferred_wave(const MatchArgs& a, const FastScratch<4, SL>
 
 // Third phase of the fast EMIT launch (kOptFuseWalk): the publishes COUNT's
 // wave tier walked with a whole wave (list 1), walked again and written here
-// instead of by an EMIT wave-tier launch of their own, taken by ticket.  A
-// wave with no ticket left exits.
+// instead of by an EMIT wave-tier launch of their own, shared out
+// round-robin over the waves of the launch.
 template <int OUT, bool NT>
 __device__ __noinline__ void emit_walked_phase(const MatchArgs& a, WaveLds& W) {
   const uint32_t lane = __lane_id();
   const uint32_t n = uni(a.status[kStWalked]);
   if (n == 0) return;
   uint2* const gstack = nullptr;   // borrowed when a walk outgrows its LDS stack
-  for (;;) {
-    const uint32_t t = wave_ticket(&a.status[kStWalkTicket]);
-    if (t >= n) break;
+  const uint32_t nw = gridDim.x * kWaves;
+  for (uint32_t t = blockIdx.x * kWaves + (threadIdx.x >> 6); t < n; t += nw) {   // static: no ticket atomics
     const uint32_t p = uni(a.deferred[(uint64_t)a.npub + t]);
     uint64_t ob, oe;
     keycache_position(a, p, ob, oe);
@@ -1313,9 +1354,15 @@ void k_match_fast(MatchArgs a) {
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
   // EMIT's phases after the chunk pass: the wide publishes, then (fused) the walked ones
+  uint64_t wide_written = 0;   // kOptWideInline: entries this wave wrote for wide publishes
   auto tail = [&]() {
     DBGW(0, 2);
-    emit_wide_phase<OUT, NT>(a, kbuf[wv]);
+    if (OUT == 0 && (a.opts & kOptWideInline)) {
+      if (wide_written && __lane_id() == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)wide_written);
+    } else {
+      emit_wide_phase<OUT, NT>(a, kbuf[wv]);
+    }
     if (OUT == 0 && (a.opts & kOptFuseWalk)) {   // records only: the range EMIT keeps 8 waves per SIMD
       __syncthreads();   // every wave of the block is done with the chunk pass's LDS
       DBGW(0, 3);
@@ -1340,12 +1387,16 @@ void k_match_fast(MatchArgs a) {
         const uint32_t q = h * GPW + g.gidx;
         const uint64_t ob = __shfl(pos, q, 64), oe = ob + __shfl(cnt, q, 64);
         const uint64_t wb = __shfl(pos, h * GPW, 64);
+        int res = kResSkip;
+        uint64_t rob = ob, roe = oe;
         if (OUT == 0) {
-          emit_wave<G, GPW, NT, VMQG_EMIT_U, true>(a, first, n, s, g, gm[wv], wv * GPW, ob, oe, wb);
+          res = emit_wave<G, GPW, NT, VMQG_EMIT_U, true>(a, first, n, s, g, gm[wv], wv * GPW, rob, roe, ob, oe, wb);
         } else if (g.gidx < n) {
-          emit_ranges_group<G>(a, first + g.gidx, s, g, ob, oe);
+          res = emit_ranges_group<G>(a, first + g.gidx, s, g, ob, oe);
         }
         wave_sync();
+        if (OUT == 0 && (a.opts & kOptWideInline))
+          wide_written += emit_wide_inline<OUT, NT, G>(a, g, first, res, rob, roe, kbuf[wv]);
       }
     }
     tail();
@@ -1362,15 +1413,21 @@ void k_match_fast(MatchArgs a) {
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
       // wide publishes go to EMIT's second phase, one atomic per wave and label
-      append_wide<G>(a, g, fl, xl, base + g.gidx);
+      append_wide<G, OUT>(a, g, fl, xl, base + g.gidx);
       const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
       if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
-    } else if (OUT == 0) {
-      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
     } else {
-      uint64_t ob, oe;
-      chunk_offsets<G, GPW>(a, base, n, g, ob, oe);
-      if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
+      int res = kResSkip;
+      uint64_t ob = 0, oe = 0;
+      if (OUT == 0) {
+        res = emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW, ob, oe);
+      } else {
+        chunk_offsets<G, GPW>(a, base, n, g, ob, oe);
+        if (g.gidx < n) res = emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
+      }
+      wave_sync();
+      if (OUT == 0 && (a.opts & kOptWideInline))
+        wide_written += emit_wide_inline<OUT, NT, G>(a, g, base, res, ob, oe, kbuf[wv]);
     }
     wave_sync();
   }
