@@ -61,7 +61,7 @@ def main():
     names = [o.split("=")[0] for o in args.opt]
     values = [[int(x) for x in o.split("=")[1].split(",")] for o in args.opt]
     variants = list(itertools.product(*values))
-    res = {str(dict(zip(names, vv))): {"step_us": [], "count_us": [], "emit_us": []} for vv in variants}
+    res = {str(dict(zip(names, vv))): {k: [] for k in ["step_us"] + [st + "_us" for st in v.STAGES]} for vv in variants}
     ref = None
     for rnd in range(args.rounds):
         for vv in variants:
@@ -84,12 +84,12 @@ def main():
                                d_offs.data_ptr(), sp)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / args.steps
-            c, e, _ = v.kernel_times()
+            stt = v.stage_times()
             v.set_timing(False)
             r = res[str(dict(zip(names, vv)))]
             r["step_us"].append(dt * 1e6)
-            r["count_us"].append(c / 1e3)
-            r["emit_us"].append(e / 1e3)
+            for st in v.STAGES:
+                r[st + "_us"].append(stt[st] / 1e3)
     out = {k: {m: statistics.median(x) for m, x in d.items()} for k, d in res.items()}
     print(json.dumps({"config": args.config, "median": out, "rounds": args.rounds, "steps": args.steps}))
 
