@@ -1099,17 +1099,9 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
     t_ev.push_back(ev);
   }
   // COUNT: fast groups, then the wave tier for what they deferred
-  // (fuse_scan: the scan launch takes COUNT's wave tier too)
   if (launch_match(a, 0, 0, st, ev[0], ev[1]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "COUNT");
-  if (opt_flags & kOptFuseScan) {
-    if (timing) {   // stage 1 made no launch: no events (collect_times counts it 0)
-      hipEventDestroy(ev[2]); hipEventDestroy(ev[3]);
-      t_ev.back()[2] = t_ev.back()[3] = nullptr;
-    }
-  } else if (launch_match(a, 0, 1, st, ev[2], ev[3]) != hipSuccess) {
-    return VMQG_E_DEVICE;
-  }
+  if (launch_match(a, 0, 1, st, ev[2], ev[3]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "COUNT wave tier");
   if (launch_scan(a, st, ev[4], ev[5]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "scan");
@@ -1155,6 +1147,7 @@ int Engine::match_status(hipStream_t st) {
   last_wave_entries = (uint64_t)c[6] | ((uint64_t)c[7] << 32);
   last_wide_entries = (uint64_t)c[24] | ((uint64_t)c[25] << 32);
   const uint32_t err = h[2 * kStatusSet];
+  if (err && debug_limit() > 0) fprintf(stderr, "vmqg debug: match status error bits 0x%x\n", err);
   if (err & 2u) return VMQG_E_FRONTIER;
   if (err & 4u) return VMQG_E_OVERFLOW;
   if (err & (8u | 16u)) return VMQG_E_DEVICE;   // count mismatch, look-back timeout

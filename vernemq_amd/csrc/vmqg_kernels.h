@@ -43,7 +43,6 @@ struct MatchArgs {
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
 constexpr uint32_t kOptWideInline = 8u; // wide publishes written by the EMIT wave that meets them (no lists)
-constexpr uint32_t kOptFuseScan = 4u;   // COUNT's wave tier in the scan launch (no COUNT wave launch)
 constexpr uint32_t kOptFuseWalk = 2u;   // EMIT's whole-wave walks in the fast EMIT launch (no EMIT wave launch)
 
 // mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier (grid a.o_waves / 4).

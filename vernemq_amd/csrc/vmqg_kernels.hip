@@ -78,7 +78,7 @@ enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, k
                   kStWideCount = 8 /* [8, 16): per XCD label */, kStWideTicket = 16 /* [16, 24) */,
                   kStWideEnt = 24 /* u64: entries written by the wide phase */,
                   kStWalkTicket = 26 /* fused walked phase of the fast EMIT (kOptFuseWalk) */,
-                  kStDeferDone = 27 /* fused scan (kOptFuseScan): deferred items done */, kStWords = 32 };
+                  kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
 #define VMQG_WIDE_RECORDS 256   // publishes with at least this many records are written by the wide phase
 #endif
@@ -993,13 +993,14 @@ struct WaveWalk {
   uint2* stack;
   uint32_t scap;
   uint64_t obase;       // output position of the publish (MODE 1)
+  uint64_t oend;        // ... and its end: no store at or past it, whatever the walk finds
   uint64_t run = 0;     // entries counted / written so far (wave-uniform)
   uint32_t nc = 0, nk = 0;
   uint64_t rm = 0;      // lane-partial remote mask (nodes < 64)
   bool dollar = false;
 
-  __device__ WaveWalk(const MatchArgs& a_, WaveLds& W_, uint2* st, uint32_t cap, uint64_t ob)
-      : a(a_), W(W_), stack(st), scap(cap), obase(ob) {}
+  __device__ WaveWalk(const MatchArgs& a_, WaveLds& W_, uint2* st, uint32_t cap, uint64_t ob, uint64_t oe)
+      : a(a_), W(W_), stack(st), scap(cap), obase(ob), oend(oe) {}
 
   __device__ void add_high(uint32_t off, uint32_t cnt) {   // remote nodes >= 64 into the set
     for (uint32_t j = 0; j < cnt; j++) {
@@ -1014,7 +1015,8 @@ struct WaveWalk {
     if (nk == 0) return;
     if (MODE == 0 && OUT == 1) { run += nk; nk = 0; return; }
     if (MODE == 1 && OUT == 1) {
-      for (uint32_t k = lane; k < nk; k += 64) store_range(a.out_rng, obase + run + k, W.keys[k].x, W.keys[k].y);
+      for (uint32_t k = lane; k < nk; k += 64)
+        if (obase + run + k < oend) store_range(a.out_rng, obase + run + k, W.keys[k].x, W.keys[k].y);
       run += nk;
       nk = 0;
       wave_sync();
@@ -1045,7 +1047,7 @@ struct WaveWalk {
 #pragma unroll
         for (int u = 0; u < U; u++) {
           const uint32_t r = r0 + 64 * u;
-          if (r < tot) store_rec<NT>(a.out, obase + run + r, v[u]);
+          if (r < tot && obase + run + r < oend) store_rec<NT>(a.out, obase + run + r, v[u]);
         }
       }
       wave_sync();
@@ -1170,6 +1172,7 @@ struct WaveWalk {
         const uint32_t b = (uint32_t)__builtin_ctzll(word);
         word &= word - 1;
         const uint32_t node = lane * 64 + b;
+        if (pos >= oend) break;
         if (OUT == 0) store_rec<NT>(a.out, pos, make_uint4((VMQG_EMIT_REMOTE << 24) | node, kNone, kNone, kNone));
         else store_range(a.out_rng, pos, node, 0u);
         pos++;
@@ -1218,14 +1221,14 @@ __device__ uint32_t claim_ostack(const MatchArgs& a) {
 template <int MODE, int OUT, bool NT>
 __device__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p, uint64_t ob, uint64_t oe) {
   const uint32_t lane = __lane_id();
-  WaveWalk<MODE, OUT, NT> w1(a, W, W.stack, kWStack, ob);
+  WaveWalk<MODE, OUT, NT> w1(a, W, W.stack, kWStack, ob, oe);
   bool ok = w1.run_publish(p);
   uint64_t total = w1.run;
   if (!ok) {
     if (MODE == 0 && lane == 0) atomicAdd(&a.status[kStTier2], 1u);
     const uint32_t slot = gstack ? kNone : claim_ostack(a);
     if (gstack || slot != kNone) {
-      WaveWalk<MODE, OUT, NT> w2(a, W, gstack ? gstack : a.o_stack + (uint64_t)slot * a.o_cap, a.o_cap, ob);
+      WaveWalk<MODE, OUT, NT> w2(a, W, gstack ? gstack : a.o_stack + (uint64_t)slot * a.o_cap, a.o_cap, ob, oe);
       ok = w2.run_publish(p);
       total = w2.run;
     }
@@ -1471,7 +1474,7 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
     for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
       const uint32_t p = uni(a.deferred[(uint64_t)a.npub + d]);
       const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
-      if (oe > (OUT ? a.rng_cap : a.out_cap)) {
+      if (oe > (OUT ? a.rng_cap : a.out_cap) || ob > oe) {
         if (lane == 0) atomicOr(a.err, kErrOverflow);
         continue;
       }
@@ -1534,96 +1537,6 @@ __global__ __launch_bounds__(256) void k_scan_offsets(MatchArgs a) {
   }
 }
 
-// COUNT's wave tier folded into the scan launch (kOptFuseScan): one ticket
-// counter hands out first the deferred publishes (items of 64, one block
-// each: 16 per wave, count_deferred_wave), then the scan tiles.  A tile
-// waits until every item is done (their counts go into the chunk totals it
-// scans).  That wait cannot block an item: every item ticket was taken
-// before any tile ticket, by a block that was running, and an item never
-// waits on anything (its walks borrow global stacks from holders that never
-// wait either).  Within a block all four waves take the same ticket, so every
-// block barrier is reached by all of them.
-template <int OUT, bool NT>
-__device__ __noinline__ void scan_item(const MatchArgs& a, uint8_t* slice, uint32_t i0, uint32_t nd) {
-  using FS = FastScratch<4, 16>;
-  const Group<4> g;
-  const FS s{reinterpret_cast<uint2*>(slice), reinterpret_cast<uint32_t*>(slice + FS::SC * FS::SLOTS * 8),
-             reinterpret_cast<uint2*>(slice + FS::SC * FS::SLOTS * 8 + FS::CC * FS::SLOTS * 4), g.gidx};
-  count_deferred_wave<OUT, NT>(a, s, g, *reinterpret_cast<WaveLds*>(slice), nullptr, i0, nd);
-}
-
-template <int OUT, bool NT>
-__global__ __launch_bounds__(256) void k_scan_fused(MatchArgs a) {
-  using FS = FastScratch<4, 16>;
-  constexpr uint32_t kListB = (FS::SC * 8 + FS::CC * 4 + FS::KC * 8) * FS::SLOTS;
-  constexpr uint32_t kSliceB = ((kListB > sizeof(WaveLds) ? kListB : (uint32_t)sizeof(WaveLds)) + 15) / 16 * 16;
-  __shared__ uint4 pool[kWaves * kSliceB / 16];
-  __shared__ uint64_t part[kScanBlock];
-  __shared__ uint32_t s_t;
-  __shared__ uint64_t s_base;
-  const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
-  const uint64_t n = (uint64_t)nchunks + 1;
-  const uint32_t ntiles = (uint32_t)((n + kScanTile - 1) / kScanTile);
-  const uint32_t nd = uni(a.status[kStDeferred]);
-  const uint32_t nitems = (nd + 63) / 64;
-  if (blockIdx.x >= nitems + ntiles) return;   // no ticket left for this block: no atomic either
-  uint8_t* slice = reinterpret_cast<uint8_t*>(pool) + (threadIdx.x >> 6) * kSliceB;
-  uint64_t* v = a.chunk;
-  for (;;) {
-    if (threadIdx.x == 0) s_t = atomicAdd(&a.status[kStTicket], 1u);
-    __syncthreads();
-    const uint32_t t = __builtin_amdgcn_readfirstlane(s_t);
-    __syncthreads();
-    if (t < nitems) {
-      scan_item<OUT, NT>(a, slice, t * 64 + (threadIdx.x >> 6) * 16, nd);
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __threadfence();
-        atomicAdd(&a.status[kStDeferDone], 1u);
-      }
-      continue;
-    }
-    const uint32_t tile = t - nitems;
-    if (tile >= ntiles) break;
-    if (nitems) {
-      if (threadIdx.x == 0) {
-        for (uint32_t spins = 0;
-             __hip_atomic_load(&a.status[kStDeferDone], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < nitems;) {
-          if (++spins > kSpinLimit) { atomicOr(a.err, kErrLookback); break; }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      __syncthreads();
-    }
-    const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
-    uint64_t x[kScanItems];
-    uint64_t acc = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kScanItems; i++) { x[i] = base + i < nchunks ? v[base + i] : 0; acc += x[i]; }
-    part[threadIdx.x] = acc;
-    __syncthreads();
-    for (uint32_t o = 1; o < kScanBlock; o <<= 1) {
-      const uint64_t tt = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-      __syncthreads();
-      part[threadIdx.x] += tt;
-      __syncthreads();
-    }
-    if (threadIdx.x < 64) {
-      const uint64_t b = lookback(a.lookback, a.lb_tag, a.err, tile, part[kScanBlock - 1]);
-      if (threadIdx.x == 0) s_base = b;
-    }
-    __syncthreads();
-    uint64_t run = s_base + part[threadIdx.x] - acc;
-#pragma unroll
-    for (uint32_t i = 0; i < kScanItems; i++) {
-      if (base + i < n) v[base + i] = run;
-      if (base + i == nchunks) a.offsets[a.npub] = run;   // the batch total
-      run += x[i];
-    }
-    __syncthreads();
-  }
-}
-
 uint32_t scan_tiles(uint64_t nchunks) { return (uint32_t)((nchunks + 1 + kScanTile - 1) / kScanTile); }
 
 // ---------------------------------------------------------------- patches
@@ -1640,17 +1553,6 @@ static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b
 
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   uint32_t g = scan_tiles((a.npub + a.gpw - 1) / a.gpw);
-  if (a.opts & kOptFuseScan) {
-    // tiles plus deferred items (unknown here): blocks beyond what the
-    // device lists exit at once
-    g = std::max<uint32_t>(g, (uint32_t)a.cus * 2u);
-    const bool nt = (a.opts & kOptNtStores) != 0;
-    auto k = a.out_rng ? (nt ? k_scan_fused<1, true> : k_scan_fused<1, false>)
-                       : (nt ? k_scan_fused<0, true> : k_scan_fused<0, false>);
-    if (t0) hipExtLaunchKernelGGL(k, dim3(g), dim3(kScanBlock), 0, st, t0, t1, 0, a);
-    else k<<<g, kScanBlock, 0, st>>>(a);
-    return hipGetLastError();
-  }
   if (g > 2048) g = 2048;
   if (t0) hipExtLaunchKernelGGL(k_scan_offsets, dim3(g), dim3(kScanBlock), 0, st, t0, t1, 0, a);
   else k_scan_offsets<<<g, kScanBlock, 0, st>>>(a);
