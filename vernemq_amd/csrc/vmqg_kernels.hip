@@ -1,38 +1,45 @@
 // HIP kernels for gfx950 (MI355X): the publish -> matched-subscriber path of
 // vmq_reg_trie:fold/4 (apps/vmq_server/src/vmq_reg_trie.erl:59-98).
 //
-// Fast tier — work unit: a GROUP of G lanes (G = 2 by default, 4 as an
-// option) owns one publish, so a 64-lane wavefront keeps 64 / G publishes in
-// flight.  The group walks the trie in chunks: up to G frontier entries
-// {path, depth} are popped from the group's LDS stack, one per lane, and each
-// active lane issues its three edge probes ('#', the publish word, '+') as
-// independent 64-B bucket loads before resolving any of them — the
-// ets:lookup calls of trie_match/4 and 'trie_match_#'/2 (:358-383), many
-// frontier nodes and many publishes per memory round trip.  '#' children and
-// end-of-topic nodes are compacted (ballot + mbcnt) into an LDS candidate
-// list; their node records (match/4, :283-303) give the subscriber-list
-// keys, compacted into an LDS key list.  The exact-topic probe (the
-// `{Topic, node()}` candidate and get_remote_subscribers/2, :62, :514-520) is
-// a fingerprint lookup computed group-parallel.  Remote nodes < 64 are OR-ed
-// into a 64-bit mask: exactly the `Remotes` dedupe of fold_/5 (:78-84).
-// The group lists are interleaved across the block's groups with an XOR
-// swizzle, so groups at the same list depth hit distinct LDS banks.
+// Fast tier — work unit: a GROUP of G lanes owns one publish.  COUNT runs
+// one lane per publish (fast_g 1, the default: 64 publishes per wave in
+// flight), EMIT two lanes per publish over the same 64-publish chunks
+// (fast_g 2 and 4 keep G lanes in both passes).  A group walks the trie from
+// an LDS frontier stack — per frontier node the word and '+' edge probes are
+// issued as independent 64-B bucket loads before either is resolved (the
+// ets:lookup calls of trie_match/4 and 'trie_match_#'/2, :358-383), the '#'
+// child read from its alias record — so many frontier nodes and many
+// publishes share each memory round trip.  '#' children and end-of-topic
+// nodes are compacted (ballot + mbcnt) into an LDS candidate list; their
+// node records (match/4, :283-303) give the subscriber-list keys.  The
+// exact-topic probe (the `{Topic, node()}` candidate and
+// get_remote_subscribers/2, :62, :514-520) is a fingerprint lookup.  Remote
+// nodes < 64 are OR-ed into a 64-bit mask: exactly the `Remotes` dedupe of
+// fold_/5 (:78-84).  The group lists are interleaved across the block's
+// groups with an XOR swizzle, so groups at the same depth hit distinct banks.
 //
-// Wave tier — a publish whose lists overflow the fast tier's, or that meets
-// a remote node >= 64, is deferred to one whole wave that walks it with
-// bounded LDS buffers, flushing candidates into keys and keys into output
-// (or into a count) as they fill: only its frontier stack needs room, and
-// that is bounded by the trie depth (tier 2: the stack in global memory,
-// sized by the host from the deepest path).  Remote nodes go to a 4,096-bit
-// set (one 64-bit word per lane at the end).  No publish is refused.
+// Keys per publish: <= 2 go to a 32-B key cache, 3..8 to spill slots; a
+// WIDE publish (more keys than that — a $share group hosted on many nodes,
+// Q2 — or >= 256 records) keeps only its totals and its candidate paths, and
+// EMIT expands it again with the whole wave (emit_many): by the wave that
+// meets it in its chunk (records mode), or in a second phase of the launch
+// from per-XCD lists shared out statically (range mode).
 //
-// Passes per batch: COUNT (fast tier: per-publish count + a 32-B key cache
-// {total, nk, remote mask, <= 2 x (record off, count)}; then the wave tiers
-// for what it deferred), a one-launch scan (counts -> offsets), EMIT (fast
-// tier from the key cache, re-walk only for publishes with > 2 keys; then the
-// wave tiers).  Output is either the 16-B records (lookup_subs + fold__,
-// :87-98) or, in range mode, one 8-B {record off, count} per non-empty
-// subscriber-list key plus {node, 0} per remote node.
+// Deferral tiers — a publish whose lists overflow the fast tier's, or that
+// meets a remote node >= 64, is retried four lanes per publish (lists 4x
+// larger) by the COUNT wave-tier launch; what overflows even those is walked
+// by one whole wave with bounded LDS buffers (flushing candidates into keys
+// and keys into output as they fill: only the frontier stack needs room,
+// bounded by the trie depth; tier 2 puts it in global memory).  EMIT walks
+// those again in a third phase of its own launch (records mode; range mode:
+// an EMIT wave-tier launch).  Remote nodes >= 64 go to a 4,096-bit set.  No
+// publish is refused.
+//
+// Launches per batch: COUNT, COUNT's wave tier (reads its list length on the
+// device: empty = ~4 us), the one-launch chunk-total scan (decoupled
+// look-back), EMIT.  Output is either the 16-B records (lookup_subs +
+// fold__, :87-98) or, in range mode, one 8-B {record off, count} per
+// non-empty subscriber-list key plus {node, 0} per remote node.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -930,8 +937,9 @@ __device__ __forceinline__ void keycache_position(const MatchArgs& a, uint32_t p
 // each, shared out statically — no ticket atomics (thousands of waves taking
 // tickets on a few counters at the end of the launch cost milliseconds).
 // Pass 1: the waves of XCD label x (blocks b with b % 8 == x: the
-// dispatcher's observed round-robin, a speed choice only) take list x's
-// first min(n_x, avg) entries, so publishes of one key share an L2; pass 2:
+// dispatcher's observed round-robin, a speed choice only; every label has
+// blocks, also in a grid of fewer than 8) take list x's first
+// min(n_x, avg) entries, so publishes of one key share an L2; pass 2:
 // what longer lists hold beyond avg goes round-robin to every wave.  A
 // publish's output position is its chunk's base (scanned) plus the counts of
 // the publishes before it in its chunk, read from the key cache (offsets[]
@@ -958,11 +966,14 @@ __device__ void emit_wide_phase(const MatchArgs& a, uint2* kb) {
     wave_sync();
   };
   const uint32_t wv = threadIdx.x >> 6;
-  // pass 1: the block's own label
-  const uint32_t x = blockIdx.x % kXcds;
-  const uint32_t wx = ((gridDim.x - x + kXcds - 1) / kXcds) * kWaves;   // waves of label x
-  const uint32_t m1 = n[x] < avg ? n[x] : avg;
-  for (uint32_t i = (blockIdx.x / kXcds) * kWaves + wv; i < m1; i += wx) one(x, i);
+  // pass 1: the labels of the block's class (class = block % C; with fewer
+  // than 8 blocks, C = the block count and a class takes several labels)
+  const uint32_t C = gridDim.x < kXcds ? gridDim.x : kXcds, cls = blockIdx.x % C;
+  const uint32_t wx = ((gridDim.x - cls + C - 1) / C) * kWaves;   // waves of the class
+  for (uint32_t x = cls; x < kXcds; x += C) {
+    const uint32_t m1 = n[x] < avg ? n[x] : avg;
+    for (uint32_t i = (blockIdx.x / C) * kWaves + wv; i < m1; i += wx) one(x, i);
+  }
   // pass 2: the overflow of longer lists, round-robin over every wave
   const uint32_t W = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
   uint32_t base = 0;
