@@ -12,6 +12,7 @@ from vernemq_amd import _lib  # noqa: E402
 
 VARIANTS = {
     "default": [],
+    "nowide": ["-DVMQG_NO_WIDE=1"],
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "nospill": ["-DVMQG_SPILL_KEYS=2"],
     "noalias": ["-DVMQG_HASH_ALIAS=0"],
@@ -27,8 +28,16 @@ VARIANTS = {
 
 def build(name, flags):
     out = os.path.join(ROOT, "build", "ab", "lib_%s.so" % name)
+    srcs = _lib.SOURCES
+    if name.startswith("git_"):   # the library as committed at a revision (sources exported to build/ab/src_<rev>)
+        rev = name[4:]
+        d = os.path.join(ROOT, "build", "ab", "src_" + rev)
+        os.makedirs(d, exist_ok=True)
+        subprocess.run("git -C %s archive %s vernemq_amd/csrc include | tar -x -C %s" % (ROOT, rev, d), shell=True,
+                       check=True)
+        srcs = [os.path.join(d, "vernemq_amd", "csrc", os.path.basename(x)) for x in _lib.SOURCES]
     cmd = ["/opt/rocm/bin/hipcc"] + _lib.FLAGS + flags + ['-DVMQG_BUILD_ID="vmqg-build:%s+%s"' % (_lib.source_id(), name),
-                                                          "-o", out] + _lib.SOURCES
+                                                          "-o", out] + srcs
     r = subprocess.run(cmd, capture_output=True, text=True)
     return name, r.returncode, r.stderr[-2000:]
 
@@ -37,5 +46,5 @@ if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
     os.makedirs(os.path.join(ROOT, "build", "ab"), exist_ok=True)
     with ThreadPoolExecutor(4) as ex:
-        for name, rc, err in ex.map(lambda n: build(n, VARIANTS[n]), names):
+        for name, rc, err in ex.map(lambda n: build(n, VARIANTS.get(n, [])), names):
             print(name, "ok" if rc == 0 else "FAILED\n" + err)

@@ -1369,7 +1369,11 @@ void k_match_fast(MatchArgs a) {
   const FS s{st, cd, ky, wv * GPW + g.gidx};
   // EMIT's phases after the chunk pass: the wide publishes, then (fused) the walked ones
   uint64_t wide_written = 0;   // kOptWideInline: entries this wave wrote for wide publishes
+#ifndef VMQG_NO_WIDE
+#define VMQG_NO_WIDE 0   // A/B only: 1 = no wide / walked phases in EMIT (wrong for batches that have them)
+#endif
   auto tail = [&]() {
+    if (VMQG_NO_WIDE) return;
     DBGW(0, 2);
     if (OUT == 0 && (a.opts & kOptWideInline)) {
       if (wide_written && __lane_id() == 0)
@@ -1409,7 +1413,7 @@ void k_match_fast(MatchArgs a) {
           res = emit_ranges_group<G>(a, first + g.gidx, s, g, ob, oe);
         }
         wave_sync();
-        if (OUT == 0 && (a.opts & kOptWideInline))
+        if (OUT == 0 && !VMQG_NO_WIDE && (a.opts & kOptWideInline))
           wide_written += emit_wide_inline<OUT, NT, G>(a, g, first, res, rob, roe, kbuf[wv]);
       }
     }
@@ -1440,7 +1444,7 @@ void k_match_fast(MatchArgs a) {
         if (g.gidx < n) res = emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
       }
       wave_sync();
-      if (OUT == 0 && (a.opts & kOptWideInline))
+      if (OUT == 0 && !VMQG_NO_WIDE && (a.opts & kOptWideInline))
         wide_written += emit_wide_inline<OUT, NT, G>(a, g, base, res, ob, oe, kbuf[wv]);
     }
     wave_sync();
