@@ -818,20 +818,20 @@ def bench_d(args):
         # alarm lists and the exact keys' records, cache-resident when their
         # publishes share an XCD); SURVEY §8(d)'s 32 B per emission is
         # reported beside it.  The roofline line is the longer launch.
-        # (library default fuse_walk: the whole-wave walks are a third phase
-        # of the fast EMIT launch, and the EMIT wave-tier launch is not made)
+        # The fast EMIT launch writes every publish's records except the
+        # wide ones' ($share groups on 4 nodes: 40 keys; alarm lists: 1,000
+        # records) and the whole-wave walks', which the EMIT tail launch
+        # writes (stats wide_entries, wave_entries).
         wave_rec = int(st1["wave_entries"])
-        fused = stages["emit_wave"] == 0
-        fast_rec = emitted - (0 if fused else wave_rec)
+        wide_rec = int(st1["wide_entries"])
+        fast_rec = emitted - wave_rec - wide_rec
         per_kernel = {
-            "emit": {"kernel": "k_match_fast<1,0,2,true,64> (EMIT fast tier + wide phase%s)"
-                               % (" + walked phase" if fused else ""), "records": fast_rec,
-                     "wide_records": int(st1["wide_entries"]), "walked_records": wave_rec,
+            "emit": {"kernel": "k_match_fast<1,0,2,true,64> (EMIT fast tier)", "records": fast_rec,
                      "bytes": 16 * fast_rec, "us": stages["emit"]},
+            "emit_tail": {"kernel": "k_match_wave<1,0,true> (EMIT tail: wide publishes + whole-wave walks)",
+                          "records": wide_rec + wave_rec, "wide_records": wide_rec, "walked_records": wave_rec,
+                          "bytes": 16 * (wide_rec + wave_rec), "us": stages["emit_wave"]},
         }
-        if not fused:
-            per_kernel["emit_wave"] = {"kernel": "k_match_wave<1,0,true> (EMIT wave tier: whole-wave walks)",
-                                       "records": wave_rec, "bytes": 16 * wave_rec, "us": stages["emit_wave"]}
         for v in per_kernel.values():
             v["GBps"] = v["bytes"] / (v["us"] * 1e3) if v["us"] else None
             v["frac"] = v["GBps"] / PEAK_HBM_GBS if v["GBps"] else None

@@ -13,6 +13,9 @@ from vernemq_amd import _lib  # noqa: E402
 VARIANTS = {
     "default": [],
     "nowide": ["-DVMQG_NO_WIDE=1"],
+    "noinline": ["-DVMQG_NO_INLINE=1"],
+    "nowalked": ["-DVMQG_NO_WALKED=1"],
+    "widecall": ["-DVMQG_WIDE_NOINLINE=1"],
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "nospill": ["-DVMQG_SPILL_KEYS=2"],
     "noalias": ["-DVMQG_HASH_ALIAS=0"],

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """The deferral-heavy scenario of test_output_offsets_of_a_large_deferral_heavy_batch
-under every combination of the fusion options: which combination fails, and
+under every fast_g and store policy: which combination fails, and
 how (debug of a VMQG_E_DEVICE)."""
 import itertools
 import os
@@ -29,11 +29,11 @@ orc.apply(evs)
 topics = [("", (b"n", b"%d" % j)) for j in range(1000)] + [("", hot)]
 want = np.array([len(x) for x in orc.fold_batch([(mp, b"pub", t) for mp, t in topics])], dtype=np.int64)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 300_000
-for fg, fw, wi in itertools.product([1, 2], [0, 1], [0, 1]):
+for fg, nt in itertools.product([1, 2, 4], [0, 1]):
     prod = H.ProductDriver(node, device=0)
     prod.apply(evs)
     v = prod.view
-    for k, x in (("fast_g", fg), ("fuse_walk", fw), ("wide_inline", wi)):
+    for k, x in (("fast_g", fg), ("nt_stores", nt)):
         v.set_option(k, x)
     arr, words = v.prepare(topics)
     idx = np.arange(n) % 1000
@@ -42,9 +42,9 @@ for fg, fw, wi in itertools.product([1, 2], [0, 1], [0, 1]):
         recs, offs = v.match_arrays(arr[idx], words)
         counts = np.diff(offs.astype(np.int64))
         bad = np.flatnonzero(counts != want[idx])
-        print("fast_g %d fuse_walk %d wide_inline %d: ok, %d counts differ%s, stats %s" % (
-            fg, fw, wi, len(bad), (" first %d got %d want %d" % (bad[0], counts[bad[0]], want[idx][bad[0]])) if len(bad) else "",
+        print("fast_g %d nt_stores %d: ok, %d counts differ%s, stats %s" % (
+            fg, nt, len(bad), (" first %d got %d want %d" % (bad[0], counts[bad[0]], want[idx][bad[0]])) if len(bad) else "",
             {k: v.stats_raw()[k] for k in ("deferred_tier1", "deferred_tier2", "retried", "many_key")}), flush=True)
     except Exception as e:
-        print("fast_g %d fuse_walk %d wide_inline %d: %s" % (fg, fw, wi, e), flush=True)
+        print("fast_g %d nt_stores %d: %s" % (fg, nt, e), flush=True)
     del prod

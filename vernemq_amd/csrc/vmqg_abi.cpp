@@ -282,9 +282,6 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
     e.opt_fast_g = (uint32_t)value;
   } else if (n == "nt_stores") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptNtStores) : (e.opt_flags & ~vmqg::kOptNtStores);
-  } else if (n == "fuse_walk" || n == "wide_inline") {
-    const uint32_t bit = n == "fuse_walk" ? vmqg::kOptFuseWalk : vmqg::kOptWideInline;
-    e.opt_flags = value ? (e.opt_flags | bit) : (e.opt_flags & ~bit);
   } else if (n == "count_bpc" || n == "emit_bpc") {
     if (value < 0 || value > 32) return VMQG_E_INVAL;
     (n == "count_bpc" ? e.opt_count_bpc : e.opt_emit_bpc) = (uint32_t)value;

@@ -944,7 +944,8 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     const uint64_t cap = next_pow2(std::max<uint64_t>(npub, 1024));
     // 32-B key cache + kSpillKeys x 8-B spilled keys per publish, then the
     // chunk totals (one per 16 or 32 publishes, + 1)
-    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + (cap / 16 + 2) * 8) != hipSuccess) return VMQG_E_NOMEM;
+    // (+ one 64-bit wide-publish mask per chunk)
+    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + 2 * (cap / 16 + 2) * 8) != hipSuccess) return VMQG_E_NOMEM;
     // publish lists: retry, whole-wave walks, eight wide lists (vmqg_kernels.hip kLists)
     if (hipMalloc(&d_deferred, 10 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
     keycache_cap = cap;
@@ -1015,6 +1016,7 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.keycache = d_keycache;
   a.keyspill = reinterpret_cast<uint2*>(static_cast<char*>(d_keycache) + keycache_cap * 32);
   a.chunk = reinterpret_cast<uint64_t*>(static_cast<char*>(d_keycache) + keycache_cap * (32 + 8 * 8));
+  a.widemask = a.chunk + (keycache_cap / 16 + 2);
   a.gpw = 64 / (opt_fast_g == 4 ? 4 : opt_fast_g == 1 ? 1 : 2);   // publishes per chunk
   a.status = d_status + kStatusSet * (call_seq & 1);
   a.status_next = d_status + kStatusSet * ((call_seq + 1) & 1);
@@ -1105,30 +1107,20 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   debug_sync(st, "COUNT wave tier");
   if (launch_scan(a, st, ev[4], ev[5]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "scan");
-  // EMIT: the fast tier (+ the wide publishes, and in records mode the
-  // whole-wave walks too unless fuse_walk is off), then the wave tier
+  // EMIT: the fast tier, then the tail (whole-wave walks, wide publishes)
   if (launch_match(a, 1, 0, st, ev[6], ev[7]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "EMIT");
-  const bool fused = !d_rng && (opt_flags & kOptFuseWalk);
-  if (fused) {
-    if (timing) {   // stage 4 made no launch: no events (collect_times counts it 0)
-      hipEventDestroy(ev[8]); hipEventDestroy(ev[9]);
-      t_ev.back()[8] = t_ev.back()[9] = nullptr;
-    }
-  } else if (launch_match(a, 1, 1, st, ev[8], ev[9]) != hipSuccess) {
-    return VMQG_E_DEVICE;
-  }
-  debug_sync(st, "EMIT wave tier");
+  if (launch_match(a, 1, 1, st, ev[8], ev[9]) != hipSuccess) return VMQG_E_DEVICE;
+  debug_sync(st, "EMIT tail");
   return VMQG_OK;
 }
 
 // Status words: two sets of per-call counters (kStatusSet words each: [0]
 // publishes the fast pass deferred to the 4-lane retry, [1] whole-wave walks
 // with a global stack, [2] scan ticket, [3] whole-wave walks, [4] wide
-// publishes, [5] fast-pass deferrals by a walk overflow, [6..7] entries
-// written by the EMIT wave tier, [8..15] wide publishes per XCD label,
-// [16..23] their tickets, [24..25] entries written by the wide phase) used by
-// alternate calls, then the error bits latched since the previous
+// publishes, [5] fast-pass deferrals by a walk overflow, [6..7] entries the
+// EMIT tail wrote for whole-wave walks, [24..25] ... for wide publishes)
+// used by alternate calls, then the error bits latched since the previous
 // vmqg_match_status.
 int Engine::match_status(hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;

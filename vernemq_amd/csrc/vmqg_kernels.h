@@ -38,12 +38,11 @@ struct MatchArgs {
   uint2* o_stack;                                 // wave tier: global frontier stacks, o_cap entries per wave
   uint32_t o_cap, o_waves;
   uint32_t* dbg;                                  // VMQG_DEBUG_SYNC only: per-wave progress words in host memory
-  uint32_t* o_slots;                              // o_waves bits: stacks borrowed by the fused phases
+  uint32_t* o_slots;                              // o_waves bits: stacks borrowed by the EMIT tail's walks
+  uint64_t* widemask;                             // per chunk of gpw publishes: its wide publishes (COUNT -> EMIT tail)
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
-constexpr uint32_t kOptWideInline = 8u; // wide publishes written by the EMIT wave that meets them (no lists)
-constexpr uint32_t kOptFuseWalk = 2u;   // EMIT's whole-wave walks in the fast EMIT launch (no EMIT wave launch)
 
 // mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier (grid a.o_waves / 4).
 // t0 / t1 (both or neither): timing events recorded by the kernel's own

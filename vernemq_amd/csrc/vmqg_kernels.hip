@@ -82,9 +82,7 @@ constexpr uint32_t kXcds = 8, kLists = 2 + kXcds;
   } while (0)
 enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, kStMany = 4, kStWalkOvf = 5,
                   kStWaveEnt = 6 /* u64: entries written by the EMIT wave tier (whole-wave walks) */,
-                  kStWideCount = 8 /* [8, 16): per XCD label */, kStWideTicket = 16 /* [16, 24) */,
-                  kStWideEnt = 24 /* u64: entries written by the wide phase */,
-                  kStWalkTicket = 26 /* fused walked phase of the fast EMIT (kOptFuseWalk) */,
+                  kStWideEnt = 24 /* u64: entries written for wide publishes by the EMIT tail */,
                   kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
 #define VMQG_WIDE_RECORDS 256   // publishes with at least this many records are written by the wide phase
@@ -612,23 +610,22 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
   return total;
 }
 
-// Appends the wide publishes among a wave's groups (fl == 1 on a group's
-// lane 0) to the wide list of their XCD label: one atomic per wave and label.
-template <int G, int OUT>
-__device__ __forceinline__ void append_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t xl,
-                                            uint32_t p) {
+// Marks the wide publishes among a wave's groups (fl == 1 on a group's lane
+// 0) in their chunk's 64-bit mask (bit = publish % gpw), which the EMIT tail
+// launch walks: the fast pass stores its chunk's whole mask (no atomics),
+// the retry ORs single bits into masks the fast pass already stored.
+template <int G, bool RETRY>
+__device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t p) {
   const uint64_t m_all = __ballot(g.lane == 0 && fl == 1);
-  if (!m_all) return;
-  if (__lane_id() == 0) atomicAdd(&a.status[kStMany], (uint32_t)__popcll(m_all));
-  if (OUT == 0 && (a.opts & kOptWideInline)) return;   // the records EMIT writes them where it finds them
-  for (uint32_t x = 0; x < kXcds; x++) {
-    const uint64_t m_x = __ballot(g.lane == 0 && fl == 1 && xl == x);
-    if (!m_x) continue;
-    uint32_t at = 0;
-    if (__lane_id() == 0) at = atomicAdd(&a.status[kStWideCount + x], (uint32_t)__popcll(m_x));
-    at = __shfl(at, 0, 64);
-    if (g.lane == 0 && fl == 1 && xl == x) a.deferred[(uint64_t)(2 + x) * a.npub + at + prefix_bits(m_x)] = p;
+  if (RETRY) {
+    if (g.lane == 0 && fl == 1)
+      atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + p / a.gpw), 1ull << (p % a.gpw));
+  } else {
+    uint64_t wm = 0;   // group bits -> publish bits of the chunk
+    for (uint64_t m = m_all; m; m &= m - 1) wm |= 1ull << ((uint32_t)__builtin_ctzll(m) / G);
+    if (__lane_id() == 0) a.widemask[p / a.gpw] = wm;   // p: the wave's first publish (+ its group index)
   }
+  if (m_all && __lane_id() == 0) atomicAdd(&a.status[kStMany], (uint32_t)__popcll(m_all));
 }
 
 // ------------------------------------------------------------- EMIT pass
@@ -769,26 +766,6 @@ __device__ void emit_many(const MatchArgs& a, uint32_t p, uint64_t ob, uint64_t 
   if (lane == 0 && run != oe - ob) atomicOr(a.err, kErrMismatch);
 }
 
-// kOptWideInline: the wide publishes among a wave's groups (resolve gave
-// kResMany), written by the whole wave right after the group pass, one after
-// the other — no publish lists, no atomics.
-template <int OUT, bool NT, int G>
-__device__ __forceinline__ uint64_t emit_wide_inline(const MatchArgs& a, const Group<G>& g, uint32_t first, int res,
-                                                     uint64_t ob, uint64_t oe, uint2* kb) {
-  uint64_t mm = __ballot(g.lane == 0 && res == kResMany), written = 0;
-  while (mm) {
-    const uint32_t l = (uint32_t)__builtin_ctzll(mm);
-    mm &= mm - 1;
-    const uint32_t p = first + l / G;
-    const uint64_t pob = uni64(((uint64_t)__shfl((uint32_t)(ob >> 32), l, 64) << 32) | __shfl((uint32_t)ob, l, 64));
-    const uint64_t poe = uni64(((uint64_t)__shfl((uint32_t)(oe >> 32), l, 64) << 32) | __shfl((uint32_t)oe, l, 64));
-    emit_many<OUT, NT, 8>(a, p, pob, poe, kb);
-    written += poe - pob;
-    wave_sync();
-  }
-  return written;
-}
-
 // Output ranges of the GPW publishes [first, first + n) of one chunk: the
 // chunk's base (the scanned chunk totals) plus the exclusive prefix of the
 // counts COUNT left in offsets[]; each group's lane 0 writes its publish's
@@ -812,12 +789,10 @@ __device__ __forceinline__ uint64_t chunk_offsets(const MatchArgs& a, uint32_t f
 // of one wave.  Resolve is per group; the copy is wave-wide over the wave's
 // output range minus the ranges of publishes the wave tier writes, so every
 // store instruction writes up to 64 x 16 B = 1 KiB contiguous.
-// Returns the group's resolve result (kResMany: a wide publish, written by
-// the caller) and its output range in [ob_out, oe_out).
 template <int G, int GPW, bool NT, int U, bool PRE = false>
-__device__ int emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const FastScratch<G>& s,
-                         const Group<G>& g, GroupMeta* gm, uint32_t slot0, uint64_t& ob_out, uint64_t& oe_out,
-                         uint64_t pre_obase = 0, uint64_t pre_oend = 0, uint64_t pre_wbase = 0) {
+__device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const FastScratch<G>& s,
+                          const Group<G>& g, GroupMeta* gm, uint32_t slot0, uint64_t pre_obase = 0,
+                          uint64_t pre_oend = 0, uint64_t pre_wbase = 0) {
   const uint32_t p = first + g.gidx;
   const bool valid = g.gidx < n;
   uint64_t obase = pre_obase, oend = pre_oend;
@@ -891,9 +866,6 @@ __device__ int emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const F
       if (w[u]) store_rec<NT>(a.out, dst[u], v[u]);
   }
   wave_sync();
-  ob_out = obase;
-  oe_out = oend;
-  return res;
 }
 
 // Range mode: each group writes its publish's non-empty keys as
@@ -922,69 +894,6 @@ __device__ int emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScrat
   const uint32_t nrem = (uint32_t)__popcll(rmask);
   for (uint32_t j = g.lane; j < nrem; j += G) store_range(a.out_rng, obase + pos + j, select_bit(rmask, j), 0u);
   return res;
-}
-
-// Output range [ob, oe) of publish p from the counts in the key cache (wave-wide).
-__device__ __forceinline__ void keycache_position(const MatchArgs& a, uint32_t p, uint64_t& ob, uint64_t& oe) {
-  const uint4* kc = reinterpret_cast<const uint4*>(a.keycache);
-  const uint32_t q = p - p % a.gpw + __lane_id();
-  const uint64_t before = q < p ? kc[(uint64_t)q * 2].x : 0u;   // a.gpw <= 64
-  ob = uni64(a.chunk[p / a.gpw] + __shfl(wave_incl_scan64(before), 63, 64));
-  oe = uni64(ob + kc[(uint64_t)p * 2].x);
-}
-
-// Second phase of the fast EMIT launch: the wide publishes, one whole wave
-// each, shared out statically — no ticket atomics (thousands of waves taking
-// tickets on a few counters at the end of the launch cost milliseconds).
-// Pass 1: the waves of XCD label x (blocks b with b % 8 == x: the
-// dispatcher's observed round-robin, a speed choice only; every label has
-// blocks, also in a grid of fewer than 8) take list x's first
-// min(n_x, avg) entries, so publishes of one key share an L2; pass 2:
-// what longer lists hold beyond avg goes round-robin to every wave.  A
-// publish's output position is its chunk's base (scanned) plus the counts of
-// the publishes before it in its chunk, read from the key cache (offsets[]
-// may still be being rewritten into positions by the wave owning the chunk).
-template <int OUT, bool NT>
-__device__ void emit_wide_phase(const MatchArgs& a, uint2* kb) {
-  uint32_t n[kXcds], total = 0;
-#pragma unroll
-  for (uint32_t x = 0; x < kXcds; x++) { n[x] = uni(a.status[kStWideCount + x]); total += n[x]; }
-  if (total == 0) return;
-  const uint32_t avg = (total + kXcds - 1) / kXcds;
-  uint64_t written = 0;
-  auto one = [&](uint32_t x, uint32_t i) {
-    const uint32_t p = uni(a.deferred[(uint64_t)(2 + x) * a.npub + i]);
-    DBGW(3, p);
-    uint64_t ob, oe;
-    keycache_position(a, p, ob, oe);
-    if (oe > (OUT ? a.rng_cap : a.out_cap)) {
-      if (__lane_id() == 0) atomicOr(a.err, kErrOverflow);
-      return;
-    }
-    emit_many<OUT, NT, 8>(a, p, ob, oe, kb);
-    written += oe - ob;
-    wave_sync();
-  };
-  const uint32_t wv = threadIdx.x >> 6;
-  // pass 1: the labels of the block's class (class = block % C; with fewer
-  // than 8 blocks, C = the block count and a class takes several labels)
-  const uint32_t C = gridDim.x < kXcds ? gridDim.x : kXcds, cls = blockIdx.x % C;
-  const uint32_t wx = ((gridDim.x - cls + C - 1) / C) * kWaves;   // waves of the class
-  for (uint32_t x = cls; x < kXcds; x += C) {
-    const uint32_t m1 = n[x] < avg ? n[x] : avg;
-    for (uint32_t i = (blockIdx.x / C) * kWaves + wv; i < m1; i += wx) one(x, i);
-  }
-  // pass 2: the overflow of longer lists, round-robin over every wave
-  const uint32_t W = gridDim.x * kWaves, gw = blockIdx.x * kWaves + wv;
-  uint32_t base = 0;
-  for (uint32_t y = 0; y < kXcds; y++) {
-    if (n[y] <= avg) continue;
-    const uint32_t len = n[y] - avg;
-    for (uint32_t j = (gw + W - base % W) % W; j < len; j += W) one(y, avg + j);
-    base += len;
-  }
-  if (written && __lane_id() == 0)
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)written);
 }
 
 // ============================================================== wave tier
@@ -1230,7 +1139,7 @@ __device__ uint32_t claim_ostack(const MatchArgs& a) {
 }
 
 template <int MODE, int OUT, bool NT>
-__device__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p, uint64_t ob, uint64_t oe) {
+__device__ __noinline__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p, uint64_t ob, uint64_t oe) {
   const uint32_t lane = __lane_id();
   WaveWalk<MODE, OUT, NT> w1(a, W, W.stack, kWStack, ob, oe);
   bool ok = w1.run_publish(p);
@@ -1281,7 +1190,7 @@ __device__ void count_deferred_wave(const MatchArgs& a, const FastScratch<4, SL>
       atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)c);
   }
   wave_sync();
-  if (retry) append_wide<4, OUT>(a, g, fl, xl, p);
+  if (retry) mark_wide<4, true>(a, g, fl, p);
   // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
   uint64_t ov = __ballot(valid && g.lane == 0 && fl >= 2);
   if (!retry && ov) {   // list 1 for EMIT (the retry's count_publish listed its own)
@@ -1294,29 +1203,6 @@ __device__ void count_deferred_wave(const MatchArgs& a, const FastScratch<4, SL>
     const uint32_t l = (uint32_t)__builtin_ctzll(ov);
     ov &= ov - 1;
     wave_publish<0, OUT, NT>(a, W, gstack, __shfl(p, l, 64), 0, 0);
-  }
-}
-
-// Third phase of the fast EMIT launch (kOptFuseWalk): the publishes COUNT's
-// wave tier walked with a whole wave (list 1), walked again and written here
-// instead of by an EMIT wave-tier launch of their own, shared out
-// round-robin over the waves of the launch.
-template <int OUT, bool NT>
-__device__ __noinline__ void emit_walked_phase(const MatchArgs& a, WaveLds& W) {
-  const uint32_t lane = __lane_id();
-  const uint32_t n = uni(a.status[kStWalked]);
-  if (n == 0) return;
-  uint2* const gstack = nullptr;   // borrowed when a walk outgrows its LDS stack
-  const uint32_t nw = gridDim.x * kWaves;
-  for (uint32_t t = blockIdx.x * kWaves + (threadIdx.x >> 6); t < n; t += nw) {   // static: no ticket atomics
-    const uint32_t p = uni(a.deferred[(uint64_t)a.npub + t]);
-    uint64_t ob, oe;
-    keycache_position(a, p, ob, oe);
-    if (oe > (OUT ? a.rng_cap : a.out_cap)) {
-      if (lane == 0) atomicOr(a.err, kErrOverflow);
-      continue;
-    }
-    wave_publish<1, OUT, NT>(a, W, gstack, p, ob, oe);
   }
 }
 
@@ -1348,47 +1234,15 @@ void k_match_fast(MatchArgs a) {
   using FS = FastScratch<G>;
   constexpr int GPW = FS::GPW;
   if (MODE == 0 && blockIdx.x == 0 && threadIdx.x < kStWords) a.status_next[threadIdx.x] = 0;
-  // LDS: COUNT {stack, candidates, keys}; EMIT {GroupMeta, keys} for its
-  // chunk pass, the same bytes as the four waves' WaveLds for the walked
-  // phase (after a block barrier), plus emit_many's key buffers
-  constexpr uint32_t kGmN = MODE == 1 && OUT == 0 ? GPW : 1;
-  constexpr uint32_t kStB = MODE == 0 ? FS::SC * FS::SLOTS * 8 : 0, kCdB = MODE == 0 ? FS::CC * FS::SLOTS * 4 : 0;
-  constexpr uint32_t kGmB = MODE == 1 ? kWaves * kGmN * (uint32_t)sizeof(GroupMeta) : 0;
-  constexpr uint32_t kKyB = FS::KC * FS::SLOTS * 8;
-  constexpr uint32_t kChunkB = kGmB + kStB + kCdB + kKyB;
-  constexpr uint32_t kWalkB = MODE == 1 && OUT == 0 ? kWaves * (uint32_t)sizeof(WaveLds) : 0;
-  __shared__ uint4 pool[((kChunkB > kWalkB ? kChunkB : kWalkB) + 15) / 16];
-  __shared__ uint2 kbuf[kWaves][MODE == 1 ? 64 : 1];   // emit_many's key buffer
-  uint8_t* pb = reinterpret_cast<uint8_t*>(pool);
-  auto gm = reinterpret_cast<GroupMeta(*)[kGmN]>(pb);
-  uint2* st = reinterpret_cast<uint2*>(pb + kGmB);
-  uint32_t* cd = reinterpret_cast<uint32_t*>(pb + kGmB + kStB);
-  uint2* ky = reinterpret_cast<uint2*>(pb + kGmB + kStB + kCdB);
+  __shared__ uint2 st[MODE == 0 ? FS::SC * FS::SLOTS : 1];
+  __shared__ uint32_t cd[MODE == 0 ? FS::CC * FS::SLOTS : 1];
+  __shared__ uint2 ky[FS::KC * FS::SLOTS];
+  __shared__ GroupMeta gm[kWaves][MODE == 1 && OUT == 0 ? GPW : 1];
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
-  // EMIT's phases after the chunk pass: the wide publishes, then (fused) the walked ones
-  uint64_t wide_written = 0;   // kOptWideInline: entries this wave wrote for wide publishes
-#ifndef VMQG_NO_WIDE
-#define VMQG_NO_WIDE 0   // A/B only: 1 = no wide / walked phases in EMIT (wrong for batches that have them)
-#endif
-  auto tail = [&]() {
-    if (VMQG_NO_WIDE) return;
-    DBGW(0, 2);
-    if (OUT == 0 && (a.opts & kOptWideInline)) {
-      if (wide_written && __lane_id() == 0)
-        atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)wide_written);
-    } else {
-      emit_wide_phase<OUT, NT>(a, kbuf[wv]);
-    }
-    if (OUT == 0 && (a.opts & kOptFuseWalk)) {   // records only: the range EMIT keeps 8 waves per SIMD
-      __syncthreads();   // every wave of the block is done with the chunk pass's LDS
-      DBGW(0, 3);
-      emit_walked_phase<OUT, NT>(a, reinterpret_cast<WaveLds*>(pb)[wv]);
-    }
-    DBGW(0, 9);
-  };
-  if (MODE == 1) DBGW(0, 1);
+  // EMIT writes every publish resolve can serve; the wide ones (kResMany)
+  // and the whole-wave walks (kDeferred) are the EMIT tail launch's
   if constexpr (MODE == 1 && CH != GPW) {
     // EMIT over the 64-publish chunks of a one-lane COUNT, as two halves of
     // GPW = 32 publishes with two lanes per publish
@@ -1405,19 +1259,14 @@ void k_match_fast(MatchArgs a) {
         const uint32_t q = h * GPW + g.gidx;
         const uint64_t ob = __shfl(pos, q, 64), oe = ob + __shfl(cnt, q, 64);
         const uint64_t wb = __shfl(pos, h * GPW, 64);
-        int res = kResSkip;
-        uint64_t rob = ob, roe = oe;
         if (OUT == 0) {
-          res = emit_wave<G, GPW, NT, VMQG_EMIT_U, true>(a, first, n, s, g, gm[wv], wv * GPW, rob, roe, ob, oe, wb);
+          emit_wave<G, GPW, NT, VMQG_EMIT_U, true>(a, first, n, s, g, gm[wv], wv * GPW, ob, oe, wb);
         } else if (g.gidx < n) {
-          res = emit_ranges_group<G>(a, first + g.gidx, s, g, ob, oe);
+          emit_ranges_group<G>(a, first + g.gidx, s, g, ob, oe);
         }
         wave_sync();
-        if (OUT == 0 && !VMQG_NO_WIDE && (a.opts & kOptWideInline))
-          wide_written += emit_wide_inline<OUT, NT, G>(a, g, first, res, rob, roe, kbuf[wv]);
       }
     }
-    tail();
     return;
   }
   const uint32_t stride = gridDim.x * kWaves * GPW;
@@ -1430,26 +1279,19 @@ void k_match_fast(MatchArgs a) {
       // the chunk's total (publishes the wave tier takes add theirs later)
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
-      // wide publishes go to EMIT's second phase, one atomic per wave and label
-      append_wide<G, OUT>(a, g, fl, xl, base + g.gidx);
+      // wide publishes: the chunk's mask for the EMIT tail launch
+      mark_wide<G, false>(a, g, fl, base);
       const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
       if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
+    } else if (OUT == 0) {
+      emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
     } else {
-      int res = kResSkip;
-      uint64_t ob = 0, oe = 0;
-      if (OUT == 0) {
-        res = emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW, ob, oe);
-      } else {
-        chunk_offsets<G, GPW>(a, base, n, g, ob, oe);
-        if (g.gidx < n) res = emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
-      }
-      wave_sync();
-      if (OUT == 0 && !VMQG_NO_WIDE && (a.opts & kOptWideInline))
-        wide_written += emit_wide_inline<OUT, NT, G>(a, g, base, res, ob, oe, kbuf[wv]);
+      uint64_t ob, oe;
+      chunk_offsets<G, GPW>(a, base, n, g, ob, oe);
+      if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
     }
     wave_sync();
   }
-  if constexpr (MODE == 1) tail();
 }
 
 // Wave tiers, one launch after each fast pass (each reads its list lengths
@@ -1465,8 +1307,12 @@ void k_match_fast(MatchArgs a) {
 //
 // EMIT: the whole-wave walks again (list 1); the wide publishes were written
 // by the fast EMIT launch's second phase.
+#ifndef VMQG_TAIL_WPE
+#define VMQG_TAIL_WPE 8   // EMIT tail: asks for 8 waves per SIMD; gfx950 build: 96 VGPRs, no spills, 5 waves
+#endif
 template <int MODE, int OUT, bool NT>
-__global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? VMQG_TAIL_WPE : 1)))
+void k_match_wave(MatchArgs a) {
   __shared__ WaveLds lds[kWaves];
   const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
@@ -1485,16 +1331,38 @@ __global__ __launch_bounds__(256) void k_match_wave(MatchArgs a) {
       count_deferred_wave<OUT, NT>(a, s, g, lds[wv], gstack, base, nd);
     return;
   } else {
+    // the whole-wave walks (list 1); a walk that outgrows its LDS stack
+    // borrows a global one (this grid has more waves than there are stacks)
+    const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
     const uint32_t n = uni(a.status[kStWalked]);
     for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
       const uint32_t p = uni(a.deferred[(uint64_t)a.npub + d]);
       const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
-      if (oe > (OUT ? a.rng_cap : a.out_cap) || ob > oe) {
+      if (oe > cap || ob > oe) {
         if (lane == 0) atomicOr(a.err, kErrOverflow);
         continue;
       }
-      wave_publish<1, OUT, NT>(a, lds[wv], gstack, p, ob, oe);
+      wave_publish<1, OUT, NT>(a, lds[wv], nullptr, p, ob, oe);
     }
+    // the wide publishes, from the chunk masks COUNT left, at the positions
+    // EMIT wrote into offsets[]
+    if (uni(a.status[kStMany]) == 0) return;
+    const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
+    uint64_t written = 0;
+    for (uint32_t c = (uint32_t)gw; c < nchunks; c += nwaves) {
+      for (uint64_t m = uni64(a.widemask[c]); m; m &= m - 1) {
+        const uint32_t p = c * a.gpw + (uint32_t)__builtin_ctzll(m);
+        const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
+        if (oe > cap || ob > oe) {
+          if (lane == 0) atomicOr(a.err, kErrOverflow);
+          continue;
+        }
+        emit_many<OUT, NT, 8>(a, p, ob, oe, lds[wv].keys);
+        written += oe - ob;
+        wave_sync();
+      }
+    }
+    if (written && lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)written);
   }
 }
 
@@ -1627,9 +1495,10 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, 
     else if (out) launch_fast<1, 1>(a, g, nt, st, t0, t1);
     else launch_fast<1, 0>(a, g, nt, st, t0, t1);
   } else {
-    // reads its list length on the device (exits at once when empty); one
-    // wave per deferred publish, each wave with its own global stack
-    const uint32_t g = a.o_waves / kWaves;
+    // reads its list lengths on the device (exits at once when empty).
+    // COUNT's: one wave per deferred publish, each wave with its own global
+    // stack; EMIT's tail: eight blocks per CU, global stacks borrowed
+    const uint32_t g = mode == 0 ? a.o_waves / kWaves : (uint32_t)a.cus * 8u;
     if (mode == 0) { if (out) launch_wave<0, 1>(a, g, nt, st, t0, t1); else launch_wave<0, 0>(a, g, nt, st, t0, t1); }
     else { if (out) launch_wave<1, 1>(a, g, nt, st, t0, t1); else launch_wave<1, 0>(a, g, nt, st, t0, t1); }
   }

@@ -319,8 +319,7 @@ class RegGpuView:
         _lib.check(self._L.vmqg_release_stream(self._h, stream or None), "vmqg_release_stream")
 
     def set_option(self, name: str, value: int):
-        """Kernel tuning knob (vmqg_set_option): "fast_g" 1|2|4, "nt_stores" 0|1, "fuse_walk" 0|1
-        (records mode: the whole-wave walks in the fast EMIT launch), "count_bpc" / "emit_bpc"."""
+        """Kernel tuning knob (vmqg_set_option): "fast_g" 1|2|4, "nt_stores" 0|1, "count_bpc" / "emit_bpc"."""
         _lib.check(self._L.vmqg_set_option(self._h, name.encode(), int(value)), "vmqg_set_option")
 
     def set_timing(self, on: bool):
