@@ -808,20 +808,14 @@ def bench_d(args):
         wait_ns = st1["apply_wait_ns"] - st0["apply_wait_ns"]
         host_ns = st1["apply_host_ns"] - st0["apply_host_ns"] - wait_ns   # host work, without GPU back-pressure
         # Each EMIT launch is charged only the records it writes (counted on
-        # the device): the fast EMIT launch writes every publish's records —
-        # the ordinary ones in its chunk pass, the wide ones ($share groups
-        # on 4 nodes: 40 keys; alarm lists: 1,000 records) in its second,
-        # XCD-labelled phase (stats wide_entries) — except those of the
-        # whole-wave walks, which the wave-tier launch writes (stats
-        # wave_entries).  Compulsory HBM bytes = 16 B written per record (the
-        # records read are the 16 MB of $share member lists, the 16 MB of
-        # alarm lists and the exact keys' records, cache-resident when their
-        # publishes share an XCD); SURVEY §8(d)'s 32 B per emission is
+        # the device): the fast EMIT launch writes every publish's records
+        # except the wide ones' ($share groups on 4 nodes: 40 keys; alarm
+        # lists: 1,000 records) and the whole-wave walks', which the EMIT
+        # tail launch writes (stats wide_entries, wave_entries).  Compulsory
+        # HBM bytes = 16 B written per record (the records read are the 16 MB
+        # of $share member lists, the 16 MB of alarm lists and the exact
+        # keys' records, cache-resident); SURVEY §8(d)'s 32 B per emission is
         # reported beside it.  The roofline line is the longer launch.
-        # The fast EMIT launch writes every publish's records except the
-        # wide ones' ($share groups on 4 nodes: 40 keys; alarm lists: 1,000
-        # records) and the whole-wave walks', which the EMIT tail launch
-        # writes (stats wide_entries, wave_entries).
         wave_rec = int(st1["wave_entries"])
         wide_rec = int(st1["wide_entries"])
         fast_rec = emitted - wave_rec - wide_rec
