@@ -1138,8 +1138,15 @@ __device__ uint32_t claim_ostack(const MatchArgs& a) {
   return __shfl(slot, 0, 64);
 }
 
+#ifndef VMQG_WALK_CALL
+#define VMQG_WALK_CALL 1   // A/B: 0 = the walk inlined into the wave-tier kernels
+#endif
 template <int MODE, int OUT, bool NT>
-__device__ __noinline__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p, uint64_t ob, uint64_t oe) {
+__device__ __attribute__((noinline)) void wave_publish_call(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p,
+                                                          uint64_t ob, uint64_t oe);
+template <int MODE, int OUT, bool NT>
+__device__ __forceinline__ void wave_publish_body(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p,
+                                                  uint64_t ob, uint64_t oe) {
   const uint32_t lane = __lane_id();
   WaveWalk<MODE, OUT, NT> w1(a, W, W.stack, kWStack, ob, oe);
   bool ok = w1.run_publish(p);
@@ -1168,6 +1175,17 @@ __device__ __noinline__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2*
     }
   }
   wave_sync();
+}
+template <int MODE, int OUT, bool NT>
+__device__ __attribute__((noinline)) void wave_publish_call(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p,
+                                                          uint64_t ob, uint64_t oe) {
+  wave_publish_body<MODE, OUT, NT>(a, W, gstack, p, ob, oe);
+}
+template <int MODE, int OUT, bool NT>
+__device__ __forceinline__ void wave_publish(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p, uint64_t ob,
+                                             uint64_t oe) {
+  if (VMQG_WALK_CALL) wave_publish_call<MODE, OUT, NT>(a, W, gstack, p, ob, oe);
+  else wave_publish_body<MODE, OUT, NT>(a, W, gstack, p, ob, oe);
 }
 
 // COUNT's deferred publishes [i0, i0 + 16) of list 0 (those < nd), one wave:
@@ -1498,7 +1516,10 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, 
     // reads its list lengths on the device (exits at once when empty).
     // COUNT's: one wave per deferred publish, each wave with its own global
     // stack; EMIT's tail: eight blocks per CU, global stacks borrowed
-    const uint32_t g = mode == 0 ? a.o_waves / kWaves : (uint32_t)a.cus * 8u;
+#ifndef VMQG_TAIL_BPC
+#define VMQG_TAIL_BPC 2   // EMIT tail blocks per CU (A/B: 2, 8; an empty launch of 8 per CU costs ~26 us)
+#endif
+    const uint32_t g = mode == 0 ? a.o_waves / kWaves : (uint32_t)a.cus * VMQG_TAIL_BPC;
     if (mode == 0) { if (out) launch_wave<0, 1>(a, g, nt, st, t0, t1); else launch_wave<0, 0>(a, g, nt, st, t0, t1); }
     else { if (out) launch_wave<1, 1>(a, g, nt, st, t0, t1); else launch_wave<1, 0>(a, g, nt, st, t0, t1); }
   }

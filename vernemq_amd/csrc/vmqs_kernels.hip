@@ -103,6 +103,10 @@ constexpr uint32_t kBitWords = kWaveMax / 32;
 #define VMQS_UNROLL 4
 #endif
 constexpr uint32_t kUnroll = VMQS_UNROLL;   // records in flight per lane (A/B: tools/build_variants.py)
+#ifndef VMQS_KIND_SCAN
+#define VMQS_KIND_SCAN 1   // A/B: 0 = no kind-word pre-pass
+#endif
+constexpr uint32_t kKindScan = 16;          // kind words in flight per lane in the pre-pass
 constexpr uint32_t kFOnL = 8u, kFOffL = 16u;
 
 struct alignas(8) WSlot { uint32_t group, flags; unsigned long long on_l, on_a, off_l, off_a; };
@@ -186,13 +190,69 @@ void k_select_wave(SArgs a) {
   const uint32_t mask = kWaveGroups - 1;
   const Record* rec = a.emits + s0;
   uint8_t* ch = a.chosen + s0;
+#if VMQS_KIND_SCAN
+  // pass 0: is there a shared member at all?  Only each record's kind word,
+  // kKindScan records per lane in flight (a 1,000-record segment in one
+  // round); most segments (exact and plain wildcard subscribers) have none
+  // and need neither the group table nor a second look at their records.
+  {
+    bool anyb = false;
+    for (uint32_t base = 0; base < n; base += 64 * kKindScan) {
+      uint32_t kw[kKindScan];
+#pragma unroll
+      for (uint32_t j = 0; j < kKindScan; j++) {
+        const uint32_t p = base + j * 64 + lane;
+        kw[j] = p < n ? rec[p].kind_node : 0u;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kKindScan; j++) anyb |= (kw[j] >> 24) == VMQG_EMIT_GROUP;
+      if (__ballot(anyb)) break;
+    }
+    if (!__ballot(anyb)) {
+      write_chosen(ch, n, nullptr, lane);
+      if (lane == 0 && a.failed) a.failed[i] = 0;
+      return;
+    }
+  }
+#endif
   for (uint32_t k = lane; k < kWaveGroups; k += 64) t[k] = WSlot{kEmpty, 0u, ~0ull, ~0ull, 0ull, 0ull};
   for (uint32_t k = lane; k < kBitWords; k += 64) win[w][k] = 0;
   lds_fence();
   __builtin_amdgcn_wave_barrier();
-  // pass 1: groups, local flags and keys in one read of the segment
+  // pass 1: groups, local flags and keys in one read of the segment.
+  // Members of a group are emitted contiguously, so most record instructions
+  // hold one group: each lane keeps running extremes for the wave's current
+  // group, and the wave reduces them and updates the group's slot only when
+  // the group changes (or at the end) — not per instruction.
   const uint64_t q = a.pub_seq + i;
   bool any = false, ovf = false;
+  uint32_t cg = kEmpty, cfl = 0;   // the current uniform group; this lane's flags for it
+  unsigned long long c_on_a = ~0ull, c_on_l = ~0ull, c_off_a = 0ull, c_off_l = 0ull;
+  auto flush = [&]() {
+    if (cg == kEmpty) return;
+    for (int o = 32; o > 0; o >>= 1) {
+      c_on_a = min(c_on_a, __shfl_xor(c_on_a, o));
+      c_on_l = min(c_on_l, __shfl_xor(c_on_l, o));
+      c_off_a = max(c_off_a, __shfl_xor(c_off_a, o));
+      c_off_l = max(c_off_l, __shfl_xor(c_off_l, o));
+    }
+    uint32_t fl = 0;
+    for (uint32_t b = 1; b <= kFOffL; b <<= 1) fl |= __ballot(cfl & b) ? b : 0u;
+    if (lane == 0) {
+      const uint32_t h = wslot_claim(t, mask, cg);
+      if (h == kEmpty) {
+        ovf = true;
+      } else {
+        if (fl) atomicOr(&t[h].flags, fl);
+        if (fl & kFOn) atomicMin(&t[h].on_a, c_on_a);
+        if (fl & kFOnL) atomicMin(&t[h].on_l, c_on_l);
+        if (fl & kFOff) atomicMax(&t[h].off_a, c_off_a);
+        if (fl & kFOffL) atomicMax(&t[h].off_l, c_off_l);
+      }
+    }
+    cg = kEmpty; cfl = 0;
+    c_on_a = ~0ull; c_on_l = ~0ull; c_off_a = 0ull; c_off_l = 0ull;
+  };
   for (uint32_t base = 0; base < n; base += 64 * kUnroll) {
     Record r[kUnroll];
 #pragma unroll
@@ -212,44 +272,26 @@ void k_select_wave(SArgs a) {
       const uint64_t mb = __ballot(isb);
       if (!mb) continue;
       any = true;
-      const uint32_t lead = __builtin_ctzll(mb);
-      const uint32_t g0 = __shfl(r[j].group, lead);
-      if (__ballot(isb && r[j].group != g0)) {   // mixed groups: per-lane atomics
+      const uint32_t g0 = __builtin_amdgcn_readfirstlane(__shfl(r[j].group, (uint32_t)__builtin_ctzll(mb)));
+      const bool mixed = __ballot(isb && r[j].group != g0) != 0;
+      if (mixed || g0 != cg) flush();
+      if (mixed) {   // mixed groups: per-lane atomics
         if (isb && !offer1(a, t, mask, r[j], sv[j], q, base + j * 64 + lane)) ovf = true;
         continue;
       }
-      // One group in this instruction (members of a group are emitted
-      // contiguously): reduce across the wave, then one lane updates the slot,
-      // instead of 64 serialised LDS atomics on one address.
-      const bool local = isb && node_of(r[j]) == a.local_node;
+      cg = g0;
+      if (!isb) continue;
+      const bool local = node_of(r[j]) == a.local_node;
       const uint32_t st = sv[j];
       const unsigned long long k = sel_key(a.seed, q, base + j * 64 + lane);
       const bool on = st == VMQS_ONLINE, off = st == VMQS_OFFLINE || st == VMQS_DRAINING;
-      unsigned long long on_a = on ? k : ~0ull, on_l = on && local ? k : ~0ull;
-      unsigned long long off_a = off ? k : 0ull, off_l = off && local ? k : 0ull;
-      for (int o = 32; o > 0; o >>= 1) {
-        on_a = min(on_a, __shfl_xor(on_a, o));
-        on_l = min(on_l, __shfl_xor(on_l, o));
-        off_a = max(off_a, __shfl_xor(off_a, o));
-        off_l = max(off_l, __shfl_xor(off_l, o));
-      }
-      const uint32_t fl = (__ballot(local) ? kFLocal : 0u) | (__ballot(on) ? kFOn : 0u) |
-                          (__ballot(on && local) ? kFOnL : 0u) | (__ballot(off) ? kFOff : 0u) |
-                          (__ballot(off && local) ? kFOffL : 0u);
-      if (lane == lead) {
-        const uint32_t h = wslot_claim(t, mask, g0);
-        if (h == kEmpty) {
-          ovf = true;
-        } else {
-          if (fl) atomicOr(&t[h].flags, fl);
-          if (fl & kFOn) atomicMin(&t[h].on_a, on_a);
-          if (fl & kFOnL) atomicMin(&t[h].on_l, on_l);
-          if (fl & kFOff) atomicMax(&t[h].off_a, off_a);
-          if (fl & kFOffL) atomicMax(&t[h].off_l, off_l);
-        }
-      }
+      cfl |= (local ? kFLocal : 0u) | (on ? kFOn : 0u) | (on && local ? kFOnL : 0u) | (off ? kFOff : 0u) |
+             (off && local ? kFOffL : 0u);
+      if (on) { c_on_a = min(c_on_a, k); if (local) c_on_l = min(c_on_l, k); }
+      if (off) { c_off_a = max(c_off_a, k); if (local) c_off_l = max(c_off_l, k); }
     }
   }
+  flush();
   if (__ballot(ovf)) {
     if (lane == 0) a.defer[atomicAdd(&a.status[0], 1u)] = i;
     return;
