@@ -13,8 +13,7 @@ from vernemq_amd import _lib  # noqa: E402
 VARIANTS = {
     "default": [],
     "tail8": ["-DVMQG_TAIL_BPC=8"],
-    "walkinline": ["-DVMQG_WALK_CALL=0"],
-    "tail8_walkinline": ["-DVMQG_TAIL_BPC=8", "-DVMQG_WALK_CALL=0"],
+    "walkcall": ["-DVMQG_WALK_CALL=1"],
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "nospill": ["-DVMQG_SPILL_KEYS=2"],
     "noalias": ["-DVMQG_HASH_ALIAS=0"],
@@ -23,7 +22,7 @@ VARIANTS = {
     "emit_u2": ["-DVMQG_EMIT_U=2"],
     "emit_u8": ["-DVMQG_EMIT_U=8"],
     "ss_u2": ["-DVMQS_UNROLL=2"],
-    "ss_nokind": ["-DVMQS_KIND_SCAN=0"],
+    "ss_kind": ["-DVMQS_KIND_SCAN=1"],
     "ss_wpe1": ["-DVMQS_WAVES_PER_EU=1"],
     "ss_wpe8_u8": ["-DVMQS_UNROLL=8"],
 }

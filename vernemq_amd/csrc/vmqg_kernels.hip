@@ -1139,7 +1139,7 @@ __device__ uint32_t claim_ostack(const MatchArgs& a) {
 }
 
 #ifndef VMQG_WALK_CALL
-#define VMQG_WALK_CALL 1   // A/B: 0 = the walk inlined into the wave-tier kernels
+#define VMQG_WALK_CALL 0   // A/B: 1 = the walk as a call (a kernel with a call sets up scratch: +4 us per empty launch)
 #endif
 template <int MODE, int OUT, bool NT>
 __device__ __attribute__((noinline)) void wave_publish_call(const MatchArgs& a, WaveLds& W, uint2* gstack, uint32_t p,
