@@ -14,6 +14,7 @@ VARIANTS = {
     "default": [],
     "tail8": ["-DVMQG_TAIL_BPC=8"],
     "walkcall": ["-DVMQG_WALK_CALL=1"],
+    "wide64": ["-DVMQG_WIDE_LANES=64"],
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "nospill": ["-DVMQG_SPILL_KEYS=2"],
     "noalias": ["-DVMQG_HASH_ALIAS=0"],

@@ -672,48 +672,56 @@ __device__ int resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, 
   return many ? kResMany : kResOk;
 }
 
-// Many-key publish p (key cache kMany), written by the whole wave into
-// [ob, oe): its candidates' node records (match/4, match_/3 :283-303) give
-// the keys, 64 at a time (lookup_subs/1 :87-94), then the exact key, then the
-// remote nodes in node order (fold_/5 :78-84) — the order and totals COUNT
-// used.  Records mode copies each batch of keys' records with 64 lanes x U
-// in flight (the key of each record from a per-lane cursor over `kb`, a
-// 64-entry LDS buffer of {record off, cum start}).
-template <int OUT, bool NT, int U>
-__device__ void emit_many(const MatchArgs& a, uint32_t p, uint64_t ob, uint64_t oe, uint2* kb) {
-  const uint32_t lane = __lane_id();
-  const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
-  const uint4 h = kc[0], k1 = kc[1];
-  const uint32_t nc = k1.x;
-  const uint64_t rmask = ((uint64_t)h.w << 32) | h.z;
-  const bool dollar = (a.pubs[p].flags & VMQG_PUB_DOLLAR) != 0;
-  // lane c < nc: candidate c; lane nc: the exact key
-  uint32_t nkeys = 0, key = 0, off0 = 0, cnt0 = 0;
-  if (lane < nc) {
-    const uint32_t path = reinterpret_cast<const uint32_t*>(a.keyspill)[(uint64_t)p * 2 * kSpillKeys + lane];
-    if (path < 2 * a.node_cap) {
-      const NodeRec r = a.nodes[path];
-      if ((r.meta & kNodeEmits) == kNodeEmits && !(dollar && (r.meta & kNodeDollarSkip))) {
-        nkeys = (r.meta >> 8) & 0xFFFFFFu;
-        key = r.key; off0 = r.off0; cnt0 = r.cnt0;
+// Wide publish p (key cache kMany), written by a group of SW lanes (two
+// publishes per wave at SW = 32, so one's chain of dependent metadata loads
+// overlaps the other's copy) into [ob, oe): its candidates' node records
+// (match/4, match_/3 :283-303) give the keys, SW at a time (lookup_subs/1
+// :87-94), then the exact key, then the remote nodes in node order (fold_/5
+// :78-84) — the order and totals COUNT used.  Records mode copies each batch
+// of keys' records with SW lanes x U in flight (the key of each record from
+// a per-lane cursor over `kb`, the group's SW-entry LDS buffer of {record
+// off, cum start}).  `act` false: the group has no publish (it still takes
+// part in nothing but the group-local shuffles).  Candidates <= 16 < SW.
+template <int OUT, bool NT, int U, int SW>
+__device__ void emit_many(const MatchArgs& a, const Group<SW>& g, bool act, uint32_t p, uint64_t ob, uint64_t oe,
+                          uint2* kb) {
+  static_assert(SW >= 32, "a lane per candidate (<= 16) plus one for the exact key");
+  const uint32_t lane = g.lane;
+  uint32_t nkeys = 0, key = 0, off0 = 0, cnt0 = 0, nc = 0;
+  uint64_t rmask = 0;
+  if (act) {
+    const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+    const uint4 h = kc[0], k1 = kc[1];
+    nc = k1.x;
+    rmask = ((uint64_t)h.w << 32) | h.z;
+    const bool dollar = (a.pubs[p].flags & VMQG_PUB_DOLLAR) != 0;
+    // lane c < nc: candidate c; lane nc: the exact key
+    if (lane < nc) {
+      const uint32_t path = reinterpret_cast<const uint32_t*>(a.keyspill)[(uint64_t)p * 2 * kSpillKeys + lane];
+      if (path < 2 * a.node_cap) {
+        const NodeRec r = a.nodes[path];
+        if ((r.meta & kNodeEmits) == kNodeEmits && !(dollar && (r.meta & kNodeDollarSkip))) {
+          nkeys = (r.meta >> 8) & 0xFFFFFFu;
+          key = r.key; off0 = r.off0; cnt0 = r.cnt0;
+        }
       }
+    } else if (lane == nc && k1.w != 0) {
+      nkeys = 1; off0 = k1.z; cnt0 = k1.w;
     }
-  } else if (lane == nc && k1.w != 0) {
-    nkeys = 1; off0 = k1.z; cnt0 = k1.w;
   }
-  const uint32_t kincl = wave_incl_scan32(nkeys);
-  const uint32_t K = __shfl(kincl, 63, 64);
+  const uint32_t kincl = g.incl_scan(nkeys);
+  const uint32_t K = g.last(kincl);
   const uint32_t kstart = kincl - nkeys;
   uint64_t run = 0;
   DBGW(6, K);
   DBGW(7, nc);
-  for (uint32_t k0 = 0; k0 < K; k0 += 64) {
+  for (uint32_t k0 = 0; k0 < K; k0 += SW) {
     const uint32_t ki = k0 + lane;
     // the candidate owning key ki: the last c whose keys start at or before it
     uint32_t c = 0;
-    for (uint32_t q = 1; q <= nc; q++) if (__shfl(kstart, q, 64) <= ki) c = q;
-    const uint32_t c_n = __shfl(nkeys, c, 64), c_key = __shfl(key, c, 64), c_ks = __shfl(kstart, c, 64);
-    const uint32_t c_off0 = __shfl(off0, c, 64), c_cnt0 = __shfl(cnt0, c, 64);
+    for (uint32_t q = 1; q <= nc; q++) if (g.bcast(kstart, q) <= ki) c = q;
+    const uint32_t c_n = g.bcast(nkeys, c), c_key = g.bcast(key, c), c_ks = g.bcast(kstart, c);
+    const uint32_t c_off0 = g.bcast(off0, c), c_cnt0 = g.bcast(cnt0, c);
     uint32_t off = 0, cnt = 0;
     if (ki < K) {
       if (c_n == 1) { off = c_off0; cnt = c_cnt0; }
@@ -723,22 +731,22 @@ __device__ void emit_many(const MatchArgs& a, uint32_t p, uint64_t ob, uint64_t 
       }
     }
     if (OUT == 1) {
-      const uint64_t mb = __ballot(cnt != 0);
+      const uint64_t mb = g.ballot(cnt != 0);
       if (cnt != 0 && ob + run + prefix_bits(mb) < oe) store_range(a.out_rng, ob + run + prefix_bits(mb), off, cnt);
       run += (uint32_t)__popcll(mb);
       continue;
     }
-    const uint32_t incl = wave_incl_scan32(cnt);
-    const uint32_t tot = __shfl(incl, 63, 64);
-    const uint32_t nb = K - k0 < 64u ? K - k0 : 64u;
+    const uint32_t incl = g.incl_scan(cnt);
+    const uint32_t tot = g.last(incl);
+    const uint32_t nb = K - k0 < (uint32_t)SW ? K - k0 : (uint32_t)SW;
     kb[lane] = make_uint2(off, incl - cnt);
     wave_sync();
     uint32_t j = 0;
-    for (uint32_t r0 = lane; r0 < tot; r0 += 64 * U) {
+    for (uint32_t r0 = lane; r0 < tot; r0 += SW * U) {
       uint4 v[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const uint32_t r = r0 + 64 * u;
+        const uint32_t r = r0 + SW * u;
         if (r < tot) {
           while (j + 1 < nb && kb[j + 1].y <= r) j++;
           const uint2 kk = kb[j];
@@ -747,7 +755,7 @@ __device__ void emit_many(const MatchArgs& a, uint32_t p, uint64_t ob, uint64_t 
       }
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const uint32_t r = r0 + 64 * u;
+        const uint32_t r = r0 + SW * u;
         if (r < tot && ob + run + r < oe) store_rec<NT>(a.out, ob + run + r, v[u]);
       }
     }
@@ -756,14 +764,14 @@ __device__ void emit_many(const MatchArgs& a, uint32_t p, uint64_t ob, uint64_t 
   }
   // remote nodes < 64 (COUNT already dropped the local node)
   const uint32_t nrem = (uint32_t)__popcll(rmask);
-  for (uint32_t j = lane; j < nrem; j += 64) {
+  for (uint32_t j = lane; j < nrem; j += SW) {
     const uint32_t node = select_bit(rmask, j);
     if (ob + run + j >= oe) break;
     if (OUT == 0) store_rec<NT>(a.out, ob + run + j, make_uint4((VMQG_EMIT_REMOTE << 24) | node, kNone, kNone, kNone));
     else store_range(a.out_rng, ob + run + j, node, 0u);
   }
   run += nrem;
-  if (lane == 0 && run != oe - ob) atomicOr(a.err, kErrMismatch);
+  if (act && lane == 0 && run != oe - ob) atomicOr(a.err, kErrMismatch);
 }
 
 // Output ranges of the GPW publishes [first, first + n) of one chunk: the
@@ -898,6 +906,10 @@ __device__ int emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScrat
 
 // ============================================================== wave tier
 constexpr uint32_t kWStack = 256, kWCand = 256, kWKeys = 256, kHiWords = kMaxNodes / 32;
+#ifndef VMQG_WIDE_LANES
+#define VMQG_WIDE_LANES 32   // lanes per wide publish in the EMIT tail (A/B: 32, 64)
+#endif
+constexpr int kWideLanes = VMQG_WIDE_LANES;
 
 struct WaveLds {
   uint2 stack[kWStack];   // tier 1's frontier stack
@@ -1363,24 +1375,37 @@ void k_match_wave(MatchArgs a) {
       wave_publish<1, OUT, NT>(a, lds[wv], nullptr, p, ob, oe);
     }
     // the wide publishes, from the chunk masks COUNT left, at the positions
-    // EMIT wrote into offsets[]
+    // EMIT wrote into offsets[]: two at a time, one per half-wave
     if (uni(a.status[kStMany]) == 0) return;
+    const Group<kWideLanes> h;
     const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
     uint64_t written = 0;
     for (uint32_t c = (uint32_t)gw; c < nchunks; c += nwaves) {
-      for (uint64_t m = uni64(a.widemask[c]); m; m &= m - 1) {
-        const uint32_t p = c * a.gpw + (uint32_t)__builtin_ctzll(m);
-        const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
-        if (oe > cap || ob > oe) {
-          if (lane == 0) atomicOr(a.err, kErrOverflow);
-          continue;
+      for (uint64_t m = uni64(a.widemask[c]); m;) {
+        uint32_t bit = 0;
+        bool act = false;
+#pragma unroll
+        for (uint32_t k = 0; k < 64 / kWideLanes; k++) {   // the k-th set bit goes to group k
+          const bool has = m != 0;
+          if (h.gidx == k) { act = has; bit = has ? (uint32_t)__builtin_ctzll(m) : 0u; }
+          if (has) m &= m - 1;
         }
-        emit_many<OUT, NT, 8>(a, p, ob, oe, lds[wv].keys);
-        written += oe - ob;
+        const uint32_t p = c * a.gpw + bit;
+        uint64_t ob = 0, oe = 0;
+        if (act) {
+          ob = a.offsets[p];
+          oe = a.offsets[p + 1];
+          if (oe > cap || ob > oe) {
+            if (h.lane == 0) atomicOr(a.err, kErrOverflow);
+            act = false;
+          }
+        }
+        emit_many<OUT, NT, 8, kWideLanes>(a, h, act, p, ob, oe, lds[wv].keys + h.gidx * kWideLanes);
+        if (act && h.lane == 0) written += oe - ob;
         wave_sync();
       }
     }
-    if (written && lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)written);
+    if (written) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)written);
   }
 }
 
