@@ -15,6 +15,8 @@ VARIANTS = {
     "tail8": ["-DVMQG_TAIL_BPC=8"],
     "walkcall": ["-DVMQG_WALK_CALL=1"],
     "wide64": ["-DVMQG_WIDE_LANES=64"],
+    "noxcd": ["-DVMQG_WIDE_XCD=0"],
+    "wide64_noxcd": ["-DVMQG_WIDE_LANES=64", "-DVMQG_WIDE_XCD=0"],
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "nospill": ["-DVMQG_SPILL_KEYS=2"],
     "noalias": ["-DVMQG_HASH_ALIAS=0"],

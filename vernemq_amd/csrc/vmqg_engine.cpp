@@ -944,8 +944,8 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     const uint64_t cap = next_pow2(std::max<uint64_t>(npub, 1024));
     // 32-B key cache + kSpillKeys x 8-B spilled keys per publish, then the
     // chunk totals (one per 16 or 32 publishes, + 1)
-    // (+ one 64-bit wide-publish mask per chunk)
-    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + 2 * (cap / 16 + 2) * 8) != hipSuccess) return VMQG_E_NOMEM;
+    // (+ per chunk a 64-bit wide-publish mask and three label planes)
+    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + 5 * (cap / 16 + 2) * 8) != hipSuccess) return VMQG_E_NOMEM;
     // publish lists: retry, whole-wave walks, eight wide lists (vmqg_kernels.hip kLists)
     if (hipMalloc(&d_deferred, 10 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
     keycache_cap = cap;
@@ -1017,6 +1017,7 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.keyspill = reinterpret_cast<uint2*>(static_cast<char*>(d_keycache) + keycache_cap * 32);
   a.chunk = reinterpret_cast<uint64_t*>(static_cast<char*>(d_keycache) + keycache_cap * (32 + 8 * 8));
   a.widemask = a.chunk + (keycache_cap / 16 + 2);
+  a.wideplane = a.widemask + (keycache_cap / 16 + 2);
   a.gpw = 64 / (opt_fast_g == 4 ? 4 : opt_fast_g == 1 ? 1 : 2);   // publishes per chunk
   a.status = d_status + kStatusSet * (call_seq & 1);
   a.status_next = d_status + kStatusSet * ((call_seq + 1) & 1);

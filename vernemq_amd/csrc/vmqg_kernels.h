@@ -40,6 +40,7 @@ struct MatchArgs {
   uint32_t* dbg;                                  // VMQG_DEBUG_SYNC only: per-wave progress words in host memory
   uint32_t* o_slots;                              // o_waves bits: stacks borrowed by the EMIT tail's walks
   uint64_t* widemask;                             // per chunk of gpw publishes: its wide publishes (COUNT -> EMIT tail)
+  uint64_t* wideplane;                            // per chunk: three bit planes of the wide publishes' XCD labels
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records

@@ -614,16 +614,38 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
 // 0) in their chunk's 64-bit mask (bit = publish % gpw), which the EMIT tail
 // launch walks: the fast pass stores its chunk's whole mask (no atomics),
 // the retry ORs single bits into masks the fast pass already stored.
+// Each wide publish also gets a 3-bit XCD label (xl: a hash of its first
+// candidate, else of its exact key), kept as three bit planes next to the
+// mask: the tail gives a chunk's label-x publishes to a wave of XCD x, so
+// publishes of one key meet that key's records in one L2.
+template <int G>
+__device__ __forceinline__ uint64_t group_bits_to_publish_bits(uint64_t m) {
+  uint64_t wm = 0;
+  for (; m; m &= m - 1) wm |= 1ull << ((uint32_t)__builtin_ctzll(m) / G);
+  return wm;
+}
+
 template <int G, bool RETRY>
-__device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t p) {
-  const uint64_t m_all = __ballot(g.lane == 0 && fl == 1);
+__device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t xl, uint32_t p) {
+  const bool w = g.lane == 0 && fl == 1;
+  const uint64_t m_all = __ballot(w);
+  const uint32_t c = p / a.gpw;
   if (RETRY) {
-    if (g.lane == 0 && fl == 1)
-      atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + p / a.gpw), 1ull << (p % a.gpw));
-  } else {
-    uint64_t wm = 0;   // group bits -> publish bits of the chunk
-    for (uint64_t m = m_all; m; m &= m - 1) wm |= 1ull << ((uint32_t)__builtin_ctzll(m) / G);
-    if (__lane_id() == 0) a.widemask[p / a.gpw] = wm;   // p: the wave's first publish (+ its group index)
+    if (w) {
+      const unsigned long long bit = 1ull << (p % a.gpw);
+      atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + c), bit);
+      for (uint32_t k = 0; k < 3; k++)
+        if ((xl >> k) & 1) atomicOr(reinterpret_cast<unsigned long long*>(a.wideplane + 3ull * c + k), bit);
+    }
+  } else {   // p: the wave's first publish; the chunk's mask and planes stored whole
+    const uint64_t wm = group_bits_to_publish_bits<G>(m_all);
+    const uint64_t p0 = group_bits_to_publish_bits<G>(__ballot(w && (xl & 1)));
+    const uint64_t p1 = group_bits_to_publish_bits<G>(__ballot(w && (xl & 2)));
+    const uint64_t p2 = group_bits_to_publish_bits<G>(__ballot(w && (xl & 4)));
+    if (__lane_id() == 0) {
+      a.widemask[c] = wm;
+      a.wideplane[3ull * c] = p0; a.wideplane[3ull * c + 1] = p1; a.wideplane[3ull * c + 2] = p2;
+    }
   }
   if (m_all && __lane_id() == 0) atomicAdd(&a.status[kStMany], (uint32_t)__popcll(m_all));
 }
@@ -910,6 +932,9 @@ constexpr uint32_t kWStack = 256, kWCand = 256, kWKeys = 256, kHiWords = kMaxNod
 #define VMQG_WIDE_LANES 32   // lanes per wide publish in the EMIT tail (A/B: 32, 64)
 #endif
 constexpr int kWideLanes = VMQG_WIDE_LANES;
+#ifndef VMQG_WIDE_XCD
+#define VMQG_WIDE_XCD 1   // A/B: 0 = wide publishes by chunk owner, no XCD labels
+#endif
 
 struct WaveLds {
   uint2 stack[kWStack];   // tier 1's frontier stack
@@ -1220,7 +1245,7 @@ __device__ void count_deferred_wave(const MatchArgs& a, const FastScratch<4, SL>
       atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)c);
   }
   wave_sync();
-  if (retry) mark_wide<4, true>(a, g, fl, p);
+  if (retry) mark_wide<4, true>(a, g, fl, xl, p);
   // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
   uint64_t ov = __ballot(valid && g.lane == 0 && fl >= 2);
   if (!retry && ov) {   // list 1 for EMIT (the retry's count_publish listed its own)
@@ -1310,7 +1335,7 @@ void k_match_fast(MatchArgs a) {
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
       // wide publishes: the chunk's mask for the EMIT tail launch
-      mark_wide<G, false>(a, g, fl, base);
+      mark_wide<G, false>(a, g, fl, xl, base);
       const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
       if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
     } else if (OUT == 0) {
@@ -1380,8 +1405,20 @@ void k_match_wave(MatchArgs a) {
     const Group<kWideLanes> h;
     const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
     uint64_t written = 0;
-    for (uint32_t c = (uint32_t)gw; c < nchunks; c += nwaves) {
-      for (uint64_t m = uni64(a.widemask[c]); m;) {
+    // VMQG_WIDE_XCD: the waves of XCD class x (block % 8) visit every chunk
+    // and take its label-x publishes; otherwise every wave its own chunks
+    const bool by_xcd = VMQG_WIDE_XCD && gridDim.x >= kXcds;
+    const uint32_t x = blockIdx.x % kXcds;
+    const uint32_t c0 = by_xcd ? (blockIdx.x / kXcds) * kWaves + wv : (uint32_t)gw;
+    const uint32_t cs = by_xcd ? ((gridDim.x - x + kXcds - 1) / kXcds) * kWaves : nwaves;
+    for (uint32_t c = c0; c < nchunks; c += cs) {
+      uint64_t m0 = uni64(a.widemask[c]);
+      if (by_xcd && m0) {
+        const uint64_t q0 = uni64(a.wideplane[3ull * c]), q1 = uni64(a.wideplane[3ull * c + 1]),
+                       q2 = uni64(a.wideplane[3ull * c + 2]);
+        m0 &= ((x & 1) ? q0 : ~q0) & ((x & 2) ? q1 : ~q1) & ((x & 4) ? q2 : ~q2);
+      }
+      for (uint64_t m = m0; m;) {
         uint32_t bit = 0;
         bool act = false;
 #pragma unroll
