@@ -14,9 +14,10 @@ VARIANTS = {
     "default": [],
     "tail8": ["-DVMQG_TAIL_BPC=8"],
     "walkcall": ["-DVMQG_WALK_CALL=1"],
-    "wide64": ["-DVMQG_WIDE_LANES=64"],
-    "noxcd": ["-DVMQG_WIDE_XCD=0"],
-    "wide64_noxcd": ["-DVMQG_WIDE_LANES=64", "-DVMQG_WIDE_XCD=0"],
+    "wide32": ["-DVMQG_WIDE_LANES=32"],
+    "xcd": ["-DVMQG_WIDE_XCD=1"],
+    "tail3": ["-DVMQG_TAIL_BPC=3"],
+    "tail4": ["-DVMQG_TAIL_BPC=4"],
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "nospill": ["-DVMQG_SPILL_KEYS=2"],
     "noalias": ["-DVMQG_HASH_ALIAS=0"],

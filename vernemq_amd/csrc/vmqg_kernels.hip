@@ -929,11 +929,11 @@ __device__ int emit_ranges_group(const MatchArgs& a, uint32_t p, const FastScrat
 // ============================================================== wave tier
 constexpr uint32_t kWStack = 256, kWCand = 256, kWKeys = 256, kHiWords = kMaxNodes / 32;
 #ifndef VMQG_WIDE_LANES
-#define VMQG_WIDE_LANES 32   // lanes per wide publish in the EMIT tail (A/B: 32, 64)
+#define VMQG_WIDE_LANES 64   // lanes per wide publish in the EMIT tail (A/B, config D: 64 -> 2,606 us, 32 -> 3,056)
 #endif
 constexpr int kWideLanes = VMQG_WIDE_LANES;
 #ifndef VMQG_WIDE_XCD
-#define VMQG_WIDE_XCD 1   // A/B: 0 = wide publishes by chunk owner, no XCD labels
+#define VMQG_WIDE_XCD 0   // A/B: 1 = label-x publishes by XCD-x waves (config D: 17.0 ms vs 2.6 ms, off)
 #endif
 
 struct WaveLds {
