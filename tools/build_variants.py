@@ -16,8 +16,9 @@ VARIANTS = {
     "walkcall": ["-DVMQG_WALK_CALL=1"],
     "wide32": ["-DVMQG_WIDE_LANES=32"],
     "xcd": ["-DVMQG_WIDE_XCD=1"],
-    "tail3": ["-DVMQG_TAIL_BPC=3"],
-    "tail4": ["-DVMQG_TAIL_BPC=4"],
+    "nowalk": ["-DVMQG_TAIL_NOWALK=1"],
+    "nowalk_u16": ["-DVMQG_TAIL_NOWALK=1", "-DVMQG_TAIL_U=16"],
+    "tail_u4": ["-DVMQG_TAIL_U=4"],
     "count_wpe5": ["-DVMQG_COUNT_WPE=5"],
     "nospill": ["-DVMQG_SPILL_KEYS=2"],
     "noalias": ["-DVMQG_HASH_ALIAS=0"],

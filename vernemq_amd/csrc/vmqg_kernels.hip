@@ -932,6 +932,9 @@ constexpr uint32_t kWStack = 256, kWCand = 256, kWKeys = 256, kHiWords = kMaxNod
 #define VMQG_WIDE_LANES 64   // lanes per wide publish in the EMIT tail (A/B, config D: 64 -> 2,606 us, 32 -> 3,056)
 #endif
 constexpr int kWideLanes = VMQG_WIDE_LANES;
+#ifndef VMQG_TAIL_U
+#define VMQG_TAIL_U 8   // records in flight per lane in the tail's wide copies
+#endif
 #ifndef VMQG_WIDE_XCD
 #define VMQG_WIDE_XCD 0   // A/B: 1 = label-x publishes by XCD-x waves (config D: 17.0 ms vs 2.6 ms, off)
 #endif
@@ -1389,7 +1392,10 @@ void k_match_wave(MatchArgs a) {
     // the whole-wave walks (list 1); a walk that outgrows its LDS stack
     // borrows a global one (this grid has more waves than there are stacks)
     const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
-    const uint32_t n = uni(a.status[kStWalked]);
+#ifndef VMQG_TAIL_NOWALK
+#define VMQG_TAIL_NOWALK 0   // A/B only (wrong with walked publishes): the tail without its walker
+#endif
+    const uint32_t n = VMQG_TAIL_NOWALK ? 0u : uni(a.status[kStWalked]);
     for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
       const uint32_t p = uni(a.deferred[(uint64_t)a.npub + d]);
       const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
@@ -1397,7 +1403,7 @@ void k_match_wave(MatchArgs a) {
         if (lane == 0) atomicOr(a.err, kErrOverflow);
         continue;
       }
-      wave_publish<1, OUT, NT>(a, lds[wv], nullptr, p, ob, oe);
+      if (!VMQG_TAIL_NOWALK) wave_publish<1, OUT, NT>(a, lds[wv], nullptr, p, ob, oe);
     }
     // the wide publishes, from the chunk masks COUNT left, at the positions
     // EMIT wrote into offsets[]: two at a time, one per half-wave
@@ -1437,7 +1443,7 @@ void k_match_wave(MatchArgs a) {
             act = false;
           }
         }
-        emit_many<OUT, NT, 8, kWideLanes>(a, h, act, p, ob, oe, lds[wv].keys + h.gidx * kWideLanes);
+        emit_many<OUT, NT, VMQG_TAIL_U, kWideLanes>(a, h, act, p, ob, oe, lds[wv].keys + h.gidx * kWideLanes);
         if (act && h.lane == 0) written += oe - ob;
         wave_sync();
       }
@@ -1579,7 +1585,7 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, 
     // COUNT's: one wave per deferred publish, each wave with its own global
     // stack; EMIT's tail: eight blocks per CU, global stacks borrowed
 #ifndef VMQG_TAIL_BPC
-#define VMQG_TAIL_BPC 2   // EMIT tail blocks per CU (A/B: 2, 8; an empty launch of 8 per CU costs ~26 us)
+#define VMQG_TAIL_BPC 8   // EMIT tail blocks per CU (A/B, config D tail: 8 -> 2,269 us, 3 -> 2,418, 2 -> 2,605; C's empty tail 4.4 vs 4.1 us)
 #endif
     const uint32_t g = mode == 0 ? a.o_waves / kWaves : (uint32_t)a.cus * VMQG_TAIL_BPC;
     if (mode == 0) { if (out) launch_wave<0, 1>(a, g, nt, st, t0, t1); else launch_wave<0, 0>(a, g, nt, st, t0, t1); }
