@@ -376,9 +376,16 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
     if (nrecs) *nrecs = 0;
     return 0;
   }
+  /* records are copies: the read lock is let go while the batch waits for
+   * the device, so an apply can land between this batch's prepare and its
+   * match (its word ids stay valid: the dictionary only grows) and a writer
+   * never waits for a queue of device calls.  Ranges index the host record
+   * table: they keep the lock until the caller has folded them. */
+  if (!ranges) vmqgb_view_read_end(v);
   pthread_mutex_lock(&v->device);
   int rc = ranges ? vmqgb_match_ranges(b, v->ctx) : vmqgb_match(b, v->ctx);
   pthread_mutex_unlock(&v->device);
+  if (!ranges) vmqgb_view_read_begin(v);
   if (!rc && ranges && recs && nrecs) rc = vmqg_records_at(v->ctx, b->epoch, recs, nrecs);
   return rc;
 }

@@ -132,9 +132,13 @@ vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v);
  * at once; vmqgb_view_match serialises only the device call. */
 void vmqgb_view_read_begin(vmqgb_view* v);
 void vmqgb_view_read_end(vmqgb_view* v);
-/* Under the read lock: vmqgb_match or vmqgb_match_ranges (ranges != 0) with
- * the device to itself; in range mode also the record table of the match's
- * epoch (vmqg_records_at) for vmqgb_fold_ranges. */
+/* Called under the read lock, returns under it: vmqgb_match or
+ * vmqgb_match_ranges (ranges != 0) with the device to itself; in range mode
+ * also the record table of the match's epoch (vmqg_records_at) for
+ * vmqgb_fold_ranges.  In records mode the lock is let go while the batch
+ * waits for the device (an apply may land between its prepare and its
+ * match: word and term ids only ever grow); range mode keeps it, as its
+ * entries index the host record table. */
 int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs);
 /* Table changes (vmqg_apply_ops, the term tables of the caller): writers. */
 void vmqgb_view_write_begin(vmqgb_view* v);
