@@ -16,7 +16,7 @@ VARIANTS = {
     "walkcall": ["-DVMQG_WALK_CALL=1"],
     "wide32": ["-DVMQG_WIDE_LANES=32"],
     "xcd": ["-DVMQG_WIDE_XCD=1"],
-    "norecwide": ["-DVMQG_WIDE_RECORDS=0x7fffffff"],
+    "recwide256": ["-DVMQG_WIDE_RECORDS=256"],
     "nowalk": ["-DVMQG_TAIL_NOWALK=1"],
     "nowalk_u16": ["-DVMQG_TAIL_NOWALK=1", "-DVMQG_TAIL_U=16"],
     "tail_u4": ["-DVMQG_TAIL_U=4"],

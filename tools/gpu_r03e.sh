@@ -9,3 +9,5 @@ O=gpurun_out/$T
 mkdir -p $O
 timeout -k 10 900 python3 -u bench.py --config E > $O/bench_E.json 2> $O/bench_E.err || { tail -20 $O/bench_E.err; exit 2; }
 cat $O/bench_E.json
+timeout -k 10 500 python3 -u bench.py --config D --no-cpu-baseline > $O/bench_D.json 2> $O/bench_D.err || { tail -20 $O/bench_D.err; exit 3; }
+cat $O/bench_D.json

@@ -85,7 +85,7 @@ enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, k
                   kStWideEnt = 24 /* u64: entries written for wide publishes by the EMIT tail */,
                   kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
-#define VMQG_WIDE_RECORDS 256   // publishes with at least this many records are written by the wide phase
+#define VMQG_WIDE_RECORDS 0x7fffffff   // A/B: a publish with at least this many records is wide too (256: config D 2,724 vs 2,526 us per batch, off)
 #endif
 enum : uint32_t { kErrFrontier = 2u, kErrOverflow = 4u, kErrMismatch = 8u };   // kErrLookback = 16 (lookback.h)
 
