@@ -19,4 +19,6 @@ for v in default nofilter; do
   VMQG_LIB_PATH=build/ab/lib_$v.so timeout -k 10 300 python tools/ab_match.py --config E --rounds 2 --steps 10 > $O/e_$v.json 2> $O/e_$v.err || { tail -5 $O/e_$v.err; exit 5; }
   echo "E $v $(cat $O/e_$v.json)"
 done
+timeout -k 10 400 tools/bin/nif_harness 2 > $O/nif.jsonl 2> $O/nif.err || { tail -5 $O/nif.err; exit 6; }
+cat $O/nif.jsonl
 echo done
