@@ -17,6 +17,7 @@ VARIANTS = {
     "wide32": ["-DVMQG_WIDE_LANES=32"],
     "xcd": ["-DVMQG_WIDE_XCD=1"],
     "recwide256": ["-DVMQG_WIDE_RECORDS=256"],
+    "nofilter": ["-DVMQG_EXACT_FILTER=0"],
     "nowalk": ["-DVMQG_TAIL_NOWALK=1"],
     "nowalk_u16": ["-DVMQG_TAIL_NOWALK=1", "-DVMQG_TAIL_U=16"],
     "tail_u4": ["-DVMQG_TAIL_U=4"],

@@ -22,6 +22,8 @@
 //             record off + count, remote-node mask}: the `{Topic, node()}`
 //             candidate of fold/4 (:62) plus vmq_trie_remote_subs (:143, :514-520).
 //   exwords : u32 pool: per exact topic its MP then its word ids (exactness check).
+//   exbits  : one bit per fingerprint class of the exact topics (8 per exact slot):
+//             a publish whose bit is clear skips the exact-table probe.
 #pragma once
 #include <stdint.h>
 
@@ -94,7 +96,9 @@ struct Layout {
   uint64_t max_mountpoints;
   uint64_t local_node;
   uint64_t max_depth;        // deepest trie path (sizes the wave tier's global stack)
-  uint64_t pad[13];
+  uint64_t exbits_off;       // exact-topic filter: one bit per fingerprint class, set for every
+  uint64_t exbits_words;     // ... exact topic placed since the last re-layout (u32 words, power of two)
+  uint64_t pad[11];
 };
 static_assert(sizeof(Layout) == 256, "layout must be 256 bytes");
 constexpr uint64_t kLayoutMagic = 0x31676D7176ull;  // "vmqg1"
@@ -121,5 +125,10 @@ VMQG_HD uint64_t fp_word(uint32_t word, uint32_t pos) {
 VMQG_HD uint64_t fp_final(uint64_t sum, uint32_t mp, uint32_t nwords) {
   return mix64(sum + mix64(((uint64_t)mp << 32) | nwords));
 }
+// The exact-topic filter's bit for a fingerprint (bits: a power of two): a
+// clear bit means no exact topic has that fingerprint, so the exact table
+// (a random HBM line) need not be probed.  Bits are never cleared between
+// re-layouts: a deleted topic's bit only costs a probe that misses.
+VMQG_HD uint64_t exbit_of(uint64_t fp, uint64_t bits) { return (fp >> 24) & (bits - 1); }
 
 }  // namespace vmqg

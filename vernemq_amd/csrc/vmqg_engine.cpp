@@ -301,6 +301,7 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) c
   const uint64_t exact_slots = next_pow2(std::max<uint64_t>(4096, std::max<uint64_t>(ex * 2 + 1024, cfg.hint_exact * 2)));
   L.exact_buckets = exact_slots / kExactSlotsPerBucket;
   L.exwords_cap = std::max<uint64_t>({16384, xw * 2, cfg.hint_exact * 8});
+  L.exbits_words = std::max<uint64_t>(2048, exact_slots * 8 / 32);   // 8 bits per exact slot, 8 KiB at least
   uint64_t o = 0;
   if (!compact && lay.total_bytes) {   // a growth re-layout never shrinks a region
     L.edge_buckets = std::max<uint64_t>(L.edge_buckets, lay.edge_buckets);
@@ -310,9 +311,10 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) c
     L.rec_cap = std::max<uint64_t>(L.rec_cap, lay.rec_cap);
     L.exact_buckets = std::max<uint64_t>(L.exact_buckets, lay.exact_buckets);
     L.exwords_cap = std::max<uint64_t>(L.exwords_cap, lay.exwords_cap);
+    L.exbits_words = std::max<uint64_t>(L.exbits_words, lay.exbits_words);
   }
   L.edge_buckets *= scale; L.node_cap *= scale; L.key_cap *= scale; L.keylist_cap *= scale;
-  L.rec_cap *= scale; L.exact_buckets *= scale; L.exwords_cap *= scale;
+  L.rec_cap *= scale; L.exact_buckets *= scale; L.exwords_cap *= scale; L.exbits_words *= scale;
   L.edge_off = o;    o = align256(o + L.edge_buckets * kEdgeSlotsPerBucket * sizeof(EdgeSlot));
   L.node_off = o;    o = align256(o + 2 * L.node_cap * sizeof(NodeRec));   // records, then '#'-child aliases
   L.keydesc_off = o; o = align256(o + L.key_cap * sizeof(KeyDesc));
@@ -320,6 +322,7 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) c
   L.rec_off = o;     o = align256(o + L.rec_cap * sizeof(Record));
   L.exact_off = o;   o = align256(o + L.exact_buckets * kExactSlotsPerBucket * sizeof(ExactSlot));
   L.exwords_off = o; o = align256(o + L.exwords_cap * sizeof(uint32_t));
+  L.exbits_off = o;  o = align256(o + L.exbits_words * sizeof(uint32_t));
   L.total_bytes = o;
   return L;
 }
@@ -559,6 +562,12 @@ bool Engine::write_topic(uint32_t ti) {
         exact_live++;
         t.slot = found;
         tab[found].fp = fp;
+        const uint64_t bit = exbit_of(fp, lay.exbits_words * 32);
+        uint32_t* xb = region<uint32_t>(lay.exbits_off) + (bit >> 5);
+        if (!(*xb & (1u << (bit & 31)))) {
+          *xb |= 1u << (bit & 31);
+          touch(lay.exbits_off + (bit >> 5) * 4, 4);
+        }
         break;
       }
       b = (b + 1) & mask;
@@ -1009,6 +1018,8 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.exact = reinterpret_cast<const ExactSlot*>(d_arena + lay.exact_off);
   a.exact_mask = lay.exact_buckets - 1;
   a.exwords = reinterpret_cast<const uint32_t*>(d_arena + lay.exwords_off);
+  a.exbits = reinterpret_cast<const uint32_t*>(d_arena + lay.exbits_off);
+  a.exbits_mask = lay.exbits_words * 32 - 1;
   a.max_mp = (uint32_t)lay.max_mountpoints;
   a.local_node = (uint32_t)lay.local_node;
   a.pubs = pubs; a.words = words; a.npub = npub;

@@ -15,6 +15,7 @@ struct MatchArgs {
   const Record* records;
   const ExactSlot* exact; uint64_t exact_mask;    // bucket mask
   const uint32_t* exwords;
+  const uint32_t* exbits; uint64_t exbits_mask;   // exact-topic filter (bits - 1)
   uint32_t max_mp, local_node;
   const vmqg_pub* pubs; const uint32_t* words; uint32_t npub, pad0;
   uint64_t* offsets;                              // npub + 1

@@ -50,6 +50,9 @@
 namespace vmqg {
 
 constexpr int kWaves = 4;          // waves per 256-thread block
+#ifndef VMQG_EXACT_FILTER
+#define VMQG_EXACT_FILTER 1        // A/B: 0 = always probe the exact table
+#endif
 #ifndef VMQG_EMIT_U
 #define VMQG_EMIT_U 8              // records in flight per lane in the fast EMIT copy (A/B: 2, 4, 8)
 #endif
@@ -279,6 +282,11 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
                                        const Group<G>& g) {
   const uint32_t L = pub.nwords;
   const uint64_t fp = publish_fp<G>(pub, w, wreg, g);
+#if VMQG_EXACT_FILTER
+  // the filter's bit (an L2-resident word) before the table's random line
+  const uint64_t xb = exbit_of(fp, a.exbits_mask + 1);
+  if (!((a.exbits[xb >> 5] >> (xb & 31)) & 1u)) return nullptr;
+#endif
   uint64_t b = fp & a.exact_mask;
   for (uint64_t iter = 0; iter <= a.exact_mask; iter++) {
     const ExactSlot* bk = a.exact + b * kExactSlotsPerBucket;
