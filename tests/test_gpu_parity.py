@@ -795,10 +795,11 @@ def test_released_stream_can_be_destroyed():
 @pytest.mark.parametrize("fast_g", [1, 2])
 def test_wide_publishes_by_record_count(mode, fast_g):
     """Publishes of one or two keys but hundreds of records (a/+ with 300
-    subscribers, plus an exact one) are wide: written wave-wide by the fast
-    EMIT launch's second phase from the wide list of their XCD label, in
-    batches that mix them with one-record publishes and with publishes of
-    several hundred records under other keys."""
+    subscribers, plus an exact one), in batches that mix them with
+    one-record publishes and with publishes of several hundred records under
+    other keys: the fast EMIT copies them (wide publishes are those with more
+    keys than the spill slots hold, not with many records: VMQG_WIDE_RECORDS,
+    A/B in DESIGN.md), and every publish's records equal the oracle's."""
     node = "n@h"
     prod = _driver(node, mode)
     prod.view.set_option("fast_g", fast_g)
@@ -819,7 +820,7 @@ def test_wide_publishes_by_record_count(mode, fast_g):
     idx = np.random.RandomState(9).randint(0, len(kinds), size=12_000)
     recs, offs = prod.match_arrays(arr[idx], words)
     st = v.stats_raw()
-    assert st["many_key"] > 0 and st["deferred_tier1"] == 0, st
+    assert st["many_key"] == 0 and st["deferred_tier1"] == 0, st
     counts = np.diff(offs.astype(np.int64))
     assert np.array_equal(counts, np.array([len(x) for x in want], dtype=np.int64)[idx])
     for i in range(0, len(idx), 5):
