@@ -364,6 +364,10 @@ void vmqgb_view_free(vmqgb_view* v) {
 vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v) { return v->ctx; }
 void vmqgb_view_read_begin(vmqgb_view* v) { pthread_rwlock_rdlock(&v->tables); }
 void vmqgb_view_read_end(vmqgb_view* v) { pthread_rwlock_unlock(&v->tables); }
+void vmqgb_view_yield(vmqgb_view* v) {   /* a waiting writer goes first (writer-preferring lock) */
+  pthread_rwlock_unlock(&v->tables);
+  pthread_rwlock_rdlock(&v->tables);
+}
 void vmqgb_view_write_begin(vmqgb_view* v) { pthread_rwlock_wrlock(&v->tables); }
 void vmqgb_view_write_end(vmqgb_view* v) { pthread_rwlock_unlock(&v->tables); }
 

@@ -132,6 +132,13 @@ vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v);
  * at once; vmqgb_view_match serialises only the device call. */
 void vmqgb_view_read_begin(vmqgb_view* v);
 void vmqgb_view_read_end(vmqgb_view* v);
+/* Lets a waiting writer in and takes the read lock back: a batcher calls it
+ * every VMQGB_YIELD_EVERY publishes while it prepares a batch, and while it
+ * folds a records-mode batch (ids only ever grow, so what it prepared or
+ * matched stays valid), so an apply waits for one slice of a batch, not for
+ * every reader's whole batch. */
+void vmqgb_view_yield(vmqgb_view* v);
+#define VMQGB_YIELD_EVERY 512
 /* Called under the read lock, returns under it: vmqgb_match or
  * vmqgb_match_ranges (ranges != 0) with the device to itself; in range mode
  * also the record table of the match's epoch (vmqg_records_at) for

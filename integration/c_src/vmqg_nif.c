@@ -310,6 +310,7 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     const ERL_NIF_TERM* el;
     ErlNifBinary topic;
     uint32_t mp;
+    if (i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(r->view);
     enif_get_list_cell(env, tail, &head, &tail);
     if (!enif_get_tuple(env, head, &arity, &el) || arity != 2 || !enif_inspect_iolist_as_binary(env, el[1], &topic)) {
       idx[i] = VMQG_E_INVAL;
@@ -326,6 +327,7 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   uint64_t nrecs = 0;
   const int rc = vmqgb_view_match(r->view, b, ranges, &recs, &nrecs);
   for (unsigned i = 0; i < n; i++) {
+    if (!ranges && i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(r->view);   /* records: copies */
     if (idx[i] < 0 || rc) { res[i] = error_term(env, idx[i] < 0 ? (int)idx[i] : rc); continue; }
     size_t cnt = 0;
     if (ranges) {

@@ -82,6 +82,7 @@ static void* batcher(void* p) {
     vmqgb_view_read_begin(view);
     vmqgb_batch_reset(&b);
     for (size_t i = 0; i < a->B; i++) {
+      if (i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(view);
       const size_t q = (lo + i) % NPUB;
       if (vmqgb_batch_add(&b, ctx, 0, (const uint8_t*)topics + q * 40, tlen[q]) < 0) { a->err = 1; break; }
     }
@@ -91,8 +92,10 @@ static void* batcher(void* p) {
     uint64_t nrecs = 0;
     int rc = vmqgb_view_match(view, &b, a->ranges, &recs, &nrecs);
     const double t2 = now();
-    for (size_t i = 0; !rc && i < b.n; i++)
+    for (size_t i = 0; !rc && i < b.n; i++) {
+      if (!a->ranges && i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(view);   /* records: copies */
       rc = a->ranges ? vmqgb_fold_ranges(&b, recs, nrecs, i, sum_entry, acc) : vmqgb_fold(&b, i, sum_entry, acc);
+    }
     vmqgb_view_read_end(view);
     const double t3 = now();
     if (rc || a->err) { a->err = rc ? rc : a->err; break; }
