@@ -368,8 +368,18 @@ void vmqgb_view_yield(vmqgb_view* v) {   /* a waiting writer goes first (writer-
   pthread_rwlock_unlock(&v->tables);
   pthread_rwlock_rdlock(&v->tables);
 }
-void vmqgb_view_write_begin(vmqgb_view* v) { pthread_rwlock_wrlock(&v->tables); }
-void vmqgb_view_write_end(vmqgb_view* v) { pthread_rwlock_unlock(&v->tables); }
+/* A writer takes the device mutex too: a records-mode batch matches without
+ * the read lock, and an apply changes what a match reads (the layout, the
+ * arena, the staging ring).  Order: the write lock, then the mutex; a mutex
+ * holder never waits for the table lock, so no cycle. */
+void vmqgb_view_write_begin(vmqgb_view* v) {
+  pthread_rwlock_wrlock(&v->tables);
+  pthread_mutex_lock(&v->device);
+}
+void vmqgb_view_write_end(vmqgb_view* v) {
+  pthread_mutex_unlock(&v->device);
+  pthread_rwlock_unlock(&v->tables);
+}
 
 int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
   if (b->n == 0) {   /* nothing to match: empty results */

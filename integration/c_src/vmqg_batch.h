@@ -147,7 +147,8 @@ void vmqgb_view_yield(vmqgb_view* v);
  * match: word and term ids only ever grow); range mode keeps it, as its
  * entries index the host record table. */
 int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs);
-/* Table changes (vmqg_apply_ops, the term tables of the caller): writers. */
+/* Table changes (vmqg_apply_ops, the term tables of the caller): writers;
+ * write_begin takes the device mutex as well (after the table lock). */
 void vmqgb_view_write_begin(vmqgb_view* v);
 void vmqgb_view_write_end(vmqgb_view* v);
 int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);   /* write_begin, apply, write_end */
