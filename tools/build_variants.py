@@ -28,6 +28,8 @@ VARIANTS = {
     "scan8": ["-DVMQG_SCAN_ITEMS=8"],
     "emit_u2": ["-DVMQG_EMIT_U=2"],
     "emit_u8": ["-DVMQG_EMIT_U=8"],
+    "emit_u12": ["-DVMQG_EMIT_U=12"],
+    "emit_u16": ["-DVMQG_EMIT_U=16"],
     "ss_u2": ["-DVMQS_UNROLL=2"],
     "ss_kind": ["-DVMQS_KIND_SCAN=1"],
     "ss_wpe1": ["-DVMQS_WAVES_PER_EU=1"],
