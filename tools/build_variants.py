@@ -34,6 +34,12 @@ VARIANTS = {
     "ss_kind": ["-DVMQS_KIND_SCAN=1"],
     "ss_wpe1": ["-DVMQS_WAVES_PER_EU=1"],
     "ss_wpe8_u8": ["-DVMQS_UNROLL=8"],
+    "rt_tile256": ["-DVMQR_TILE_ROWS=256"],
+    "rt_tile512": ["-DVMQR_TILE_ROWS=512"],
+    "rt_tile512_u8": ["-DVMQR_TILE_ROWS=512", "-DVMQR_U=8"],
+    "rt_tile2048": ["-DVMQR_TILE_ROWS=2048"],
+    "rt_u2": ["-DVMQR_U=2"],
+    "rt_u8": ["-DVMQR_U=8"],
 }
 
 
