@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VMQG_ABI_VERSION 3
+#define VMQG_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------- */
 #define VMQG_OK 0
@@ -96,6 +96,8 @@ typedef struct vmqg_op {
 
 /* ---- publishes and matches ------------------------------------------- */
 #define VMQG_PUB_DOLLAR 1u   /* first topic word starts with '$' (MQTT-4.7.2-1) */
+#define VMQG_PUB_UNKNOWN 2u  /* set by vmqg_prepare_publish*: a word was not in the dictionary
+                                (VMQG_WORD_UNKNOWN); ignored by the match */
 
 typedef struct vmqg_pub {
   uint32_t mountpoint;
@@ -183,6 +185,26 @@ int vmqg_intern_words(vmqg_ctx* ctx, const uint8_t* bytes, const uint64_t* offs,
  * reference rejects. */
 int vmqg_prepare_publish(vmqg_ctx* ctx, uint32_t mountpoint, const uint8_t* topic, size_t len,
                          uint32_t* words_out, uint32_t cap, vmqg_pub* pub);
+
+/* Batched vmqg_prepare_publish (ABI 4): n topics at once, their dictionary
+ * probes software-pipelined (a block of topics' lookups is prefetched before
+ * any is resolved) — the per-publish host cost of a fold/4 batch.  Topic i is
+ * topics[i][0 .. lens[i]) of mountpoint mountpoints[i].  rc_out[i] = 0 or
+ * VMQG_E_INVAL (validate_topic rejects it: pubs_out[i] is zeroed and it has no
+ * words); pubs_out[i].word_off indexes words_out.  A topic of len bytes has at
+ * most len + 1 words: with wcap >= sum(lens[i] + 1) the call cannot overflow;
+ * otherwise it may return VMQG_E_OVERFLOW (outputs undefined).  *nwords_out =
+ * word ids written.  Same read-only contract as vmqg_prepare_publish. */
+int vmqg_prepare_publishes(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints, const uint8_t* const* topics,
+                           const size_t* lens, vmqg_pub* pubs_out, int32_t* rc_out, uint32_t* words_out,
+                           size_t wcap, size_t* nwords_out);
+
+/* Words interned so far: grows whenever a filter brings a new word.  A
+ * publish prepared with VMQG_PUB_UNKNOWN before the dictionary grew may name
+ * a word that has subscriptions now, so it must be prepared again before it
+ * is matched on newer tables (integration/c_src/vmqg_batch.c does).  Safe to
+ * call concurrently with writers (an atomic read). */
+uint64_t vmqg_dict_generation(vmqg_ctx* ctx);
 
 /* ---- deltas --------------------------------------------------------- */
 /* Applies a batch of subscribe/unsubscribe ops with the exact semantics of
@@ -275,6 +297,37 @@ int vmqg_records(vmqg_ctx* ctx, const vmqg_emit** recs, uint64_t* n);
  * refusals too. */
 int vmqg_epoch(vmqg_ctx* ctx, uint64_t* epoch);
 int vmqg_records_at(vmqg_ctx* ctx, uint64_t epoch, const vmqg_emit** recs, uint64_t* n);
+
+/* ---- pipelined host-buffer matching (ABI 4) ---------------------------- */
+/* vmqg_match_batch is one synchronous round trip.  A host that matches many
+ * batches back to back (the NIF's combining submitter, integration/c_src/
+ * vmqg_batch.c) keeps several in flight instead: an hbatch owns pinned host
+ * and device buffers for one batch, and its three phases are separate calls
+ *   submit   H2D of the inputs (on the hbatch's own copy stream), then the
+ *            match and the D2H of its offsets on the context's stream;
+ *            returns at once.  Needs the context to itself (like every call
+ *            that changes or reads device tables): callers serialise it with
+ *            vmqg_apply_ops and the other match calls.
+ *   offsets  waits for the match; *total = entries.  VMQG_E_OVERFLOW when the
+ *            output did not fit (the hbatch's output grows to *total for the
+ *            next submit: submit again), VMQG_E_FRONTIER likewise (the next
+ *            submit uses a larger wave-tier stack).
+ *   entries  D2H of the entries on the hbatch's copy stream; waits.
+ * offsets and entries touch only the hbatch: they may run while another
+ * thread submits the next batch (its H2D and kernels overlap this batch's
+ * D2H).  Results are those of the table epoch *epoch (vmqg_epoch at submit).
+ * Each submit also collects and clears the error bits its own match latched,
+ * so hbatches in flight never report each other's errors (and a
+ * vmqg_match_status afterwards does not see them). */
+typedef struct vmqg_hbatch vmqg_hbatch;
+vmqg_hbatch* vmqg_hbatch_new(vmqg_ctx* ctx);
+void vmqg_hbatch_free(vmqg_hbatch* hb);
+/* pinned input buffers with room for npub publishes and nwords word ids */
+int vmqg_hbatch_inputs(vmqg_hbatch* hb, size_t npub, size_t nwords, vmqg_pub** pubs, uint32_t** words);
+/* ranges != 0: vmqg_match_ranges semantics (8-B entries), else vmqg_match_batch (16-B records) */
+int vmqg_hbatch_submit(vmqg_ctx* ctx, vmqg_hbatch* hb, size_t npub, size_t nwords, int ranges);
+int vmqg_hbatch_offsets(vmqg_hbatch* hb, const uint64_t** offsets, uint64_t* total, uint64_t* epoch);
+int vmqg_hbatch_entries(vmqg_hbatch* hb, const void** entries);
 
 /* ---- introspection --------------------------------------------------- */
 int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out);

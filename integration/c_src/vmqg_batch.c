@@ -133,15 +133,34 @@ int vmqgb_batch_init(vmqgb_batch* b, size_t cap_hint) {
   return 0;
 }
 
-void vmqgb_batch_reset(vmqgb_batch* b) { b->n = b->nwords = b->out_n = b->rng_n = 0; }
+void vmqgb_batch_reset(vmqgb_batch* b) {
+  b->n = b->nwords = b->out_n = b->rng_n = 0;
+  b->n_unk = b->raw_n = 0;
+  b->dict_gen = 0;
+}
 
 void vmqgb_batch_free(vmqgb_batch* b) {
-  free(b->pubs); free(b->words); free(b->offsets); free(b->out); free(b->rng);
+  free(b->pubs); free(b->words); free(b->offs_buf); free(b->out); free(b->rng_buf);
+  free(b->unk); free(b->raw);
   memset(b, 0, sizeof(*b));
+}
+
+/* remembers publish i's raw topic when it holds a word the dictionary did not know */
+static int note_unknown(vmqgb_batch* b, size_t i, const uint8_t* topic, size_t len) {
+  if (grow((void**)&b->unk, &b->unk_cap, 3 * (b->n_unk + 1), sizeof(uint32_t))) return VMQG_E_NOMEM;
+  if (grow((void**)&b->raw, &b->raw_cap, b->raw_n + len, 1)) return VMQG_E_NOMEM;
+  memcpy(b->raw + b->raw_n, topic, len);
+  b->unk[3 * b->n_unk] = (uint32_t)i;
+  b->unk[3 * b->n_unk + 1] = (uint32_t)b->raw_n;
+  b->unk[3 * b->n_unk + 2] = (uint32_t)len;
+  b->n_unk++;
+  b->raw_n += len;
+  return 0;
 }
 
 long vmqgb_batch_add(vmqgb_batch* b, vmqg_ctx* ctx, uint32_t mountpoint, const uint8_t* topic, size_t len) {
   if (grow((void**)&b->pubs, &b->cap, b->n + 1, sizeof(vmqg_pub))) return VMQG_E_NOMEM;
+  if (b->n == 0) b->dict_gen = vmqg_dict_generation(ctx);
   /* a topic of len bytes has at most len + 1 words */
   size_t room = b->wcap - b->nwords;
   if (room < 16 && grow((void**)&b->words, &b->wcap, b->nwords + 16, sizeof(uint32_t))) return VMQG_E_NOMEM;
@@ -156,15 +175,79 @@ long vmqgb_batch_add(vmqgb_batch* b, vmqg_ctx* ctx, uint32_t mountpoint, const u
     }
     if (rc) return rc;
     pub.word_off = (uint32_t)b->nwords;
+    if ((pub.flags & VMQG_PUB_UNKNOWN) && note_unknown(b, b->n, topic, len)) return VMQG_E_NOMEM;
     b->nwords += pub.nwords;
     b->pubs[b->n] = pub;
     return (long)b->n++;
   }
 }
 
+int vmqgb_batch_add_many(vmqgb_batch* b, vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints,
+                         const uint8_t* const* topics, const size_t* lens, long* idx_out) {
+  if (!n) return 0;
+  if (b->n == 0) b->dict_gen = vmqg_dict_generation(ctx);
+  size_t need = 0;
+  for (size_t i = 0; i < n; i++) need += lens[i] + 1;
+  if (grow((void**)&b->pubs, &b->cap, b->n + n, sizeof(vmqg_pub))) return VMQG_E_NOMEM;
+  if (grow((void**)&b->words, &b->wcap, b->nwords + need, sizeof(uint32_t))) return VMQG_E_NOMEM;
+  int32_t stack_rc[256];
+  int32_t* rcs = n <= 256 ? stack_rc : (int32_t*)malloc(n * sizeof(int32_t));
+  if (!rcs) return VMQG_E_NOMEM;
+  vmqg_pub* P = b->pubs + b->n;
+  size_t nw = 0;
+  int rc = vmqg_prepare_publishes(ctx, n, mountpoints, topics, lens, P, rcs, b->words + b->nwords, b->wcap - b->nwords, &nw);
+  if (rc) { if (rcs != stack_rc) free(rcs); return rc; }
+  /* compact: rejected topics take no slot in the batch */
+  size_t k = b->n;
+  for (size_t i = 0; i < n; i++) {
+    if (rcs[i]) { idx_out[i] = rcs[i]; continue; }
+    vmqg_pub pub = P[i];
+    pub.word_off += (uint32_t)b->nwords;
+    if ((pub.flags & VMQG_PUB_UNKNOWN) && note_unknown(b, k, topics[i], lens[i])) { rc = VMQG_E_NOMEM; break; }
+    b->pubs[k] = pub;
+    idx_out[i] = (long)k++;
+  }
+  if (rcs != stack_rc) free(rcs);
+  if (rc) return rc;
+  b->n = k;
+  b->nwords += nw;
+  return 0;
+}
+
+int vmqgb_batch_recheck(vmqgb_batch* b, vmqg_ctx* ctx) {
+  if (!b->n_unk) return 0;
+  const uint64_t gen = vmqg_dict_generation(ctx);
+  if (gen == b->dict_gen) return 0;
+  int changed = 0;
+  uint32_t tmp[64];
+  for (size_t u = 0; u < b->n_unk; u++) {
+    vmqg_pub* pub = &b->pubs[b->unk[3 * u]];
+    const uint8_t* t = b->raw + b->unk[3 * u + 1];
+    const size_t len = b->unk[3 * u + 2];
+    uint32_t* w = pub->nwords <= 64 ? tmp : (uint32_t*)malloc(pub->nwords * sizeof(uint32_t));
+    if (!w) return VMQG_E_NOMEM;
+    vmqg_pub np;
+    const int rc = vmqg_prepare_publish(ctx, pub->mountpoint, t, len, w, pub->nwords, &np);
+    if (!rc && np.nwords == pub->nwords && memcmp(w, b->words + pub->word_off, np.nwords * sizeof(uint32_t))) {
+      memcpy(b->words + pub->word_off, w, np.nwords * sizeof(uint32_t));
+      pub->flags = np.flags;
+      changed = 1;
+    }
+    if (w != tmp) free(w);
+    if (rc) return rc;
+  }
+  b->dict_gen = gen;
+  return changed;
+}
+
 int vmqgb_batch_append(vmqgb_batch* dst, const vmqgb_batch* src) {
   if (grow((void**)&dst->pubs, &dst->cap, dst->n + src->n, sizeof(vmqg_pub))) return VMQG_E_NOMEM;
   if (grow((void**)&dst->words, &dst->wcap, dst->nwords + src->nwords, sizeof(uint32_t))) return VMQG_E_NOMEM;
+  if (dst->n == 0 || (src->n && src->dict_gen < dst->dict_gen)) dst->dict_gen = src->dict_gen;
+  for (size_t u = 0; u < src->n_unk; u++) {
+    const uint32_t* e = src->unk + 3 * u;
+    if (note_unknown(dst, dst->n + e[0], src->raw + e[1], e[2])) return VMQG_E_NOMEM;
+  }
   memcpy(dst->words + dst->nwords, src->words, src->nwords * sizeof(uint32_t));
   for (size_t i = 0; i < src->n; i++) {
     vmqg_pub p = src->pubs[i];
@@ -176,16 +259,16 @@ int vmqgb_batch_append(vmqgb_batch* dst, const vmqgb_batch* src) {
   return 0;
 }
 
-static int ensure_offsets(vmqgb_batch* b) {   /* n + 1 entries, sized per call */
-  void* p = realloc(b->offsets, (b->n + 1) * sizeof(uint64_t));
-  if (!p) return VMQG_E_NOMEM;
-  b->offsets = (uint64_t*)p;
+static int ensure_offsets(vmqgb_batch* b) {   /* n + 1 owned entries */
+  if (grow((void**)&b->offs_buf, &b->offs_cap, b->n + 1, sizeof(uint64_t))) return VMQG_E_NOMEM;
+  b->offsets = b->offs_buf;
   return 0;
 }
 
 int vmqgb_match(vmqgb_batch* b, vmqg_ctx* ctx) {
   if (ensure_offsets(b)) return VMQG_E_NOMEM;
   if (!b->out_cap && grow((void**)&b->out, &b->out_cap, b->n * 4 + 64, sizeof(vmqg_emit))) return VMQG_E_NOMEM;
+  if (vmqg_epoch(ctx, &b->epoch)) return VMQG_E_INVAL;
   for (;;) {
     size_t need = 0;
     const int rc = vmqg_match_batch(ctx, b->pubs, b->n, b->words, b->nwords, b->out, b->out_cap, &need, b->offsets);
@@ -202,12 +285,14 @@ int vmqgb_match(vmqgb_batch* b, vmqg_ctx* ctx) {
 int vmqgb_match_ranges(vmqgb_batch* b, vmqg_ctx* ctx) {
   if (ensure_offsets(b)) return VMQG_E_NOMEM;
   if (vmqg_epoch(ctx, &b->epoch)) return VMQG_E_INVAL;
-  if (!b->rng_cap && grow((void**)&b->rng, &b->rng_cap, b->n * 2 + 64, sizeof(vmqg_range))) return VMQG_E_NOMEM;
+  if (!b->rng_cap && grow((void**)&b->rng_buf, &b->rng_cap, b->n * 2 + 64, sizeof(vmqg_range))) return VMQG_E_NOMEM;
+  b->rng = b->rng_buf;
   for (;;) {
     size_t need = 0;
     const int rc = vmqg_match_ranges(ctx, b->pubs, b->n, b->words, b->nwords, b->rng, b->rng_cap, &need, b->offsets);
     if (rc == VMQG_E_OVERFLOW && need > b->rng_cap) {
-      if (grow((void**)&b->rng, &b->rng_cap, need, sizeof(vmqg_range))) return VMQG_E_NOMEM;
+      if (grow((void**)&b->rng_buf, &b->rng_cap, need, sizeof(vmqg_range))) return VMQG_E_NOMEM;
+      b->rng = b->rng_buf;
       continue;
     }
     if (rc) return rc;
@@ -334,10 +419,41 @@ int vmqgb_ops_apply(vmqgb_ops* o, vmqg_ctx* ctx, uint64_t* epoch) {
 }
 
 /* ------------------------------------------------------------------ view */
+/* One combined device call in flight (or folded from): the batches it
+ * serves, its pinned buffers (vmqg_hbatch) and its results. */
+typedef struct vmqgb_req vmqgb_req;
+struct vmqgb_req {
+  vmqgb_batch* b;
+  int dev_ranges;            /* device mode wanted: 1 ranges, 0 records */
+  int done, rc;
+  size_t base;               /* first publish of the batch in its round */
+  struct vmqgb_round* round;
+  vmqgb_req* next;
+};
+
+typedef struct vmqgb_round {
+  vmqg_hbatch* hb;
+  int busy;                  /* taken by a combiner, or leased by batches still reading it */
+  int refs;
+  int dev_ranges;
+  const uint64_t* offs;      /* results (pinned, the hbatch's) */
+  const void* out;
+  uint64_t epoch;
+} vmqgb_round;
+
 struct vmqgb_view {
   vmqg_ctx* ctx;
-  pthread_rwlock_t tables;   /* readers: batchers; writers: applies */
-  pthread_mutex_t device;    /* one device call at a time */
+  pthread_rwlock_t tables;   /* readers: batchers; writers: applies, interning */
+  pthread_mutex_t device;    /* the context's device side (submits, applies) */
+  pthread_mutex_t q_mu;      /* the queue, the rounds, the counters */
+  pthread_cond_t q_cv;
+  vmqgb_req* q_head;
+  vmqgb_req* q_tail;
+  int in_kernels;            /* rounds submitted whose offsets are not back */
+  int pipelined;             /* the context has a device: hbatch rounds */
+  int device_records;
+  vmqgb_round rounds[VMQGB_ROUNDS];
+  vmqgb_view_stats st;
 };
 
 vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx) {
@@ -350,14 +466,24 @@ vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx) {
   const int r1 = pthread_rwlock_init(&v->tables, &a);
   pthread_rwlockattr_destroy(&a);
   const int r2 = pthread_mutex_init(&v->device, NULL);
-  if (r1 || r2) { free(v); return NULL; }
+  const int r3 = pthread_mutex_init(&v->q_mu, NULL);
+  const int r4 = pthread_cond_init(&v->q_cv, NULL);
+  if (r1 || r2 || r3 || r4) { free(v); return NULL; }
+  v->pipelined = 1;
+  for (int i = 0; i < VMQGB_ROUNDS; i++) {
+    v->rounds[i].hb = vmqg_hbatch_new(ctx);   /* NULL on a host-engine-only context */
+    if (!v->rounds[i].hb) v->pipelined = 0;
+  }
   return v;
 }
 
 void vmqgb_view_free(vmqgb_view* v) {
   if (!v) return;
+  for (int i = 0; i < VMQGB_ROUNDS; i++) vmqg_hbatch_free(v->rounds[i].hb);
   pthread_rwlock_destroy(&v->tables);
   pthread_mutex_destroy(&v->device);
+  pthread_mutex_destroy(&v->q_mu);
+  pthread_cond_destroy(&v->q_cv);
   free(v);
 }
 
@@ -368,33 +494,206 @@ void vmqgb_view_yield(vmqgb_view* v) {   /* a waiting writer goes first (writer-
   pthread_rwlock_unlock(&v->tables);
   pthread_rwlock_rdlock(&v->tables);
 }
-/* A writer takes the device mutex too: a records-mode batch matches without
- * the read lock, and an apply changes what a match reads (the layout, the
- * arena, the staging ring).  Order: the write lock, then the mutex; a mutex
- * holder never waits for the table lock, so no cycle. */
-void vmqgb_view_write_begin(vmqgb_view* v) {
-  pthread_rwlock_wrlock(&v->tables);
+void vmqgb_view_write_begin(vmqgb_view* v) { pthread_rwlock_wrlock(&v->tables); }
+void vmqgb_view_write_end(vmqgb_view* v) { pthread_rwlock_unlock(&v->tables); }
+
+/* The apply changes what a device call reads (the layout, the arena, the
+ * staging ring): it takes the device mutex too, after the table lock (a
+ * mutex holder never waits for the table lock, so no cycle).  Rounds already
+ * submitted stay on the epoch they were submitted at (stream order). */
+int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
   pthread_mutex_lock(&v->device);
-}
-void vmqgb_view_write_end(vmqgb_view* v) {
+  const int rc = vmqgb_ops_apply(o, v->ctx, epoch);
   pthread_mutex_unlock(&v->device);
-  pthread_rwlock_unlock(&v->tables);
+  return rc;
 }
 
-int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
-  if (b->n == 0) {   /* nothing to match: empty results */
-    if (ensure_offsets(b)) return VMQG_E_NOMEM;
-    b->offsets[0] = 0;
-    b->out_n = b->rng_n = 0;
-    if (recs) *recs = NULL;
-    if (nrecs) *nrecs = 0;
+int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
+  vmqgb_view_write_begin(v);
+  const int rc = vmqgb_view_apply_ops(v, o, epoch);
+  vmqgb_view_write_end(v);
+  return rc;
+}
+
+void vmqgb_view_set_device_records(vmqgb_view* v, int on) { v->device_records = on != 0; }
+
+void vmqgb_view_get_stats(vmqgb_view* v, vmqgb_view_stats* out) {
+  pthread_mutex_lock(&v->q_mu);
+  *out = v->st;
+  pthread_mutex_unlock(&v->q_mu);
+}
+
+static void round_release(vmqgb_view* v, vmqgb_round* r) {   /* q_mu held */
+  if (--r->refs == 0) {
+    r->busy = 0;
+    pthread_cond_broadcast(&v->q_cv);
+  }
+}
+
+void vmqgb_view_release(vmqgb_view* v, vmqgb_batch* b) {
+  if (!b->lease) return;
+  pthread_mutex_lock(&v->q_mu);
+  round_release(v, (vmqgb_round*)b->lease);
+  pthread_mutex_unlock(&v->q_mu);
+  b->lease = NULL;
+  b->offsets = b->offs_buf;
+  b->rng = b->rng_buf;
+}
+
+/* A combiner's round: the taken batches' publishes and words concatenated
+ * into the hbatch's pinned inputs, one submit under the device mutex, the
+ * offsets (the next round may start then), the entries, the hand-out. */
+static void run_round(vmqgb_view* v, vmqgb_round* r, vmqgb_req* list) {
+  size_t n = 0, nw = 0;
+  for (vmqgb_req* q = list; q; q = q->next) { q->base = n; n += q->b->n; nw += q->b->nwords; }
+  vmqg_pub* P = NULL;
+  uint32_t* W = NULL;
+  int rc = vmqg_hbatch_inputs(r->hb, n, nw, &P, &W);
+  if (!rc) {
+    size_t wb = 0;
+    for (vmqgb_req* q = list; q; q = q->next) {
+      const vmqgb_batch* b = q->b;
+      memcpy(W + wb, b->words, b->nwords * sizeof(uint32_t));
+      vmqg_pub* d = P + q->base;
+      for (size_t i = 0; i < b->n; i++) {
+        d[i] = b->pubs[i];
+        d[i].word_off += (uint32_t)wb;
+      }
+      wb += b->nwords;
+    }
+  }
+  const uint64_t* offs = NULL;
+  uint64_t total = 0, epoch = 0;
+  for (int attempt = 0; !rc; attempt++) {
+    pthread_mutex_lock(&v->device);
+    rc = vmqg_hbatch_submit(v->ctx, r->hb, n, nw, r->dev_ranges);
+    pthread_mutex_unlock(&v->device);
+    if (rc) break;
+    rc = vmqg_hbatch_offsets(r->hb, &offs, &total, &epoch);
+    if ((rc == VMQG_E_OVERFLOW || rc == VMQG_E_FRONTIER) && attempt < 8) {   /* larger output / stack: again */
+      pthread_mutex_lock(&v->q_mu);
+      v->st.overflow_retries++;
+      pthread_mutex_unlock(&v->q_mu);
+      rc = 0;
+      continue;
+    }
+    break;
+  }
+  pthread_mutex_lock(&v->q_mu);
+  v->in_kernels--;
+  pthread_cond_broadcast(&v->q_cv);
+  pthread_mutex_unlock(&v->q_mu);
+  const void* out = NULL;
+  if (!rc) rc = vmqg_hbatch_entries(r->hb, &out);
+  r->offs = offs;
+  r->out = out;
+  r->epoch = epoch;
+  pthread_mutex_lock(&v->q_mu);
+  v->st.rounds++;
+  v->st.round_publishes += n;
+  if (n > v->st.max_round_publishes) v->st.max_round_publishes = n;
+  r->refs = 0;
+  for (vmqgb_req* q = list; q; q = q->next) {
+    v->st.round_batches++;
+    q->rc = rc;
+    q->round = rc ? NULL : r;
+    if (!rc) r->refs++;
+    q->done = 1;
+  }
+  if (r->refs == 0) r->busy = 0;
+  pthread_cond_broadcast(&v->q_cv);
+  pthread_mutex_unlock(&v->q_mu);
+}
+
+/* Queues req and returns when a round has served it (q_mu not held on entry
+ * or exit).  A waiting batcher becomes the combiner when fewer than two
+ * rounds are in the kernels and a round is free: it takes the queued batches
+ * of the head's device mode, up to VMQGB_ROUND_MAX publishes. */
+static void combine(vmqgb_view* v, vmqgb_req* req) {
+  pthread_mutex_lock(&v->q_mu);
+  req->done = 0;
+  req->next = NULL;
+  if (v->q_tail) v->q_tail->next = req; else v->q_head = req;
+  v->q_tail = req;
+  while (!req->done) {
+    vmqgb_round* r = NULL;
+    if (v->q_head && v->in_kernels < 2)
+      for (int i = 0; i < VMQGB_ROUNDS && !r; i++) if (!v->rounds[i].busy) r = &v->rounds[i];
+    if (!r) { pthread_cond_wait(&v->q_cv, &v->q_mu); continue; }
+    /* take the head's mode, FIFO, up to the round's publish budget */
+    const int mode = v->q_head->dev_ranges;
+    vmqgb_req *list = NULL, *tail = NULL, **pp = &v->q_head, *last = NULL;
+    size_t n = 0;
+    while (*pp) {
+      vmqgb_req* q = *pp;
+      if (q->dev_ranges == mode && (n == 0 || n + q->b->n <= VMQGB_ROUND_MAX)) {
+        *pp = q->next;
+        q->next = NULL;
+        if (tail) tail->next = q; else list = q;
+        tail = q;
+        n += q->b->n;
+      } else {
+        last = q;
+        pp = &q->next;
+      }
+    }
+    v->q_tail = last;
+    r->busy = 1;
+    r->dev_ranges = mode;
+    v->in_kernels++;
+    pthread_mutex_unlock(&v->q_mu);
+    run_round(v, r, list);
+    pthread_mutex_lock(&v->q_mu);
+  }
+  pthread_mutex_unlock(&v->q_mu);
+}
+
+/* records mode: the batch's records copied out of its round (device
+ * records) or expanded from the host record table of the round's epoch
+ * (device ranges); offsets rebased to the batch.  Read lock held. */
+static int take_records(vmqgb_view* v, vmqgb_batch* b, vmqgb_req* q) {
+  const vmqgb_round* r = q->round;
+  const uint64_t* o = r->offs + q->base;
+  if (ensure_offsets(b)) return VMQG_E_NOMEM;
+  if (!r->dev_ranges) {
+    const uint64_t first = o[0], cnt = o[b->n] - first;
+    if (grow((void**)&b->out, &b->out_cap, cnt + 1, sizeof(vmqg_emit))) return VMQG_E_NOMEM;
+    memcpy(b->out, (const vmqg_emit*)r->out + first, cnt * sizeof(vmqg_emit));
+    for (size_t i = 0; i <= b->n; i++) b->offsets[i] = o[i] - first;
+    b->out_n = cnt;
     return 0;
   }
-  /* records are copies: the read lock is let go while the batch waits for
-   * the device, so an apply can land between this batch's prepare and its
-   * match (its word ids stay valid: the dictionary only grows) and a writer
-   * never waits for a queue of device calls.  Ranges index the host record
-   * table: they keep the lock until the caller has folded them. */
+  const vmqg_emit* recs = NULL;
+  uint64_t nrecs = 0;
+  int rc = vmqg_records_at(v->ctx, r->epoch, &recs, &nrecs);
+  if (rc) return rc;   /* VMQG_E_STATE: an apply rewrote record slots since the round */
+  const vmqg_range* g = (const vmqg_range*)r->out;
+  uint64_t cnt = 0;
+  for (uint64_t k = o[0]; k < o[b->n]; k++) cnt += g[k].count ? g[k].count : 1;
+  if (grow((void**)&b->out, &b->out_cap, cnt + 1, sizeof(vmqg_emit))) return VMQG_E_NOMEM;
+  vmqg_emit* dst = b->out;
+  b->offsets[0] = 0;
+  for (size_t i = 0; i < b->n; i++) {
+    for (uint64_t k = o[i]; k < o[i + 1]; k++) {
+      const vmqg_range e = g[k];
+      if (e.count == 0) {   /* remote node (fold_/5, vmq_reg_trie.erl:78-84) */
+        dst->kind_node = (VMQG_EMIT_REMOTE << 24) | e.off;
+        dst->group = dst->subscriber = dst->subinfo = VMQG_NONE;
+        dst++;
+        continue;
+      }
+      if ((uint64_t)e.off + e.count > nrecs) return VMQG_E_STATE;
+      memcpy(dst, recs + e.off, (size_t)e.count * sizeof(vmqg_emit));
+      dst += e.count;
+    }
+    b->offsets[i + 1] = (uint64_t)(dst - b->out);
+  }
+  b->out_n = cnt;
+  return 0;
+}
+
+/* the pre-pipeline path: one synchronous device call under the mutex */
+static int match_direct(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
   if (!ranges) vmqgb_view_read_end(v);
   pthread_mutex_lock(&v->device);
   int rc = ranges ? vmqgb_match_ranges(b, v->ctx) : vmqgb_match(b, v->ctx);
@@ -404,9 +703,75 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
   return rc;
 }
 
-int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
-  vmqgb_view_write_begin(v);
-  const int rc = vmqgb_ops_apply(o, v->ctx, epoch);
-  vmqgb_view_write_end(v);
-  return rc;
+int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
+  vmqgb_view_release(v, b);
+  if (recs) *recs = NULL;
+  if (nrecs) *nrecs = 0;
+  if (b->n == 0) {   /* nothing to match: empty results */
+    if (ensure_offsets(b)) return VMQG_E_NOMEM;
+    b->offsets[0] = 0;
+    b->out_n = b->rng_n = 0;
+    return 0;
+  }
+  if (!v->pipelined) return match_direct(v, b, ranges, recs, nrecs);
+  vmqgb_req q;
+  memset(&q, 0, sizeof q);
+  q.b = b;
+  if (ranges) {
+    /* the read lock stays: no apply (and no new word) until the caller has folded */
+    for (int attempt = 0;; attempt++) {
+      q.dev_ranges = 1;
+      combine(v, &q);
+      if (q.rc) return q.rc;
+      const vmqgb_round* r = q.round;
+      b->lease = q.round;
+      b->offsets = (uint64_t*)(r->offs + q.base);
+      b->rng = (vmqg_range*)r->out;
+      b->rng_n = r->offs[q.base + b->n] - r->offs[q.base];
+      b->epoch = r->epoch;
+      const int rc = vmqgb_batch_recheck(b, v->ctx);   /* a writer got in at a prepare yield */
+      if (rc < 0) return rc;
+      if (rc == 1 && attempt < 16) {
+        b->stale_rematches++;
+        vmqgb_view_release(v, b);
+        pthread_mutex_lock(&v->q_mu);
+        v->st.stale_rematches++;
+        pthread_mutex_unlock(&v->q_mu);
+        continue;
+      }
+      break;
+    }
+    if (recs && nrecs) return vmqg_records_at(v->ctx, b->epoch, recs, nrecs);
+    return 0;
+  }
+  /* records: the read lock stays until the records are copied out (the
+   * expansion reads the host record table of the round's epoch); the fold
+   * that follows works on copies and may yield it */
+  int dev_ranges = !v->device_records;
+  for (int attempt = 0;; attempt++) {
+    q.dev_ranges = dev_ranges;
+    combine(v, &q);
+    if (q.rc) return q.rc;
+    int rc = take_records(v, b, &q);
+    b->epoch = q.round->epoch;
+    pthread_mutex_lock(&v->q_mu);
+    round_release(v, q.round);
+    if (!rc) { if (dev_ranges) v->st.expanded_batches++; else v->st.device_record_batches++; }
+    if (rc == VMQG_E_STATE) v->st.state_retries++;
+    pthread_mutex_unlock(&v->q_mu);
+    if (rc == VMQG_E_STATE && dev_ranges) { dev_ranges = 0; continue; }   /* the device copies the records */
+    if (rc) return rc;
+    /* a word unknown at prepare time may have subscriptions on the tables
+     * this batch was matched on: prepare those publishes again and match */
+    rc = vmqgb_batch_recheck(b, v->ctx);
+    if (rc < 0) return rc;
+    if (rc == 1 && attempt < 16) {
+      b->stale_rematches++;
+      pthread_mutex_lock(&v->q_mu);
+      v->st.stale_rematches++;
+      pthread_mutex_unlock(&v->q_mu);
+      continue;
+    }
+    return 0;
+  }
 }

@@ -62,13 +62,30 @@ typedef struct vmqgb_batch {
   vmqg_pub* pubs;
   uint32_t* words;
   size_t n, cap, nwords, wcap;
-  /* match output */
+  /* match output: publish i's entries are out[offsets[i] .. offsets[i+1])
+   * (records) or rng[...] (ranges).  offsets / rng may point into the view's
+   * pipeline buffers after vmqgb_view_match (ranges mode) until
+   * vmqgb_view_release or the batch's next match. */
   uint64_t* offsets;    /* n + 1 */
-  vmqg_emit* out;       /* records mode */
+  vmqg_emit* out;       /* records mode (owned) */
   size_t out_cap, out_n;
   vmqg_range* rng;      /* range mode */
   size_t rng_cap, rng_n;
-  uint64_t epoch;       /* table epoch of the last match (vmqg_epoch): ranges index that epoch's records */
+  uint64_t epoch;       /* table epoch the results are from (vmqg_epoch): ranges index that epoch's records */
+  /* owned storage behind offsets / rng */
+  uint64_t* offs_buf;
+  size_t offs_cap;
+  vmqg_range* rng_buf;
+  /* publishes prepared with a word the dictionary did not know (VMQG_PUB_UNKNOWN):
+   * their raw topics, so they can be prepared again if the dictionary grew
+   * before their match (vmqg_dict_generation) */
+  uint64_t dict_gen;
+  uint32_t* unk;        /* publish index, raw offset, raw length: 3 per entry */
+  size_t n_unk, unk_cap;
+  uint8_t* raw;
+  size_t raw_n, raw_cap;
+  void* lease;          /* the view pipeline round the outputs point into */
+  uint32_t stale_rematches;   /* matches repeated because a publish's unknown word became known */
 } vmqgb_batch;
 
 int vmqgb_batch_init(vmqgb_batch* b, size_t cap_hint);
@@ -77,8 +94,17 @@ void vmqgb_batch_free(vmqgb_batch* b);
 /* Adds one publish (raw topic bytes).  Returns its index in the batch, or a
  * negative VMQG_E_* (VMQG_E_INVAL: validate_topic rejects the topic). */
 long vmqgb_batch_add(vmqgb_batch* b, vmqg_ctx* ctx, uint32_t mountpoint, const uint8_t* topic, size_t len);
+/* Adds n publishes at once (vmqg_prepare_publishes: the dictionary probes of
+ * a block of topics overlap).  idx_out[i] = index in the batch or a negative
+ * VMQG_E_* for topic i, as vmqgb_batch_add.  Returns 0 or VMQG_E_NOMEM. */
+int vmqgb_batch_add_many(vmqgb_batch* b, vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints,
+                         const uint8_t* const* topics, const size_t* lens, long* idx_out);
 /* Appends every publish of src (per-thread batches -> one match call). */
 int vmqgb_batch_append(vmqgb_batch* dst, const vmqgb_batch* src);
+/* Prepares the publishes holding unknown words again if the dictionary grew
+ * since they were prepared (readers' lock held).  Returns 1 if a word id
+ * changed (the batch must be matched again), 0 if not, or a VMQG_E_*. */
+int vmqgb_batch_recheck(vmqgb_batch* b, vmqg_ctx* ctx);
 
 /* vmqg_match_batch / vmqg_match_ranges with the output grown on
  * VMQG_E_OVERFLOW; the outputs stay in the batch. */
@@ -127,31 +153,67 @@ typedef struct vmqgb_view vmqgb_view;
 vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx);
 void vmqgb_view_free(vmqgb_view* v);   /* does not destroy the context */
 vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v);
-/* A batcher's critical section: read_begin, vmqgb_batch_add for each of its
- * publishes, vmqgb_view_match, the fold, read_end.  Any number of batchers
- * at once; vmqgb_view_match serialises only the device call. */
+/* A batcher's critical section: read_begin, vmqgb_batch_add(_many) for its
+ * publishes, vmqgb_view_match, the fold, vmqgb_view_release, read_end.  Any
+ * number of batchers at once.
+ *
+ * The device side is a combining, pipelined submitter: a batcher queues its
+ * prepared batch; whichever waiting batcher finds the pipeline free takes
+ * every batch queued at that moment and matches them as ONE device call
+ * (vmqg_hbatch_*: one H2D, one launch sequence, one D2H), then hands each
+ * batch its slice.  Up to two such rounds are in the kernels at once and up
+ * to VMQGB_ROUNDS exist, so round k+1's inputs are copied and matched while
+ * round k's results come back and round k-1's are folded.  The device works
+ * in range mode ({record off, count} per key: 16 B per config-C publish over
+ * PCIe instead of 1,040 B of records); a records-mode batch is expanded from
+ * the host record table of its round's epoch into the batch's own buffer
+ * (byte-identical to what the device would have copied; if an apply has
+ * rewritten record slots since, the batch is matched again with device-side
+ * records). */
 void vmqgb_view_read_begin(vmqgb_view* v);
 void vmqgb_view_read_end(vmqgb_view* v);
 /* Lets a waiting writer in and takes the read lock back: a batcher calls it
  * every VMQGB_YIELD_EVERY publishes while it prepares a batch, and while it
- * folds a records-mode batch (ids only ever grow, so what it prepared or
- * matched stays valid), so an apply waits for one slice of a batch, not for
- * every reader's whole batch. */
+ * folds a records-mode batch (its records are copies), so an apply waits for
+ * one slice of a batch, not for every reader's whole batch. */
 void vmqgb_view_yield(vmqgb_view* v);
 #define VMQGB_YIELD_EVERY 512
-/* Called under the read lock, returns under it: vmqgb_match or
- * vmqgb_match_ranges (ranges != 0) with the device to itself; in range mode
- * also the record table of the match's epoch (vmqg_records_at) for
- * vmqgb_fold_ranges.  In records mode the lock is let go while the batch
- * waits for the device (an apply may land between its prepare and its
- * match: word and term ids only ever grow); range mode keeps it, as its
- * entries index the host record table. */
+#define VMQGB_ROUNDS 4
+#define VMQGB_ROUND_MAX (1u << 17)   /* publishes per combined round */
+/* Called under the read lock, returns under it: the batch's results
+ * (offsets + out in records mode, offsets + rng in range mode) and, in range
+ * mode, the record table of the match's epoch (vmqg_records_at) for
+ * vmqgb_fold_ranges.  The lock is held while the batch waits for its round,
+ * so a writer waits at most for the rounds in flight (one device round trip)
+ * and the results are the tables' answer at one epoch.  If the dictionary
+ * grew between the batch's prepare slices (a writer got in at a yield) and a
+ * publish's unknown word is known now, the batch is prepared and matched
+ * again (vmqgb_batch_recheck).  Records mode copies its records out (the fold
+ * may then yield the lock); range mode's entries index the host record
+ * table, so its fold keeps the lock. */
 int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs);
-/* Table changes (vmqg_apply_ops, the term tables of the caller): writers;
- * write_begin takes the device mutex as well (after the table lock). */
+/* Ends the batch's use of the pipeline buffers its range-mode results point
+ * into (also done by its next vmqgb_view_match). */
+void vmqgb_view_release(vmqgb_view* v, vmqgb_batch* b);
+/* Table changes (vmqg_apply_ops, the word dictionary, the caller's term
+ * tables): writers.  INVARIANT: the word dictionary only grows under the
+ * write lock (vmqgb_ops_add interns), so a prepare under the read lock sees
+ * a stable dictionary.  write_begin takes the table lock only; the device
+ * mutex is taken (after it) only around the apply itself (vmqgb_view_apply_ops),
+ * so a writer that only interns (the NIF's add_init) never waits for a
+ * device call. */
 void vmqgb_view_write_begin(vmqgb_view* v);
 void vmqgb_view_write_end(vmqgb_view* v);
-int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);   /* write_begin, apply, write_end */
+int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);   /* inside write_begin/end */
+int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);       /* write_begin, apply, write_end */
+/* Knobs and counters of the submitter (tools/nif_harness.c reports them). */
+void vmqgb_view_set_device_records(vmqgb_view* v, int on);   /* records over PCIe instead of host expansion */
+typedef struct vmqgb_view_stats {
+  uint64_t rounds, round_publishes, round_batches, max_round_publishes;
+  uint64_t expanded_batches, device_record_batches, state_retries, stale_rematches;
+  uint64_t overflow_retries;
+} vmqgb_view_stats;
+void vmqgb_view_get_stats(vmqgb_view* v, vmqgb_view_stats* out);
 
 #ifdef __cplusplus
 }

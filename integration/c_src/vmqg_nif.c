@@ -28,9 +28,10 @@
  * publishes and building the result terms under the view's read lock, only
  * the device call itself taking turns — as vmq_reg_trie:fold/4 runs in
  * every caller's process (vmq_reg_trie.erl:59-66, read_concurrency tables
- * :136-137).  apply/3, add_init/6 and flush_init/1 (the subscription changes
- * and the term tables they intern) are writers.  Every NIF that can wait for
- * a lock or the device is a dirty one.
+ * :136-137); the device calls of all batchers are combined (vmqgb_view_match).
+ * apply/3, apply_many/2, add_init/6 and flush_init/1 (the subscription
+ * changes and the term tables they intern) are writers.  Every NIF that can
+ * wait for a lock or the device is a dirty one.
  */
 #include <erl_nif.h>
 #include <stdint.h>
@@ -194,6 +195,31 @@ static int add_change(ErlNifEnv* env, vmqg_res* r, uint32_t kind, ERL_NIF_TERM s
   return 0;
 }
 
+/* The changes of one subscriber event: [{add | del, Topic, SubInfo, Node}]
+ * in vmq_subscriber:fold/3 order (deletes first), into r->ops. */
+static int add_changes(ErlNifEnv* env, vmqg_res* r, ERL_NIF_TERM sid, ERL_NIF_TERM changes) {
+  ERL_NIF_TERM head, tail = changes;
+  const ERL_NIF_TERM a_add = enif_make_atom(env, "add");
+  while (enif_get_list_cell(env, tail, &head, &tail)) {
+    int arity;
+    const ERL_NIF_TERM* el;
+    if (!enif_get_tuple(env, head, &arity, &el) || arity != 4) return VMQG_E_INVAL;
+    const uint32_t kind = enif_is_identical(el[0], a_add) ? VMQG_OP_ADD : VMQG_OP_DEL;
+    const int rc = add_change(env, r, kind, sid, el[1], el[2], el[3]);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+/* Under the write lock: applies the pending add_init ops (they keep their
+ * order before anything applied after them); their failure is returned. */
+static int flush_pending(vmqg_res* r) {
+  if (!r->ops.n) return 0;
+  const int rc = vmqgb_view_apply_ops(r->view, &r->ops, NULL);
+  vmqgb_ops_reset(&r->ops);
+  return rc;
+}
+
 /* apply(Ctx, SubscriberId, [{add | del, Topic, SubInfo, Node}]) -> ok | {error, _}
  * (handle_event/2, vmq_reg_trie.erl:240-277) */
 static ERL_NIF_TERM nif_apply(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
@@ -201,32 +227,51 @@ static ERL_NIF_TERM nif_apply(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   vmqg_res* r = get_res(env, argv[0]);
   if (!r) return enif_make_badarg(env);
   vmqgb_view_write_begin(r->view);
-  if (r->ops.n) vmqgb_ops_apply(&r->ops, r->ctx, NULL);   /* pending add_init ops keep their order */
+  int rc = flush_pending(r);
+  if (!rc) rc = add_changes(env, r, argv[1], argv[2]);
+  if (!rc) rc = vmqgb_view_apply_ops(r->view, &r->ops, NULL);
   vmqgb_ops_reset(&r->ops);
-  ERL_NIF_TERM head, tail = argv[2];
-  int rc = 0;
+  vmqgb_view_write_end(r->view);
+  return rc ? error_term(env, rc) : a_ok;
+}
+
+/* apply_many(Ctx, [{SubscriberId, Changes}]) -> ok | {error, _}: the events
+ * vmq_reg_gpu_view drained from its mailbox, in arrival order, as ONE
+ * vmqg_apply_ops (one write-lock section, one patch upload).  Applying the
+ * concatenation is applying them one after the other: every event's deletes
+ * precede its adds, and events keep their order (vmq_reg_trie.erl:240-251).
+ * An invalid change rejects the whole call with nothing applied (the view
+ * then applies the events one by one to isolate it). */
+static ERL_NIF_TERM nif_apply_many(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  if (!r) return enif_make_badarg(env);
+  vmqgb_view_write_begin(r->view);
+  int rc = flush_pending(r);
+  ERL_NIF_TERM head, tail = argv[1];
   while (!rc && enif_get_list_cell(env, tail, &head, &tail)) {
     int arity;
     const ERL_NIF_TERM* el;
-    if (!enif_get_tuple(env, head, &arity, &el) || arity != 4) { rc = VMQG_E_INVAL; break; }
-    const uint32_t kind = enif_is_identical(el[0], enif_make_atom(env, "add")) ? VMQG_OP_ADD : VMQG_OP_DEL;
-    rc = add_change(env, r, kind, argv[1], el[1], el[2], el[3]);
+    if (!enif_get_tuple(env, head, &arity, &el) || arity != 2) { rc = VMQG_E_INVAL; break; }
+    rc = add_changes(env, r, el[0], el[1]);
   }
-  if (!rc) rc = vmqgb_ops_apply(&r->ops, r->ctx, NULL);
+  if (!rc) rc = vmqgb_view_apply_ops(r->view, &r->ops, NULL);
   vmqgb_ops_reset(&r->ops);
   vmqgb_view_write_end(r->view);
   return rc ? error_term(env, rc) : a_ok;
 }
 
 /* add_init(Ctx, MP, Topic, SubscriberId, SubInfo, Node) -> ok: one
- * initialize_trie/2 tuple (vmq_reg_trie.erl:305-316), applied in batches */
+ * initialize_trie/2 tuple (vmq_reg_trie.erl:305-316), applied in batches.
+ * Only the table lock: interning terms and words never waits for a device
+ * call; the device mutex is taken for the apply every 65,536 changes. */
 static ERL_NIF_TERM nif_add_init(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   (void)argc;
   vmqg_res* r = get_res(env, argv[0]);
   if (!r) return enif_make_badarg(env);
   vmqgb_view_write_begin(r->view);
   int rc = add_change(env, r, VMQG_OP_ADD, argv[3], argv[2], argv[4], argv[5]);
-  if (!rc && r->ops.n >= 65536) rc = vmqgb_ops_apply(&r->ops, r->ctx, NULL);
+  if (!rc && r->ops.n >= 65536) rc = flush_pending(r);
   vmqgb_view_write_end(r->view);
   return rc ? error_term(env, rc) : a_ok;
 }
@@ -236,7 +281,7 @@ static ERL_NIF_TERM nif_flush_init(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
   vmqg_res* r = get_res(env, argv[0]);
   if (!r) return enif_make_badarg(env);
   vmqgb_view_write_begin(r->view);
-  const int rc = r->ops.n ? vmqgb_ops_apply(&r->ops, r->ctx, NULL) : 0;
+  const int rc = flush_pending(r);
   vmqgb_view_write_end(r->view);
   return rc ? error_term(env, rc) : a_ok;
 }
@@ -288,7 +333,9 @@ static ERL_NIF_TERM nif_batch_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
 /* match(Ctx, Batch, [{MP, TopicBin}], records | ranges) -> [{ok, Entries} | {error, Reason}]
  * (fold/4 for a batch of callers, vmq_reg_trie.erl:59-98); dirty CPU.
  * Batchers run this concurrently: the tables are read-locked from the first
- * publish prepared to the last term built; the device call takes turns. */
+ * publish prepared to the last term built (yielded every VMQGB_YIELD_EVERY
+ * publishes while preparing, and while folding records); the batch joins the
+ * view's combining submitter for the device call (vmqgb_view_match). */
 static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   (void)argc;
   vmqg_res* r = get_res(env, argv[0]);
@@ -299,29 +346,64 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     return enif_make_badarg(env);
   const int ranges = enif_is_identical(argv[3], a_ranges);
   vmqgb_batch* b = &br->b;
-  long* idx = (long*)enif_alloc((n ? n : 1) * sizeof(long));
-  ERL_NIF_TERM* res = (ERL_NIF_TERM*)enif_alloc((n ? n : 1) * sizeof(ERL_NIF_TERM));
-  if (!idx || !res) { enif_free(idx); enif_free(res); return enif_make_badarg(env); }
-  vmqgb_view_read_begin(r->view);
-  vmqgb_batch_reset(b);
-  ERL_NIF_TERM head, tail = argv[2];
+  const size_t m = n ? n : 1;
+  long* idx = (long*)enif_alloc(m * sizeof(long));
+  ERL_NIF_TERM* res = (ERL_NIF_TERM*)enif_alloc(m * sizeof(ERL_NIF_TERM));
+  const uint8_t** tp = (const uint8_t**)enif_alloc(m * sizeof(*tp));
+  size_t* tl = (size_t*)enif_alloc(m * sizeof(size_t));
+  uint32_t* mps = (uint32_t*)enif_alloc(m * sizeof(uint32_t));
+  if (!idx || !res || !tp || !tl || !mps) {
+    enif_free(idx); enif_free(res); enif_free(tp); enif_free(tl); enif_free(mps);
+    return enif_make_badarg(env);
+  }
+  /* the topics' bytes (valid for this call) and their mountpoint ids; the
+   * MP of the previous publish is reused when identical (one term_to_binary
+   * per distinct mountpoint run, not per publish) */
+  ERL_NIF_TERM head, tail = argv[2], last_mp = 0;
+  uint32_t last_id = r->max_mountpoints;
   for (unsigned i = 0; i < n; i++) {
     int arity;
     const ERL_NIF_TERM* el;
     ErlNifBinary topic;
-    uint32_t mp;
-    if (i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(r->view);
     enif_get_list_cell(env, tail, &head, &tail);
+    idx[i] = 0;
     if (!enif_get_tuple(env, head, &arity, &el) || arity != 2 || !enif_inspect_iolist_as_binary(env, el[1], &topic)) {
       idx[i] = VMQG_E_INVAL;
+      tp[i] = NULL; tl[i] = 0; mps[i] = 0;
       continue;
     }
-    ErlNifBinary mpb;
-    if (!enif_term_to_binary(env, el[0], &mpb)) { idx[i] = VMQG_E_NOMEM; continue; }
-    const int known = vmqgb_lookup(r->mps, mpb.data, mpb.size, &mp) == 0;
-    enif_release_binary(&mpb);
-    /* an unknown mountpoint has no subscriptions: an id past every root matches nothing */
-    idx[i] = vmqgb_batch_add(b, r->ctx, known ? mp : r->max_mountpoints, topic.data, topic.size);
+    tp[i] = topic.data;
+    tl[i] = topic.size;
+    if (!last_mp || !enif_is_identical(el[0], last_mp)) {
+      ErlNifBinary mpb;
+      last_mp = el[0];
+      last_id = r->max_mountpoints;   /* an unknown mountpoint has no subscriptions: an id past every root */
+      if (enif_term_to_binary(env, el[0], &mpb)) {
+        uint32_t id;
+        vmqgb_view_read_begin(r->view);
+        if (vmqgb_lookup(r->mps, mpb.data, mpb.size, &id) == 0) last_id = id;
+        vmqgb_view_read_end(r->view);
+        enif_release_binary(&mpb);
+      }
+    }
+    mps[i] = last_id;
+  }
+  vmqgb_view_read_begin(r->view);
+  vmqgb_batch_reset(b);
+  /* the batched prepare, slice by slice (a writer gets in between slices) */
+  for (unsigned lo = 0; lo < n; lo += VMQGB_YIELD_EVERY) {
+    const unsigned hi = lo + VMQGB_YIELD_EVERY < n ? lo + VMQGB_YIELD_EVERY : n;
+    if (lo) vmqgb_view_yield(r->view);
+    /* rejected terms keep their error; the others get their batch index */
+    unsigned k = 0;
+    for (unsigned i = lo; i < hi; i++)
+      if (idx[i] == 0) { tp[lo + k] = tp[i]; tl[lo + k] = tl[i]; mps[lo + k] = mps[i]; k++; }
+    long* sub = (long*)enif_alloc((k ? k : 1) * sizeof(long));
+    const int rc = sub ? vmqgb_batch_add_many(b, r->ctx, k, mps + lo, tp + lo, tl + lo, sub) : VMQG_E_NOMEM;
+    unsigned j = 0;
+    for (unsigned i = lo; i < hi; i++)
+      if (idx[i] == 0) idx[i] = rc ? rc : sub[j++];
+    enif_free(sub);
   }
   const vmqg_emit* recs = NULL;
   uint64_t nrecs = 0;
@@ -342,10 +424,10 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     res[i] = frc ? error_term(env, frc) : enif_make_tuple2(env, a_ok, enif_make_list_from_array(env, acc.out, (unsigned)acc.n));
     enif_free(acc.out);
   }
+  vmqgb_view_release(r->view, b);
   vmqgb_view_read_end(r->view);
   ERL_NIF_TERM list = enif_make_list_from_array(env, res, n);
-  enif_free(res);
-  enif_free(idx);
+  enif_free(res); enif_free(idx); enif_free(tp); enif_free(tl); enif_free(mps);
   return list;
 }
 
@@ -382,6 +464,7 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
 static ErlNifFunc funcs[] = {
     {"create", 1, nif_create, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"apply", 3, nif_apply, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"apply_many", 2, nif_apply_many, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"add_init", 6, nif_add_init, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"flush_init", 1, nif_flush_init, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"batch_new", 1, nif_batch_new, 0},

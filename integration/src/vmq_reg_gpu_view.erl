@@ -25,6 +25,16 @@
 %% while an apply changes them) and the initial load.  It never queues a
 %% fold request, so no event can delay one.
 %%
+%% Events are coalesced: vmq_reg_trie applies each subscriber event with a
+%% few ETS inserts in its gen_server (vmq_reg_trie.erl:198-210, 240-251); here
+%% an apply is a write-lock section plus a table patch upload, so on each
+%% event the view drains the further subscriber events already in its
+%% mailbox (a selective receive with a 0 timeout, up to ?MAX_COALESCE) and
+%% applies the group with ONE vmqg_nif:apply_many/2.  The group is applied
+%% in arrival order, each event's deletes before its adds, which is what
+%% applying the events one after the other does; under load the groups grow
+%% with the backlog, so the view keeps up with config D's 100k changes/s.
+%%
 %% Install: reg_views = [vmq_reg_trie, vmq_reg_gpu_view] (shadow) or
 %% default_reg_view = vmq_reg_gpu_view (vmq_server.schema:115-137).  The NIF
 %% (c_src/vmqg_nif.c) and priv/libvmqgpu.so come from this repository.
@@ -49,6 +59,8 @@
          code_change/3]).
 
 -define(SERVER, ?MODULE).
+%% subscriber events applied per vmqg_nif:apply_many/2 at most
+-define(MAX_COALESCE, 10000).
 
 -record(state, {ctx,                    % vmqg_nif resource (vmqg_ctx + term tables)
                 batchers,               % tuple of vmq_reg_gpu_batcher pids
@@ -113,7 +125,7 @@ init([]) ->
 
 handle_call({event, Event}, _From, State) ->
     %% used only for testing/microbenchmarking, as vmq_reg_trie.erl:167-170
-    {reply, ok, handle_event(Event, State)};
+    {reply, ok, handle_events([Event], State)};
 handle_call(_Request, _From, State) ->
     {reply, ok, State}.
 
@@ -121,14 +133,15 @@ handle_cast(_Msg, State) ->
     {noreply, State}.
 
 handle_info(subscribers_loaded, #state{event_queue=Q} = State) ->
-    State1 = lists:foldl(fun handle_event/2, State#state{status=ready}, queue:to_list(Q)),
+    %% the events queued during the initial load, replayed in order (:198-205)
+    State1 = replay(queue:to_list(Q), State#state{status=ready}),
     {Subs, _} = stats(),
     lager:info("loaded ~p subscriptions into ~p", [Subs, ?MODULE]),
     {noreply, State1#state{event_queue=undefined}};
 handle_info(Event, #state{status=init, event_queue=Q} = State) ->
     {noreply, State#state{event_queue=queue:in(Event, Q)}};
 handle_info(Event, State) ->
-    {noreply, handle_event(Event, State)}.
+    {noreply, handle_events([Event | drain_events(?MAX_COALESCE - 1, [])], State)}.
 
 terminate(_Reason, _State) ->
     persistent_term:erase({?MODULE, batchers}),
@@ -142,20 +155,68 @@ code_change(_OldVsn, State, _Extra) ->
 %%% Internal functions
 %%%===================================================================
 
-%% handle_event/2 (vmq_reg_trie.erl:240-251): the same diff, the same order
-%% (deletes, then adds); the NIF turns the changes into one vmqg_apply_ops.
-handle_event(Event, #state{ctx=Ctx, event_handler=Handler} = State) ->
+%% The subscriber events already in the mailbox, oldest first (a selective
+%% receive keeps their relative order; other messages stay where they are).
+%% The shapes are the metadata events vmq_subscriber_db's handler converts
+%% (vmq_subscriber_db.erl:56-71).
+drain_events(0, Acc) ->
+    lists:reverse(Acc);
+drain_events(N, Acc) ->
+    receive
+        {updated, {vmq, subscriber}, _, _, _} = E -> drain_events(N - 1, [E | Acc]);
+        {deleted, {vmq, subscriber}, _, _} = E -> drain_events(N - 1, [E | Acc])
+    after 0 ->
+        lists:reverse(Acc)
+    end.
+
+replay([], State) ->
+    State;
+replay(Events, State) ->
+    {Group, Rest} = case length(Events) > ?MAX_COALESCE of
+                        true -> lists:split(?MAX_COALESCE, Events);
+                        false -> {Events, []}
+                    end,
+    replay(Rest, handle_events(Group, State)).
+
+%% handle_event/2 (vmq_reg_trie.erl:240-251) for a group of events: the same
+%% diff per event, the same order (deletes, then adds; event after event);
+%% the NIF turns the whole group into one vmqg_apply_ops.  If the group is
+%% refused (a malformed change: nothing was applied) the events are applied
+%% one by one, so only the offending one fails, as it would alone.
+handle_events(Events, #state{ctx=Ctx, event_handler=Handler} = State) ->
+    AllChanges = lists:foldr(fun(E, Acc) ->
+                                     case event_changes(Handler, E) of
+                                         ignore -> Acc;
+                                         C -> [C | Acc]
+                                     end
+                             end, [], Events),
+    case AllChanges of
+        [] ->
+            ok;
+        Changes ->
+            case vmqg_nif:apply_many(Ctx, Changes) of
+                ok ->
+                    ok;
+                {error, _} ->
+                    lists:foreach(fun({SubscriberId, Ch}) ->
+                                          ok = vmqg_nif:apply(Ctx, SubscriberId, Ch)
+                                  end, Changes)
+            end
+    end,
+    State.
+
+%% {SubscriberId, [{Kind, Topic, SubInfo, Node}]} of one event, or ignore
+event_changes(Handler, Event) ->
     case Handler(Event) of
         {delete, SubscriberId, Subscriptions} ->
             Removed = vmq_subscriber:get_changes(Subscriptions),
-            ok = vmqg_nif:apply(Ctx, SubscriberId, changes(del, Removed));
+            {SubscriberId, changes(del, Removed)};
         {update, SubscriberId, OldValue, NewValue} ->
             {ToRemove, ToAdd} = vmq_subscriber:get_changes(OldValue, NewValue),
-            ok = vmqg_nif:apply(Ctx, SubscriberId, changes(del, ToRemove) ++ changes(add, ToAdd));
+            {SubscriberId, changes(del, ToRemove) ++ changes(add, ToAdd)};
         ignore ->
-            ok
-    end,
-    State.
+            ignore
+    end.
 
 %% [{Node, [{Topic, SubInfo}]}] (vmq_subscriber:get_changes/1,2) in the
 %% order vmq_subscriber:fold/3 (vmq_subscriber.erl:184-196) visits it ->

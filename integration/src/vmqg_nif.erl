@@ -1,6 +1,6 @@
 %% vmqg_nif — NIF stubs of c_src/vmqg_nif.c (libvmqgpu behind vmq_reg_gpu_view).
 -module(vmqg_nif).
--export([create/1, apply/3, add_init/6, flush_init/1, batch_new/1, match/4, stats/1]).
+-export([create/1, apply/3, apply_many/2, add_init/6, flush_init/1, batch_new/1, match/4, stats/1]).
 -on_load(init/0).
 
 init() ->
@@ -14,6 +14,9 @@ init() ->
 create(_Opts) -> erlang:nif_error(nif_not_loaded).
 %% Ctx, SubscriberId, [{add | del, Topic, SubInfo, Node}] -> ok | {error, term()}
 apply(_Ctx, _SubscriberId, _Changes) -> erlang:nif_error(nif_not_loaded).
+%% Ctx, [{SubscriberId, [{add | del, Topic, SubInfo, Node}]}] -> ok | {error, term()}
+%% (a group of events as one apply; nothing applied on error)
+apply_many(_Ctx, _EventChanges) -> erlang:nif_error(nif_not_loaded).
 %% Ctx, MP, Topic, SubscriberId, SubInfo, Node -> ok | {error, term()}
 add_init(_Ctx, _MP, _Topic, _SubscriberId, _SubInfo, _Node) -> erlang:nif_error(nif_not_loaded).
 flush_init(_Ctx) -> erlang:nif_error(nif_not_loaded).

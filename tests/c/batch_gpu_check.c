@@ -23,6 +23,28 @@
  *                                         "zz/<k>" (no publish matches them)
  *                                         <rounds> times: the matches
  *                                         must not change
+ *   X S|U <node> <sub> <info> <mp> <filter>
+ *                                         a change of the current churn group
+ *   G                                     ends a churn group
+ *   W <records|ranges> <threads> <batch> <passes>
+ *                                         batchers match every publish
+ *                                         over and over (at least <passes>
+ *                                         times, yielding every 512
+ *                                         publishes as the NIF does) while a
+ *                                         writer applies the churn groups one
+ *                                         apply each, ~1 ms apart: changes
+ *                                         that DO alter the answers, some
+ *                                         bringing words that publishes
+ *                                         already hold.  Writes "W <e0>
+ *                                         <groups> <lines>", then per group
+ *                                         "g <k> <epoch after>", then per
+ *                                         matched publish "<i> <epoch> <rc>
+ *                                         entries..." (the epoch its batch's
+ *                                         answer is from; the test compares
+ *                                         it with the oracle at that epoch),
+ *                                         then "v <rounds> <stale rematches>
+ *                                         <batches>"; the groups are then
+ *                                         forgotten (the next X opens anew)
  * group is the $share group's text ("-" for none).
  * Exit 0 after writing everything; non-zero with a message otherwise. */
 #define _GNU_SOURCE
@@ -42,14 +64,16 @@ static size_t npubs, pcap;
 static char** gname;     /* group text by word id */
 static size_t gcap;
 
+typedef struct { char* buf; size_t n, cap; } sbuf;
+
 typedef struct {
   int tid, T, ranges;
   size_t B;
-  char** lines;          /* per publish: its output line */
+  char** lines;          /* per publish: its output line (M / C) */
+  int passes;            /* W: passes at least, and until the writer is done */
+  sbuf* wout;            /* W: this batcher's output lines */
   int err;
 } bt_t;
-
-typedef struct { char* buf; size_t n, cap; } sbuf;
 
 static void sput(sbuf* s, const char* t) {
   const size_t l = strlen(t);
@@ -72,36 +96,66 @@ static int put_entry(void* acc, const vmqgb_entry* e) {
   return 0;
 }
 
-/* one batcher, exactly as vmqg_nif.c's match/4: batches t, t + T, ... */
+static volatile int writer_done;
+
+/* one batch of publishes [lo, lo + n) exactly as vmqg_nif.c's match/4: the
+ * batched prepare in slices with a yield between, the combined device call,
+ * the fold (records: yielding), the release; one output line per publish */
+static int one_batch(bt_t* a, vmqgb_batch* b, long* idx, size_t lo, size_t n, char** lines, sbuf* wout) {
+  vmqgb_view_read_begin(view);
+  vmqgb_batch_reset(b);
+  for (size_t s0 = 0; s0 < n; s0 += VMQGB_YIELD_EVERY) {
+    const size_t k = n - s0 < VMQGB_YIELD_EVERY ? n - s0 : VMQGB_YIELD_EVERY;
+    if (s0) vmqgb_view_yield(view);
+    const uint8_t* tp[VMQGB_YIELD_EVERY];
+    size_t tl[VMQGB_YIELD_EVERY];
+    uint32_t mp[VMQGB_YIELD_EVERY];
+    for (size_t i = 0; i < k; i++) {
+      tp[i] = (const uint8_t*)pubs[lo + s0 + i].topic;
+      tl[i] = pubs[lo + s0 + i].len;
+      mp[i] = pubs[lo + s0 + i].mp;
+    }
+    const int rc = vmqgb_batch_add_many(b, ctx, k, mp, tp, tl, idx + s0);
+    if (rc) { vmqgb_view_read_end(view); return rc; }
+  }
+  const vmqg_emit* recs = NULL;
+  uint64_t nrecs = 0;
+  const int rc = vmqgb_view_match(view, b, a->ranges, &recs, &nrecs);
+  for (size_t i = 0; i < n; i++) {
+    if (!a->ranges && i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(view);   /* records: copies */
+    sbuf s = {0, 0, 0};
+    char h[64];
+    int frc = idx[i] < 0 ? (int)idx[i] : rc;
+    sput(&s, "");
+    if (!frc) frc = a->ranges ? vmqgb_fold_ranges(b, recs, nrecs, (size_t)idx[i], put_entry, &s)
+                              : vmqgb_fold(b, (size_t)idx[i], put_entry, &s);
+    if (wout) snprintf(h, sizeof h, "%zu %llu %d", lo + i, (unsigned long long)b->epoch, frc);
+    else snprintf(h, sizeof h, "%zu %d", lo + i, frc);
+    sbuf line = {0, 0, 0};
+    sput(&line, h);
+    if (!frc) sput(&line, s.buf);
+    free(s.buf);
+    if (wout) { sput(wout, line.buf); sput(wout, "\n"); free(line.buf); }
+    else lines[lo + i] = line.buf;
+  }
+  vmqgb_view_release(view, b);
+  vmqgb_view_read_end(view);
+  return 0;
+}
+
+/* one batcher: batches t, t + T, ... (W: pass after pass) */
 static void* batcher(void* p) {
   bt_t* a = (bt_t*)p;
   vmqgb_batch b;
   if (vmqgb_batch_init(&b, a->B)) { a->err = VMQG_E_NOMEM; return NULL; }
   long* idx = (long*)malloc(a->B * sizeof(long));
-  for (size_t lo = (size_t)a->tid * a->B; lo < npubs; lo += (size_t)a->T * a->B) {
-    const size_t n = lo + a->B <= npubs ? a->B : npubs - lo;
-    vmqgb_view_read_begin(view);
-    vmqgb_batch_reset(&b);
-    for (size_t i = 0; i < n; i++)
-      idx[i] = vmqgb_batch_add(&b, ctx, pubs[lo + i].mp, (const uint8_t*)pubs[lo + i].topic, pubs[lo + i].len);
-    const vmqg_emit* recs = NULL;
-    uint64_t nrecs = 0;
-    const int rc = vmqgb_view_match(view, &b, a->ranges, &recs, &nrecs);
-    for (size_t i = 0; i < n; i++) {
-      sbuf s = {0, 0, 0};
-      char h[64];
-      int frc = idx[i] < 0 ? (int)idx[i] : rc;
-      sput(&s, "");
-      if (!frc) frc = a->ranges ? vmqgb_fold_ranges(&b, recs, nrecs, (size_t)idx[i], put_entry, &s)
-                                : vmqgb_fold(&b, (size_t)idx[i], put_entry, &s);
-      snprintf(h, sizeof h, "%zu %d", lo + i, frc);
-      sbuf line = {0, 0, 0};
-      sput(&line, h);
-      if (!frc) sput(&line, s.buf);
-      free(s.buf);
-      a->lines[lo + i] = line.buf;
+  for (int pass = 0; !a->err; pass++) {
+    if (a->wout ? (pass >= a->passes && writer_done) : pass >= 1) break;
+    for (size_t lo = (size_t)a->tid * a->B; lo < npubs && !a->err; lo += (size_t)a->T * a->B) {
+      const size_t n = lo + a->B <= npubs ? a->B : npubs - lo;
+      const int rc = one_batch(a, &b, idx, lo, n, a->lines, a->wout);
+      if (rc) a->err = rc;
     }
-    vmqgb_view_read_end(view);
   }
   free(idx);
   vmqgb_batch_free(&b);
@@ -120,7 +174,7 @@ static void* churner(void* p) {   /* a writer: S/U pairs nobody's publishes matc
     const uint32_t kind = (r / 97) % 2 ? VMQG_OP_DEL : VMQG_OP_ADD;
     vmqgb_view_write_begin(view);
     int rc = vmqgb_ops_add_filter(&ops, ctx, kind, 0, (const uint8_t*)f, (size_t)l, 0, 900000 + (uint32_t)(r % 97), 0);
-    if (!rc) rc = vmqgb_ops_apply(&ops, ctx, NULL);
+    if (!rc) rc = vmqgb_view_apply_ops(view, &ops, NULL);
     vmqgb_view_write_end(view);
     if (rc) c->err = rc;
   }
@@ -136,7 +190,7 @@ static int run_match(FILE* out, int ranges, int T, size_t B, int churn_rounds) {
   churn_t cc = {churn_rounds, 0};
   if (churn_rounds) pthread_create(&cw, NULL, churner, &cc);
   for (int t = 0; t < T; t++) {
-    a[t] = (bt_t){t, T, ranges, B, lines, 0};
+    a[t] = (bt_t){t, T, ranges, B, lines, 0, NULL, 0};
     pthread_create(&th[t], NULL, batcher, &a[t]);
   }
   int err = 0;
@@ -147,6 +201,82 @@ static int run_match(FILE* out, int ranges, int T, size_t B, int churn_rounds) {
     for (size_t i = 0; i < npubs; i++) { fprintf(out, "%s\n", lines[i] ? lines[i] : "missing"); free(lines[i]); }
   }
   free(lines); free(a); free(th);
+  return err;
+}
+
+/* "<node> <sub> <info> <mp> <filter>" of an S/U/X line into ops (interning
+ * its words: callers hold the view's write lock when batchers run) */
+static int add_change_line(vmqgb_ops* ops, const char* rest, uint32_t kind) {
+  unsigned node, sub, info, mp;
+  int off = 0;
+  if (sscanf(rest, "%u %u %u %u %n", &node, &sub, &info, &mp, &off) < 4) return VMQG_E_INVAL;
+  const char* f = rest + off;
+  const size_t fl = strlen(f);
+  if (fl > 7 && memcmp(f, "$share/", 7) == 0) {   /* remember the group's text by its word id */
+    const char* g = f + 7;
+    const char* e = strchr(g, '/');
+    uint64_t offs[2] = {0, (uint64_t)(e - g)};
+    uint32_t wid;
+    if (vmqg_intern_words(ctx, (const uint8_t*)g, offs, 1, 1, &wid)) return VMQG_E_INVAL;
+    if (wid >= gcap) return VMQG_E_LIMIT;   /* gname is sized once: batchers read it concurrently */
+    if (!gname[wid]) gname[wid] = strndup(g, (size_t)(e - g));
+  }
+  return vmqgb_ops_add_filter(ops, ctx, kind, mp, (const uint8_t*)f, fl, node, sub, info);
+}
+
+/* W: the churn groups, applied by a writer while batchers match */
+static char*** groups;           /* groups[k]: NULL-terminated change lines ("S ..." / "U ...") */
+static size_t ngroups;
+
+typedef struct { uint64_t* epochs; int err; } wr_t;
+
+static void* group_writer(void* p) {
+  wr_t* w = (wr_t*)p;
+  vmqgb_ops ops;
+  vmqgb_ops_init(&ops);
+  for (size_t k = 0; k < ngroups && !w->err; k++) {
+    struct timespec ts = {0, 1000000};
+    nanosleep(&ts, NULL);
+    vmqgb_view_write_begin(view);
+    for (char** l = groups[k]; *l && !w->err; l++)
+      if (add_change_line(&ops, *l + 2, (*l)[0] == 'S' ? VMQG_OP_ADD : VMQG_OP_DEL)) w->err = VMQG_E_INVAL;
+    if (!w->err) w->err = vmqgb_view_apply_ops(view, &ops, &w->epochs[k]);
+    vmqgb_ops_reset(&ops);
+    vmqgb_view_write_end(view);
+  }
+  writer_done = 1;
+  vmqgb_ops_free(&ops);
+  return NULL;
+}
+
+static int run_w(FILE* out, int ranges, int T, size_t B, int passes) {
+  uint64_t e0 = 0;
+  vmqg_epoch(ctx, &e0);
+  bt_t* a = (bt_t*)calloc((size_t)T, sizeof(bt_t));
+  sbuf* wo = (sbuf*)calloc((size_t)T, sizeof(sbuf));
+  pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
+  pthread_t cw;
+  wr_t w = {(uint64_t*)calloc(ngroups + 1, sizeof(uint64_t)), 0};
+  writer_done = 0;
+  for (int t = 0; t < T; t++) {
+    a[t] = (bt_t){t, T, ranges, B, NULL, passes, &wo[t], 0};
+    sput(&wo[t], "");
+    pthread_create(&th[t], NULL, batcher, &a[t]);
+  }
+  pthread_create(&cw, NULL, group_writer, &w);
+  int err = 0;
+  pthread_join(cw, NULL);
+  if (w.err) err = w.err;
+  for (int t = 0; t < T; t++) { pthread_join(th[t], NULL); if (a[t].err) err = a[t].err; }
+  if (!err) {
+    size_t lines = 0;
+    for (int t = 0; t < T; t++) for (size_t i = 0; i < wo[t].n; i++) lines += wo[t].buf[i] == '\n';
+    fprintf(out, "W %llu %zu %zu\n", (unsigned long long)e0, ngroups, lines);
+    for (size_t k = 0; k < ngroups; k++) fprintf(out, "g %zu %llu\n", k, (unsigned long long)w.epochs[k]);
+    for (int t = 0; t < T; t++) fputs(wo[t].buf, out);
+  }
+  for (int t = 0; t < T; t++) free(wo[t].buf);
+  free(a); free(wo); free(th); free(w.epochs);
   return err;
 }
 
@@ -163,36 +293,37 @@ int main(int argc, char** argv) {
   ctx = vmqg_create(&cfg, &err);
   if (!ctx) { fprintf(stderr, "vmqg_create: %d\n", err); return 3; }
   view = vmqgb_view_new(ctx);
+  gcap = 1u << 20;   /* group names by word id, sized once (batchers read it while a writer adds) */
+  gname = (char**)calloc(gcap, sizeof(char*));
   vmqgb_ops ops;
   vmqgb_ops_init(&ops);
   char* line = NULL;
+  int group_open = 0;
   size_t lcap = 0;
   ssize_t ln;
   while ((ln = getline(&line, &lcap, in)) > 0) {
     if (line[ln - 1] == '\n') line[--ln] = 0;
     if (line[0] == 'S' || line[0] == 'U') {
-      unsigned node, sub, info, mp;
-      int off = 0;
-      if (sscanf(line + 2, "%u %u %u %u %n", &node, &sub, &info, &mp, &off) < 4) { fprintf(stderr, "bad: %s\n", line); return 4; }
-      const char* f = line + 2 + off;
-      const size_t fl = strlen(f);
-      if (fl > 7 && memcmp(f, "$share/", 7) == 0) {   /* remember the group's text by its word id */
-        const char* g = f + 7;
-        const char* e = strchr(g, '/');
-        uint64_t offs[2] = {0, (uint64_t)(e - g)};
-        uint32_t wid;
-        if (vmqg_intern_words(ctx, (const uint8_t*)g, offs, 1, 1, &wid)) return 5;
-        if (wid >= gcap) {
-          size_t nc = gcap ? gcap : 64;
-          while (nc <= wid) nc *= 2;
-          gname = (char**)realloc(gname, nc * sizeof(char*));
-          memset(gname + gcap, 0, (nc - gcap) * sizeof(char*));
-          gcap = nc;
-        }
-        if (!gname[wid]) gname[wid] = strndup(g, (size_t)(e - g));
+      if (add_change_line(&ops, line + 2, line[0] == 'S' ? VMQG_OP_ADD : VMQG_OP_DEL)) {
+        fprintf(stderr, "bad change: %s\n", line);
+        return 6;
       }
-      if (vmqgb_ops_add_filter(&ops, ctx, line[0] == 'S' ? VMQG_OP_ADD : VMQG_OP_DEL, mp, (const uint8_t*)f, fl, node,
-                               sub, info)) { fprintf(stderr, "add_filter failed: %s\n", line); return 6; }
+    } else if (line[0] == 'G') {
+      group_open = 0;
+    } else if (line[0] == 'X') {
+      if (!group_open) {   /* the first X after a G (or the start) opens a group */
+        groups = (char***)realloc(groups, (ngroups + 1) * sizeof(char**));
+        groups[ngroups] = (char**)calloc(1, sizeof(char*));
+        ngroups++;
+        group_open = 1;
+      }
+      char** g = groups[ngroups - 1];
+      size_t k = 0;
+      while (g[k]) k++;
+      g = (char**)realloc(g, (k + 2) * sizeof(char*));
+      g[k] = strdup(line + 2);
+      g[k + 1] = NULL;
+      groups[ngroups - 1] = g;
     } else if (line[0] == 'A') {
       const int rc = vmqgb_view_apply(view, &ops, NULL);
       if (rc) { fprintf(stderr, "apply: %d\n", rc); return 7; }
@@ -205,6 +336,22 @@ int main(int argc, char** argv) {
       pubs[npubs].topic = strdup(line + 2 + off);
       pubs[npubs].len = strlen(pubs[npubs].topic);
       npubs++;
+    } else if (line[0] == 'W') {
+      char mode[16];
+      int T = 1, passes = 1;
+      size_t B = 1;
+      if (sscanf(line + 2, "%15s %d %zu %d", mode, &T, &B, &passes) < 4 || T < 1 || T > 64 || B < 1) return 9;
+      vmqgb_view_stats s0, s1;
+      vmqgb_view_get_stats(view, &s0);
+      const int rc = run_w(out, strcmp(mode, "ranges") == 0, T, B, passes);
+      if (rc) { fprintf(stderr, "W: %d\n", rc); return 11; }
+      vmqgb_view_get_stats(view, &s1);
+      fprintf(out, "v %llu %llu %llu\n", (unsigned long long)(s1.rounds - s0.rounds),
+              (unsigned long long)(s1.stale_rematches - s0.stale_rematches),
+              (unsigned long long)(s1.round_batches - s0.round_batches));
+      for (size_t k = 0; k < ngroups; k++) { for (char** l = groups[k]; *l; l++) free(*l); free(groups[k]); }
+      ngroups = 0;
+      group_open = 0;
     } else if (line[0] == 'M' || line[0] == 'C') {
       char mode[16];
       int T = 1, rounds = 0;

@@ -68,9 +68,57 @@ int main(void) {
   CHECK(vmqgb_batch_add(&b2, ctx, 0, longt, 4001) == 1);
   CHECK(b2.pubs[1].nwords == 2001);
   CHECK(b1.n == 1 && b1.pubs[0].nwords == 3 && b1.words[1] == VMQG_WORD_UNKNOWN);
-  CHECK(b2.pubs[0].flags == VMQG_PUB_DOLLAR);
+  CHECK(b2.pubs[0].flags == (VMQG_PUB_DOLLAR | VMQG_PUB_UNKNOWN));   /* "$SYS", "x": no filter has them */
+  CHECK(b1.pubs[0].flags == VMQG_PUB_UNKNOWN && b1.n_unk == 1 && b2.n_unk == 1);   /* the long topic is all "a": known */
   CHECK(vmqgb_batch_append(&b1, &b2) == 0);
   CHECK(b1.n == 3 && b1.pubs[1].word_off == 3 && b1.pubs[2].word_off == 5 && b1.nwords == 3 + 2 + 2001);
+  CHECK(b1.n_unk == 2 && b1.unk[3] == 1);   /* the appended batch's unknown publishes follow */
+
+  /* the batched prepare agrees with the one-topic form, rejects per topic */
+  {
+    const char* ts[6] = {"a/b/c", "a//c", "a/+/c", "$SYS/x", "/a", "q/#"};
+    const uint8_t* tp[6];
+    size_t tl[6];
+    uint32_t mps[6] = {0, 0, 0, 0, 3, 0};
+    long idx[6];
+    for (int i = 0; i < 6; i++) { tp[i] = (const uint8_t*)ts[i]; tl[i] = strlen(ts[i]); }
+    vmqgb_batch bm, bs;
+    CHECK(vmqgb_batch_init(&bm, 1) == 0 && vmqgb_batch_init(&bs, 1) == 0);
+    CHECK(vmqgb_batch_add_many(&bm, ctx, 6, mps, tp, tl, idx) == 0);
+    CHECK(idx[0] == 0 && idx[1] == 1 && idx[2] == VMQG_E_INVAL && idx[3] == 2 && idx[4] == 3 && idx[5] == VMQG_E_INVAL);
+    for (int i = 0; i < 6; i++) if (idx[i] >= 0) CHECK(vmqgb_batch_add(&bs, ctx, mps[i], tp[i], tl[i]) >= 0);
+    CHECK(bm.n == 4 && bs.n == 4 && bm.nwords == bs.nwords);
+    CHECK(memcmp(bm.pubs, bs.pubs, 4 * sizeof(vmqg_pub)) == 0 && memcmp(bm.words, bs.words, bm.nwords * 4) == 0);
+    CHECK(bm.pubs[1].flags == 0 && bm.pubs[3].mountpoint == 3 && bm.words[4] != VMQG_WORD_UNKNOWN);   /* "a//c" known */
+    /* a word interned after the prepare: recheck finds it, updates the ids */
+    CHECK(vmqgb_batch_recheck(&bm, ctx) == 0);
+    CHECK(vmqgb_ops_add_filter(&ops, ctx, VMQG_OP_ADD, 0, (const uint8_t*)"a/b/#", 5, 0, 4, 0) == 0);
+    CHECK(vmqgb_batch_recheck(&bm, ctx) == 1 && bm.words[1] != VMQG_WORD_UNKNOWN && !(bm.pubs[0].flags & VMQG_PUB_UNKNOWN));
+    CHECK(vmqgb_batch_recheck(&bm, ctx) == 0);
+    CHECK(vmqgb_ops_apply(&ops, ctx, &epoch) == 0 && epoch == 2);
+    vmqgb_batch_free(&bm);
+    vmqgb_batch_free(&bs);
+  }
+  /* the view on a host-only context: no pipeline, the device call refused */
+  {
+    vmqgb_view* v = vmqgb_view_new(ctx);
+    CHECK(v != NULL);
+    vmqgb_batch bv;
+    CHECK(vmqgb_batch_init(&bv, 4) == 0);
+    vmqgb_view_read_begin(v);
+    CHECK(vmqgb_batch_add(&bv, ctx, 0, (const uint8_t*)"a/b/c", 5) == 0);
+    const vmqg_emit* r0 = NULL;
+    uint64_t n0 = 0;
+    CHECK(vmqgb_view_match(v, &bv, 0, NULL, NULL) == VMQG_E_DEVICE);
+    CHECK(vmqgb_view_match(v, &bv, 1, &r0, &n0) == VMQG_E_DEVICE);
+    vmqgb_view_release(v, &bv);
+    vmqgb_view_read_end(v);
+    vmqgb_view_stats vs;
+    vmqgb_view_get_stats(v, &vs);
+    CHECK(vs.rounds == 0);
+    vmqgb_batch_free(&bv);
+    vmqgb_view_free(v);
+  }
   /* a host-only context refuses to match (no CPU fallback) */
   CHECK(vmqgb_match(&b1, ctx) == VMQG_E_DEVICE);
   CHECK(vmqgb_match_ranges(&b1, ctx) == VMQG_E_DEVICE);
@@ -81,7 +129,7 @@ int main(void) {
                              {(VMQG_EMIT_GROUP << 24) | 2, 77, 12, 0},
                              {(VMQG_EMIT_LOCAL << 24) | 0, VMQG_NONE, 13, 0}};
   b1.n = 2;
-  b1.offsets = (uint64_t*)realloc(b1.offsets, 3 * sizeof(uint64_t));
+  b1.offsets = b1.offs_buf = (uint64_t*)realloc(b1.offs_buf, 3 * sizeof(uint64_t));
   b1.offsets[0] = 0; b1.offsets[1] = 3; b1.offsets[2] = 4;
   b1.out = (vmqg_emit*)realloc(b1.out, 4 * sizeof(vmqg_emit));
   b1.out[0] = recs[1]; b1.out[1] = recs[2]; b1.out[2] = (vmqg_emit){(VMQG_EMIT_REMOTE << 24) | 70, VMQG_NONE, VMQG_NONE, VMQG_NONE};
@@ -91,7 +139,7 @@ int main(void) {
   CHECK(got[0].kind == VMQG_EMIT_LOCAL && got[0].subscriber == 11 && got[0].subinfo == 2);
   CHECK(got[1].kind == VMQG_EMIT_GROUP && got[1].node == 2 && got[1].group == 77);
   CHECK(got[2].kind == VMQG_EMIT_REMOTE && got[2].node == 70);
-  b1.rng = (vmqg_range*)realloc(b1.rng, 3 * sizeof(vmqg_range));
+  b1.rng = b1.rng_buf = (vmqg_range*)realloc(b1.rng_buf, 3 * sizeof(vmqg_range));
   b1.rng[0] = (vmqg_range){1, 2};    /* records 1, 2 */
   b1.rng[1] = (vmqg_range){70, 0};   /* remote node 70 */
   b1.rng[2] = (vmqg_range){3, 1};

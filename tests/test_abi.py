@@ -32,7 +32,7 @@ def test_every_declared_symbol_is_exported():
     assert not missing, missing
     bound = {name for name, _, _ in _lib.SIGNATURES}
     assert set(decl) == bound, set(decl) ^ bound
-    assert L.vmqg_abi_version() == 3
+    assert L.vmqg_abi_version() == 4
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -194,7 +194,58 @@ def test_prepare_publish_follows_validate_topic():
             assert rc == _lib.E_INVAL, c
     t = b"$SYS/x"
     assert L.vmqg_prepare_publish(v.handle, 0, t, len(t), words.ctypes.data, 64, ctypes.byref(pub)) == 0
-    assert pub.flags == _lib.PUB_DOLLAR and pub.nwords == 2
+    assert pub.flags == _lib.PUB_DOLLAR | _lib.PUB_UNKNOWN and pub.nwords == 2
+    t = b"foo/baz"
+    assert L.vmqg_prepare_publish(v.handle, 0, t, len(t), words.ctypes.data, 64, ctypes.byref(pub)) == 0
+    assert pub.flags == 0
+
+
+def test_batched_prepare_equals_the_single_form():
+    """vmqg_prepare_publishes (the pipelined dictionary probes) gives, topic
+    for topic, what vmqg_prepare_publish gives: same rejections, same words,
+    same flags — on the validate_topic KATs, long words (> 16 bytes, verified
+    beyond the slot's inline prefix), empty levels, many blocks."""
+    from tests import scenarios as S
+    from vernemq_amd.reg_view import PUB_DTYPE, RegGpuView
+    v = RegGpuView(device=-1)
+    known = [b"foo", b"baz", b"a" * 16, b"a" * 17, b"b" * 40, b"", b"w%d" % 7]
+    v.intern_words(known + [b"x%d" % i for i in range(3000)], create=True)
+    L = _lib.lib()
+    topics = [c["topic"].encode() for c in S.load("topic_validation.json")["cases"] if c["type"] == "publish"]
+    topics += [b"a" * 16 + b"/" + b"a" * 17, b"a" * 17 + b"/" + b"a" * 16 + b"x", b"b" * 40 + b"/b" * 3,
+               b"b" * 39 + b"c", b"/foo//baz/", b"$SYS/foo", b"w7/+", b"#"]
+    topics += [b"x%d/foo/y%d" % (i, i % 5) for i in range(700)]
+    n = len(topics)
+    ptrs = (ctypes.c_char_p * n)(*topics)
+    lens = np.array([len(t) for t in topics], dtype=np.uint64)
+    mps = np.arange(n, dtype=np.uint32) % 3
+    pubs = np.zeros(n, dtype=PUB_DTYPE)
+    rcs = np.zeros(n, dtype=np.int32)
+    cap = int((lens + 1).sum())
+    words = np.zeros(cap, dtype=np.uint32)
+    nw = ctypes.c_size_t(0)
+    assert L.vmqg_prepare_publishes(v.handle, n, mps.ctypes.data, ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data,
+                                    pubs.ctypes.data, rcs.ctypes.data, words.ctypes.data, cap, ctypes.byref(nw)) == 0
+    one = np.zeros(64, dtype=np.uint32)
+    total = 0
+    for i, t in enumerate(topics):
+        pub = _lib.Pub()
+        rc = L.vmqg_prepare_publish(v.handle, int(mps[i]), t, len(t), one.ctypes.data, 64, ctypes.byref(pub))
+        assert rc == rcs[i], (t, rc, rcs[i])
+        if rc:
+            continue
+        p = pubs[i]
+        assert (p["mountpoint"], p["nwords"], p["flags"]) == (pub.mountpoint, pub.nwords, pub.flags), t
+        assert list(words[p["word_off"]:p["word_off"] + p["nwords"]]) == list(one[:pub.nwords]), t
+        total += pub.nwords
+    assert total == nw.value
+    # too small a word buffer is refused, not overrun
+    assert L.vmqg_prepare_publishes(v.handle, n, mps.ctypes.data, ctypes.cast(ptrs, ctypes.c_void_p), lens.ctypes.data,
+                                    pubs.ctypes.data, rcs.ctypes.data, words.ctypes.data, 10, ctypes.byref(nw)) == \
+        _lib.E_OVERFLOW
+    g0 = L.vmqg_dict_generation(v.handle)
+    v.intern_words([b"brand-new"], create=True)
+    assert L.vmqg_dict_generation(v.handle) == g0 + 1
 
 
 def test_intern_reserved_words():

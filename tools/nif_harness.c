@@ -4,25 +4,35 @@
  * 1,000,000 devices/{d}/telemetry/# + 64 devices/+/telemetry/#, publishes
  * devices/{d}/telemetry/m{k} as raw topic bytes, d uniform in [0, 1.25M).
  *
- Threading exactly as the NIF's (vmqg_nif.c match/4 under
+ * Threading exactly as the NIF's (vmqg_nif.c match/4 under
  * vmq_reg_gpu_batcher): T batcher threads, each with its own batch of B
  * publishes, each batch under the view's read lock (vmqgb_view_*):
- *   prepare  vmqg_prepare_publish on raw topics (vmq_topic:validate_topic +
- *            word lookup), into the batcher's batch
- *   match    vmqgb_view_match: vmqgb_match (records: H2D + kernels + D2H of
- *            every record) or vmqgb_match_ranges (D2H of {record off, count}
- *            entries only); the device call is the only serialised step
+ *   prepare  vmqgb_batch_add_many on raw topics (vmq_topic:validate_topic +
+ *            word lookup), slices of VMQGB_YIELD_EVERY with a yield between
+ *   match    vmqgb_view_match: the combining submitter (batches queued at
+ *            once matched as one device call, rounds pipelined)
  *   fold     every FoldFun argument of every publish (the NIF builds one term
  *            per entry here; the harness sums the ids)
- * and once more with a writer applying config D's 100k changes/s (write
- * lock) while 16 batchers run.  Prints one JSON line per configuration.
- * Needs a GPU.  argv[1]: seconds per configuration (default 3).
+ * Sections (argv[2..], default all):
+ *   scale    1..48 batchers, records and ranges
+ *   devrec   records copied by the device over PCIe (vmqgb_view_set_device_records)
+ *   churn    subscriber events at 100k/s (config D's 1 %/s of 10M) while 16
+ *            and 32 batchers run, applied the way the Erlang view applies
+ *            them: "single" = one vmqgb_view_apply per event (round 3's
+ *            vmq_reg_gpu_view), "coalesced" = every event queued since the
+ *            last apply in one apply (vmq_reg_gpu_view's drain_events +
+ *            vmqg_nif:apply_many); the events unsubscribe and resubscribe
+ *            real devices/{d}/telemetry/# filters, so they change answers
+ *   load     initialize_trie while matching: a writer interning new
+ *            subscriptions as vmqg_nif:add_init does (table lock only, an
+ *            apply every 65,536) while 16 batchers run
+ * Prints one JSON line per configuration.  Needs a GPU.  argv[1]: seconds
+ * per configuration (default 3).
  *
- * build: gcc -O2 -std=gnu11 -pthread -Iinclude -Iintegration/c_src tools/nif_harness.c \
- *        integration/c_src/vmqg_batch.c -Lvernemq_amd -l:libvmqgpu.so \
- *        -Wl,-rpath,'$ORIGIN/../../vernemq_amd' -o tools/bin/nif_harness
+ * build: see tools/Makefile (gcc -O2 -pthread ... integration/c_src/vmqg_batch.c -l:libvmqgpu.so)
  */
 #define _GNU_SOURCE
+
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -48,8 +58,11 @@ static uint64_t splitmix(void) {
 static vmqg_ctx* ctx;
 static vmqgb_view* view;
 static char* topics;            /* NPUB topics, 40 bytes each, NUL padded */
-static uint16_t* tlen;
+static size_t* tlen;
+static const uint8_t** tptr;
+static uint32_t* tmp0;           /* mountpoint 0 for every publish */
 static size_t NPUB;
+static const size_t NDEV = 1000000, NWILD = 64;
 
 static int sum_entry(void* acc, const vmqgb_entry* e) {
   uint64_t* s = (uint64_t*)acc;
@@ -59,9 +72,6 @@ static int sum_entry(void* acc, const vmqgb_entry* e) {
 }
 
 /* ------------------------------------------------------------ batchers */
-/* One batcher thread = one vmq_reg_gpu_batcher process and its match/4 NIF
- * call (integration/c_src/vmqg_nif.c): its own batch, the view's read lock
- * around prepare, the device call (serialised by the view) and the fold. */
 typedef struct {
   int tid, T, ranges;
   size_t B;
@@ -75,27 +85,30 @@ static void* batcher(void* p) {
   bt_t* a = (bt_t*)p;
   vmqgb_batch b;
   vmqgb_batch_init(&b, a->B);
+  long* idx = (long*)malloc(a->B * sizeof(long));
   uint64_t acc[2] = {0, 0};
   size_t lo = ((size_t)a->tid * a->B * 7919) % NPUB;
   while (now() < a->t_end) {
     const double t0 = now();
     vmqgb_view_read_begin(view);
     vmqgb_batch_reset(&b);
-    for (size_t i = 0; i < a->B; i++) {
-      if (i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(view);
-      const size_t q = (lo + i) % NPUB;
-      if (vmqgb_batch_add(&b, ctx, 0, (const uint8_t*)topics + q * 40, tlen[q]) < 0) { a->err = 1; break; }
+    if (lo + a->B > NPUB) lo = 0;
+    for (size_t s = 0; s < a->B; s += VMQGB_YIELD_EVERY) {
+      const size_t k = a->B - s < VMQGB_YIELD_EVERY ? a->B - s : VMQGB_YIELD_EVERY;
+      if (s) vmqgb_view_yield(view);
+      if (vmqgb_batch_add_many(&b, ctx, k, tmp0 + lo + s, tptr + lo + s, tlen + lo + s, idx + s)) { a->err = 1; break; }
     }
     lo = (lo + (size_t)a->T * a->B) % NPUB;
     const double t1 = now();
     const vmqg_emit* recs = NULL;
     uint64_t nrecs = 0;
-    int rc = vmqgb_view_match(view, &b, a->ranges, &recs, &nrecs);
+    int rc = a->err ? 0 : vmqgb_view_match(view, &b, a->ranges, &recs, &nrecs);
     const double t2 = now();
     for (size_t i = 0; !rc && i < b.n; i++) {
       if (!a->ranges && i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(view);   /* records: copies */
       rc = a->ranges ? vmqgb_fold_ranges(&b, recs, nrecs, i, sum_entry, acc) : vmqgb_fold(&b, i, sum_entry, acc);
     }
+    vmqgb_view_release(view, &b);
     vmqgb_view_read_end(view);
     const double t3 = now();
     if (rc || a->err) { a->err = rc ? rc : a->err; break; }
@@ -105,47 +118,222 @@ static void* batcher(void* p) {
   }
   a->sum = acc[0];
   a->entries = acc[1];
+  free(idx);
   vmqgb_batch_free(&b);
   return NULL;
 }
 
-/* config D's churn rate on this shape: a writer applying `ops` subscription
- * changes every `period` seconds (half adds, half deletes of extra device
- * filters that no publish matches) while the batchers run */
-typedef struct { double t_end, period; int ops; uint64_t applied; double t_apply; int err; } churn_t;
+/* ------------------------------------------------------------- churn */
+/* subscriber events: device d's devices/{d}/telemetry/# unsubscribed, later
+ * subscribed again (one change per event, as a one-topic SUBSCRIBE /
+ * UNSUBSCRIBE makes), produced at `rate` per second with their due times */
+typedef struct { uint32_t d, kind; double t; } event_t;
+typedef struct {
+  double t_end, rate;
+  int coalesce;                 /* 0: one apply per event; 1: everything queued in one apply */
+  pthread_mutex_t mu;
+  event_t* q;
+  size_t cap, head, tail;       /* ring */
+  uint64_t produced, applied, applies, max_group;
+  double lag_sum, lag_max, wait_max, apply_sum;
+  double* lags;                 /* sample of lags for percentiles */
+  size_t nlags, lags_cap;
+  size_t max_backlog;
+  int err;
+} churn_t;
 
-static void* churner(void* p) {
+static void* producer(void* p) {
+  churn_t* c = (churn_t*)p;
+  const double t0 = now();
+  uint64_t k = 0;
+  while (now() < c->t_end && !c->err) {
+    const double due = now();
+    const uint64_t want = (uint64_t)((due - t0) * c->rate);
+    pthread_mutex_lock(&c->mu);
+    for (; k < want; k++) {
+      const size_t used = c->tail - c->head;
+      if (used == c->cap) break;   /* the writer fell too far behind: stop producing (reported as backlog) */
+      event_t* e = &c->q[c->tail % c->cap];
+      /* a rotating window of 20,000 devices: unsubscribe them, then resubscribe */
+      e->d = (uint32_t)((k % 20000) * 50);
+      e->kind = (k / 20000) % 2 ? VMQG_OP_ADD : VMQG_OP_DEL;
+      e->t = t0 + (double)k / c->rate;
+      c->tail++;
+      c->produced++;
+      if (c->tail - c->head > c->max_backlog) c->max_backlog = c->tail - c->head;
+    }
+    pthread_mutex_unlock(&c->mu);
+    struct timespec ts = {0, 200000};
+    nanosleep(&ts, NULL);
+  }
+  return NULL;
+}
+
+static void* applier(void* p) {   /* the vmq_reg_gpu_view gen_server */
   churn_t* c = (churn_t*)p;
   vmqgb_ops ops;
   vmqgb_ops_init(&ops);
-  uint32_t k = 0;
-  double next = now();
+  event_t* grp = (event_t*)malloc(10000 * sizeof(event_t));
+  char f[64];
   while (now() < c->t_end && !c->err) {
-    while (now() < next) { struct timespec ts = {0, 200000}; nanosleep(&ts, NULL); }
-    next += c->period;
-    vmqgb_ops_reset(&ops);
-    for (int i = 0; i < c->ops; i++, k++) {
-      char f[48];
-      const uint32_t slot = k % 20000;
-      const int l = snprintf(f, sizeof f, "churn/%u/telemetry/#", slot);
-      const uint32_t kind = (k / 20000) % 2 ? VMQG_OP_DEL : VMQG_OP_ADD;
-      if (vmqgb_ops_add_filter(&ops, ctx, kind, 0, (const uint8_t*)f, (size_t)l, 0, 2000000 + slot, 1)) { c->err = 1; break; }
-    }
+    pthread_mutex_lock(&c->mu);
+    size_t n = c->tail - c->head;
+    if (!c->coalesce && n > 1) n = 1;
+    if (n > 10000) n = 10000;
+    for (size_t i = 0; i < n; i++) grp[i] = c->q[(c->head + i) % c->cap];
+    c->head += n;
+    pthread_mutex_unlock(&c->mu);
+    if (!n) { struct timespec ts = {0, 50000}; nanosleep(&ts, NULL); continue; }
     const double t0 = now();
-    if (!c->err && vmqgb_view_apply(view, &ops, NULL)) c->err = 2;
-    c->t_apply += now() - t0;
-    c->applied += (uint64_t)c->ops;
+    vmqgb_view_write_begin(view);   /* interning happens under the table lock (the NIF's add_change) */
+    const double t1 = now();
+    for (size_t i = 0; i < n; i++) {
+      const int l = snprintf(f, sizeof f, "devices/%u/telemetry/#", grp[i].d);
+      if (vmqgb_ops_add_filter(&ops, ctx, grp[i].kind, 0, (const uint8_t*)f, (size_t)l, 0, grp[i].d, grp[i].d % 3)) {
+        c->err = 1;
+        break;
+      }
+    }
+    const int rc = c->err ? 0 : vmqgb_view_apply_ops(view, &ops, NULL);
+    vmqgb_ops_reset(&ops);
+    vmqgb_view_write_end(view);
+    const double t2 = now();
+    if (rc) { c->err = 2; break; }
+    if (t1 - t0 > c->wait_max) c->wait_max = t1 - t0;
+    c->apply_sum += t2 - t0;
+    c->applies++;
+    c->applied += n;
+    if (n > c->max_group) c->max_group = n;
+    for (size_t i = 0; i < n; i++) {
+      const double lag = t2 - grp[i].t;
+      c->lag_sum += lag;
+      if (lag > c->lag_max) c->lag_max = lag;
+      if (c->nlags < c->lags_cap) c->lags[c->nlags++] = lag;
+    }
   }
+  free(grp);
   vmqgb_ops_free(&ops);
   return NULL;
 }
 
+static int cmp_d(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : x > y;
+}
+
+/* ------------------------------------------------------------- load */
+/* initialize_trie while matching: vmqg_nif:add_init's locking (table lock
+ * per subscription, the device mutex only for the apply of every 65,536) */
+typedef struct { double t_end; uint64_t added, applies; double wait_max; int err; } load_t;
+
+static void* loader(void* p) {
+  load_t* L = (load_t*)p;
+  vmqgb_ops ops;
+  vmqgb_ops_init(&ops);
+  char f[64];
+  uint64_t k = 0;
+  while (now() < L->t_end && !L->err) {
+    const double t0 = now();
+    vmqgb_view_write_begin(view);
+    const double w = now() - t0;
+    if (w > L->wait_max) L->wait_max = w;
+    const int l = snprintf(f, sizeof f, "fleet/%llu/telemetry/#", (unsigned long long)k);
+    if (vmqgb_ops_add_filter(&ops, ctx, VMQG_OP_ADD, 0, (const uint8_t*)f, (size_t)l, 0, 3000000 + (uint32_t)k, 1))
+      L->err = 1;
+    if (!L->err && ops.n >= 65536) {
+      if (vmqgb_view_apply_ops(view, &ops, NULL)) L->err = 2;
+      vmqgb_ops_reset(&ops);
+      L->applies++;
+    }
+    vmqgb_view_write_end(view);
+    k++;
+  }
+  vmqgb_view_write_begin(view);
+  if (ops.n && vmqgb_view_apply_ops(view, &ops, NULL)) L->err = 2;
+  vmqgb_view_write_end(view);
+  L->added = k;
+  vmqgb_ops_free(&ops);
+  return NULL;
+}
+
+/* ----------------------------------------------------------------- run */
+static uint64_t checksum;
+
+static int run(const char* section, int T, size_t B, int ranges, double secs, churn_t* cc, load_t* ld) {
+  bt_t a[64];
+  pthread_t th[64], cw[2];
+  vmqgb_view_stats s0, s1;
+  vmqgb_view_get_stats(view, &s0);
+  const double tstart = now(), t_end = tstart + secs;
+  if (cc) {
+    cc->t_end = t_end;
+    pthread_create(&cw[0], NULL, producer, cc);
+    pthread_create(&cw[1], NULL, applier, cc);
+  }
+  if (ld) { ld->t_end = t_end; pthread_create(&cw[0], NULL, loader, ld); }
+  for (int t = 0; t < T; t++) {
+    memset(&a[t], 0, sizeof a[t]);
+    a[t].tid = t; a[t].T = T; a[t].ranges = ranges; a[t].B = B; a[t].t_end = t_end;
+    pthread_create(&th[t], NULL, batcher, &a[t]);
+  }
+  uint64_t pubs = 0, ents = 0, nb = 0;
+  double tp = 0, tm = 0, tf = 0;
+  int err = 0;
+  for (int t = 0; t < T; t++) {
+    pthread_join(th[t], NULL);
+    if (a[t].err) { fprintf(stderr, "batcher %d failed: %d\n", t, a[t].err); err = 4; }
+    pubs += a[t].pubs; ents += a[t].entries; nb += a[t].batches; checksum += a[t].sum;
+    tp += a[t].t_prep; tm += a[t].t_match; tf += a[t].t_fold;
+  }
+  if (cc) { pthread_join(cw[0], NULL); pthread_join(cw[1], NULL); if (cc->err) { fprintf(stderr, "churn failed %d\n", cc->err); err = 5; } }
+  if (ld) { pthread_join(cw[0], NULL); if (ld->err) { fprintf(stderr, "load failed %d\n", ld->err); err = 6; } }
+  const double el = now() - tstart;
+  vmqgb_view_get_stats(view, &s1);
+  const uint64_t rounds = s1.rounds - s0.rounds;
+  printf("{\"section\": \"%s\", \"mode\": \"%s\", \"batchers\": %d, \"batch\": %zu, \"seconds\": %.2f, "
+         "\"publishes\": %llu, \"entries\": %llu, \"publishes_per_s\": %.4g, \"entries_per_s\": %.4g, "
+         "\"per_batch_ms\": {\"prepare\": %.3f, \"match\": %.3f, \"fold\": %.3f}, "
+         "\"rounds\": %llu, \"publishes_per_round\": %.0f, \"batches_per_round\": %.2f, "
+         "\"expanded_batches\": %llu, \"device_record_batches\": %llu, \"state_retries\": %llu, "
+         "\"stale_rematches\": %llu, \"overflow_retries\": %llu",
+         section, ranges ? "ranges" : "records", T, B, el, (unsigned long long)pubs, (unsigned long long)ents,
+         pubs / el, ents / el, nb ? tp * 1e3 / nb : 0, nb ? tm * 1e3 / nb : 0, nb ? tf * 1e3 / nb : 0,
+         (unsigned long long)rounds, rounds ? (double)(s1.round_publishes - s0.round_publishes) / rounds : 0.0,
+         rounds ? (double)(s1.round_batches - s0.round_batches) / rounds : 0.0,
+         (unsigned long long)(s1.expanded_batches - s0.expanded_batches),
+         (unsigned long long)(s1.device_record_batches - s0.device_record_batches),
+         (unsigned long long)(s1.state_retries - s0.state_retries),
+         (unsigned long long)(s1.stale_rematches - s0.stale_rematches),
+         (unsigned long long)(s1.overflow_retries - s0.overflow_retries));
+  if (cc) {
+    qsort(cc->lags, cc->nlags, sizeof(double), cmp_d);
+    const double p50 = cc->nlags ? cc->lags[cc->nlags / 2] : 0, p99 = cc->nlags ? cc->lags[(size_t)(cc->nlags * 0.99)] : 0;
+    printf(", \"churn\": {\"delivery\": \"%s\", \"events_per_s_offered\": %.4g, \"events_applied_per_s\": %.4g, "
+           "\"applies\": %llu, \"mean_events_per_apply\": %.1f, \"max_events_per_apply\": %llu, "
+           "\"backlog_at_end\": %llu, \"max_backlog\": %zu, \"lag_ms\": {\"p50\": %.3f, \"p99\": %.3f, \"max\": %.3f}, "
+           "\"max_write_lock_wait_ms\": %.3f, \"mean_apply_section_ms\": %.3f}",
+           cc->coalesce ? "coalesced" : "single", cc->produced / el, cc->applied / el, (unsigned long long)cc->applies,
+           cc->applies ? (double)cc->applied / cc->applies : 0.0, (unsigned long long)cc->max_group,
+           (unsigned long long)(cc->produced - cc->applied), cc->max_backlog, p50 * 1e3, p99 * 1e3, cc->lag_max * 1e3,
+           cc->wait_max * 1e3, cc->applies ? cc->apply_sum * 1e3 / cc->applies : 0.0);
+  }
+  if (ld)
+    printf(", \"load\": {\"subscriptions_added_per_s\": %.4g, \"applies\": %llu, \"max_write_lock_wait_ms\": %.3f}",
+           ld->added / el, (unsigned long long)ld->applies, ld->wait_max * 1e3);
+  printf(", \"build\": \"%s\"}\n", vmqg_build_id());
+  fflush(stdout);
+  return err;
+}
+
+static int want(int argc, char** argv, const char* s) {
+  if (argc <= 2) return 1;
+  for (int i = 2; i < argc; i++) if (!strcmp(argv[i], s)) return 1;
+  return 0;
+}
+
 int main(int argc, char** argv) {
-  const size_t NDEV = 1000000, NWILD = 64;
   NPUB = (size_t)1 << 20;
   const double secs = argc > 1 ? atof(argv[1]) : 3.0;
-  const int threads_list[] = {1, 4, 8, 16, 32};
-  const size_t batch_list[] = {1024, 4096};
   vmqg_config cfg;
   memset(&cfg, 0, sizeof cfg);
   cfg.device = 0;
@@ -155,76 +343,86 @@ int main(int argc, char** argv) {
   ctx = vmqg_create(&cfg, &err);
   if (!ctx) { fprintf(stderr, "vmqg_create: %d\n", err); return 1; }
   view = vmqgb_view_new(ctx);
-  /* subscriptions through the NIF's op layer: subscriber ids from an interner */
-  vmqgb_interner* subs = vmqgb_interner_new();
+  /* subscriptions through the NIF's op layer; subscriber id = device index
+   * (c{d}), the wildcard subscribers after them */
   vmqgb_ops ops;
   vmqgb_ops_init(&ops);
-  char buf[64];
   double t0 = now();
   for (size_t d = 0; d < NDEV + NWILD; d++) {
-    const int ln = d < NDEV ? snprintf(buf, sizeof buf, "c%zu", d) : snprintf(buf, sizeof buf, "w%zu", d - NDEV);
-    const uint32_t sid = vmqgb_intern(subs, buf, (size_t)ln);
     char f[64];
     const int fl = d < NDEV ? snprintf(f, sizeof f, "devices/%zu/telemetry/#", d) : snprintf(f, sizeof f, "devices/+/telemetry/#");
-    if (vmqgb_ops_add_filter(&ops, ctx, VMQG_OP_ADD, 0, (const uint8_t*)f, (size_t)fl, 0, sid, (uint32_t)(d % 3))) return 2;
-    if (ops.n == 65536 || d + 1 == NDEV + NWILD) {
-      if (vmqgb_view_apply(view, &ops, NULL)) { fprintf(stderr, "apply failed\n"); return 3; }
+    vmqgb_view_write_begin(view);
+    if (vmqgb_ops_add_filter(&ops, ctx, VMQG_OP_ADD, 0, (const uint8_t*)f, (size_t)fl, 0, (uint32_t)d, (uint32_t)(d % 3))) return 2;
+    if ((ops.n == 65536 || d + 1 == NDEV + NWILD) && vmqgb_view_apply_ops(view, &ops, NULL)) {
+      fprintf(stderr, "apply failed\n");
+      return 3;
     }
+    vmqgb_view_write_end(view);
   }
   const double load_s = now() - t0;
   /* raw publish topics */
   topics = (char*)calloc(NPUB, 40);
-  tlen = (uint16_t*)calloc(NPUB, sizeof(uint16_t));
+  tlen = (size_t*)calloc(NPUB, sizeof(size_t));
+  tptr = (const uint8_t**)calloc(NPUB, sizeof(*tptr));
+  tmp0 = (uint32_t*)calloc(NPUB, sizeof(uint32_t));
   for (size_t i = 0; i < NPUB; i++) {
     const uint64_t r = splitmix();
-    tlen[i] = (uint16_t)snprintf(topics + i * 40, 40, "devices/%llu/telemetry/m%llu",
-                                 (unsigned long long)(r % (NDEV + NDEV / 4)), (unsigned long long)((r >> 40) % 16));
+    tlen[i] = (size_t)snprintf(topics + i * 40, 40, "devices/%llu/telemetry/m%llu",
+                               (unsigned long long)(r % (NDEV + NDEV / 4)), (unsigned long long)((r >> 40) % 16));
+    tptr[i] = (const uint8_t*)topics + i * 40;
   }
   fprintf(stderr, "loaded %zu subscriptions in %.1fs\n", NDEV + NWILD, load_s);
-  uint64_t checksum = 0;
-  for (int churn = 0; churn < 2; churn++) {
-    for (int mode = 0; mode < 2; mode++) {
-      for (size_t ti = 0; ti < sizeof threads_list / sizeof threads_list[0]; ti++) {
-        for (size_t bi = 0; bi < sizeof batch_list / sizeof batch_list[0]; bi++) {
-          const int T = threads_list[ti];
-          const size_t B = batch_list[bi];
-          if (churn && (T != 16 || B != 4096)) continue;   /* churn: the shipped shape only */
-          bt_t a[64];
-          pthread_t th[64], cw;
-          churn_t cc = {0, 0.01, 1000, 0, 0, 0};   /* 100k ops/s: config D's 1 %/s of 10M */
-          const double tstart = now(), t_end = tstart + secs;
-          cc.t_end = t_end;
-          if (churn) pthread_create(&cw, NULL, churner, &cc);
-          for (int t = 0; t < T; t++) {
-            memset(&a[t], 0, sizeof a[t]);
-            a[t].tid = t; a[t].T = T; a[t].ranges = mode; a[t].B = B; a[t].t_end = t_end;
-            pthread_create(&th[t], NULL, batcher, &a[t]);
+  int rc = 0;
+  if (want(argc, argv, "scale")) {
+    const int threads_list[] = {1, 8, 16, 24, 32, 48};
+    for (int mode = 0; mode < 2 && !rc; mode++)
+      for (size_t ti = 0; ti < sizeof threads_list / sizeof threads_list[0] && !rc; ti++)
+        rc = run("scale", threads_list[ti], 4096, mode, secs, NULL, NULL);
+  }
+  if (want(argc, argv, "devrec") && !rc) {
+    vmqgb_view_set_device_records(view, 1);
+    rc = run("devrec", 16, 4096, 0, secs, NULL, NULL);
+    if (!rc) rc = run("devrec", 32, 4096, 0, secs, NULL, NULL);
+    vmqgb_view_set_device_records(view, 0);
+  }
+  if (want(argc, argv, "churn")) {
+    for (int co = 0; co < 2 && !rc; co++)
+      for (int mode = 0; mode < 2 && !rc; mode++)
+        for (int T = 16; T <= 32 && !rc; T += 16) {
+          churn_t cc;
+          memset(&cc, 0, sizeof cc);
+          pthread_mutex_init(&cc.mu, NULL);
+          cc.rate = 100000;
+          cc.coalesce = co;
+          cc.cap = 1u << 21;
+          cc.q = (event_t*)malloc(cc.cap * sizeof(event_t));
+          cc.lags_cap = 1u << 22;
+          cc.lags = (double*)malloc(cc.lags_cap * sizeof(double));
+          rc = run("churn", T, 4096, mode, secs, &cc, NULL);
+          free(cc.q);
+          free(cc.lags);
+          /* resubscribe what the run left unsubscribed (the next run starts from the full set) */
+          vmqgb_view_write_begin(view);
+          for (uint32_t k = 0; k < 20000; k++) {
+            char f[64];
+            const int l = snprintf(f, sizeof f, "devices/%u/telemetry/#", k * 50);
+            vmqgb_ops_add_filter(&ops, ctx, VMQG_OP_DEL, 0, (const uint8_t*)f, (size_t)l, 0, k * 50, (k * 50) % 3);
+            vmqgb_ops_add_filter(&ops, ctx, VMQG_OP_ADD, 0, (const uint8_t*)f, (size_t)l, 0, k * 50, (k * 50) % 3);
           }
-          uint64_t pubs = 0, ents = 0, nb = 0;
-          double tp = 0, tm = 0, tf = 0;
-          for (int t = 0; t < T; t++) {
-            pthread_join(th[t], NULL);
-            if (a[t].err) { fprintf(stderr, "batcher %d failed: %d\n", t, a[t].err); return 4; }
-            pubs += a[t].pubs; ents += a[t].entries; nb += a[t].batches; checksum += a[t].sum;
-            tp += a[t].t_prep; tm += a[t].t_match; tf += a[t].t_fold;
-          }
-          if (churn) { pthread_join(cw, NULL); if (cc.err) { fprintf(stderr, "churn failed\n"); return 5; } }
-          const double el = now() - tstart;
-          printf("{\"threading\": \"vmqg_nif batchers (vmqgb_view)\", \"mode\": \"%s\", \"batchers\": %d, "
-                 "\"batch\": %zu, \"seconds\": %.2f, \"publishes\": %llu, \"entries\": %llu, \"publishes_per_s\": %.4g, "
-                 "\"entries_per_s\": %.4g, \"per_batch_ms\": {\"prepare\": %.3f, \"match\": %.3f, \"fold\": %.3f}, "
-                 "\"churn_ops_per_s\": %.4g, \"apply_ms_per_batch\": %.3f, \"load_s\": %.1f}\n",
-                 mode ? "ranges" : "records", T, B, el, (unsigned long long)pubs, (unsigned long long)ents, pubs / el,
-                 ents / el, nb ? tp * 1e3 / nb : 0, nb ? tm * 1e3 / nb : 0, nb ? tf * 1e3 / nb : 0,
-                 churn ? cc.applied / el : 0.0, churn && cc.applied ? cc.t_apply * 1e3 / (cc.applied / cc.ops) : 0.0,
-                 load_s);
-          fflush(stdout);
+          if (vmqgb_view_apply_ops(view, &ops, NULL)) rc = 7;
+          vmqgb_view_write_end(view);
         }
-      }
+  }
+  if (want(argc, argv, "load") && !rc) {
+    for (int mode = 0; mode < 2 && !rc; mode++) {
+      load_t ld;
+      memset(&ld, 0, sizeof ld);
+      rc = run("load", 16, 4096, mode, secs, NULL, &ld);
     }
   }
   fprintf(stderr, "checksum %llu\n", (unsigned long long)checksum);
+  vmqgb_ops_free(&ops);
   vmqgb_view_free(view);
   vmqg_destroy(ctx);
-  return 0;
+  return rc;
 }

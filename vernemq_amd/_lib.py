@@ -36,6 +36,7 @@ WORD_PLUS, WORD_HASH, WORD_SHARE, WORD_UNKNOWN = 0, 1, 2, 0xFFFFFFFF
 NONE = 0xFFFFFFFF
 OP_ADD, OP_DEL = 1, 2
 PUB_DOLLAR = 1
+PUB_UNKNOWN = 2
 EMIT_LOCAL, EMIT_GROUP, EMIT_REMOTE = 1, 2, 3
 CFG_REPLICA = 1
 LAYOUT_BYTES = 256
@@ -130,6 +131,14 @@ SIGNATURES = [
     ("vmqg_destroy", None, [_P]),
     ("vmqg_intern_words", ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
     ("vmqg_prepare_publish", ctypes.c_int, [_P, _U32, ctypes.c_char_p, _SZ, _P, _U32, ctypes.POINTER(Pub)]),
+    ("vmqg_prepare_publishes", ctypes.c_int, [_P, _SZ, _P, _P, _P, _P, _P, _P, _SZ, ctypes.POINTER(_SZ)]),
+    ("vmqg_dict_generation", _U64, [_P]),
+    ("vmqg_hbatch_new", _P, [_P]),
+    ("vmqg_hbatch_free", None, [_P]),
+    ("vmqg_hbatch_inputs", ctypes.c_int, [_P, _SZ, _SZ, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    ("vmqg_hbatch_submit", ctypes.c_int, [_P, _P, _SZ, _SZ, ctypes.c_int]),
+    ("vmqg_hbatch_offsets", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
+    ("vmqg_hbatch_entries", ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     ("vmqg_apply_ops", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, ctypes.POINTER(_U64)]),
     ("vmqg_match_batch", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
     ("vmqg_match_device", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),

@@ -74,23 +74,99 @@ int vmqg_prepare_publish(vmqg_ctx* ctx, uint32_t mountpoint, const uint8_t* topi
   if (!ctx || !pub || (len && !topic)) return VMQG_E_INVAL;
   if (len == 0 || len > 65536) return VMQG_E_INVAL;
   GUARD_BEGIN
-  uint32_t n = 0;
+  uint32_t n = 0, unknown = 0;
   size_t start = 0;
   for (size_t i = 0; i <= len; i++) {
     if (i < len && (topic[i] == '+' || topic[i] == '#')) return VMQG_E_INVAL;
     if (i == len || topic[i] == '/') {
       if (n >= cap) return VMQG_E_OVERFLOW;
-      words_out[n++] = ctx->e.intern(topic + start, i - start, false);
+      const uint32_t id = ctx->e.intern(topic + start, i - start, false);
+      unknown |= id == vmqg::kUnknownWord;
+      words_out[n++] = id;
       start = i + 1;
     }
   }
   pub->mountpoint = mountpoint;
   pub->word_off = 0;
   pub->nwords = n;
-  pub->flags = topic[0] == '$' ? VMQG_PUB_DOLLAR : 0u;
+  pub->flags = (topic[0] == '$' ? VMQG_PUB_DOLLAR : 0u) | (unknown ? VMQG_PUB_UNKNOWN : 0u);
   return VMQG_OK;
   GUARD_END
 }
+
+// The batched form: topics are split block by block; every word of a block is
+// hashed and its dictionary slot prefetched, then the block's words are
+// resolved — the probes of ~kBlock topics overlap instead of each costing a
+// full memory round trip (a 1M-word dictionary is 64 MB of slots).
+int vmqg_prepare_publishes(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints, const uint8_t* const* topics,
+                           const size_t* lens, vmqg_pub* pubs_out, int32_t* rc_out, uint32_t* words_out,
+                           size_t wcap, size_t* nwords_out) {
+  if (!ctx || (n && (!mountpoints || !topics || !lens || !pubs_out || !rc_out || !words_out))) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  const vmqg::WordDict& d = ctx->e.dict;
+  constexpr size_t kBlock = 64;
+  static thread_local std::vector<vmqg::WordDict::Key> keys;
+  size_t nw = 0;
+  for (size_t lo = 0; lo < n; lo += kBlock) {
+    const size_t hi = std::min(n, lo + kBlock);
+    keys.clear();
+    // split + validate (vmq_topic:validate_topic(publish, T), vmq_topic.erl:82-112),
+    // hash and prefetch; words_out holds the key index until resolved
+    for (size_t t = lo; t < hi; t++) {
+      const uint8_t* tp = topics[t];
+      const size_t len = lens[t];
+      vmqg_pub& pub = pubs_out[t];
+      pub = vmqg_pub{mountpoints[t], (uint32_t)nw, 0, 0};
+      rc_out[t] = VMQG_OK;
+      if (len == 0 || len > 65536 || !tp) { rc_out[t] = VMQG_E_INVAL; pub.mountpoint = 0; continue; }
+      if (nw + len + 1 > wcap) {
+        // a topic of len bytes has <= len + 1 words: count them before giving up
+        size_t words = 1;
+        for (size_t i = 0; i < len; i++) words += tp[i] == '/';
+        if (nw + words > wcap) return VMQG_E_OVERFLOW;
+      }
+      const size_t k0 = keys.size();
+      size_t start = 0;
+      bool bad = false;
+      for (size_t i = 0; i <= len; i++) {
+        const uint8_t c = i < len ? tp[i] : '/';
+        if (c == '+' || c == '#') { bad = true; break; }
+        if (c == '/') {
+          keys.push_back(vmqg::WordDict::key(tp + start, i - start));
+          d.prefetch(keys.back());
+          words_out[nw + pub.nwords++] = (uint32_t)(keys.size() - 1);
+          start = i + 1;
+        }
+      }
+      if (bad) {
+        keys.resize(k0);
+        rc_out[t] = VMQG_E_INVAL;
+        pub = vmqg_pub{0, (uint32_t)nw, 0, 0};
+        continue;
+      }
+      if (tp[0] == '$') pub.flags |= VMQG_PUB_DOLLAR;
+      nw += pub.nwords;
+    }
+    // resolve the block's words (their slots are on their way)
+    for (size_t t = lo; t < hi; t++) {
+      vmqg_pub& pub = pubs_out[t];
+      if (rc_out[t]) continue;
+      uint32_t unknown = 0;
+      for (uint32_t j = 0; j < pub.nwords; j++) {
+        uint32_t& w = words_out[pub.word_off + j];
+        const uint32_t f = d.find(keys[w]);
+        w = f == vmqg::WordDict::kVoid ? vmqg::kUnknownWord : f;
+        unknown |= w == vmqg::kUnknownWord;
+      }
+      if (unknown) pub.flags |= VMQG_PUB_UNKNOWN;
+    }
+  }
+  if (nwords_out) *nwords_out = nw;
+  return VMQG_OK;
+  GUARD_END
+}
+
+uint64_t vmqg_dict_generation(vmqg_ctx* ctx) { return ctx ? ctx->e.dict.generation() : 0; }
 
 int vmqg_apply_ops(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords,
                    uint64_t* epoch_out) {
@@ -172,6 +248,164 @@ int vmqg_match_ranges(vmqg_ctx* ctx, const vmqg_pub* pubs, size_t npub, const ui
   GUARD_END
 }
 
+// ---- pipelined host-buffer matching (vmqg_hbatch_*) --------------------
+struct vmqg_hbatch {
+  int device = -1;
+  hipStream_t cs = nullptr;                     // copy stream: H2D of the inputs, D2H of the entries
+  hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_out = nullptr;
+  vmqg_pub* h_pubs = nullptr; uint32_t* h_words = nullptr; uint64_t* h_offs = nullptr;
+  void* h_out = nullptr; uint32_t* h_err = nullptr;
+  uint64_t h_pubs_cap = 0, h_words_cap = 0, h_offs_cap = 0, h_out_cap = 0;   // bytes
+  void* d_pubs = nullptr; void* d_words = nullptr; void* d_offs = nullptr; void* d_out = nullptr;
+  uint64_t d_pubs_cap = 0, d_words_cap = 0, d_offs_cap = 0, d_out_cap = 0;   // bytes
+  uint64_t want_entries = 0;   // output capacity (entries) of the next submit
+  uint64_t out_entries = 0;    // ... of the submitted one
+  size_t npub = 0, esz = 16;
+  uint64_t epoch = 0, total = 0;
+  bool frontier = false;
+  int state = 0;               // 0 idle, 1 submitted, 2 offsets read
+};
+
+static int grow_pinned(void** p, uint64_t* cap, uint64_t need) {
+  if (*cap >= need) return VMQG_OK;
+  if (*p) hipHostFree(*p);
+  *p = nullptr;
+  uint64_t c = 4096;
+  while (c < need) c <<= 1;
+  if (hipHostMalloc(p, c, hipHostMallocDefault) != hipSuccess) { *cap = 0; return VMQG_E_NOMEM; }
+  *cap = c;
+  return VMQG_OK;
+}
+
+vmqg_hbatch* vmqg_hbatch_new(vmqg_ctx* ctx) {
+  if (!ctx || !ctx->e.has_device) return nullptr;
+  vmqg_hbatch* hb = new (std::nothrow) vmqg_hbatch();
+  if (!hb) return nullptr;
+  hb->device = ctx->e.device;
+  hipSetDevice(hb->device);
+  const unsigned evf = hipEventDisableTiming | hipEventBlockingSync;   // waiters sleep: batchers need the cores
+  if (hipStreamCreateWithFlags(&hb->cs, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&hb->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&hb->ev_k, evf) != hipSuccess || hipEventCreateWithFlags(&hb->ev_out, evf) != hipSuccess ||
+      hipHostMalloc((void**)&hb->h_err, 64, hipHostMallocDefault) != hipSuccess) {
+    vmqg_hbatch_free(hb);
+    return nullptr;
+  }
+  return hb;
+}
+
+void vmqg_hbatch_free(vmqg_hbatch* hb) {
+  if (!hb) return;
+  hipSetDevice(hb->device);
+  if (hb->cs) hipStreamSynchronize(hb->cs);
+  if (hb->state == 1 && hb->ev_k) hipEventSynchronize(hb->ev_k);
+  for (hipEvent_t e : {hb->ev_in, hb->ev_k, hb->ev_out}) if (e) hipEventDestroy(e);
+  for (void* p : {(void*)hb->h_pubs, (void*)hb->h_words, (void*)hb->h_offs, hb->h_out, (void*)hb->h_err})
+    if (p) hipHostFree(p);
+  for (void* p : {hb->d_pubs, hb->d_words, hb->d_offs, hb->d_out}) if (p) hipFree(p);
+  if (hb->cs) hipStreamDestroy(hb->cs);
+  delete hb;
+}
+
+int vmqg_hbatch_inputs(vmqg_hbatch* hb, size_t npub, size_t nwords, vmqg_pub** pubs, uint32_t** words) {
+  if (!hb || !pubs || !words || hb->state == 1) return VMQG_E_INVAL;
+  int rc;
+  if ((rc = grow_pinned((void**)&hb->h_pubs, &hb->h_pubs_cap, (npub + 1) * sizeof(vmqg_pub))) ||
+      (rc = grow_pinned((void**)&hb->h_words, &hb->h_words_cap, (nwords + 1) * sizeof(uint32_t))))
+    return rc;
+  *pubs = hb->h_pubs;
+  *words = hb->h_words;
+  return VMQG_OK;
+}
+
+int vmqg_hbatch_submit(vmqg_ctx* ctx, vmqg_hbatch* hb, size_t npub, size_t nwords, int ranges) {
+  if (!ctx || !hb || hb->state == 1 || npub > 0xFFFFFFF0u) return VMQG_E_INVAL;
+  if (npub && (hb->h_pubs_cap < npub * sizeof(vmqg_pub) || hb->h_words_cap < nwords * sizeof(uint32_t)))
+    return VMQG_E_INVAL;
+  GUARD_BEGIN
+  Engine& e = ctx->e;
+  if (!e.has_device || e.device != hb->device) return VMQG_E_DEVICE;
+  for (size_t i = 0; i < npub; i++)
+    if (hb->h_pubs[i].nwords == 0 || (uint64_t)hb->h_pubs[i].word_off + hb->h_pubs[i].nwords > nwords)
+      return VMQG_E_INVAL;
+  hipSetDevice(e.device);
+  const size_t esz = ranges ? sizeof(vmqg_range) : sizeof(vmqg_emit);
+  if (hb->esz != esz) hb->want_entries = 0;   // a mode change restarts the output sizing
+  hb->esz = esz;
+  hb->want_entries = std::max<uint64_t>(hb->want_entries, (uint64_t)npub * (ranges ? 4 : 8) + 1024);
+  int rc;
+  if ((rc = grow(&hb->d_pubs, &hb->d_pubs_cap, (npub + 1) * sizeof(vmqg_pub))) ||
+      (rc = grow(&hb->d_words, &hb->d_words_cap, (nwords + 1) * sizeof(uint32_t))) ||
+      (rc = grow(&hb->d_offs, &hb->d_offs_cap, (npub + 1) * sizeof(uint64_t))) ||
+      (rc = grow(&hb->d_out, &hb->d_out_cap, hb->want_entries * esz)) ||
+      (rc = grow_pinned((void**)&hb->h_offs, &hb->h_offs_cap, (npub + 1) * sizeof(uint64_t))))
+    return rc;
+  hb->out_entries = hb->d_out_cap / esz;
+  if (hb->frontier) {   // the last match overflowed a tier-2 stack: a larger one (as match_host)
+    e.o_cap_floor = std::max<uint64_t>(e.o_cap_floor, (uint64_t)e.o_cap * 4);
+    hb->frontier = false;
+  }
+  // inputs on the copy stream, so they overlap the kernels already queued
+  if (npub) {
+    if (hipMemcpyAsync(hb->d_pubs, hb->h_pubs, npub * sizeof(vmqg_pub), hipMemcpyHostToDevice, hb->cs) != hipSuccess ||
+        (nwords && hipMemcpyAsync(hb->d_words, hb->h_words, nwords * 4, hipMemcpyHostToDevice, hb->cs) != hipSuccess) ||
+        hipEventRecord(hb->ev_in, hb->cs) != hipSuccess || hipStreamWaitEvent(e.stream, hb->ev_in, 0) != hipSuccess)
+      return VMQG_E_DEVICE;
+  }
+  vmqg::Record* rec = ranges ? nullptr : static_cast<vmqg::Record*>(hb->d_out);
+  vmqg_range* rng = ranges ? static_cast<vmqg_range*>(hb->d_out) : nullptr;
+  rc = e.match_device(static_cast<const vmqg_pub*>(hb->d_pubs), (uint32_t)npub, static_cast<const uint32_t*>(hb->d_words),
+                      rec, rec ? hb->out_entries : 0, rng, rng ? hb->out_entries : 0, static_cast<uint64_t*>(hb->d_offs),
+                      e.stream);
+  if (rc) return rc;
+  // this match's offsets and error bits back, and the bits cleared for the next call
+  uint32_t* d_err = e.d_status + 2 * Engine::kStatusSet;
+  if (hipMemcpyAsync(hb->h_offs, hb->d_offs, (npub + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, e.stream) != hipSuccess ||
+      hipMemcpyAsync(hb->h_err, d_err, 4, hipMemcpyDeviceToHost, e.stream) != hipSuccess ||
+      hipMemsetAsync(d_err, 0, 4, e.stream) != hipSuccess || hipEventRecord(hb->ev_k, e.stream) != hipSuccess)
+    return VMQG_E_DEVICE;
+  hb->npub = npub;
+  hb->epoch = e.epoch;
+  hb->state = 1;
+  return VMQG_OK;
+  GUARD_END
+}
+
+int vmqg_hbatch_offsets(vmqg_hbatch* hb, const uint64_t** offsets, uint64_t* total, uint64_t* epoch) {
+  if (!hb || hb->state == 0) return VMQG_E_INVAL;
+  hipSetDevice(hb->device);
+  if (hb->state == 1) {
+    if (hipEventSynchronize(hb->ev_k) != hipSuccess) { hb->state = 0; return VMQG_E_DEVICE; }
+    hb->state = 2;
+  }
+  hb->total = hb->h_offs[hb->npub];
+  if (offsets) *offsets = hb->h_offs;
+  if (total) *total = hb->total;
+  if (epoch) *epoch = hb->epoch;
+  const uint32_t err = *hb->h_err;
+  if (err & 2u) { hb->frontier = true; hb->state = 0; return VMQG_E_FRONTIER; }
+  if ((err & 4u) || hb->total > hb->out_entries) {
+    hb->want_entries = hb->total + hb->total / 4 + 1024;
+    hb->state = 0;
+    return VMQG_E_OVERFLOW;
+  }
+  if (err & (8u | 16u)) { hb->state = 0; return VMQG_E_DEVICE; }
+  return VMQG_OK;
+}
+
+int vmqg_hbatch_entries(vmqg_hbatch* hb, const void** entries) {
+  if (!hb || hb->state != 2) return VMQG_E_INVAL;
+  hipSetDevice(hb->device);
+  hb->state = 0;
+  int rc;
+  if ((rc = grow_pinned(&hb->h_out, &hb->h_out_cap, hb->total * hb->esz + 16))) return rc;
+  if (hb->total && (hipMemcpyAsync(hb->h_out, hb->d_out, hb->total * hb->esz, hipMemcpyDeviceToHost, hb->cs) != hipSuccess ||
+                    hipEventRecord(hb->ev_out, hb->cs) != hipSuccess || hipEventSynchronize(hb->ev_out) != hipSuccess))
+    return VMQG_E_DEVICE;
+  if (entries) *entries = hb->h_out;
+  return VMQG_OK;
+}
+
 int vmqg_match_device(vmqg_ctx* ctx, const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words,
                       vmqg_emit* d_out, uint64_t out_cap, uint64_t* d_offsets, void* stream) {
   if (!ctx || !d_offsets || (npub && (!d_pubs || !d_words))) return VMQG_E_INVAL;
@@ -245,7 +479,7 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->epoch = e.epoch;
   out->rebuilds = e.rebuilds;
   out->paths = e.paths.size();
-  out->words = e.word_text.size();
+  out->words = e.dict.size();
   out->deferred_tier1 = e.last_deferred[0];
   out->deferred_tier2 = e.last_deferred[1];
   out->ops_applied = e.ops_applied;
@@ -349,6 +583,11 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
   vmqg::Layout L;
   memcpy(&L, layout, sizeof(L));
   if (L.magic != vmqg::kLayoutMagic) return VMQG_E_INVAL;
+  // every match reads the exact-topic filter bits: a layout whose filter is
+  // missing or outside the image would send find_exact out of bounds
+  if (L.exbits_words == 0 || (L.exbits_words & (L.exbits_words - 1)) != 0 || L.exbits_off % 4 != 0 ||
+      L.exbits_off > L.total_bytes || L.exbits_words * 4 > L.total_bytes - L.exbits_off)
+    return VMQG_E_INVAL;
   hipSetDevice(e.device);
   hipStream_t st = vmqg::caller_stream(stream);
   if (e.d_arena_bytes < L.total_bytes) {

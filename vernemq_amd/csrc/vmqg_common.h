@@ -101,7 +101,7 @@ struct Layout {
   uint64_t pad[11];
 };
 static_assert(sizeof(Layout) == 256, "layout must be 256 bytes");
-constexpr uint64_t kLayoutMagic = 0x31676D7176ull;  // "vmqg1"
+constexpr uint64_t kLayoutMagic = 0x32676D7176ull;  // "vmqg2" (exbits_off / exbits_words are read by every match)
 
 // 24-byte patch record: write 16 bytes at arena offset `off` (16-B aligned).
 struct Patch { uint64_t off; uint32_t data[4]; };

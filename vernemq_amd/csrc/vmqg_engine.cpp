@@ -80,14 +80,12 @@ int Engine::init(const vmqg_config& c) {
 
 // ------------------------------------------------------------ dictionary
 uint32_t Engine::intern(const uint8_t* b, size_t n, bool create) {
-  std::string s(reinterpret_cast<const char*>(b), n);
-  auto it = word_index.find(s);
-  if (it != word_index.end()) return it->second;
-  if (!create) return kUnknownWord;
-  uint32_t id = (uint32_t)word_text.size();
-  word_text.push_back(s);
-  word_index.emplace(std::move(s), id);
-  return id;
+  const WordDict::Key k = WordDict::key(b, n);
+  if (!create) {
+    const uint32_t id = dict.find(k);
+    return id == WordDict::kVoid ? kUnknownWord : id;
+  }
+  return dict.intern(k);
 }
 
 // ------------------------------------------------------------- paths/keys
@@ -822,7 +820,7 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
     if (o.mountpoint >= cfg.max_mountpoints || o.node >= cfg.max_nodes) return VMQG_E_LIMIT;
     if (o.nwords == 0 || (uint64_t)o.word_off + o.nwords > nwords) return VMQG_E_INVAL;
     const uint32_t* w = words + o.word_off;
-    for (uint32_t j = 0; j < o.nwords; j++) if (w[j] >= word_text.size()) return VMQG_E_INVAL;
+    for (uint32_t j = 0; j < o.nwords; j++) if (w[j] >= dict.size()) return VMQG_E_INVAL;
     // [<<"$share">>, Group] has no topic: triples([]) has no clause (vmq_topic.erl:71)
     if (o.nwords == 2 && w[0] == kShare) return VMQG_E_INVAL;
     // only wildcard and $share topics enter the trie (add_complex_topic/4 :318-319)
@@ -1195,7 +1193,7 @@ std::string Engine::dump() {
   };
   auto show_words = [&](const std::vector<uint32_t>& w) {
     std::string o = "[";
-    for (size_t i = 0; i < w.size(); i++) { if (i) o += ","; o += esc(word_text[w[i]]); }
+    for (size_t i = 0; i < w.size(); i++) { if (i) o += ","; o += esc(word_text(w[i])); }
     return o + "]";
   };
   auto nid = [&](uint32_t p) {
@@ -1206,11 +1204,11 @@ std::string Engine::dump() {
   for (uint64_t i = 0; i < lay.edge_buckets * kEdgeSlotsPerBucket; i++) {
     const EdgeSlot& e = et[i];
     if (e.parent == kEmpty || e.parent == kTomb) continue;
-    lines.push_back("trie " + nid(e.parent) + " " + esc(word_text[e.word]) + " -> " + show_words(path_words(e.child)));
+    lines.push_back("trie " + nid(e.parent) + " " + esc(word_text(e.word)) + " -> " + show_words(path_words(e.child)));
   }
   auto show_nog = [&](const Nog& n) {
     return n.group == kNone ? "node#" + std::to_string(n.node)
-                            : "{node#" + std::to_string(n.node) + "," + esc(word_text[n.group]) + "}";
+                            : "{node#" + std::to_string(n.node) + "," + esc(word_text(n.group)) + "}";
   };
   for (uint32_t p = 0; p < paths.size(); p++) {
     const PathInfo& P = paths[p];
@@ -1230,14 +1228,14 @@ std::string Engine::dump() {
   auto show_key = [&](const KeyInfo& K) {
     const TopicInfo& t = topics[K.topic_id];
     if (K.group != kNone)
-      return "{mp#" + std::to_string(t.mp) + "," + esc(word_text[K.group]) + "," + show_words(t.words) + "}";
+      return "{mp#" + std::to_string(t.mp) + "," + esc(word_text(K.group)) + "," + show_words(t.words) + "}";
     return "{mp#" + std::to_string(t.mp) + "," + show_words(t.words) + "}";
   };
   auto show_val = [&](const Record& r) {
     const uint32_t kind = r.kind_node >> 24, node = r.kind_node & 0xFFFFFF;
     const std::string sid = "sub#" + std::to_string(r.subscriber), si = "info#" + std::to_string(r.subinfo);
     if (kind == VMQG_EMIT_GROUP)
-      return "{node#" + std::to_string(node) + "," + esc(word_text[r.group]) + "," + sid + "," + si + "}";
+      return "{node#" + std::to_string(node) + "," + esc(word_text(r.group)) + "," + sid + "," + si + "}";
     return "{" + sid + "," + si + "}";
   };
   for (const KeyInfo& K : keys) {

@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <cstring>
 #include <cstdlib>
 #include <memory>
 #include <new>
@@ -110,6 +112,84 @@ class FlatIndex {
   uint64_t n_ = 0;
 };
 
+// Word dictionary: topic words -> dense ids (vmq_topic words; the interning
+// contract of SURVEY §7).  Open addressing over 32-B slots holding the word's
+// 64-bit hash, id, length and first 16 bytes, so looking up a word of at most
+// 16 bytes touches one cache line — the publish hot path (vmqg_prepare_publish*)
+// is one such lookup per word, and the batched form prefetches a block of
+// topics' slots before resolving any.  Lookups never write: readers share the
+// dictionary under the host view's read lock; inserts come from writers.
+class WordDict {
+ public:
+  static constexpr uint32_t kVoid = 0xFFFFFFFFu;
+  // a word as the lookup sees it: hash and its first 16 bytes, zero padded
+  struct Key { uint64_t h, k0, k1; const uint8_t* p; size_t n; };
+  static Key key(const uint8_t* p, size_t n) {
+    Key k{0, 0, 0, p, n};
+    uint8_t buf[16] = {0};
+    memcpy(buf, p, n < 16 ? n : 16);
+    memcpy(&k.k0, buf, 8);
+    memcpy(&k.k1, buf + 8, 8);
+    uint64_t h = mix64(k.k0 ^ (0x9E3779B97F4A7C15ull * (n + 1))) ^ k.k1;
+    for (size_t i = 16; i < n; i += 8) {
+      uint64_t v = 0;
+      memcpy(&v, p + i, n - i < 8 ? n - i : 8);
+      h = mix64(h ^ v) + i;
+    }
+    k.h = mix64(h);
+    return k;
+  }
+  void prefetch(const Key& k) const {
+    if (mask_) __builtin_prefetch(&slots_[k.h & mask_]);
+  }
+  uint32_t find(const Key& k) const {
+    if (!mask_) return kVoid;
+    for (uint64_t i = k.h & mask_;; i = (i + 1) & mask_) {
+      const Slot& s = slots_[i];
+      if (s.id == kVoid) return kVoid;
+      if (s.h == k.h && s.len == k.n && s.k0 == k.k0 && s.k1 == k.k1 &&
+          (k.n <= 16 || memcmp(text_[s.id].data() + 16, k.p + 16, k.n - 16) == 0))
+        return s.id;
+    }
+  }
+  // id of the word, added as the next dense id when absent
+  uint32_t intern(const Key& k) {
+    const uint32_t f = find(k);
+    if (f != kVoid) return f;
+    if ((text_.size() + 1) * 2 > slots_.size()) regrow(std::max<uint64_t>(1024, slots_.size() * 2));
+    const uint32_t id = (uint32_t)text_.size();
+    text_.emplace_back(reinterpret_cast<const char*>(k.p), k.n);
+    put(Slot{k.h, id, (uint32_t)k.n, k.k0, k.k1});
+    count_.store(text_.size(), std::memory_order_release);
+    return id;
+  }
+  const std::string& text(uint32_t id) const { return text_[id]; }
+  size_t size() const { return text_.size(); }
+  // words interned so far, readable without the lock (the batch layer's
+  // staleness check of prepared publishes that held unknown words)
+  uint64_t generation() const { return count_.load(std::memory_order_acquire); }
+
+ private:
+  struct alignas(32) Slot { uint64_t h; uint32_t id, len; uint64_t k0, k1; };
+  void put(const Slot& s) {
+    for (uint64_t i = s.h & mask_;; i = (i + 1) & mask_)
+      if (slots_[i].id == kVoid) { slots_[i] = s; return; }
+  }
+  void regrow(uint64_t want) {
+    uint64_t cap = 1;
+    while (cap < want) cap <<= 1;
+    HugeVec<Slot> old;
+    old.swap(slots_);
+    slots_.assign(cap, Slot{0, kVoid, 0, 0, 0});
+    mask_ = cap - 1;
+    for (const Slot& s : old) if (s.id != kVoid) put(s);
+  }
+  HugeVec<Slot> slots_;
+  uint64_t mask_ = 0;
+  std::vector<std::string> text_;
+  std::atomic<uint64_t> count_{0};
+};
+
 struct PathInfo {
   uint32_t parent, word, mp, depth;
   uint64_t in_slot = ~0ull;         // edge-table slot of the edge (parent, word) -> this path, if present
@@ -167,8 +247,7 @@ struct Engine {
   bool has_device = false;
 
   // ---- dictionary
-  std::unordered_map<std::string, uint32_t> word_index;
-  std::vector<std::string> word_text;
+  WordDict dict;
 
   // ---- logical state
   HugeVec<PathInfo> paths;                              // ids [0, max_mp) are roots
@@ -250,6 +329,7 @@ struct Engine {
 
   // dictionary
   uint32_t intern(const uint8_t* b, size_t n, bool create);
+  const std::string& word_text(uint32_t id) const { return dict.text(id); }
 
   // state machine (vmq_reg_trie.erl:253-539)
   int apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords);

@@ -623,6 +623,8 @@ def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None, part: s
       miss (d >= n_dev): S_p = 17 (13 + 1 + 3),                       R_p = 64
     part: "all" = B_p; "lookup" = 8(L_p+1) + 16 S_p (the walk, COUNT kernel);
     "emit" = 32 R_p (record read + write, EMIT kernel);
+    "lookup_tx" = the transaction-granular form of "lookup" (SURVEY §8(d)):
+    every logical lookup charged a whole 64-B line, 8(L_p+1) + 64 S_p;
     "emit_compulsory" = the bytes EMIT cannot avoid moving through HBM:
     16 R_p written + 40 B per publish read (32-B key cache, its offset) +
     16 B per DISTINCT record of the batch (the 64 shared wildcard records
@@ -642,6 +644,8 @@ def algorithmic_bytes_c(w: Workload, lo: int = 0, hi: int | None = None, part: s
         distinct = int(np.unique(d[d < w.notes["n_dev"]]).size) + w.notes["n_wild"]
         writes = 16 * (n_hit * (w.notes["n_wild"] + 1) + n_miss * w.notes["n_wild"])
         return writes + 40 * (hi - lo) + 16 * distinct
+    if part == "lookup_tx":
+        return n_hit * (8 * 5 + 64 * 26) + n_miss * (8 * 5 + 64 * 17)
     return {"all": look + emit, "lookup": look, "emit": emit}[part]
 
 
