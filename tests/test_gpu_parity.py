@@ -826,3 +826,132 @@ def test_wide_publishes_by_record_count(mode, fast_g):
     for i in range(0, len(idx), 5):
         got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
         assert got == sorted(want[idx[i]]), (i, kinds[idx[i]])
+
+
+def _device_match_records(v, pubs, words, total_hint):
+    """Device-buffer records match (vmqg_match_device, the bench's path):
+    returns the device output tensor (int32 view of the 16-B records) and the
+    offsets on the host; the output is sized from the known answer."""
+    import torch
+    dev = torch.device("cuda", 0)
+    d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
+    d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
+    n = len(pubs)
+    cap = int(total_hint) + 1024
+    d_out = torch.empty(cap * 4, dtype=torch.int32, device=dev)
+    d_offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+    v.match_device(d_pubs.data_ptr(), n, d_words.data_ptr(), d_out.data_ptr(), cap, d_offs.data_ptr(), sp)
+    torch.cuda.synchronize()
+    assert v.match_status(sp) == 0
+    return d_out, d_offs.cpu().numpy()
+
+
+def _sample_records(v, d_out, offs, sample):
+    """The records of the sampled publishes, gathered on the device, decoded."""
+    import torch
+    from vernemq_amd.reg_view import EMIT_DTYPE
+    lo = offs[sample].astype(np.int64)
+    hi = offs[np.asarray(sample) + 1].astype(np.int64)
+    lens = hi - lo
+    pos = np.repeat(lo - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(int(lens.sum()))
+    idx = torch.from_numpy(pos).to(d_out.device)
+    recs = d_out.view(-1, 4).index_select(0, idx).cpu().numpy().view(EMIT_DTYPE).reshape(-1)
+    out, k = [], 0
+    for n in lens:
+        out.append(sorted(H.canon(v.decode(recs[j])) for j in range(k, k + int(n))))
+        k += int(n)
+    return out
+
+
+def test_config_d_full_size_under_churn():
+    """Verdict r3 item 5: config D at FULL size (10M live subscriptions, 8M
+    exact + 1M site/s/+/alarm/# + 1M $share members on 4 nodes; 2^20
+    publishes of which 30 % write hundreds to thousands of records) in the
+    driver's GPU run: every publish's count against the known answer
+    (workloads.config_d_counts), after the bulk load and after each of two
+    10,000-op churn batches; plus a 2,048-publish oracle sample each time.
+    The sample's publishes name 8 sites and 8 job queues, and the oracle
+    holds exactly the subscriptions those can match (a site's exact and
+    alarm filters, every group on a queue: a publish only meets filters with
+    its own literal words), so the sample check is exact at full size.
+    vmq_reg_trie.erl:305-316 (bulk load), :68-72 and :301-303 (Q2 on the
+    $share groups, each member emitted once per hosting node)."""
+    from vernemq_amd import workloads as W
+    from vernemq_amd.reg_view import RegGpuView
+    w = W.config_d()
+    n_live = w.notes["n_live"]
+    v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes,
+                   hints={"edges": 4 * n_live // 5, "paths": 4 * n_live // 5, "keys": n_live,
+                          "records": n_live * 11 // 10, "exact": n_live})   # bench.py's config-D sizing
+    ids = w.load_into(v, n=n_live)
+    ch = W.Churn(w)
+    pubs, words = w.publish_arrays(v)
+    # the sample: publishes on 8 sites / 8 queues; the oracle holds what they can match
+    T = w.tw.reshape(-1, 5)
+    a = w.pw_off[:-1]
+    first, second = w.pw[a], w.pw[a + 1] - 5
+    is_jobs = first == 4
+    sites = np.unique(second[~is_jobs])[::125][:8]
+    queues = np.unique(second[is_jobs])[::125][:8]
+    cand = np.flatnonzero((~is_jobs & np.isin(second, sites)) | (is_jobs & np.isin(second, queues)))
+    sample = cand[np.linspace(0, len(cand) - 1, 2048).astype(np.int64)]
+    relevant = ((T[:, 0] == 0) & np.isin(T[:, 1] - 8, sites)) | ((T[:, 0] == 6) & np.isin(T[:, 3] - 8, queues))
+    orc = O.TrieOracle(w.self_node)
+    orc.apply_raw(feed.init_bytes(w, idx=np.flatnonzero(relevant[:n_live])))
+    for step in range(3):
+        if step:
+            dels, adds = ch.batch(10_000)
+            ops, wds = ch.ops(ids, dels, adds)
+            v.apply_op_arrays(ops, wds)
+            orc.apply(ch.events(dels[relevant[dels]], adds[relevant[adds]]))
+        want_counts = W.config_d_counts(w, ch.live)
+        d_out, offs = _device_match_records(v, pubs, words, want_counts.sum())
+        counts = np.diff(offs.astype(np.int64))
+        assert np.array_equal(counts, want_counts), (step, int(np.count_nonzero(counts != want_counts)))
+        got = _sample_records(v, d_out, offs, sample)
+        want = orc.fold_batch([("", b"pub", w.pub_topic(int(i))) for i in sample])
+        bad = [k for k in range(len(sample)) if got[k] != sorted(want[k])]
+        assert not bad, (step, len(bad), w.pub_topic(int(sample[bad[0]])), got[bad[0]][:4], sorted(want[bad[0]])[:4])
+        assert sum(len(x) for x in got) > len(sample)
+        del d_out
+
+
+def test_config_e_scale_02_oracle_sample():
+    """Verdict r3 item 5: config E at 0.2 scale (10M subscriptions over 1,000
+    Zipf-sized mountpoints, 12 levels, 2^20 Zipf(1.1) hot-topic publishes,
+    library defaults) in the driver's GPU run: a 2,048-publish sample in the
+    mountpoints of <= 1M subscriptions against an oracle holding exactly
+    those mountpoints' subscriptions (a publish only walks its own
+    mountpoint's trie, so the check is exact), plus every publish's count
+    against the range-mode expansion of a second match."""
+    from vernemq_amd import workloads as W
+    from vernemq_amd.reg_view import RegGpuView
+    w = W.config_e(scale=0.2)
+    n = w.n_subs
+    v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes, max_mountpoints=max(1024, len(w.mps) + 1),
+                   hints={"edges": 2 * n, "paths": 2 * n, "keys": n * 5 // 4, "records": n * 5 // 4,
+                          "exact": n * 5 // 4})
+    w.load_into(v)
+    pubs, words = w.publish_arrays(v)
+    # records: counts, then a sample
+    rng, roffs = v.match_ranges(pubs, words)
+    cnt_r = np.zeros(len(pubs), dtype=np.int64)
+    per = np.where(rng["count"] > 0, rng["count"], 1).astype(np.int64)
+    np.add.at(cnt_r, np.repeat(np.arange(len(pubs)), np.diff(roffs.astype(np.int64))), per)
+    d_out, offs = _device_match_records(v, pubs, words, cnt_r.sum())
+    assert np.array_equal(np.diff(offs.astype(np.int64)), cnt_r)
+    per_mp = np.bincount(w.client_mp, minlength=len(w.mps))
+    small = per_mp <= 1_000_000
+    cand = np.flatnonzero(small[w.pub_mp])
+    sample = cand[np.linspace(0, len(cand) - 1, 2048).astype(np.int64)]
+    mps = np.unique(w.pub_mp[sample])
+    subs_idx = np.flatnonzero(np.isin(w.client_mp[w.sub_client], mps))
+    orc = O.TrieOracle(w.self_node)
+    for lo in range(0, len(subs_idx), 1 << 18):
+        orc.apply_raw(feed.init_bytes(w, idx=subs_idx[lo:lo + (1 << 18)]))
+    got = _sample_records(v, d_out, offs, sample)
+    want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(int(i))) for i in sample])
+    bad = [k for k in range(len(sample)) if got[k] != sorted(want[k])]
+    assert not bad, (len(bad), w.pub_topic(int(sample[bad[0]])))
+    assert sum(len(x) for x in got) > len(sample) // 4

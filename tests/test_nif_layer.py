@@ -264,3 +264,176 @@ def test_batchers_while_a_writer_changes_the_answers(tmp_path):
             for i, got in by_state.get(j, []):
                 assert got == want[i], (j, i, pubs[i], got[:4], want[i][:4])
         assert changed > 0   # the writer's groups did change answers
+
+
+def _build_nif_check(tmp_path):
+    """tools-style build of tests/c/nif_mock_check.c: the NIF glue
+    (integration/c_src/vmqg_nif.c) with vmqg_batch.c over the erl_nif test
+    double (tests/c/mock_erl_nif), -Wall -Wextra -Werror."""
+    from vernemq_amd import _lib
+    lib_dir = os.path.dirname(_lib.LIB_PATH)
+    exe = tmp_path / "nif_mock_check"
+    subprocess.run(["gcc", "-std=gnu11", "-O1", "-Wall", "-Wextra", "-Werror", "-pthread",
+                    "-I", os.path.join(ROOT, "tests", "c", "mock_erl_nif"), "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(ROOT, "integration", "c_src"), "-o", str(exe),
+                    os.path.join(ROOT, "tests", "c", "nif_mock_check.c"),
+                    os.path.join(ROOT, "tests", "c", "mock_erl_nif", "erl_nif_mock.c"),
+                    os.path.join(ROOT, "integration", "c_src", "vmqg_nif.c"),
+                    os.path.join(ROOT, "integration", "c_src", "vmqg_batch.c"),
+                    "-L", lib_dir, "-l:libvmqgpu.so", "-Wl,-rpath," + lib_dir], check=True)
+    return exe
+
+
+def _nif_glue_script(device, seed=5, n_subs=1500, n_pubs=1200):
+    """An initial load through add_init/6 (mountpoints "" and "mp1", $share
+    groups on several nodes, v4 QoS), subscriber events through apply_many/2
+    (coalesced groups, deletes before adds within an event) and apply/3, a
+    group refused as a whole (an invalid topic: nothing applied), and
+    publishes; plus the same history as oracle events."""
+    import random
+    r = random.Random(seed)
+    words = ["a", "b", "c", "d"]
+    node_names = ["n0@h", "n1@h", "n2@h", "n70@h"]
+    node_ids = [0, 1, 2, 70]
+
+    def rand_filter():
+        pre = ["$share", r.choice(["g1", "g2"])] if r.random() < 0.2 else []
+        L = r.randint(1, 4)
+        t = ["+" if r.random() < 0.25 else ("#" if (i == L - 1 and r.random() < 0.2) else r.choice(words))
+             for i in range(L)]
+        return "/".join(pre + t)
+
+    lines = ["N %d" % device]
+    events = []
+    live = {}
+    for k in range(n_subs):
+        mp = "mp1" if r.random() < 0.2 else "-"
+        ni = r.choice(range(4)) if r.random() < 0.3 else 0
+        f, q = rand_filter(), r.randint(0, 2)
+        live[k] = (mp, ni, q, f)
+        lines.append("I %d %s c%d %d %s" % (node_ids[ni], mp, k, q, f))
+        events.append(("updated", ("" if mp == "-" else mp, b"c%d" % k), None,
+                       [(node_names[ni], True, [(tuple(x.encode() for x in f.split("/")), q)])]))
+    lines += ["F", "T"]
+
+    def ev_lines(k, changes):   # one subscriber event: its changes, deletes first
+        mp = live.get(k, ("-",))[0]
+        out = ["V %s c%d" % (mp, k)]
+        for kind, ni, q, f in changes:
+            out.append("C %s %d %d %s" % (kind, node_ids[ni], q, f))
+        return out
+
+    oracle_groups = []
+    for g in range(6):
+        evs = []
+        for _ in range(r.randint(3, 40)):
+            k = r.choice(sorted(live))
+            mp, ni, q, f = live[k]
+            f2, q2 = rand_filter(), r.randint(0, 2)
+            # a resubscription with another filter: {updated, Old, New} -> del old, add new
+            lines.extend(ev_lines(k, [("del", ni, q, f), ("add", ni, q2, f2)]))
+            old = [(node_names[ni], True, [(tuple(x.encode() for x in f.split("/")), q)])]
+            new = [(node_names[ni], True, [(tuple(x.encode() for x in f2.split("/")), q2)])]
+            evs.append(("updated", ("" if mp == "-" else mp, b"c%d" % k), old, new))
+            live[k] = (mp, ni, q2, f2)
+        lines.append("A" if g % 2 == 0 else "S")
+        lines.append("T")
+        oracle_groups.append(evs)
+    # a group with one malformed change: refused whole, the table unchanged
+    k = sorted(live)[0]
+    lines.extend(ev_lines(k, [("add", 0, 1, "a/zz/q")]))
+    lines.extend(["V - bad", "C add 0 1 !", "A", "T"])
+    for _ in range(n_pubs):
+        L = r.randint(1, 5)
+        t = "/".join(r.choice(words) for _ in range(L))
+        if r.random() < 0.05:
+            t = "$SYS/" + t
+        lines.append("P %s %s" % ("mp1" if r.random() < 0.25 else "-", t))
+    lines.append("P - a/+/b")   # a publish the reference rejects (validate_topic): {error, invalid_topic}
+    lines += ["M records", "M ranges", "T"]
+    return "\n".join(lines) + "\n", node_names, node_ids, events, oracle_groups
+
+
+def _run_nif_check(tmp_path, device):
+    exe = _build_nif_check(tmp_path)
+    script, node_names, node_ids, events, groups = _nif_glue_script(device)
+    (tmp_path / "n.txt").write_text(script)
+    r = subprocess.run([str(exe), str(tmp_path / "n.txt"), str(tmp_path / "o.txt")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    return script, (tmp_path / "o.txt").read_text().splitlines(), node_names, node_ids, events, groups
+
+
+def test_nif_glue_runs_over_the_erl_nif_double(tmp_path):
+    """The NIF glue compiled (-Werror) and run through its ErlNifFunc table
+    on a host-engine context: add_init/flush_init, apply_many/2 and apply/3
+    return ok and grow the table like the events; a group holding one
+    malformed change is refused whole (nothing applied: stats/1 unchanged);
+    match/4 fails loudly per publish without a device (no CPU fallback)."""
+    from oracle import oracle as O
+    script, out, node_names, node_ids, events, groups = _run_nif_check(tmp_path, -1)
+    res = [l for l in out if l[0] in "FAST"]
+    assert res[0] == "F ok" and res[1].startswith("T ")
+    applies = [l for l in res if l[0] in "AS"]
+    assert all(x == "ok" for l in applies[:-1] for x in l.split()[1:]), applies
+    assert applies[-1] == "A {error,invalid_topic}"
+    ts = [int(l.split()[1]) for l in res if l[0] == "T"]
+    # stats/1 = {NrOfSubs + NrOfRemoteSubs, _} (vmq_reg_trie.erl:101-112), after every step
+    orc = O.TrieOracle(node_names[0])
+    orc.apply(events)
+    want = [orc.sizes()["stats_subs"]]
+    for g in groups:
+        orc.apply(g)
+        want.append(orc.sizes()["stats_subs"])
+    assert ts[:len(want)] == want, (ts, want)
+    assert ts[-2] == ts[-3] == want[-1]   # the refused group changed nothing
+    m = [l for l in out if l[0].isdigit()]
+    assert m and all(" error device" in l or " error invalid_topic" in l for l in m), m[:3]
+    assert m[-1].endswith("error invalid_topic")
+
+
+@pytest.mark.gpu
+def test_nif_glue_matches_the_oracle_on_the_gpu(tmp_path):
+    """The same NIF calls on the GPU: after the initial load and the
+    coalesced / single event applies, match/4 (records and ranges) returns,
+    per publish, the FoldFun entries the oracle's fold/4 gives — built as
+    Erlang terms by the glue ({SubscriberId, SubInfo}, {Node, Group,
+    SubscriberId, SubInfo}, Node) and read back from the terms."""
+    from oracle import oracle as O
+    script, out, node_names, node_ids, events, groups = _run_nif_check(tmp_path, 0)
+    name = {"n%d@h" % nid: node_names[i] for i, nid in enumerate(node_ids)}
+    orc = O.TrieOracle(node_names[0])
+    orc.apply(events)
+    for g in groups:
+        orc.apply(g)
+    pubs = []
+    for l in script.splitlines():
+        if l.startswith("P "):
+            _, mp, t = l.split(" ", 2)
+            pubs.append(("" if mp == "-" else mp, tuple(x.encode() for x in t.split("/"))))
+    want = [sorted(x) for x in orc.fold_batch([(mp, b"pub", t) for mp, t in pubs[:-1]])]
+    blocks, cur = [], None
+    for l in out:
+        if l.startswith("M "):
+            cur = []
+            blocks.append(cur)
+        elif cur is not None and l[0].isdigit():
+            cur.append(l)
+    assert len(blocks) == 2
+    for blk in blocks:
+        assert len(blk) == len(pubs) and blk[-1].endswith("error invalid_topic")
+        for i, l in enumerate(blk[:-1]):
+            f = l.split(" ")
+            assert f[1] == "ok", l
+            ents = []
+            for e in f[2:]:
+                p = e.split(",")
+                if p[0] == "A":
+                    ents.append(("A", ("" if p[1] == "-" else p[1], p[2].encode()), O.subinfo_repr(int(p[3]))))
+                elif p[0] == "B":
+                    ents.append(("B", name[p[1]], p[2].encode(), ("" if p[3] == "-" else p[3], p[4].encode()),
+                                 O.subinfo_repr(int(p[5]))))
+                else:
+                    ents.append(("C", name[p[1]]))
+            assert sorted(ents) == want[i], (i, pubs[i], sorted(ents)[:4], want[i][:4])
+    assert sum(len(x) for x in want) > len(want)
