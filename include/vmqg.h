@@ -151,6 +151,11 @@ typedef struct vmqg_stats_s {
   uint64_t wave_entries;    /* entries (records or ranges) written by the EMIT  */
                             /* wave-tier launch (the whole-wave walks)          */
   uint64_t wide_entries;    /* entries written by the wide phase                */
+  /* ABI 4: batch-wide dedupe of the last checked match batch                   */
+  uint64_t dedup;           /* publishes whose (MP, topic) another publish of   */
+                            /* the batch walked: listed as its duplicates       */
+  uint64_t dedup_walked;    /* of those, walked after all (representative       */
+                            /* deferred, or a fingerprint collision)            */
 } vmqg_stats_t;
 
 /* ---- lifecycle ------------------------------------------------------- */
@@ -342,7 +347,11 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *                          publish in COUNT, two in EMIT over the same 64-publish chunks)
  *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
  *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8;
- *                          defaults 4 and 16) */
+ *                          defaults 4 and 16)
+ *   "dedupe"    0 | 1 | 2  batch-wide dedupe of repeated (MP, topic) publishes in
+ *                          COUNT: off, on, or auto (default: on while more than
+ *                          one publish in five repeats another, judged on the
+ *                          previous call — sampled on 1 chunk in 16 while off) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the match kernels over the last

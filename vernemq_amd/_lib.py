@@ -80,7 +80,8 @@ class Stats(ctypes.Structure):
                 ("subs", "device_bytes", "trie_edges", "trie_nodes", "trie_topics", "subs_objects",
                  "fanout_objects", "remote_keys", "epoch", "rebuilds", "paths", "words",
                  "deferred_tier1", "deferred_tier2", "ops_applied", "apply_host_ns", "apply_upload_ns", "apply_wait_ns", "patch_bytes",
-                 "image_bytes", "max_depth", "many_key", "retried", "wave_entries", "wide_entries")]
+                 "image_bytes", "max_depth", "many_key", "retried", "wave_entries", "wide_entries",
+                 "dedup", "dedup_walked")]
 
 
 class RConfig(ctypes.Structure):

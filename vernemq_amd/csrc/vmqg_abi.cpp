@@ -493,6 +493,8 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->retried = e.last_retried;
   out->wave_entries = e.last_wave_entries;
   out->wide_entries = e.last_wide_entries;
+  out->dedup = e.last_dedup;
+  out->dedup_walked = e.last_dedup_walked;
   return VMQG_OK;
 }
 
@@ -516,6 +518,9 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
     e.opt_fast_g = (uint32_t)value;
   } else if (n == "nt_stores") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptNtStores) : (e.opt_flags & ~vmqg::kOptNtStores);
+  } else if (n == "dedupe") {
+    if (value < 0 || value > 2) return VMQG_E_INVAL;
+    e.opt_dedupe = (uint32_t)value;
   } else if (n == "count_bpc" || n == "emit_bpc") {
     if (value < 0 || value > 32) return VMQG_E_INVAL;
     (n == "count_bpc" ? e.opt_count_bpc : e.opt_emit_bpc) = (uint32_t)value;

@@ -32,7 +32,7 @@ Engine::~Engine() {
       hipFree(sg.d);
     }
     hipFree(d_arena); hipFree(d_status); hipFree(d_deferred);
-    hipFree(d_keycache);
+    hipFree(d_keycache); hipFree(d_dd);
     hipFree(d_lookback); hipFree(d_ostack);
     hipFree(d_pubs); hipFree(d_words); hipFree(d_offs); hipFree(d_out);
     if (stream) hipStreamDestroy(stream);
@@ -950,13 +950,30 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     keycache_cap = deferred_cap = 0;
     const uint64_t cap = next_pow2(std::max<uint64_t>(npub, 1024));
     // 32-B key cache + kSpillKeys x 8-B spilled keys per publish, then the
-    // chunk totals (one per 16 or 32 publishes, + 1)
-    // (+ per chunk a 64-bit wide-publish mask and three label planes)
-    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + 5 * (cap / 16 + 2) * 8) != hipSuccess) return VMQG_E_NOMEM;
-    // publish lists: retry, whole-wave walks, eight wide lists (vmqg_kernels.hip kLists)
-    if (hipMalloc(&d_deferred, 10 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
+    // chunk totals (one per 16, 32 or 64 publishes, + 1), per chunk a 64-bit
+    // wide-publish mask, then one fast-pass bit per publish
+    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + 2 * (cap / 16 + 2) * 8 + (cap / 32 + 2) * 4) != hipSuccess)
+      return VMQG_E_NOMEM;
+    // publish lists: retry, whole-wave walks, duplicates, their slots, huge (vmqg_kernels.hip kLists)
+    if (hipMalloc(&d_deferred, 5 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
     keycache_cap = cap;
     deferred_cap = cap;
+  }
+  // the dedupe table: 2 slots per publish, older calls' slots free by their tag
+  const uint64_t slots = next_pow2(std::max<uint64_t>(2 * npub, 4096));
+  if (slots > dd_slots) {
+    if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
+    hipFree(d_dd);
+    d_dd = nullptr;
+    dd_slots = 0;
+    if (hipMalloc(&d_dd, slots * 12) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMemsetAsync(d_dd, 0, slots * 12, st) != hipSuccess) return VMQG_E_DEVICE;
+    dd_slots = slots;
+    dd_tag = 0;
+  }
+  if (++dd_tag >= (1u << 24)) {   // tags are 24 bits: clear before reuse
+    if (hipMemsetAsync(d_dd, 0, dd_slots * 12, st) != hipSuccess) return VMQG_E_DEVICE;
+    dd_tag = 1;
   }
   return VMQG_OK;
 }
@@ -1026,7 +1043,13 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.keyspill = reinterpret_cast<uint2*>(static_cast<char*>(d_keycache) + keycache_cap * 32);
   a.chunk = reinterpret_cast<uint64_t*>(static_cast<char*>(d_keycache) + keycache_cap * (32 + 8 * 8));
   a.widemask = a.chunk + (keycache_cap / 16 + 2);
-  a.wideplane = a.widemask + (keycache_cap / 16 + 2);
+  a.fastdone = reinterpret_cast<uint32_t*>(a.widemask + (keycache_cap / 16 + 2));
+  a.dd_key = static_cast<uint64_t*>(d_dd);
+  a.dd_rep = reinterpret_cast<uint32_t*>(static_cast<char*>(d_dd) + dd_slots * 8);
+  a.dd_mask = dd_slots - 1;
+  a.dd_tag = dd_tag;
+  a.dd_force = opt_dedupe;
+  a.dd_mode = d_status + kStatusDdMode;
   a.gpw = 64 / (opt_fast_g == 4 ? 4 : opt_fast_g == 1 ? 1 : 2);   // publishes per chunk
   a.status = d_status + kStatusSet * (call_seq & 1);
   a.status_next = d_status + kStatusSet * ((call_seq + 1) & 1);
@@ -1148,6 +1171,8 @@ int Engine::match_status(hipStream_t st) {
   last_many = c[4];
   last_wave_entries = (uint64_t)c[6] | ((uint64_t)c[7] << 32);
   last_wide_entries = (uint64_t)c[24] | ((uint64_t)c[25] << 32);
+  last_dedup = c[8];
+  last_dedup_walked = c[10];
   const uint32_t err = h[2 * kStatusSet];
   if (err && debug_limit() > 0) fprintf(stderr, "vmqg debug: match status error bits 0x%x\n", err);
   if (err & 2u) return VMQG_E_FRONTIER;

@@ -290,6 +290,8 @@ struct Engine {
   uint32_t* d_deferred = nullptr; uint64_t deferred_cap = 0;   // publishes
   uint64_t call_seq = 0; uint32_t last_set = 0;                // status set of the next / last match call
   void* d_keycache = nullptr; uint64_t keycache_cap = 0;   // publishes
+  void* d_dd = nullptr; uint64_t dd_slots = 0; uint32_t dd_tag = 0;   // batch-wide dedupe table
+  uint32_t opt_dedupe = 2;                                 // vmqg_set_option "dedupe": 0 off, 1 on, 2 auto
   // host-buffer match staging
   void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
   void* d_words = nullptr; uint64_t d_words_cap = 0;
@@ -311,12 +313,14 @@ struct Engine {
   uint32_t last_many = 0, last_retried = 0;    // ... many-key publishes / retried four lanes per publish
   uint64_t last_wave_entries = 0;              // ... entries (records or ranges) the EMIT wave tier wrote
   uint64_t last_wide_entries = 0;              // ... entries the fast EMIT's wide phase wrote
+  uint64_t last_dedup = 0, last_dedup_walked = 0;  // ... duplicates served from a representative / walked anyway
   // epoch of the last apply that rewrote a record slot (or re-laid out the
   // arena): range results of an older epoch index records that may have
   // changed (vmqg_records_at refuses them)
   uint64_t rec_epoch = 0;
   // device status: two per-call counter sets of kStatusSet words, then the sticky error word
   static constexpr uint32_t kStatusSet = 32, kStatusBytes = 512;
+  static constexpr uint32_t kStatusDdMode = 100;   // persistent word: the dedupe mode the last call chose
   // per-launch timing: COUNT fast tier, COUNT wave tier, scan, EMIT fast tier, EMIT wave tier
   static constexpr int kTimedStages = 5;
   std::vector<std::array<hipEvent_t, 2 * kTimedStages>> t_ev;

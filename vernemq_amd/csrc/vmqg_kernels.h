@@ -30,7 +30,7 @@ struct MatchArgs {
                                                   // [3] publishes EMIT hands to the wave tier (none today)
   uint32_t* status_next;                          // the next call's counters (zeroed by this call)
   uint32_t* err;                                  // error bits, sticky until vmqg_match_status
-  uint32_t* deferred;                             // 2 x npub: publishes deferred by COUNT, then by EMIT
+  uint32_t* deferred;                             // kLists x npub: retry, whole-wave walks, duplicates + slots
   uint32_t fast_g, opts;                          // tuning: lanes per publish (2|4), kOpt* bits
   uint32_t count_bpc, emit_bpc;                   // tuning: fast-tier grid cap in blocks per CU (0 = 8)
   uint32_t cus, pad2;                             // compute units of the device
@@ -41,7 +41,13 @@ struct MatchArgs {
   uint32_t* dbg;                                  // VMQG_DEBUG_SYNC only: per-wave progress words in host memory
   uint32_t* o_slots;                              // o_waves bits: stacks borrowed by the EMIT tail's walks
   uint64_t* widemask;                             // per chunk of gpw publishes: its wide publishes (COUNT -> EMIT tail)
-  uint64_t* wideplane;                            // per chunk: three bit planes of the wide publishes' XCD labels
+  // batch-wide dedupe (COUNT -> the COUNT wave tier's fixup)
+  uint64_t* dd_key;                               // dd_mask + 1 slots: {call tag: 24, fingerprint bits: 40}
+  uint32_t* dd_rep;                               // ... the publish that claimed the slot
+  uint64_t dd_mask;
+  uint32_t dd_tag, dd_force;                      // this call's tag (never 0); 0 off, 1 on, 2 auto (dd_mode)
+  uint32_t* dd_mode;                              // persistent: the mode the last call's fixup chose
+  uint32_t* fastdone;                             // bit per publish: served by COUNT's fast pass
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records

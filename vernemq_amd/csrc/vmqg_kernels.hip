@@ -20,10 +20,11 @@
 //
 // Keys per publish: <= 2 go to a 32-B key cache, 3..8 to spill slots; a
 // WIDE publish (more keys than that — a $share group hosted on many nodes,
-// Q2 — or >= 256 records) keeps only its totals and its candidate paths, and
-// EMIT expands it again with the whole wave (emit_many): by the wave that
-// meets it in its chunk (records mode), or in a second phase of the launch
-// from per-XCD lists shared out statically (range mode).
+// Q2) keeps only its totals and its candidate paths, marked in its chunk's
+// 64-bit mask; the EMIT tail launch expands it again with the whole wave
+// (emit_many).  A publish whose (MP, topic) another publish of the batch
+// already walks is not walked again (batch-wide dedupe, k_match_fast and
+// dedupe_fixup): it takes the representative's key cache and count.
 //
 // Deferral tiers — a publish whose lists overflow the fast tier's, or that
 // meets a remote node >= 64, is retried four lanes per publish (lists 4x
@@ -72,10 +73,18 @@ constexpr uint32_t kMany = 0xFFFFFFFDu;     // key cache: more keys than the lis
 // vmqg_match_status).
 // Publish lists (a.deferred, kLists x npub entries): [0, npub) publishes the
 // fast pass could not hold (retried four lanes per publish by the COUNT
-// wave-tier launch), [npub, 2 npub) publishes walked by a whole wave, then
-// eight lists of wide publishes (many keys, or >= kWideRecords records),
-// one per XCD label, written wave-wide by the second phase of the fast EMIT.
-constexpr uint32_t kXcds = 8, kLists = 2 + kXcds;
+// wave-tier launch), [npub, 2 npub) publishes walked by a whole wave,
+// [2 npub, 3 npub) duplicates of a batch-wide dedupe representative,
+// [3 npub, 4 npub) their dedupe-table slots and [4 npub, 5 npub) the huge
+// publishes (records mode, >= kHugeRecords records: copied by every wave of
+// the EMIT tail, a segment each).
+constexpr uint32_t kLists = 5;
+#ifndef VMQG_HUGE_RECORDS
+#define VMQG_HUGE_RECORDS 65536
+#endif
+constexpr uint32_t kHugeRecords = VMQG_HUGE_RECORDS;
+constexpr uint32_t kHugeFlag = 0x40000000u;  // key cache word 1 (nk <= 8): a huge publish, the tail copies it
+constexpr uint32_t kHugeSeg = 64 * 8 * 4;     // records per tail wave and segment
 // progress words of the calling wave (VMQG_DEBUG_SYNC diagnosis; a.dbg null otherwise)
 #define DBGW(slot, v)                                                                                        \
   do {                                                                                                       \
@@ -86,6 +95,9 @@ constexpr uint32_t kXcds = 8, kLists = 2 + kXcds;
 enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, kStMany = 4, kStWalkOvf = 5,
                   kStWaveEnt = 6 /* u64: entries written by the EMIT wave tier (whole-wave walks) */,
                   kStWideEnt = 24 /* u64: entries written for wide publishes by the EMIT tail */,
+                  kStDup = 8 /* duplicates listed for the fixup */, kStDupTried = 9 /* publishes probed */,
+                  kStDupWalked = 10 /* duplicates walked after all (representative deferred / words differ) */,
+                  kStHuge = 11 /* huge publishes listed for the tail */,
                   kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
 #define VMQG_WIDE_RECORDS 0x7fffffff   // A/B: a publish with at least this many records is wide too (256: config D 2,724 vs 2,526 us per batch, off)
@@ -565,19 +577,59 @@ __device__ __forceinline__ void store_range(vmqg_range* out, uint64_t i, uint32_
 // 0) says how it was served: 0 fast tier, 1 many-key mode, 2 deferred by a
 // walk overflow, 3 deferred otherwise (remote nodes >= 64).  Deferred
 // publishes go to list RETRY ? 2 (whole-wave walks) : 0 (the 4-lane retry).
+// Batch-wide dedupe: the slot of (MP, topic) in the call's dedupe table
+// (open addressing over 64-bit keys {call tag: 24, fingerprint bits: 40},
+// slots of older calls count as free), claimed by CAS.  Returns true when
+// another publish of this call holds the slot (p is its duplicate: the
+// fixup checks the words and takes the representative's results), false
+// when p claimed it (p represents the topic) or found no room.  One lane.
+__device__ bool dedupe_probe(const MatchArgs& a, uint64_t fp, uint32_t p, uint32_t& slot) {
+  const unsigned long long key = ((unsigned long long)a.dd_tag << 40) | (fp >> 24);
+  uint64_t i = fp & a.dd_mask;
+  for (uint32_t probe = 0; probe < 32; probe++, i = (i + 1) & a.dd_mask) {
+    unsigned long long* k = reinterpret_cast<unsigned long long*>(a.dd_key + i);
+    unsigned long long cur = __hip_atomic_load(k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if (cur == key) { slot = (uint32_t)i; return true; }
+      if ((cur >> 40) == a.dd_tag) break;   // another topic of this call: the next slot
+      const unsigned long long prev = atomicCAS(k, cur, key);
+      if (prev == cur) { a.dd_rep[i] = p; slot = (uint32_t)i; return false; }
+      cur = prev;
+    }
+  }
+  slot = kNone;
+  return false;
+}
+
 template <int G, int OUT, bool RETRY = false, uint32_t SL = kWaves * (64 / G)>
 __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G, SL>& s, const Group<G>& g,
-                                  uint32_t& fl, uint32_t& xl) {
+                                  uint32_t& fl, bool dedupe = false, uint32_t* dslot = nullptr) {
   const vmqg_pub pub = a.pubs[p];
+  if (dedupe) {
+    // the same (MP, topic) walked by another publish of the batch: a
+    // duplicate (fl 4), listed for the fixup, which gives it the
+    // representative's key cache and count (the answer of one topic at one
+    // epoch is one answer)
+    const uint32_t* w = a.words + pub.word_off;
+    const uint32_t wreg = g.lane < pub.nwords ? w[g.lane] : kUnknownWord;
+    const uint64_t fp = publish_fp<G>(pub, w, wreg, g);
+    uint32_t slot = kNone, dup = 0;
+    if (g.lane == 0 && pub.nwords > 0) dup = dedupe_probe(a, fp, p, slot);
+    if (g.bcast(dup, 0)) {   // the caller lists it (one atomic per wave)
+      fl = 4;
+      *dslot = slot;
+      if (g.lane == 0) {
+        a.offsets[p] = 0;
+        reinterpret_cast<uint4*>(a.keycache)[(uint64_t)p * 2] = make_uint4(0, kDeferred, 0, 0);
+      }
+      return 0;
+    }
+  }
   const Matched m = walk_publish<G, SL>(a, pub, s, g);
   fl = 0;
-  // wide publishes — more keys than the spill slots hold, or many records —
-  // are written by a whole wave in EMIT's second phase, expanded again from
-  // their candidates; their XCD label (a hash of the first candidate, else
-  // of the exact key) sends publishes of one key to one XCD, whose L2 then
-  // keeps the key's records for all of them
+  // wide publishes — more keys than the spill slots hold — are written by a
+  // whole wave in the EMIT tail launch, expanded again from their candidates
   const bool many = !m.overflow && (m.many || m.nk > VMQG_SPILL_KEYS || m.ksum >= VMQG_WIDE_RECORDS);
-  xl = ((m.nc ? s.cd(0) : m.ex_off) * 0x9E3779B1u) >> 29;
   // 3..8 keys: the group copies its key list to the publish's spill slots
   const bool spill = !m.overflow && !many && m.nk > 2;
   if (spill)
@@ -605,15 +657,22 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
     kc[0] = make_uint4(total, kMany, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
     kc[1] = make_uint4(m.nc, m.ksum, m.ex_off, m.ex_cnt);
     fl = 1;
-  } else if (m.nk <= 2) {
-    const uint2 k0 = m.nk > 0 ? s.ky(0) : make_uint2(0, 0);
-    const uint2 k1 = m.nk > 1 ? s.ky(1) : make_uint2(0, m.ksum);
-    const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
-    kc[0] = make_uint4(total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
-    kc[1] = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
   } else {
-    kc[0] = make_uint4(total, m.nk, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
-    kc[1] = make_uint4(0, m.ksum, 0, 0);
+    // a huge records-mode publish (R2's one topic of 4M subscribers): every
+    // wave of the EMIT tail copies a segment of it (one wave would take ms)
+    const bool huge = OUT == 0 && total >= kHugeRecords;
+    const uint32_t hf = huge ? kHugeFlag : 0u;
+    if (huge) a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
+    if (m.nk <= 2) {
+      const uint2 k0 = m.nk > 0 ? s.ky(0) : make_uint2(0, 0);
+      const uint2 k1 = m.nk > 1 ? s.ky(1) : make_uint2(0, m.ksum);
+      const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
+      kc[0] = make_uint4(total, m.nk | hf, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
+      kc[1] = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
+    } else {
+      kc[0] = make_uint4(total, m.nk | hf, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
+      kc[1] = make_uint4(0, m.ksum, 0, 0);
+    }
   }
   return total;
 }
@@ -621,11 +680,8 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
 // Marks the wide publishes among a wave's groups (fl == 1 on a group's lane
 // 0) in their chunk's 64-bit mask (bit = publish % gpw), which the EMIT tail
 // launch walks: the fast pass stores its chunk's whole mask (no atomics),
-// the retry ORs single bits into masks the fast pass already stored.
-// Each wide publish also gets a 3-bit XCD label (xl: a hash of its first
-// candidate, else of its exact key), kept as three bit planes next to the
-// mask: the tail gives a chunk's label-x publishes to a wave of XCD x, so
-// publishes of one key meet that key's records in one L2.
+// the retry and the dedupe fixup OR single bits into masks the fast pass
+// already stored.
 template <int G>
 __device__ __forceinline__ uint64_t group_bits_to_publish_bits(uint64_t m) {
   uint64_t wm = 0;
@@ -634,26 +690,14 @@ __device__ __forceinline__ uint64_t group_bits_to_publish_bits(uint64_t m) {
 }
 
 template <int G, bool RETRY>
-__device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t xl, uint32_t p) {
+__device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t p) {
   const bool w = g.lane == 0 && fl == 1;
   const uint64_t m_all = __ballot(w);
   const uint32_t c = p / a.gpw;
   if (RETRY) {
-    if (w) {
-      const unsigned long long bit = 1ull << (p % a.gpw);
-      atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + c), bit);
-      for (uint32_t k = 0; k < 3; k++)
-        if ((xl >> k) & 1) atomicOr(reinterpret_cast<unsigned long long*>(a.wideplane + 3ull * c + k), bit);
-    }
-  } else {   // p: the wave's first publish; the chunk's mask and planes stored whole
-    const uint64_t wm = group_bits_to_publish_bits<G>(m_all);
-    const uint64_t p0 = group_bits_to_publish_bits<G>(__ballot(w && (xl & 1)));
-    const uint64_t p1 = group_bits_to_publish_bits<G>(__ballot(w && (xl & 2)));
-    const uint64_t p2 = group_bits_to_publish_bits<G>(__ballot(w && (xl & 4)));
-    if (__lane_id() == 0) {
-      a.widemask[c] = wm;
-      a.wideplane[3ull * c] = p0; a.wideplane[3ull * c + 1] = p1; a.wideplane[3ull * c + 2] = p2;
-    }
+    if (w) atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + c), 1ull << (p % a.gpw));
+  } else if (__lane_id() == 0) {   // p: the wave's first publish; the chunk's mask stored whole
+    a.widemask[c] = group_bits_to_publish_bits<G>(m_all);
   }
   if (m_all && __lane_id() == 0) atomicAdd(&a.status[kStMany], (uint32_t)__popcll(m_all));
 }
@@ -682,6 +726,7 @@ __device__ int resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, 
   uint32_t total;
   if (h.y == kDeferred) return kResSkip;   // written by the wave tier
   const bool many = h.y == kMany;
+  if (!many && (h.y & kHugeFlag)) return kResSkip;   // written by the EMIT tail, segment by segment
   if (many) {
     total = h.x;
   } else {
@@ -943,10 +988,6 @@ constexpr int kWideLanes = VMQG_WIDE_LANES;
 #ifndef VMQG_TAIL_U
 #define VMQG_TAIL_U 8   // records in flight per lane in the tail's wide copies
 #endif
-#ifndef VMQG_WIDE_XCD
-#define VMQG_WIDE_XCD 0   // A/B: 1 = label-x publishes by XCD-x waves (config D: 17.0 ms vs 2.6 ms, off)
-#endif
-
 struct WaveLds {
   uint2 stack[kWStack];   // tier 1's frontier stack
   uint32_t cand[kWCand];  // candidate paths awaiting resolution
@@ -1236,27 +1277,25 @@ __device__ __forceinline__ void wave_publish(const MatchArgs& a, WaveLds& W, uin
   else wave_publish_body<MODE, OUT, NT>(a, W, gstack, p, ob, oe);
 }
 
-// COUNT's deferred publishes [i0, i0 + 16) of list 0 (those < nd), one wave:
+// A deferred publish per group of four lanes (sixteen per wave, `valid`):
 // retried four lanes per publish (a publish served there gets its key cache
 // as in the fast pass and its count added to its chunk's total); what
 // overflows even those lists (or all, at fast_g 4, whose fast pass already
 // had them) is walked by the whole wave and listed for EMIT (list 1).
 template <int OUT, bool NT, uint32_t SL>
-__device__ void count_deferred_wave(const MatchArgs& a, const FastScratch<4, SL>& s, const Group<4>& g, WaveLds& W,
-                                    uint2* gstack, uint32_t i0, uint32_t nd) {
+__device__ void count_deferred_group(const MatchArgs& a, const FastScratch<4, SL>& s, const Group<4>& g, WaveLds& W,
+                                     uint2* gstack, bool valid, uint32_t p) {
   const uint32_t lane = __lane_id();
   const bool retry = a.fast_g != 4;
-  const uint32_t i = i0 + g.gidx;
-  const bool valid = i < nd;
-  const uint32_t p = valid ? a.deferred[i] : 0u;
-  uint32_t fl = 2, c = 0, xl = 0;
+  if (!valid) p = 0;
+  uint32_t fl = 2, c = 0;
   if (retry && valid) {
-    c = count_publish<4, OUT, true, SL>(a, p, s, g, fl, xl);
+    c = count_publish<4, OUT, true, SL>(a, p, s, g, fl);
     if (g.lane == 0 && fl <= 1)
       atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)c);
   }
   wave_sync();
-  if (retry) mark_wide<4, true>(a, g, fl, xl, p);
+  if (retry) mark_wide<4, true>(a, g, fl, p);
   // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
   uint64_t ov = __ballot(valid && g.lane == 0 && fl >= 2);
   if (!retry && ov) {   // list 1 for EMIT (the retry's count_publish listed its own)
@@ -1270,6 +1309,63 @@ __device__ void count_deferred_wave(const MatchArgs& a, const FastScratch<4, SL>
     ov &= ov - 1;
     wave_publish<0, OUT, NT>(a, W, gstack, __shfl(p, l, 64), 0, 0);
   }
+}
+
+// The duplicates COUNT listed (list 2, their table slots in list 3),
+// [base, base + 64) of them, one per lane: a duplicate whose representative
+// the fast pass served (its bit in a.fastdone, which nothing rewrites after
+// COUNT) and whose (MP, words) are the representative's takes its key cache
+// (+ spill slots), its count (added to its chunk's total) and its wide mark.
+// The others — a representative deferred to this launch, or a fingerprint
+// collision — are returned compacted into the wave's lanes (`mine`, their
+// number returned) for the caller to walk like COUNT's deferred publishes.
+__device__ uint32_t dedupe_fixup_slice(const MatchArgs& a, WaveLds& W, uint32_t base, uint32_t nd, uint32_t& mine) {
+  const uint32_t lane = __lane_id();
+  const uint32_t i = base + lane;
+  const bool valid = i < nd;
+  uint32_t p = 0;
+  bool ok = false;
+  if (valid) {
+    p = a.deferred[2ull * a.npub + i];
+    const uint32_t slot = a.deferred[3ull * a.npub + i];
+    const uint32_t rep = slot <= a.dd_mask ? a.dd_rep[slot] : kNone;
+    if (rep < a.npub && rep != p && ((a.fastdone[rep / 32] >> (rep % 32)) & 1u)) {
+      const vmqg_pub P = a.pubs[p], R = a.pubs[rep];
+      ok = P.mountpoint == R.mountpoint && P.nwords == R.nwords;
+      for (uint32_t k = 0; ok && k < P.nwords; k++) ok = a.words[P.word_off + k] == a.words[R.word_off + k];
+      if (ok) {
+        const uint4* rk = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)rep * 2;
+        uint4* pk = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
+        const uint4 h = rk[0], k1 = rk[1];
+        pk[0] = h;
+        pk[1] = k1;
+        // spilled keys (3..8) or a wide publish's candidate paths: 64 B
+        const uint32_t nkf = h.y == kMany ? 0u : h.y & ~kHugeFlag;
+        if (h.y == kMany || (nkf > 2 && nkf <= kSpillKeys)) {
+          const uint4* rs = reinterpret_cast<const uint4*>(a.keyspill + (uint64_t)rep * kSpillKeys);
+          uint4* ps = reinterpret_cast<uint4*>(a.keyspill + (uint64_t)p * kSpillKeys);
+#pragma unroll
+          for (int q = 0; q < 4; q++) ps[q] = rs[q];
+        }
+        a.offsets[p] = h.x;
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)h.x);
+        if (h.y == kMany) atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + p / a.gpw), 1ull << (p % a.gpw));
+        else if (h.y & kHugeFlag) a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
+      }
+    }
+  }
+  const uint64_t many = __ballot(ok && reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2].y == kMany);
+  const uint64_t walk = __ballot(valid && !ok);
+  const uint32_t nw = (uint32_t)__popcll(walk);
+  if (lane == 0) {
+    if (many) atomicAdd(&a.status[kStMany], (uint32_t)__popcll(many));
+    if (nw) atomicAdd(&a.status[kStDupWalked], nw);
+  }
+  if (valid && !ok) W.cand[prefix_bits(walk)] = p;
+  wave_sync();
+  mine = W.cand[lane];   // read out before any walk reuses the buffer
+  wave_sync();
+  return uni(nw);
 }
 
 // --------------------------------------------------------------- kernels
@@ -1307,6 +1403,14 @@ void k_match_fast(MatchArgs a) {
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
+  // batch-wide dedupe (COUNT): a.dd_force 1 always, 0 never, 2 by the mode
+  // the previous call's fixup left (sampling 1 chunk in 16 while it is off)
+  bool dd_all = false, dd_sample = false;
+  if (MODE == 0 && a.dd_key) {
+    const uint32_t mode = a.dd_force == 2 ? uni(*a.dd_mode) : a.dd_force;
+    dd_all = mode == 1;
+    dd_sample = a.dd_force == 2;
+  }
   // EMIT writes every publish resolve can serve; the wide ones (kResMany)
   // and the whole-wave walks (kDeferred) are the EMIT tail launch's
   if constexpr (MODE == 1 && CH != GPW) {
@@ -1340,15 +1444,40 @@ void k_match_fast(MatchArgs a) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
     if (MODE == 0) {
       uint64_t c = 0;
-      uint32_t fl = 0, xl = 0;
-      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl, xl);
+      uint32_t fl = 0;
+      // dedupe every chunk (mode on) or every 16th (sampling the batch's
+      // repetition for the next call's mode, dedupe_fixup)
+      const bool dd = dd_all || (dd_sample && (base / GPW) % 16 == 0);
+      uint32_t dslot = kNone;
+      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl, dd, &dslot);
+      if (dd) {   // the chunk's duplicates into lists 2 / 3, one atomic per wave
+        const uint64_t tried = __ballot(g.gidx < n && g.lane == 0), dm = __ballot(g.gidx < n && g.lane == 0 && fl == 4);
+        uint32_t at = 0;
+        if (__lane_id() == 0) {
+          atomicAdd(&a.status[kStDupTried], (uint32_t)__popcll(tried));
+          if (dm) at = atomicAdd(&a.status[kStDup], (uint32_t)__popcll(dm));
+        }
+        at = __shfl(at, 0, 64);
+        if (g.gidx < n && g.lane == 0 && fl == 4) {
+          const uint32_t k = at + prefix_bits(dm);
+          a.deferred[2ull * a.npub + k] = base + g.gidx;
+          a.deferred[3ull * a.npub + k] = dslot;
+        }
+      }
       // the chunk's total (publishes the wave tier takes add theirs later)
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
       // wide publishes: the chunk's mask for the EMIT tail launch
-      mark_wide<G, false>(a, g, fl, xl, base);
+      mark_wide<G, false>(a, g, fl, base);
       const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
       if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
+      // served here (fast tier or wide): a duplicate of it may take its results
+      const uint64_t done = group_bits_to_publish_bits<G>(__ballot(g.gidx < n && g.lane == 0 && fl <= 1));
+      if (__lane_id() == 0) {
+        if (GPW == 64) { a.fastdone[base / 32] = (uint32_t)done; a.fastdone[base / 32 + 1] = (uint32_t)(done >> 32); }
+        else if (GPW == 32) a.fastdone[base / 32] = (uint32_t)done;
+        else reinterpret_cast<uint16_t*>(a.fastdone)[base / 16] = (uint16_t)done;
+      }
     } else if (OUT == 0) {
       emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
     } else {
@@ -1392,9 +1521,39 @@ void k_match_wave(MatchArgs a) {
     __shared__ uint2 ky[FS::KC * FS::SLOTS];
     const Group<4> g;
     const FS s{st, cd, ky, wv * GPW + g.gidx};
-    const uint32_t nd = uni(a.status[kStDeferred]);
-    for (uint32_t base = (uint32_t)gw * GPW; base < nd; base += nwaves * GPW)
-      count_deferred_wave<OUT, NT>(a, s, g, lds[wv], gstack, base, nd);
+    // block 0 sets the next call's dedupe mode from this call's counts:
+    // on while more than one publish in five repeats another
+    if (gw == 0 && lane == 0 && a.dd_key) {
+      const uint32_t tried = a.status[kStDupTried], dups = a.status[kStDup];
+      if (tried >= 256) *a.dd_mode = dups * 5u > tried ? 1u : 0u;
+    }
+    // COUNT's deferred publishes (list 0), sixteen per wave, then the
+    // duplicates the fixup could not serve, sixteen at a time (one call
+    // site of the retry: the walk is inlined once)
+    const uint32_t nd = uni(a.status[kStDeferred]), ndup = uni(a.status[kStDup]);
+    uint32_t d0 = (uint32_t)gw * GPW, dbase = (uint32_t)gw * 64;
+    uint32_t mine = 0, nmine = 0, taken = 0;
+    for (;;) {
+      bool valid;
+      uint32_t p;
+      if (d0 < nd) {
+        valid = d0 + g.gidx < nd;
+        p = a.deferred[valid ? d0 + g.gidx : 0];
+        d0 += nwaves * GPW;
+      } else {
+        while (taken >= nmine && dbase < ndup) {
+          nmine = dedupe_fixup_slice(a, lds[wv], dbase, ndup, mine);
+          taken = 0;
+          dbase += nwaves * 64;
+        }
+        if (taken >= nmine) break;
+        valid = taken + g.gidx < nmine;
+        p = __shfl(mine, (int)((taken + g.gidx) & 63), 64);
+        taken += GPW;
+      }
+      count_deferred_group<OUT, NT>(a, s, g, lds[wv], gstack, valid, p);
+      wave_sync();
+    }
     return;
   } else {
     // the whole-wave walks (list 1); a walk that outgrows its LDS stack
@@ -1413,25 +1572,56 @@ void k_match_wave(MatchArgs a) {
       }
       if (!VMQG_TAIL_NOWALK) wave_publish<1, OUT, NT>(a, lds[wv], nullptr, p, ob, oe);
     }
+    // the huge publishes, every wave a segment of each (records mode)
+    if (OUT == 0) {
+      const uint32_t nh = uni(a.status[kStHuge]);
+      for (uint32_t hi = 0; hi < nh; hi++) {
+        const uint32_t p = uni(a.deferred[4ull * a.npub + hi]);
+        const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
+        if (oe > cap || ob > oe) {
+          if (gw == 0 && lane == 0) atomicOr(a.err, kErrOverflow);
+          continue;
+        }
+        const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+        const uint4 h = kc[0], k1 = kc[1];
+        const uint32_t nk = h.y & ~kHugeFlag, ksum = k1.y + k1.w;
+        const uint64_t rmask = ((uint64_t)h.w << 32) | h.z;
+        if (gw == 0 && lane == 0 && oe - ob != h.x) atomicOr(a.err, kErrMismatch);
+        // keys {off, cum start}: the key cache's two, or the spill slots
+        const uint2* sp = a.keyspill + (uint64_t)p * kSpillKeys;
+        auto ks = [&](uint32_t i) -> uint2 {
+          if (nk > 2) return sp[i];
+          return i == 0 ? make_uint2(k1.x, 0u) : make_uint2(k1.z, k1.y);
+        };
+        const uint64_t total = oe - ob;
+        const uint64_t nseg = (total + kHugeSeg - 1) / kHugeSeg;
+        for (uint64_t sg = gw; sg < nseg; sg += nwaves) {
+          const uint64_t r0 = sg * kHugeSeg;
+          const uint32_t n = (uint32_t)(total - r0 < kHugeSeg ? total - r0 : kHugeSeg);
+          for (uint32_t j = lane; j < n; j += 64 * 8) {
+            uint4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              const uint32_t r = j + 64 * u;
+              if (r < n) v[u] = emission(a, ks, nk == 0 ? 1u : nk, ksum, rmask, (uint32_t)(r0 + r));
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              const uint32_t r = j + 64 * u;
+              if (r < n) store_rec<NT>(a.out, ob + r0 + r, v[u]);
+            }
+          }
+        }
+      }
+    }
     // the wide publishes, from the chunk masks COUNT left, at the positions
     // EMIT wrote into offsets[]: two at a time, one per half-wave
     if (uni(a.status[kStMany]) == 0) return;
     const Group<kWideLanes> h;
     const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
     uint64_t written = 0;
-    // VMQG_WIDE_XCD: the waves of XCD class x (block % 8) visit every chunk
-    // and take its label-x publishes; otherwise every wave its own chunks
-    const bool by_xcd = VMQG_WIDE_XCD && gridDim.x >= kXcds;
-    const uint32_t x = blockIdx.x % kXcds;
-    const uint32_t c0 = by_xcd ? (blockIdx.x / kXcds) * kWaves + wv : (uint32_t)gw;
-    const uint32_t cs = by_xcd ? ((gridDim.x - x + kXcds - 1) / kXcds) * kWaves : nwaves;
-    for (uint32_t c = c0; c < nchunks; c += cs) {
-      uint64_t m0 = uni64(a.widemask[c]);
-      if (by_xcd && m0) {
-        const uint64_t q0 = uni64(a.wideplane[3ull * c]), q1 = uni64(a.wideplane[3ull * c + 1]),
-                       q2 = uni64(a.wideplane[3ull * c + 2]);
-        m0 &= ((x & 1) ? q0 : ~q0) & ((x & 2) ? q1 : ~q1) & ((x & 4) ? q2 : ~q2);
-      }
+    for (uint32_t c = (uint32_t)gw; c < nchunks; c += nwaves) {
+      const uint64_t m0 = uni64(a.widemask[c]);
       for (uint64_t m = m0; m;) {
         uint32_t bit = 0;
         bool act = false;
