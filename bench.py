@@ -406,7 +406,8 @@ def main():
             "verified_counts": verified,
             "kernel_us": stages,
             "served": {"deferred": served["deferred_tier1"], "retried": served["retried"], "many_key": served["many_key"],
-                       "wave_entries": served["wave_entries"], "wide_entries": served["wide_entries"]},
+                       "wave_entries": served["wave_entries"], "wide_entries": served["wide_entries"],
+                       "dedup": served["dedup"], "dedup_walked": served["dedup_walked"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
                          "kernel": "k_match_fast<1,0,2,true,64> (EMIT)",
@@ -629,7 +630,8 @@ def bench_other(args):
         "arena_bytes": st["device_bytes"], "trie_edges": st["trie_edges"], "paths": st["paths"],
         "rebuilds": st["rebuilds"], "deferred": [st["deferred_tier1"], st["deferred_tier2"]],
         "served": {"deferred": st["deferred_tier1"], "retried": st["retried"],
-                   "many_key": st["many_key"], "wave_entries": st["wave_entries"], "wide_entries": st["wide_entries"]},
+                   "many_key": st["many_key"], "wave_entries": st["wave_entries"], "wide_entries": st["wide_entries"],
+                   "dedup": st["dedup"], "dedup_walked": st["dedup_walked"]},
         "build_id": _lib.build_id()}), flush=True)
 
 
@@ -759,7 +761,7 @@ def bench_d(args):
     log("rank %d: match batch %.2f ms -> %d match batches per %.0f ms churn period"
         % (rank, t_match * 1e3, per_period, period_s * 1e3))
     st0 = view.stats_raw()
-    view.set_timing(True)
+    view.set_timing(False)   # `value` from uninstrumented periods; kernel times from a pass after
     acc = {"apply": 0.0, "delta": 0.0, "patches": 0}
     if dist:
         dist.barrier()
@@ -774,9 +776,16 @@ def bench_d(args):
     rc = view.match_status(sp)
     if rc != 0:
         raise RuntimeError("match status %d" % rc)
+    st1 = view.stats_raw()   # how the last timed batch was served (deferred / many-key / wave-tier entries)
+    view.set_timing(True)    # the instrumented pass: per-launch times of 5 match batches
+    for _ in range(5):
+        match()
+    torch.cuda.synchronize()
     count_ns, emit_ns, _ = view.kernel_times()
     stages = stage_us(view)
-    st1 = view.stats_raw()   # how the last timed batch was served (deferred / many-key / wave-tier entries)
+    view.set_timing(False)
+    if view.match_status(sp) != 0:
+        raise RuntimeError("match status (instrumented pass)")
     emitted = int(d_offs[-1].item())
     # parity: every rank matches rank 0's (unrolled) batch; replicas must
     # equal the primary byte for byte, and all the live set's known answer
@@ -909,7 +918,8 @@ def bench_d(args):
             "verified": {"known_answer": known, "replicas_equal": replicas_equal, "images_equal": images_equal},
             "kernel_us": stages,
             "served": {"deferred": st1["deferred_tier1"], "retried": st1["retried"],
-                       "many_key": st1["many_key"], "wave_entries": wave_rec, "wide_entries": st1["wide_entries"]},
+                       "many_key": st1["many_key"], "wave_entries": wave_rec, "wide_entries": st1["wide_entries"],
+                       "dedup": st1["dedup"], "dedup_walked": st1["dedup_walked"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS if achieved else None,
                          "traffic": load_pmc_traffic("k_match_fast<1" if dom_key == "emit" else "k_match_wave<1",

@@ -351,7 +351,10 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "dedupe"    0 | 1 | 2  batch-wide dedupe of repeated (MP, topic) publishes in
  *                          COUNT: off, on, or auto (default: on while more than
  *                          one publish in five repeats another, judged on the
- *                          previous call — sampled on 1 chunk in 16 while off) */
+ *                          previous call — sampled on 1 chunk in 16 while off)
+ *   "groups"    0 | 1      records mode: publishes of >= 128 records grouped by what
+ *                          they emit and written group by group by the EMIT tail
+ *                          (default 1) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the match kernels over the last

@@ -1034,3 +1034,33 @@ def test_batch_dedupe_auto_mode_follows_the_repetition():
     assert np.array_equal(np.diff(o2.astype(np.int64)), c1[rep]) and np.array_equal(np.diff(o3.astype(np.int64)), c1[rep])
     want = orc.fold_batch([(mp, b"pub", t) for mp, t in distinct[:3000]])
     assert np.array_equal(c1[:3000], [len(x) for x in want])
+
+
+def test_output_groups_and_dedupe_write_the_same_bytes():
+    """The EMIT tail's output groups (big publishes written group by group)
+    and COUNT's batch dedupe change where and when records are written, not
+    what: on config D at 1/20 scale (alarm publishes of 1,000 records, $share
+    jobs of 400) the offsets and every record byte are equal with each of
+    them off and on; the default build's records are checked against the
+    oracle by test_config_d_churn_parity."""
+    from vernemq_amd import workloads as W
+    from vernemq_amd.reg_view import RegGpuView
+    w = W.config_d(scale=0.05, n_pubs=60_000)
+    v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
+    w.load_into(v, n=w.notes["n_live"])
+    pubs, words = w.publish_arrays(v)
+    outs = []
+    for groups, dedupe in ((0, 0), (1, 0), (1, 1), (0, 1)):
+        v.set_option("groups", groups)
+        v.set_option("dedupe", dedupe)
+        recs, offs = v.match_arrays(pubs, words)
+        st = v.stats_raw()
+        outs.append((np.asarray(offs).copy(), np.asarray(recs).view(np.uint8).copy()))
+        if dedupe:
+            assert st["dedup"] > 0
+    v.set_option("groups", 1)
+    v.set_option("dedupe", 2)
+    for o, r in outs[1:]:
+        assert np.array_equal(o, outs[0][0])
+        assert np.array_equal(r, outs[0][1])
+    assert int(outs[0][0][-1]) > 1000 * len(pubs) // 10

@@ -521,6 +521,9 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   } else if (n == "dedupe") {
     if (value < 0 || value > 2) return VMQG_E_INVAL;
     e.opt_dedupe = (uint32_t)value;
+  } else if (n == "groups") {
+    if (value < 0 || value > 1) return VMQG_E_INVAL;
+    e.opt_groups = (uint32_t)value;
   } else if (n == "count_bpc" || n == "emit_bpc") {
     if (value < 0 || value > 32) return VMQG_E_INVAL;
     (n == "count_bpc" ? e.opt_count_bpc : e.opt_emit_bpc) = (uint32_t)value;

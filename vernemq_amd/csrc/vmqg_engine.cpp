@@ -32,7 +32,7 @@ Engine::~Engine() {
       hipFree(sg.d);
     }
     hipFree(d_arena); hipFree(d_status); hipFree(d_deferred);
-    hipFree(d_keycache); hipFree(d_dd);
+    hipFree(d_keycache); hipFree(d_dd); hipFree(d_groups);
     hipFree(d_lookback); hipFree(d_ostack);
     hipFree(d_pubs); hipFree(d_words); hipFree(d_offs); hipFree(d_out);
     if (stream) hipStreamDestroy(stream);
@@ -971,8 +971,20 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     dd_slots = slots;
     dd_tag = 0;
   }
+  // output groups: 256-B slots, a 16th of the publishes (slots of older calls free by the same tag)
+  const uint64_t gslots = next_pow2(std::max<uint64_t>(npub / 16, 1024));
+  if (gslots > gs_slots) {
+    if (hipStreamSynchronize(st) != hipSuccess) return VMQG_E_DEVICE;
+    hipFree(d_groups);
+    d_groups = nullptr;
+    gs_slots = 0;
+    if (hipMalloc(&d_groups, gslots * 256) != hipSuccess) return VMQG_E_NOMEM;
+    if (hipMemsetAsync(d_groups, 0, gslots * 256, st) != hipSuccess) return VMQG_E_DEVICE;
+    gs_slots = gslots;
+  }
   if (++dd_tag >= (1u << 24)) {   // tags are 24 bits: clear before reuse
     if (hipMemsetAsync(d_dd, 0, dd_slots * 12, st) != hipSuccess) return VMQG_E_DEVICE;
+    if (hipMemsetAsync(d_groups, 0, gs_slots * 256, st) != hipSuccess) return VMQG_E_DEVICE;
     dd_tag = 1;
   }
   return VMQG_OK;
@@ -1050,6 +1062,8 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.dd_tag = dd_tag;
   a.dd_force = opt_dedupe;
   a.dd_mode = d_status + kStatusDdMode;
+  a.groups = opt_groups ? d_groups : nullptr;
+  a.gs_mask = gs_slots - 1;
   a.gpw = 64 / (opt_fast_g == 4 ? 4 : opt_fast_g == 1 ? 1 : 2);   // publishes per chunk
   a.status = d_status + kStatusSet * (call_seq & 1);
   a.status_next = d_status + kStatusSet * ((call_seq + 1) & 1);

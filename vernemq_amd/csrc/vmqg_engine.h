@@ -292,6 +292,8 @@ struct Engine {
   void* d_keycache = nullptr; uint64_t keycache_cap = 0;   // publishes
   void* d_dd = nullptr; uint64_t dd_slots = 0; uint32_t dd_tag = 0;   // batch-wide dedupe table
   uint32_t opt_dedupe = 2;                                 // vmqg_set_option "dedupe": 0 off, 1 on, 2 auto
+  void* d_groups = nullptr; uint64_t gs_slots = 0;         // output groups (records mode)
+  uint32_t opt_groups = 1;                                 // vmqg_set_option "groups": 0 off, 1 on
   // host-buffer match staging
   void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
   void* d_words = nullptr; uint64_t d_words_cap = 0;

@@ -48,6 +48,7 @@ struct MatchArgs {
   uint32_t dd_tag, dd_force;                      // this call's tag (never 0); 0 off, 1 on, 2 auto (dd_mode)
   uint32_t* dd_mode;                              // persistent: the mode the last call's fixup chose
   uint32_t* fastdone;                             // bit per publish: served by COUNT's fast pass
+  void* groups; uint64_t gs_mask;                 // output groups (records mode): 256-B slots, tagged by dd_tag
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records

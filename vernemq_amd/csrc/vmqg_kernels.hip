@@ -85,6 +85,25 @@ constexpr uint32_t kLists = 5;
 constexpr uint32_t kHugeRecords = VMQG_HUGE_RECORDS;
 constexpr uint32_t kHugeFlag = 0x40000000u;  // key cache word 1 (nk <= 8): a huge publish, the tail copies it
 constexpr uint32_t kHugeSeg = 64 * 8 * 4;     // records per tail wave and segment
+// Output groups (records mode): publishes of >= kGroupMin records with <= 2
+// keys or wide are grouped by a signature of what they emit (key cache, or
+// candidates + exact key + remote nodes + the '$' flag) into slots of
+// kGroupCap; the EMIT tail writes a slot's members back to back from one
+// wave, so their source lists are read from HBM once per slot and from that
+// CU's L1 / L2 for the rest (config D: every site/s/x/alarm/z publish copies
+// site s's 1,000-record list, every jobs/q/x publish queue q's 40 keys).
+#ifndef VMQG_GROUP_MIN
+#define VMQG_GROUP_MIN 128
+#endif
+constexpr uint32_t kGroupMin = VMQG_GROUP_MIN;
+constexpr uint32_t kGroupCap = 60;
+constexpr uint32_t kGroupFlag = 0x20000000u;  // key cache word 1 (nk <= 2): a grouped publish, the tail writes it
+struct alignas(16) GroupSlot {
+  unsigned long long word;   // {call tag: 24, signature: 32, members: 8}
+  uint32_t pad[2];
+  uint32_t m[kGroupCap];     // member publishes
+};
+static_assert(sizeof(GroupSlot) == 256, "");
 // progress words of the calling wave (VMQG_DEBUG_SYNC diagnosis; a.dbg null otherwise)
 #define DBGW(slot, v)                                                                                        \
   do {                                                                                                       \
@@ -98,6 +117,7 @@ enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, k
                   kStDup = 8 /* duplicates listed for the fixup */, kStDupTried = 9 /* publishes probed */,
                   kStDupWalked = 10 /* duplicates walked after all (representative deferred / words differ) */,
                   kStHuge = 11 /* huge publishes listed for the tail */,
+                  kStGrouped = 12 /* publishes in output groups */,
                   kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
 #define VMQG_WIDE_RECORDS 0x7fffffff   // A/B: a publish with at least this many records is wide too (256: config D 2,724 vs 2,526 us per batch, off)
@@ -601,6 +621,34 @@ __device__ bool dedupe_probe(const MatchArgs& a, uint64_t fp, uint32_t p, uint32
   return false;
 }
 
+// Joins publish p to the output group of signature `sig` (a slot with room,
+// or a new one claimed by CAS; full slots chain to the next).  One lane.
+__device__ bool group_insert(const MatchArgs& a, uint64_t sig64, uint32_t p) {
+  GroupSlot* gs = reinterpret_cast<GroupSlot*>(a.groups);
+  const unsigned long long T = (unsigned long long)a.dd_tag << 40;
+  const uint32_t sig = (uint32_t)(sig64 >> 32);
+  uint64_t i = sig64 & a.gs_mask;
+  for (uint32_t probe = 0; probe < 32; probe++, i = (i + 1) & a.gs_mask) {
+    unsigned long long* wp = &gs[i].word;
+    unsigned long long w = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if ((w >> 40) != a.dd_tag) {   // a slot of an older call: claim it as member 0
+        const unsigned long long prev = atomicCAS(wp, w, T | ((unsigned long long)sig << 8) | 1ull);
+        if (prev == w) { gs[i].m[0] = p; return true; }
+        w = prev;
+        continue;
+      }
+      if ((uint32_t)(w >> 8) != sig) break;                 // another signature
+      const uint32_t n = (uint32_t)(w & 0xFF);
+      if (n >= kGroupCap) break;                            // full: the chain goes on in the next slot
+      const unsigned long long prev = atomicCAS(wp, w, w + 1);
+      if (prev == w) { gs[i].m[n] = p; return true; }
+      w = prev;
+    }
+  }
+  return false;   // no room: EMIT writes it as usual
+}
+
 template <int G, int OUT, bool RETRY = false, uint32_t SL = kWaves * (64 / G)>
 __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G, SL>& s, const Group<G>& g,
                                   uint32_t& fl, bool dedupe = false, uint32_t* dslot = nullptr) {
@@ -657,18 +705,30 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
     kc[0] = make_uint4(total, kMany, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
     kc[1] = make_uint4(m.nc, m.ksum, m.ex_off, m.ex_cnt);
     fl = 1;
+    if (OUT == 0 && total >= kGroupMin && a.groups) {   // an output group instead of the chunk mask: fl 5
+      uint64_t sig = mix64(((uint64_t)m.ex_off << 32) ^ m.ex_cnt ^ ((uint64_t)(pub.flags & VMQG_PUB_DOLLAR) << 63));
+      sig = mix64(sig ^ m.rmask) ^ m.nc;
+      for (uint32_t i = 0; i < m.nc; i++) sig = mix64(sig + s.cd(i));
+      if (group_insert(a, sig, p)) fl = 5;
+    }
   } else {
     // a huge records-mode publish (R2's one topic of 4M subscribers): every
     // wave of the EMIT tail copies a segment of it (one wave would take ms)
     const bool huge = OUT == 0 && total >= kHugeRecords;
-    const uint32_t hf = huge ? kHugeFlag : 0u;
+    uint32_t hf = huge ? kHugeFlag : 0u;
     if (huge) a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
     if (m.nk <= 2) {
       const uint2 k0 = m.nk > 0 ? s.ky(0) : make_uint2(0, 0);
       const uint2 k1 = m.nk > 1 ? s.ky(1) : make_uint2(0, m.ksum);
       const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
+      const uint4 w1 = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
+      if (OUT == 0 && !huge && total >= kGroupMin && a.groups &&
+          group_insert(a, mix64(mix64(((uint64_t)w1.x << 32) | w1.y) ^ (((uint64_t)w1.z << 32) | w1.w)) ^ m.rmask, p)) {
+        hf = kGroupFlag;   // the EMIT tail writes it with its output group: fl 6
+        fl = 6;
+      }
       kc[0] = make_uint4(total, m.nk | hf, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
-      kc[1] = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
+      kc[1] = w1;
     } else {
       kc[0] = make_uint4(total, m.nk | hf, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
       kc[1] = make_uint4(0, m.ksum, 0, 0);
@@ -726,7 +786,7 @@ __device__ int resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, 
   uint32_t total;
   if (h.y == kDeferred) return kResSkip;   // written by the wave tier
   const bool many = h.y == kMany;
-  if (!many && (h.y & kHugeFlag)) return kResSkip;   // written by the EMIT tail, segment by segment
+  if (!many && (h.y & (kHugeFlag | kGroupFlag))) return kResSkip;   // the EMIT tail writes it (segments / groups)
   if (many) {
     total = h.x;
   } else {
@@ -847,6 +907,35 @@ __device__ void emit_many(const MatchArgs& a, const Group<SW>& g, bool act, uint
   }
   run += nrem;
   if (act && lane == 0 && run != oe - ob) atomicOr(a.err, kErrMismatch);
+}
+
+// A grouped publish of <= 2 keys (key cache {off0, c0, off1, c1}) written
+// by the whole wave into [ob, oe): key 0's records, key 1's, then the
+// remote nodes in node order (fold_/5, vmq_reg_trie.erl:78-84).
+template <bool NT>
+__device__ void emit_keys2(const MatchArgs& a, uint4 h, uint4 k1, uint64_t ob, uint64_t oe) {
+  const uint32_t lane = __lane_id();
+  const uint32_t c0 = k1.y, ks = k1.y + k1.w;
+  const uint64_t rm = ((uint64_t)h.w << 32) | h.z;
+  const uint32_t tot = (uint32_t)(oe - ob);
+  for (uint32_t r0 = lane; r0 < tot; r0 += 64 * 8) {
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t r = r0 + 64 * u;
+      if (r < tot) {
+        if (r < c0) v[u] = *reinterpret_cast<const uint4*>(a.records + k1.x + r);
+        else if (r < ks) v[u] = *reinterpret_cast<const uint4*>(a.records + k1.z + (r - c0));
+        else v[u] = make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rm, r - ks), kNone, kNone, kNone);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t r = r0 + 64 * u;
+      if (r < tot) store_rec<NT>(a.out, ob + r, v[u]);
+    }
+  }
+  if (lane == 0 && tot != h.x) atomicOr(a.err, kErrMismatch);
 }
 
 // Output ranges of the GPW publishes [first, first + n) of one chunk: the
@@ -1291,13 +1380,17 @@ __device__ void count_deferred_group(const MatchArgs& a, const FastScratch<4, SL
   uint32_t fl = 2, c = 0;
   if (retry && valid) {
     c = count_publish<4, OUT, true, SL>(a, p, s, g, fl);
-    if (g.lane == 0 && fl <= 1)
+    if (g.lane == 0 && (fl <= 1 || fl >= 5))
       atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)c);
   }
   wave_sync();
-  if (retry) mark_wide<4, true>(a, g, fl, p);
+  if (retry) {
+    mark_wide<4, true>(a, g, fl, p);
+    const uint32_t n_grp = (uint32_t)__popcll(__ballot(valid && g.lane == 0 && fl >= 5));
+    if (lane == 0 && n_grp) atomicAdd(&a.status[kStGrouped], n_grp);
+  }
   // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
-  uint64_t ov = __ballot(valid && g.lane == 0 && fl >= 2);
+  uint64_t ov = __ballot(valid && g.lane == 0 && (fl == 2 || fl == 3));
   if (!retry && ov) {   // list 1 for EMIT (the retry's count_publish listed its own)
     uint32_t at = 0;
     if (lane == 0) at = atomicAdd(&a.status[kStWalked], (uint32_t)__popcll(ov));
@@ -1336,7 +1429,9 @@ __device__ uint32_t dedupe_fixup_slice(const MatchArgs& a, WaveLds& W, uint32_t 
       if (ok) {
         const uint4* rk = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)rep * 2;
         uint4* pk = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
-        const uint4 h = rk[0], k1 = rk[1];
+        uint4 h = rk[0];
+        const uint4 k1 = rk[1];
+        if (h.y != kMany) h.y &= ~kGroupFlag;   // not a member of the representative's group: EMIT writes it
         pk[0] = h;
         pk[1] = k1;
         // spilled keys (3..8) or a wide publish's candidate paths: 64 B
@@ -1471,8 +1566,10 @@ void k_match_fast(MatchArgs a) {
       mark_wide<G, false>(a, g, fl, base);
       const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
       if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
+      const uint32_t n_grp = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl >= 5));
+      if (__lane_id() == 0 && n_grp) atomicAdd(&a.status[kStGrouped], n_grp);
       // served here (fast tier or wide): a duplicate of it may take its results
-      const uint64_t done = group_bits_to_publish_bits<G>(__ballot(g.gidx < n && g.lane == 0 && fl <= 1));
+      const uint64_t done = group_bits_to_publish_bits<G>(__ballot(g.gidx < n && g.lane == 0 && (fl <= 1 || fl >= 5)));
       if (__lane_id() == 0) {
         if (GPW == 64) { a.fastdone[base / 32] = (uint32_t)done; a.fastdone[base / 32 + 1] = (uint32_t)(done >> 32); }
         else if (GPW == 32) a.fastdone[base / 32] = (uint32_t)done;
@@ -1614,39 +1711,57 @@ void k_match_wave(MatchArgs a) {
         }
       }
     }
-    // the wide publishes, from the chunk masks COUNT left, at the positions
-    // EMIT wrote into offsets[]: two at a time, one per half-wave
-    if (uni(a.status[kStMany]) == 0) return;
-    const Group<kWideLanes> h;
+    // then, one publish at a time per wave (one call site of each writer,
+    // so the walk and copy code is inlined once): the output groups — a
+    // slot's members back to back, their sources staying in this CU's L1 /
+    // L2 after the first member — and then the wide publishes of the chunk
+    // masks COUNT left, at the positions EMIT wrote into offsets[]
+    bool groups_on = OUT == 0 && uni(a.status[kStGrouped]) != 0;
+    bool wide_on = uni(a.status[kStMany]) != 0;
+    if (!groups_on && !wide_on) return;
+    const GroupSlot* gs = reinterpret_cast<const GroupSlot*>(a.groups);
     const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
-    uint64_t written = 0;
-    for (uint32_t c = (uint32_t)gw; c < nchunks; c += nwaves) {
-      const uint64_t m0 = uni64(a.widemask[c]);
-      for (uint64_t m = m0; m;) {
-        uint32_t bit = 0;
-        bool act = false;
-#pragma unroll
-        for (uint32_t k = 0; k < 64 / kWideLanes; k++) {   // the k-th set bit goes to group k
-          const bool has = m != 0;
-          if (h.gidx == k) { act = has; bit = has ? (uint32_t)__builtin_ctzll(m) : 0u; }
-          if (has) m &= m - 1;
+    uint64_t si = gw, cur = 0, m = 0, written = 0;
+    uint32_t j = 0, gn = 0, c = (uint32_t)gw, cc = 0;
+    for (;;) {
+      uint32_t p = 0;
+      bool have = false;
+      if (groups_on) {
+        while (j >= gn && si <= a.gs_mask) {
+          const unsigned long long w = uni64(gs[si].word);
+          gn = (w >> 40) == a.dd_tag ? (uint32_t)(w & 0xFF) : 0u;
+          j = 0;
+          cur = si;
+          si += nwaves;
         }
-        const uint32_t p = c * a.gpw + bit;
-        uint64_t ob = 0, oe = 0;
-        if (act) {
-          ob = a.offsets[p];
-          oe = a.offsets[p + 1];
-          if (oe > cap || ob > oe) {
-            if (h.lane == 0) atomicOr(a.err, kErrOverflow);
-            act = false;
-          }
-        }
-        emit_many<OUT, NT, VMQG_TAIL_U, kWideLanes>(a, h, act, p, ob, oe, lds[wv].keys + h.gidx * kWideLanes);
-        if (act && h.lane == 0) written += oe - ob;
-        wave_sync();
+        if (j < gn) { p = uni(gs[cur].m[j]); j++; have = true; }
+        else groups_on = false;
       }
+      if (!have && wide_on) {
+        while (m == 0 && c < nchunks) { m = uni64(a.widemask[c]); cc = c; c += nwaves; }
+        if (m) {
+          p = cc * a.gpw + (uint32_t)__builtin_ctzll(m);
+          m &= m - 1;
+          have = true;
+        } else {
+          wide_on = false;
+        }
+      }
+      if (!have) break;
+      if (p >= a.npub) { if (lane == 0) atomicOr(a.err, kErrMismatch); continue; }
+      const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
+      if (oe > cap || ob > oe) {
+        if (lane == 0) atomicOr(a.err, kErrOverflow);
+        continue;
+      }
+      const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+      const uint4 h = kc[0], k1 = kc[1];
+      if (uni(h.y) == kMany) emit_many<OUT, NT, VMQG_TAIL_U, 64>(a, Group<64>(), true, p, ob, oe, lds[wv].keys);
+      else if (OUT == 0) emit_keys2<NT>(a, h, k1, ob, oe);
+      written += oe - ob;
+      wave_sync();
     }
-    if (written) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)written);
+    if (written && lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)written);
   }
 }
 
