@@ -15,7 +15,6 @@ VARIANTS = {
     "tail8": ["-DVMQG_TAIL_BPC=8"],
     "walkcall": ["-DVMQG_WALK_CALL=1"],
     "wide32": ["-DVMQG_WIDE_LANES=32"],
-    "xcd": ["-DVMQG_WIDE_XCD=1"],
     "recwide256": ["-DVMQG_WIDE_RECORDS=256"],
     "nofilter": ["-DVMQG_EXACT_FILTER=0"],
     "nowalk": ["-DVMQG_TAIL_NOWALK=1"],
