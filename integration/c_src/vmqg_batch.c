@@ -347,6 +347,28 @@ int vmqgb_fold_ranges(const vmqgb_batch* b, const vmqg_emit* recs, uint64_t nrec
   return 0;
 }
 
+int vmqgb_fold_spans(const vmqgb_batch* b, int ranges, const vmqg_emit* recs, uint64_t nrecs, size_t i,
+                     vmqgb_span_fn fn, void* acc) {
+  if (i >= b->n) return VMQG_E_INVAL;
+  if (!ranges) {
+    const uint64_t lo = b->offsets[i], hi = b->offsets[i + 1];
+    return hi > lo ? fn(acc, b->out + lo, (size_t)(hi - lo)) : 0;
+  }
+  for (uint64_t k = b->offsets[i]; k < b->offsets[i + 1]; k++) {
+    const vmqg_range g = b->rng[k];
+    int r;
+    if (g.count == 0) {   /* remote node (vmq_reg_trie.erl:78-84) */
+      const vmqg_emit e = {(VMQG_EMIT_REMOTE << 24) | g.off, VMQG_NONE, VMQG_NONE, VMQG_NONE};
+      r = fn(acc, &e, 1);
+    } else {
+      if ((uint64_t)g.off + g.count > nrecs) return VMQG_E_STATE;   /* table changed under the ranges */
+      r = fn(acc, recs + g.off, g.count);
+    }
+    if (r) return r;
+  }
+  return 0;
+}
+
 /* ------------------------------------------------------------------- ops */
 int vmqgb_ops_init(vmqgb_ops* o) {
   memset(o, 0, sizeof(*o));
@@ -450,6 +472,7 @@ struct vmqgb_view {
   vmqgb_req* q_head;
   vmqgb_req* q_tail;
   int in_kernels;            /* rounds submitted whose offsets are not back */
+  int inflight;              /* ... at most this many */
   int pipelined;             /* the context has a device: hbatch rounds */
   int device_records;
   vmqgb_round rounds[VMQGB_ROUNDS];
@@ -470,6 +493,7 @@ vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx) {
   const int r4 = pthread_cond_init(&v->q_cv, NULL);
   if (r1 || r2 || r3 || r4) { free(v); return NULL; }
   v->pipelined = 1;
+  v->inflight = 2;
   for (int i = 0; i < VMQGB_ROUNDS; i++) {
     v->rounds[i].hb = vmqg_hbatch_new(ctx);   /* NULL on a host-engine-only context */
     if (!v->rounds[i].hb) v->pipelined = 0;
@@ -516,6 +540,12 @@ int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
 }
 
 void vmqgb_view_set_device_records(vmqgb_view* v, int on) { v->device_records = on != 0; }
+void vmqgb_view_set_inflight(vmqgb_view* v, int n) {
+  pthread_mutex_lock(&v->q_mu);
+  v->inflight = n < 1 ? 1 : n > VMQGB_ROUNDS - 1 ? VMQGB_ROUNDS - 1 : n;
+  pthread_cond_broadcast(&v->q_cv);
+  pthread_mutex_unlock(&v->q_mu);
+}
 
 void vmqgb_view_get_stats(vmqgb_view* v, vmqgb_view_stats* out) {
   pthread_mutex_lock(&v->q_mu);
@@ -606,9 +636,9 @@ static void run_round(vmqgb_view* v, vmqgb_round* r, vmqgb_req* list) {
 }
 
 /* Queues req and returns when a round has served it (q_mu not held on entry
- * or exit).  A waiting batcher becomes the combiner when fewer than two
- * rounds are in the kernels and a round is free: it takes the queued batches
- * of the head's device mode, up to VMQGB_ROUND_MAX publishes. */
+ * or exit).  A waiting batcher becomes the combiner when fewer than
+ * v->inflight rounds are in the kernels and a round is free: it takes the
+ * queued batches of the head's device mode, up to VMQGB_ROUND_MAX publishes. */
 static void combine(vmqgb_view* v, vmqgb_req* req) {
   pthread_mutex_lock(&v->q_mu);
   req->done = 0;
@@ -617,7 +647,7 @@ static void combine(vmqgb_view* v, vmqgb_req* req) {
   v->q_tail = req;
   while (!req->done) {
     vmqgb_round* r = NULL;
-    if (v->q_head && v->in_kernels < 2)
+    if (v->q_head && v->in_kernels < v->inflight)
       for (int i = 0; i < VMQGB_ROUNDS && !r; i++) if (!v->rounds[i].busy) r = &v->rounds[i];
     if (!r) { pthread_cond_wait(&v->q_cv, &v->q_mu); continue; }
     /* take the head's mode, FIFO, up to the round's publish budget */

@@ -125,6 +125,15 @@ int vmqgb_fold(const vmqgb_batch* b, size_t i, vmqgb_fold_fn fn, void* acc);
 /* range mode, expanded over the context's record table */
 int vmqgb_fold_ranges(const vmqgb_batch* b, const vmqg_emit* recs, uint64_t nrecs, size_t i, vmqgb_fold_fn fn,
                       void* acc);
+/* The same FoldFun arguments in the same order, handed over as runs of
+ * consecutive 16-B records (vmqg_emit: kind << 24 | node, group, subscriber,
+ * subinfo): one call per publish in records mode, one per key range in range
+ * mode (a remote node: a run of one record built on the stack).  `recs` /
+ * `nrecs`: the record table of the batch's epoch in range mode, ignored in
+ * records mode.  One indirect call per run instead of per entry. */
+typedef int (*vmqgb_span_fn)(void* acc, const vmqg_emit* run, size_t n);
+int vmqgb_fold_spans(const vmqgb_batch* b, int ranges, const vmqg_emit* recs, uint64_t nrecs, size_t i,
+                     vmqgb_span_fn fn, void* acc);
 
 /* ---- subscription ops -------------------------------------------------- */
 typedef struct vmqgb_ops {
@@ -161,8 +170,8 @@ vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v);
  * prepared batch; whichever waiting batcher finds the pipeline free takes
  * every batch queued at that moment and matches them as ONE device call
  * (vmqg_hbatch_*: one H2D, one launch sequence, one D2H), then hands each
- * batch its slice.  Up to two such rounds are in the kernels at once and up
- * to VMQGB_ROUNDS exist, so round k+1's inputs are copied and matched while
+ * batch its slice.  Up to two such rounds (vmqgb_view_set_inflight) are in
+ * the kernels at once and up to VMQGB_ROUNDS exist, so round k+1's inputs are copied and matched while
  * round k's results come back and round k-1's are folded.  The device works
  * in range mode ({record off, count} per key: 16 B per config-C publish over
  * PCIe instead of 1,040 B of records); a records-mode batch is expanded from
@@ -178,7 +187,7 @@ void vmqgb_view_read_end(vmqgb_view* v);
  * one slice of a batch, not for every reader's whole batch. */
 void vmqgb_view_yield(vmqgb_view* v);
 #define VMQGB_YIELD_EVERY 512
-#define VMQGB_ROUNDS 4
+#define VMQGB_ROUNDS 6
 #define VMQGB_ROUND_MAX (1u << 17)   /* publishes per combined round */
 /* Called under the read lock, returns under it: the batch's results
  * (offsets + out in records mode, offsets + rng in range mode) and, in range
@@ -208,6 +217,7 @@ int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);   /* ins
 int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);       /* write_begin, apply, write_end */
 /* Knobs and counters of the submitter (tools/nif_harness.c reports them). */
 void vmqgb_view_set_device_records(vmqgb_view* v, int on);   /* records over PCIe instead of host expansion */
+void vmqgb_view_set_inflight(vmqgb_view* v, int n);          /* rounds in the kernels at once: 1..VMQGB_ROUNDS-1 (2) */
 typedef struct vmqgb_view_stats {
   uint64_t rounds, round_publishes, round_batches, max_round_publishes;
   uint64_t expanded_batches, device_record_batches, state_retries, stale_rematches;

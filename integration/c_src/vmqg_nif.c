@@ -315,6 +315,16 @@ static int make_entry(void* accp, const vmqgb_entry* e) {
   return 0;
 }
 
+/* a run of consecutive records (vmqgb_fold_spans): one term each, in order */
+static int make_entries(void* accp, const vmqg_emit* run, size_t n) {
+  for (size_t j = 0; j < n; j++) {
+    const vmqgb_entry e = {run[j].kind_node >> 24, run[j].kind_node & 0xFFFFFFu, run[j].group, run[j].subscriber,
+                           run[j].subinfo};
+    make_entry(accp, &e);
+  }
+  return 0;
+}
+
 /* batch_new(Ctx) -> {ok, Batch}: a batcher's own publish batch */
 static ERL_NIF_TERM nif_batch_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   (void)argc;
@@ -418,8 +428,7 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
       cnt = vmqgb_count_of(b, (size_t)idx[i]);
     }
     fold_acc acc = {env, r, (ERL_NIF_TERM*)enif_alloc((cnt ? cnt : 1) * sizeof(ERL_NIF_TERM)), 0};
-    const int frc = ranges ? vmqgb_fold_ranges(b, recs, nrecs, (size_t)idx[i], make_entry, &acc)
-                           : vmqgb_fold(b, (size_t)idx[i], make_entry, &acc);
+    const int frc = vmqgb_fold_spans(b, ranges, recs, nrecs, (size_t)idx[i], make_entries, &acc);
     /* a fold that stops early (a range beyond the table) is this publish's error, never a partial list */
     res[i] = frc ? error_term(env, frc) : enif_make_tuple2(env, a_ok, enif_make_list_from_array(env, acc.out, (unsigned)acc.n));
     enif_free(acc.out);

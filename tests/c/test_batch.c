@@ -16,6 +16,17 @@ static int collect(void* acc, const vmqgb_entry* e) {
   return 0;
 }
 
+typedef struct { vmqgb_entry* p; int runs; } span_acc;
+static int collect_span(void* accp, const vmqg_emit* r, size_t n) {
+  span_acc* a = (span_acc*)accp;
+  for (size_t j = 0; j < n; j++) {
+    const vmqgb_entry e = {r[j].kind_node >> 24, r[j].kind_node & 0xFFFFFFu, r[j].group, r[j].subscriber, r[j].subinfo};
+    *a->p++ = e;
+  }
+  a->runs++;
+  return 0;
+}
+
 int main(void) {
   /* interner: dense ids, both directions, growth past the first table */
   vmqgb_interner* t = vmqgb_interner_new();
@@ -150,6 +161,18 @@ int main(void) {
   q = got2;
   CHECK(vmqgb_fold_ranges(&b1, recs, 4, 1, collect, &q) == 0 && q - got2 == 1 && got2[0].subscriber == 13);
   CHECK(vmqgb_fold_ranges(&b1, recs, 3, 1, collect, &q) == VMQG_E_STATE);   /* range past the table */
+  /* runs of records: the same entries in the same order, one call per range / per publish */
+  vmqgb_entry got3[8];
+  span_acc sa = {got3, 0};
+  CHECK(vmqgb_fold_spans(&b1, 1, recs, 4, 0, collect_span, &sa) == 0 && sa.p - got3 == 3 && sa.runs == 2);
+  CHECK(memcmp(got, got3, 3 * sizeof(vmqgb_entry)) == 0);
+  sa.p = got3;
+  CHECK(vmqgb_fold_spans(&b1, 1, recs, 3, 1, collect_span, &sa) == VMQG_E_STATE);
+  b1.offsets[0] = 0; b1.offsets[1] = 3; b1.offsets[2] = 4;   /* records mode again */
+  sa.p = got3; sa.runs = 0;
+  CHECK(vmqgb_fold_spans(&b1, 0, NULL, 0, 0, collect_span, &sa) == 0 && sa.p - got3 == 3 && sa.runs == 1);
+  CHECK(memcmp(got, got3, 3 * sizeof(vmqgb_entry)) == 0);
+  CHECK(vmqgb_fold_spans(&b1, 0, NULL, 0, 2, collect_span, &sa) == VMQG_E_INVAL);
   vmqgb_batch_free(&b1);
   vmqgb_batch_free(&b2);
   vmqgb_ops_free(&ops);

@@ -838,17 +838,24 @@ def _device_match_records(v, pubs, words, total_hint):
     d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
     n = len(pubs)
     cap = int(total_hint) + 1024
-    d_out = torch.empty(cap * 4, dtype=torch.int32, device=dev)
+    d_out = torch.full((cap * 4,), -1, dtype=torch.int32, device=dev)   # a position never written stays all-ones
     d_offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream().cuda_stream
     v.match_device(d_pubs.data_ptr(), n, d_words.data_ptr(), d_out.data_ptr(), cap, d_offs.data_ptr(), sp)
     torch.cuda.synchronize()
     assert v.match_status(sp) == 0
-    return d_out, d_offs.cpu().numpy()
+    offs = d_offs.cpu().numpy()
+    holes = torch.nonzero((d_out.view(-1, 4)[:int(offs[-1])] == -1).all(dim=1)).flatten().cpu().numpy()
+    if len(holes):
+        pub = np.searchsorted(offs.astype(np.int64), holes, side="right") - 1
+        raise AssertionError("%d record positions never written, in %d publishes (first %d: count %d)" % (
+            len(holes), len(np.unique(pub)), int(pub[0]), int(offs[pub[0] + 1] - offs[pub[0]])))
+    return d_out, offs
 
 
-def _sample_records(v, d_out, offs, sample):
-    """The records of the sampled publishes, gathered on the device, decoded."""
+def _sample_records(v, d_out, offs, sample, sub_term=None):
+    """The records of the sampled publishes, gathered on the device, decoded
+    (sub_term: SubscriberId terms of a lean workload, RegGpuView.decode)."""
     import torch
     from vernemq_amd.reg_view import EMIT_DTYPE
     lo = offs[sample].astype(np.int64)
@@ -859,7 +866,7 @@ def _sample_records(v, d_out, offs, sample):
     recs = d_out.view(-1, 4).index_select(0, idx).cpu().numpy().view(EMIT_DTYPE).reshape(-1)
     out, k = [], 0
     for n in lens:
-        out.append(sorted(H.canon(v.decode(recs[j])) for j in range(k, k + int(n))))
+        out.append(sorted(H.canon(v.decode(recs[j], sub_term)) for j in range(k, k + int(n))))
         k += int(n)
     return out
 
@@ -950,7 +957,7 @@ def test_config_e_scale_02_oracle_sample():
     orc = O.TrieOracle(w.self_node)
     for lo in range(0, len(subs_idx), 1 << 18):
         orc.apply_raw(feed.init_bytes(w, idx=subs_idx[lo:lo + (1 << 18)]))
-    got = _sample_records(v, d_out, offs, sample)
+    got = _sample_records(v, d_out, offs, sample, w.client_term)   # lean workload: subscriber id = client index
     want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(int(i))) for i in sample])
     bad = [k for k in range(len(sample)) if got[k] != sorted(want[k])]
     assert not bad, (len(bad), w.pub_topic(int(sample[bad[0]])))
@@ -1064,3 +1071,32 @@ def test_output_groups_and_dedupe_write_the_same_bytes():
         assert np.array_equal(o, outs[0][0])
         assert np.array_equal(r, outs[0][1])
     assert int(outs[0][0][-1]) > 1000 * len(pubs) // 10
+
+
+def test_group_slots_of_older_calls_do_not_survive_a_tag_restart():
+    """Output-group slots are claimed per call by the dedupe tag; the tag
+    restarts when the dedupe table grows.  Call 1: 1,000 publishes of g/x
+    (200 records, one key: output groups); call 2: 3,000 publishes of s/y
+    (3 keys, spilled) — a bigger batch, so the dedupe table grows while the
+    group table does not.  Call 2's publishes 0..999 must not be taken for
+    call 1's group members (the tail would write them as one-key publishes)."""
+    node = "n@h"
+    prod = _driver(node)
+    v = prod.view
+    v.set_option("dedupe", 0)
+    orc = O.TrieOracle(node)
+    evs = [("updated", ("", b"g%d" % i), None, [(node, True, [((b"g", b"x"), i % 3)])]) for i in range(200)]
+    for i, f in enumerate([(b"s", b"y"), (b"s", b"+"), (b"+", b"y")]):
+        evs.append(("updated", ("", b"s%d" % i), None, [(node, True, [(f, 1)])]))
+    prod.apply(evs)
+    orc.apply(evs)
+    want_g, want_s = orc.fold_batch([("", b"pub", (b"g", b"x")), ("", b"pub", (b"s", b"y"))])
+    arr, words = v.prepare([("", (b"g", b"x")), ("", (b"s", b"y"))])
+    recs, offs = prod.match_arrays(arr[np.zeros(1000, dtype=np.int64)], words)
+    assert np.array_equal(np.diff(offs.astype(np.int64)), np.full(1000, len(want_g)))
+    for n in (3000, 3000):
+        recs, offs = prod.match_arrays(arr[np.ones(n, dtype=np.int64)], words)
+        assert np.array_equal(np.diff(offs.astype(np.int64)), np.full(n, len(want_s)))
+        for i in list(range(0, 1000, 37)) + [n - 1]:
+            got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
+            assert got == sorted(want_s), i

@@ -71,6 +71,17 @@ static int sum_entry(void* acc, const vmqgb_entry* e) {
   return 0;
 }
 
+/* the same per-entry work over a run of records (vmqgb_fold_spans) */
+static int sum_span(void* acc, const vmqg_emit* r, size_t n) {
+  uint64_t* s = (uint64_t*)acc;
+  uint64_t x = 0;
+  for (size_t j = 0; j < n; j++) x += r[j].subscriber ^ r[j].subinfo ^ (r[j].kind_node & 0xFFFFFFu);
+  s[0] += x;
+  s[1] += n;
+  return 0;
+}
+static int fold_spans = 1;   /* 0: one callback per entry (vmqgb_fold / vmqgb_fold_ranges) */
+
 /* ------------------------------------------------------------ batchers */
 typedef struct {
   int tid, T, ranges;
@@ -106,7 +117,8 @@ static void* batcher(void* p) {
     const double t2 = now();
     for (size_t i = 0; !rc && i < b.n; i++) {
       if (!a->ranges && i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(view);   /* records: copies */
-      rc = a->ranges ? vmqgb_fold_ranges(&b, recs, nrecs, i, sum_entry, acc) : vmqgb_fold(&b, i, sum_entry, acc);
+      if (fold_spans) rc = vmqgb_fold_spans(&b, a->ranges, recs, nrecs, i, sum_span, acc);
+      else rc = a->ranges ? vmqgb_fold_ranges(&b, recs, nrecs, i, sum_entry, acc) : vmqgb_fold(&b, i, sum_entry, acc);
     }
     vmqgb_view_release(view, &b);
     vmqgb_view_read_end(view);
@@ -290,13 +302,13 @@ static int run(const char* section, int T, size_t B, int ranges, double secs, ch
   const double el = now() - tstart;
   vmqgb_view_get_stats(view, &s1);
   const uint64_t rounds = s1.rounds - s0.rounds;
-  printf("{\"section\": \"%s\", \"mode\": \"%s\", \"batchers\": %d, \"batch\": %zu, \"seconds\": %.2f, "
+  printf("{\"section\": \"%s\", \"mode\": \"%s\", \"fold\": \"%s\", \"batchers\": %d, \"batch\": %zu, \"seconds\": %.2f, "
          "\"publishes\": %llu, \"entries\": %llu, \"publishes_per_s\": %.4g, \"entries_per_s\": %.4g, "
          "\"per_batch_ms\": {\"prepare\": %.3f, \"match\": %.3f, \"fold\": %.3f}, "
          "\"rounds\": %llu, \"publishes_per_round\": %.0f, \"batches_per_round\": %.2f, "
          "\"expanded_batches\": %llu, \"device_record_batches\": %llu, \"state_retries\": %llu, "
          "\"stale_rematches\": %llu, \"overflow_retries\": %llu",
-         section, ranges ? "ranges" : "records", T, B, el, (unsigned long long)pubs, (unsigned long long)ents,
+         section, ranges ? "ranges" : "records", fold_spans ? "spans" : "entries", T, B, el, (unsigned long long)pubs, (unsigned long long)ents,
          pubs / el, ents / el, nb ? tp * 1e3 / nb : 0, nb ? tm * 1e3 / nb : 0, nb ? tf * 1e3 / nb : 0,
          (unsigned long long)rounds, rounds ? (double)(s1.round_publishes - s0.round_publishes) / rounds : 0.0,
          rounds ? (double)(s1.round_batches - s0.round_batches) / rounds : 0.0,
@@ -378,6 +390,18 @@ int main(int argc, char** argv) {
     for (int mode = 0; mode < 2 && !rc; mode++)
       for (size_t ti = 0; ti < sizeof threads_list / sizeof threads_list[0] && !rc; ti++)
         rc = run("scale", threads_list[ti], 4096, mode, secs, NULL, NULL);
+    /* the per-entry callback (the round-3 fold) beside it; bigger batches */
+    fold_spans = 0;
+    for (int mode = 0; mode < 2 && !rc; mode++) rc = run("scale", 16, 4096, mode, secs, NULL, NULL);
+    fold_spans = 1;
+    for (int mode = 0; mode < 2 && !rc; mode++)
+      for (int T = 16; T <= 32 && !rc; T += 16) rc = run("scale", T, 16384, mode, secs, NULL, NULL);
+  }
+  if (want(argc, argv, "inflight")) {   /* three rounds in the kernels at once instead of two */
+    vmqgb_view_set_inflight(view, 3);
+    for (int mode = 0; mode < 2 && !rc; mode++)
+      for (int T = 16; T <= 32 && !rc; T += 16) rc = run("inflight3", T, 4096, mode, secs, NULL, NULL);
+    vmqgb_view_set_inflight(view, 2);
   }
   if (want(argc, argv, "devrec") && !rc) {
     vmqgb_view_set_device_records(view, 1);

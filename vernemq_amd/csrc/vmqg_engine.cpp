@@ -970,6 +970,8 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     if (hipMemsetAsync(d_dd, 0, slots * 12, st) != hipSuccess) return VMQG_E_DEVICE;
     dd_slots = slots;
     dd_tag = 0;
+    // the tags restart: output-group slots of older calls must not carry one
+    if (d_groups && hipMemsetAsync(d_groups, 0, gs_slots * 256, st) != hipSuccess) return VMQG_E_DEVICE;
   }
   // output groups: 256-B slots, a 16th of the publishes (slots of older calls free by the same tag)
   const uint64_t gslots = next_pow2(std::max<uint64_t>(npub / 16, 1024));

@@ -31,14 +31,16 @@
 // larger) by the COUNT wave-tier launch; what overflows even those is walked
 // by one whole wave with bounded LDS buffers (flushing candidates into keys
 // and keys into output as they fill: only the frontier stack needs room,
-// bounded by the trie depth; tier 2 puts it in global memory).  EMIT walks
-// those again in a third phase of its own launch (records mode; range mode:
-// an EMIT wave-tier launch).  Remote nodes >= 64 go to a 4,096-bit set.  No
-// publish is refused.
+// bounded by the trie depth; tier 2 puts it in global memory).  The EMIT
+// tail launch walks those again and writes them (records and range mode
+// alike).  Remote nodes >= 64 go to a 4,096-bit set.  No publish is refused.
 //
-// Launches per batch: COUNT, COUNT's wave tier (reads its list length on the
-// device: empty = ~4 us), the one-launch chunk-total scan (decoupled
-// look-back), EMIT.  Output is either the 16-B records (lookup_subs +
+// Launches per batch: COUNT, COUNT's wave tier (deferred publishes and the
+// dedupe fixup; reads its list lengths on the device: empty = ~4 us), the
+// one-launch chunk-total scan (decoupled look-back), EMIT, the EMIT tail
+// (whole-wave walks, huge publishes, output groups, wide publishes; empty =
+// ~4 us).  Every hand-off of payload between workgroups crosses one of these
+// launch boundaries.  Output is either the 16-B records (lookup_subs +
 // fold__, :87-98) or, in range mode, one 8-B {record off, count} per
 // non-empty subscriber-list key plus {node, 0} per remote node.
 #include <hip/hip_ext.h>
@@ -1597,10 +1599,11 @@ void k_match_fast(MatchArgs a) {
 // EMIT: list 1).  With fast_g 4 the fast pass already had these lists: its
 // deferrals go straight to the whole-wave walk.
 //
-// EMIT: the whole-wave walks again (list 1); the wide publishes were written
-// by the fast EMIT launch's second phase.
+// EMIT tail: the whole-wave walks again (list 1), then the huge publishes
+// (every wave a segment of each), the output groups (a slot's members back
+// to back) and the wide publishes of the chunk masks (one per wave).
 #ifndef VMQG_TAIL_WPE
-#define VMQG_TAIL_WPE 8   // EMIT tail: asks for 8 waves per SIMD; gfx950 build: 96 VGPRs, no spills, 5 waves
+#define VMQG_TAIL_WPE 8   // EMIT tail: asks for 8 waves per SIMD; gfx950 build (round 4): 151 VGPRs, 3 waves (groups, huge, wide, walks in one loop)
 #endif
 template <int MODE, int OUT, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? VMQG_TAIL_WPE : 1)))

@@ -283,14 +283,18 @@ class RegGpuView:
         eoffs = np.concatenate([[0], np.cumsum(sums)])
         return out, eoffs.astype(np.uint64)
 
-    def decode(self, rec) -> object:
-        """One 16-B record -> the FoldFun entry term."""
+    def decode(self, rec, sub_term=None) -> object:
+        """One 16-B record -> the FoldFun entry term.  sub_term(id): the
+        SubscriberId term of an id the caller chose itself (a lean workload's
+        client index, workloads.Workload.client_term); default: this view's
+        subscriber interner."""
         kind, node = int(rec["kind_node"]) >> 24, int(rec["kind_node"]) & 0xFFFFFF
+        sub = sub_term or self.subscribers.terms.__getitem__
         if kind == _lib.EMIT_LOCAL:
-            return (self.subscribers.terms[rec["subscriber"]], self.subinfos.terms[rec["subinfo"]])
+            return (sub(int(rec["subscriber"])), self.subinfos.terms[rec["subinfo"]])
         if kind == _lib.EMIT_GROUP:
             return (self.nodes.terms[node], self._word_text[int(rec["group"])],
-                    self.subscribers.terms[rec["subscriber"]], self.subinfos.terms[rec["subinfo"]])
+                    sub(int(rec["subscriber"])), self.subinfos.terms[rec["subinfo"]])
         return self.nodes.terms[node]
 
     def fold_batch(self, pubs):
