@@ -259,3 +259,50 @@ def test_intern_reserved_words():
     assert list(ids) == [_lib.WORD_PLUS, _lib.WORD_HASH, _lib.WORD_SHARE, _lib.WORD_UNKNOWN]
     assert L.vmqg_intern_words(v.handle, blob, offs.ctypes.data, 4, 1, ids.ctypes.data) == 0
     assert ids[3] == 3
+
+
+def test_prepare_split_matches_a_plain_split():
+    """The prepare's word split (8 bytes at a time) and word keys (16-byte
+    loads that never cross into the next page past the topic) against a
+    plain bytes.split(b"/") + dictionary lookup: random topics over an
+    alphabet heavy in '/', '+', '#', NUL, 0x01 and 0x80+ bytes (the
+    zero-byte trick's false-positive cases), every length 1..80, and each
+    topic also placed so that it ends exactly at a page boundary."""
+    import random
+    from vernemq_amd.reg_view import RegGpuView
+    v = RegGpuView(device=-1)
+    r = random.Random(11)
+    alphabet = [b"/", b"/", b"/", b"a", b"b", b"\x00", b"\x01", b"\x2e", b"\x30", b"\x80", b"\xff", b"+", b"#"]
+    topics = []
+    for n in range(1, 81):
+        for _ in range(12):
+            t = b"".join(r.choice(alphabet) for _ in range(n))
+            if r.random() < 0.5:
+                t = t.replace(b"+", b"c").replace(b"#", b"d")
+            topics.append(t)
+    words = sorted({w for t in topics for w in t.split(b"/")})
+    v.intern_words(words[::2], create=True)   # half the words known
+    L = _lib.lib()
+    page = 4096
+    buf = np.zeros(4 * page, dtype=np.uint8)
+    base = (buf.ctypes.data + page - 1) // page * page
+    out = np.zeros(128, dtype=np.uint32)
+    for t in topics:
+        want_rc = _lib.E_INVAL if (b"+" in t or b"#" in t) else 0
+        parts = t.split(b"/")
+        want = v.intern_words(parts, create=False) if not want_rc else None
+        for where in ("heap", "page_end"):
+            if where == "heap":
+                ptr = ctypes.c_char_p(t)
+            else:
+                at = base + page - len(t)   # the topic's last byte is the page's last
+                ctypes.memmove(at, t, len(t))
+                ptr = ctypes.cast(ctypes.c_void_p(at), ctypes.c_char_p)
+            pub = _lib.Pub()
+            rc = L.vmqg_prepare_publish(v.handle, 0, ptr, len(t), out.ctypes.data, 128, ctypes.byref(pub))
+            assert rc == want_rc, (t, where, rc)
+            if rc:
+                continue
+            assert pub.nwords == len(parts), (t, where)
+            assert list(out[:pub.nwords]) == list(want), (t, where)
+            assert bool(pub.flags & _lib.PUB_DOLLAR) == t.startswith(b"$")

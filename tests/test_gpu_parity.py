@@ -1024,10 +1024,12 @@ def test_batch_dedupe_auto_mode_follows_the_repetition():
     v = prod.view
     orc = O.TrieOracle(node)
     evs = [("updated", ("", b"c%d" % j), None, [(node, True, [((b"d", b"%d" % j, b"#"), 1)])]) for j in range(3000)]
-    evs.append(("updated", ("", b"all"), None, [(node, True, [((b"d", b"+", b"t"), 0)])]))
+    evs += [("updated", ("", b"all%d" % k), None, [(node, True, [((b"d", b"+", b"t%d" % k), 0)])]) for k in range(20)]
     prod.apply(evs)
     orc.apply(evs)
-    distinct = [("", (b"d", b"%d" % j, b"t")) for j in range(60_000)]
+    # 60,000 distinct topics of known words only (publishes whose unknown
+    # words sit at the same places are one topic to the matcher: deduped)
+    distinct = [("", (b"d", b"%d" % (j % 3000), b"t%d" % (j // 3000))) for j in range(60_000)]
     arr, words = v.prepare(distinct)
     _, o1 = prod.match_arrays(arr, words)
     _, o1b = prod.match_arrays(arr, words)
@@ -1100,3 +1102,36 @@ def test_group_slots_of_older_calls_do_not_survive_a_tag_restart():
         for i in list(range(0, 1000, 37)) + [n - 1]:
             got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
             assert got == sorted(want_s), i
+
+
+def test_more_global_stack_walks_than_stacks():
+    """the EMIT tail borrows tier-2 global stacks from a bitmap
+    (o_waves of them) while its grid has far more waves.  4,096 publishes
+    of x^16 (each a 2^16-wide frontier walked by a whole wave with a global
+    stack, dedupe off so every one is walked) make more concurrent borrowers
+    than stacks: every count must be 65,536, sampled publishes must equal
+    the oracle, the call's status must be clean, and a second call must
+    succeed (the bitmap was released)."""
+    import itertools
+    node = "n@h"
+    prod = _driver(node)
+    v = prod.view
+    v.set_option("dedupe", 0)
+    orc = O.TrieOracle(node)
+    subs = [("updated", ("", b"s%d" % i), None, [(node, True, [(combo, i % 3)])])
+            for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=16))]
+    for lo in range(0, len(subs), 8192):
+        prod.apply(subs[lo:lo + 8192])
+        orc.apply(subs[lo:lo + 8192])
+    want = sorted(orc.fold_batch([("", b"pub", (b"x",) * 16)])[0])
+    arr, words = v.prepare([("", (b"x",) * 16)])
+    n = 4096
+    for call in range(2):
+        recs, offs = prod.match_arrays(arr[np.zeros(n, dtype=np.int64)], words)
+        assert np.array_equal(np.diff(offs.astype(np.int64)), np.full(n, 1 << 16)), call
+        for i in (0, 1, n // 2, n - 1):
+            got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
+            assert got == want, (call, i)
+        st = v.stats_raw()
+        assert st["deferred_tier2"] >= n, st
+        del recs

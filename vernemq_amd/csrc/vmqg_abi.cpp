@@ -67,6 +67,40 @@ int vmqg_intern_words(vmqg_ctx* ctx, const uint8_t* bytes, const uint64_t* offs,
   GUARD_END
 }
 
+// The words of a publish topic, 8 bytes at a time: on_word(start, len) per
+// '/'-separated word (empty words kept), false as soon as a '+' or '#'
+// appears (vmq_topic:validate_topic(publish, T), vmq_topic.erl:82-112).
+// Loads never cross into the next page past the topic's end.
+}  // extern "C"
+template <class F>
+static inline bool split_publish_topic(const uint8_t* p, size_t len, F&& on_word) {
+  constexpr uint64_t kOnes = 0x0101010101010101ull, kHigh = 0x8080808080808080ull;
+  size_t start = 0;
+  for (size_t i = 0; i < len; i += 8) {
+    const size_t m = len - i < 8 ? len - i : 8;
+    uint64_t x = 0;
+    if (m == 8 || (((uintptr_t)(p + i) & 4095) <= 4096 - 8)) memcpy(&x, p + i, 8);
+    else memcpy(&x, p + i, m);
+    const uint64_t valid = m == 8 ? ~0ull : ~0ull >> (64 - 8 * m);
+    auto eq = [x, valid](uint8_t c) {
+      const uint64_t y = x ^ (kOnes * c);
+      return (y - kOnes) & ~y & kHigh & valid;   // exact per byte below the first match, enough for "any"
+    };
+    if (eq('+') | eq('#')) return false;
+    for (uint64_t sl = eq('/'); sl; sl &= sl - 1) {
+      // the zero-byte trick can flag a false byte only above a true one:
+      // confirm each candidate separator
+      const size_t j = i + ((size_t)__builtin_ctzll(sl) >> 3);
+      if (p[j] != '/') continue;
+      on_word(start, j - start);
+      start = j + 1;
+    }
+  }
+  on_word(start, len - start);
+  return true;
+}
+extern "C" {
+
 // vmq_topic:validate_topic(publish, Topic)  (vmq_topic.erl:82-112): split on
 // '/', keep empty words, reject '+' / '#' anywhere, size 0 or > 65,536.
 int vmqg_prepare_publish(vmqg_ctx* ctx, uint32_t mountpoint, const uint8_t* topic, size_t len,
@@ -75,17 +109,15 @@ int vmqg_prepare_publish(vmqg_ctx* ctx, uint32_t mountpoint, const uint8_t* topi
   if (len == 0 || len > 65536) return VMQG_E_INVAL;
   GUARD_BEGIN
   uint32_t n = 0, unknown = 0;
-  size_t start = 0;
-  for (size_t i = 0; i <= len; i++) {
-    if (i < len && (topic[i] == '+' || topic[i] == '#')) return VMQG_E_INVAL;
-    if (i == len || topic[i] == '/') {
-      if (n >= cap) return VMQG_E_OVERFLOW;
-      const uint32_t id = ctx->e.intern(topic + start, i - start, false);
-      unknown |= id == vmqg::kUnknownWord;
-      words_out[n++] = id;
-      start = i + 1;
-    }
-  }
+  bool over = false;
+  const bool ok = split_publish_topic(topic, len, [&](size_t start, size_t wl) {
+    if (n >= cap) { over = true; return; }
+    const uint32_t id = ctx->e.intern(topic + start, wl, false);
+    unknown |= id == vmqg::kUnknownWord;
+    words_out[n++] = id;
+  });
+  if (!ok) return VMQG_E_INVAL;
+  if (over) return VMQG_E_OVERFLOW;
   pub->mountpoint = mountpoint;
   pub->word_off = 0;
   pub->nwords = n;
@@ -126,18 +158,11 @@ int vmqg_prepare_publishes(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints,
         if (nw + words > wcap) return VMQG_E_OVERFLOW;
       }
       const size_t k0 = keys.size();
-      size_t start = 0;
-      bool bad = false;
-      for (size_t i = 0; i <= len; i++) {
-        const uint8_t c = i < len ? tp[i] : '/';
-        if (c == '+' || c == '#') { bad = true; break; }
-        if (c == '/') {
-          keys.push_back(vmqg::WordDict::key(tp + start, i - start));
-          d.prefetch(keys.back());
-          words_out[nw + pub.nwords++] = (uint32_t)(keys.size() - 1);
-          start = i + 1;
-        }
-      }
+      const bool bad = !split_publish_topic(tp, len, [&](size_t start, size_t wl) {
+        keys.push_back(vmqg::WordDict::key(tp + start, wl));
+        d.prefetch(keys.back());
+        words_out[nw + pub.nwords++] = (uint32_t)(keys.size() - 1);
+      });
       if (bad) {
         keys.resize(k0);
         rc_out[t] = VMQG_E_INVAL;

@@ -126,10 +126,19 @@ class WordDict {
   struct Key { uint64_t h, k0, k1; const uint8_t* p; size_t n; };
   static Key key(const uint8_t* p, size_t n) {
     Key k{0, 0, 0, p, n};
-    uint8_t buf[16] = {0};
-    memcpy(buf, p, n < 16 ? n : 16);
-    memcpy(&k.k0, buf, 8);
-    memcpy(&k.k1, buf + 8, 8);
+    if (((uintptr_t)p & 4095) <= 4096 - 16) {
+      // 16 bytes readable without crossing a page: two loads, the bytes
+      // past the word masked off (the same zero padding as below)
+      memcpy(&k.k0, p, 8);
+      memcpy(&k.k1, p + 8, 8);
+      if (n < 8) { k.k0 &= n ? ~0ull >> (64 - 8 * n) : 0ull; k.k1 = 0; }
+      else if (n < 16) k.k1 &= n > 8 ? ~0ull >> (64 - 8 * (n - 8)) : 0ull;
+    } else {
+      uint8_t buf[16] = {0};
+      memcpy(buf, p, n < 16 ? n : 16);
+      memcpy(&k.k0, buf, 8);
+      memcpy(&k.k1, buf + 8, 8);
+    }
     uint64_t h = mix64(k.k0 ^ (0x9E3779B97F4A7C15ull * (n + 1))) ^ k.k1;
     for (size_t i = 16; i < n; i += 8) {
       uint64_t v = 0;
