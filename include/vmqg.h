@@ -142,9 +142,9 @@ typedef struct vmqg_stats_s {
   uint64_t image_bytes;     /*   full-image bytes shipped (re-layouts)           */
   uint64_t max_depth;       /* deepest trie path (levels)                       */
   /* ABI 3: how the last checked match batch was served                        */
-  uint64_t many_key;        /* wide publishes: more keys than the fast tier's   */
-                            /* lists or >= 256 records, written wave-wide by    */
-                            /* the fast EMIT launch's second phase (no walk)    */
+  uint64_t many_key;        /* wide publishes: more keys than the spill slots   */
+                            /* hold, written wave-wide by the EMIT tail launch  */
+                            /* from their candidates (no walk)                  */
   uint64_t retried;         /* publishes the one-lane fast pass could not hold, */
                             /* retried four lanes per publish (the rest of them */
                             /* are the deferred_tier1 walks)                    */
@@ -156,6 +156,9 @@ typedef struct vmqg_stats_s {
                             /* the batch walked: listed as its duplicates       */
   uint64_t dedup_walked;    /* of those, walked after all (representative       */
                             /* deferred, or a fingerprint collision)            */
+  uint64_t error_bits;      /* device error bits the last check collected: 2 a  */
+                            /* frontier stack overflowed or none was free, 4    */
+                            /* output overflow, 8 count mismatch, 16 look-back  */
 } vmqg_stats_t;
 
 /* ---- lifecycle ------------------------------------------------------- */
@@ -350,8 +353,8 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *                          defaults 4 and 16)
  *   "dedupe"    0 | 1 | 2  batch-wide dedupe of repeated (MP, topic) publishes in
  *                          COUNT: off, on, or auto (default: on while more than
- *                          one publish in five repeats another, judged on the
- *                          previous call — sampled on 1 chunk in 16 while off)
+ *                          half the publishes repeat another, judged on the
+ *                          previous call — sampled on 1 chunk in 64 while off)
  *   "groups"    0 | 1      records mode: publishes of >= 128 records grouped by what
  *                          they emit and written group by group by the EMIT tail
  *                          (default 1) */

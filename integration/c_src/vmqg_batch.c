@@ -369,6 +369,14 @@ int vmqgb_fold_spans(const vmqgb_batch* b, int ranges, const vmqg_emit* recs, ui
   return 0;
 }
 
+void vmqgb_prefetch_entries(const vmqgb_batch* b, int ranges, const vmqg_emit* recs, uint64_t nrecs, size_t i) {
+  if (!ranges || i >= b->n) return;
+  for (uint64_t k = b->offsets[i]; k < b->offsets[i + 1]; k++) {
+    const vmqg_range g = b->rng[k];
+    if (g.count && g.off < nrecs) __builtin_prefetch(recs + g.off);
+  }
+}
+
 /* ------------------------------------------------------------------- ops */
 int vmqgb_ops_init(vmqgb_ops* o) {
   memset(o, 0, sizeof(*o));

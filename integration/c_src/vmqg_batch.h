@@ -134,6 +134,13 @@ int vmqgb_fold_ranges(const vmqgb_batch* b, const vmqg_emit* recs, uint64_t nrec
 typedef int (*vmqgb_span_fn)(void* acc, const vmqg_emit* run, size_t n);
 int vmqgb_fold_spans(const vmqgb_batch* b, int ranges, const vmqg_emit* recs, uint64_t nrecs, size_t i,
                      vmqgb_span_fn fn, void* acc);
+/* Range mode: starts loading the first record of each of publish i's key
+ * ranges (a publish's own subscribers sit at a random place of the record
+ * table: one cache miss per range otherwise).  A fold loop calls it for
+ * publish i + VMQGB_PREFETCH_AHEAD before folding publish i.  No-op in
+ * records mode and past the batch. */
+void vmqgb_prefetch_entries(const vmqgb_batch* b, int ranges, const vmqg_emit* recs, uint64_t nrecs, size_t i);
+#define VMQGB_PREFETCH_AHEAD 16
 
 /* ---- subscription ops -------------------------------------------------- */
 typedef struct vmqgb_ops {

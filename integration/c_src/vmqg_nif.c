@@ -428,6 +428,8 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
       cnt = vmqgb_count_of(b, (size_t)idx[i]);
     }
     fold_acc acc = {env, r, (ERL_NIF_TERM*)enif_alloc((cnt ? cnt : 1) * sizeof(ERL_NIF_TERM)), 0};
+    if (i + VMQGB_PREFETCH_AHEAD < n && idx[i + VMQGB_PREFETCH_AHEAD] >= 0)
+      vmqgb_prefetch_entries(b, ranges, recs, nrecs, (size_t)idx[i + VMQGB_PREFETCH_AHEAD]);
     const int frc = vmqgb_fold_spans(b, ranges, recs, nrecs, (size_t)idx[i], make_entries, &acc);
     /* a fold that stops early (a range beyond the table) is this publish's error, never a partial list */
     res[i] = frc ? error_term(env, frc) : enif_make_tuple2(env, a_ok, enif_make_list_from_array(env, acc.out, (unsigned)acc.n));

@@ -1016,12 +1016,13 @@ def test_batch_dedupe_repeated_topics(mode, fast_g):
 
 
 def test_batch_dedupe_auto_mode_follows_the_repetition():
-    """dedupe 2 (the default): off while the sampled chunks show little
+    """dedupe 2 (auto): off while the sampled chunks show little
     repetition (a batch of distinct topics), on from the call after a batch
     that repeats — and the answers are the same either way."""
     node = "n@h"
     prod = _driver(node)
     v = prod.view
+    v.set_option("dedupe", 2)   # auto (the library default is off: DESIGN.md)
     orc = O.TrieOracle(node)
     evs = [("updated", ("", b"c%d" % j), None, [(node, True, [((b"d", b"%d" % j, b"#"), 1)])]) for j in range(3000)]
     evs += [("updated", ("", b"all%d" % k), None, [(node, True, [((b"d", b"+", b"t%d" % k), 0)])]) for k in range(20)]
@@ -1034,7 +1035,7 @@ def test_batch_dedupe_auto_mode_follows_the_repetition():
     _, o1 = prod.match_arrays(arr, words)
     _, o1b = prod.match_arrays(arr, words)
     assert v.stats_raw()["dedup"] == 0   # sampled, nothing repeats: stays off
-    rep = np.random.default_rng(3).integers(0, 500, 60_000)
+    rep = np.random.default_rng(3).integers(0, 100, 60_000)
     _, o2 = prod.match_arrays(arr[rep], words)      # sampled chunks see the repetition
     _, o3 = prod.match_arrays(arr[rep], words)      # ... so this call dedupes every chunk
     assert v.stats_raw()["dedup"] > 50_000
@@ -1086,6 +1087,7 @@ def test_group_slots_of_older_calls_do_not_survive_a_tag_restart():
     prod = _driver(node)
     v = prod.view
     v.set_option("dedupe", 0)
+    v.set_option("groups", 1)
     orc = O.TrieOracle(node)
     evs = [("updated", ("", b"g%d" % i), None, [(node, True, [((b"g", b"x"), i % 3)])]) for i in range(200)]
     for i, f in enumerate([(b"s", b"y"), (b"s", b"+"), (b"+", b"y")]):

@@ -39,6 +39,7 @@ VARIANTS = {
     "rt_tile2048": ["-DVMQR_TILE_ROWS=2048"],
     "rt_u2": ["-DVMQR_U=2"],
     "rt_u8": ["-DVMQR_U=8"],
+    "nofence": ["-DVMQG_STACK_FENCES=0"],
 }
 
 

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Retained-walk tile/unroll A/B (build/ab from tools/build_variants.py), the
 # retained parity tests on each variant, then rocprofv3 sessions (kernel
-# trace + PMC) of RT, SS and AC on the default build.
+# trace + PMC) of RT, AC and SS on the default build (build-tagged summaries).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/${1:-r03n}
+O=gpurun_out/${1:-r04rt}
 mkdir -p $O
 for v in default rt_tile256 rt_tile512 rt_tile2048 rt_u8 default; do
   so=build/ab/lib_$v.so
@@ -18,8 +18,8 @@ for v in rt_tile256 rt_tile512 rt_tile2048; do
   VMQG_LIB_PATH=build/ab/lib_$v.so timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_retain.py -m gpu > $O/tests_$v.log 2>&1 || { tail -30 $O/tests_$v.log; exit 3; }
   echo "$v tests: $(tail -1 $O/tests_$v.log)"
 done
-for c in RT AC; do
-  LITE=1 OUT=$O/prof_$c BENCH_ARGS="--config $c" TAG=r03_$c bash tools/profile_session.sh > $O/prof_$c.log 2>&1 || { tail -20 $O/prof_$c.log; exit 4; }
+for c in RT AC SS; do
+  LITE=1 OUT=$O/prof_$c BENCH_ARGS="--config $c" TAG=r04_$c bash tools/profile_session.sh > $O/prof_$c.log 2>&1 || { tail -20 $O/prof_$c.log; exit 4; }
   tail -3 $O/prof_$c.log
 done
 echo done

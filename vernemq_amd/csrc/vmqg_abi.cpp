@@ -1,5 +1,7 @@
 // extern "C" boundary of libvmqgpu (include/vmqg.h).  No C++ exception and
 // no torch type crosses it; every entry point maps onto the Engine.
+#include <sched.h>
+
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -285,11 +287,26 @@ struct vmqg_hbatch {
   uint64_t d_pubs_cap = 0, d_words_cap = 0, d_offs_cap = 0, d_out_cap = 0;   // bytes
   uint64_t want_entries = 0;   // output capacity (entries) of the next submit
   uint64_t out_entries = 0;    // ... of the submitted one
+  uint64_t spec_entries = 0;   // entries already copied back with the offsets (speculative D2H)
+  double per_pub = 2.0;        // entries per publish seen so far (sizes the speculative copy)
   size_t npub = 0, esz = 16;
   uint64_t epoch = 0, total = 0;
   bool frontier = false;
   int state = 0;               // 0 idle, 1 submitted, 2 offsets read
 };
+
+// Waits for a round's event by polling (with yields) for up to ~2 ms, then
+// blocking: an interrupt-driven wake-up costs tens of microseconds per round,
+// a poll of the completion signal under one; the poller yields its core to
+// the batchers that are preparing or folding.
+static hipError_t wait_event(hipEvent_t ev) {
+  for (int i = 0; i < 20000; i++) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q != hipErrorNotReady) return q;
+    sched_yield();
+  }
+  return hipEventSynchronize(ev);
+}
 
 static int grow_pinned(void** p, uint64_t* cap, uint64_t need) {
   if (*cap >= need) return VMQG_OK;
@@ -383,11 +400,19 @@ int vmqg_hbatch_submit(vmqg_ctx* ctx, vmqg_hbatch* hb, size_t npub, size_t nword
                       rec, rec ? hb->out_entries : 0, rng, rng ? hb->out_entries : 0, static_cast<uint64_t*>(hb->d_offs),
                       e.stream);
   if (rc) return rc;
-  // this match's offsets and error bits back, and the bits cleared for the next call
+  // this match's offsets and error bits back, and the bits cleared for the
+  // next call; with them, speculatively, as many entries as this hbatch's
+  // batches have had per publish (+ 25 %): when they all fit, the entries
+  // need no second round trip (one wait per round instead of two)
   uint32_t* d_err = e.d_status + 2 * Engine::kStatusSet;
+  hb->spec_entries = std::min<uint64_t>(hb->out_entries, (uint64_t)(hb->per_pub * 1.25 * (double)npub) + 256);
+  if ((rc = grow_pinned(&hb->h_out, &hb->h_out_cap, hb->spec_entries * esz + 16))) return rc;
   if (hipMemcpyAsync(hb->h_offs, hb->d_offs, (npub + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, e.stream) != hipSuccess ||
       hipMemcpyAsync(hb->h_err, d_err, 4, hipMemcpyDeviceToHost, e.stream) != hipSuccess ||
-      hipMemsetAsync(d_err, 0, 4, e.stream) != hipSuccess || hipEventRecord(hb->ev_k, e.stream) != hipSuccess)
+      hipMemsetAsync(d_err, 0, 4, e.stream) != hipSuccess ||
+      (hb->spec_entries &&
+       hipMemcpyAsync(hb->h_out, hb->d_out, hb->spec_entries * esz, hipMemcpyDeviceToHost, e.stream) != hipSuccess) ||
+      hipEventRecord(hb->ev_k, e.stream) != hipSuccess)
     return VMQG_E_DEVICE;
   hb->npub = npub;
   hb->epoch = e.epoch;
@@ -400,10 +425,11 @@ int vmqg_hbatch_offsets(vmqg_hbatch* hb, const uint64_t** offsets, uint64_t* tot
   if (!hb || hb->state == 0) return VMQG_E_INVAL;
   hipSetDevice(hb->device);
   if (hb->state == 1) {
-    if (hipEventSynchronize(hb->ev_k) != hipSuccess) { hb->state = 0; return VMQG_E_DEVICE; }
+    if (wait_event(hb->ev_k) != hipSuccess) { hb->state = 0; return VMQG_E_DEVICE; }
     hb->state = 2;
   }
   hb->total = hb->h_offs[hb->npub];
+  if (hb->npub) hb->per_pub = 0.75 * hb->per_pub + 0.25 * ((double)hb->total / (double)hb->npub);
   if (offsets) *offsets = hb->h_offs;
   if (total) *total = hb->total;
   if (epoch) *epoch = hb->epoch;
@@ -422,11 +448,24 @@ int vmqg_hbatch_entries(vmqg_hbatch* hb, const void** entries) {
   if (!hb || hb->state != 2) return VMQG_E_INVAL;
   hipSetDevice(hb->device);
   hb->state = 0;
-  int rc;
-  if ((rc = grow_pinned(&hb->h_out, &hb->h_out_cap, hb->total * hb->esz + 16))) return rc;
-  if (hb->total && (hipMemcpyAsync(hb->h_out, hb->d_out, hb->total * hb->esz, hipMemcpyDeviceToHost, hb->cs) != hipSuccess ||
-                    hipEventRecord(hb->ev_out, hb->cs) != hipSuccess || hipEventSynchronize(hb->ev_out) != hipSuccess))
-    return VMQG_E_DEVICE;
+  if (hb->total > hb->spec_entries) {   // the rest, behind the speculative part already here
+    const uint64_t have = hb->spec_entries;
+    if (hb->h_out_cap < hb->total * hb->esz + 16) {   // a larger pinned buffer: keep what arrived
+      void* nb = nullptr;
+      uint64_t ncap = 0;
+      int rc;
+      if ((rc = grow_pinned(&nb, &ncap, hb->total * hb->esz + 16))) return rc;
+      memcpy(nb, hb->h_out, have * hb->esz);
+      hipHostFree(hb->h_out);
+      hb->h_out = nb;
+      hb->h_out_cap = ncap;
+    }
+    char* dst = static_cast<char*>(hb->h_out) + have * hb->esz;
+    const char* src = static_cast<const char*>(hb->d_out) + have * hb->esz;
+    if (hipMemcpyAsync(dst, src, (hb->total - have) * hb->esz, hipMemcpyDeviceToHost, hb->cs) != hipSuccess ||
+        hipEventRecord(hb->ev_out, hb->cs) != hipSuccess || wait_event(hb->ev_out) != hipSuccess)
+      return VMQG_E_DEVICE;
+  }
   if (entries) *entries = hb->h_out;
   return VMQG_OK;
 }
@@ -520,6 +559,7 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->wide_entries = e.last_wide_entries;
   out->dedup = e.last_dedup;
   out->dedup_walked = e.last_dedup_walked;
+  out->error_bits = e.last_err_bits;
   return VMQG_OK;
 }
 

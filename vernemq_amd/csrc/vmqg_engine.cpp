@@ -1190,6 +1190,7 @@ int Engine::match_status(hipStream_t st) {
   last_dedup = c[8];
   last_dedup_walked = c[10];
   const uint32_t err = h[2 * kStatusSet];
+  last_err_bits = err;
   if (err && debug_limit() > 0) fprintf(stderr, "vmqg debug: match status error bits 0x%x\n", err);
   if (err & 2u) return VMQG_E_FRONTIER;
   if (err & 4u) return VMQG_E_OVERFLOW;

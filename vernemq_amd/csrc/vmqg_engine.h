@@ -300,9 +300,9 @@ struct Engine {
   uint64_t call_seq = 0; uint32_t last_set = 0;                // status set of the next / last match call
   void* d_keycache = nullptr; uint64_t keycache_cap = 0;   // publishes
   void* d_dd = nullptr; uint64_t dd_slots = 0; uint32_t dd_tag = 0;   // batch-wide dedupe table
-  uint32_t opt_dedupe = 2;                                 // vmqg_set_option "dedupe": 0 off, 1 on, 2 auto
+  uint32_t opt_dedupe = 0;                                 // vmqg_set_option "dedupe": 0 off (default: A/B, DESIGN), 1 on, 2 auto
   void* d_groups = nullptr; uint64_t gs_slots = 0;         // output groups (records mode)
-  uint32_t opt_groups = 1;                                 // vmqg_set_option "groups": 0 off, 1 on
+  uint32_t opt_groups = 0;                                 // vmqg_set_option "groups": 0 off (default: A/B, DESIGN), 1 on
   // host-buffer match staging
   void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
   void* d_words = nullptr; uint64_t d_words_cap = 0;
@@ -325,6 +325,7 @@ struct Engine {
   uint64_t last_wave_entries = 0;              // ... entries (records or ranges) the EMIT wave tier wrote
   uint64_t last_wide_entries = 0;              // ... entries the fast EMIT's wide phase wrote
   uint64_t last_dedup = 0, last_dedup_walked = 0;  // ... duplicates served from a representative / walked anyway
+  uint32_t last_err_bits = 0;   // error bits the last match_status collected
   // epoch of the last apply that rewrote a record slot (or re-laid out the
   // arena): range results of an older epoch index records that may have
   // changed (vmqg_records_at refuses them)

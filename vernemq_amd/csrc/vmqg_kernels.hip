@@ -81,11 +81,22 @@ constexpr uint32_t kMany = 0xFFFFFFFDu;     // key cache: more keys than the lis
 // publishes (records mode, >= kHugeRecords records: copied by every wave of
 // the EMIT tail, a segment each).
 constexpr uint32_t kLists = 5;
+// dedupe 2 (auto): while off, one chunk in kDdSampleEvery probes the table;
+// the next call dedupes every chunk when more than half the sampled
+// publishes repeated a topic (config E: 86 %; C: 20 %, its repeats being the
+// unknown-device publishes, cheap walks; D: 33 %)
+constexpr uint32_t kDdSampleEvery = 64;
 #ifndef VMQG_HUGE_RECORDS
 #define VMQG_HUGE_RECORDS 65536
 #endif
 constexpr uint32_t kHugeRecords = VMQG_HUGE_RECORDS;
 constexpr uint32_t kHugeFlag = 0x40000000u;  // key cache word 1 (nk <= 8): a huge publish, the tail copies it
+#ifndef VMQG_WALK_U
+#define VMQG_WALK_U 4   // records in flight per lane in a whole-wave walk's copy (8: the tail at 151 VGPRs, 3 waves/SIMD; 4: 128, 4)
+#endif
+#ifndef VMQG_TAIL_U
+#define VMQG_TAIL_U 8   // records in flight per lane in the tail's copies (wide, grouped, huge)
+#endif
 constexpr uint32_t kHugeSeg = 64 * 8 * 4;     // records per tail wave and segment
 // Output groups (records mode): publishes of >= kGroupMin records with <= 2
 // keys or wide are grouped by a signature of what they emit (key cache, or
@@ -623,6 +634,21 @@ __device__ bool dedupe_probe(const MatchArgs& a, uint64_t fp, uint32_t p, uint32
   return false;
 }
 
+// Output-group signatures: what a publish emits.  <= 2 keys: its key-cache
+// word {off0, c0, off1, c1} and remote mask; wide: its candidates, exact
+// key, remote mask and '$' flag (the order-relevant inputs of emit_many).
+__device__ __forceinline__ uint64_t group_sig_keys(uint4 w1, uint64_t rmask) {
+  return mix64(mix64(((uint64_t)w1.x << 32) | w1.y) ^ (((uint64_t)w1.z << 32) | w1.w)) ^ rmask;
+}
+template <class CandFn>
+__device__ __forceinline__ uint64_t group_sig_many(uint32_t ex_off, uint32_t ex_cnt, bool dollar, uint64_t rmask,
+                                                   uint32_t nc, CandFn cand) {
+  uint64_t sig = mix64(((uint64_t)ex_off << 32) ^ ex_cnt ^ ((uint64_t)dollar << 63));
+  sig = mix64(sig ^ rmask) ^ nc;
+  for (uint32_t i = 0; i < nc; i++) sig = mix64(sig + cand(i));
+  return sig;
+}
+
 // Joins publish p to the output group of signature `sig` (a slot with room,
 // or a new one claimed by CAS; full slots chain to the next).  One lane.
 __device__ bool group_insert(const MatchArgs& a, uint64_t sig64, uint32_t p) {
@@ -708,9 +734,8 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
     kc[1] = make_uint4(m.nc, m.ksum, m.ex_off, m.ex_cnt);
     fl = 1;
     if (OUT == 0 && total >= kGroupMin && a.groups) {   // an output group instead of the chunk mask: fl 5
-      uint64_t sig = mix64(((uint64_t)m.ex_off << 32) ^ m.ex_cnt ^ ((uint64_t)(pub.flags & VMQG_PUB_DOLLAR) << 63));
-      sig = mix64(sig ^ m.rmask) ^ m.nc;
-      for (uint32_t i = 0; i < m.nc; i++) sig = mix64(sig + s.cd(i));
+      const uint64_t sig = group_sig_many(m.ex_off, m.ex_cnt, (pub.flags & VMQG_PUB_DOLLAR) != 0, m.rmask, m.nc,
+                                          [&](uint32_t i) { return s.cd(i); });
       if (group_insert(a, sig, p)) fl = 5;
     }
   } else {
@@ -724,8 +749,7 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
       const uint2 k1 = m.nk > 1 ? s.ky(1) : make_uint2(0, m.ksum);
       const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
       const uint4 w1 = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
-      if (OUT == 0 && !huge && total >= kGroupMin && a.groups &&
-          group_insert(a, mix64(mix64(((uint64_t)w1.x << 32) | w1.y) ^ (((uint64_t)w1.z << 32) | w1.w)) ^ m.rmask, p)) {
+      if (OUT == 0 && !huge && total >= kGroupMin && a.groups && group_insert(a, group_sig_keys(w1, m.rmask), p)) {
         hf = kGroupFlag;   // the EMIT tail writes it with its output group: fl 6
         fl = 6;
       }
@@ -920,10 +944,11 @@ __device__ void emit_keys2(const MatchArgs& a, uint4 h, uint4 k1, uint64_t ob, u
   const uint32_t c0 = k1.y, ks = k1.y + k1.w;
   const uint64_t rm = ((uint64_t)h.w << 32) | h.z;
   const uint32_t tot = (uint32_t)(oe - ob);
-  for (uint32_t r0 = lane; r0 < tot; r0 += 64 * 8) {
-    uint4 v[8];
+  constexpr int U = VMQG_TAIL_U;
+  for (uint32_t r0 = lane; r0 < tot; r0 += 64 * U) {
+    uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < U; u++) {
       const uint32_t r = r0 + 64 * u;
       if (r < tot) {
         if (r < c0) v[u] = *reinterpret_cast<const uint4*>(a.records + k1.x + r);
@@ -932,7 +957,7 @@ __device__ void emit_keys2(const MatchArgs& a, uint4 h, uint4 k1, uint64_t ob, u
       }
     }
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < U; u++) {
       const uint32_t r = r0 + 64 * u;
       if (r < tot) store_rec<NT>(a.out, ob + r, v[u]);
     }
@@ -1076,9 +1101,6 @@ constexpr uint32_t kWStack = 256, kWCand = 256, kWKeys = 256, kHiWords = kMaxNod
 #define VMQG_WIDE_LANES 64   // lanes per wide publish in the EMIT tail (A/B, config D: 64 -> 2,606 us, 32 -> 3,056)
 #endif
 constexpr int kWideLanes = VMQG_WIDE_LANES;
-#ifndef VMQG_TAIL_U
-#define VMQG_TAIL_U 8   // records in flight per lane in the tail's wide copies
-#endif
 struct WaveLds {
   uint2 stack[kWStack];   // tier 1's frontier stack
   uint32_t cand[kWCand];  // candidate paths awaiting resolution
@@ -1134,7 +1156,7 @@ struct WaveWalk {
     }
     wave_sync();
     if (MODE == 1) {
-      constexpr int U = 8;
+      constexpr int U = VMQG_WALK_U;
       const uint32_t n = nk;
       auto ks = [&](uint32_t i) -> uint2 { return W.keys[i]; };
       for (uint32_t r0 = lane; r0 < tot; r0 += 64 * U) {
@@ -1294,6 +1316,26 @@ struct WaveWalk {
 // the second walk: claimed from the bitmap a.o_slots, released after.  A
 // wave that finds every stack taken waits for one; a holder is in the middle
 // of a walk, which never waits on anything, so it always comes back.
+//
+// A stack's bytes pass from holder to holder inside one launch, across XCDs
+// whose L2s are not coherent: a holder's dirty stack lines left in its XCD's
+// L2 could be written back to HBM AFTER the next holder (another XCD) wrote
+// the same addresses, and the next holder's re-read after an eviction would
+// see the old entries (test_more_global_stack_walks_than_stacks: 3,072
+// concurrent records-mode walks, 45 count mismatches without this).  So the
+// holder releases at agent scope (L2 write-back) before it clears its bit,
+// and the claimer acquires at agent scope (this CU's L1 invalidated) after
+// it set it (MI355X_MICROARCH.md, inter-workgroup visibility).
+#ifndef VMQG_STACK_FENCES
+#define VMQG_STACK_FENCES 1   // A/B only: 0 = the round-3 hand-off without fences (wrong under contention)
+#endif
+__device__ __forceinline__ void release_ostack(const MatchArgs& a, uint32_t slot) {
+  if (VMQG_STACK_FENCES) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  atomicAnd(a.o_slots + slot / 32, ~(1u << (slot % 32)));
+}
 __device__ uint32_t claim_ostack(const MatchArgs& a) {
   const uint32_t lane = __lane_id(), nw = (a.o_waves + 31) / 32;
   uint32_t slot = kNone;
@@ -1313,6 +1355,10 @@ __device__ uint32_t claim_ostack(const MatchArgs& a) {
         if (spins > (1u << 20)) break;   // none came back (never expected): the walk is refused loudly
         __builtin_amdgcn_s_sleep(8);
       }
+    }
+    if (VMQG_STACK_FENCES && slot != kNone) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
   return __shfl(slot, 0, 64);
@@ -1339,7 +1385,8 @@ __device__ __forceinline__ void wave_publish_body(const MatchArgs& a, WaveLds& W
       ok = w2.run_publish(p);
       total = w2.run;
     }
-    if (slot != kNone && lane == 0) atomicAnd(a.o_slots + slot / 32, ~(1u << (slot % 32)));
+    wave_sync();   // every lane's stack stores issued before the release
+    if (slot != kNone && lane == 0) release_ostack(a, slot);
     if (!ok && lane == 0) atomicOr(a.err, kErrFrontier);
   }
   if (ok && lane == 0) {
@@ -1414,12 +1461,13 @@ __device__ void count_deferred_group(const MatchArgs& a, const FastScratch<4, SL
 // The others — a representative deferred to this launch, or a fingerprint
 // collision — are returned compacted into the wave's lanes (`mine`, their
 // number returned) for the caller to walk like COUNT's deferred publishes.
+template <int OUT>
 __device__ uint32_t dedupe_fixup_slice(const MatchArgs& a, WaveLds& W, uint32_t base, uint32_t nd, uint32_t& mine) {
   const uint32_t lane = __lane_id();
   const uint32_t i = base + lane;
   const bool valid = i < nd;
   uint32_t p = 0;
-  bool ok = false;
+  bool ok = false, grouped = false;
   if (valid) {
     p = a.deferred[2ull * a.npub + i];
     const uint32_t slot = a.deferred[3ull * a.npub + i];
@@ -1433,7 +1481,13 @@ __device__ uint32_t dedupe_fixup_slice(const MatchArgs& a, WaveLds& W, uint32_t 
         uint4* pk = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
         uint4 h = rk[0];
         const uint4 k1 = rk[1];
-        if (h.y != kMany) h.y &= ~kGroupFlag;   // not a member of the representative's group: EMIT writes it
+        const uint64_t rmask = ((uint64_t)h.w << 32) | h.z;
+        if (h.y != kMany && (h.y & kGroupFlag)) {
+          // the representative's output group, found again by its signature
+          // (or EMIT writes the duplicate itself)
+          grouped = OUT == 0 && a.groups && group_insert(a, group_sig_keys(k1, rmask), p);
+          if (!grouped) h.y &= ~kGroupFlag;
+        }
         pk[0] = h;
         pk[1] = k1;
         // spilled keys (3..8) or a wide publish's candidate paths: 64 B
@@ -1446,12 +1500,22 @@ __device__ uint32_t dedupe_fixup_slice(const MatchArgs& a, WaveLds& W, uint32_t 
         }
         a.offsets[p] = h.x;
         atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)h.x);
-        if (h.y == kMany) atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + p / a.gpw), 1ull << (p % a.gpw));
-        else if (h.y & kHugeFlag) a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
+        if (h.y == kMany) {
+          if (OUT == 0 && a.groups && h.x >= kGroupMin) {
+            const uint32_t* cands = reinterpret_cast<const uint32_t*>(a.keyspill) + (uint64_t)p * 2 * kSpillKeys;
+            grouped = group_insert(a, group_sig_many(k1.z, k1.w, (P.flags & VMQG_PUB_DOLLAR) != 0, rmask, k1.x,
+                                                     [&](uint32_t c) { return cands[c]; }), p);
+          }
+          if (!grouped) atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + p / a.gpw), 1ull << (p % a.gpw));
+        } else if (h.y & kHugeFlag) {
+          a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
+        }
       }
     }
   }
-  const uint64_t many = __ballot(ok && reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2].y == kMany);
+  const uint32_t n_grp = (uint32_t)__popcll(__ballot(grouped));
+  if (lane == 0 && n_grp) atomicAdd(&a.status[kStGrouped], n_grp);
+  const uint64_t many = __ballot(ok && !grouped && reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2].y == kMany);
   const uint64_t walk = __ballot(valid && !ok);
   const uint32_t nw = (uint32_t)__popcll(walk);
   if (lane == 0) {
@@ -1501,7 +1565,7 @@ void k_match_fast(MatchArgs a) {
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
   // batch-wide dedupe (COUNT): a.dd_force 1 always, 0 never, 2 by the mode
-  // the previous call's fixup left (sampling 1 chunk in 16 while it is off)
+  // the previous call's fixup left (sampling 1 chunk in kDdSampleEvery while it is off)
   bool dd_all = false, dd_sample = false;
   if (MODE == 0 && a.dd_key) {
     const uint32_t mode = a.dd_force == 2 ? uni(*a.dd_mode) : a.dd_force;
@@ -1544,7 +1608,7 @@ void k_match_fast(MatchArgs a) {
       uint32_t fl = 0;
       // dedupe every chunk (mode on) or every 16th (sampling the batch's
       // repetition for the next call's mode, dedupe_fixup)
-      const bool dd = dd_all || (dd_sample && (base / GPW) % 16 == 0);
+      const bool dd = dd_all || (dd_sample && (base / GPW) % kDdSampleEvery == 0);
       uint32_t dslot = kNone;
       if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl, dd, &dslot);
       if (dd) {   // the chunk's duplicates into lists 2 / 3, one atomic per wave
@@ -1603,7 +1667,7 @@ void k_match_fast(MatchArgs a) {
 // (every wave a segment of each), the output groups (a slot's members back
 // to back) and the wide publishes of the chunk masks (one per wave).
 #ifndef VMQG_TAIL_WPE
-#define VMQG_TAIL_WPE 8   // EMIT tail: asks for 8 waves per SIMD; gfx950 build (round 4): 151 VGPRs, 3 waves (groups, huge, wide, walks in one loop)
+#define VMQG_TAIL_WPE 8   // EMIT tail: asks for 8 waves per SIMD; gfx950 build (round 4): 128 VGPRs, 4 waves (groups, huge, wide, walks in one kernel)
 #endif
 template <int MODE, int OUT, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? VMQG_TAIL_WPE : 1)))
@@ -1625,7 +1689,7 @@ void k_match_wave(MatchArgs a) {
     // on while more than one publish in five repeats another
     if (gw == 0 && lane == 0 && a.dd_key) {
       const uint32_t tried = a.status[kStDupTried], dups = a.status[kStDup];
-      if (tried >= 256) *a.dd_mode = dups * 5u > tried ? 1u : 0u;
+      if (tried >= 256) *a.dd_mode = dups * 2u > tried ? 1u : 0u;
     }
     // COUNT's deferred publishes (list 0), sixteen per wave, then the
     // duplicates the fixup could not serve, sixteen at a time (one call
@@ -1642,7 +1706,7 @@ void k_match_wave(MatchArgs a) {
         d0 += nwaves * GPW;
       } else {
         while (taken >= nmine && dbase < ndup) {
-          nmine = dedupe_fixup_slice(a, lds[wv], dbase, ndup, mine);
+          nmine = dedupe_fixup_slice<OUT>(a, lds[wv], dbase, ndup, mine);
           taken = 0;
           dbase += nwaves * 64;
         }
@@ -1698,15 +1762,16 @@ void k_match_wave(MatchArgs a) {
         for (uint64_t sg = gw; sg < nseg; sg += nwaves) {
           const uint64_t r0 = sg * kHugeSeg;
           const uint32_t n = (uint32_t)(total - r0 < kHugeSeg ? total - r0 : kHugeSeg);
-          for (uint32_t j = lane; j < n; j += 64 * 8) {
-            uint4 v[8];
+          constexpr int U = VMQG_TAIL_U;
+          for (uint32_t j = lane; j < n; j += 64 * U) {
+            uint4 v[U];
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
+            for (int u = 0; u < U; u++) {
               const uint32_t r = j + 64 * u;
               if (r < n) v[u] = emission(a, ks, nk == 0 ? 1u : nk, ksum, rmask, (uint32_t)(r0 + r));
             }
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
+            for (int u = 0; u < U; u++) {
               const uint32_t r = j + 64 * u;
               if (r < n) store_rec<NT>(a.out, ob + r0 + r, v[u]);
             }
