@@ -677,9 +677,23 @@ __device__ bool group_insert(const MatchArgs& a, uint64_t sig64, uint32_t p) {
   return false;   // no room: EMIT writes it as usual
 }
 
+// Block-level aggregation of COUNT's fast pass (one global atomic per block
+// and counter, not per wave or per publish: 16,384 waves adding to ONE word
+// take 200 us serialised on MI355X, spread over 64 words 9 us —
+// tools/atomic_probe.hip, profiles/atomic_probe_r04.jsonl).  The deferred
+// publishes are buffered in LDS and appended to list 0 with one atomic per
+// block at the end (a full buffer falls back to the global counter).
+constexpr uint32_t kDefBuf = 510;
+struct CountAgg {
+  uint32_t many, walkovf, grouped, tried;   // per-block sums of the status counters
+  uint32_t ndef, base;                      // buffered deferred publishes; their list-0 base
+  uint32_t def[kDefBuf];
+};
+
 template <int G, int OUT, bool RETRY = false, uint32_t SL = kWaves * (64 / G)>
 __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G, SL>& s, const Group<G>& g,
-                                  uint32_t& fl, bool dedupe = false, uint32_t* dslot = nullptr) {
+                                  uint32_t& fl, bool dedupe = false, uint32_t* dslot = nullptr,
+                                  CountAgg* agg = nullptr) {
   const vmqg_pub pub = a.pubs[p];
   if (dedupe) {
     // the same (MP, topic) walked by another publish of the batch: a
@@ -717,8 +731,13 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
   if (g.lane != 0) return 0;
   uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
   if (m.overflow) {   // a later tier counts it (and writes offsets[p])
-    const uint32_t idx = atomicAdd(&a.status[RETRY ? kStWalked : kStDeferred], 1u);
-    a.deferred[(RETRY ? (uint64_t)a.npub : 0ull) + idx] = p;   // each list holds npub entries
+    const uint32_t k = !RETRY && agg ? atomicAdd(&agg->ndef, 1u) : kDefBuf;   // LDS
+    if (k < kDefBuf) {
+      agg->def[k] = p;
+    } else {
+      const uint32_t idx = atomicAdd(&a.status[RETRY ? kStWalked : kStDeferred], 1u);
+      a.deferred[(RETRY ? (uint64_t)a.npub : 0ull) + idx] = p;   // each list holds npub entries
+    }
     a.offsets[p] = 0;
     kc[0] = make_uint4(0, kDeferred, 0, 0);
     fl = m.walk_ovf ? 2 : 3;
@@ -776,7 +795,8 @@ __device__ __forceinline__ uint64_t group_bits_to_publish_bits(uint64_t m) {
 }
 
 template <int G, bool RETRY>
-__device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t p) {
+__device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g, uint32_t fl, uint32_t p,
+                                          uint32_t* many = nullptr) {
   const bool w = g.lane == 0 && fl == 1;
   const uint64_t m_all = __ballot(w);
   const uint32_t c = p / a.gpw;
@@ -785,7 +805,7 @@ __device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g,
   } else if (__lane_id() == 0) {   // p: the wave's first publish; the chunk's mask stored whole
     a.widemask[c] = group_bits_to_publish_bits<G>(m_all);
   }
-  if (m_all && __lane_id() == 0) atomicAdd(&a.status[kStMany], (uint32_t)__popcll(m_all));
+  if (m_all && __lane_id() == 0) atomicAdd(many ? many : &a.status[kStMany], (uint32_t)__popcll(m_all));
 }
 
 // ------------------------------------------------------------- EMIT pass
@@ -1600,6 +1620,12 @@ void k_match_fast(MatchArgs a) {
     }
     return;
   }
+  __shared__ uint32_t agg_raw[MODE == 0 ? sizeof(CountAgg) / 4 : 1];
+  CountAgg* agg = MODE == 0 ? reinterpret_cast<CountAgg*>(agg_raw) : nullptr;
+  if (MODE == 0) {
+    if (threadIdx.x < 6) (&agg->many)[threadIdx.x] = 0;
+    __syncthreads();
+  }
   const uint32_t stride = gridDim.x * kWaves * GPW;
   for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
@@ -1610,12 +1636,12 @@ void k_match_fast(MatchArgs a) {
       // repetition for the next call's mode, dedupe_fixup)
       const bool dd = dd_all || (dd_sample && (base / GPW) % kDdSampleEvery == 0);
       uint32_t dslot = kNone;
-      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl, dd, &dslot);
+      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl, dd, &dslot, agg);
       if (dd) {   // the chunk's duplicates into lists 2 / 3, one atomic per wave
         const uint64_t tried = __ballot(g.gidx < n && g.lane == 0), dm = __ballot(g.gidx < n && g.lane == 0 && fl == 4);
         uint32_t at = 0;
         if (__lane_id() == 0) {
-          atomicAdd(&a.status[kStDupTried], (uint32_t)__popcll(tried));
+          atomicAdd(&agg->tried, (uint32_t)__popcll(tried));
           if (dm) at = atomicAdd(&a.status[kStDup], (uint32_t)__popcll(dm));
         }
         at = __shfl(at, 0, 64);
@@ -1629,14 +1655,15 @@ void k_match_fast(MatchArgs a) {
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
       // wide publishes: the chunk's mask for the EMIT tail launch
-      mark_wide<G, false>(a, g, fl, base);
+      mark_wide<G, false>(a, g, fl, base, &agg->many);
       const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
-      if (__lane_id() == 0 && n_wovf) atomicAdd(&a.status[kStWalkOvf], n_wovf);
+      if (__lane_id() == 0 && n_wovf) atomicAdd(&agg->walkovf, n_wovf);
       const uint32_t n_grp = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl >= 5));
-      if (__lane_id() == 0 && n_grp) atomicAdd(&a.status[kStGrouped], n_grp);
-      // served here (fast tier or wide): a duplicate of it may take its results
+      if (__lane_id() == 0 && n_grp) atomicAdd(&agg->grouped, n_grp);
+      // served here (fast tier or wide): a duplicate of it may take its
+      // results (only a deduped chunk can hold a representative)
       const uint64_t done = group_bits_to_publish_bits<G>(__ballot(g.gidx < n && g.lane == 0 && (fl <= 1 || fl >= 5)));
-      if (__lane_id() == 0) {
+      if (dd && __lane_id() == 0) {
         if (GPW == 64) { a.fastdone[base / 32] = (uint32_t)done; a.fastdone[base / 32 + 1] = (uint32_t)(done >> 32); }
         else if (GPW == 32) a.fastdone[base / 32] = (uint32_t)done;
         else reinterpret_cast<uint16_t*>(a.fastdone)[base / 16] = (uint16_t)done;
@@ -1649,6 +1676,17 @@ void k_match_fast(MatchArgs a) {
       if (g.gidx < n) emit_ranges_group<G>(a, base + g.gidx, s, g, ob, oe);
     }
     wave_sync();
+  }
+  if (MODE == 0) {   // the block's counters and deferred publishes, one global atomic each
+    __syncthreads();
+    const uint32_t nd = agg->ndef < kDefBuf ? agg->ndef : kDefBuf;
+    if (threadIdx.x == 0) agg->base = nd ? atomicAdd(&a.status[kStDeferred], nd) : 0u;
+    if (threadIdx.x == 64 && agg->many) atomicAdd(&a.status[kStMany], agg->many);
+    if (threadIdx.x == 128 && agg->walkovf) atomicAdd(&a.status[kStWalkOvf], agg->walkovf);
+    if (threadIdx.x == 192 && agg->grouped) atomicAdd(&a.status[kStGrouped], agg->grouped);
+    if (threadIdx.x == 1 && agg->tried) atomicAdd(&a.status[kStDupTried], agg->tried);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) a.deferred[agg->base + i] = agg->def[i];
   }
 }
 
@@ -1673,6 +1711,12 @@ template <int MODE, int OUT, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? VMQG_TAIL_WPE : 1)))
 void k_match_wave(MatchArgs a) {
   __shared__ WaveLds lds[kWaves];
+  __shared__ unsigned long long s_wsum;   // EMIT tail: the block's wide / grouped entries
+  __shared__ uint32_t s_wdone;            // ... and its waves done
+  if (MODE == 1) {
+    if (threadIdx.x == 0) { s_wsum = 0; s_wdone = 0; }
+    __syncthreads();
+  }
   const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
   const uint32_t nwaves = gridDim.x * kWaves;
@@ -1686,7 +1730,7 @@ void k_match_wave(MatchArgs a) {
     const Group<4> g;
     const FS s{st, cd, ky, wv * GPW + g.gidx};
     // block 0 sets the next call's dedupe mode from this call's counts:
-    // on while more than one publish in five repeats another
+    // on while more than half the sampled publishes repeat another
     if (gw == 0 && lane == 0 && a.dd_key) {
       const uint32_t tried = a.status[kStDupTried], dups = a.status[kStDup];
       if (tried >= 256) *a.dd_mode = dups * 2u > tried ? 1u : 0u;
@@ -1786,50 +1830,59 @@ void k_match_wave(MatchArgs a) {
     // masks COUNT left, at the positions EMIT wrote into offsets[]
     bool groups_on = OUT == 0 && uni(a.status[kStGrouped]) != 0;
     bool wide_on = uni(a.status[kStMany]) != 0;
-    if (!groups_on && !wide_on) return;
-    const GroupSlot* gs = reinterpret_cast<const GroupSlot*>(a.groups);
-    const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
-    uint64_t si = gw, cur = 0, m = 0, written = 0;
-    uint32_t j = 0, gn = 0, c = (uint32_t)gw, cc = 0;
-    for (;;) {
-      uint32_t p = 0;
-      bool have = false;
-      if (groups_on) {
-        while (j >= gn && si <= a.gs_mask) {
-          const unsigned long long w = uni64(gs[si].word);
-          gn = (w >> 40) == a.dd_tag ? (uint32_t)(w & 0xFF) : 0u;
-          j = 0;
-          cur = si;
-          si += nwaves;
+    uint64_t written = 0;
+    if (groups_on || wide_on) {
+      const GroupSlot* gs = reinterpret_cast<const GroupSlot*>(a.groups);
+      const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
+      uint64_t si = gw, cur = 0, m = 0;
+      uint32_t j = 0, gn = 0, c = (uint32_t)gw, cc = 0;
+      for (;;) {
+        uint32_t p = 0;
+        bool have = false;
+        if (groups_on) {
+          while (j >= gn && si <= a.gs_mask) {
+            const unsigned long long w = uni64(gs[si].word);
+            gn = (w >> 40) == a.dd_tag ? (uint32_t)(w & 0xFF) : 0u;
+            j = 0;
+            cur = si;
+            si += nwaves;
+          }
+          if (j < gn) { p = uni(gs[cur].m[j]); j++; have = true; }
+          else groups_on = false;
         }
-        if (j < gn) { p = uni(gs[cur].m[j]); j++; have = true; }
-        else groups_on = false;
-      }
-      if (!have && wide_on) {
-        while (m == 0 && c < nchunks) { m = uni64(a.widemask[c]); cc = c; c += nwaves; }
-        if (m) {
-          p = cc * a.gpw + (uint32_t)__builtin_ctzll(m);
-          m &= m - 1;
-          have = true;
-        } else {
-          wide_on = false;
+        if (!have && wide_on) {
+          while (m == 0 && c < nchunks) { m = uni64(a.widemask[c]); cc = c; c += nwaves; }
+          if (m) {
+            p = cc * a.gpw + (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            have = true;
+          } else {
+            wide_on = false;
+          }
         }
+        if (!have) break;
+        if (p >= a.npub) { if (lane == 0) atomicOr(a.err, kErrMismatch); continue; }
+        const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
+        if (oe > cap || ob > oe) {
+          if (lane == 0) atomicOr(a.err, kErrOverflow);
+          continue;
+        }
+        const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+        const uint4 h = kc[0], k1 = kc[1];
+        if (uni(h.y) == kMany) emit_many<OUT, NT, VMQG_TAIL_U, 64>(a, Group<64>(), true, p, ob, oe, lds[wv].keys);
+        else if (OUT == 0) emit_keys2<NT>(a, h, k1, ob, oe);
+        written += oe - ob;
+        wave_sync();
       }
-      if (!have) break;
-      if (p >= a.npub) { if (lane == 0) atomicOr(a.err, kErrMismatch); continue; }
-      const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
-      if (oe > cap || ob > oe) {
-        if (lane == 0) atomicOr(a.err, kErrOverflow);
-        continue;
-      }
-      const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
-      const uint4 h = kc[0], k1 = kc[1];
-      if (uni(h.y) == kMany) emit_many<OUT, NT, VMQG_TAIL_U, 64>(a, Group<64>(), true, p, ob, oe, lds[wv].keys);
-      else if (OUT == 0) emit_keys2<NT>(a, h, k1, ob, oe);
-      written += oe - ob;
-      wave_sync();
     }
-    if (written && lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), (unsigned long long)written);
+    // the block's entries in one global atomic (its last wave adds them)
+    if (lane == 0) {
+      if (written) __hip_atomic_fetch_add(&s_wsum, (unsigned long long)written, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (__hip_atomic_fetch_add(&s_wdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == kWaves - 1) {
+        const unsigned long long tot = __hip_atomic_load(&s_wsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(a.status + kStWideEnt), tot);
+      }
+    }
   }
 }
 
