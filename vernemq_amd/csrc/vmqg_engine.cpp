@@ -33,6 +33,7 @@ Engine::~Engine() {
     }
     hipFree(d_arena); hipFree(d_status); hipFree(d_deferred);
     hipFree(d_keycache); hipFree(d_dd); hipFree(d_groups);
+    if (h_ddmode) hipHostFree(h_ddmode);
     hipFree(d_lookback); hipFree(d_ostack);
     hipFree(d_pubs); hipFree(d_words); hipFree(d_offs); hipFree(d_out);
     if (stream) hipStreamDestroy(stream);
@@ -66,6 +67,12 @@ int Engine::init(const vmqg_config& c) {
     has_device = true;
     if (hipMalloc(&d_status, kStatusBytes) != hipSuccess) return VMQG_E_NOMEM;
     if (hipMemset(d_status, 0, kStatusBytes) != hipSuccess) return VMQG_E_DEVICE;
+    // the dedupe mode word the COUNT wave tier writes and the host reads
+    // before each call (whether to launch the claim pass)
+    if (hipHostMalloc((void**)&h_ddmode, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return VMQG_E_NOMEM;
+    *h_ddmode = 0;
+    if (hipHostGetDevicePointer((void**)&d_ddmode_host, h_ddmode, 0) != hipSuccess) return VMQG_E_DEVICE;
     for (Stage& sg : stage)
       if (hipEventCreateWithFlags(&sg.ev, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
     if (hipDeviceGetAttribute(&cu_count, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cu_count < 1)
@@ -952,7 +959,7 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     // 32-B key cache + kSpillKeys x 8-B spilled keys per publish, then the
     // chunk totals (one per 16, 32 or 64 publishes, + 1), per chunk a 64-bit
     // wide-publish mask, then one fast-pass bit per publish
-    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + 2 * (cap / 16 + 2) * 8 + (cap / 32 + 2) * 4) != hipSuccess)
+    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + 3 * (cap / 16 + 2) * 8 + (cap / 32 + 2) * 4) != hipSuccess)
       return VMQG_E_NOMEM;
     // publish lists: retry, whole-wave walks, duplicates, their slots, huge (vmqg_kernels.hip kLists)
     if (hipMalloc(&d_deferred, 5 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
@@ -1057,12 +1064,18 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.keyspill = reinterpret_cast<uint2*>(static_cast<char*>(d_keycache) + keycache_cap * 32);
   a.chunk = reinterpret_cast<uint64_t*>(static_cast<char*>(d_keycache) + keycache_cap * (32 + 8 * 8));
   a.widemask = a.chunk + (keycache_cap / 16 + 2);
-  a.fastdone = reinterpret_cast<uint32_t*>(a.widemask + (keycache_cap / 16 + 2));
+  a.ddmask = a.widemask + (keycache_cap / 16 + 2);
+  a.fastdone = reinterpret_cast<uint32_t*>(a.ddmask + (keycache_cap / 16 + 2));
   a.dd_key = static_cast<uint64_t*>(d_dd);
   a.dd_rep = reinterpret_cast<uint32_t*>(static_cast<char*>(d_dd) + dd_slots * 8);
   a.dd_mask = dd_slots - 1;
   a.dd_tag = dd_tag;
-  a.dd_force = opt_dedupe;
+  // dedupe: 1 on (claim pass + table reads), 2 auto: on while the last
+  // decision the device wrote to the host-mapped word says so, else the
+  // sampled CAS probe on one chunk in 64
+  a.dd_force = opt_dedupe == 2 ? (*reinterpret_cast<volatile uint32_t*>(h_ddmode) ? 1u : 2u) : opt_dedupe;
+  a.dd_claimed = a.dd_force == 1;
+  a.dd_host = d_ddmode_host;
   a.dd_mode = d_status + kStatusDdMode;
   a.groups = opt_groups ? d_groups : nullptr;
   a.gs_mask = gs_slots - 1;
@@ -1144,11 +1157,14 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   call_seq++;
   // kernel timing (vmqg_set_timing): events written by each dispatch itself
   // (hipExtLaunchKernel), so timing adds no marker packets between launches
-  std::array<hipEvent_t, 2 * kTimedStages> ev{};
+  std::array<hipEvent_t, 2 * kTimedEvents> ev{};
   if (timing) {
-    for (auto& e : ev) hipEventCreate(&e);
+    for (int k = 0; k < 2 * kTimedStages; k++) hipEventCreate(&ev[k]);
+    if (a.dd_claimed) { hipEventCreate(&ev[10]); hipEventCreate(&ev[11]); }
     t_ev.push_back(ev);
   }
+  // dedupe on: the claim pass fills the table COUNT reads (timed with COUNT)
+  if (a.dd_claimed && launch_dd_claim(a, st, ev[10], ev[11]) != hipSuccess) return VMQG_E_DEVICE;
   // COUNT: fast groups, then the wave tier for what they deferred
   if (launch_match(a, 0, 0, st, ev[0], ev[1]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "COUNT");
@@ -1203,10 +1219,10 @@ void Engine::collect_times() {
   hipSetDevice(device);
   for (auto& ev : t_ev) {
     hipEventSynchronize(ev[2 * kTimedStages - 1] ? ev[2 * kTimedStages - 1] : ev[2 * kTimedStages - 3]);
-    for (int k = 0; k < kTimedStages; k++) {
+    for (int k = 0; k < kTimedEvents; k++) {
       float ms = 0;
       if (ev[2 * k]) hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);   // null: the stage made no launch
-      sum_stage_ns[k] += ms * 1e6;
+      sum_stage_ns[k < kTimedStages ? k : 0] += ms * 1e6;   // the dedupe claim pass counts as COUNT
     }
     n_timed++;
     for (auto e : ev) if (e) hipEventDestroy(e);

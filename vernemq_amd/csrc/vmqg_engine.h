@@ -325,6 +325,8 @@ struct Engine {
   uint64_t last_wave_entries = 0;              // ... entries (records or ranges) the EMIT wave tier wrote
   uint64_t last_wide_entries = 0;              // ... entries the fast EMIT's wide phase wrote
   uint64_t last_dedup = 0, last_dedup_walked = 0;  // ... duplicates served from a representative / walked anyway
+  uint32_t* h_ddmode = nullptr;      // host-mapped dedupe mode word (written by the device)
+  uint32_t* d_ddmode_host = nullptr; // ... its device address
   uint32_t last_err_bits = 0;   // error bits the last match_status collected
   // epoch of the last apply that rewrote a record slot (or re-laid out the
   // arena): range results of an older epoch index records that may have
@@ -334,8 +336,8 @@ struct Engine {
   static constexpr uint32_t kStatusSet = 32, kStatusBytes = 512;
   static constexpr uint32_t kStatusDdMode = 100;   // persistent word: the dedupe mode the last call chose
   // per-launch timing: COUNT fast tier, COUNT wave tier, scan, EMIT fast tier, EMIT wave tier
-  static constexpr int kTimedStages = 5;
-  std::vector<std::array<hipEvent_t, 2 * kTimedStages>> t_ev;
+  static constexpr int kTimedStages = 5, kTimedEvents = 6;   // + the dedupe claim pass (summed into COUNT)
+  std::vector<std::array<hipEvent_t, 2 * kTimedEvents>> t_ev;
   double sum_stage_ns[kTimedStages] = {0, 0, 0, 0, 0}; uint64_t n_timed = 0;
 
   std::string dump_text;

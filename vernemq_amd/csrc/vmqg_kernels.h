@@ -49,6 +49,9 @@ struct MatchArgs {
   uint32_t* dd_mode;                              // persistent: the mode the last call's fixup chose
   uint32_t* fastdone;                             // bit per publish: served by COUNT's fast pass
   void* groups; uint64_t gs_mask;                 // output groups (records mode): 256-B slots, tagged by dd_tag
+  uint64_t* ddmask;                               // per chunk: its duplicates (COUNT -> the fix-up)
+  uint32_t dd_claimed, pad3;                      // this call's table was filled by k_dd_claim (read, no CAS)
+  uint32_t* dd_host;                              // host-mapped word: the dedupe mode for the next calls
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
@@ -62,5 +65,8 @@ hipError_t launch_match(const MatchArgs& a, int mode, int tier, hipStream_t st, 
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 uint32_t scan_tiles(uint64_t nchunks);   // look-back tiles of the chunk-total scan
 hipError_t launch_patches(uint8_t* arena, const void* d_patches, uint64_t n, hipStream_t st);
+// batch dedupe, mode on: every publish stores {tag | fingerprint, publish}
+// into its table slot (plain stores, the last writer wins) before COUNT
+hipError_t launch_dd_claim(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 
 }  // namespace vmqg

@@ -616,8 +616,11 @@ __device__ __forceinline__ void store_range(vmqg_range* out, uint64_t i, uint32_
 // another publish of this call holds the slot (p is its duplicate: the
 // fixup checks the words and takes the representative's results), false
 // when p claimed it (p represents the topic) or found no room.  One lane.
+__device__ __forceinline__ unsigned long long dd_key_of(const MatchArgs& a, uint64_t fp) {
+  return ((unsigned long long)a.dd_tag << 40) | (fp >> 24);
+}
 __device__ bool dedupe_probe(const MatchArgs& a, uint64_t fp, uint32_t p, uint32_t& slot) {
-  const unsigned long long key = ((unsigned long long)a.dd_tag << 40) | (fp >> 24);
+  const unsigned long long key = dd_key_of(a, fp);
   uint64_t i = fp & a.dd_mask;
   for (uint32_t probe = 0; probe < 32; probe++, i = (i + 1) & a.dd_mask) {
     unsigned long long* k = reinterpret_cast<unsigned long long*>(a.dd_key + i);
@@ -687,15 +690,19 @@ constexpr uint32_t kDefBuf = 510;
 struct CountAgg {
   uint32_t many, walkovf, grouped, tried;   // per-block sums of the status counters
   uint32_t ndef, base;                      // buffered deferred publishes; their list-0 base
+  uint32_t dups, pad;
   uint32_t def[kDefBuf];
 };
 
-template <int G, int OUT, bool RETRY = false, uint32_t SL = kWaves * (64 / G)>
+// FEAT: batch dedupe and output groups compiled in (the COUNT variant the
+// host picks when either is on: their code costs the lean variant scratch
+// spills, 79 -> 90 us on config C)
+template <int G, int OUT, bool RETRY = false, uint32_t SL = kWaves * (64 / G), bool FEAT = true>
 __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G, SL>& s, const Group<G>& g,
                                   uint32_t& fl, bool dedupe = false, uint32_t* dslot = nullptr,
                                   CountAgg* agg = nullptr) {
   const vmqg_pub pub = a.pubs[p];
-  if (dedupe) {
+  if (FEAT && dedupe) {
     // the same (MP, topic) walked by another publish of the batch: a
     // duplicate (fl 4), listed for the fixup, which gives it the
     // representative's key cache and count (the answer of one topic at one
@@ -704,7 +711,20 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
     const uint32_t wreg = g.lane < pub.nwords ? w[g.lane] : kUnknownWord;
     const uint64_t fp = publish_fp<G>(pub, w, wreg, g);
     uint32_t slot = kNone, dup = 0;
-    if (g.lane == 0 && pub.nwords > 0) dup = dedupe_probe(a, fp, p, slot);
+    if (g.lane == 0 && pub.nwords > 0 && pub.mountpoint < a.max_mp) {
+      if (a.dd_claimed) {
+        // k_dd_claim filled the table one launch ago: plain loads (a hot
+        // topic's slot stays in L2), no CAS.  The slot's last writer is the
+        // representative; a publish of another topic in the slot is walked.
+        const uint32_t i = (uint32_t)(fp & a.dd_mask);
+        if (a.dd_key[i] == dd_key_of(a, fp)) {
+          const uint32_t rep = a.dd_rep[i];
+          if (rep != p) { dup = 1; slot = i; }
+        }
+      } else {
+        dup = dedupe_probe(a, fp, p, slot);
+      }
+    }
     if (g.bcast(dup, 0)) {   // the caller lists it (one atomic per wave)
       fl = 4;
       *dslot = slot;
@@ -752,7 +772,7 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
     kc[0] = make_uint4(total, kMany, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
     kc[1] = make_uint4(m.nc, m.ksum, m.ex_off, m.ex_cnt);
     fl = 1;
-    if (OUT == 0 && total >= kGroupMin && a.groups) {   // an output group instead of the chunk mask: fl 5
+    if (FEAT && OUT == 0 && total >= kGroupMin && a.groups) {   // an output group instead of the chunk mask: fl 5
       const uint64_t sig = group_sig_many(m.ex_off, m.ex_cnt, (pub.flags & VMQG_PUB_DOLLAR) != 0, m.rmask, m.nc,
                                           [&](uint32_t i) { return s.cd(i); });
       if (group_insert(a, sig, p)) fl = 5;
@@ -768,7 +788,8 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
       const uint2 k1 = m.nk > 1 ? s.ky(1) : make_uint2(0, m.ksum);
       const uint32_t c0 = m.nk > 1 ? k1.y : m.ksum;
       const uint4 w1 = make_uint4(k0.x, c0, k1.x, m.ksum - c0);
-      if (OUT == 0 && !huge && total >= kGroupMin && a.groups && group_insert(a, group_sig_keys(w1, m.rmask), p)) {
+      if (FEAT && OUT == 0 && !huge && total >= kGroupMin && a.groups &&
+          group_insert(a, group_sig_keys(w1, m.rmask), p)) {
         hf = kGroupFlag;   // the EMIT tail writes it with its output group: fl 6
         fl = 6;
       }
@@ -1473,8 +1494,8 @@ __device__ void count_deferred_group(const MatchArgs& a, const FastScratch<4, SL
   }
 }
 
-// The duplicates COUNT listed (list 2, their table slots in list 3),
-// [base, base + 64) of them, one per lane: a duplicate whose representative
+// The duplicates of chunk c (its bits in a.ddmask, their table slots in list
+// 3 at the publish's index), one per lane: a duplicate whose representative
 // the fast pass served (its bit in a.fastdone, which nothing rewrites after
 // COUNT) and whose (MP, words) are the representative's takes its key cache
 // (+ spill slots), its count (added to its chunk's total) and its wide mark.
@@ -1482,15 +1503,17 @@ __device__ void count_deferred_group(const MatchArgs& a, const FastScratch<4, SL
 // collision — are returned compacted into the wave's lanes (`mine`, their
 // number returned) for the caller to walk like COUNT's deferred publishes.
 template <int OUT>
-__device__ uint32_t dedupe_fixup_slice(const MatchArgs& a, WaveLds& W, uint32_t base, uint32_t nd, uint32_t& mine) {
+__device__ uint32_t dedupe_fixup_chunk(const MatchArgs& a, WaveLds& W, uint32_t c, uint32_t& mine, uint32_t& n_many,
+                                       uint32_t& n_walked) {
   const uint32_t lane = __lane_id();
-  const uint32_t i = base + lane;
-  const bool valid = i < nd;
-  uint32_t p = 0;
+  const uint64_t dm = uni64(a.ddmask[c]);
+  uint32_t p = c * a.gpw + lane;
+  const bool valid = dm != 0 && lane < a.gpw && ((dm >> lane) & 1) && p < a.npub;
+  if (!valid) p = 0;
   bool ok = false, grouped = false;
+  uint64_t add = 0;
   if (valid) {
-    p = a.deferred[2ull * a.npub + i];
-    const uint32_t slot = a.deferred[3ull * a.npub + i];
+    const uint32_t slot = a.deferred[3ull * a.npub + p];
     const uint32_t rep = slot <= a.dd_mask ? a.dd_rep[slot] : kNone;
     if (rep < a.npub && rep != p && ((a.fastdone[rep / 32] >> (rep % 32)) & 1u)) {
       const vmqg_pub P = a.pubs[p], R = a.pubs[rep];
@@ -1519,7 +1542,7 @@ __device__ uint32_t dedupe_fixup_slice(const MatchArgs& a, WaveLds& W, uint32_t 
           for (int q = 0; q < 4; q++) ps[q] = rs[q];
         }
         a.offsets[p] = h.x;
-        atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)h.x);
+        add = h.x;   // the chunk's total: one atomic for the chunk, below
         if (h.y == kMany) {
           if (OUT == 0 && a.groups && h.x >= kGroupMin) {
             const uint32_t* cands = reinterpret_cast<const uint32_t*>(a.keyspill) + (uint64_t)p * 2 * kSpillKeys;
@@ -1533,15 +1556,15 @@ __device__ uint32_t dedupe_fixup_slice(const MatchArgs& a, WaveLds& W, uint32_t 
       }
     }
   }
+  const uint64_t tot = __shfl(wave_incl_scan64(add), 63, 64);
+  if (lane == 0 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + c), (unsigned long long)tot);
   const uint32_t n_grp = (uint32_t)__popcll(__ballot(grouped));
-  if (lane == 0 && n_grp) atomicAdd(&a.status[kStGrouped], n_grp);
+  if (lane == 0 && n_grp) atomicAdd(&a.status[kStGrouped], n_grp);   // output groups on only
   const uint64_t many = __ballot(ok && !grouped && reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2].y == kMany);
   const uint64_t walk = __ballot(valid && !ok);
   const uint32_t nw = (uint32_t)__popcll(walk);
-  if (lane == 0) {
-    if (many) atomicAdd(&a.status[kStMany], (uint32_t)__popcll(many));
-    if (nw) atomicAdd(&a.status[kStDupWalked], nw);
-  }
+  n_many += (uint32_t)__popcll(many);   // summed per block by the caller
+  n_walked += nw;
   if (valid && !ok) W.cand[prefix_bits(walk)] = p;
   wave_sync();
   mine = W.cand[lane];   // read out before any walk reuses the buffer
@@ -1564,7 +1587,7 @@ __device__ __forceinline__ void chunk_positions64(const MatchArgs& a, uint32_t f
   if (valid) a.offsets[first + lane] = pos;
 }
 
-template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
+template <int MODE, int OUT, int G, bool NT, int CH = 64 / G, bool FEAT = false>
 #ifndef VMQG_COUNT_WPE
 #define VMQG_COUNT_WPE 4    // COUNT waves per SIMD the register budget must allow, 2+ lanes per publish (A/B: 4, 5)
 #endif
@@ -1587,9 +1610,8 @@ void k_match_fast(MatchArgs a) {
   // batch-wide dedupe (COUNT): a.dd_force 1 always, 0 never, 2 by the mode
   // the previous call's fixup left (sampling 1 chunk in kDdSampleEvery while it is off)
   bool dd_all = false, dd_sample = false;
-  if (MODE == 0 && a.dd_key) {
-    const uint32_t mode = a.dd_force == 2 ? uni(*a.dd_mode) : a.dd_force;
-    dd_all = mode == 1;
+  if (FEAT && MODE == 0 && a.dd_key) {   // the host's choice for this call (vmqg_set_option "dedupe", dd_host)
+    dd_all = a.dd_force == 1;
     dd_sample = a.dd_force == 2;
   }
   // EMIT writes every publish resolve can serve; the wide ones (kResMany)
@@ -1623,7 +1645,7 @@ void k_match_fast(MatchArgs a) {
   __shared__ uint32_t agg_raw[MODE == 0 ? sizeof(CountAgg) / 4 : 1];
   CountAgg* agg = MODE == 0 ? reinterpret_cast<CountAgg*>(agg_raw) : nullptr;
   if (MODE == 0) {
-    if (threadIdx.x < 6) (&agg->many)[threadIdx.x] = 0;
+    if (threadIdx.x < 8) (&agg->many)[threadIdx.x] = 0;
     __syncthreads();
   }
   const uint32_t stride = gridDim.x * kWaves * GPW;
@@ -1636,21 +1658,20 @@ void k_match_fast(MatchArgs a) {
       // repetition for the next call's mode, dedupe_fixup)
       const bool dd = dd_all || (dd_sample && (base / GPW) % kDdSampleEvery == 0);
       uint32_t dslot = kNone;
-      if (g.gidx < n) c = count_publish<G, OUT>(a, base + g.gidx, s, g, fl, dd, &dslot, agg);
-      if (dd) {   // the chunk's duplicates into lists 2 / 3, one atomic per wave
-        const uint64_t tried = __ballot(g.gidx < n && g.lane == 0), dm = __ballot(g.gidx < n && g.lane == 0 && fl == 4);
-        uint32_t at = 0;
+      if (g.gidx < n) c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, base + g.gidx, s, g, fl, dd, &dslot, agg);
+      // the chunk's duplicates: a bit each in its chunk's mask, the table
+      // slot naming the representative at list 3 [publish] (no atomics)
+      uint64_t dm = 0;
+      if (dd) {
+        const uint64_t tried = __ballot(g.gidx < n && g.lane == 0);
+        dm = __ballot(g.gidx < n && g.lane == 0 && fl == 4);
         if (__lane_id() == 0) {
-          atomicAdd(&agg->tried, (uint32_t)__popcll(tried));
-          if (dm) at = atomicAdd(&a.status[kStDup], (uint32_t)__popcll(dm));
+          atomicAdd(&agg->tried, (uint32_t)__popcll(tried));   // LDS
+          if (dm) atomicAdd(&agg->dups, (uint32_t)__popcll(dm));
         }
-        at = __shfl(at, 0, 64);
-        if (g.gidx < n && g.lane == 0 && fl == 4) {
-          const uint32_t k = at + prefix_bits(dm);
-          a.deferred[2ull * a.npub + k] = base + g.gidx;
-          a.deferred[3ull * a.npub + k] = dslot;
-        }
+        if (g.gidx < n && g.lane == 0 && fl == 4) a.deferred[3ull * a.npub + base + g.gidx] = dslot;
       }
+      if (FEAT && __lane_id() == 0) a.ddmask[base / GPW] = group_bits_to_publish_bits<G>(dm);
       // the chunk's total (publishes the wave tier takes add theirs later)
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
@@ -1685,6 +1706,7 @@ void k_match_fast(MatchArgs a) {
     if (threadIdx.x == 128 && agg->walkovf) atomicAdd(&a.status[kStWalkOvf], agg->walkovf);
     if (threadIdx.x == 192 && agg->grouped) atomicAdd(&a.status[kStGrouped], agg->grouped);
     if (threadIdx.x == 1 && agg->tried) atomicAdd(&a.status[kStDupTried], agg->tried);
+    if (threadIdx.x == 2 && agg->dups) atomicAdd(&a.status[kStDup], agg->dups);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) a.deferred[agg->base + i] = agg->def[i];
   }
@@ -1712,11 +1734,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ?
 void k_match_wave(MatchArgs a) {
   __shared__ WaveLds lds[kWaves];
   __shared__ unsigned long long s_wsum;   // EMIT tail: the block's wide / grouped entries
-  __shared__ uint32_t s_wdone;            // ... and its waves done
-  if (MODE == 1) {
-    if (threadIdx.x == 0) { s_wsum = 0; s_wdone = 0; }
-    __syncthreads();
-  }
+  __shared__ uint32_t s_cnt[2];           // COUNT wave tier: the fix-up's wide / walked duplicates
+  __shared__ uint32_t s_wdone;            // the block's waves done (its last wave flushes the sums)
+  if (threadIdx.x == 0) { s_wsum = 0; s_cnt[0] = 0; s_cnt[1] = 0; s_wdone = 0; }
+  __syncthreads();
   const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
   const uint32_t nwaves = gridDim.x * kWaves;
@@ -1731,16 +1752,21 @@ void k_match_wave(MatchArgs a) {
     const FS s{st, cd, ky, wv * GPW + g.gidx};
     // block 0 sets the next call's dedupe mode from this call's counts:
     // on while more than half the sampled publishes repeat another
-    if (gw == 0 && lane == 0 && a.dd_key) {
+    if (gw == 0 && lane == 0 && a.dd_key && a.dd_force) {
       const uint32_t tried = a.status[kStDupTried], dups = a.status[kStDup];
-      if (tried >= 256) *a.dd_mode = dups * 2u > tried ? 1u : 0u;
+      if (tried >= 256) {
+        const uint32_t mode = dups * 2u > tried ? 1u : 0u;
+        *a.dd_mode = mode;
+        if (a.dd_host) *a.dd_host = mode;   // host-mapped: the host reads it before its next calls
+      }
     }
     // COUNT's deferred publishes (list 0), sixteen per wave, then the
     // duplicates the fixup could not serve, sixteen at a time (one call
     // site of the retry: the walk is inlined once)
     const uint32_t nd = uni(a.status[kStDeferred]), ndup = uni(a.status[kStDup]);
-    uint32_t d0 = (uint32_t)gw * GPW, dbase = (uint32_t)gw * 64;
-    uint32_t mine = 0, nmine = 0, taken = 0;
+    const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
+    uint32_t d0 = (uint32_t)gw * GPW, dchunk = ndup ? (uint32_t)gw : nchunks;
+    uint32_t mine = 0, nmine = 0, taken = 0, n_many = 0, n_walked = 0;
     for (;;) {
       bool valid;
       uint32_t p;
@@ -1749,10 +1775,10 @@ void k_match_wave(MatchArgs a) {
         p = a.deferred[valid ? d0 + g.gidx : 0];
         d0 += nwaves * GPW;
       } else {
-        while (taken >= nmine && dbase < ndup) {
-          nmine = dedupe_fixup_slice<OUT>(a, lds[wv], dbase, ndup, mine);
+        while (taken >= nmine && dchunk < nchunks) {
+          nmine = dedupe_fixup_chunk<OUT>(a, lds[wv], dchunk, mine, n_many, n_walked);
           taken = 0;
-          dbase += nwaves * 64;
+          dchunk += nwaves;
         }
         if (taken >= nmine) break;
         valid = taken + g.gidx < nmine;
@@ -1761,6 +1787,17 @@ void k_match_wave(MatchArgs a) {
       }
       count_deferred_group<OUT, NT>(a, s, g, lds[wv], gstack, valid, p);
       wave_sync();
+    }
+    // the fix-up's counters, summed per block (the block's last wave adds them)
+    if (lane == 0) {
+      if (n_many) atomicAdd(&s_cnt[0], n_many);
+      if (n_walked) atomicAdd(&s_cnt[1], n_walked);
+      if (__hip_atomic_fetch_add(&s_wdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == kWaves - 1) {
+        const uint32_t m = __hip_atomic_load(&s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t w = __hip_atomic_load(&s_cnt[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (m) atomicAdd(&a.status[kStMany], m);
+        if (w) atomicAdd(&a.status[kStDupWalked], w);
+      }
     }
     return;
   } else {
@@ -1951,8 +1988,40 @@ __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uin
   }
 }
 
+// ------------------------------------------------------------ dedupe claim
+// Batch dedupe with the mode on: every publish stores its key and its id
+// into its table slot with plain stores; within the launch the last writer
+// wins (per XCD L2, then at write-back), and COUNT — one launch later, so
+// every L2 sees the final table — reads the slot with plain loads: the last
+// writer represents its topic, a publish of another topic in the slot just
+// walks.  No atomics: a hot topic's slot is one line every publish of it
+// would otherwise CAS (tools/atomic_probe.hip: 16 hot slots, 1.2 ms per
+// 2^20 CAS; plain stores 7 us).
+__global__ __launch_bounds__(256) void k_dd_claim(MatchArgs a) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < a.npub; p += gridDim.x * blockDim.x) {
+    const vmqg_pub pub = a.pubs[p];
+    if (pub.nwords == 0 || pub.mountpoint >= a.max_mp) continue;
+    const uint32_t* w = a.words + pub.word_off;
+    uint64_t part = 0;
+    for (uint32_t i = 0; i < pub.nwords; i++) part += fp_word(w[i], i);
+    const uint64_t fp = fp_final(part, pub.mountpoint, pub.nwords);
+    const uint32_t i = (uint32_t)(fp & a.dd_mask);
+    a.dd_key[i] = dd_key_of(a, fp);
+    a.dd_rep[i] = p;
+  }
+}
+
 // ---------------------------------------------------------------- launch
 static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+hipError_t launch_dd_claim(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  uint32_t g = div_up(a.npub, 256);
+  if (g > a.cus * 8) g = a.cus * 8;
+  if (g < 1) g = 1;
+  if (t0) hipExtLaunchKernelGGL(k_dd_claim, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+  else k_dd_claim<<<g, 256, 0, st>>>(a);
+  return hipGetLastError();
+}
 
 hipError_t launch_scan(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   uint32_t g = scan_tiles((a.npub + a.gpw - 1) / a.gpw);
@@ -1964,6 +2033,14 @@ hipError_t launch_scan(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEve
 
 template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
 static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  // COUNT with dedupe or output groups on: the FEAT variant
+  if constexpr (MODE == 0) {
+    if (a.dd_force != 0 || a.groups != nullptr) {
+      if (t0) hipExtLaunchKernelGGL(k_match_fast<MODE, OUT, G, NT, CH, true>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+      else k_match_fast<MODE, OUT, G, NT, CH, true><<<g, 256, 0, st>>>(a);
+      return;
+    }
+  }
   if (t0) hipExtLaunchKernelGGL(k_match_fast<MODE, OUT, G, NT, CH>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
   else k_match_fast<MODE, OUT, G, NT, CH><<<g, 256, 0, st>>>(a);
 }
