@@ -150,7 +150,7 @@ typedef struct vmqg_stats_s {
                             /* are the deferred_tier1 walks)                    */
   uint64_t wave_entries;    /* entries (records or ranges) written by the EMIT  */
                             /* wave-tier launch (the whole-wave walks)          */
-  uint64_t wide_entries;    /* entries written by the wide phase                */
+  uint64_t wide_entries;    /* entries the EMIT tail wrote for wide publishes    */
   /* ABI 4: batch-wide dedupe of the last checked match batch                   */
   uint64_t dedup;           /* publishes whose (MP, topic) another publish of   */
                             /* the batch walked: listed as its duplicates       */
@@ -352,12 +352,14 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8;
  *                          defaults 4 and 16)
  *   "dedupe"    0 | 1 | 2  batch-wide dedupe of repeated (MP, topic) publishes in
- *                          COUNT: off, on, or auto (default: on while more than
- *                          half the publishes repeat another, judged on the
- *                          previous call — sampled on 1 chunk in 64 while off)
+ *                          COUNT: off (the default: it loses its A/B),
+ *                          on (a claim pass, then duplicates take their
+ *                          representative's result), or auto (on while more
+ *                          than half the publishes repeat another, judged on
+ *                          the previous calls — sampled on 1 chunk in 64 while off)
  *   "groups"    0 | 1      records mode: publishes of >= 128 records grouped by what
  *                          they emit and written group by group by the EMIT tail
- *                          (default 1) */
+ *                          (default 0: it loses its A/B) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the match kernels over the last

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Needs the session-a build in a worktree: git worktree add build/wt_a ba59b7f, then build its library there.)
 # Round 4: config C on the session-a build (worktree build/wt_a, commit
 # ba59b7f) and the current build, alternated on one box.
 set -o pipefail

@@ -18,6 +18,7 @@ for v in rt_tile256 rt_tile512 rt_tile2048; do
   VMQG_LIB_PATH=build/ab/lib_$v.so timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_retain.py -m gpu > $O/tests_$v.log 2>&1 || { tail -30 $O/tests_$v.log; exit 3; }
   echo "$v tests: $(tail -1 $O/tests_$v.log)"
 done
+[ -n "${NOPROF:-}" ] && { echo done; exit 0; }   # NOPROF=1: the A/B and tests only
 for c in RT AC SS; do
   LITE=1 OUT=$O/prof_$c BENCH_ARGS="--config $c" TAG=r04_$c bash tools/profile_session.sh > $O/prof_$c.log 2>&1 || { tail -20 $O/prof_$c.log; exit 4; }
   tail -3 $O/prof_$c.log

@@ -323,7 +323,7 @@ struct Engine {
   uint32_t last_deferred[2] = {0, 0};   // whole-wave walks (LDS / global stack) of the last checked batch
   uint32_t last_many = 0, last_retried = 0;    // ... many-key publishes / retried four lanes per publish
   uint64_t last_wave_entries = 0;              // ... entries (records or ranges) the EMIT wave tier wrote
-  uint64_t last_wide_entries = 0;              // ... entries the fast EMIT's wide phase wrote
+  uint64_t last_wide_entries = 0;              // ... entries the EMIT tail wrote for wide publishes
   uint64_t last_dedup = 0, last_dedup_walked = 0;  // ... duplicates served from a representative / walked anyway
   uint32_t* h_ddmode = nullptr;      // host-mapped dedupe mode word (written by the device)
   uint32_t* d_ddmode_host = nullptr; // ... its device address
