@@ -357,6 +357,7 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *                          representative's result), or auto (on while more
  *                          than half the publishes repeat another, judged on
  *                          the previous calls — sampled on 1 chunk in 64 while off)
+ *   "dd_g"      1 | 4      dedupe on: lanes per representative in COUNT (default 4)
  *   "groups"    0 | 1      records mode: publishes of >= 128 records grouped by what
  *                          they emit and written group by group by the EMIT tail
  *                          (default 0: it loses its A/B) */

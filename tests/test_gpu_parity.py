@@ -211,6 +211,7 @@ def test_wide_frontier_deferred_tiers(levels, tier, mode):
     import itertools
     node = "n@h"
     prod = _driver(node, mode)
+    prod.view.set_option("dedupe", 0)   # this test pins the deferral tiers' counters
     orc = O.TrieOracle(node)
     subs = []
     for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=levels)):
@@ -236,6 +237,7 @@ def test_frontier_2_16_is_answered():
     import itertools
     node = "n@h"
     prod = _driver(node)
+    prod.view.set_option("dedupe", 0)   # this test pins the deferral tiers' counters
     orc = O.TrieOracle(node)
     subs = [("updated", ("", b"s%d" % i), None, [(node, True, [(combo, i % 3)])])
             for i, combo in enumerate(itertools.product([b"x", b"+"], repeat=16))]
@@ -516,6 +518,7 @@ def test_output_offsets_of_a_large_deferral_heavy_batch(mode, fast_g):
     import itertools
     node = "n@h"
     prod = _driver(node, mode)
+    prod.view.set_option("dedupe", 0)   # this test pins the deferral tiers' counters
     prod.view.set_option("fast_g", fast_g)
     orc = O.TrieOracle(node)
     evs = []
@@ -603,6 +606,7 @@ def test_many_key_publishes_stay_in_the_fast_tier(mode, fast_g):
     with ordinary publishes in one batch."""
     node = "n0@h"
     prod = _driver(node, mode, nodes=[node] + ["n%d@h" % k for k in range(1, 8)])
+    prod.view.set_option("dedupe", 0)   # this test pins the deferral tiers' counters
     prod.view.set_option("fast_g", fast_g)
     orc = O.TrieOracle(node)
     evs = _many_key_events(node)
@@ -733,6 +737,7 @@ def test_retry_tier_serves_one_lane_overflows(mode, fast_g):
     import itertools
     node = "n@h"
     prod = _driver(node, mode)
+    prod.view.set_option("dedupe", 0)   # this test pins the deferral tiers' counters
     prod.view.set_option("fast_g", fast_g)
     orc = O.TrieOracle(node)
     evs = []
@@ -802,6 +807,7 @@ def test_wide_publishes_by_record_count(mode, fast_g):
     A/B in DESIGN.md), and every publish's records equal the oracle's."""
     node = "n@h"
     prod = _driver(node, mode)
+    prod.view.set_option("dedupe", 0)   # this test pins the deferral tiers' counters
     prod.view.set_option("fast_g", fast_g)
     orc = O.TrieOracle(node)
     sub = lambda cid, t, q: ("updated", ("", cid), None, [(node, True, [(t, q)])])
@@ -966,7 +972,8 @@ def test_config_e_scale_02_oracle_sample():
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("fast_g", [1, 2, 4])
-def test_batch_dedupe_repeated_topics(mode, fast_g):
+@pytest.mark.parametrize("dd_g", [1, 4])
+def test_batch_dedupe_repeated_topics(mode, fast_g, dd_g):
     """Batch-wide dedupe (verdict r3 item 4): 200,000 publishes drawn from 1,001
     topics — repeats across chunk and wave boundaries, many of them of
     h/x/y/z, which 31 filters match (deferred by the fast tier, so its
@@ -980,6 +987,7 @@ def test_batch_dedupe_repeated_topics(mode, fast_g):
     v = prod.view
     v.set_option("fast_g", fast_g)
     v.set_option("dedupe", 1)
+    v.set_option("dd_g", dd_g)
     orc = O.TrieOracle(node)
     evs = []
     hot = (b"h", b"x", b"y", b"z")
@@ -1011,18 +1019,19 @@ def test_batch_dedupe_repeated_topics(mode, fast_g):
         got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
         assert got == sorted(want[idx[i]]), i
     assert st["dedup"] > n // 2, st
-    if fast_g != 4:
+    if fast_g != 4 and dd_g == 1:
         assert st["dedup_walked"] > 0, st   # duplicates of the deferred h/x/y/z representatives
 
 
 def test_batch_dedupe_auto_mode_follows_the_repetition():
-    """dedupe 2 (auto): off while the sampled chunks show little
-    repetition (a batch of distinct topics), on from the call after a batch
-    that repeats — and the answers are the same either way."""
+    """dedupe 2 (auto): one call in 64 runs deduped to measure the batch's
+    repetition; the calls after it dedupe while more than half its publishes
+    repeat, and stop when a probe sees distinct topics — with the same
+    answers either way."""
     node = "n@h"
     prod = _driver(node)
     v = prod.view
-    v.set_option("dedupe", 2)   # auto (the library default is off: DESIGN.md)
+    v.set_option("dedupe", 2)
     orc = O.TrieOracle(node)
     evs = [("updated", ("", b"c%d" % j), None, [(node, True, [((b"d", b"%d" % j, b"#"), 1)])]) for j in range(3000)]
     evs += [("updated", ("", b"all%d" % k), None, [(node, True, [((b"d", b"+", b"t%d" % k), 0)])]) for k in range(20)]
@@ -1032,16 +1041,23 @@ def test_batch_dedupe_auto_mode_follows_the_repetition():
     # words sit at the same places are one topic to the matcher: deduped)
     distinct = [("", (b"d", b"%d" % (j % 3000), b"t%d" % (j // 3000))) for j in range(60_000)]
     arr, words = v.prepare(distinct)
-    _, o1 = prod.match_arrays(arr, words)
+    _, o1 = prod.match_arrays(arr, words)            # the first call is a probe: nothing repeats
+    assert v.stats_raw()["dedup"] == 0
     _, o1b = prod.match_arrays(arr, words)
-    assert v.stats_raw()["dedup"] == 0   # sampled, nothing repeats: stays off
-    rep = np.random.default_rng(3).integers(0, 100, 60_000)
-    _, o2 = prod.match_arrays(arr[rep], words)      # sampled chunks see the repetition
-    _, o3 = prod.match_arrays(arr[rep], words)      # ... so this call dedupes every chunk
-    assert v.stats_raw()["dedup"] > 50_000
     c1 = np.diff(o1.astype(np.int64))
     assert np.array_equal(c1, np.diff(o1b.astype(np.int64)))
-    assert np.array_equal(np.diff(o2.astype(np.int64)), c1[rep]) and np.array_equal(np.diff(o3.astype(np.int64)), c1[rep])
+    rep = np.random.default_rng(3).integers(0, 100, 60_000)
+    for _ in range(64):                              # one of these is a probe that sees the repetition
+        _, o2 = prod.match_arrays(arr[rep], words)
+        assert np.array_equal(np.diff(o2.astype(np.int64)), c1[rep])
+    _, o3 = prod.match_arrays(arr[rep], words)       # ... so this call dedupes
+    assert v.stats_raw()["dedup"] > 50_000
+    assert np.array_equal(np.diff(o3.astype(np.int64)), c1[rep])
+    for _ in range(64):                              # distinct topics again: a probe turns it off
+        prod.match_arrays(arr, words)
+    _, o4 = prod.match_arrays(arr, words)
+    assert v.stats_raw()["dedup"] == 0
+    assert np.array_equal(np.diff(o4.astype(np.int64)), c1)
     want = orc.fold_batch([(mp, b"pub", t) for mp, t in distinct[:3000]])
     assert np.array_equal(c1[:3000], [len(x) for x in want])
 
@@ -1137,3 +1153,29 @@ def test_more_global_stack_walks_than_stacks():
         st = v.stats_raw()
         assert st["deferred_tier2"] >= n, st
         del recs
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_dedupe_keeps_dollar_topics_apart(mode):
+    """z/b and $SYS/b carry the same word ids when neither first word is a
+    filter word (one unknown id), but '$SYS/b' must not match '+/b' or '#'
+    (MQTT-4.7.2-1, vmq_reg_trie.erl:457-462): dedupe must not make one the
+    other's duplicate, whichever order they come in."""
+    node = "n@h"
+    prod = _driver(node, mode)
+    v = prod.view
+    v.set_option("dedupe", 1)
+    orc = O.TrieOracle(node)
+    evs = [("updated", ("", b"w%d" % i), None, [(node, True, [(f, i % 3)])])
+           for i, f in enumerate([(b"+", b"b"), (b"#",), (b"q", b"b")])]
+    prod.apply(evs)
+    orc.apply(evs)
+    topics = [("", (b"z", b"b")), ("", (b"$SYS", b"b")), ("", (b"y", b"b")), ("", (b"$X", b"b"))]
+    want = [sorted(x) for x in orc.fold_batch([(mp, b"pub", t) for mp, t in topics])]
+    assert want[0] != want[1]
+    arr, words = v.prepare(topics)
+    for order in (np.arange(4000) % 4, (np.arange(4000) % 4)[::-1].copy()):
+        recs, offs = prod.match_arrays(arr[order], words)
+        for i in list(range(0, 4000, 7)) + list(range(3990, 4000)):
+            got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
+            assert got == want[order[i]], (i, topics[order[i]])

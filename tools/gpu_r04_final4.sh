@@ -12,3 +12,5 @@ timeout -k 10 300 tools/bin/nif_harness 3 scale churn load > $O/nif_harness.json
 for c in RT AC SS; do
   LITE=1 OUT=$O/prof_$c BENCH_ARGS="--config $c" TAG=r04_$c bash tools/profile_session.sh > $O/prof_$c.log 2>&1 || exit 4
 done
+# config D's line again, now that pmc_d.json is of this build (traffic reported)
+timeout -k 10 420 python -u bench.py --config D > $O/bench_D.json 2> $O/bench_D.err

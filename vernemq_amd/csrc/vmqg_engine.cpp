@@ -1070,11 +1070,27 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.dd_rep = reinterpret_cast<uint32_t*>(static_cast<char*>(d_dd) + dd_slots * 8);
   a.dd_mask = dd_slots - 1;
   a.dd_tag = dd_tag;
-  // dedupe: 1 on (claim pass + table reads), 2 auto: on while the last
-  // decision the device wrote to the host-mapped word says so, else the
-  // sampled CAS probe on one chunk in 64
-  a.dd_force = opt_dedupe == 2 ? (*reinterpret_cast<volatile uint32_t*>(h_ddmode) ? 1u : 2u) : opt_dedupe;
-  a.dd_claimed = a.dd_force == 1;
+  // dedupe: 1 on (claim + classify passes, COUNT walks the representatives
+  // only), 2 auto: on while the last decision the device wrote to the
+  // host-mapped word says so
+  // (auto: while off, a probe call runs deduped anyway to measure the
+  // repetition — the first call, then after 64, 128, ... up to 8,192 calls
+  // while the probes keep finding distinct topics)
+  bool claimed = opt_dedupe == 1;
+  if (opt_dedupe == 2) {
+    if (*reinterpret_cast<volatile uint32_t*>(h_ddmode)) {
+      claimed = true;
+      dd_gap = 64;
+      dd_next = call_seq + 64;
+    } else if (call_seq >= dd_next) {
+      claimed = true;
+      dd_next = call_seq + dd_gap;
+      dd_gap = std::min<uint64_t>(dd_gap * 2, 8192);
+    }
+  }
+  a.dd_force = claimed ? 1u : 0u;
+  a.dd_claimed = claimed;
+  a.dd_g = opt_dd_g;
   a.dd_host = d_ddmode_host;
   a.dd_mode = d_status + kStatusDdMode;
   a.groups = opt_groups ? d_groups : nullptr;
@@ -1160,13 +1176,17 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   std::array<hipEvent_t, 2 * kTimedEvents> ev{};
   if (timing) {
     for (int k = 0; k < 2 * kTimedStages; k++) hipEventCreate(&ev[k]);
-    if (a.dd_claimed) { hipEventCreate(&ev[10]); hipEventCreate(&ev[11]); }
+    if (a.dd_claimed) for (int k = 10; k < 16; k++) hipEventCreate(&ev[k]);
     t_ev.push_back(ev);
   }
-  // dedupe on: the claim pass fills the table COUNT reads (timed with COUNT)
-  if (a.dd_claimed && launch_dd_claim(a, st, ev[10], ev[11]) != hipSuccess) return VMQG_E_DEVICE;
-  // COUNT: fast groups, then the wave tier for what they deferred
+  // dedupe on: the claim and classify passes (timed with COUNT)
+  if (a.dd_claimed && (launch_dd_claim(a, st, ev[10], ev[11]) != hipSuccess ||
+                       launch_dd_classify(a, st, ev[12], ev[13]) != hipSuccess))
+    return VMQG_E_DEVICE;
+  // COUNT: fast groups (with dedupe on, the representatives, then the
+  // duplicates' fix-up), then the wave tier for what they deferred
   if (launch_match(a, 0, 0, st, ev[0], ev[1]) != hipSuccess) return VMQG_E_DEVICE;
+  if (a.dd_claimed && launch_dd_fixup(a, st, ev[14], ev[15]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "COUNT");
   if (launch_match(a, 0, 1, st, ev[2], ev[3]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "COUNT wave tier");

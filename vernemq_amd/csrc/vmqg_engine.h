@@ -300,8 +300,9 @@ struct Engine {
   uint64_t call_seq = 0; uint32_t last_set = 0;                // status set of the next / last match call
   void* d_keycache = nullptr; uint64_t keycache_cap = 0;   // publishes
   void* d_dd = nullptr; uint64_t dd_slots = 0; uint32_t dd_tag = 0;   // batch-wide dedupe table
-  uint32_t opt_dedupe = 0;                                 // vmqg_set_option "dedupe": 0 off (default: A/B, DESIGN), 1 on, 2 auto
+  uint32_t opt_dedupe = 2;                                 // vmqg_set_option "dedupe": 0 off, 1 on, 2 auto (default)
   void* d_groups = nullptr; uint64_t gs_slots = 0;         // output groups (records mode)
+  uint32_t opt_dd_g = 4;                                   // vmqg_set_option "dd_g": lanes per representative (1|4)
   uint32_t opt_groups = 0;                                 // vmqg_set_option "groups": 0 off (default: A/B, DESIGN), 1 on
   // host-buffer match staging
   void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
@@ -326,6 +327,7 @@ struct Engine {
   uint64_t last_wide_entries = 0;              // ... entries the EMIT tail wrote for wide publishes
   uint64_t last_dedup = 0, last_dedup_walked = 0;  // ... duplicates served from a representative / walked anyway
   uint32_t* h_ddmode = nullptr;      // host-mapped dedupe mode word (written by the device)
+  mutable uint64_t dd_next = 0, dd_gap = 64;   // auto dedupe: the next probe call, the gap after it
   uint32_t* d_ddmode_host = nullptr; // ... its device address
   uint32_t last_err_bits = 0;   // error bits the last match_status collected
   // epoch of the last apply that rewrote a record slot (or re-laid out the
@@ -336,7 +338,7 @@ struct Engine {
   static constexpr uint32_t kStatusSet = 32, kStatusBytes = 512;
   static constexpr uint32_t kStatusDdMode = 100;   // persistent word: the dedupe mode the last call chose
   // per-launch timing: COUNT fast tier, COUNT wave tier, scan, EMIT fast tier, EMIT wave tier
-  static constexpr int kTimedStages = 5, kTimedEvents = 6;   // + the dedupe claim pass (summed into COUNT)
+  static constexpr int kTimedStages = 5, kTimedEvents = 8;   // + the dedupe claim / classify / fix-up passes (into COUNT)
   std::vector<std::array<hipEvent_t, 2 * kTimedEvents>> t_ev;
   double sum_stage_ns[kTimedStages] = {0, 0, 0, 0, 0}; uint64_t n_timed = 0;
 

@@ -50,7 +50,7 @@ struct MatchArgs {
   uint32_t* fastdone;                             // bit per publish: served by COUNT's fast pass
   void* groups; uint64_t gs_mask;                 // output groups (records mode): 256-B slots, tagged by dd_tag
   uint64_t* ddmask;                               // per chunk: its duplicates (COUNT -> the fix-up)
-  uint32_t dd_claimed, pad3;                      // this call's table was filled by k_dd_claim (read, no CAS)
+  uint32_t dd_claimed, dd_g;                      // dedupe on this call; lanes per representative in COUNT (1|2|4)
   uint32_t* dd_host;                              // host-mapped word: the dedupe mode for the next calls
 };
 
@@ -68,5 +68,10 @@ hipError_t launch_patches(uint8_t* arena, const void* d_patches, uint64_t n, hip
 // batch dedupe, mode on: every publish stores {tag | fingerprint, publish}
 // into its table slot (plain stores, the last writer wins) before COUNT
 hipError_t launch_dd_claim(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+// ... then sorts the publishes into representatives (list 2, COUNT walks
+// them) and duplicates (chunk masks; their representative at list 3)
+hipError_t launch_dd_classify(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+// after COUNT: duplicates take their representative's results, or join list 0
+hipError_t launch_dd_fixup(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 
 }  // namespace vmqg

@@ -81,11 +81,6 @@ constexpr uint32_t kMany = 0xFFFFFFFDu;     // key cache: more keys than the lis
 // publishes (records mode, >= kHugeRecords records: copied by every wave of
 // the EMIT tail, a segment each).
 constexpr uint32_t kLists = 5;
-// dedupe 2 (auto): while off, one chunk in kDdSampleEvery probes the table;
-// the next call dedupes every chunk when more than half the sampled
-// publishes repeated a topic (config E: 86 %; C: 20 %, its repeats being the
-// unknown-device publishes, cheap walks; D: 33 %)
-constexpr uint32_t kDdSampleEvery = 64;
 #ifndef VMQG_HUGE_RECORDS
 #define VMQG_HUGE_RECORDS 65536
 #endif
@@ -131,6 +126,7 @@ enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, k
                   kStDupWalked = 10 /* duplicates walked after all (representative deferred / words differ) */,
                   kStHuge = 11 /* huge publishes listed for the tail */,
                   kStGrouped = 12 /* publishes in output groups */,
+                  kStReps = 13 /* dedupe on: publishes COUNT walks (list 2) */,
                   kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
 #define VMQG_WIDE_RECORDS 0x7fffffff   // A/B: a publish with at least this many records is wide too (256: config D 2,724 vs 2,526 us per batch, off)
@@ -610,31 +606,8 @@ __device__ __forceinline__ void store_range(vmqg_range* out, uint64_t i, uint32_
 // 0) says how it was served: 0 fast tier, 1 many-key mode, 2 deferred by a
 // walk overflow, 3 deferred otherwise (remote nodes >= 64).  Deferred
 // publishes go to list RETRY ? 2 (whole-wave walks) : 0 (the 4-lane retry).
-// Batch-wide dedupe: the slot of (MP, topic) in the call's dedupe table
-// (open addressing over 64-bit keys {call tag: 24, fingerprint bits: 40},
-// slots of older calls count as free), claimed by CAS.  Returns true when
-// another publish of this call holds the slot (p is its duplicate: the
-// fixup checks the words and takes the representative's results), false
-// when p claimed it (p represents the topic) or found no room.  One lane.
 __device__ __forceinline__ unsigned long long dd_key_of(const MatchArgs& a, uint64_t fp) {
   return ((unsigned long long)a.dd_tag << 40) | (fp >> 24);
-}
-__device__ bool dedupe_probe(const MatchArgs& a, uint64_t fp, uint32_t p, uint32_t& slot) {
-  const unsigned long long key = dd_key_of(a, fp);
-  uint64_t i = fp & a.dd_mask;
-  for (uint32_t probe = 0; probe < 32; probe++, i = (i + 1) & a.dd_mask) {
-    unsigned long long* k = reinterpret_cast<unsigned long long*>(a.dd_key + i);
-    unsigned long long cur = __hip_atomic_load(k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-      if (cur == key) { slot = (uint32_t)i; return true; }
-      if ((cur >> 40) == a.dd_tag) break;   // another topic of this call: the next slot
-      const unsigned long long prev = atomicCAS(k, cur, key);
-      if (prev == cur) { a.dd_rep[i] = p; slot = (uint32_t)i; return false; }
-      cur = prev;
-    }
-  }
-  slot = kNone;
-  return false;
 }
 
 // Output-group signatures: what a publish emits.  <= 2 keys: its key-cache
@@ -699,42 +672,8 @@ struct CountAgg {
 // spills, 79 -> 90 us on config C)
 template <int G, int OUT, bool RETRY = false, uint32_t SL = kWaves * (64 / G), bool FEAT = true>
 __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G, SL>& s, const Group<G>& g,
-                                  uint32_t& fl, bool dedupe = false, uint32_t* dslot = nullptr,
-                                  CountAgg* agg = nullptr) {
+                                  uint32_t& fl, CountAgg* agg = nullptr) {
   const vmqg_pub pub = a.pubs[p];
-  if (FEAT && dedupe) {
-    // the same (MP, topic) walked by another publish of the batch: a
-    // duplicate (fl 4), listed for the fixup, which gives it the
-    // representative's key cache and count (the answer of one topic at one
-    // epoch is one answer)
-    const uint32_t* w = a.words + pub.word_off;
-    const uint32_t wreg = g.lane < pub.nwords ? w[g.lane] : kUnknownWord;
-    const uint64_t fp = publish_fp<G>(pub, w, wreg, g);
-    uint32_t slot = kNone, dup = 0;
-    if (g.lane == 0 && pub.nwords > 0 && pub.mountpoint < a.max_mp) {
-      if (a.dd_claimed) {
-        // k_dd_claim filled the table one launch ago: plain loads (a hot
-        // topic's slot stays in L2), no CAS.  The slot's last writer is the
-        // representative; a publish of another topic in the slot is walked.
-        const uint32_t i = (uint32_t)(fp & a.dd_mask);
-        if (a.dd_key[i] == dd_key_of(a, fp)) {
-          const uint32_t rep = a.dd_rep[i];
-          if (rep != p) { dup = 1; slot = i; }
-        }
-      } else {
-        dup = dedupe_probe(a, fp, p, slot);
-      }
-    }
-    if (g.bcast(dup, 0)) {   // the caller lists it (one atomic per wave)
-      fl = 4;
-      *dslot = slot;
-      if (g.lane == 0) {
-        a.offsets[p] = 0;
-        reinterpret_cast<uint4*>(a.keycache)[(uint64_t)p * 2] = make_uint4(0, kDeferred, 0, 0);
-      }
-      return 0;
-    }
-  }
   const Matched m = walk_publish<G, SL>(a, pub, s, g);
   fl = 0;
   // wide publishes — more keys than the spill slots hold — are written by a
@@ -1494,83 +1433,6 @@ __device__ void count_deferred_group(const MatchArgs& a, const FastScratch<4, SL
   }
 }
 
-// The duplicates of chunk c (its bits in a.ddmask, their table slots in list
-// 3 at the publish's index), one per lane: a duplicate whose representative
-// the fast pass served (its bit in a.fastdone, which nothing rewrites after
-// COUNT) and whose (MP, words) are the representative's takes its key cache
-// (+ spill slots), its count (added to its chunk's total) and its wide mark.
-// The others — a representative deferred to this launch, or a fingerprint
-// collision — are returned compacted into the wave's lanes (`mine`, their
-// number returned) for the caller to walk like COUNT's deferred publishes.
-template <int OUT>
-__device__ uint32_t dedupe_fixup_chunk(const MatchArgs& a, WaveLds& W, uint32_t c, uint32_t& mine, uint32_t& n_many,
-                                       uint32_t& n_walked) {
-  const uint32_t lane = __lane_id();
-  const uint64_t dm = uni64(a.ddmask[c]);
-  uint32_t p = c * a.gpw + lane;
-  const bool valid = dm != 0 && lane < a.gpw && ((dm >> lane) & 1) && p < a.npub;
-  if (!valid) p = 0;
-  bool ok = false, grouped = false;
-  uint64_t add = 0;
-  if (valid) {
-    const uint32_t slot = a.deferred[3ull * a.npub + p];
-    const uint32_t rep = slot <= a.dd_mask ? a.dd_rep[slot] : kNone;
-    if (rep < a.npub && rep != p && ((a.fastdone[rep / 32] >> (rep % 32)) & 1u)) {
-      const vmqg_pub P = a.pubs[p], R = a.pubs[rep];
-      ok = P.mountpoint == R.mountpoint && P.nwords == R.nwords;
-      for (uint32_t k = 0; ok && k < P.nwords; k++) ok = a.words[P.word_off + k] == a.words[R.word_off + k];
-      if (ok) {
-        const uint4* rk = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)rep * 2;
-        uint4* pk = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
-        uint4 h = rk[0];
-        const uint4 k1 = rk[1];
-        const uint64_t rmask = ((uint64_t)h.w << 32) | h.z;
-        if (h.y != kMany && (h.y & kGroupFlag)) {
-          // the representative's output group, found again by its signature
-          // (or EMIT writes the duplicate itself)
-          grouped = OUT == 0 && a.groups && group_insert(a, group_sig_keys(k1, rmask), p);
-          if (!grouped) h.y &= ~kGroupFlag;
-        }
-        pk[0] = h;
-        pk[1] = k1;
-        // spilled keys (3..8) or a wide publish's candidate paths: 64 B
-        const uint32_t nkf = h.y == kMany ? 0u : h.y & ~kHugeFlag;
-        if (h.y == kMany || (nkf > 2 && nkf <= kSpillKeys)) {
-          const uint4* rs = reinterpret_cast<const uint4*>(a.keyspill + (uint64_t)rep * kSpillKeys);
-          uint4* ps = reinterpret_cast<uint4*>(a.keyspill + (uint64_t)p * kSpillKeys);
-#pragma unroll
-          for (int q = 0; q < 4; q++) ps[q] = rs[q];
-        }
-        a.offsets[p] = h.x;
-        add = h.x;   // the chunk's total: one atomic for the chunk, below
-        if (h.y == kMany) {
-          if (OUT == 0 && a.groups && h.x >= kGroupMin) {
-            const uint32_t* cands = reinterpret_cast<const uint32_t*>(a.keyspill) + (uint64_t)p * 2 * kSpillKeys;
-            grouped = group_insert(a, group_sig_many(k1.z, k1.w, (P.flags & VMQG_PUB_DOLLAR) != 0, rmask, k1.x,
-                                                     [&](uint32_t c) { return cands[c]; }), p);
-          }
-          if (!grouped) atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + p / a.gpw), 1ull << (p % a.gpw));
-        } else if (h.y & kHugeFlag) {
-          a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
-        }
-      }
-    }
-  }
-  const uint64_t tot = __shfl(wave_incl_scan64(add), 63, 64);
-  if (lane == 0 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + c), (unsigned long long)tot);
-  const uint32_t n_grp = (uint32_t)__popcll(__ballot(grouped));
-  if (lane == 0 && n_grp) atomicAdd(&a.status[kStGrouped], n_grp);   // output groups on only
-  const uint64_t many = __ballot(ok && !grouped && reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2].y == kMany);
-  const uint64_t walk = __ballot(valid && !ok);
-  const uint32_t nw = (uint32_t)__popcll(walk);
-  n_many += (uint32_t)__popcll(many);   // summed per block by the caller
-  n_walked += nw;
-  if (valid && !ok) W.cand[prefix_bits(walk)] = p;
-  wave_sync();
-  mine = W.cand[lane];   // read out before any walk reuses the buffer
-  wave_sync();
-  return uni(nw);
-}
 
 // --------------------------------------------------------------- kernels
 // Positions of the publishes of a 64-publish chunk (the chunks of a one-lane
@@ -1607,13 +1469,6 @@ void k_match_fast(MatchArgs a) {
   const Group<G> g;
   const uint32_t wv = threadIdx.x >> 6;
   const FS s{st, cd, ky, wv * GPW + g.gidx};
-  // batch-wide dedupe (COUNT): a.dd_force 1 always, 0 never, 2 by the mode
-  // the previous call's fixup left (sampling 1 chunk in kDdSampleEvery while it is off)
-  bool dd_all = false, dd_sample = false;
-  if (FEAT && MODE == 0 && a.dd_key) {   // the host's choice for this call (vmqg_set_option "dedupe", dd_host)
-    dd_all = a.dd_force == 1;
-    dd_sample = a.dd_force == 2;
-  }
   // EMIT writes every publish resolve can serve; the wide ones (kResMany)
   // and the whole-wave walks (kDeferred) are the EMIT tail launch's
   if constexpr (MODE == 1 && CH != GPW) {
@@ -1649,29 +1504,47 @@ void k_match_fast(MatchArgs a) {
     __syncthreads();
   }
   const uint32_t stride = gridDim.x * kWaves * GPW;
+  if constexpr (MODE == 0 && FEAT) {
+    if (a.dd_claimed) {
+      // batch dedupe on: only the representatives k_dd_classify listed (list
+      // 2), GPW per wave, dense; their chunks' totals, masks and fast-pass
+      // bits were zeroed by k_dd_claim and are accumulated here (atomics on
+      // one word per chunk, not one word for the launch)
+      const uint32_t nr = uni(a.status[kStReps]);
+      const uint32_t* R = a.deferred + 2ull * a.npub;
+      for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < nr; base += stride) {
+        const uint32_t n = nr - base < (uint32_t)GPW ? nr - base : (uint32_t)GPW;
+        uint32_t fl = 2, p = 0;
+        uint64_t c = 0;
+        if (g.gidx < n) {
+          p = R[base + g.gidx];
+          c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, p, s, g, fl, agg);
+        }
+        if (g.gidx < n && g.lane == 0) {
+          const uint32_t ch = p / a.gpw;
+          if (c) atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + ch), (unsigned long long)c);
+          if (fl <= 1 || fl >= 5) atomicOr(a.fastdone + p / 32, 1u << (p % 32));
+          if (fl == 1) atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + ch), 1ull << (p % a.gpw));
+        }
+        const uint32_t n_many = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl == 1));
+        const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl == 2));
+        const uint32_t n_grp = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl >= 5));
+        if (__lane_id() == 0) {
+          if (n_many) atomicAdd(&agg->many, n_many);
+          if (n_wovf) atomicAdd(&agg->walkovf, n_wovf);
+          if (n_grp) atomicAdd(&agg->grouped, n_grp);
+        }
+        wave_sync();
+      }
+    }
+  }
   for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < a.npub; base += stride) {
     const uint32_t n = a.npub - base < (uint32_t)GPW ? a.npub - base : (uint32_t)GPW;
     if (MODE == 0) {
+      if (FEAT && a.dd_claimed) break;   // the representatives' loop above did the work
       uint64_t c = 0;
       uint32_t fl = 0;
-      // dedupe every chunk (mode on) or every 16th (sampling the batch's
-      // repetition for the next call's mode, dedupe_fixup)
-      const bool dd = dd_all || (dd_sample && (base / GPW) % kDdSampleEvery == 0);
-      uint32_t dslot = kNone;
-      if (g.gidx < n) c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, base + g.gidx, s, g, fl, dd, &dslot, agg);
-      // the chunk's duplicates: a bit each in its chunk's mask, the table
-      // slot naming the representative at list 3 [publish] (no atomics)
-      uint64_t dm = 0;
-      if (dd) {
-        const uint64_t tried = __ballot(g.gidx < n && g.lane == 0);
-        dm = __ballot(g.gidx < n && g.lane == 0 && fl == 4);
-        if (__lane_id() == 0) {
-          atomicAdd(&agg->tried, (uint32_t)__popcll(tried));   // LDS
-          if (dm) atomicAdd(&agg->dups, (uint32_t)__popcll(dm));
-        }
-        if (g.gidx < n && g.lane == 0 && fl == 4) a.deferred[3ull * a.npub + base + g.gidx] = dslot;
-      }
-      if (FEAT && __lane_id() == 0) a.ddmask[base / GPW] = group_bits_to_publish_bits<G>(dm);
+      if (g.gidx < n) c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, base + g.gidx, s, g, fl, agg);
       // the chunk's total (publishes the wave tier takes add theirs later)
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
@@ -1681,14 +1554,6 @@ void k_match_fast(MatchArgs a) {
       if (__lane_id() == 0 && n_wovf) atomicAdd(&agg->walkovf, n_wovf);
       const uint32_t n_grp = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl >= 5));
       if (__lane_id() == 0 && n_grp) atomicAdd(&agg->grouped, n_grp);
-      // served here (fast tier or wide): a duplicate of it may take its
-      // results (only a deduped chunk can hold a representative)
-      const uint64_t done = group_bits_to_publish_bits<G>(__ballot(g.gidx < n && g.lane == 0 && (fl <= 1 || fl >= 5)));
-      if (dd && __lane_id() == 0) {
-        if (GPW == 64) { a.fastdone[base / 32] = (uint32_t)done; a.fastdone[base / 32 + 1] = (uint32_t)(done >> 32); }
-        else if (GPW == 32) a.fastdone[base / 32] = (uint32_t)done;
-        else reinterpret_cast<uint16_t*>(a.fastdone)[base / 16] = (uint16_t)done;
-      }
     } else if (OUT == 0) {
       emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
     } else {
@@ -1705,8 +1570,6 @@ void k_match_fast(MatchArgs a) {
     if (threadIdx.x == 64 && agg->many) atomicAdd(&a.status[kStMany], agg->many);
     if (threadIdx.x == 128 && agg->walkovf) atomicAdd(&a.status[kStWalkOvf], agg->walkovf);
     if (threadIdx.x == 192 && agg->grouped) atomicAdd(&a.status[kStGrouped], agg->grouped);
-    if (threadIdx.x == 1 && agg->tried) atomicAdd(&a.status[kStDupTried], agg->tried);
-    if (threadIdx.x == 2 && agg->dups) atomicAdd(&a.status[kStDup], agg->dups);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) a.deferred[agg->base + i] = agg->def[i];
   }
@@ -1734,9 +1597,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ?
 void k_match_wave(MatchArgs a) {
   __shared__ WaveLds lds[kWaves];
   __shared__ unsigned long long s_wsum;   // EMIT tail: the block's wide / grouped entries
-  __shared__ uint32_t s_cnt[2];           // COUNT wave tier: the fix-up's wide / walked duplicates
   __shared__ uint32_t s_wdone;            // the block's waves done (its last wave flushes the sums)
-  if (threadIdx.x == 0) { s_wsum = 0; s_cnt[0] = 0; s_cnt[1] = 0; s_wdone = 0; }
+  if (threadIdx.x == 0) { s_wsum = 0; s_wdone = 0; }
   __syncthreads();
   const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
   const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv;
@@ -1752,7 +1614,7 @@ void k_match_wave(MatchArgs a) {
     const FS s{st, cd, ky, wv * GPW + g.gidx};
     // block 0 sets the next call's dedupe mode from this call's counts:
     // on while more than half the sampled publishes repeat another
-    if (gw == 0 && lane == 0 && a.dd_key && a.dd_force) {
+    if (gw == 0 && lane == 0 && a.dd_claimed) {
       const uint32_t tried = a.status[kStDupTried], dups = a.status[kStDup];
       if (tried >= 256) {
         const uint32_t mode = dups * 2u > tried ? 1u : 0u;
@@ -1763,41 +1625,14 @@ void k_match_wave(MatchArgs a) {
     // COUNT's deferred publishes (list 0), sixteen per wave, then the
     // duplicates the fixup could not serve, sixteen at a time (one call
     // site of the retry: the walk is inlined once)
-    const uint32_t nd = uni(a.status[kStDeferred]), ndup = uni(a.status[kStDup]);
-    const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
-    uint32_t d0 = (uint32_t)gw * GPW, dchunk = ndup ? (uint32_t)gw : nchunks;
-    uint32_t mine = 0, nmine = 0, taken = 0, n_many = 0, n_walked = 0;
-    for (;;) {
-      bool valid;
-      uint32_t p;
-      if (d0 < nd) {
-        valid = d0 + g.gidx < nd;
-        p = a.deferred[valid ? d0 + g.gidx : 0];
-        d0 += nwaves * GPW;
-      } else {
-        while (taken >= nmine && dchunk < nchunks) {
-          nmine = dedupe_fixup_chunk<OUT>(a, lds[wv], dchunk, mine, n_many, n_walked);
-          taken = 0;
-          dchunk += nwaves;
-        }
-        if (taken >= nmine) break;
-        valid = taken + g.gidx < nmine;
-        p = __shfl(mine, (int)((taken + g.gidx) & 63), 64);
-        taken += GPW;
-      }
+    // (with dedupe on, k_dd_fixup appended the duplicates it could not
+    // serve to list 0: they are walked here like COUNT's own deferrals)
+    const uint32_t nd = uni(a.status[kStDeferred]);
+    for (uint32_t d0 = (uint32_t)gw * GPW; d0 < nd; d0 += nwaves * GPW) {
+      const bool valid = d0 + g.gidx < nd;
+      const uint32_t p = a.deferred[valid ? d0 + g.gidx : 0];
       count_deferred_group<OUT, NT>(a, s, g, lds[wv], gstack, valid, p);
       wave_sync();
-    }
-    // the fix-up's counters, summed per block (the block's last wave adds them)
-    if (lane == 0) {
-      if (n_many) atomicAdd(&s_cnt[0], n_many);
-      if (n_walked) atomicAdd(&s_cnt[1], n_walked);
-      if (__hip_atomic_fetch_add(&s_wdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == kWaves - 1) {
-        const uint32_t m = __hip_atomic_load(&s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t w = __hip_atomic_load(&s_cnt[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (m) atomicAdd(&a.status[kStMany], m);
-        if (w) atomicAdd(&a.status[kStDupWalked], w);
-      }
     }
     return;
   } else {
@@ -1999,6 +1834,14 @@ __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uin
 // 2^20 CAS; plain stores 7 us).
 __global__ __launch_bounds__(256) void k_dd_claim(MatchArgs a) {
   for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < a.npub; p += gridDim.x * blockDim.x) {
+    // COUNT accumulates the representatives' chunk totals, masks and bits
+    if (p % a.gpw == 0) {
+      const uint32_t c = p / a.gpw;
+      a.chunk[c] = 0;
+      a.widemask[c] = 0;
+      a.ddmask[c] = 0;
+    }
+    if (p % 32 == 0) a.fastdone[p / 32] = 0;
     const vmqg_pub pub = a.pubs[p];
     if (pub.nwords == 0 || pub.mountpoint >= a.max_mp) continue;
     const uint32_t* w = a.words + pub.word_off;
@@ -2011,8 +1854,186 @@ __global__ __launch_bounds__(256) void k_dd_claim(MatchArgs a) {
   }
 }
 
+// After the claim: each publish reads its slot (plain loads: a hot topic's
+// slot stays in L2).  The slot's last writer, or a publish whose slot holds
+// another topic, walks: it joins the representatives' list (list 2, dense,
+// buffered in LDS, one atomic per block); a publish whose words equal its
+// slot's writer's is a duplicate (a bit in its chunk's mask, the
+// representative at list 3 [publish]).  Each block takes one contiguous
+// range of publishes.
+constexpr uint32_t kClsBuf = 4096;
+__global__ __launch_bounds__(256) void k_dd_classify(MatchArgs a) {
+  __shared__ uint32_t buf[kClsBuf];
+  __shared__ uint32_t nbuf, dups, base;
+  if (threadIdx.x == 0) { nbuf = 0; dups = 0; }
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.status[kStDupTried] = a.npub;
+  __syncthreads();
+  const uint32_t per = (uint32_t)(((uint64_t)a.npub + gridDim.x - 1) / gridDim.x + 255) & ~255u;
+  const uint32_t lo = blockIdx.x * per, hi = lo + per < a.npub ? lo + per : a.npub;
+  for (uint32_t b0 = lo; b0 < hi; b0 += 256) {
+    const uint32_t p = b0 + threadIdx.x;
+    bool walk = false, dup = false;
+    uint32_t rep = kNone;
+    if (p < hi) {
+      const vmqg_pub pub = a.pubs[p];
+      walk = true;
+      if (pub.nwords > 0 && pub.mountpoint < a.max_mp) {
+        const uint32_t* w = a.words + pub.word_off;
+        uint64_t part = 0;
+        for (uint32_t i = 0; i < pub.nwords; i++) part += fp_word(w[i], i);
+        const uint64_t fp = fp_final(part, pub.mountpoint, pub.nwords);
+        const uint32_t i = (uint32_t)(fp & a.dd_mask);
+        if (a.dd_key[i] == dd_key_of(a, fp)) {
+          rep = a.dd_rep[i];
+          if (rep != p && rep < a.npub) {
+            // same MP, flags and word ids: the same answer (a word no filter
+            // has is one id, and only the '$' flag, which the ids do not
+            // carry, changes what the same ids match)
+            const vmqg_pub R = a.pubs[rep];
+            bool eq = R.mountpoint == pub.mountpoint && R.nwords == pub.nwords && R.flags == pub.flags;
+            for (uint32_t k = 0; eq && k < pub.nwords; k++) eq = a.words[R.word_off + k] == w[k];
+            dup = eq;
+            walk = !eq;
+          }
+        }
+      }
+    }
+    if (dup) {
+      a.deferred[3ull * a.npub + p] = rep;
+      atomicOr(reinterpret_cast<unsigned long long*>(a.ddmask + p / a.gpw), 1ull << (p % a.gpw));
+      atomicAdd(&dups, 1u);   // LDS
+    }
+    if (walk) {
+      const uint32_t k = atomicAdd(&nbuf, 1u);   // LDS
+      buf[k] = p;
+    }
+    __syncthreads();
+    if (nbuf + 256 > kClsBuf || b0 + 256 >= hi) {   // flush: one global atomic for the block
+      if (threadIdx.x == 0) base = nbuf ? atomicAdd(&a.status[kStReps], nbuf) : 0u;
+      __syncthreads();
+      for (uint32_t k = threadIdx.x; k < nbuf; k += blockDim.x) a.deferred[2ull * a.npub + base + k] = buf[k];
+      __syncthreads();
+      if (threadIdx.x == 0) nbuf = 0;
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0 && dups) atomicAdd(&a.status[kStDup], dups);
+}
+
+// After COUNT: every duplicate whose representative COUNT's fast pass
+// served takes its key cache, spill slots and count (one lane per publish,
+// one wave per 64 publishes, so the loads of many duplicates are in flight
+// at once); the others — their representative was deferred — join list 0,
+// which the COUNT wave tier walks like COUNT's own deferrals.
+template <int OUT>
+__global__ __launch_bounds__(256) void k_dd_fixup(MatchArgs a) {
+  __shared__ uint32_t buf[kDefBuf];
+  __shared__ uint32_t nbuf, base, n_many, n_walk, n_grp;
+  if (threadIdx.x == 0) { nbuf = 0; n_many = 0; n_walk = 0; n_grp = 0; }
+  __syncthreads();
+  const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+  const uint32_t stride = gridDim.x * kWaves * 64;
+  for (uint32_t b0 = (blockIdx.x * kWaves + wv) * 64; b0 < a.npub; b0 += stride) {
+    const uint32_t p = b0 + lane;
+    const bool valid = p < a.npub && ((a.ddmask[p / a.gpw] >> (p % a.gpw)) & 1);
+    bool ok = false, grouped = false, walk = false;
+    uint64_t add = 0;
+    if (valid) {
+      const uint32_t rep = a.deferred[3ull * a.npub + p];
+      ok = rep < a.npub && rep != p && ((a.fastdone[rep / 32] >> (rep % 32)) & 1u);
+      walk = !ok;
+      if (ok) {
+        const uint4* rk = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)rep * 2;
+        uint4* pk = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
+        uint4 h = rk[0];
+        const uint4 k1 = rk[1];
+        const uint64_t rmask = ((uint64_t)h.w << 32) | h.z;
+        if (h.y != kMany && (h.y & kGroupFlag)) {   // the representative's output group (groups on only)
+          grouped = OUT == 0 && a.groups && group_insert(a, group_sig_keys(k1, rmask), p);
+          if (!grouped) h.y &= ~kGroupFlag;
+        }
+        pk[0] = h;
+        pk[1] = k1;
+        const uint32_t nkf = h.y == kMany ? 0u : h.y & ~(kHugeFlag | kGroupFlag);
+        if (h.y == kMany || (nkf > 2 && nkf <= kSpillKeys)) {   // spilled keys or candidate paths: 64 B
+          const uint4* rs = reinterpret_cast<const uint4*>(a.keyspill + (uint64_t)rep * kSpillKeys);
+          uint4* ps = reinterpret_cast<uint4*>(a.keyspill + (uint64_t)p * kSpillKeys);
+#pragma unroll
+          for (int q = 0; q < 4; q++) ps[q] = rs[q];
+        }
+        a.offsets[p] = h.x;
+        add = h.x;
+        if (h.y == kMany) {
+          if (OUT == 0 && a.groups && h.x >= kGroupMin) {
+            const uint32_t* cands = reinterpret_cast<const uint32_t*>(a.keyspill) + (uint64_t)p * 2 * kSpillKeys;
+            grouped = group_insert(a, group_sig_many(k1.z, k1.w, (a.pubs[p].flags & VMQG_PUB_DOLLAR) != 0, rmask,
+                                                     k1.x, [&](uint32_t c) { return cands[c]; }), p);
+          }
+          if (!grouped) atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + p / a.gpw), 1ull << (p % a.gpw));
+        } else if (h.y & kHugeFlag) {
+          a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
+        }
+      } else {
+        a.offsets[p] = 0;
+        reinterpret_cast<uint4*>(a.keycache)[(uint64_t)p * 2] = make_uint4(0, kDeferred, 0, 0);
+      }
+    }
+    // the chunk totals: one atomic per chunk the wave covers
+    if (a.gpw == 64) {
+      const uint64_t tot = __shfl(wave_incl_scan64(add), 63, 64);
+      if (lane == 0 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + b0 / 64), (unsigned long long)tot);
+    } else if (add) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + p / a.gpw), (unsigned long long)add);
+    }
+    const uint32_t nm = (uint32_t)__popcll(__ballot(ok && !grouped && reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2].y == kMany));
+    const uint32_t ng = (uint32_t)__popcll(__ballot(grouped));
+    const uint64_t wm = __ballot(walk);
+    if (lane == 0) {
+      if (nm) atomicAdd(&n_many, nm);
+      if (ng) atomicAdd(&n_grp, ng);
+      if (wm) atomicAdd(&n_walk, (uint32_t)__popcll(wm));
+    }
+    if (walk) {   // to list 0 (LDS buffer; a full buffer goes straight to the global list)
+      const uint32_t k = atomicAdd(&nbuf, 1u);
+      if (k < kDefBuf) buf[k] = p;
+      else a.deferred[atomicAdd(&a.status[kStDeferred], 1u)] = p;
+    }
+  }
+  __syncthreads();
+  const uint32_t nd = nbuf < kDefBuf ? nbuf : kDefBuf;
+  if (threadIdx.x == 0) base = nd ? atomicAdd(&a.status[kStDeferred], nd) : 0u;
+  if (threadIdx.x == 64 && n_many) atomicAdd(&a.status[kStMany], n_many);
+  if (threadIdx.x == 128 && n_walk) atomicAdd(&a.status[kStDupWalked], n_walk);
+  if (threadIdx.x == 192 && n_grp) atomicAdd(&a.status[kStGrouped], n_grp);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) a.deferred[base + i] = buf[i];
+}
+
 // ---------------------------------------------------------------- launch
 static inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+hipError_t launch_dd_fixup(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  uint32_t g = div_up(a.npub, kWaves * 64);
+  if (g > (uint32_t)a.cus * 8) g = (uint32_t)a.cus * 8;
+  if (g < 1) g = 1;
+  if (a.out_rng) {
+    if (t0) hipExtLaunchKernelGGL(k_dd_fixup<1>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+    else k_dd_fixup<1><<<g, 256, 0, st>>>(a);
+  } else {
+    if (t0) hipExtLaunchKernelGGL(k_dd_fixup<0>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+    else k_dd_fixup<0><<<g, 256, 0, st>>>(a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_dd_classify(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  uint32_t g = a.cus * 8;   // one contiguous range of publishes per block: 8 blocks per CU
+  if (g > div_up(a.npub, 256)) g = div_up(a.npub, 256);
+  if (g < 1) g = 1;
+  if (t0) hipExtLaunchKernelGGL(k_dd_classify, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+  else k_dd_classify<<<g, 256, 0, st>>>(a);
+  return hipGetLastError();
+}
 
 hipError_t launch_dd_claim(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   uint32_t g = div_up(a.npub, 256);
@@ -2047,6 +2068,17 @@ static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEve
 
 template <int MODE, int OUT>
 static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  if (MODE == 0 && a.dd_claimed && a.dd_g == 4 && a.fast_g != 4) {
+    // dedupe on: the representatives are few, so COUNT gives each four lanes
+    // (more waves to hide each walk's dependent steps; lists 4x larger)
+    g = (uint32_t)((a.npub + kWaves * 16 - 1) / (kWaves * 16));
+    const uint32_t cap = (uint32_t)a.cus * (a.count_bpc ? a.count_bpc : 8u);
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    if (nt) launch_fast_k<0, OUT, 4, true>(a, g, st, t0, t1);
+    else launch_fast_k<0, OUT, 4, false>(a, g, st, t0, t1);
+    return;
+  }
   if (a.fast_g == 4) {
     if (nt) launch_fast_k<MODE, OUT, 4, true>(a, g, st, t0, t1);
     else launch_fast_k<MODE, OUT, 4, false>(a, g, st, t0, t1);
