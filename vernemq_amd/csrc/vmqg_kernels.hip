@@ -1627,10 +1627,15 @@ void k_match_wave(MatchArgs a) {
     // site of the retry: the walk is inlined once)
     // (with dedupe on, k_dd_fixup appended the duplicates it could not
     // serve to list 0: they are walked here like COUNT's own deferrals)
+    // A short list (no more publishes than waves) is mostly heavy
+    // publishes — what overflowed four lanes already (dedupe on) or a few
+    // wide frontiers: one per wave, so their whole-wave walks run side by
+    // side instead of one after another in the first few waves.
     const uint32_t nd = uni(a.status[kStDeferred]);
-    for (uint32_t d0 = (uint32_t)gw * GPW; d0 < nd; d0 += nwaves * GPW) {
-      const bool valid = d0 + g.gidx < nd;
-      const uint32_t p = a.deferred[valid ? d0 + g.gidx : 0];
+    const uint32_t per = nd <= nwaves ? 1u : GPW;
+    for (uint32_t d0 = (uint32_t)gw * per; d0 < nd; d0 += nwaves * per) {
+      const bool valid = g.gidx < per && d0 + g.gidx < nd;
+      const uint32_t p = a.deferred[valid ? d0 + g.gidx : d0];
       count_deferred_group<OUT, NT>(a, s, g, lds[wv], gstack, valid, p);
       wave_sync();
     }
