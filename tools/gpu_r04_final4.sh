@@ -14,3 +14,7 @@ for c in RT AC SS; do
 done
 # config D's line again, now that pmc_d.json is of this build (traffic reported)
 timeout -k 10 420 python -u bench.py --config D > $O/bench_D.json 2> $O/bench_D.err
+# config C's line again, now that pmc_latest.json is of this build (traffic reported)
+timeout -k 10 300 python -u bench.py > $O/bench_C.json 2> $O/bench_C.err
+# config E's line again, now that pmc_e.json is of this build (traffic reported)
+timeout -k 10 900 python -u bench.py --config E > $O/bench_E.json 2> $O/bench_E.err
