@@ -1828,6 +1828,31 @@ __global__ __launch_bounds__(256) void k_apply_patches(uint8_t* arena, const uin
   }
 }
 
+// One lane's fingerprint of its publish (claim / classify): the word loads
+// are issued four at a time, not one dependent round trip per level.
+__device__ __forceinline__ uint64_t lane_pub_fp(const MatchArgs& a, const vmqg_pub& pub) {
+  const uint32_t* w = a.words + pub.word_off;
+  const uint32_t n = pub.nwords;
+  uint64_t part = 0;
+  uint32_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    const uint32_t x0 = w[i], x1 = w[i + 1], x2 = w[i + 2], x3 = w[i + 3];
+    part += fp_word(x0, i) + fp_word(x1, i + 1) + fp_word(x2, i + 2) + fp_word(x3, i + 3);
+  }
+  for (; i < n; i++) part += fp_word(w[i], i);
+  return fp_final(part, pub.mountpoint, n);
+}
+
+// Two publishes' word ids equal (four loads in flight per step).
+__device__ __forceinline__ bool lane_words_equal(const uint32_t* x, const uint32_t* y, uint32_t n) {
+  bool eq = true;
+  uint32_t k = 0;
+  for (; eq && k + 4 <= n; k += 4)
+    eq = ((x[k] ^ y[k]) | (x[k + 1] ^ y[k + 1]) | (x[k + 2] ^ y[k + 2]) | (x[k + 3] ^ y[k + 3])) == 0;
+  for (; eq && k < n; k++) eq = x[k] == y[k];
+  return eq;
+}
+
 // ------------------------------------------------------------ dedupe claim
 // Batch dedupe with the mode on: every publish stores its key and its id
 // into its table slot with plain stores; within the launch the last writer
@@ -1849,10 +1874,7 @@ __global__ __launch_bounds__(256) void k_dd_claim(MatchArgs a) {
     if (p % 32 == 0) a.fastdone[p / 32] = 0;
     const vmqg_pub pub = a.pubs[p];
     if (pub.nwords == 0 || pub.mountpoint >= a.max_mp) continue;
-    const uint32_t* w = a.words + pub.word_off;
-    uint64_t part = 0;
-    for (uint32_t i = 0; i < pub.nwords; i++) part += fp_word(w[i], i);
-    const uint64_t fp = fp_final(part, pub.mountpoint, pub.nwords);
+    const uint64_t fp = lane_pub_fp(a, pub);
     const uint32_t i = (uint32_t)(fp & a.dd_mask);
     a.dd_key[i] = dd_key_of(a, fp);
     a.dd_rep[i] = p;
@@ -1883,10 +1905,7 @@ __global__ __launch_bounds__(256) void k_dd_classify(MatchArgs a) {
       const vmqg_pub pub = a.pubs[p];
       walk = true;
       if (pub.nwords > 0 && pub.mountpoint < a.max_mp) {
-        const uint32_t* w = a.words + pub.word_off;
-        uint64_t part = 0;
-        for (uint32_t i = 0; i < pub.nwords; i++) part += fp_word(w[i], i);
-        const uint64_t fp = fp_final(part, pub.mountpoint, pub.nwords);
+        const uint64_t fp = lane_pub_fp(a, pub);
         const uint32_t i = (uint32_t)(fp & a.dd_mask);
         if (a.dd_key[i] == dd_key_of(a, fp)) {
           rep = a.dd_rep[i];
@@ -1895,23 +1914,30 @@ __global__ __launch_bounds__(256) void k_dd_classify(MatchArgs a) {
             // has is one id, and only the '$' flag, which the ids do not
             // carry, changes what the same ids match)
             const vmqg_pub R = a.pubs[rep];
-            bool eq = R.mountpoint == pub.mountpoint && R.nwords == pub.nwords && R.flags == pub.flags;
-            for (uint32_t k = 0; eq && k < pub.nwords; k++) eq = a.words[R.word_off + k] == w[k];
+            const bool eq = R.mountpoint == pub.mountpoint && R.nwords == pub.nwords && R.flags == pub.flags &&
+                            lane_words_equal(a.words + R.word_off, a.words + pub.word_off, pub.nwords);
             dup = eq;
             walk = !eq;
           }
         }
       }
     }
-    if (dup) {
-      a.deferred[3ull * a.npub + p] = rep;
-      atomicOr(reinterpret_cast<unsigned long long*>(a.ddmask + p / a.gpw), 1ull << (p % a.gpw));
-      atomicAdd(&dups, 1u);   // LDS
+    // A wave holds 64 consecutive publishes from a multiple of 64 (ranges
+    // start at multiples of 256), so each of its chunks' duplicate masks is a
+    // slice of one ballot, stored whole by the chunk's first lane: no atomics
+    // on the mask words, and one LDS atomic per wave for each count.
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t m_dup = __ballot(dup), m_walk = __ballot(walk);
+    if (dup) a.deferred[3ull * a.npub + p] = rep;
+    if (p < hi && p % a.gpw == 0)
+      a.ddmask[p / a.gpw] = (m_dup >> lane) & (a.gpw == 64 ? ~0ull : (1ull << a.gpw) - 1);
+    uint32_t k0 = 0;
+    if (lane == 0) {
+      if (m_dup) atomicAdd(&dups, (uint32_t)__popcll(m_dup));   // LDS
+      if (m_walk) k0 = atomicAdd(&nbuf, (uint32_t)__popcll(m_walk));   // LDS
     }
-    if (walk) {
-      const uint32_t k = atomicAdd(&nbuf, 1u);   // LDS
-      buf[k] = p;
-    }
+    k0 = uni(k0);
+    if (walk) buf[k0 + prefix_bits(m_walk)] = p;
     __syncthreads();
     if (nbuf + 256 > kClsBuf || b0 + 256 >= hi) {   // flush: one global atomic for the block
       if (threadIdx.x == 0) base = nbuf ? atomicAdd(&a.status[kStReps], nbuf) : 0u;
