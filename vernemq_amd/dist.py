@@ -39,7 +39,7 @@ def _comm_device(dist, device, group=None):
 def gather_counts(dist, values, device, group=None):
     """All-gather a small int64 vector from every rank -> [world, k] array."""
     import torch
-    t = torch.as_tensor(np.asarray(values, dtype=np.int64), device=_comm_device(dist, device, group))
+    t = torch.as_tensor(np.array(values, dtype=np.int64), device=_comm_device(dist, device, group))   # a copy: callers may pass read-only views
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
     dist.all_gather(out, t, group=group)
     return np.stack([o.cpu().numpy() for o in out])
