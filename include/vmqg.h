@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VMQG_ABI_VERSION 4
+#define VMQG_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------- */
 #define VMQG_OK 0
@@ -102,9 +102,15 @@ typedef struct vmqg_op {
 typedef struct vmqg_pub {
   uint32_t mountpoint;
   uint32_t word_off;    /* index of the first word id in `words`            */
-  uint32_t nwords;      /* >= 1                                             */
+  uint32_t nwords;      /* >= 0: fold/4 answers an empty Topic list too       */
   uint32_t flags;       /* VMQG_PUB_*                                       */
 } vmqg_pub;
+/* Word ids of a publish are looked up, not validated: VMQG_WORD_PLUS /
+ * VMQG_WORD_HASH in a publish are the literal words "+" / "#", matched as
+ * vmq_reg_trie:trie_match/4 matches them (the W probe of [W, <<"+">>] takes
+ * the "+" edge, so a "+" word walks it twice, vmq_reg_trie.erl:366-375), and
+ * the `{Topic, node()}` candidate finds a wildcard filter's own local key
+ * (:62, :257-260).  VMQG_WORD_UNKNOWN matches only "+" and "#" edges. */
 
 #define VMQG_EMIT_LOCAL 1u   /* {SubscriberId, SubInfo}               */
 #define VMQG_EMIT_GROUP 2u   /* {Node, Group, SubscriberId, SubInfo}  */
@@ -206,6 +212,20 @@ int vmqg_prepare_publish(vmqg_ctx* ctx, uint32_t mountpoint, const uint8_t* topi
 int vmqg_prepare_publishes(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints, const uint8_t* const* topics,
                            const size_t* lens, vmqg_pub* pubs_out, int32_t* rc_out, uint32_t* words_out,
                            size_t wcap, size_t* nwords_out);
+
+/* Publishes given as Topic word lists, the form vmq_reg_trie:fold/4 takes
+ * (vmq_reg_trie.erl:59-66; plugin publishes reach it unvalidated,
+ * vmq_reg.erl:572-594): no split, no validation.  Publish i has counts[i]
+ * words (0 allowed); word k of the batch is words[k][0 .. lens[k]), in
+ * publish order.  Each word is one dictionary lookup: "+" / "#" give their
+ * reserved ids, a word no filter has (one holding a '/', say) gives
+ * VMQG_WORD_UNKNOWN.  flags: VMQG_PUB_DOLLAR when the first word starts with
+ * '$', VMQG_PUB_UNKNOWN as vmqg_prepare_publishes.  words_out receives
+ * sum(counts) ids (VMQG_E_OVERFLOW if wcap is smaller); pubs_out[i].word_off
+ * indexes it.  Same read-only contract as vmqg_prepare_publish (ABI 5). */
+int vmqg_prepare_word_lists(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints, const uint32_t* counts,
+                            const uint8_t* const* words, const size_t* lens, vmqg_pub* pubs_out,
+                            uint32_t* words_out, size_t wcap, size_t* nwords_out);
 
 /* Words interned so far: grows whenever a filter brings a new word.  A
  * publish prepared with VMQG_PUB_UNKNOWN before the dictionary grew may name
@@ -352,11 +372,15 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8;
  *                          defaults 4 and 16)
  *   "dedupe"    0 | 1 | 2  batch-wide dedupe of repeated (MP, topic) publishes in
- *                          COUNT: off (the default: it loses its A/B),
- *                          on (a claim pass, then duplicates take their
- *                          representative's result), or auto (on while more
- *                          than half the publishes repeat another, judged on
- *                          the previous calls — sampled on 1 chunk in 64 while off)
+ *                          COUNT: off, on (a claim and a classify pass, COUNT
+ *                          walks one representative per topic, a fix-up pass
+ *                          gives the duplicates its result), or auto (2, the
+ *                          default: on while more than half the publishes of
+ *                          the last deduped call repeated another; while off,
+ *                          whole calls are probed deduped — the first call,
+ *                          then after 64, 128, ... up to 8,192 calls while the
+ *                          probes keep finding distinct topics — and a call of
+ *                          fewer than 256 publishes is never probed)
  *   "dd_g"      1 | 4      dedupe on: lanes per representative in COUNT (default 4)
  *   "groups"    0 | 1      records mode: publishes of >= 128 records grouped by what
  *                          they emit and written group by group by the EMIT tail

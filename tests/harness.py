@@ -24,10 +24,13 @@ class ProductDriver:
     mode "records": vmqg_match_batch (16-B FoldFun records); "ranges":
     vmqg_match_ranges, expanded on the host against vmqg_records."""
 
-    def __init__(self, node: str, device: int = 0, mode: str = "records", **kw):
+    def __init__(self, node: str, device: int = 0, mode: str = "records", word_lists: bool = False, **kw):
         from vernemq_amd.reg_view import RegGpuView
         self.view = RegGpuView(node=node, device=device, **kw)
         self.mode = mode
+        # word_lists: publishes prepared by the library (vmqg_prepare_word_lists),
+        # the Topic list as fold/4 takes it; else by the Python mirror's prepare
+        self.word_lists = word_lists
 
     def apply(self, events):
         self.view.handle_events(events)
@@ -43,7 +46,10 @@ class ProductDriver:
 
     def fold_batch(self, pubs):
         v = self.view
-        arr, words = v.prepare([(mp, t if isinstance(t, (bytes, bytearray)) else tuple(t)) for mp, t in pubs])
+        if self.word_lists:
+            arr, words = v.prepare_word_lists([(mp, tuple(t)) for mp, t in pubs])
+        else:
+            arr, words = v.prepare([(mp, t if isinstance(t, (bytes, bytearray)) else tuple(t)) for mp, t in pubs])
         recs, offs = self.match_arrays(arr, words)
         return [[canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1]))] for i in range(len(arr))]
 

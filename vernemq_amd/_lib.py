@@ -133,6 +133,7 @@ SIGNATURES = [
     ("vmqg_intern_words", ctypes.c_int, [_P, _P, _P, _U32, ctypes.c_int, _P]),
     ("vmqg_prepare_publish", ctypes.c_int, [_P, _U32, ctypes.c_char_p, _SZ, _P, _U32, ctypes.POINTER(Pub)]),
     ("vmqg_prepare_publishes", ctypes.c_int, [_P, _SZ, _P, _P, _P, _P, _P, _P, _SZ, ctypes.POINTER(_SZ)]),
+    ("vmqg_prepare_word_lists", ctypes.c_int, [_P, _SZ, _P, _P, _P, _P, _P, _P, _SZ, ctypes.POINTER(_SZ)]),
     ("vmqg_dict_generation", _U64, [_P]),
     ("vmqg_hbatch_new", _P, [_P]),
     ("vmqg_hbatch_free", None, [_P]),

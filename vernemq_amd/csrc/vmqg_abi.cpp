@@ -81,7 +81,12 @@ static inline bool split_publish_topic(const uint8_t* p, size_t len, F&& on_word
   for (size_t i = 0; i < len; i += 8) {
     const size_t m = len - i < 8 ? len - i : 8;
     uint64_t x = 0;
-    if (m == 8 || (((uintptr_t)(p + i) & 4095) <= 4096 - 8)) memcpy(&x, p + i, 8);
+#if defined(__SANITIZE_ADDRESS__)
+    constexpr bool kWide = false;   // a page-safe over-read is still one to ASan
+#else
+    constexpr bool kWide = true;
+#endif
+    if (m == 8 || (kWide && ((uintptr_t)(p + i) & 4095) <= 4096 - 8)) memcpy(&x, p + i, 8);
     else memcpy(&x, p + i, m);
     const uint64_t valid = m == 8 ? ~0ull : ~0ull >> (64 - 8 * m);
     auto eq = [x, valid](uint8_t c) {
@@ -193,6 +198,55 @@ int vmqg_prepare_publishes(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints,
   GUARD_END
 }
 
+// fold/4 takes the Topic word list as given (vmq_reg_trie.erl:59-66): each
+// word looked up as one dictionary key, nothing split or validated.  Blocks
+// of publishes are hashed and prefetched before they are resolved, as above.
+int vmqg_prepare_word_lists(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints, const uint32_t* counts,
+                            const uint8_t* const* words, const size_t* lens, vmqg_pub* pubs_out,
+                            uint32_t* words_out, size_t wcap, size_t* nwords_out) {
+  if (!ctx || (n && (!mountpoints || !counts || !pubs_out))) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  const vmqg::WordDict& d = ctx->e.dict;
+  constexpr size_t kBlock = 64;
+  static thread_local std::vector<vmqg::WordDict::Key> keys;
+  size_t nw = 0;
+  for (size_t lo = 0; lo < n; lo += kBlock) {
+    const size_t hi = std::min(n, lo + kBlock);
+    keys.clear();
+    const size_t nw0 = nw;
+    for (size_t t = lo; t < hi; t++) {
+      const uint32_t c = counts[t];
+      if (nw + c > wcap) return VMQG_E_OVERFLOW;
+      if (c && (!words || !lens || !words_out)) return VMQG_E_INVAL;
+      vmqg_pub& pub = pubs_out[t];
+      pub = vmqg_pub{mountpoints[t], (uint32_t)nw, c, 0};
+      for (uint32_t j = 0; j < c; j++) {
+        const uint8_t* p = words[nw + j];
+        const size_t l = lens[nw + j];
+        if (l && !p) return VMQG_E_INVAL;
+        static const uint8_t kNoBytes[16] = {0};   // an empty binary may come without a pointer
+        keys.push_back(vmqg::WordDict::key(l ? p : kNoBytes, l));
+        d.prefetch(keys.back());
+      }
+      // MQTT-4.7.2-1 is decided on the first word's first byte (vmq_reg_trie.erl:285-288)
+      if (c && lens[nw] && words[nw][0] == '$') pub.flags |= VMQG_PUB_DOLLAR;
+      nw += c;
+    }
+    for (size_t k = 0; k < nw - nw0; k++) {
+      const uint32_t f = d.find(keys[k]);
+      words_out[nw0 + k] = f == vmqg::WordDict::kVoid ? vmqg::kUnknownWord : f;
+    }
+    for (size_t t = lo; t < hi; t++) {
+      vmqg_pub& pub = pubs_out[t];
+      for (uint32_t j = 0; j < pub.nwords; j++)
+        if (words_out[pub.word_off + j] == vmqg::kUnknownWord) { pub.flags |= VMQG_PUB_UNKNOWN; break; }
+    }
+  }
+  if (nwords_out) *nwords_out = nw;
+  return VMQG_OK;
+  GUARD_END
+}
+
 uint64_t vmqg_dict_generation(vmqg_ctx* ctx) { return ctx ? ctx->e.dict.generation() : 0; }
 
 int vmqg_apply_ops(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords,
@@ -225,7 +279,7 @@ static int match_host(Engine& e, const vmqg_pub* pubs, size_t npub, const uint32
                       void* out, size_t esz, size_t out_cap, size_t* out_n, uint64_t* offsets) {
   if (!e.has_device) return VMQG_E_DEVICE;
   for (size_t i = 0; i < npub; i++)
-    if (pubs[i].nwords == 0 || (uint64_t)pubs[i].word_off + pubs[i].nwords > nwords) return VMQG_E_INVAL;
+    if ((uint64_t)pubs[i].word_off + pubs[i].nwords > nwords) return VMQG_E_INVAL;   // 0 words: fold(MP, [])
   hipSetDevice(e.device);
   int rc;
   if ((rc = grow(&e.d_pubs, &e.d_pubs_cap, (npub + 1) * sizeof(vmqg_pub)))) return rc;
@@ -368,7 +422,7 @@ int vmqg_hbatch_submit(vmqg_ctx* ctx, vmqg_hbatch* hb, size_t npub, size_t nword
   Engine& e = ctx->e;
   if (!e.has_device || e.device != hb->device) return VMQG_E_DEVICE;
   for (size_t i = 0; i < npub; i++)
-    if (hb->h_pubs[i].nwords == 0 || (uint64_t)hb->h_pubs[i].word_off + hb->h_pubs[i].nwords > nwords)
+    if ((uint64_t)hb->h_pubs[i].word_off + hb->h_pubs[i].nwords > nwords)
       return VMQG_E_INVAL;
   hipSetDevice(e.device);
   const size_t esz = ranges ? sizeof(vmqg_range) : sizeof(vmqg_emit);

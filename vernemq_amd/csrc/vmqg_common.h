@@ -18,12 +18,22 @@
 //             vmq_trie_subs key ({MP,Topic} or {MP,Group,Topic}) (:141-142).
 //   keylist : u32 pool of key ids for filters with >= 2 node entries.
 //   records : 16-B emission records (vmqg_emit) grouped per key.
-//   exact   : open-addressed hash of non-wildcard (MP, Topic) -> {local key's
-//             record off + count, remote-node mask}: the `{Topic, node()}`
-//             candidate of fold/4 (:62) plus vmq_trie_remote_subs (:143, :514-520).
-//   exwords : u32 pool: per exact topic its MP then its word ids (exactness check).
-//   exbits  : one bit per fingerprint class of the exact topics (8 per exact slot):
-//             a publish whose bit is clear skips the exact-table probe.
+//   exact   : open-addressed hash of (MP, Topic) -> {local key's record off +
+//             count, remote-node mask}: the `{Topic, node()}` candidate of
+//             fold/4 (:62) plus vmq_trie_remote_subs (:143, :514-520), for
+//             every topic with a local key or remote entries — wildcard
+//             filters too: fold/4 takes the Topic word list as given, so a
+//             publish whose words are literally "a", "+" finds the local key
+//             of the filter a/+ (add_subscriber keys every local
+//             subscription, :257-260, :498-501).  64-B slots holding the MP
+//             and the first 7 words, two per 128-B bucket: one line verifies
+//             a topic of <= 7 words.
+//   exwords : u32 pool: per exact topic its words beyond the 7th, then
+//             {count, remote nodes >= 64} (only when it has some).
+//   exbits  : one bit per fingerprint class of the non-wildcard exact topics
+//             (one per exact slot, so it stays L2-resident): a publish whose
+//             bit is clear skips the exact-table probe (a publish holding a
+//             '+' / '#' word always probes).
 #pragma once
 #include <stdint.h>
 
@@ -63,22 +73,29 @@ struct alignas(16) EdgeSlot { uint32_t parent, word, child, flags; };
 struct alignas(16) NodeRec { uint32_t meta, key, rmask_lo, rmask_hi, off0, cnt0, hi_off, hi_cnt; };
 struct alignas(8) KeyDesc { uint32_t off, count; };
 struct alignas(16) Record { uint32_t kind_node, group, subscriber, subinfo; };
-// ExactSlot.nwords bit: remote nodes >= 64 follow the words in exwords
-// ({count, node ids}); the slot's rmask holds the nodes < 64.
+// ExactSlot.nwords bit: remote nodes >= 64 follow in exwords ({count, node
+// ids}, after the words beyond the inline ones); the slot's rmask holds the
+// nodes < 64.
 constexpr uint32_t kExactHigh = 0x40000000u;
-struct alignas(16) ExactSlot {
+constexpr uint32_t kExactInline = 7;   // words held in the slot itself
+struct alignas(64) ExactSlot {
   uint64_t fp;
-  uint32_t nwords, words_off;   // nwords == kEmpty / kTomb marks free slots; exwords[words_off] = MP
+  uint32_t nwords, words_off;   // nwords == kEmpty / kTomb marks free slots; exwords[words_off..]: words [7, L),
+                                // then the high-node list (kNone when there is neither)
   uint32_t off, count;          // the local {MP,Topic} key's records (count 0: none)
   uint64_t rmask;               // remote nodes with exact subscriptions
+  uint32_t mp;
+  uint32_t w[kExactInline];     // words [0, min(L, 7)); the rest 0
 };
 static_assert(sizeof(EdgeSlot) == 16 && sizeof(NodeRec) == 32 && sizeof(Record) == 16, "");
-static_assert(sizeof(ExactSlot) == 32 && sizeof(KeyDesc) == 8, "");
+static_assert(sizeof(ExactSlot) == 64 && sizeof(KeyDesc) == 8, "");
+// exwords entries before a slot's high-node list
+VMQG_HD uint32_t exact_tail_words(uint32_t L) { return L > kExactInline ? L - kExactInline : 0u; }
 
 constexpr uint32_t kEdgeSlotsPerBucket = 4;
 constexpr uint32_t kMaxNodes = 4096;        // VMQG_MAX_NODES: one 64-bit bitset word per lane
 constexpr uint32_t kLowNodes = 64;          // nodes held in the inline 64-bit masks
-constexpr uint32_t kExactSlotsPerBucket = 2;
+constexpr uint32_t kExactSlotsPerBucket = 2;   // 128-B buckets: one L2 line per probe
 
 // Arena layout.  Fixed-size POD: it is what a replica needs to read an image
 // (VMQG_LAYOUT_BYTES in vmqg.h bounds it).
@@ -97,11 +114,11 @@ struct Layout {
   uint64_t local_node;
   uint64_t max_depth;        // deepest trie path (sizes the wave tier's global stack)
   uint64_t exbits_off;       // exact-topic filter: one bit per fingerprint class, set for every
-  uint64_t exbits_words;     // ... exact topic placed since the last re-layout (u32 words, power of two)
+  uint64_t exbits_words;     // ... non-wildcard exact topic placed since the last re-layout (u32 words, power of two)
   uint64_t pad[11];
 };
 static_assert(sizeof(Layout) == 256, "layout must be 256 bytes");
-constexpr uint64_t kLayoutMagic = 0x32676D7176ull;  // "vmqg2" (exbits_off / exbits_words are read by every match)
+constexpr uint64_t kLayoutMagic = 0x33676D7176ull;  // "vmqg3" (64-B exact slots with inline words; exbits one per slot)
 
 // 24-byte patch record: write 16 bytes at arena offset `off` (16-B aligned).
 struct Patch { uint64_t off; uint32_t data[4]; };

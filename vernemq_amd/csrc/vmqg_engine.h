@@ -126,9 +126,14 @@ class WordDict {
   struct Key { uint64_t h, k0, k1; const uint8_t* p; size_t n; };
   static Key key(const uint8_t* p, size_t n) {
     Key k{0, 0, 0, p, n};
-    if (((uintptr_t)p & 4095) <= 4096 - 16) {
-      // 16 bytes readable without crossing a page: two loads, the bytes
-      // past the word masked off (the same zero padding as below)
+#if defined(__SANITIZE_ADDRESS__)
+    constexpr bool kWide = false;   // the page-safe over-read below is still an over-read to ASan
+#else
+    constexpr bool kWide = true;
+#endif
+    if (n >= 16 || (kWide && ((uintptr_t)p & 4095) <= 4096 - 16)) {
+      // 16 bytes readable (the word's own, or without crossing a page): two
+      // loads, the bytes past the word masked off (the same zero padding as below)
       memcpy(&k.k0, p, 8);
       memcpy(&k.k1, p + 8, 8);
       if (n < 8) { k.k0 &= n ? ~0ull >> (64 - 8 * n) : 0ull; k.k1 = 0; }
@@ -243,11 +248,11 @@ struct TopicInfo {
   std::vector<uint32_t> words;
   uint32_t local_key = kNone;
   uint32_t path = kNone;            // trie path of the same (MP, Topic), once created
-  uint8_t dirty = 0, exact_ok = 0;
+  uint8_t dirty = 0, wild = 0;      // wild: a '+' / '#' word (no exbits filter bit: only such a publish equals it)
   std::vector<std::pair<uint32_t, int64_t>> remote;
   uint64_t slot = ~0ull;
   uint32_t words_off = kNone;
-  uint32_t xw_len = 0;              // exwords entries owned: MP, words, [count, remote nodes >= 64]
+  uint32_t xw_len = 0;              // exwords entries owned: words beyond the inline ones, [count, remote nodes >= 64]
 };
 
 struct Engine {

@@ -280,7 +280,12 @@ __device__ __forceinline__ StepOut probe_step(const MatchArgs& a, const Group<G>
   uint32_t wd = kUnknownWord;
   if (act && !at_end) wd = d < (uint32_t)G ? wsh : w[d];
   const bool do_h = act && (fl & kHasHash);
-  const bool do_w = act && !at_end && (fl & kHasWord) && wd != kPlus && wd != kHash && wd != kUnknownWord;
+  // the W probe of [W, <<"+">>] (:366-375) for any word the dictionary has:
+  // a publish word equal to '+' (or '#') probes that edge literally — so a
+  // '+' word follows the '+' edge twice, as the reference's foldl does (a
+  // plugin publish's Topic reaches fold/4 unvalidated, vmq_reg.erl:572-594)
+  const uint32_t wneed = wd == kPlus ? kHasPlus : wd == kHash ? kHasHash : kHasWord;
+  const bool do_w = act && !at_end && (fl & wneed) && wd != kUnknownWord;
   const bool do_p = act && !at_end && (fl & kHasPlus);
   const uint64_t bw = edge_hash(node, wd) & a.edge_mask;
   const uint64_t bp = edge_hash(node, kPlus) & a.edge_mask;
@@ -306,27 +311,37 @@ __device__ __forceinline__ StepOut probe_step(const MatchArgs& a, const Group<G>
   return o;
 }
 
-// Exact-topic fingerprint of the publish, computed by the G lanes of a group.
+// Exact-topic fingerprint of the publish, computed by the G lanes of a group;
+// `wild`: the publish holds a '+' / '#' word (only a wildcard topic, which
+// has no filter bit, can equal it).
 template <int G>
 __device__ __forceinline__ uint64_t publish_fp(const vmqg_pub& pub, const uint32_t* w, uint32_t wreg,
-                                               const Group<G>& g) {
+                                               const Group<G>& g, bool& wild) {
   const uint32_t L = pub.nwords;
   uint64_t part = 0;
-  for (uint32_t i = g.lane; i < L; i += G) part += fp_word(i < (uint32_t)G ? wreg : w[i], i);
+  bool wl = false;
+  for (uint32_t i = g.lane; i < L; i += G) {
+    const uint32_t x = i < (uint32_t)G ? wreg : w[i];
+    part += fp_word(x, i);
+    wl |= x == kPlus || x == kHash;
+  }
+  wild = g.ballot(wl) != 0;
   return fp_final(g.sum64(part), pub.mountpoint, L);
 }
 
-// The exact slot of (MP, Topic), or null: fingerprint probe, then the stored
-// MP and words compared group-parallel.
+// The exact slot of (MP, Topic), or null: fingerprint probe, then the MP and
+// words compared group-parallel — the slot holds the first 7 words (one
+// 128-B line verifies a topic of <= 7 words), exwords the rest.
 template <int G>
 __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, const uint32_t* w, uint32_t wreg,
                                        const Group<G>& g) {
   const uint32_t L = pub.nwords;
-  const uint64_t fp = publish_fp<G>(pub, w, wreg, g);
+  bool wild;
+  const uint64_t fp = publish_fp<G>(pub, w, wreg, g, wild);
 #if VMQG_EXACT_FILTER
   // the filter's bit (an L2-resident word) before the table's random line
   const uint64_t xb = exbit_of(fp, a.exbits_mask + 1);
-  if (!((a.exbits[xb >> 5] >> (xb & 31)) & 1u)) return nullptr;
+  if (!wild && !((a.exbits[xb >> 5] >> (xb & 31)) & 1u)) return nullptr;
 #endif
   uint64_t b = fp & a.exact_mask;
   for (uint64_t iter = 0; iter <= a.exact_mask; iter++) {
@@ -336,10 +351,12 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
       const ExactSlot& e = bk[j];
       const uint32_t nw = e.nwords;
       if (nw == kEmpty) { seen_empty = true; break; }
-      if (e.fp != fp || (nw & ~kExactHigh) != L) continue;
-      const uint32_t* xw = a.exwords + e.words_off;
-      bool diff = g.lane == 0 && xw[0] != pub.mountpoint;
-      for (uint32_t i = g.lane; i < L; i += G) diff |= xw[1 + i] != (i < (uint32_t)G ? wreg : w[i]);
+      if (e.fp != fp || (nw & ~kExactHigh) != L || e.mp != pub.mountpoint) continue;
+      bool diff = false;
+      for (uint32_t i = g.lane; i < L; i += G) {
+        const uint32_t x = i < (uint32_t)G ? wreg : w[i];
+        diff |= (i < kExactInline ? e.w[i] : a.exwords[e.words_off + (i - kExactInline)]) != x;
+      }
       if (g.ballot(diff) == 0) return &e;
     }
     if (seen_empty) break;
@@ -402,7 +419,7 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
   const uint32_t L = pub.nwords;
   const uint32_t* w = a.words + pub.word_off;
   const bool dollar = (pub.flags & VMQG_PUB_DOLLAR) != 0;
-  const bool mp_ok = pub.mountpoint < a.max_mp && L > 0;
+  const bool mp_ok = pub.mountpoint < a.max_mp;   // L == 0: the root alone (trie_match/4 :361-363)
   // lane i of the group keeps word i (i < G); deeper words come from memory
   const uint32_t wreg = g.lane < L ? w[g.lane] : kUnknownWord;
   Matched m{0, 0, 0, 0, 0, false, false, false, 0, 0, 0};
@@ -1208,7 +1225,8 @@ struct WaveWalk {
     const uint32_t L = pub.nwords;
     const uint32_t* w = a.words + pub.word_off;
     dollar = (pub.flags & VMQG_PUB_DOLLAR) != 0;
-    const bool mp_ok = pub.mountpoint < a.max_mp && L > 0;
+    // an empty Topic list walks the root alone: trie_match(MP, root, [], _) (:361-363)
+    const bool mp_ok = pub.mountpoint < a.max_mp;
     const uint32_t wreg = lane < L ? w[lane] : kUnknownWord;
     for (uint32_t i = lane; i < kHiWords; i += 64) W.hb[i] = 0;
     uint32_t sp = 0;
@@ -1248,8 +1266,8 @@ struct WaveWalk {
           if (lane == 0) W.keys[nk] = make_uint2(e->off, e->count);
           nk += 1;
         }
-        if (nw & kExactHigh) {   // {count, ids} after the MP and the words
-          const uint32_t* hl = a.exwords + e->words_off + 1 + L;
+        if (nw & kExactHigh) {   // {count, ids} after the words beyond the inline ones
+          const uint32_t* hl = a.exwords + e->words_off + exact_tail_words(L);
           const uint32_t cnt = hl[0];
           for (uint32_t j = lane; j < cnt; j += 64) {
             const uint32_t n = hl[1 + j];

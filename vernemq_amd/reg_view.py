@@ -204,6 +204,30 @@ class RegGpuView:
             off += len(topic)
         return arr, self.intern_words(allw, create=False)
 
+    def prepare_word_lists(self, pubs):
+        """pubs: iterable of (mountpoint, word tuple) -> (PUB_DTYPE array, word
+        id array) through the library's vmqg_prepare_word_lists: the Topic list
+        exactly as fold/4 receives it (vmq_reg_trie.erl:59-66) — no split, no
+        validation; "+" / "#" words are the literal words, any word no filter
+        has (one holding a '/', say) is UNKNOWN, an empty list has no words."""
+        pubs = list(pubs)
+        n = len(pubs)
+        mps = np.array([self.mountpoints.ids.get(mp, self.max_mountpoints) for mp, _ in pubs], dtype=np.uint32)
+        counts = np.array([len(t) for _, t in pubs], dtype=np.uint32)
+        flat = [bytes(w) for _, t in pubs for w in t]
+        nw = len(flat)
+        bufs = [ctypes.create_string_buffer(w, max(1, len(w))) for w in flat]
+        ptrs = (ctypes.c_void_p * max(1, nw))(*[ctypes.addressof(b) for b in bufs])
+        lens = np.array([len(w) for w in flat] or [0], dtype=np.uint64)
+        arr = np.zeros(max(1, n), dtype=PUB_DTYPE)
+        words = np.zeros(max(1, nw), dtype=np.uint32)
+        got = ctypes.c_size_t(0)
+        _lib.check(self._L.vmqg_prepare_word_lists(self._h, n, mps.ctypes.data, counts.ctypes.data, ptrs,
+                                                   lens.ctypes.data, arr.ctypes.data, words.ctypes.data, nw,
+                                                   ctypes.byref(got)), "vmqg_prepare_word_lists")
+        assert got.value == nw
+        return arr[:n], words[:nw]
+
     def match_arrays(self, pubs: np.ndarray, words: np.ndarray, out_cap: int | None = None):
         """Device match of a prepared batch -> (EMIT_DTYPE records, uint64 offsets[n+1])."""
         pubs = np.ascontiguousarray(pubs, dtype=PUB_DTYPE)
