@@ -77,6 +77,39 @@ def load_pmc_traffic(kernel: str, summary: str = "pmc_latest.json"):
     return max(cands, key=lambda v: v.get("total_ns", 0))["hbm_bytes_per_launch"]
 
 
+def launch_ranks(args):
+    """`--gpus N` without a launcher: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set
+    as torch.distributed.run sets them) and return the worst exit code.  The
+    parent never touches the GPU (no HIP call before or after the children
+    start: it only waits for them).  Under a launcher (WORLD_SIZE set) the
+    launcher's rank count must equal --gpus.  Returns None when this process
+    is a rank itself."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            log("--gpus %d but WORLD_SIZE=%s: the rank count must equal --gpus" % (args.gpus, world_env))
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        log("rank exit codes %s" % rcs)
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,6 +142,9 @@ def main():
     ap.add_argument("--churn-batch", type=int, default=10_000)
     ap.add_argument("--churn-rate-batches", type=float, default=10.0, help="delta batches per second (1%%/s at 10M)")
     args = ap.parse_args()
+    rc = launch_ranks(args)
+    if rc is not None:
+        return rc
     if args.config == "D":
         return bench_d(args)
     if args.config == "RT":
@@ -149,7 +185,8 @@ def main():
         t0 = time.time()
         view = RegGpuView(node=w.self_node, device=local, nodes=w.nodes,
                           hints={"edges": 3 * args.n_dev + 1024, "paths": 3 * args.n_dev + 1024,
-                                 "keys": args.n_dev + 1024, "records": args.n_dev + 1024})
+                                 "keys": args.n_dev + 1024, "records": args.n_dev + 1024,
+                                 "exact": args.n_dev + 1024})   # the filters' own local keys (fold/4 :62)
         w.load_into(view)
         load_s = time.time() - t0
         pwid = view.intern_words(w.pub_words, create=False).astype(np.int64)
@@ -1270,4 +1307,4 @@ def bench_shared(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -186,6 +186,7 @@ int vmqgb_batch_add_many(vmqgb_batch* b, vmqg_ctx* ctx, size_t n, const uint32_t
                          const uint8_t* const* topics, const size_t* lens, long* idx_out) {
   if (!n) return 0;
   if (b->n == 0) b->dict_gen = vmqg_dict_generation(ctx);
+  const size_t n_unk0 = b->n_unk, raw0 = b->raw_n;   /* restored on failure: no note may name a slot past b->n */
   size_t need = 0;
   for (size_t i = 0; i < n; i++) need += lens[i] + 1;
   if (grow((void**)&b->pubs, &b->cap, b->n + n, sizeof(vmqg_pub))) return VMQG_E_NOMEM;
@@ -208,8 +209,83 @@ int vmqgb_batch_add_many(vmqgb_batch* b, vmqg_ctx* ctx, size_t n, const uint32_t
     idx_out[i] = (long)k++;
   }
   if (rcs != stack_rc) free(rcs);
-  if (rc) return rc;
+  if (rc) { b->n_unk = n_unk0; b->raw_n = raw0; return rc; }
   b->n = k;
+  b->nwords += nw;
+  return 0;
+}
+
+/* a word list as its unknown-word note: {u32 len, bytes} per word */
+static int note_unknown_words(vmqgb_batch* b, size_t i, uint32_t cnt, const uint8_t* const* words, const size_t* lens) {
+  size_t bytes = 0;
+  for (uint32_t j = 0; j < cnt; j++) bytes += 4 + (lens[j] == VMQGB_NOT_BINARY ? 0 : lens[j]);
+  if (bytes >= VMQGB_RAW_WORDS) return VMQG_E_NOMEM;
+  if (grow((void**)&b->unk, &b->unk_cap, 3 * (b->n_unk + 1), sizeof(uint32_t))) return VMQG_E_NOMEM;
+  if (grow((void**)&b->raw, &b->raw_cap, b->raw_n + bytes, 1)) return VMQG_E_NOMEM;
+  uint8_t* d = b->raw + b->raw_n;
+  for (uint32_t j = 0; j < cnt; j++) {
+    const uint32_t l = lens[j] == VMQGB_NOT_BINARY ? 0xFFFFFFFFu : (uint32_t)lens[j];
+    memcpy(d, &l, 4);
+    d += 4;
+    if (l != 0xFFFFFFFFu && l) { memcpy(d, words[j], l); d += l; }
+  }
+  b->unk[3 * b->n_unk] = (uint32_t)i;
+  b->unk[3 * b->n_unk + 1] = (uint32_t)b->raw_n;
+  b->unk[3 * b->n_unk + 2] = (uint32_t)bytes | VMQGB_RAW_WORDS;
+  b->n_unk++;
+  b->raw_n += bytes;
+  return 0;
+}
+
+/* vmqg_prepare_word_lists over n publishes into pubs / words_out; list
+ * elements that are not binaries (VMQGB_NOT_BINARY) become VMQG_WORD_UNKNOWN */
+static int prepare_lists(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints, const uint32_t* counts,
+                         const uint8_t* const* words, const size_t* lens, size_t nw, vmqg_pub* pubs,
+                         uint32_t* words_out) {
+  size_t stack_l[256] = {0};
+  size_t* l = nw <= 256 ? stack_l : (size_t*)malloc(nw * sizeof(size_t));
+  if (!l) return VMQG_E_NOMEM;
+  int nonbin = 0;
+  for (size_t k = 0; k < nw; k++) {
+    l[k] = lens[k] == VMQGB_NOT_BINARY ? 0 : lens[k];
+    nonbin |= lens[k] == VMQGB_NOT_BINARY;
+  }
+  size_t got = 0;
+  const int rc = vmqg_prepare_word_lists(ctx, n, mountpoints, counts, words, l, pubs, words_out, nw, &got);
+  if (l != stack_l) free(l);
+  if (rc) return rc;
+  if (nonbin) {
+    for (size_t i = 0; i < n; i++)
+      for (uint32_t j = 0; j < pubs[i].nwords; j++)
+        if (lens[pubs[i].word_off + j] == VMQGB_NOT_BINARY) {
+          words_out[pubs[i].word_off + j] = VMQG_WORD_UNKNOWN;
+          pubs[i].flags |= VMQG_PUB_UNKNOWN;
+        }
+  }
+  return 0;
+}
+
+int vmqgb_batch_add_word_lists(vmqgb_batch* b, vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints,
+                               const uint32_t* counts, const uint8_t* const* words, const size_t* lens,
+                               long* idx_out) {
+  if (!n) return 0;
+  if (b->n == 0) b->dict_gen = vmqg_dict_generation(ctx);
+  size_t nw = 0;
+  for (size_t i = 0; i < n; i++) nw += counts[i];
+  if (grow((void**)&b->pubs, &b->cap, b->n + n, sizeof(vmqg_pub))) return VMQG_E_NOMEM;
+  if (grow((void**)&b->words, &b->wcap, b->nwords + nw + 1, sizeof(uint32_t))) return VMQG_E_NOMEM;
+  vmqg_pub* P = b->pubs + b->n;
+  int rc = prepare_lists(ctx, n, mountpoints, counts, words, lens, nw, P, b->words + b->nwords);
+  if (rc) return rc;
+  const size_t n_unk0 = b->n_unk, raw0 = b->raw_n;
+  for (size_t i = 0; i < n && !rc; i++) {
+    const uint32_t off = P[i].word_off;
+    if (P[i].flags & VMQG_PUB_UNKNOWN) rc = note_unknown_words(b, b->n + i, P[i].nwords, words + off, lens + off);
+    P[i].word_off = off + (uint32_t)b->nwords;
+    idx_out[i] = (long)(b->n + i);
+  }
+  if (rc) { b->n_unk = n_unk0; b->raw_n = raw0; return rc; }
+  b->n += n;
   b->nwords += nw;
   return 0;
 }
@@ -223,11 +299,32 @@ int vmqgb_batch_recheck(vmqgb_batch* b, vmqg_ctx* ctx) {
   for (size_t u = 0; u < b->n_unk; u++) {
     vmqg_pub* pub = &b->pubs[b->unk[3 * u]];
     const uint8_t* t = b->raw + b->unk[3 * u + 1];
-    const size_t len = b->unk[3 * u + 2];
+    const uint32_t rl = b->unk[3 * u + 2];
+    const size_t len = rl & ~VMQGB_RAW_WORDS;
     uint32_t* w = pub->nwords <= 64 ? tmp : (uint32_t*)malloc(pub->nwords * sizeof(uint32_t));
     if (!w) return VMQG_E_NOMEM;
     vmqg_pub np;
-    const int rc = vmqg_prepare_publish(ctx, pub->mountpoint, t, len, w, pub->nwords, &np);
+    int rc;
+    if (rl & VMQGB_RAW_WORDS) {   /* a word list: decode its {len, bytes} words */
+      const uint32_t c = pub->nwords;
+      const uint8_t** wp = (const uint8_t**)malloc((c ? c : 1) * sizeof(*wp));
+      size_t* wl = (size_t*)malloc((c ? c : 1) * sizeof(size_t));
+      rc = wp && wl ? 0 : VMQG_E_NOMEM;
+      const uint8_t* q = t;
+      for (uint32_t j = 0; !rc && j < c; j++) {
+        uint32_t l;
+        memcpy(&l, q, 4);
+        q += 4;
+        wp[j] = q;
+        wl[j] = l == 0xFFFFFFFFu ? VMQGB_NOT_BINARY : l;
+        if (l != 0xFFFFFFFFu) q += l;
+      }
+      if (!rc) rc = prepare_lists(ctx, 1, &pub->mountpoint, &c, wp, wl, c, &np, w);
+      free(wp);
+      free(wl);
+    } else {
+      rc = vmqg_prepare_publish(ctx, pub->mountpoint, t, len, w, pub->nwords, &np);
+    }
     if (!rc && np.nwords == pub->nwords && memcmp(w, b->words + pub->word_off, np.nwords * sizeof(uint32_t))) {
       memcpy(b->words + pub->word_off, w, np.nwords * sizeof(uint32_t));
       pub->flags = np.flags;

@@ -77,16 +77,20 @@ typedef struct vmqgb_batch {
   size_t offs_cap;
   vmqg_range* rng_buf;
   /* publishes prepared with a word the dictionary did not know (VMQG_PUB_UNKNOWN):
-   * their raw topics, so they can be prepared again if the dictionary grew
-   * before their match (vmqg_dict_generation) */
+   * their raw topics (or word lists), so they can be prepared again if the
+   * dictionary grew before their match (vmqg_dict_generation) */
   uint64_t dict_gen;
-  uint32_t* unk;        /* publish index, raw offset, raw length: 3 per entry */
+  uint32_t* unk;        /* publish index, raw offset, raw length (| VMQGB_RAW_WORDS): 3 per entry */
   size_t n_unk, unk_cap;
   uint8_t* raw;
   size_t raw_n, raw_cap;
   void* lease;          /* the view pipeline round the outputs point into */
   uint32_t stale_rematches;   /* matches repeated because a publish's unknown word became known */
 } vmqgb_batch;
+
+/* unk raw length flag: the raw bytes are a word list ({u32 len, bytes} per
+ * word, len 0xFFFFFFFF for a non-binary element), not a topic to split */
+#define VMQGB_RAW_WORDS 0x80000000u
 
 int vmqgb_batch_init(vmqgb_batch* b, size_t cap_hint);
 void vmqgb_batch_reset(vmqgb_batch* b);   /* keeps the buffers */
@@ -99,6 +103,16 @@ long vmqgb_batch_add(vmqgb_batch* b, vmqg_ctx* ctx, uint32_t mountpoint, const u
  * VMQG_E_* for topic i, as vmqgb_batch_add.  Returns 0 or VMQG_E_NOMEM. */
 int vmqgb_batch_add_many(vmqgb_batch* b, vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints,
                          const uint8_t* const* topics, const size_t* lens, long* idx_out);
+/* Adds n publishes given as Topic word lists, the form vmq_reg_trie:fold/4
+ * takes (vmq_reg_trie.erl:59-66): publish i has counts[i] words (0 allowed),
+ * word k of the call is words[k][0 .. lens[k]) — vmqg_prepare_word_lists, no
+ * split, no validation.  lens[k] == VMQGB_NOT_BINARY marks a list element that
+ * is not a binary: it equals no filter word (VMQG_WORD_UNKNOWN).  idx_out[i] =
+ * index in the batch.  Returns 0 or VMQG_E_NOMEM (the batch unchanged). */
+#define VMQGB_NOT_BINARY ((size_t)-1)
+int vmqgb_batch_add_word_lists(vmqgb_batch* b, vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints,
+                               const uint32_t* counts, const uint8_t* const* words, const size_t* lens,
+                               long* idx_out);
 /* Appends every publish of src (per-thread batches -> one match call). */
 int vmqgb_batch_append(vmqgb_batch* dst, const vmqgb_batch* src);
 /* Prepares the publishes holding unknown words again if the dictionary grew

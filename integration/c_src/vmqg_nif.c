@@ -6,7 +6,11 @@
  * overflow retry, the fold and the op batches are vmqg_batch.c (plain C,
  * compiled and unit-tested in this repository: tests/test_nif_layer.py,
  * tools/nif_harness.c).  This file is written against the documented
- * erl_nif API (OTP 21+) and is NOT compiled here: the image has no OTP.
+ * erl_nif API of OTP 19.3 .. 21 (the releases the reference is tested on,
+ * .travis.yml: the newest calls are enif_term_to_binary, OTP 19.0, and
+ * enif_schedule_nif / enif_system_info's dirty_scheduler_support, OTP
+ * 17.3); OTP is not in this image, so it is compiled and run over an
+ * erl_nif test double (tests/c/mock_erl_nif, tests/c/nif_mock_check.c).
  *
  * Build (in apps/vmq_server, rebar3 port_specs or a Makefile):
  *   cc -O2 -fPIC -shared -I$ERTS/include -I<repo>/include -I<repo>/integration/c_src \
@@ -340,8 +344,12 @@ static ERL_NIF_TERM nif_batch_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
   return enif_make_tuple2(env, a_ok, t);
 }
 
-/* match(Ctx, Batch, [{MP, TopicBin}], records | ranges) -> [{ok, Entries} | {error, Reason}]
+/* match(Ctx, Batch, [{MP, Topic}], records | ranges) -> [{ok, Entries} | {error, Reason}]
  * (fold/4 for a batch of callers, vmq_reg_trie.erl:59-98); dirty CPU.
+ * Topic is the word list fold/4 was given, used as given (no join, no
+ * split, no validate_topic: a plugin publish reaches fold/4 unvalidated,
+ * vmq_reg.erl:572-594): each element one dictionary lookup, an element that
+ * is not a binary equal to no filter word, [] the root alone.
  * Batchers run this concurrently: the tables are read-locked from the first
  * publish prepared to the last term built (yielded every VMQGB_YIELD_EVERY
  * publishes while preparing, and while folding records); the batch joins the
@@ -359,31 +367,34 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   const size_t m = n ? n : 1;
   long* idx = (long*)enif_alloc(m * sizeof(long));
   ERL_NIF_TERM* res = (ERL_NIF_TERM*)enif_alloc(m * sizeof(ERL_NIF_TERM));
-  const uint8_t** tp = (const uint8_t**)enif_alloc(m * sizeof(*tp));
-  size_t* tl = (size_t*)enif_alloc(m * sizeof(size_t));
+  ERL_NIF_TERM* topics = (ERL_NIF_TERM*)enif_alloc(m * sizeof(ERL_NIF_TERM));
+  uint32_t* cnt = (uint32_t*)enif_alloc(m * sizeof(uint32_t));
   uint32_t* mps = (uint32_t*)enif_alloc(m * sizeof(uint32_t));
-  if (!idx || !res || !tp || !tl || !mps) {
-    enif_free(idx); enif_free(res); enif_free(tp); enif_free(tl); enif_free(mps);
+  if (!idx || !res || !topics || !cnt || !mps) {
+    enif_free(idx); enif_free(res); enif_free(topics); enif_free(cnt); enif_free(mps);
     return enif_make_badarg(env);
   }
-  /* the topics' bytes (valid for this call) and their mountpoint ids; the
+  /* pass 1: each publish's Topic list and length, and its mountpoint id; the
    * MP of the previous publish is reused when identical (one term_to_binary
    * per distinct mountpoint run, not per publish) */
   ERL_NIF_TERM head, tail = argv[2], last_mp = 0;
   uint32_t last_id = r->max_mountpoints;
+  size_t total = 0;
   for (unsigned i = 0; i < n; i++) {
     int arity;
     const ERL_NIF_TERM* el;
-    ErlNifBinary topic;
+    unsigned len = 0;
     enif_get_list_cell(env, tail, &head, &tail);
     idx[i] = 0;
-    if (!enif_get_tuple(env, head, &arity, &el) || arity != 2 || !enif_inspect_iolist_as_binary(env, el[1], &topic)) {
-      idx[i] = VMQG_E_INVAL;
-      tp[i] = NULL; tl[i] = 0; mps[i] = 0;
+    cnt[i] = 0;
+    mps[i] = 0;
+    if (!enif_get_tuple(env, head, &arity, &el) || arity != 2 || !enif_get_list_length(env, el[1], &len)) {
+      idx[i] = VMQG_E_INVAL;   /* fold/4's is_list(Topic) guard (vmq_reg_trie.erl:60) */
       continue;
     }
-    tp[i] = topic.data;
-    tl[i] = topic.size;
+    topics[i] = el[1];
+    cnt[i] = len;
+    total += len;
     if (!last_mp || !enif_is_identical(el[0], last_mp)) {
       ErlNifBinary mpb;
       last_mp = el[0];
@@ -398,23 +409,48 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     }
     mps[i] = last_id;
   }
+  /* pass 2: every word's bytes (valid for this call) */
+  const uint8_t** wp = (const uint8_t**)enif_alloc((total ? total : 1) * sizeof(*wp));
+  size_t* wl = (size_t*)enif_alloc((total ? total : 1) * sizeof(size_t));
+  if (!wp || !wl) {
+    enif_free(wp); enif_free(wl);
+    enif_free(idx); enif_free(res); enif_free(topics); enif_free(cnt); enif_free(mps);
+    return enif_make_badarg(env);
+  }
+  size_t k = 0;
+  for (unsigned i = 0; i < n; i++) {
+    if (idx[i]) continue;
+    ERL_NIF_TERM wt = topics[i], w;
+    while (enif_get_list_cell(env, wt, &w, &wt)) {
+      ErlNifBinary wb;
+      if (enif_inspect_binary(env, w, &wb)) { wp[k] = wb.data; wl[k] = wb.size; }
+      else { wp[k] = NULL; wl[k] = VMQGB_NOT_BINARY; }   /* equals no filter word */
+      k++;
+    }
+  }
   vmqgb_view_read_begin(r->view);
   vmqgb_batch_reset(b);
   /* the batched prepare, slice by slice (a writer gets in between slices) */
+  size_t wbase = 0;
   for (unsigned lo = 0; lo < n; lo += VMQGB_YIELD_EVERY) {
     const unsigned hi = lo + VMQGB_YIELD_EVERY < n ? lo + VMQGB_YIELD_EVERY : n;
     if (lo) vmqgb_view_yield(r->view);
-    /* rejected terms keep their error; the others get their batch index */
-    unsigned k = 0;
+    /* rejected terms keep their error; the others are prepared together */
+    unsigned q = 0;
+    size_t sw = 0;
     for (unsigned i = lo; i < hi; i++)
-      if (idx[i] == 0) { tp[lo + k] = tp[i]; tl[lo + k] = tl[i]; mps[lo + k] = mps[i]; k++; }
-    long* sub = (long*)enif_alloc((k ? k : 1) * sizeof(long));
-    const int rc = sub ? vmqgb_batch_add_many(b, r->ctx, k, mps + lo, tp + lo, tl + lo, sub) : VMQG_E_NOMEM;
+      if (idx[i] == 0) { mps[lo + q] = mps[i]; cnt[lo + q] = cnt[i]; sw += cnt[i]; q++; }
+    long* sub = (long*)enif_alloc((q ? q : 1) * sizeof(long));
+    const int rc = sub ? vmqgb_batch_add_word_lists(b, r->ctx, q, mps + lo, cnt + lo, wp + wbase, wl + wbase, sub)
+                       : VMQG_E_NOMEM;
+    wbase += sw;
     unsigned j = 0;
     for (unsigned i = lo; i < hi; i++)
       if (idx[i] == 0) idx[i] = rc ? rc : sub[j++];
     enif_free(sub);
   }
+  enif_free(wp);
+  enif_free(wl);
   const vmqg_emit* recs = NULL;
   uint64_t nrecs = 0;
   const int rc = vmqgb_view_match(r->view, b, ranges, &recs, &nrecs);
@@ -438,7 +474,7 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   vmqgb_view_release(r->view, b);
   vmqgb_view_read_end(r->view);
   ERL_NIF_TERM list = enif_make_list_from_array(env, res, n);
-  enif_free(res); enif_free(idx); enif_free(tp); enif_free(tl); enif_free(mps);
+  enif_free(res); enif_free(idx); enif_free(topics); enif_free(cnt); enif_free(mps);
   return list;
 }
 
@@ -455,8 +491,34 @@ static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   return enif_make_tuple2(env, enif_make_uint64(env, st.subs), enif_make_uint64(env, st.device_bytes));
 }
 
+/* Dirty schedulers: every call that can wait for the table lock or the
+ * device runs on one (add_init applies a 65,536-op batch: host engine +
+ * upload).  The table registers plain NIFs that reschedule themselves with
+ * enif_schedule_nif (erl_nif 2.7, OTP 17.3+), dirty when the emulator has
+ * dirty schedulers — the default from OTP 20; OTP 19.3 only when built with
+ * --enable-dirty-schedulers — and on the calling scheduler otherwise, so
+ * the library loads on every OTP the reference supports (19.3, 20.3, 21.1,
+ * .travis.yml).  Dirty flags in the table itself would refuse the load on
+ * an emulator without them. */
+static int g_dirty;
+
+#define RESCHEDULE(name, impl, kind)                                                    \
+  static ERL_NIF_TERM name(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {        \
+    return enif_schedule_nif(env, #impl, g_dirty ? (kind) : 0, impl, argc, argv);       \
+  }
+RESCHEDULE(d_create, nif_create, ERL_NIF_DIRTY_JOB_IO_BOUND)
+RESCHEDULE(d_apply, nif_apply, ERL_NIF_DIRTY_JOB_CPU_BOUND)
+RESCHEDULE(d_apply_many, nif_apply_many, ERL_NIF_DIRTY_JOB_CPU_BOUND)
+RESCHEDULE(d_add_init, nif_add_init, ERL_NIF_DIRTY_JOB_CPU_BOUND)
+RESCHEDULE(d_flush_init, nif_flush_init, ERL_NIF_DIRTY_JOB_CPU_BOUND)
+RESCHEDULE(d_match, nif_match, ERL_NIF_DIRTY_JOB_CPU_BOUND)
+RESCHEDULE(d_stats, nif_stats, ERL_NIF_DIRTY_JOB_CPU_BOUND)
+
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   (void)priv; (void)info;
+  ErlNifSysInfo si;
+  enif_system_info(&si, sizeof si);
+  g_dirty = si.dirty_scheduler_support != 0;
   RES = enif_open_resource_type(env, NULL, "vmqg_ctx", res_dtor, ERL_NIF_RT_CREATE, NULL);
   BRES = enif_open_resource_type(env, NULL, "vmqg_batch", bres_dtor, ERL_NIF_RT_CREATE, NULL);
   a_ok = enif_make_atom(env, "ok");
@@ -470,17 +532,15 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   return RES && BRES ? 0 : 1;
 }
 
-/* every call that can wait for the table lock or the device runs on a dirty
- * scheduler (add_init applies a 65,536-op batch: host engine + upload) */
 static ErlNifFunc funcs[] = {
-    {"create", 1, nif_create, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"apply", 3, nif_apply, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"apply_many", 2, nif_apply_many, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"add_init", 6, nif_add_init, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"flush_init", 1, nif_flush_init, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"create", 1, d_create, 0},
+    {"apply", 3, d_apply, 0},
+    {"apply_many", 2, d_apply_many, 0},
+    {"add_init", 6, d_add_init, 0},
+    {"flush_init", 1, d_flush_init, 0},
     {"batch_new", 1, nif_batch_new, 0},
-    {"match", 4, nif_match, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"stats", 1, nif_stats, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"match", 4, d_match, 0},
+    {"stats", 1, d_stats, 0},
 };
 
 ERL_NIF_INIT(vmqg_nif, funcs, load, NULL, NULL, NULL)

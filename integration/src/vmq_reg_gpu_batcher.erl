@@ -32,7 +32,7 @@
 -record(state, {ctx,           % vmqg_nif view resource
                 batch,         % this batcher's vmqg_nif batch resource
                 mode=records,  % records | ranges (app env gpu_reg_view_output)
-                pending=[],    % [{From, MP, TopicBin}], newest first
+                pending=[],    % [{From, MP, Topic}], newest first (Topic: the word list fold/4 got)
                 npending=0}).
 
 start_link(Ctx, Mode) ->
@@ -42,8 +42,8 @@ init([Ctx, Mode]) ->
     {ok, Batch} = vmqg_nif:batch_new(Ctx),
     {ok, #state{ctx=Ctx, batch=Batch, mode=Mode}}.
 
-handle_call({match, MP, TopicBin}, From, #state{pending=P, npending=N} = State) ->
-    State1 = State#state{pending=[{From, MP, TopicBin} | P], npending=N + 1},
+handle_call({match, MP, Topic}, From, #state{pending=P, npending=N} = State) ->
+    State1 = State#state{pending=[{From, MP, Topic} | P], npending=N + 1},
     case N + 1 >= ?MAX_BATCH of
         true -> noreply(flush(State1));
         false -> noreply(State1)
@@ -77,9 +77,8 @@ noreply(State) -> {noreply, State, 0}.
 reply(Reply, #state{npending=0} = State) -> {reply, Reply, State};
 reply(Reply, State) -> {reply, Reply, State, 0}.
 
-%% One NIF call for every queued fold request (dirty CPU scheduler: topic
-%% splitting + interning, the GPU match, term construction), then one reply
-%% per caller.  Publishes the reference rejects are rejected per caller.
+%% One NIF call for every queued fold request (dirty CPU scheduler: word
+%% lookups, the GPU match, term construction), then one reply per caller.
 flush(#state{pending=[]} = State) ->
     State;
 flush(#state{ctx=Ctx, batch=B, mode=Mode, pending=P} = State) ->

@@ -39,16 +39,27 @@
 %% default_reg_view = vmq_reg_gpu_view (vmq_server.schema:115-137).  The NIF
 %% (c_src/vmqg_nif.c) and priv/libvmqgpu.so come from this repository.
 %%
+%% OTP: the reference supports 18.0+ and is tested on 19.3, 20.3 and 21.1
+%% (rebar.config:2, .travis.yml).  This module and the batcher use only
+%% gen_server, ets (named table, read_concurrency), queue, lists:foldl /
+%% foldr / reverse / split / zip, application:get_env/3,
+%% erlang:system_info(scheduler_id | schedulers), spawn_link, selective
+%% receive — all older than OTP 18 (no persistent_term, no lists:join,
+%% no maps-only API).  The NIF reschedules itself onto dirty schedulers when
+%% the emulator has them (vmqg_nif.c, load/3).
+%%
 %% Not compiled in this repository's image (no OTP); its C core
 %% (c_src/vmqg_batch.c, the batchers' locking protocol included) is compiled
-%% and tested (tests/test_nif_layer.py, tools/nif_harness.c).
+%% and tested (tests/test_nif_layer.py, tools/nif_harness.c), and the NIF
+%% glue runs over an erl_nif test double (tests/c/nif_mock_check.c).
 -module(vmq_reg_gpu_view).
 -behaviour(gen_server).
 -behaviour(vmq_reg_view).
 
 -export([start_link/0,
          fold/4,
-         stats/0]).
+         stats/0,
+         shadow_stats/0]).
 
 %% gen_server callbacks
 -export([init/1,
@@ -61,6 +72,8 @@
 -define(SERVER, ?MODULE).
 %% subscriber events applied per vmqg_nif:apply_many/2 at most
 -define(MAX_COALESCE, 10000).
+%% shadow-compare counters (public: every fold caller bumps them)
+-define(SHADOW, vmq_reg_gpu_view_shadow).
 
 -record(state, {ctx,                    % vmqg_nif resource (vmqg_ctx + term tables)
                 batchers,               % tuple of vmq_reg_gpu_batcher pids
@@ -76,23 +89,73 @@ start_link() ->
 
 %% vmq_reg_view callback (vmq_reg_view.erl:20-25; called by vmq_reg:publish/5,
 %% vmq_reg.erl:260, and vmq_cluster_com:process/2, vmq_cluster_com.erl:156).
+%% Topic goes to the NIF as the word list it is (vmq_reg_trie:fold/4 walks it
+%% as given, vmq_reg_trie.erl:59-66: a plugin publish is not validated,
+%% vmq_reg.erl:572-594) — '+' / '#' words, words holding '/', [] included.
 fold({MP, _} = SubscriberId, Topic, FoldFun, Acc) when is_list(Topic) ->
-    TopicBin = iolist_to_binary(lists:join(<<"/">>, Topic)),
-    Batchers = persistent_term:get({?MODULE, batchers}),
+    Entries = match(MP, Topic),
+    shadow(SubscriberId, Topic, Entries),
+    lists:foldl(fun(Entry, AccAcc) -> FoldFun(Entry, SubscriberId, AccAcc) end, Acc, Entries).
+
+match(MP, Topic) ->
+    Batchers = ets:lookup_element(?MODULE, batchers, 2),
     Batcher = element(erlang:system_info(scheduler_id) rem tuple_size(Batchers) + 1, Batchers),
-    case gen_server:call(Batcher, {match, MP, TopicBin}, infinity) of
-        {ok, Entries} ->
-            lists:foldl(fun(Entry, AccAcc) -> FoldFun(Entry, SubscriberId, AccAcc) end,
-                        Acc, Entries);
-        {error, Reason} ->
-            error({vmq_reg_gpu_view, Reason})
+    case gen_server:call(Batcher, {match, MP, Topic}, infinity) of
+        {ok, Entries} -> Entries;
+        {error, Reason} -> error({vmq_reg_gpu_view, Reason})
+    end.
+
+%% Shadow compare.  With reg_views = [vmq_reg_trie, vmq_reg_gpu_view] both
+%% views receive every subscriber event (vmq_reg_sup.erl:42-47, 86-87), so
+%% vmq_reg_trie is a live oracle: app env gpu_reg_view_shadow = N > 0 folds
+%% one publish in N through vmq_reg_trie:fold/4 as well and compares the
+%% entry multisets (FoldFun argument lists, sorted).  A difference is folded
+%% once more on both views before it counts (an event may have reached one
+%% view's tables and not yet the other's); mismatches are counted and logged
+%% with the topic, and shadow_stats/0 returns {Sampled, Mismatched}.  The
+%% caller's own FoldFun always runs over the GPU view's entries.
+shadow(SubscriberId, Topic, Entries) ->
+    case ets:lookup(?SHADOW, every) of
+        [{every, N}] when N > 0 ->
+            case rand:uniform(N) of
+                1 -> shadow_compare(SubscriberId, Topic, Entries);
+                _ -> ok
+            end;
+        _ ->
+            ok
+    end.
+
+shadow_compare({MP, _} = SubscriberId, Topic, Entries) ->
+    Collect = fun(E, _, A) -> [E | A] end,
+    Trie = lists:sort(vmq_reg_trie:fold(SubscriberId, Topic, Collect, [])),
+    ets:update_counter(?SHADOW, sampled, 1),
+    case lists:sort(Entries) of
+        Trie ->
+            ok;
+        _ ->
+            Gpu2 = lists:sort(match(MP, Topic)),
+            case lists:sort(vmq_reg_trie:fold(SubscriberId, Topic, Collect, [])) of
+                Gpu2 ->
+                    ok;
+                Trie2 ->
+                    ets:update_counter(?SHADOW, mismatched, 1),
+                    lager:warning("~p: fold of ~p on ~p differs from vmq_reg_trie: ~p entries vs ~p",
+                                  [?MODULE, Topic, MP, length(Gpu2), length(Trie2)])
+            end
+    end.
+
+shadow_stats() ->
+    case catch ets:lookup(?SHADOW, sampled) of
+        [{sampled, S}] -> {S, ets:lookup_element(?SHADOW, mismatched, 2)};
+        _ -> {0, 0}
     end.
 
 %% stats/0 as vmq_reg_trie:stats/0 (vmq_reg_trie.erl:101-112):
-%% {NrOfSubs + NrOfRemoteSubs, Memory}, memory being the device arena.
+%% {NrOfSubs + NrOfRemoteSubs, Memory}, memory being the device arena.  Like
+%% vmq_reg_trie's info/2 (:114-118) it answers 0s while the view is down.
 stats() ->
-    case persistent_term:get({?MODULE, ctx}, undefined) of
-        undefined -> {0, 0};
+    case catch ets:lookup_element(?MODULE, ctx, 2) of
+        {'EXIT', _} -> {0, 0};
         Ctx -> vmqg_nif:stats(Ctx)
     end.
 
@@ -102,13 +165,19 @@ stats() ->
 init([]) ->
     Device = application:get_env(vmq_server, gpu_reg_view_device, 0),
     {ok, Ctx} = vmqg_nif:create(#{device => Device, local_node => node()}),
-    persistent_term:put({?MODULE, ctx}, Ctx),
+    %% the callers' lookups: a read_concurrency table this process owns
+    %% (gone with it), as vmq_reg_trie's tables are (vmq_reg_trie.erl:136-143)
+    ?MODULE = ets:new(?MODULE, [named_table, protected, {read_concurrency, true}]),
+    true = ets:insert(?MODULE, {ctx, Ctx}),
+    ?SHADOW = ets:new(?SHADOW, [named_table, public, {write_concurrency, true}, {read_concurrency, true}]),
+    true = ets:insert(?SHADOW, [{every, application:get_env(vmq_server, gpu_reg_view_shadow, 0)},
+                                {sampled, 0}, {mismatched, 0}]),
     %% fold/4 batchers, one per scheduler (linked: they die with the view)
     Mode = application:get_env(vmq_server, gpu_reg_view_output, records),
     Batchers = list_to_tuple(
                  [begin {ok, Pid} = vmq_reg_gpu_batcher:start_link(Ctx, Mode), Pid end
                   || _ <- lists:seq(1, erlang:system_info(schedulers))]),
-    persistent_term:put({?MODULE, batchers}, Batchers),
+    true = ets:insert(?MODULE, {batchers, Batchers}),
     Self = self(),
     spawn_link(
       fun() ->
@@ -144,8 +213,6 @@ handle_info(Event, State) ->
     {noreply, handle_events([Event | drain_events(?MAX_COALESCE - 1, [])], State)}.
 
 terminate(_Reason, _State) ->
-    persistent_term:erase({?MODULE, batchers}),
-    persistent_term:erase({?MODULE, ctx}),
     ok.
 
 code_change(_OldVsn, State, _Extra) ->

@@ -22,7 +22,8 @@ add_init(_Ctx, _MP, _Topic, _SubscriberId, _SubInfo, _Node) -> erlang:nif_error(
 flush_init(_Ctx) -> erlang:nif_error(nif_not_loaded).
 %% Ctx -> {ok, Batch}: a batcher's own publish batch
 batch_new(_Ctx) -> erlang:nif_error(nif_not_loaded).
-%% Ctx, Batch, [{MP, TopicBin}], records | ranges -> [{ok, [Entry]} | {error, term()}]
+%% Ctx, Batch, [{MP, Topic}], records | ranges -> [{ok, [Entry]} | {error, term()}]
+%% (Topic: the word list vmq_reg_view:fold/4 got, used as given)
 match(_Ctx, _Batch, _Publishes, _Mode) -> erlang:nif_error(nif_not_loaded).
 %% Ctx -> {NrOfSubs, DeviceBytes}
 stats(_Ctx) -> erlang:nif_error(nif_not_loaded).

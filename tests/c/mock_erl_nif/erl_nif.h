@@ -1,5 +1,5 @@
 /*
- * erl_nif.h — a TEST DOUBLE of the documented erl_nif API (OTP 21+), just
+ * erl_nif.h — a TEST DOUBLE of the documented erl_nif API (OTP 19.3+), just
  * the part integration/c_src/vmqg_nif.c uses, so that the NIF glue is
  * compiled with -Wall -Werror and run by tests/c/nif_mock_check.c
  * (tests/test_nif_layer.py).  OTP is not in this image; this is not the OTP
@@ -50,6 +50,19 @@ typedef struct {
     return &e;                                                                                \
   }
 
+typedef struct {
+  int driver_major_version, driver_minor_version;
+  char* erts_version;
+  char* otp_release;
+  int thread_support, smp_support, async_threads, scheduler_threads, nif_major_version, nif_minor_version;
+  int dirty_scheduler_support;
+} ErlNifSysInfo;
+void enif_system_info(ErlNifSysInfo* sip, size_t si_size);
+/* mock: runs fp at once on the calling thread (no scheduler to hand it to) */
+ERL_NIF_TERM enif_schedule_nif(ErlNifEnv* env, const char* fun_name, int flags,
+                               ERL_NIF_TERM (*fp)(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]), int argc,
+                               const ERL_NIF_TERM argv[]);
+
 /* memory */
 void* enif_alloc(size_t size);
 void* enif_realloc(void* ptr, size_t size);
@@ -64,12 +77,15 @@ ERL_NIF_TERM enif_make_tuple4(ErlNifEnv* env, ERL_NIF_TERM a, ERL_NIF_TERM b, ER
 ERL_NIF_TERM enif_make_list_from_array(ErlNifEnv* env, const ERL_NIF_TERM arr[], unsigned cnt);
 ERL_NIF_TERM enif_make_string(ErlNifEnv* env, const char* string, ErlNifCharEncoding encoding);
 ERL_NIF_TERM enif_make_uint64(ErlNifEnv* env, uint64_t i);
+ERL_NIF_TERM enif_make_uint(ErlNifEnv* env, unsigned i);
+ERL_NIF_TERM enif_make_tuple_from_array(ErlNifEnv* env, const ERL_NIF_TERM arr[], unsigned cnt);
 ERL_NIF_TERM enif_make_badarg(ErlNifEnv* env);
 ERL_NIF_TERM enif_make_copy(ErlNifEnv* dst_env, ERL_NIF_TERM src_term);
 ERL_NIF_TERM enif_make_resource(ErlNifEnv* env, void* obj);
 
 /* term inspection */
 int enif_get_int(ErlNifEnv* env, ERL_NIF_TERM term, int* ip);
+int enif_get_uint(ErlNifEnv* env, ERL_NIF_TERM term, unsigned* ip);
 int enif_get_tuple(ErlNifEnv* env, ERL_NIF_TERM term, int* arity, const ERL_NIF_TERM** array);
 int enif_get_list_length(ErlNifEnv* env, ERL_NIF_TERM term, unsigned* len);
 int enif_get_list_cell(ErlNifEnv* env, ERL_NIF_TERM list, ERL_NIF_TERM* head, ERL_NIF_TERM* tail);

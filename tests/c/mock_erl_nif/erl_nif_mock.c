@@ -107,6 +107,11 @@ ERL_NIF_TERM enif_make_string(ErlNifEnv* env, const char* s, ErlNifCharEncoding 
   return l;
 }
 ERL_NIF_TERM enif_make_uint64(ErlNifEnv* env, uint64_t i) { (void)env; return make_int((int64_t)i); }
+ERL_NIF_TERM enif_make_uint(ErlNifEnv* env, unsigned i) { (void)env; return make_int((int64_t)i); }
+ERL_NIF_TERM enif_make_tuple_from_array(ErlNifEnv* env, const ERL_NIF_TERM arr[], unsigned cnt) {
+  (void)env;
+  return make_tuple(cnt, arr);
+}
 ERL_NIF_TERM enif_make_badarg(ErlNifEnv* env) { return enif_make_atom(env, "$badarg_exception"); }
 ERL_NIF_TERM enif_make_copy(ErlNifEnv* dst_env, ERL_NIF_TERM src_term) { (void)dst_env; return src_term; }
 ERL_NIF_TERM enif_make_resource(ErlNifEnv* env, void* obj) {
@@ -121,6 +126,12 @@ int enif_get_int(ErlNifEnv* env, ERL_NIF_TERM term, int* ip) {
   (void)env;
   if (C(term)->type != T_INT) return 0;
   *ip = (int)C(term)->i;
+  return 1;
+}
+int enif_get_uint(ErlNifEnv* env, ERL_NIF_TERM term, unsigned* ip) {
+  (void)env;
+  if (C(term)->type != T_INT || C(term)->i < 0 || C(term)->i > 0xFFFFFFFFll) return 0;
+  *ip = (unsigned)C(term)->i;
   return 1;
 }
 int enif_get_tuple(ErlNifEnv* env, ERL_NIF_TERM term, int* arity, const ERL_NIF_TERM** array) {
@@ -285,6 +296,20 @@ int enif_get_resource(ErlNifEnv* env, ERL_NIF_TERM term, ErlNifResourceType* typ
   if (c->type != T_RES || ((res_hdr*)c->res - 1)->type != type) return 0;
   *objp = c->res;
   return 1;
+}
+
+void enif_system_info(ErlNifSysInfo* sip, size_t si_size) {
+  memset(sip, 0, si_size);
+  sip->nif_major_version = 2;
+  sip->nif_minor_version = 11;   /* OTP 19 */
+  sip->dirty_scheduler_support = getenv("MOCK_NO_DIRTY") ? 0 : 1;
+}
+ERL_NIF_TERM enif_schedule_nif(ErlNifEnv* env, const char* fun_name, int flags,
+                               ERL_NIF_TERM (*fp)(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]), int argc,
+                               const ERL_NIF_TERM argv[]) {
+  (void)fun_name;
+  if (flags & ~(ERL_NIF_DIRTY_JOB_IO_BOUND | ERL_NIF_DIRTY_JOB_CPU_BOUND)) return enif_make_badarg(env);
+  return fp(env, argc, argv);
 }
 
 /* ---- for the check program ---------------------------------------------- */

@@ -14,7 +14,8 @@
  *   C <add|del> <node> <qos> <filter>   a change of the open event ("!" filter: [] , an invalid topic)
  *   A                                   apply_many(Ctx, the events since the last A / S)
  *   S                                   apply(Ctx, SubscriberId, Changes) per event since the last A / S
- *   P <mp> <topic>                      a publish
+ *   P <mp> <topic>                      a publish: its Topic word list (split on '/'; "%2F" a '/'
+ *                                       inside a word, "~x" the atom x, "!" the empty list)
  *   M <records|ranges>                  match(Ctx, Batch, every publish so far, Mode)
  *   T                                   stats(Ctx)
  * output: "A <result>", "S <result>...", "T <subs>", "M <n>" then per
@@ -56,6 +57,30 @@ static ERL_NIF_TERM topic_term(const char* f) {
     const char* e = strchr(s, '/');
     const size_t l = e ? (size_t)(e - s) : strlen(s);
     w[n++] = mock_make_binary(s, l);
+    if (!e || n == 256) break;
+    s = e + 1;
+  }
+  return enif_make_list_from_array(env, w, n);
+}
+/* a publish's Topic list: words split on '/', "%2F" a '/' inside a word,
+ * a word "~name" the atom name (a list element that is not a binary), "!"
+ * the empty list */
+static ERL_NIF_TERM pub_topic_term(const char* f) {
+  if (!strcmp(f, "!")) return enif_make_list_from_array(env, NULL, 0);
+  ERL_NIF_TERM w[256];
+  unsigned n = 0;
+  const char* s = f;
+  for (;;) {
+    const char* e = strchr(s, '/');
+    const size_t l = e ? (size_t)(e - s) : strlen(s);
+    char buf[4096];
+    size_t k = 0;
+    for (size_t i = 0; i < l && k < sizeof buf; i++) {
+      if (s[i] == '%' && i + 2 < l + 0 && s[i + 1] == '2' && (s[i + 2] == 'F' || s[i + 2] == 'f')) { buf[k++] = '/'; i += 2; }
+      else buf[k++] = s[i];
+    }
+    if (k && buf[0] == '~') { buf[k] = 0; w[n++] = enif_make_atom(env, buf + 1); }
+    else w[n++] = mock_make_binary(buf, k);
     if (!e || n == 256) break;
     s = e + 1;
   }
@@ -197,7 +222,7 @@ int main(int argc, char** argv) {
       nev = 0;
     } else if (line[0] == 'P') {
       if (sscanf(line + 2, "%63s %4095s", a1, topic) != 2) return 8;
-      const ERL_NIF_TERM el[2] = {mp_term(a1), mock_make_binary(topic, strlen(topic))};
+      const ERL_NIF_TERM el[2] = {mp_term(a1), pub_topic_term(topic)};
       pubs = (ERL_NIF_TERM*)realloc(pubs, (npubs + 1) * sizeof(ERL_NIF_TERM));
       pubs[npubs++] = mock_make_tuple(2, el);
     } else if (line[0] == 'M') {
