@@ -636,33 +636,42 @@ def bench_other(args):
 
     # roofline of the dominant kernel: COUNT with SURVEY §8(d)'s lookup bytes
     # 8(L+1) + 16 S_p (S_p from the oracle's counters on the sample), or EMIT
-    # with 32 B per emission (16-B record read + 16-B written).  When the EMIT
-    # tail outweighs the fast EMIT (R2: one publish of 4,096,000 records,
-    # copied by every wave of the tail), the two EMIT launches are priced
-    # together: between them they write every emission.
+    # with its compulsory bytes: 16 B written per emission, the 8-B offset and
+    # the 32-B key cache per publish (the records it copies are read from
+    # lists that many publishes share, so they are not priced per emission;
+    # SURVEY's 32 B per emission is reported beside as survey_model_*).  When
+    # the EMIT tail outweighs the fast EMIT (R2: one publish of 4,096,000
+    # records, copied by every wave of the tail), the two EMIT launches are
+    # priced together.  frac_physical = the PMC HBM bytes of the same build
+    # (profiles/pmc_<config>.json) over the same time.
     roof = None
     tail_ns = stages["emit_wave"] * 1e3 if stages else 0.0
     if count_ns or emit_ns:
         pmc = "pmc_%s.json" % args.config.lower()
+        survey = None
         if count_ns >= emit_ns + tail_ns:
             alg = b_p["lookup"] * npub if b_p else None
             kern, ns, model = "k_match_fast<0,...> (COUNT)", count_ns, "8(L+1) + 16 S_p per publish, S_p averaged " \
                                                                       "over the oracle sample"
             traffic = load_pmc_traffic("k_match_fast<0", pmc)
         elif emit_ns >= tail_ns:
-            alg = 32 * em
-            kern, ns, model = "EMIT", emit_ns, "32 B per emission (16-B record read + 16-B written)"
+            alg, survey = 16 * em + 40 * npub, 32 * em
+            kern, ns = "k_match_fast<1,...> (EMIT)", emit_ns
+            model = "16 B written per emission + 8-B offset and 32-B key cache per publish"
             traffic = load_pmc_traffic("k_match_fast<1", pmc)
         else:
-            alg = 32 * em
+            alg, survey = 16 * em + 40 * npub, 32 * em
             kern, ns = "EMIT + EMIT tail (k_match_fast<1> + k_match_wave<1>, per call)", emit_ns + tail_ns
-            model = "32 B per emission (16-B record read + 16-B written), both EMIT launches of a call"
+            model = "16 B written per emission + 8-B offset and 32-B key cache per publish, both EMIT launches"
             t1, t2 = load_pmc_traffic("k_match_fast<1", pmc), load_pmc_traffic("k_match_wave<1", pmc)
             traffic = t1 + t2 if t1 is not None and t2 is not None else None
         ach = alg / ns if alg else None
         roof = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": traffic,
-                "kernel": kern, "algorithmic_bytes_per_launch": alg, "bytes_model": model}
+                "frac_physical": traffic / ns / PEAK_HBM_GBS if traffic else None,
+                "kernel": kern, "kernel_us": ns / 1e3, "algorithmic_bytes_per_launch": alg, "bytes_model": model,
+                "survey_model_bytes": survey,
+                "survey_model_frac": survey / ns / PEAK_HBM_GBS if survey else None}
     print(json.dumps({
         "metric": "publishes/sec (config %s)" % args.config, "value": npub * args.steps / el, "unit": "publishes/s",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps,
