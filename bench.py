@@ -77,6 +77,13 @@ def load_pmc_traffic(kernel: str, summary: str = "pmc_latest.json"):
     return max(cands, key=lambda v: v.get("total_ns", 0))["hbm_bytes_per_launch"]
 
 
+def apply_opts(view, args):
+    """--vmqg-opt NAME=VALUE knobs (vmqg_set_option: tuning only)."""
+    for kv in args.vmqg_opt:
+        k, v = kv.split("=", 1)
+        view.set_option(k, int(v))
+
+
 def launch_ranks(args):
     """`--gpus N` without a launcher: start N rank processes of this script
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set
@@ -141,6 +148,8 @@ def main():
     ap.add_argument("--force-device", type=int, default=-1, help="rehearsal: every rank on this device")
     ap.add_argument("--churn-batch", type=int, default=10_000)
     ap.add_argument("--churn-rate-batches", type=float, default=10.0, help="delta batches per second (1%%/s at 10M)")
+    ap.add_argument("--vmqg-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="vmqg_set_option on every matcher context (A/B runs; results unchanged)")
     args = ap.parse_args()
     rc = launch_ranks(args)
     if rc is not None:
@@ -205,6 +214,7 @@ def main():
         dist.broadcast(pw_t, 0)
         pwid = pw_t.cpu().numpy()
         log("rank %d: trie image %.1f MB replicated" % (rank, nbytes / 1e6))
+    apply_opts(view, args)
 
     pubs, words = w.publish_arrays_ids(pwid, np.array([0], dtype=np.uint32))
     npub = len(pubs)
@@ -519,6 +529,7 @@ def bench_other(args):
     fast_g = args.fast_g
     if fast_g:
         view.set_option("fast_g", fast_g)
+    apply_opts(view, args)
     st = view.stats_raw()
     log("config %s: %d subs generated in %.1fs, loaded in %.1fs (host engine %.1fs), %s"
         % (args.config, n, gen_s, load_s, st["apply_host_ns"] / 1e9, st))
@@ -756,6 +767,7 @@ def bench_d(args):
         dist.broadcast(pw_t, 0)
         pwid = pw_t.cpu().numpy()
         log("rank %d: config D image %.1f MB replicated" % (rank, nbytes / 1e6))
+    apply_opts(view, args)
     pubs, words = w.publish_arrays_ids(pwid, np.array([0], dtype=np.uint32))
     npub = len(pubs)
     pubs0 = pubs

@@ -106,6 +106,22 @@ def test_config_full_parity(cfg, mode):
     assert sum(len(x) for x in got) > n // 10   # the workload does match
 
 
+@pytest.mark.parametrize("exfilter", [0, 1])
+def test_exact_filter_modes_give_the_same_answers(exfilter):
+    """The exbits filter only decides whether the exact table is probed:
+    forced off and forced on, config A equals the oracle publish for publish
+    (the default, auto, is what every other test runs)."""
+    from vernemq_amd import workloads as W
+    w = W.CONFIGS["A"]()
+    v, orc = _load_both(w)
+    v.set_option("exfilter", exfilter)
+    n = w.n_pubs
+    got = _gpu_canon(v, w, 0, n)
+    want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in range(n)])
+    bad = [i for i in range(n) if got[i] != sorted(want[i])]
+    assert not bad, (len(bad), w.pub_topic(bad[0]))
+
+
 def test_store_policies_write_the_same_records():
     """Both EMIT store policies (vmqg_set_option "nt_stores": non-temporal,
     the default, and plain) write the same bytes; the default is checked

@@ -643,6 +643,9 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   } else if (n == "groups") {
     if (value < 0 || value > 1) return VMQG_E_INVAL;
     e.opt_groups = (uint32_t)value;
+  } else if (n == "exfilter") {
+    if (value < 0 || value > 2) return VMQG_E_INVAL;
+    e.opt_exfilter = (uint32_t)value;
   } else if (n == "dd_g") {
     if (value != 1 && value != 4) return VMQG_E_INVAL;
     e.opt_dd_g = (uint32_t)value;

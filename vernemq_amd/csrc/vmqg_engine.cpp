@@ -71,7 +71,8 @@ int Engine::init(const vmqg_config& c) {
     // before each call (whether to launch the claim pass)
     if (hipHostMalloc((void**)&h_ddmode, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
       return VMQG_E_NOMEM;
-    *h_ddmode = 0;
+    h_ddmode[0] = 0;
+    h_ddmode[1] = 0;
     if (hipHostGetDevicePointer((void**)&d_ddmode_host, h_ddmode, 0) != hipSuccess) return VMQG_E_DEVICE;
     for (Stage& sg : stage)
       if (hipEventCreateWithFlags(&sg.ev, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
@@ -1107,6 +1108,9 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
       dd_gap = std::min<uint64_t>(dd_gap * 2, 8192);
     }
   }
+  // the exbits filter: on until the device's counters say most lookups pass it
+  const uint32_t xm = reinterpret_cast<volatile uint32_t*>(h_ddmode)[1];
+  a.exfilter = opt_exfilter == 2 ? (xm == 2u ? 0u : 1u) : opt_exfilter;
   a.dd_force = claimed ? 1u : 0u;
   a.dd_claimed = claimed;
   a.dd_g = opt_dd_g;

@@ -17,7 +17,8 @@ struct MatchArgs {
   const uint32_t* exwords;
   const uint32_t* exbits; uint64_t exbits_mask;   // exact-topic filter (bits - 1)
   uint32_t max_mp, local_node;
-  const vmqg_pub* pubs; const uint32_t* words; uint32_t npub, pad0;
+  const vmqg_pub* pubs; const uint32_t* words; uint32_t npub;
+  uint32_t exfilter;                              // 1: test the exbits filter before the exact table (auto, see exmode)
   uint64_t* offsets;                              // npub + 1
   void* keycache;                                 // npub x 32 B (COUNT -> EMIT)
   uint64_t* chunk;                                // per chunk of gpw publishes: COUNT's total, then its output base
@@ -51,7 +52,8 @@ struct MatchArgs {
   void* groups; uint64_t gs_mask;                 // output groups (records mode): 256-B slots, tagged by dd_tag
   uint64_t* ddmask;                               // per chunk: its duplicates (COUNT -> the fix-up)
   uint32_t dd_claimed, dd_g;                      // dedupe on this call; lanes per representative in COUNT (1|2|4)
-  uint32_t* dd_host;                              // host-mapped word: the dedupe mode for the next calls
+  uint32_t* dd_host;                              // host-mapped words: [0] the dedupe mode, [1] the exbits-filter
+                                                  // mode for the next calls
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records

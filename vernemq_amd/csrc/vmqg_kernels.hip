@@ -127,6 +127,9 @@ enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, k
                   kStHuge = 11 /* huge publishes listed for the tail */,
                   kStGrouped = 12 /* publishes in output groups */,
                   kStReps = 13 /* dedupe on: publishes COUNT walks (list 2) */,
+                  kStExTry = 14 /* COUNT's fast pass: publishes that looked up their exact topic */,
+                  kStExPass = 15 /* ... of those, the exbits filter let probe the table */,
+                  kStExHit = 16 /* ... of those, found their topic */,
                   kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
 #define VMQG_WIDE_RECORDS 0x7fffffff   // A/B: a publish with at least this many records is wide too (256: config D 2,724 vs 2,526 us per batch, off)
@@ -331,18 +334,26 @@ __device__ __forceinline__ uint64_t publish_fp(const vmqg_pub& pub, const uint32
 
 // The exact slot of (MP, Topic), or null: fingerprint probe, then the MP and
 // words compared group-parallel — the slot holds the first 7 words (one
-// 128-B line verifies a topic of <= 7 words), exwords the rest.
+// 128-B line verifies a topic of <= 7 words), exwords the rest.  `xst`
+// (COUNT's fast pass counts it): 1 looked up, 2 the table probed, 4 found.
+// The exbits filter (a.exfilter) saves the table's line for a publish with
+// no exact topic but costs its own line for one with; the COUNT wave tier
+// turns it off while most lookups pass it and on while most miss (exmode).
 template <int G>
 __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, const uint32_t* w, uint32_t wreg,
-                                       const Group<G>& g) {
+                                       const Group<G>& g, uint32_t& xst) {
   const uint32_t L = pub.nwords;
   bool wild;
   const uint64_t fp = publish_fp<G>(pub, w, wreg, g, wild);
+  xst = wild ? 0u : 1u;
 #if VMQG_EXACT_FILTER
   // the filter's bit (an L2-resident word) before the table's random line
-  const uint64_t xb = exbit_of(fp, a.exbits_mask + 1);
-  if (!wild && !((a.exbits[xb >> 5] >> (xb & 31)) & 1u)) return nullptr;
+  if (a.exfilter && !wild) {
+    const uint64_t xb = exbit_of(fp, a.exbits_mask + 1);
+    if (!((a.exbits[xb >> 5] >> (xb & 31)) & 1u)) return nullptr;
+  }
 #endif
+  xst |= 2u;
   uint64_t b = fp & a.exact_mask;
   for (uint64_t iter = 0; iter <= a.exact_mask; iter++) {
     const ExactSlot* bk = a.exact + b * kExactSlotsPerBucket;
@@ -352,12 +363,15 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
       const uint32_t nw = e.nwords;
       if (nw == kEmpty) { seen_empty = true; break; }
       if (e.fp != fp || (nw & ~kExactHigh) != L || e.mp != pub.mountpoint) continue;
+      // inline words, then the rest (two loops: one loop selecting between
+      // the two loads costs the one-lane COUNT 16 B of scratch spills)
       bool diff = false;
-      for (uint32_t i = g.lane; i < L; i += G) {
-        const uint32_t x = i < (uint32_t)G ? wreg : w[i];
-        diff |= (i < kExactInline ? e.w[i] : a.exwords[e.words_off + (i - kExactInline)]) != x;
-      }
-      if (g.ballot(diff) == 0) return &e;
+      const uint32_t Li = L < kExactInline ? L : kExactInline;
+      for (uint32_t i = g.lane; i < Li; i += G) diff |= e.w[i] != (i < (uint32_t)G ? wreg : w[i]);
+      uint32_t i1 = g.lane;
+      if (i1 < kExactInline) i1 += (kExactInline - i1 + G - 1) / G * G;
+      for (uint32_t i = i1; i < L; i += G) diff |= a.exwords[e.words_off + (i - kExactInline)] != (i < (uint32_t)G ? wreg : w[i]);
+      if (g.ballot(diff) == 0) { xst |= 4u; return &e; }
     }
     if (seen_empty) break;
     b = (b + 1) & a.exact_mask;
@@ -395,6 +409,7 @@ struct Matched {
   bool walk_ovf;                        // ... because the frontier or candidate list overflowed
   bool many;                            // more keys than the key list holds: totals only (nk, keys unset);
   uint32_t nc, ex_off, ex_cnt;          // the candidates stay in the LDS list, the exact key is {ex_off, ex_cnt}
+  uint32_t xst;                         // find_exact's lookup bits (1 looked up, 2 probed, 4 found)
 };
 
 // Records and non-empty keys of one multi-key candidate (its keylist ids ->
@@ -422,7 +437,7 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
   const bool mp_ok = pub.mountpoint < a.max_mp;   // L == 0: the root alone (trie_match/4 :361-363)
   // lane i of the group keeps word i (i < G); deeper words come from memory
   const uint32_t wreg = g.lane < L ? w[g.lane] : kUnknownWord;
-  Matched m{0, 0, 0, 0, 0, false, false, false, 0, 0, 0};
+  Matched m{0, 0, 0, 0, 0, false, false, false, 0, 0, 0, 0};
   uint32_t nc = 0, sp = 0;
   if (mp_ok) {
     if (g.lane == 0) s.st(0) = make_uint2(pub.mountpoint, kHasAll << 28);   // {MP, root}: probe all
@@ -519,7 +534,7 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
 
   // ---- the exact candidate {Topic, node()} and remote exact subscribers (:62, :514-520)
   if (!m.overflow && mp_ok) {
-    const ExactSlot* e = find_exact<G>(a, pub, w, wreg, g);
+    const ExactSlot* e = find_exact<G>(a, pub, w, wreg, g, m.xst);
     if (e) {
       const uint4 q = *reinterpret_cast<const uint4*>(&e->off);   // {off, count, rmask lo, hi}
       rmask |= ((uint64_t)q.w << 32) | q.z;
@@ -678,21 +693,37 @@ __device__ bool group_insert(const MatchArgs& a, uint64_t sig64, uint32_t p) {
 // block at the end (a full buffer falls back to the global counter).
 constexpr uint32_t kDefBuf = 510;
 struct CountAgg {
-  uint32_t many, walkovf, grouped, tried;   // per-block sums of the status counters
+  uint32_t many, walkovf, grouped, extry;   // per-block sums of the status counters
   uint32_t ndef, base;                      // buffered deferred publishes; their list-0 base
-  uint32_t dups, pad;
+  uint32_t expass, exhit;                   // exact lookups: probed, found (extry: looked up)
   uint32_t def[kDefBuf];
 };
+
+// The exact-lookup bits of a wave's groups (find_exact's xst on each
+// group's lane 0) into the block's counters: three ballots, one LDS atomic each.
+template <int G>
+__device__ __forceinline__ void count_exact(CountAgg* agg, const Group<G>& g, bool valid, uint32_t xst) {
+  const bool l0 = valid && g.lane == 0;
+  const uint32_t nt = (uint32_t)__popcll(__ballot(l0 && (xst & 1u)));
+  const uint32_t np = (uint32_t)__popcll(__ballot(l0 && (xst & 3u) == 3u));
+  const uint32_t nh = (uint32_t)__popcll(__ballot(l0 && (xst & 5u) == 5u));
+  if (__lane_id() == 0 && nt) {
+    atomicAdd(&agg->extry, nt);
+    atomicAdd(&agg->expass, np);
+    atomicAdd(&agg->exhit, nh);
+  }
+}
 
 // FEAT: batch dedupe and output groups compiled in (the COUNT variant the
 // host picks when either is on: their code costs the lean variant scratch
 // spills, 79 -> 90 us on config C)
 template <int G, int OUT, bool RETRY = false, uint32_t SL = kWaves * (64 / G), bool FEAT = true>
 __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G, SL>& s, const Group<G>& g,
-                                  uint32_t& fl, CountAgg* agg = nullptr) {
+                                  uint32_t& fl, CountAgg* agg = nullptr, uint32_t* xst = nullptr) {
   const vmqg_pub pub = a.pubs[p];
   const Matched m = walk_publish<G, SL>(a, pub, s, g);
   fl = 0;
+  if (xst) *xst = m.xst;
   // wide publishes — more keys than the spill slots hold — are written by a
   // whole wave in the EMIT tail launch, expanded again from their candidates
   const bool many = !m.overflow && (m.many || m.nk > VMQG_SPILL_KEYS || m.ksum >= VMQG_WIDE_RECORDS);
@@ -1257,7 +1288,8 @@ struct WaveWalk {
     }
     flush_cands();
     if (mp_ok) {
-      const ExactSlot* e = find_exact<64>(a, pub, w, wreg, g);
+      uint32_t xst;
+      const ExactSlot* e = find_exact<64>(a, pub, w, wreg, g, xst);
       if (e) {
         const uint32_t nw = e->nwords;
         rm |= e->rmask;
@@ -1532,12 +1564,13 @@ void k_match_fast(MatchArgs a) {
       const uint32_t* R = a.deferred + 2ull * a.npub;
       for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < nr; base += stride) {
         const uint32_t n = nr - base < (uint32_t)GPW ? nr - base : (uint32_t)GPW;
-        uint32_t fl = 2, p = 0;
+        uint32_t fl = 2, p = 0, xst = 0;
         uint64_t c = 0;
         if (g.gidx < n) {
           p = R[base + g.gidx];
-          c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, p, s, g, fl, agg);
+          c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, p, s, g, fl, agg, &xst);
         }
+        count_exact<G>(agg, g, g.gidx < n, xst);
         if (g.gidx < n && g.lane == 0) {
           const uint32_t ch = p / a.gpw;
           if (c) atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + ch), (unsigned long long)c);
@@ -1561,8 +1594,9 @@ void k_match_fast(MatchArgs a) {
     if (MODE == 0) {
       if (FEAT && a.dd_claimed) break;   // the representatives' loop above did the work
       uint64_t c = 0;
-      uint32_t fl = 0;
-      if (g.gidx < n) c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, base + g.gidx, s, g, fl, agg);
+      uint32_t fl = 0, xst = 0;
+      if (g.gidx < n) c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, base + g.gidx, s, g, fl, agg, &xst);
+      count_exact<G>(agg, g, g.gidx < n, xst);
       // the chunk's total (publishes the wave tier takes add theirs later)
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
@@ -1588,6 +1622,11 @@ void k_match_fast(MatchArgs a) {
     if (threadIdx.x == 64 && agg->many) atomicAdd(&a.status[kStMany], agg->many);
     if (threadIdx.x == 128 && agg->walkovf) atomicAdd(&a.status[kStWalkOvf], agg->walkovf);
     if (threadIdx.x == 192 && agg->grouped) atomicAdd(&a.status[kStGrouped], agg->grouped);
+    if (threadIdx.x == 32 && agg->extry) {
+      atomicAdd(&a.status[kStExTry], agg->extry);
+      atomicAdd(&a.status[kStExPass], agg->expass);
+      atomicAdd(&a.status[kStExHit], agg->exhit);
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) a.deferred[agg->base + i] = agg->def[i];
   }
@@ -1638,6 +1677,16 @@ void k_match_wave(MatchArgs a) {
         const uint32_t mode = dups * 2u > tried ? 1u : 0u;
         *a.dd_mode = mode;
         if (a.dd_host) *a.dd_host = mode;   // host-mapped: the host reads it before its next calls
+      }
+    }
+    // the exbits filter for the next calls: off while more than 3/4 of the
+    // lookups pass it (its line is then an extra line per publish: R1), on
+    // while fewer than half find their topic (C: none has one)
+    if (gw == 0 && lane == 1 && a.dd_host) {
+      const uint32_t t = a.status[kStExTry], q = a.status[kStExPass], h = a.status[kStExHit];
+      if (t >= 4096) {
+        const uint32_t mode = a.exfilter ? (q * 4u > t * 3u ? 0u : 1u) : (h * 2u < t ? 1u : 0u);
+        a.dd_host[1] = mode + 2u;   // 2 off, 3 on (0: never decided)
       }
     }
     // COUNT's deferred publishes (list 0), sixteen per wave, then the
