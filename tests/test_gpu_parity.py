@@ -122,6 +122,32 @@ def test_exact_filter_modes_give_the_same_answers(exfilter):
     assert not bad, (len(bad), w.pub_topic(bad[0]))
 
 
+@pytest.mark.parametrize("heavy_min", [2, 40])
+def test_heavy_publishes_copied_by_xcd_write_the_same_bytes(heavy_min):
+    """Heavy publishes (vmqg_set_option "heavy_min": >= that many records
+    from <= 2 keys) are copied by the EMIT tail on the XCD their first key
+    hashes to instead of by the fast EMIT: the output is byte-identical to
+    heavy_min 0 and equal to the oracle (config A, records mode), with dedupe
+    off and on (duplicates take their representative's bucket)."""
+    from vernemq_amd import workloads as W
+    w = W.CONFIGS["A"]()
+    v, orc = _load_both(w)
+    pubs, words = w.publish_arrays(v)
+    outs = []
+    for hm, dd in ((0, 0), (heavy_min, 0), (heavy_min, 1)):
+        v.set_option("heavy_min", hm)
+        v.set_option("dedupe", dd)
+        recs, offs = v.match_arrays(pubs, words)
+        outs.append((np.asarray(offs).copy(), np.asarray(recs).view(np.uint8).copy()))
+    for o in outs[1:]:
+        assert np.array_equal(o[0], outs[0][0]) and np.array_equal(o[1], outs[0][1])
+    n = w.n_pubs
+    got = _gpu_canon(v, w, 0, n)
+    want = orc.fold_batch([(w.mps[w.pub_mp[i]], b"pub", w.pub_topic(i)) for i in range(n)])
+    assert all(got[i] == sorted(want[i]) for i in range(n))
+    assert int((np.diff(outs[0][0].astype(np.int64)) >= heavy_min).sum()) > 100   # the path is exercised
+
+
 def test_store_policies_write_the_same_records():
     """Both EMIT store policies (vmqg_set_option "nt_stores": non-temporal,
     the default, and plain) write the same bytes; the default is checked

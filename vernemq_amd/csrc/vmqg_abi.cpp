@@ -643,6 +643,9 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   } else if (n == "groups") {
     if (value < 0 || value > 1) return VMQG_E_INVAL;
     e.opt_groups = (uint32_t)value;
+  } else if (n == "heavy_min") {
+    if (value < 0 || value > (1 << 30)) return VMQG_E_INVAL;
+    e.opt_heavy_min = (uint32_t)value;
   } else if (n == "exfilter") {
     if (value < 0 || value > 2) return VMQG_E_INVAL;
     e.opt_exfilter = (uint32_t)value;

@@ -976,7 +976,8 @@ int Engine::ensure_match_scratch(uint64_t npub, hipStream_t st) {
     // 32-B key cache + kSpillKeys x 8-B spilled keys per publish, then the
     // chunk totals (one per 16, 32 or 64 publishes, + 1), per chunk a 64-bit
     // wide-publish mask, then one fast-pass bit per publish
-    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + 3 * (cap / 16 + 2) * 8 + (cap / 32 + 2) * 4) != hipSuccess)
+    // ... then a heavy-publish bucket byte per publish
+    if (hipMalloc(&d_keycache, cap * (32 + 8 * 8) + 3 * (cap / 16 + 2) * 8 + (cap / 32 + 2) * 4 + cap + 64) != hipSuccess)
       return VMQG_E_NOMEM;
     // publish lists: retry, whole-wave walks, duplicates, their slots, huge (vmqg_kernels.hip kLists)
     if (hipMalloc(&d_deferred, 5 * cap * sizeof(uint32_t)) != hipSuccess) return VMQG_E_NOMEM;
@@ -1083,6 +1084,8 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.widemask = a.chunk + (keycache_cap / 16 + 2);
   a.ddmask = a.widemask + (keycache_cap / 16 + 2);
   a.fastdone = reinterpret_cast<uint32_t*>(a.ddmask + (keycache_cap / 16 + 2));
+  a.heavybyte = reinterpret_cast<uint8_t*>(a.fastdone + (keycache_cap / 32 + 2));
+  a.heavy_min = opt_heavy_min;
   a.dd_key = static_cast<uint64_t*>(d_dd);
   a.dd_rep = reinterpret_cast<uint32_t*>(static_cast<char*>(d_dd) + dd_slots * 8);
   a.dd_mask = dd_slots - 1;

@@ -310,6 +310,7 @@ struct Engine {
   uint32_t opt_dd_g = 4;                                   // vmqg_set_option "dd_g": lanes per representative (1|4)
   uint32_t opt_groups = 0;                                 // vmqg_set_option "groups": 0 off (default: A/B, DESIGN), 1 on
   uint32_t opt_exfilter = 2;                               // vmqg_set_option "exfilter": 0 off, 1 on, 2 auto (default)
+  uint32_t opt_heavy_min = 0;                              // vmqg_set_option "heavy_min": records mode, EMIT tail by XCD (0 off)
   // host-buffer match staging
   void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
   void* d_words = nullptr; uint64_t d_words_cap = 0;

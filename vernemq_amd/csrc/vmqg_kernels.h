@@ -52,6 +52,8 @@ struct MatchArgs {
   void* groups; uint64_t gs_mask;                 // output groups (records mode): 256-B slots, tagged by dd_tag
   uint64_t* ddmask;                               // per chunk: its duplicates (COUNT -> the fix-up)
   uint32_t dd_claimed, dd_g;                      // dedupe on this call; lanes per representative in COUNT (1|2|4)
+  uint8_t* heavybyte;                             // per publish: 1 + its first key's bucket if heavy, else 0
+  uint32_t heavy_min, pad3;                       // records mode: heavy publishes have >= this many records (0 off)
   uint32_t* dd_host;                              // host-mapped words: [0] the dedupe mode, [1] the exbits-filter
                                                   // mode for the next calls
 };

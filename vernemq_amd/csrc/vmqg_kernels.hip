@@ -106,6 +106,18 @@ constexpr uint32_t kHugeSeg = 64 * 8 * 4;     // records per tail wave and segme
 constexpr uint32_t kGroupMin = VMQG_GROUP_MIN;
 constexpr uint32_t kGroupCap = 60;
 constexpr uint32_t kGroupFlag = 0x20000000u;  // key cache word 1 (nk <= 2): a grouped publish, the tail writes it
+// Heavy publishes (records mode, a.heavy_min > 0): >= heavy_min records from
+// <= 2 keys.  Their sources are lists many publishes share (config D: site
+// s's 1,000 alarm records for every site/s/x/alarm/z publish); copied by the
+// fast EMIT, each is fetched into whichever XCD's L2 the chunk lands on, so
+// every XCD pulls every list (3.4 GB fetched for 4.2 GB written per batch).
+// COUNT buckets them by their first key (kXcds buckets, one per XCD: a byte
+// per publish, 1 + bucket, 0 for the others) and the EMIT tail's blocks
+// b ≡ x (mod 8) — which run on XCD x (profiles/xcd_probe_r04.txt) — copy
+// bucket x: each list is read into one L2.
+constexpr uint32_t kHeavyFlag = 0x10000000u;  // key cache word 1 (nk <= 2): a heavy publish, the tail copies it
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t heavy_bucket(uint32_t off0) { return (off0 * 0x9E3779B1u) >> 29; }   // top 3 bits
 struct alignas(16) GroupSlot {
   unsigned long long word;   // {call tag: 24, signature: 32, members: 8}
   uint32_t pad[2];
@@ -130,6 +142,7 @@ enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, k
                   kStExTry = 14 /* COUNT's fast pass: publishes that looked up their exact topic */,
                   kStExPass = 15 /* ... of those, the exbits filter let probe the table */,
                   kStExHit = 16 /* ... of those, found their topic */,
+                  kStHeavy = 17 /* heavy publishes the EMIT tail copies by XCD */,
                   kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
 #define VMQG_WIDE_RECORDS 0x7fffffff   // A/B: a publish with at least this many records is wide too (256: config D 2,724 vs 2,526 us per batch, off)
@@ -691,11 +704,12 @@ __device__ bool group_insert(const MatchArgs& a, uint64_t sig64, uint32_t p) {
 // tools/atomic_probe.hip, profiles/atomic_probe_r04.jsonl).  The deferred
 // publishes are buffered in LDS and appended to list 0 with one atomic per
 // block at the end (a full buffer falls back to the global counter).
-constexpr uint32_t kDefBuf = 510;
+constexpr uint32_t kDefBuf = 509;
 struct CountAgg {
   uint32_t many, walkovf, grouped, extry;   // per-block sums of the status counters
   uint32_t ndef, base;                      // buffered deferred publishes; their list-0 base
   uint32_t expass, exhit;                   // exact lookups: probed, found (extry: looked up)
+  uint32_t heavy;                           // heavy publishes marked for the EMIT tail
   uint32_t def[kDefBuf];
 };
 
@@ -738,6 +752,7 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
   if (g.lane != 0) return 0;
   uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
   if (m.overflow) {   // a later tier counts it (and writes offsets[p])
+    a.heavybyte[p] = 0;
     const uint32_t k = !RETRY && agg ? atomicAdd(&agg->ndef, 1u) : kDefBuf;   // LDS
     if (k < kDefBuf) {
       agg->def[k] = p;
@@ -752,6 +767,7 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
   }
   const uint32_t total = out_total<OUT>(m);
   a.offsets[p] = total;
+  uint32_t hb = 0;   // 1 + bucket for a heavy publish (heavybyte), else 0
   // key cache: total, nk, remote mask, up to two {record off, count}
   // (3..8 keys: the keys in the spill slots, kc[1].y = their record total;
   // many keys: kc[1] = {candidates, record total, the exact key's off, count})
@@ -779,7 +795,11 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
           group_insert(a, group_sig_keys(w1, m.rmask), p)) {
         hf = kGroupFlag;   // the EMIT tail writes it with its output group: fl 6
         fl = 6;
+      } else if (OUT == 0 && !huge && a.heavy_min && total >= a.heavy_min) {
+        hf = kHeavyFlag;   // the EMIT tail copies it on its first key's XCD: fl 8
+        fl = 8;
       }
+      hb = hf == kHeavyFlag ? 1 + heavy_bucket(k0.x) : 0u;
       kc[0] = make_uint4(total, m.nk | hf, (uint32_t)m.rmask, (uint32_t)(m.rmask >> 32));
       kc[1] = w1;
     } else {
@@ -787,6 +807,7 @@ __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScra
       kc[1] = make_uint4(0, m.ksum, 0, 0);
     }
   }
+  a.heavybyte[p] = (uint8_t)hb;
   return total;
 }
 
@@ -840,7 +861,7 @@ __device__ int resolve(const MatchArgs& a, uint32_t p, const FastScratch<G>& s, 
   uint32_t total;
   if (h.y == kDeferred) return kResSkip;   // written by the wave tier
   const bool many = h.y == kMany;
-  if (!many && (h.y & (kHugeFlag | kGroupFlag))) return kResSkip;   // the EMIT tail writes it (segments / groups)
+  if (!many && (h.y & (kHugeFlag | kGroupFlag | kHeavyFlag))) return kResSkip;   // the EMIT tail writes it
   if (many) {
     total = h.x;
   } else {
@@ -1465,7 +1486,9 @@ __device__ void count_deferred_group(const MatchArgs& a, const FastScratch<4, SL
   wave_sync();
   if (retry) {
     mark_wide<4, true>(a, g, fl, p);
-    const uint32_t n_grp = (uint32_t)__popcll(__ballot(valid && g.lane == 0 && fl >= 5));
+    const uint32_t n_heavy = (uint32_t)__popcll(__ballot(valid && g.lane == 0 && fl == 8));
+    if (lane == 0 && n_heavy) atomicAdd(&a.status[kStHeavy], n_heavy);
+    const uint32_t n_grp = (uint32_t)__popcll(__ballot(valid && g.lane == 0 && (fl == 5 || fl == 6)));
     if (lane == 0 && n_grp) atomicAdd(&a.status[kStGrouped], n_grp);
   }
   // what the retry could not hold (or all, at fast_g 4): one whole-wave walk each
@@ -1550,7 +1573,7 @@ void k_match_fast(MatchArgs a) {
   __shared__ uint32_t agg_raw[MODE == 0 ? sizeof(CountAgg) / 4 : 1];
   CountAgg* agg = MODE == 0 ? reinterpret_cast<CountAgg*>(agg_raw) : nullptr;
   if (MODE == 0) {
-    if (threadIdx.x < 8) (&agg->many)[threadIdx.x] = 0;
+    if (threadIdx.x < 9) (&agg->many)[threadIdx.x] = 0;
     __syncthreads();
   }
   const uint32_t stride = gridDim.x * kWaves * GPW;
@@ -1577,9 +1600,11 @@ void k_match_fast(MatchArgs a) {
           if (fl <= 1 || fl >= 5) atomicOr(a.fastdone + p / 32, 1u << (p % 32));
           if (fl == 1) atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + ch), 1ull << (p % a.gpw));
         }
+        const uint32_t n_heavy = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl == 8));
+        if (__lane_id() == 0 && n_heavy) atomicAdd(&agg->heavy, n_heavy);
         const uint32_t n_many = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl == 1));
         const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl == 2));
-        const uint32_t n_grp = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl >= 5));
+        const uint32_t n_grp = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && (fl == 5 || fl == 6)));
         if (__lane_id() == 0) {
           if (n_many) atomicAdd(&agg->many, n_many);
           if (n_wovf) atomicAdd(&agg->walkovf, n_wovf);
@@ -1602,9 +1627,11 @@ void k_match_fast(MatchArgs a) {
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
       // wide publishes: the chunk's mask for the EMIT tail launch
       mark_wide<G, false>(a, g, fl, base, &agg->many);
+      const uint32_t n_heavy = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl == 8));
+      if (__lane_id() == 0 && n_heavy) atomicAdd(&agg->heavy, n_heavy);
       const uint32_t n_wovf = (uint32_t)__popcll(__ballot(g.lane == 0 && fl == 2));
       if (__lane_id() == 0 && n_wovf) atomicAdd(&agg->walkovf, n_wovf);
-      const uint32_t n_grp = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && fl >= 5));
+      const uint32_t n_grp = (uint32_t)__popcll(__ballot(g.gidx < n && g.lane == 0 && (fl == 5 || fl == 6)));
       if (__lane_id() == 0 && n_grp) atomicAdd(&agg->grouped, n_grp);
     } else if (OUT == 0) {
       emit_wave<G, GPW, NT, VMQG_EMIT_U>(a, base, n, s, g, gm[wv], wv * GPW);
@@ -1622,6 +1649,7 @@ void k_match_fast(MatchArgs a) {
     if (threadIdx.x == 64 && agg->many) atomicAdd(&a.status[kStMany], agg->many);
     if (threadIdx.x == 128 && agg->walkovf) atomicAdd(&a.status[kStWalkOvf], agg->walkovf);
     if (threadIdx.x == 192 && agg->grouped) atomicAdd(&a.status[kStGrouped], agg->grouped);
+    if (threadIdx.x == 96 && agg->heavy) atomicAdd(&a.status[kStHeavy], agg->heavy);
     if (threadIdx.x == 32 && agg->extry) {
       atomicAdd(&a.status[kStExTry], agg->extry);
       atomicAdd(&a.status[kStExPass], agg->expass);
@@ -1773,13 +1801,21 @@ void k_match_wave(MatchArgs a) {
     // L2 after the first member — and then the wide publishes of the chunk
     // masks COUNT left, at the positions EMIT wrote into offsets[]
     bool groups_on = OUT == 0 && uni(a.status[kStGrouped]) != 0;
+    bool heavy_on = OUT == 0 && uni(a.status[kStHeavy]) != 0;
     bool wide_on = uni(a.status[kStMany]) != 0;
     uint64_t written = 0;
-    if (groups_on || wide_on) {
+    if (groups_on || heavy_on || wide_on) {
       const GroupSlot* gs = reinterpret_cast<const GroupSlot*>(a.groups);
       const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
       uint64_t si = gw, cur = 0, m = 0;
       uint32_t j = 0, gn = 0, c = (uint32_t)gw, cc = 0;
+      // heavy publishes: the blocks b = x (mod kXcds) — on XCD x — take the
+      // bucket-x publishes, their waves striding over 64-publish blocks
+      const uint32_t nblk = (a.npub + 63) / 64;
+      const uint32_t hx = blockIdx.x & (kXcds - 1);
+      const uint32_t hstride = (gridDim.x - hx + kXcds - 1) / kXcds * kWaves;
+      uint32_t hc = (blockIdx.x / kXcds) * kWaves + wv, hcc = 0;
+      uint64_t hm = 0;
       for (;;) {
         uint32_t p = 0;
         bool have = false;
@@ -1793,6 +1829,22 @@ void k_match_wave(MatchArgs a) {
           }
           if (j < gn) { p = uni(gs[cur].m[j]); j++; have = true; }
           else groups_on = false;
+        }
+        if (!have && heavy_on) {
+          // 64 publishes' bucket bytes per step, one per lane
+          while (hm == 0 && hc < nblk) {
+            const uint32_t q = hc * 64 + lane;
+            hm = __ballot(q < a.npub && a.heavybyte[q] == 1 + hx);
+            hcc = hc;
+            hc += hstride;
+          }
+          if (hm) {
+            p = hcc * 64 + (uint32_t)__builtin_ctzll(hm);
+            hm &= hm - 1;
+            have = true;
+          } else {
+            heavy_on = false;
+          }
         }
         if (!have && wide_on) {
           while (m == 0 && c < nchunks) { m = uni64(a.widemask[c]); cc = c; c += nwaves; }
@@ -1939,6 +1991,7 @@ __global__ __launch_bounds__(256) void k_dd_claim(MatchArgs a) {
       a.ddmask[c] = 0;
     }
     if (p % 32 == 0) a.fastdone[p / 32] = 0;
+    a.heavybyte[p] = 0;   // COUNT walks only the representatives
     const vmqg_pub pub = a.pubs[p];
     if (pub.nwords == 0 || pub.mountpoint >= a.max_mp) continue;
     const uint64_t fp = lane_pub_fp(a, pub);
@@ -2052,7 +2105,7 @@ __global__ __launch_bounds__(256) void k_dd_fixup(MatchArgs a) {
         }
         pk[0] = h;
         pk[1] = k1;
-        const uint32_t nkf = h.y == kMany ? 0u : h.y & ~(kHugeFlag | kGroupFlag);
+        const uint32_t nkf = h.y == kMany ? 0u : h.y & ~(kHugeFlag | kGroupFlag | kHeavyFlag);
         if (h.y == kMany || (nkf > 2 && nkf <= kSpillKeys)) {   // spilled keys or candidate paths: 64 B
           const uint4* rs = reinterpret_cast<const uint4*>(a.keyspill + (uint64_t)rep * kSpillKeys);
           uint4* ps = reinterpret_cast<uint4*>(a.keyspill + (uint64_t)p * kSpillKeys);
@@ -2070,6 +2123,9 @@ __global__ __launch_bounds__(256) void k_dd_fixup(MatchArgs a) {
           if (!grouped) atomicOr(reinterpret_cast<unsigned long long*>(a.widemask + p / a.gpw), 1ull << (p % a.gpw));
         } else if (h.y & kHugeFlag) {
           a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
+        } else if (h.y & kHeavyFlag) {   // the representative's bucket: the same first key
+          a.heavybyte[p] = (uint8_t)(1 + heavy_bucket(k1.x));
+          atomicAdd(&a.status[kStHeavy], 1u);
         }
       } else {
         a.offsets[p] = 0;
