@@ -513,7 +513,9 @@ def bench_other(args):
         w = W.CONFIGS[args.config]()
     gen_s = time.time() - t0
     n = w.n_subs
-    hints = {"edges": 2 * n, "paths": 2 * n, "keys": n * 5 // 4, "records": n * 5 // 4, "exact": n * 5 // 4}
+    # the exact table holds every topic with a local key or remote entries (at
+    # most one per subscription): sized for n, it is planned at load <= 0.5
+    hints = {"edges": 2 * n, "paths": 2 * n, "keys": n * 5 // 4, "records": n * 5 // 4, "exact": n}
     view = RegGpuView(node=w.self_node, device=0, nodes=w.nodes, max_mountpoints=max(1024, len(w.mps) + 1),
                       hints=hints)
     t0 = time.time()

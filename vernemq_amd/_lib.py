@@ -275,6 +275,8 @@ def lib():
     _share_torch_hip_runtime()
     L = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
+        if path != LIB_PATH and not hasattr(L, name):
+            continue   # an A/B build of an older revision (VMQG_LIB_PATH): the entry points it has
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
