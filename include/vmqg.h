@@ -18,11 +18,25 @@
  *
  * Conventions: every call returns 0 (VMQG_OK) or a negative VMQG_E_* code; no
  * exception crosses the ABI.  The caller owns every buffer; the library never
- * keeps a caller pointer after a call returns.  One context is not
- * re-entrant (the NIF batcher serialises calls); separate contexts (one per
+ * keeps a caller pointer after a call returns.  Separate contexts (one per
  * GPU) are independent.  vmqg_apply_ops and the match calls on one context
  * are ordered on the context's stream, so a match batch observes either all
  * or none of an apply batch (epoch semantics).
+ *
+ * Concurrency on one context (ABI 6; vmq_reg_trie's tables are read_concurrency
+ * ETS with one writer, vmq_reg_trie.erl:136-137).  Three roles:
+ *   readers  any number at once, never waiting, alongside everything below:
+ *            vmqg_prepare_publish / _publishes / _word_lists,
+ *            vmqg_intern_words with create = 0, vmqg_dict_generation,
+ *            vmqg_records_pin / _unpin;
+ *   writer   one at a time: vmqg_intern_words with create = 1 and
+ *            vmqg_apply_stage — these run alongside the readers and alongside
+ *            device calls;
+ *   device   one at a time (the caller's lock): the match calls, the hbatch
+ *            calls, vmqg_apply_commit, vmqg_match_status, the option and
+ *            timing calls.
+ * vmqg_apply_ops (stage + commit) is both writer and device.  Any other call
+ * (stats, dump, replica calls) wants the context to itself.
  */
 #ifndef VMQG_H
 #define VMQG_H
@@ -34,7 +48,7 @@
 extern "C" {
 #endif
 
-#define VMQG_ABI_VERSION 5
+#define VMQG_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------- */
 #define VMQG_OK 0
@@ -244,6 +258,21 @@ uint64_t vmqg_dict_generation(vmqg_ctx* ctx);
 int vmqg_apply_ops(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words,
                    size_t nwords, uint64_t* epoch_out);
 
+/* vmqg_apply_ops in its two halves (ABI 6), so that the host work of an apply
+ * does not hold up matching:
+ *   vmqg_apply_stage   the host half (the state machine, the host mirror, the
+ *                      patch list, the readers' record buffer): a writer call,
+ *                      run while match calls are queued and running (they
+ *                      read only the device tables); VMQG_E_STATE if the
+ *                      previous stage is not committed yet.  A rejected batch
+ *                      (validation) stages nothing.
+ *   vmqg_apply_commit  the device half: ships the staged patches (or image)
+ *                      on the context stream; matches queued after it see the
+ *                      new tables, *epoch_out = their epoch.  A device call.
+ *                      No-op when nothing is staged. */
+int vmqg_apply_stage(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords);
+int vmqg_apply_commit(vmqg_ctx* ctx, uint64_t* epoch_out);
+
 /* ---- matching -------------------------------------------------------- */
 /* Host-buffer match of npub publishes.  offsets[0..npub] receives the
  * exclusive prefix of per-publish emission counts (offsets[npub] = total);
@@ -326,6 +355,17 @@ int vmqg_records(vmqg_ctx* ctx, const vmqg_emit** recs, uint64_t* n);
 int vmqg_epoch(vmqg_ctx* ctx, uint64_t* epoch);
 int vmqg_records_at(vmqg_ctx* ctx, uint64_t epoch, const vmqg_emit** recs, uint64_t* n);
 
+/* Concurrent expansion (ABI 6): readers' copies of the record table, kept by
+ * vmqg_apply_stage once vmqg_set_option(ctx, "reader_records", 1) turned them
+ * on (primary contexts).  vmqg_records_pin returns a record table valid for
+ * range results of `epoch` and a pin that keeps it unchanged until
+ * vmqg_records_unpin; never waits.  Two copies are kept (left-right): the
+ * writer updates the one no reader is pinned on, so a pin of the current or
+ * the previous apply's epoch succeeds; VMQG_E_STATE for an older epoch whose
+ * records have since changed (the caller matches again).  A reader call. */
+int vmqg_records_pin(vmqg_ctx* ctx, uint64_t epoch, const vmqg_emit** recs, uint64_t* n, uint32_t* pin);
+void vmqg_records_unpin(vmqg_ctx* ctx, uint32_t pin);
+
 /* ---- pipelined host-buffer matching (ABI 4) ---------------------------- */
 /* vmqg_match_batch is one synchronous round trip.  A host that matches many
  * batches back to back (the NIF's combining submitter, integration/c_src/
@@ -384,7 +424,15 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "dd_g"      1 | 4      dedupe on: lanes per representative in COUNT (default 4)
  *   "groups"    0 | 1      records mode: publishes of >= 128 records grouped by what
  *                          they emit and written group by group by the EMIT tail
- *                          (default 0: it loses its A/B) */
+ *                          (default 0: it loses its A/B)
+ *   "exfilter"  0 | 1 | 2  exact-topic lookups behind the 1-bit-per-slot filter:
+ *                          off, on, or auto (2, the default: the device's counts
+ *                          of a call of >= 4,096 lookups decide the next calls)
+ *   "heavy_min" 0..2^30    records mode: publishes of >= that many records from
+ *                          <= 2 keys are copied by the EMIT tail on the XCD their
+ *                          first key hashes to (0, the default: off)
+ *   "reader_records" 1     keep the readers' record buffers (vmqg_records_pin);
+ *                          a writer call, made before readers start */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the match kernels over the last

@@ -2,7 +2,6 @@
  * vmqg_batch.c — see vmqg_batch.h.  Plain C99, no OTP, no HIP: only the
  * libvmqgpu C ABI.
  */
-#define _GNU_SOURCE   /* pthread_rwlockattr_setkind_np: writers are not starved by readers */
 #include "vmqg_batch.h"
 
 #include <pthread.h>
@@ -570,8 +569,8 @@ typedef struct vmqgb_round {
 
 struct vmqgb_view {
   vmqg_ctx* ctx;
-  pthread_rwlock_t tables;   /* readers: batchers; writers: applies, interning */
-  pthread_mutex_t device;    /* the context's device side (submits, applies) */
+  pthread_mutex_t wr;        /* writers: interning, applies (batchers never take it) */
+  pthread_mutex_t device;    /* the context's device side (submits, commits) */
   pthread_mutex_t q_mu;      /* the queue, the rounds, the counters */
   pthread_cond_t q_cv;
   vmqgb_req* q_head;
@@ -588,11 +587,7 @@ vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx) {
   vmqgb_view* v = (vmqgb_view*)calloc(1, sizeof(*v));
   if (!v) return NULL;
   v->ctx = ctx;
-  pthread_rwlockattr_t a;
-  pthread_rwlockattr_init(&a);
-  pthread_rwlockattr_setkind_np(&a, PTHREAD_RWLOCK_PREFER_WRITER_NONRECURSIVE_NP);
-  const int r1 = pthread_rwlock_init(&v->tables, &a);
-  pthread_rwlockattr_destroy(&a);
+  const int r1 = pthread_mutex_init(&v->wr, NULL);
   const int r2 = pthread_mutex_init(&v->device, NULL);
   const int r3 = pthread_mutex_init(&v->q_mu, NULL);
   const int r4 = pthread_cond_init(&v->q_cv, NULL);
@@ -603,13 +598,16 @@ vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx) {
     v->rounds[i].hb = vmqg_hbatch_new(ctx);   /* NULL on a host-engine-only context */
     if (!v->rounds[i].hb) v->pipelined = 0;
   }
+  /* the readers' record buffers: records-mode expansion and range folds read
+   * them while the writer stages the next apply */
+  if (v->pipelined && vmqg_set_option(ctx, "reader_records", 1) != VMQG_OK) v->pipelined = 0;
   return v;
 }
 
 void vmqgb_view_free(vmqgb_view* v) {
   if (!v) return;
   for (int i = 0; i < VMQGB_ROUNDS; i++) vmqg_hbatch_free(v->rounds[i].hb);
-  pthread_rwlock_destroy(&v->tables);
+  pthread_mutex_destroy(&v->wr);
   pthread_mutex_destroy(&v->device);
   pthread_mutex_destroy(&v->q_mu);
   pthread_cond_destroy(&v->q_cv);
@@ -617,24 +615,28 @@ void vmqgb_view_free(vmqgb_view* v) {
 }
 
 vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v) { return v->ctx; }
-void vmqgb_view_read_begin(vmqgb_view* v) { pthread_rwlock_rdlock(&v->tables); }
-void vmqgb_view_read_end(vmqgb_view* v) { pthread_rwlock_unlock(&v->tables); }
-void vmqgb_view_yield(vmqgb_view* v) {   /* a waiting writer goes first (writer-preferring lock) */
-  pthread_rwlock_unlock(&v->tables);
-  pthread_rwlock_rdlock(&v->tables);
-}
-void vmqgb_view_write_begin(vmqgb_view* v) { pthread_rwlock_wrlock(&v->tables); }
-void vmqgb_view_write_end(vmqgb_view* v) { pthread_rwlock_unlock(&v->tables); }
+void vmqgb_view_write_begin(vmqgb_view* v) { pthread_mutex_lock(&v->wr); }
+void vmqgb_view_write_end(vmqgb_view* v) { pthread_mutex_unlock(&v->wr); }
 
-/* The apply changes what a device call reads (the layout, the arena, the
- * staging ring): it takes the device mutex too, after the table lock (a
- * mutex holder never waits for the table lock, so no cycle).  Rounds already
- * submitted stay on the epoch they were submitted at (stream order). */
+/* The host half runs beside the rounds in flight and the batchers' prepares
+ * and folds (vmqg_apply_stage reads and writes only the host state and the
+ * readers' record buffer nobody is pinned on); the upload takes a turn at
+ * the device (the device mutex, after the writer mutex: a device-mutex
+ * holder never waits for the writer mutex, so no cycle).  Rounds already
+ * submitted stay on the epoch they were submitted at (stream order).  The
+ * ops are consumed either way. */
 int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
+  __atomic_thread_fence(__ATOMIC_RELEASE);   /* the caller's term tables before the ids reach any result */
+  int rc = o->n ? vmqg_apply_stage(v->ctx, o->ops, o->n, o->words, o->nwords) : VMQG_OK;
+  if (rc == VMQG_E_INVAL || rc == VMQG_E_LIMIT || rc == VMQG_E_STATE) {   /* rejected: nothing staged */
+    o->n = o->nwords = 0;
+    return rc;
+  }
   pthread_mutex_lock(&v->device);
-  const int rc = vmqgb_ops_apply(o, v->ctx, epoch);
+  const int rc2 = vmqg_apply_commit(v->ctx, epoch);
   pthread_mutex_unlock(&v->device);
-  return rc;
+  o->n = o->nwords = 0;
+  return rc ? rc : rc2;
 }
 
 int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
@@ -666,6 +668,10 @@ static void round_release(vmqgb_view* v, vmqgb_round* r) {   /* q_mu held */
 }
 
 void vmqgb_view_release(vmqgb_view* v, vmqgb_batch* b) {
+  if (b->rec_pinned) {
+    vmqg_records_unpin(v->ctx, b->rec_pin);
+    b->rec_pinned = 0;
+  }
   if (!b->lease) return;
   pthread_mutex_lock(&v->q_mu);
   round_release(v, (vmqgb_round*)b->lease);
@@ -784,8 +790,10 @@ static void combine(vmqgb_view* v, vmqgb_req* req) {
 }
 
 /* records mode: the batch's records copied out of its round (device
- * records) or expanded from the host record table of the round's epoch
- * (device ranges); offsets rebased to the batch.  Read lock held. */
+ * records) or expanded from the readers' record table of the round's epoch
+ * (device ranges, pinned for the copy); offsets rebased to the batch. */
+static int expand_ranges(vmqgb_batch* b, const uint64_t* o, const vmqg_range* g, const vmqg_emit* recs,
+                         uint64_t nrecs);
 static int take_records(vmqgb_view* v, vmqgb_batch* b, vmqgb_req* q) {
   const vmqgb_round* r = q->round;
   const uint64_t* o = r->offs + q->base;
@@ -798,14 +806,22 @@ static int take_records(vmqgb_view* v, vmqgb_batch* b, vmqgb_req* q) {
     b->out_n = cnt;
     return 0;
   }
-  const vmqg_emit* recs = NULL;
-  uint64_t nrecs = 0;
-  int rc = vmqg_records_at(v->ctx, r->epoch, &recs, &nrecs);
-  if (rc) return rc;   /* VMQG_E_STATE: an apply rewrote record slots since the round */
   const vmqg_range* g = (const vmqg_range*)r->out;
   uint64_t cnt = 0;
   for (uint64_t k = o[0]; k < o[b->n]; k++) cnt += g[k].count ? g[k].count : 1;
   if (grow((void**)&b->out, &b->out_cap, cnt + 1, sizeof(vmqg_emit))) return VMQG_E_NOMEM;
+  const vmqg_emit* recs = NULL;
+  uint64_t nrecs = 0;
+  uint32_t pin = 0;
+  int rc = vmqg_records_pin(v->ctx, r->epoch, &recs, &nrecs, &pin);
+  if (rc) return rc;   /* VMQG_E_STATE: two applies rewrote record slots since the round */
+  rc = expand_ranges(b, o, g, recs, nrecs);
+  vmqg_records_unpin(v->ctx, pin);
+  return rc;
+}
+
+static int expand_ranges(vmqgb_batch* b, const uint64_t* o, const vmqg_range* g, const vmqg_emit* recs,
+                         uint64_t nrecs) {
   vmqg_emit* dst = b->out;
   b->offsets[0] = 0;
   for (size_t i = 0; i < b->n; i++) {
@@ -823,19 +839,18 @@ static int take_records(vmqgb_view* v, vmqgb_batch* b, vmqgb_req* q) {
     }
     b->offsets[i + 1] = (uint64_t)(dst - b->out);
   }
-  b->out_n = cnt;
+  b->out_n = b->offsets[b->n];
   return 0;
 }
 
-/* the pre-pipeline path: one synchronous device call under the mutex */
+/* without a device (host-engine contexts): one synchronous call, which
+ * reports VMQG_E_DEVICE */
 static int match_direct(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
-  if (!ranges) vmqgb_view_read_end(v);
+  (void)recs; (void)nrecs;
   pthread_mutex_lock(&v->device);
-  int rc = ranges ? vmqgb_match_ranges(b, v->ctx) : vmqgb_match(b, v->ctx);
+  const int rc = ranges ? vmqgb_match_ranges(b, v->ctx) : vmqgb_match(b, v->ctx);
   pthread_mutex_unlock(&v->device);
-  if (!ranges) vmqgb_view_read_begin(v);
-  if (!rc && ranges && recs && nrecs) rc = vmqg_records_at(v->ctx, b->epoch, recs, nrecs);
-  return rc;
+  return rc ? rc : VMQG_E_DEVICE;
 }
 
 int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
@@ -853,7 +868,8 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
   memset(&q, 0, sizeof q);
   q.b = b;
   if (ranges) {
-    /* the read lock stays: no apply (and no new word) until the caller has folded */
+    /* the round's entries stay in its buffers and the record table of its
+     * epoch stays pinned until the caller has folded (vmqgb_view_release) */
     for (int attempt = 0;; attempt++) {
       q.dev_ranges = 1;
       combine(v, &q);
@@ -864,7 +880,19 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
       b->rng = (vmqg_range*)r->out;
       b->rng_n = r->offs[q.base + b->n] - r->offs[q.base];
       b->epoch = r->epoch;
-      const int rc = vmqgb_batch_recheck(b, v->ctx);   /* a writer got in at a prepare yield */
+      const vmqg_emit* rt = NULL;
+      uint64_t nrt = 0;
+      int rc = vmqg_records_pin(v->ctx, b->epoch, &rt, &nrt, &b->rec_pin);
+      if (rc == 0) b->rec_pinned = 1;
+      if (rc == VMQG_E_STATE && attempt < 16) {   /* two applies rewrote record slots since the round */
+        vmqgb_view_release(v, b);
+        pthread_mutex_lock(&v->q_mu);
+        v->st.state_retries++;
+        pthread_mutex_unlock(&v->q_mu);
+        continue;
+      }
+      if (rc) return rc;
+      rc = vmqgb_batch_recheck(b, v->ctx);   /* a word became known after the prepare */
       if (rc < 0) return rc;
       if (rc == 1 && attempt < 16) {
         b->stale_rematches++;
@@ -874,14 +902,13 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
         pthread_mutex_unlock(&v->q_mu);
         continue;
       }
-      break;
+      if (recs) *recs = rt;
+      if (nrecs) *nrecs = nrt;
+      return 0;
     }
-    if (recs && nrecs) return vmqg_records_at(v->ctx, b->epoch, recs, nrecs);
-    return 0;
   }
-  /* records: the read lock stays until the records are copied out (the
-   * expansion reads the host record table of the round's epoch); the fold
-   * that follows works on copies and may yield it */
+  /* records: the records are copied out of the round (the expansion pins
+   * the record table of the round's epoch for the copy only) */
   int dev_ranges = !v->device_records;
   for (int attempt = 0;; attempt++) {
     q.dev_ranges = dev_ranges;

@@ -19,19 +19,20 @@
  *   - subscription ops: {Topic words, Node, SubscriberId, SubInfo} changes
  *     (deletes before adds, vmq_reg_trie.erl:245-248) -> vmqg_op batches.
  *
- *   - the view: the locking protocol the NIF runs fold/4 callers under
- *     (vmqgb_view_*), so that every batcher prepares its batch and folds its
- *     results in parallel — as vmq_reg_trie:fold/4 runs in every caller's
- *     process against read_concurrency tables (vmq_reg_trie.erl:59-66,
- *     136-137) — and only the device call is serialised.
+ *   - the view: how the NIF runs fold/4 callers (vmqgb_view_*): every
+ *     batcher prepares its batch and folds its results in parallel, without
+ *     a lock and without waiting for writers — as vmq_reg_trie:fold/4 runs in
+ *     every caller's process against read_concurrency tables with one writer
+ *     (vmq_reg_trie.erl:59-66, 136-137) — and only device calls take turns.
  *
  * Threading: an interner or a batch is owned by one thread at a time.
- * vmqgb_batch_add only reads the context's dictionary (vmqg_prepare_publish),
- * so per-thread batches may be filled concurrently while no other call
- * modifies the context; vmqgb_batch_append merges them for one match call.
- * vmqgb_view: readers (a batch's prepare, device call and fold) share the
- * tables; a writer (vmqg_apply_ops, through vmqgb_view_apply) excludes them
- * and is not starved by them; device calls take turns.
+ * vmqgb_batch_add* only reads the context's dictionary (a reader call of
+ * include/vmqg.h, safe beside the one writer), so batches are filled
+ * concurrently with each other and with table changes; vmqgb_batch_append
+ * merges them for one match call.  vmqgb_view: batchers never take a lock
+ * the writer holds; writers (interning, vmqgb_view_apply_ops) take turns on
+ * the view's writer mutex; the host half of an apply runs beside the device
+ * rounds, only its upload takes a turn at the device.
  */
 #ifndef VMQG_BATCH_H
 #define VMQG_BATCH_H
@@ -85,6 +86,8 @@ typedef struct vmqgb_batch {
   uint8_t* raw;
   size_t raw_n, raw_cap;
   void* lease;          /* the view pipeline round the outputs point into */
+  uint32_t rec_pin;     /* range mode: the record table pinned for the fold (vmqg_records_pin) */
+  int rec_pinned;
   uint32_t stale_rematches;   /* matches repeated because a publish's unknown word became known */
 } vmqgb_batch;
 
@@ -116,7 +119,7 @@ int vmqgb_batch_add_word_lists(vmqgb_batch* b, vmqg_ctx* ctx, size_t n, const ui
 /* Appends every publish of src (per-thread batches -> one match call). */
 int vmqgb_batch_append(vmqgb_batch* dst, const vmqgb_batch* src);
 /* Prepares the publishes holding unknown words again if the dictionary grew
- * since they were prepared (readers' lock held).  Returns 1 if a word id
+ * since they were prepared.  Returns 1 if a word id
  * changed (the batch must be matched again), 0 if not, or a VMQG_E_*. */
 int vmqgb_batch_recheck(vmqgb_batch* b, vmqg_ctx* ctx);
 
@@ -183,55 +186,41 @@ typedef struct vmqgb_view vmqgb_view;
 vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx);
 void vmqgb_view_free(vmqgb_view* v);   /* does not destroy the context */
 vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v);
-/* A batcher's critical section: read_begin, vmqgb_batch_add(_many) for its
- * publishes, vmqgb_view_match, the fold, vmqgb_view_release, read_end.  Any
- * number of batchers at once.
+/* A batcher's sequence: vmqgb_batch_add* for its publishes, vmqgb_view_match,
+ * the fold, vmqgb_view_release.  Any number of batchers at once, no lock
+ * held in between, alongside writers.
  *
  * The device side is a combining, pipelined submitter: a batcher queues its
  * prepared batch; whichever waiting batcher finds the pipeline free takes
  * every batch queued at that moment and matches them as ONE device call
  * (vmqg_hbatch_*: one H2D, one launch sequence, one D2H), then hands each
  * batch its slice.  Up to two such rounds (vmqgb_view_set_inflight) are in
- * the kernels at once and up to VMQGB_ROUNDS exist, so round k+1's inputs are copied and matched while
- * round k's results come back and round k-1's are folded.  The device works
- * in range mode ({record off, count} per key: 16 B per config-C publish over
- * PCIe instead of 1,040 B of records); a records-mode batch is expanded from
- * the host record table of its round's epoch into the batch's own buffer
- * (byte-identical to what the device would have copied; if an apply has
- * rewritten record slots since, the batch is matched again with device-side
- * records). */
-void vmqgb_view_read_begin(vmqgb_view* v);
-void vmqgb_view_read_end(vmqgb_view* v);
-/* Lets a waiting writer in and takes the read lock back: a batcher calls it
- * every VMQGB_YIELD_EVERY publishes while it prepares a batch, and while it
- * folds a records-mode batch (its records are copies), so an apply waits for
- * one slice of a batch, not for every reader's whole batch. */
-void vmqgb_view_yield(vmqgb_view* v);
-#define VMQGB_YIELD_EVERY 512
+ * the kernels at once and up to VMQGB_ROUNDS exist, so round k+1's inputs are
+ * copied and matched while round k's results come back and round k-1's are
+ * folded.  The device works in range mode ({record off, count} per key: 16 B
+ * per config-C publish over PCIe instead of 1,040 B of records); a
+ * records-mode batch is expanded from the readers' record table of its
+ * round's epoch (vmqg_records_pin) into the batch's own buffer (byte-identical
+ * to what the device would have copied; if two applies have rewritten record
+ * slots since, the batch is matched again with device-side records). */
 #define VMQGB_ROUNDS 6
 #define VMQGB_ROUND_MAX (1u << 17)   /* publishes per combined round */
-/* Called under the read lock, returns under it: the batch's results
- * (offsets + out in records mode, offsets + rng in range mode) and, in range
- * mode, the record table of the match's epoch (vmqg_records_at) for
- * vmqgb_fold_ranges.  The lock is held while the batch waits for its round,
- * so a writer waits at most for the rounds in flight (one device round trip)
- * and the results are the tables' answer at one epoch.  If the dictionary
- * grew between the batch's prepare slices (a writer got in at a yield) and a
- * publish's unknown word is known now, the batch is prepared and matched
- * again (vmqgb_batch_recheck).  Records mode copies its records out (the fold
- * may then yield the lock); range mode's entries index the host record
- * table, so its fold keeps the lock. */
+/* The batch's results (offsets + out in records mode, offsets + rng in range
+ * mode) — every publish's answer from the tables of one epoch, b->epoch —
+ * and, in range mode, the record table of that epoch, pinned until
+ * vmqgb_view_release, for vmqgb_fold_ranges / _spans.  If the dictionary grew
+ * after the batch was prepared and a publish's unknown word is known now, the
+ * batch is prepared and matched again (vmqgb_batch_recheck). */
 int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs);
 /* Ends the batch's use of the pipeline buffers its range-mode results point
- * into (also done by its next vmqgb_view_match). */
+ * into and of its pinned record table (also done by its next
+ * vmqgb_view_match). */
 void vmqgb_view_release(vmqgb_view* v, vmqgb_batch* b);
-/* Table changes (vmqg_apply_ops, the word dictionary, the caller's term
- * tables): writers.  INVARIANT: the word dictionary only grows under the
- * write lock (vmqgb_ops_add interns), so a prepare under the read lock sees
- * a stable dictionary.  write_begin takes the table lock only; the device
- * mutex is taken (after it) only around the apply itself (vmqgb_view_apply_ops),
- * so a writer that only interns (the NIF's add_init) never waits for a
- * device call. */
+/* Table changes (the word dictionary, the caller's term tables, the apply):
+ * writers, one at a time (write_begin / write_end: the view's writer mutex;
+ * batchers never take it).  vmqgb_view_apply_ops stages the apply's host
+ * half with no other lock (vmqg_apply_stage: matches keep running) and takes
+ * the device mutex only for its upload (vmqg_apply_commit). */
 void vmqgb_view_write_begin(vmqgb_view* v);
 void vmqgb_view_write_end(vmqgb_view* v);
 int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);   /* inside write_begin/end */

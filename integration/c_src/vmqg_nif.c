@@ -29,13 +29,15 @@
  * Concurrency (vmqgb_view, vmqg_batch.c): vmq_reg_gpu_view runs one batcher
  * process per scheduler; each calls match/4 with its own batch resource, and
  * those calls run in parallel on dirty CPU schedulers — preparing the
- * publishes and building the result terms under the view's read lock, only
- * the device call itself taking turns — as vmq_reg_trie:fold/4 runs in
- * every caller's process (vmq_reg_trie.erl:59-66, read_concurrency tables
- * :136-137); the device calls of all batchers are combined (vmqgb_view_match).
- * apply/3, apply_many/2, add_init/6 and flush_init/1 (the subscription
- * changes and the term tables they intern) are writers.  Every NIF that can
- * wait for a lock or the device is a dirty one.
+ * publishes and building the result terms without a lock and without ever
+ * waiting for a writer, only the device call itself taking turns — as
+ * vmq_reg_trie:fold/4 runs in every caller's process (vmq_reg_trie.erl:59-66,
+ * read_concurrency tables with one writer :136-137); the device calls of all
+ * batchers are combined (vmqgb_view_match).  apply/3, apply_many/2,
+ * add_init/6 and flush_init/1 (the subscription changes and the term tables
+ * they intern) are writers, one at a time: the term tables only grow, in
+ * chunks that never move, so readers index them while a writer adds.  Every
+ * NIF that can wait for a lock or the device is a dirty one.
  */
 #include <erl_nif.h>
 #include <stdint.h>
@@ -44,15 +46,22 @@
 #include "vmqg.h"
 #include "vmqg_batch.h"
 
+/* Terms by id: TS_CHUNK-term chunks published whole (release) before any
+ * result can carry one of their ids; a chunk never moves, so a batcher reads
+ * a term while the writer adds others.  Terms of a process-independent env
+ * stay where they are as the env grows. */
+#define TS_CHUNK_BITS 14
+#define TS_CHUNK (1u << TS_CHUNK_BITS)
+#define TS_CHUNKS (1u << 18)      /* ids < 2^32 */
 typedef struct {
   ErlNifEnv* env;                 /* owns the stored terms */
-  ERL_NIF_TERM* terms;
-  size_t n, cap;
+  ERL_NIF_TERM** dir;             /* TS_CHUNKS chunk pointers */
 } term_store;
 
 typedef struct {
   vmqg_ctx* ctx;
   vmqgb_view* view;               /* batchers (readers) vs. table changes (writers) */
+  ErlNifMutex* mp_mu;             /* the mountpoint interner: batchers look up, writers add */
   vmqgb_interner *mps, *nodes, *subs, *infos;
   term_store node_t, sub_t, info_t, group_t;   /* group_t indexed by word id */
   vmqgb_ops ops;                  /* apply/3 and add_init/6 accumulation (under the write lock) */
@@ -69,18 +78,39 @@ static ErlNifResourceType* BRES;
 static ERL_NIF_TERM a_ok, a_error, a_invalid_topic, a_device, a_nomem, a_badarg, a_records, a_ranges;
 
 /* ------------------------------------------------------------ helpers */
-static int store_put(term_store* s, size_t id, ERL_NIF_TERM t) {
-  if (id >= s->cap) {
-    size_t c = s->cap ? s->cap * 2 : 1024;
-    while (c <= id) c *= 2;
-    ERL_NIF_TERM* nt = (ERL_NIF_TERM*)enif_realloc(s->terms, c * sizeof(ERL_NIF_TERM));
-    if (!nt) return 0;
-    s->terms = nt;
-    s->cap = c;
-  }
-  if (id >= s->n) s->n = id + 1;
-  s->terms[id] = enif_make_copy(s->env, t);
+static int store_init(term_store* s) {
+  s->env = enif_alloc_env();
+  s->dir = (ERL_NIF_TERM**)enif_alloc(TS_CHUNKS * sizeof(ERL_NIF_TERM*));
+  if (!s->env || !s->dir) return 0;
+  memset(s->dir, 0, TS_CHUNKS * sizeof(ERL_NIF_TERM*));
   return 1;
+}
+
+static void store_free(term_store* s) {
+  if (s->dir)
+    for (size_t c = 0; c < TS_CHUNKS; c++) if (s->dir[c]) enif_free(s->dir[c]);
+  enif_free(s->dir);
+  if (s->env) enif_free_env(s->env);
+}
+
+/* the writer only */
+static int store_put(term_store* s, size_t id, ERL_NIF_TERM t) {
+  if (!s->dir || (id >> TS_CHUNK_BITS) >= TS_CHUNKS) return 0;
+  ERL_NIF_TERM* ch = s->dir[id >> TS_CHUNK_BITS];
+  if (!ch) {
+    ch = (ERL_NIF_TERM*)enif_alloc(TS_CHUNK * sizeof(ERL_NIF_TERM));
+    if (!ch) return 0;
+    memset(ch, 0, TS_CHUNK * sizeof(ERL_NIF_TERM));
+    __atomic_store_n(&s->dir[id >> TS_CHUNK_BITS], ch, __ATOMIC_RELEASE);
+  }
+  ch[id & (TS_CHUNK - 1)] = enif_make_copy(s->env, t);
+  return 1;
+}
+
+/* readers: an id from a match result (stored before the apply that made it reachable) */
+static ERL_NIF_TERM store_get(const term_store* s, uint32_t id) {
+  const ERL_NIF_TERM* ch = __atomic_load_n(&s->dir[id >> TS_CHUNK_BITS], __ATOMIC_ACQUIRE);
+  return ch ? ch[id & (TS_CHUNK - 1)] : 0;
 }
 
 /* id of a term (created on first sight), its copy stored under the id */
@@ -93,6 +123,14 @@ static int term_id(vmqgb_interner* in, term_store* st, ErlNifEnv* env, ERL_NIF_T
   if (*id == VMQG_NONE) return 0;
   if (st && *id >= before) return store_put(st, *id, t);
   return 1;
+}
+
+/* the mountpoint interner is shared with the batchers' lookups */
+static int mp_id(vmqg_res* r, ErlNifEnv* env, ERL_NIF_TERM t, uint32_t* id) {
+  enif_mutex_lock(r->mp_mu);
+  const int ok = term_id(r->mps, NULL, env, t, id);
+  enif_mutex_unlock(r->mp_mu);
+  return ok;
 }
 
 static ERL_NIF_TERM error_term(ErlNifEnv* env, int rc) {
@@ -108,9 +146,10 @@ static void res_dtor(ErlNifEnv* env, void* obj) {
   vmqgb_interner_free(r->mps); vmqgb_interner_free(r->nodes);
   vmqgb_interner_free(r->subs); vmqgb_interner_free(r->infos);
   term_store* ts[4] = {&r->node_t, &r->sub_t, &r->info_t, &r->group_t};
-  for (int i = 0; i < 4; i++) { if (ts[i]->env) enif_free_env(ts[i]->env); enif_free(ts[i]->terms); }
+  for (int i = 0; i < 4; i++) store_free(ts[i]);
   vmqgb_ops_free(&r->ops);
   vmqgb_view_free(r->view);
+  if (r->mp_mu) enif_mutex_destroy(r->mp_mu);
 }
 
 static void bres_dtor(ErlNifEnv* env, void* obj) {
@@ -139,8 +178,12 @@ static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   memset(r, 0, sizeof(*r));
   r->mps = vmqgb_interner_new(); r->nodes = vmqgb_interner_new();
   r->subs = vmqgb_interner_new(); r->infos = vmqgb_interner_new();
-  r->node_t.env = enif_alloc_env(); r->sub_t.env = enif_alloc_env();
-  r->info_t.env = enif_alloc_env(); r->group_t.env = enif_alloc_env();
+  r->mp_mu = enif_mutex_create("vmqg_mp");
+  if (!r->mp_mu || !store_init(&r->node_t) || !store_init(&r->sub_t) || !store_init(&r->info_t) ||
+      !store_init(&r->group_t)) {
+    enif_release_resource(r);
+    return error_term(env, VMQG_E_NOMEM);
+  }
   vmqgb_ops_init(&r->ops);
   r->max_mountpoints = 1024;
   uint32_t id;
@@ -168,7 +211,7 @@ static int add_change(ErlNifEnv* env, vmqg_res* r, uint32_t kind, ERL_NIF_TERM s
   const ERL_NIF_TERM* sid_el;
   if (!enif_get_tuple(env, sid, &arity, &sid_el) || arity != 2) return VMQG_E_INVAL;
   uint32_t mp, sub, info, nd;
-  if (!term_id(r->mps, NULL, env, sid_el[0], &mp) || mp >= r->max_mountpoints) return VMQG_E_LIMIT;
+  if (!mp_id(r, env, sid_el[0], &mp) || mp >= r->max_mountpoints) return VMQG_E_LIMIT;
   if (!term_id(r->subs, &r->sub_t, env, sid, &sub) || !term_id(r->infos, &r->info_t, env, subinfo, &info) ||
       !term_id(r->nodes, &r->node_t, env, node, &nd))
     return VMQG_E_NOMEM;
@@ -305,15 +348,15 @@ static int make_entry(void* accp, const vmqgb_entry* e) {
   ErlNifEnv* env = acc->env;
   ERL_NIF_TERM t;
   if (e->kind == VMQG_EMIT_LOCAL) {          /* {SubscriberId, SubInfo} */
-    t = enif_make_tuple2(env, enif_make_copy(env, r->sub_t.terms[e->subscriber]),
-                         enif_make_copy(env, r->info_t.terms[e->subinfo]));
+    t = enif_make_tuple2(env, enif_make_copy(env, store_get(&r->sub_t, e->subscriber)),
+                         enif_make_copy(env, store_get(&r->info_t, e->subinfo)));
   } else if (e->kind == VMQG_EMIT_GROUP) {   /* {Node, Group, SubscriberId, SubInfo} */
-    t = enif_make_tuple4(env, enif_make_copy(env, r->node_t.terms[e->node]),
-                         enif_make_copy(env, r->group_t.terms[e->group]),
-                         enif_make_copy(env, r->sub_t.terms[e->subscriber]),
-                         enif_make_copy(env, r->info_t.terms[e->subinfo]));
+    t = enif_make_tuple4(env, enif_make_copy(env, store_get(&r->node_t, e->node)),
+                         enif_make_copy(env, store_get(&r->group_t, e->group)),
+                         enif_make_copy(env, store_get(&r->sub_t, e->subscriber)),
+                         enif_make_copy(env, store_get(&r->info_t, e->subinfo)));
   } else {                                   /* Node */
-    t = enif_make_copy(env, r->node_t.terms[e->node]);
+    t = enif_make_copy(env, store_get(&r->node_t, e->node));
   }
   acc->out[acc->n++] = t;
   return 0;
@@ -350,10 +393,11 @@ static ERL_NIF_TERM nif_batch_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
  * split, no validate_topic: a plugin publish reaches fold/4 unvalidated,
  * vmq_reg.erl:572-594): each element one dictionary lookup, an element that
  * is not a binary equal to no filter word, [] the root alone.
- * Batchers run this concurrently: the tables are read-locked from the first
- * publish prepared to the last term built (yielded every VMQGB_YIELD_EVERY
- * publishes while preparing, and while folding records); the batch joins the
- * view's combining submitter for the device call (vmqgb_view_match). */
+ * Batchers run this concurrently and never wait for a writer: the prepare
+ * reads the lock-free dictionary, the batch joins the view's combining
+ * submitter for the device call (vmqgb_view_match), and the terms are built
+ * from the batch's own records (records mode) or from the record table of
+ * its epoch pinned until the end (ranges). */
 static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   (void)argc;
   vmqg_res* r = get_res(env, argv[0]);
@@ -401,9 +445,9 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
       last_id = r->max_mountpoints;   /* an unknown mountpoint has no subscriptions: an id past every root */
       if (enif_term_to_binary(env, el[0], &mpb)) {
         uint32_t id;
-        vmqgb_view_read_begin(r->view);
+        enif_mutex_lock(r->mp_mu);
         if (vmqgb_lookup(r->mps, mpb.data, mpb.size, &id) == 0) last_id = id;
-        vmqgb_view_read_end(r->view);
+        enif_mutex_unlock(r->mp_mu);
         enif_release_binary(&mpb);
       }
     }
@@ -428,25 +472,18 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
       k++;
     }
   }
-  vmqgb_view_read_begin(r->view);
   vmqgb_batch_reset(b);
-  /* the batched prepare, slice by slice (a writer gets in between slices) */
-  size_t wbase = 0;
-  for (unsigned lo = 0; lo < n; lo += VMQGB_YIELD_EVERY) {
-    const unsigned hi = lo + VMQGB_YIELD_EVERY < n ? lo + VMQGB_YIELD_EVERY : n;
-    if (lo) vmqgb_view_yield(r->view);
-    /* rejected terms keep their error; the others are prepared together */
+  /* the batched prepare: rejected terms keep their error, the others are
+   * prepared together */
+  {
     unsigned q = 0;
-    size_t sw = 0;
-    for (unsigned i = lo; i < hi; i++)
-      if (idx[i] == 0) { mps[lo + q] = mps[i]; cnt[lo + q] = cnt[i]; sw += cnt[i]; q++; }
+    for (unsigned i = 0; i < n; i++)
+      if (idx[i] == 0) { mps[q] = mps[i]; cnt[q] = cnt[i]; q++; }
     long* sub = (long*)enif_alloc((q ? q : 1) * sizeof(long));
-    const int rc = sub ? vmqgb_batch_add_word_lists(b, r->ctx, q, mps + lo, cnt + lo, wp + wbase, wl + wbase, sub)
-                       : VMQG_E_NOMEM;
-    wbase += sw;
+    const int prc = sub ? vmqgb_batch_add_word_lists(b, r->ctx, q, mps, cnt, wp, wl, sub) : VMQG_E_NOMEM;
     unsigned j = 0;
-    for (unsigned i = lo; i < hi; i++)
-      if (idx[i] == 0) idx[i] = rc ? rc : sub[j++];
+    for (unsigned i = 0; i < n; i++)
+      if (idx[i] == 0) idx[i] = prc ? prc : sub[j++];
     enif_free(sub);
   }
   enif_free(wp);
@@ -454,8 +491,8 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   const vmqg_emit* recs = NULL;
   uint64_t nrecs = 0;
   const int rc = vmqgb_view_match(r->view, b, ranges, &recs, &nrecs);
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);   /* the term tables as of the results' epoch */
   for (unsigned i = 0; i < n; i++) {
-    if (!ranges && i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(r->view);   /* records: copies */
     if (idx[i] < 0 || rc) { res[i] = error_term(env, idx[i] < 0 ? (int)idx[i] : rc); continue; }
     size_t cnt = 0;
     if (ranges) {
@@ -472,7 +509,6 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     enif_free(acc.out);
   }
   vmqgb_view_release(r->view, b);
-  vmqgb_view_read_end(r->view);
   ERL_NIF_TERM list = enif_make_list_from_array(env, res, n);
   enif_free(res); enif_free(idx); enif_free(topics); enif_free(cnt); enif_free(mps);
   return list;
@@ -484,9 +520,9 @@ static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   vmqg_res* r = get_res(env, argv[0]);
   if (!r) return enif_make_badarg(env);
   vmqg_stats_t st;
-  vmqgb_view_read_begin(r->view);   /* never the device lock: metrics polling does not wait for a match */
+  vmqgb_view_write_begin(r->view);   /* the writer's turn, never the device's: polling does not wait for a match */
   const int rc = vmqg_stats(r->ctx, &st);
-  vmqgb_view_read_end(r->view);
+  vmqgb_view_write_end(r->view);
   if (rc) return error_term(env, rc);
   return enif_make_tuple2(env, enif_make_uint64(env, st.subs), enif_make_uint64(env, st.device_bytes));
 }

@@ -21,19 +21,21 @@
 %% order of one publisher's publishes is kept (vmq_in_order_delivery_SUITE).
 %%
 %% This gen_server owns the view: the NIF resource, the batchers, the
-%% subscriber-change events (applied as writers: no match reads the tables
-%% while an apply changes them) and the initial load.  It never queues a
-%% fold request, so no event can delay one.
+%% subscriber-change events (applied as the one writer: the batchers never
+%% wait for an apply, an apply's host half runs beside their device rounds,
+%% and every fold answers from the tables of one epoch) and the initial load.
+%% It never queues a fold request, so no event can delay one.
 %%
 %% Events are coalesced: vmq_reg_trie applies each subscriber event with a
 %% few ETS inserts in its gen_server (vmq_reg_trie.erl:198-210, 240-251); here
-%% an apply is a write-lock section plus a table patch upload, so on each
-%% event the view drains the further subscriber events already in its
-%% mailbox (a selective receive with a 0 timeout, up to ?MAX_COALESCE) and
-%% applies the group with ONE vmqg_nif:apply_many/2.  The group is applied
-%% in arrival order, each event's deletes before its adds, which is what
-%% applying the events one after the other does; under load the groups grow
-%% with the backlog, so the view keeps up with config D's 100k changes/s.
+%% an apply is a host-table update plus a patch upload, so the view applies
+%% a window of events with ONE vmqg_nif:apply_many/2: from the first event,
+%% the subscriber events that arrive within ?WINDOW_MS ms or until there are
+%% ?WINDOW_EVENTS of them, plus whatever backlog is already queued (up to
+%% ?MAX_COALESCE; selective receive).  The group is applied in arrival order,
+%% each event's deletes before its adds, which is what applying the events
+%% one after the other does; config D's 100k changes/s become ~100 applies/s
+%% of 1,000 events, each visible to folds within a few ms.
 %%
 %% Install: reg_views = [vmq_reg_trie, vmq_reg_gpu_view] (shadow) or
 %% default_reg_view = vmq_reg_gpu_view (vmq_server.schema:115-137).  The NIF
@@ -44,8 +46,8 @@
 %% gen_server, ets (named table, read_concurrency), queue, lists:foldl /
 %% foldr / reverse / split / zip, application:get_env/3,
 %% erlang:system_info(scheduler_id | schedulers), spawn_link, selective
-%% receive — all older than OTP 18 (no persistent_term, no lists:join,
-%% no maps-only API).  The NIF reschedules itself onto dirty schedulers when
+%% receive, os:timestamp/0 — all older than OTP 18 (no persistent_term, no
+%% lists:join, no maps-only API).  The NIF reschedules itself onto dirty schedulers when
 %% the emulator has them (vmqg_nif.c, load/3).
 %%
 %% Not compiled in this repository's image (no OTP); its C core
@@ -72,6 +74,10 @@
 -define(SERVER, ?MODULE).
 %% subscriber events applied per vmqg_nif:apply_many/2 at most
 -define(MAX_COALESCE, 10000).
+%% the coalescing window: an apply waits at most this long after its first
+%% event for more, or until it has this many
+-define(WINDOW_MS, 2).
+-define(WINDOW_EVENTS, 1000).
 %% shadow-compare counters (public: every fold caller bumps them)
 -define(SHADOW, vmq_reg_gpu_view_shadow).
 
@@ -210,7 +216,8 @@ handle_info(subscribers_loaded, #state{event_queue=Q} = State) ->
 handle_info(Event, #state{status=init, event_queue=Q} = State) ->
     {noreply, State#state{event_queue=queue:in(Event, Q)}};
 handle_info(Event, State) ->
-    {noreply, handle_events([Event | drain_events(?MAX_COALESCE - 1, [])], State)}.
+    Deadline = now_ms() + ?WINDOW_MS,
+    {noreply, handle_events([Event | drain_events(?MAX_COALESCE - 1, ?WINDOW_EVENTS - 1, Deadline, [])], State)}.
 
 terminate(_Reason, _State) ->
     ok.
@@ -222,19 +229,28 @@ code_change(_OldVsn, State, _Extra) ->
 %%% Internal functions
 %%%===================================================================
 
-%% The subscriber events already in the mailbox, oldest first (a selective
-%% receive keeps their relative order; other messages stay where they are).
-%% The shapes are the metadata events vmq_subscriber_db's handler converts
-%% (vmq_subscriber_db.erl:56-71).
-drain_events(0, Acc) ->
+%% The window's subscriber events, oldest first (a selective receive keeps
+%% their relative order; other messages stay where they are): while fewer
+%% than W have come, wait for the next until Deadline; then only take what
+%% is already queued, N at most.  The shapes are the metadata events
+%% vmq_subscriber_db's handler converts (vmq_subscriber_db.erl:56-71).
+drain_events(0, _W, _Deadline, Acc) ->
     lists:reverse(Acc);
-drain_events(N, Acc) ->
+drain_events(N, W, Deadline, Acc) ->
+    Timeout = case W > 0 of
+                  true -> erlang:max(0, Deadline - now_ms());
+                  false -> 0
+              end,
     receive
-        {updated, {vmq, subscriber}, _, _, _} = E -> drain_events(N - 1, [E | Acc]);
-        {deleted, {vmq, subscriber}, _, _} = E -> drain_events(N - 1, [E | Acc])
-    after 0 ->
+        {updated, {vmq, subscriber}, _, _, _} = E -> drain_events(N - 1, W - 1, Deadline, [E | Acc]);
+        {deleted, {vmq, subscriber}, _, _} = E -> drain_events(N - 1, W - 1, Deadline, [E | Acc])
+    after Timeout ->
         lists:reverse(Acc)
     end.
+
+now_ms() ->
+    {M, S, U} = os:timestamp(),
+    (M * 1000000 + S) * 1000 + U div 1000.
 
 replay([], State) ->
     State;
@@ -248,8 +264,12 @@ replay(Events, State) ->
 %% handle_event/2 (vmq_reg_trie.erl:240-251) for a group of events: the same
 %% diff per event, the same order (deletes, then adds; event after event);
 %% the NIF turns the whole group into one vmqg_apply_ops.  If the group is
-%% refused (a malformed change: nothing was applied) the events are applied
-%% one by one, so only the offending one fails, as it would alone.
+%% refused as malformed (invalid_topic / badarg: validated before anything
+%% is applied) the events are applied one by one, so only the offending one
+%% fails, as it would alone.  Any other failure (nomem, device) may have left
+%% part of the group applied: replaying it would apply that part twice, so
+%% the view stops instead, and its supervisor's restart loads the tables
+%% afresh (initialize_trie, vmq_reg_trie.erl:305-316).
 handle_events(Events, #state{ctx=Ctx, event_handler=Handler} = State) ->
     AllChanges = lists:foldr(fun(E, Acc) ->
                                      case event_changes(Handler, E) of
@@ -264,10 +284,12 @@ handle_events(Events, #state{ctx=Ctx, event_handler=Handler} = State) ->
             case vmqg_nif:apply_many(Ctx, Changes) of
                 ok ->
                     ok;
-                {error, _} ->
+                {error, Malformed} when Malformed =:= invalid_topic; Malformed =:= badarg ->
                     lists:foreach(fun({SubscriberId, Ch}) ->
                                           ok = vmqg_nif:apply(Ctx, SubscriberId, Ch)
-                                  end, Changes)
+                                  end, Changes);
+                {error, Reason} ->
+                    exit({vmqg_apply_failed, Reason})
             end
     end,
     State.

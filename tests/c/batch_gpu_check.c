@@ -1,8 +1,8 @@
 /* GPU check of the NIF's C core (integration/c_src/vmqg_batch.c) driven the
- * way vmqg_nif.c drives it: batcher threads, each with its own batch, under
- * the view's locking protocol (read lock: prepare, device call, fold; the
- * device call serialised), subscription changes as writers — against the
- * oracle (tests/test_nif_layer.py compares the output).
+ * way vmqg_nif.c drives it: batcher threads, each with its own batch (no
+ * lock: prepare, device call through the combining submitter, fold),
+ * subscription changes as writers beside them — against the oracle
+ * (tests/test_nif_layer.py compares the output).
  *
  * usage: batch_gpu_check <script> <out>
  * script lines (fields separated by one space; the topic/filter is the rest
@@ -29,8 +29,7 @@
  *   W <records|ranges> <threads> <batch> <passes>
  *                                         batchers match every publish
  *                                         over and over (at least <passes>
- *                                         times, yielding every 512
- *                                         publishes as the NIF does) while a
+ *                                         times) while a
  *                                         writer applies the churn groups one
  *                                         apply each, ~1 ms apart: changes
  *                                         that DO alter the answers, some
@@ -99,30 +98,25 @@ static int put_entry(void* acc, const vmqgb_entry* e) {
 static volatile int writer_done;
 
 /* one batch of publishes [lo, lo + n) exactly as vmqg_nif.c's match/4: the
- * batched prepare in slices with a yield between, the combined device call,
- * the fold (records: yielding), the release; one output line per publish */
+ * batched prepare, the combined device call, the fold, the release (no lock
+ * anywhere); one output line per publish */
 static int one_batch(bt_t* a, vmqgb_batch* b, long* idx, size_t lo, size_t n, char** lines, sbuf* wout) {
-  vmqgb_view_read_begin(view);
   vmqgb_batch_reset(b);
-  for (size_t s0 = 0; s0 < n; s0 += VMQGB_YIELD_EVERY) {
-    const size_t k = n - s0 < VMQGB_YIELD_EVERY ? n - s0 : VMQGB_YIELD_EVERY;
-    if (s0) vmqgb_view_yield(view);
-    const uint8_t* tp[VMQGB_YIELD_EVERY];
-    size_t tl[VMQGB_YIELD_EVERY];
-    uint32_t mp[VMQGB_YIELD_EVERY];
-    for (size_t i = 0; i < k; i++) {
-      tp[i] = (const uint8_t*)pubs[lo + s0 + i].topic;
-      tl[i] = pubs[lo + s0 + i].len;
-      mp[i] = pubs[lo + s0 + i].mp;
-    }
-    const int rc = vmqgb_batch_add_many(b, ctx, k, mp, tp, tl, idx + s0);
-    if (rc) { vmqgb_view_read_end(view); return rc; }
+  const uint8_t** tp = (const uint8_t**)malloc(n * sizeof(*tp));
+  size_t* tl = (size_t*)malloc(n * sizeof(size_t));
+  uint32_t* mp = (uint32_t*)malloc(n * sizeof(uint32_t));
+  for (size_t i = 0; i < n; i++) {
+    tp[i] = (const uint8_t*)pubs[lo + i].topic;
+    tl[i] = pubs[lo + i].len;
+    mp[i] = pubs[lo + i].mp;
   }
+  const int prc = vmqgb_batch_add_many(b, ctx, n, mp, tp, tl, idx);
+  free(tp); free(tl); free(mp);
+  if (prc) return prc;
   const vmqg_emit* recs = NULL;
   uint64_t nrecs = 0;
   const int rc = vmqgb_view_match(view, b, a->ranges, &recs, &nrecs);
   for (size_t i = 0; i < n; i++) {
-    if (!a->ranges && i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(view);   /* records: copies */
     sbuf s = {0, 0, 0};
     char h[64];
     int frc = idx[i] < 0 ? (int)idx[i] : rc;
@@ -139,7 +133,6 @@ static int one_batch(bt_t* a, vmqgb_batch* b, long* idx, size_t lo, size_t n, ch
     else lines[lo + i] = line.buf;
   }
   vmqgb_view_release(view, b);
-  vmqgb_view_read_end(view);
   return 0;
 }
 

@@ -96,6 +96,13 @@ int enif_is_identical(ERL_NIF_TERM lhs, ERL_NIF_TERM rhs);
 int enif_term_to_binary(ErlNifEnv* env, ERL_NIF_TERM term, ErlNifBinary* bin);
 void enif_release_binary(ErlNifBinary* bin);
 
+/* threads (erl_drv / erl_nif mutexes) */
+typedef struct enif_mutex_t ErlNifMutex;
+ErlNifMutex* enif_mutex_create(char* name);
+void enif_mutex_destroy(ErlNifMutex* mtx);
+void enif_mutex_lock(ErlNifMutex* mtx);
+void enif_mutex_unlock(ErlNifMutex* mtx);
+
 /* resources */
 ErlNifResourceType* enif_open_resource_type(ErlNifEnv* env, const char* module_str, const char* name,
                                             ErlNifResourceDtor* dtor, ErlNifResourceFlags flags,

@@ -376,3 +376,15 @@ void mock_print(FILE* f, ERL_NIF_TERM t) {
 }
 
 const char* mock_atom_name(ERL_NIF_TERM t) { return C(t)->type == T_ATOM ? (const char*)C(t)->bytes : NULL; }
+
+/* mutexes: pthread mutexes, as the emulator's on Linux */
+struct enif_mutex_t { pthread_mutex_t m; };
+ErlNifMutex* enif_mutex_create(char* name) {
+  (void)name;
+  ErlNifMutex* x = (ErlNifMutex*)calloc(1, sizeof(ErlNifMutex));
+  if (x && pthread_mutex_init(&x->m, NULL) != 0) { free(x); return NULL; }
+  return x;
+}
+void enif_mutex_destroy(ErlNifMutex* mtx) { if (mtx) { pthread_mutex_destroy(&mtx->m); free(mtx); } }
+void enif_mutex_lock(ErlNifMutex* mtx) { pthread_mutex_lock(&mtx->m); }
+void enif_mutex_unlock(ErlNifMutex* mtx) { pthread_mutex_unlock(&mtx->m); }

@@ -116,14 +116,12 @@ int main(void) {
     CHECK(v != NULL);
     vmqgb_batch bv;
     CHECK(vmqgb_batch_init(&bv, 4) == 0);
-    vmqgb_view_read_begin(v);
     CHECK(vmqgb_batch_add(&bv, ctx, 0, (const uint8_t*)"a/b/c", 5) == 0);
     const vmqg_emit* r0 = NULL;
     uint64_t n0 = 0;
     CHECK(vmqgb_view_match(v, &bv, 0, NULL, NULL) == VMQG_E_DEVICE);
     CHECK(vmqgb_view_match(v, &bv, 1, &r0, &n0) == VMQG_E_DEVICE);
     vmqgb_view_release(v, &bv);
-    vmqgb_view_read_end(v);
     vmqgb_view_stats vs;
     vmqgb_view_get_stats(v, &vs);
     CHECK(vs.rounds == 0);

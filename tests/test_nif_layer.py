@@ -25,6 +25,24 @@ def test_batch_layer_unit(tmp_path):
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
 
 
+def test_readers_beside_the_writer_on_a_host_context(tmp_path):
+    """tests/c/rcu_check.c: six reader threads prepare word lists and pin the
+    readers' record table while one writer interns words and rewrites a key
+    at every apply (include/vmqg.h ABI 6 roles): every word id a reader sees
+    is the one interned, every pinned table is exactly its epoch's."""
+    from vernemq_amd import _lib
+    lib_dir = os.path.dirname(_lib.LIB_PATH)
+    exe = tmp_path / "rcu_check"
+    subprocess.run(["gcc", "-std=gnu11", "-O1", "-Wall", "-Wextra", "-Werror", "-pthread",
+                    "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "integration", "c_src"),
+                    "-o", str(exe), os.path.join(ROOT, "tests", "c", "rcu_check.c"),
+                    os.path.join(ROOT, "integration", "c_src", "vmqg_batch.c"),
+                    "-L", lib_dir, "-l:libvmqgpu.so", "-Wl,-rpath," + lib_dir], check=True)
+    for _ in range(3):
+        r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+
+
 def test_nif_sources_are_present():
     """The Erlang drop-in and its NIF glue ship as files (OTP is not in this
     image: they are not compiled here; their C core above is)."""

@@ -6,9 +6,10 @@
  *
  * Threading exactly as the NIF's (vmqg_nif.c match/4 under
  * vmq_reg_gpu_batcher): T batcher threads, each with its own batch of B
- * publishes, each batch under the view's read lock (vmqgb_view_*):
- *   prepare  vmqgb_batch_add_many on raw topics (vmq_topic:validate_topic +
- *            word lookup), slices of VMQGB_YIELD_EVERY with a yield between
+ * publishes, no lock anywhere on their path (vmqgb_view_*):
+ *   prepare  vmqgb_batch_add_word_lists on the Topic word lists fold/4 is
+ *            handed (one dictionary lookup per word; the lists are split
+ *            once at start-up, as the Erlang side hands them over split)
  *   match    vmqgb_view_match: the combining submitter (batches queued at
  *            once matched as one device call, rounds pipelined)
  *   fold     every FoldFun argument of every publish (the NIF builds one term
@@ -18,13 +19,14 @@
  *   devrec   records copied by the device over PCIe (vmqgb_view_set_device_records)
  *   churn    subscriber events at 100k/s (config D's 1 %/s of 10M) while 16
  *            and 32 batchers run, applied the way the Erlang view applies
- *            them: "single" = one vmqgb_view_apply per event (round 3's
- *            vmq_reg_gpu_view), "coalesced" = every event queued since the
- *            last apply in one apply (vmq_reg_gpu_view's drain_events +
- *            vmqg_nif:apply_many); the events unsubscribe and resubscribe
- *            real devices/{d}/telemetry/# filters, so they change answers
+ *            them (vmq_reg_gpu_view's drain_events + vmqg_nif:apply_many):
+ *            "coalesced" = the events of a window — from the first event
+ *            queued, 2 ms or 1,000 events, whichever comes first — in one
+ *            apply; the events unsubscribe and resubscribe real
+ *            devices/{d}/telemetry/# filters, so they change answers
+ *   churn1   the same with one apply per event ("single": round 3's view)
  *   load     initialize_trie while matching: a writer interning new
- *            subscriptions as vmqg_nif:add_init does (table lock only, an
+ *            subscriptions as vmqg_nif:add_init does (the writer mutex, an
  *            apply every 65,536) while 16 batchers run
  * Prints one JSON line per configuration.  Needs a GPU.  argv[1]: seconds
  * per configuration (default 3).
@@ -61,6 +63,10 @@ static char* topics;            /* NPUB topics, 40 bytes each, NUL padded */
 static size_t* tlen;
 static const uint8_t** tptr;
 static uint32_t* tmp0;           /* mountpoint 0 for every publish */
+static uint32_t* wcnt;           /* publish i: its word list, words [woff[i], woff[i] + wcnt[i]) */
+static size_t* woff;
+static const uint8_t** wptr;
+static size_t* wlen;
 static size_t NPUB;
 static const size_t NDEV = 1000000, NWILD = 64;
 
@@ -101,14 +107,10 @@ static void* batcher(void* p) {
   size_t lo = ((size_t)a->tid * a->B * 7919) % NPUB;
   while (now() < a->t_end) {
     const double t0 = now();
-    vmqgb_view_read_begin(view);
     vmqgb_batch_reset(&b);
     if (lo + a->B > NPUB) lo = 0;
-    for (size_t s = 0; s < a->B; s += VMQGB_YIELD_EVERY) {
-      const size_t k = a->B - s < VMQGB_YIELD_EVERY ? a->B - s : VMQGB_YIELD_EVERY;
-      if (s) vmqgb_view_yield(view);
-      if (vmqgb_batch_add_many(&b, ctx, k, tmp0 + lo + s, tptr + lo + s, tlen + lo + s, idx + s)) { a->err = 1; break; }
-    }
+    if (vmqgb_batch_add_word_lists(&b, ctx, a->B, tmp0 + lo, wcnt + lo, wptr + woff[lo], wlen + woff[lo], idx))
+      a->err = 1;
     lo = (lo + (size_t)a->T * a->B) % NPUB;
     const double t1 = now();
     const vmqg_emit* recs = NULL;
@@ -116,7 +118,6 @@ static void* batcher(void* p) {
     int rc = a->err ? 0 : vmqgb_view_match(view, &b, a->ranges, &recs, &nrecs);
     const double t2 = now();
     for (size_t i = 0; !rc && i < b.n; i++) {
-      if (!a->ranges && i && i % VMQGB_YIELD_EVERY == 0) vmqgb_view_yield(view);   /* records: copies */
       if (fold_spans) {
         vmqgb_prefetch_entries(&b, a->ranges, recs, nrecs, i + VMQGB_PREFETCH_AHEAD);
         rc = vmqgb_fold_spans(&b, a->ranges, recs, nrecs, i, sum_span, acc);
@@ -124,7 +125,6 @@ static void* batcher(void* p) {
       else rc = a->ranges ? vmqgb_fold_ranges(&b, recs, nrecs, i, sum_entry, acc) : vmqgb_fold(&b, i, sum_entry, acc);
     }
     vmqgb_view_release(view, &b);
-    vmqgb_view_read_end(view);
     const double t3 = now();
     if (rc || a->err) { a->err = rc ? rc : a->err; break; }
     a->pubs += b.n;
@@ -145,7 +145,7 @@ static void* batcher(void* p) {
 typedef struct { uint32_t d, kind; double t; } event_t;
 typedef struct {
   double t_end, rate;
-  int coalesce;                 /* 0: one apply per event; 1: everything queued in one apply */
+  int coalesce;                 /* 0: one apply per event; 1: a window's events in one apply */
   pthread_mutex_t mu;
   event_t* q;
   size_t cap, head, tail;       /* ring */
@@ -193,6 +193,8 @@ static void* applier(void* p) {   /* the vmq_reg_gpu_view gen_server */
   while (now() < c->t_end && !c->err) {
     pthread_mutex_lock(&c->mu);
     size_t n = c->tail - c->head;
+    /* the window: 2 ms after its first event, or 1,000 events (vmq_reg_gpu_view) */
+    if (c->coalesce && n && n < 1000 && now() - c->q[c->head % c->cap].t < 0.002) n = 0;
     if (!c->coalesce && n > 1) n = 1;
     if (n > 10000) n = 10000;
     for (size_t i = 0; i < n; i++) grp[i] = c->q[(c->head + i) % c->cap];
@@ -200,7 +202,7 @@ static void* applier(void* p) {   /* the vmq_reg_gpu_view gen_server */
     pthread_mutex_unlock(&c->mu);
     if (!n) { struct timespec ts = {0, 50000}; nanosleep(&ts, NULL); continue; }
     const double t0 = now();
-    vmqgb_view_write_begin(view);   /* interning happens under the table lock (the NIF's add_change) */
+    vmqgb_view_write_begin(view);   /* interning is the writer's (the NIF's add_change) */
     const double t1 = now();
     for (size_t i = 0; i < n; i++) {
       const int l = snprintf(f, sizeof f, "devices/%u/telemetry/#", grp[i].d);
@@ -386,6 +388,20 @@ int main(int argc, char** argv) {
                                (unsigned long long)(r % (NDEV + NDEV / 4)), (unsigned long long)((r >> 40) % 16));
     tptr[i] = (const uint8_t*)topics + i * 40;
   }
+  /* the word lists fold/4 is handed (split once, as the Erlang side passes them) */
+  wcnt = (uint32_t*)calloc(NPUB, sizeof(uint32_t));
+  woff = (size_t*)calloc(NPUB + 1, sizeof(size_t));
+  wptr = (const uint8_t**)calloc(NPUB * 4, sizeof(*wptr));
+  wlen = (size_t*)calloc(NPUB * 4, sizeof(size_t));
+  size_t nw = 0;
+  for (size_t i = 0; i < NPUB; i++) {
+    woff[i] = nw;
+    size_t st = 0;
+    for (size_t j = 0; j <= tlen[i]; j++)
+      if (j == tlen[i] || tptr[i][j] == '/') { wptr[nw] = tptr[i] + st; wlen[nw] = j - st; nw++; st = j + 1; }
+    wcnt[i] = (uint32_t)(nw - woff[i]);
+  }
+  woff[NPUB] = nw;
   fprintf(stderr, "loaded %zu subscriptions in %.1fs\n", NDEV + NWILD, load_s);
   int rc = 0;
   if (want(argc, argv, "scale")) {
@@ -412,8 +428,10 @@ int main(int argc, char** argv) {
     if (!rc) rc = run("devrec", 32, 4096, 0, secs, NULL, NULL);
     vmqgb_view_set_device_records(view, 0);
   }
-  if (want(argc, argv, "churn")) {
+  {
+    /* "churn": the windowed applies; "churn1" (named only): one apply per event */
     for (int co = 0; co < 2 && !rc; co++)
+      if (co == 1 ? want(argc, argv, "churn") : argc > 2 && want(argc, argv, "churn1"))
       for (int mode = 0; mode < 2 && !rc; mode++)
         for (int T = 16; T <= 32 && !rc; T += 16) {
           churn_t cc;

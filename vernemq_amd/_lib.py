@@ -142,6 +142,8 @@ SIGNATURES = [
     ("vmqg_hbatch_offsets", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     ("vmqg_hbatch_entries", ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     ("vmqg_apply_ops", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, ctypes.POINTER(_U64)]),
+    ("vmqg_apply_stage", ctypes.c_int, [_P, _P, _SZ, _P, _SZ]),
+    ("vmqg_apply_commit", ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
     ("vmqg_match_batch", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
     ("vmqg_match_device", ctypes.c_int, [_P, _P, _U32, _P, _P, _U64, _P, _P]),
     ("vmqg_match_status", ctypes.c_int, [_P, _P]),
@@ -154,6 +156,8 @@ SIGNATURES = [
     ("vmqs_release_stream", ctypes.c_int, [_P, _P]),
     ("vmqg_epoch", ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
     ("vmqg_records_at", ctypes.c_int, [_P, _U64, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
+    ("vmqg_records_pin", ctypes.c_int, [_P, _U64, ctypes.POINTER(_P), ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_uint32)]),
+    ("vmqg_records_unpin", None, [_P, ctypes.c_uint32]),
     ("vmqg_replica_sync_layout", ctypes.c_int, [_P, _P]),
     ("vmqg_stats", ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
     ("vmqg_dump", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_SZ)]),

@@ -249,14 +249,28 @@ int vmqg_prepare_word_lists(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints
 
 uint64_t vmqg_dict_generation(vmqg_ctx* ctx) { return ctx ? ctx->e.dict.generation() : 0; }
 
-int vmqg_apply_ops(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords,
-                   uint64_t* epoch_out) {
+int vmqg_apply_stage(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords) {
   if (!ctx || (n && !ops) || (nwords && !words)) return VMQG_E_INVAL;
   GUARD_BEGIN
-  int rc = ctx->e.apply_ops(ops, n, words, nwords);
+  return ctx->e.stage_ops(ops, n, words, nwords);
+  GUARD_END
+}
+
+int vmqg_apply_commit(vmqg_ctx* ctx, uint64_t* epoch_out) {
+  if (!ctx) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  const int rc = ctx->e.commit();
   if (epoch_out) *epoch_out = ctx->e.epoch;
   return rc;
   GUARD_END
+}
+
+int vmqg_apply_ops(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords,
+                   uint64_t* epoch_out) {
+  const int rc = vmqg_apply_stage(ctx, ops, n, words, nwords);
+  if (rc && (!ctx || !ctx->e.staged)) return rc;   // rejected before any change
+  const int rc2 = vmqg_apply_commit(ctx, epoch_out);
+  return rc ? rc : rc2;
 }
 
 static int grow(void** p, uint64_t* cap, uint64_t need) {
@@ -569,6 +583,18 @@ int vmqg_records_at(vmqg_ctx* ctx, uint64_t epoch, const vmqg_emit** recs, uint6
   return vmqg_records(ctx, recs, n);
 }
 
+int vmqg_records_pin(vmqg_ctx* ctx, uint64_t epoch, const vmqg_emit** recs, uint64_t* n, uint32_t* pin) {
+  if (!ctx || !recs || !n || !pin) return VMQG_E_INVAL;
+  const vmqg::Record* r = nullptr;
+  const int rc = ctx->e.records_pin(epoch, &r, n, pin);
+  *recs = reinterpret_cast<const vmqg_emit*>(r);
+  return rc;
+}
+
+void vmqg_records_unpin(vmqg_ctx* ctx, uint32_t pin) {
+  if (ctx) ctx->e.records_unpin(pin);
+}
+
 int vmqg_release_stream(vmqg_ctx* ctx, void* stream) {
   if (!ctx) return VMQG_E_INVAL;
   if (!ctx->e.has_device) return VMQG_OK;
@@ -646,6 +672,9 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   } else if (n == "heavy_min") {
     if (value < 0 || value > (1 << 30)) return VMQG_E_INVAL;
     e.opt_heavy_min = (uint32_t)value;
+  } else if (n == "reader_records") {   // the readers' record buffers (vmqg_records_pin): on only
+    if (value != 1 || e.replica) return VMQG_E_INVAL;
+    e.enable_reader_records();
   } else if (n == "exfilter") {
     if (value < 0 || value > 2) return VMQG_E_INVAL;
     e.opt_exfilter = (uint32_t)value;
@@ -697,8 +726,8 @@ int vmqg_kernel_times_ex(vmqg_ctx* ctx, double* stage_ns, uint64_t* launches) {
 int vmqg_arena(vmqg_ctx* ctx, void** d_ptr, uint64_t* bytes, uint8_t* layout_out) {
   if (!ctx) return VMQG_E_INVAL;
   if (d_ptr) *d_ptr = ctx->e.d_arena;
-  if (bytes) *bytes = ctx->e.lay.total_bytes;
-  if (layout_out) memcpy(layout_out, &ctx->e.lay, sizeof(vmqg::Layout));
+  if (bytes) *bytes = ctx->e.dlay.total_bytes;
+  if (layout_out) memcpy(layout_out, &ctx->e.dlay, sizeof(vmqg::Layout));
   return VMQG_OK;
 }
 
@@ -734,6 +763,7 @@ int vmqg_replica_load(vmqg_ctx* ctx, const uint8_t* layout, const void* d_src, v
     e.d_arena_bytes = L.total_bytes;
   }
   e.lay = L;
+  e.dlay = L;
   // after the matches already queued, before the ones queued later
   if (e.order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
   if (hipMemcpyAsync(e.d_arena, d_src, L.total_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
@@ -762,6 +792,7 @@ int vmqg_replica_sync_layout(vmqg_ctx* ctx, const uint8_t* layout) {
   a.max_depth = b.max_depth = 0;
   if (memcmp(&a, &b, sizeof(a)) != 0) return VMQG_E_STATE;
   e.lay.max_depth = L.max_depth;
+  e.dlay.max_depth = L.max_depth;
   return VMQG_OK;
 }
 

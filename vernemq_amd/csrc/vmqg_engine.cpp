@@ -834,7 +834,18 @@ void Engine::handle_delete(const vmqg_op& op, const uint32_t* w) {
 }
 
 int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords) {
+  const int rc = stage_ops(ops, n, words, nwords);
+  if (rc && !staged) return rc;   // rejected before any change
+  const int rc2 = commit();
+  return rc ? rc : rc2;
+}
+
+// The host half of an apply: the state machine, the mirror, the patch list,
+// the readers' record buffer.  Runs while match calls are queued and
+// running (they read only the device side: dlay, the arena, scratch).
+int Engine::stage_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords) {
   if (replica) return VMQG_E_STATE;
+  if (staged) return VMQG_E_STATE;   // the previous stage is not committed yet
   const auto t0 = std::chrono::steady_clock::now();
   // validate the whole batch before touching state
   uint64_t add_words = 0;
@@ -851,6 +862,8 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
     if (o.kind == VMQG_OP_ADD && ((o.nwords >= 3 && w[0] == kShare) || contains_wildcard(w, o.nwords)))
       add_words += o.nwords;
   }
+  staged = true;
+  staged_epoch = epoch + 1;
   // the edge table must absorb every edge this batch could add
   if ((edge_live + edge_tomb + add_words) * 10 > lay.edge_buckets * kEdgeSlotsPerBucket * 7) rebuild(add_words);
   for (size_t i = 0; i < n; i++) {
@@ -871,25 +884,39 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
   for (uint32_t t : dirty_topics) topics[t].dirty = 0;
   dirty_keys.clear(); dirty_paths.clear(); dirty_topics.clear();
   lay.max_depth = max_depth;   // replicas size their stacks from the layout
-  epoch++;
   ops_applied += n;
+  stage_patches();
+  if (rb_on) publish_records();
+  patches_ready = true;
+  apply_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                       std::chrono::steady_clock::now() - t0).count();
+  return VMQG_OK;
+}
+
+// The device half: ships what the stage left (serialised with match calls
+// by the caller), after which matches see the new tables.
+int Engine::commit() {
+  if (!staged) return VMQG_OK;
+  if (!patches_ready) {   // a stage that ended early (out of memory): ship what it changed
+    stage_patches();
+    if (rb_on) publish_records();
+  }
   const auto t1 = std::chrono::steady_clock::now();
   const int rc = upload();
-  const auto t2 = std::chrono::steady_clock::now();
-  apply_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t0).count();
-  apply_upload_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+  staged = false;
+  patches_ready = false;
+  epoch = staged_epoch;
+  apply_upload_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                         std::chrono::steady_clock::now() - t1).count();
   return rc;
 }
 
-// --------------------------------------------------------------- device
-// Ships the pending changes: a patch batch (the 16-B dirty chunks), or the
-// whole image after a re-layout.  Patches are staged in a ring of pinned
-// buffers and applied by k_apply_patches on the context stream after
-// everything queued before (matches included); the call does not wait for
-// them.  A full image is copied synchronously (re-layouts are rare and the
-// arena may be reallocated).
-int Engine::upload() {
+// The pending changes as a patch list (the 16-B dirty chunks) or, after a
+// re-layout, the whole image; the record slots among them (rec_epoch, the
+// readers' buffers).
+void Engine::stage_patches() {
   last_patches.clear();
+  rb_changed.clear();
   if (!full_image && dirty_chunks.size() * sizeof(Patch) > lay.total_bytes / 2) {
     // patches would outweigh the image (bulk loads): ship the image instead
     full_image = true;
@@ -900,9 +927,13 @@ int Engine::upload() {
   if (!full_image) {
     last_patches.reserve(dirty_chunks.size());
     const uint8_t* base = reinterpret_cast<const uint8_t*>(mirror.data());
+    static_assert(sizeof(Record) == 16, "a record is one 16-B chunk");
     const uint64_t rec_lo = lay.rec_off >> 4, rec_hi = (lay.rec_off + lay.rec_cap * sizeof(Record)) >> 4;
     for (uint64_t c : dirty_chunks) {
-      if (c >= rec_lo && c < rec_hi) rec_epoch = epoch;   // a record slot rewritten: older ranges are stale
+      if (c >= rec_lo && c < rec_hi) {   // a record slot rewritten: older ranges are stale
+        rec_epoch = staged_epoch;
+        if (rb_on) rb_changed.push_back(c - rec_lo);
+      }
       Patch p;
       p.off = c * 16;
       memcpy(p.data, base + p.off, 16);
@@ -913,8 +944,82 @@ int Engine::upload() {
     patch_bytes += last_patches.size() * sizeof(Patch);
   } else {
     image_bytes += lay.total_bytes;
-    rec_epoch = epoch;   // re-laid out: every record may have moved
+    rec_epoch = staged_epoch;   // re-laid out: every record may have moved
   }
+}
+
+// Left-right update of the readers' record buffers: close the inactive one,
+// wait for the readers still on it (rounds more than one apply old: rare),
+// bring it to this stage's records, open it and send new readers there.
+void Engine::publish_records() {
+  const uint32_t cur = rb_active.load(std::memory_order_relaxed);
+  RecBuf& b = rb[cur ^ 1];
+  b.closed.store(1, std::memory_order_seq_cst);
+  if (b.readers.load(std::memory_order_seq_cst) != 0) {
+    const auto w0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0; b.readers.load(std::memory_order_seq_cst) != 0; spin++)
+      if (spin > 256) sched_yield();
+    rb_waits++;
+    rb_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                      std::chrono::steady_clock::now() - w0).count();
+  }
+  const Record* src = region<Record>(lay.rec_off);
+  if (last_full || rb_full_next || b.recs.size() != lay.rec_cap) {
+    b.recs.assign(src, src + lay.rec_cap);
+  } else {
+    for (uint64_t i : rb_prev) b.recs[i] = src[i];
+    for (uint64_t i : rb_changed) b.recs[i] = src[i];
+  }
+  b.epoch = staged_epoch;
+  b.rec_epoch = rec_epoch;
+  b.closed.store(0, std::memory_order_seq_cst);
+  rb_active.store(cur ^ 1, std::memory_order_release);
+  rb_full_next = last_full;
+  rb_prev.swap(rb_changed);
+}
+
+// Both buffers from the committed state (the writer's side, before any reader).
+void Engine::enable_reader_records() {
+  if (rb_on) return;
+  const Record* src = region<Record>(lay.rec_off);
+  for (RecBuf& b : rb) {
+    b.recs.assign(src, src + lay.rec_cap);
+    b.epoch = epoch;
+    b.rec_epoch = rec_epoch;
+    b.closed.store(0, std::memory_order_seq_cst);
+  }
+  rb_prev.clear();
+  rb_full_next = false;
+  rb_on = true;
+}
+
+// A reader's pin on a buffer holding the records of epoch `ep` (its round's):
+// the active one, else the other while it is still open.  Never waits.
+int Engine::records_pin(uint64_t ep, const Record** recs, uint64_t* n, uint32_t* pin) {
+  if (!rb_on) return VMQG_E_STATE;
+  const uint32_t first = rb_active.load(std::memory_order_acquire);
+  for (uint32_t k = 0; k < 2; k++) {
+    RecBuf& b = rb[first ^ k];
+    b.readers.fetch_add(1, std::memory_order_seq_cst);
+    if (!b.closed.load(std::memory_order_seq_cst) && b.rec_epoch <= ep && ep <= b.epoch) {
+      *recs = b.recs.data();
+      *n = b.recs.size();
+      *pin = first ^ k;
+      return VMQG_OK;
+    }
+    b.readers.fetch_sub(1, std::memory_order_release);
+  }
+  return VMQG_E_STATE;
+}
+
+// --------------------------------------------------------------- device
+// Ships the staged changes: a patch batch or the whole image.  Patches are
+// staged in a ring of pinned buffers and applied by k_apply_patches on the
+// context stream after everything queued before (matches included); the
+// call does not wait for them.  A full image is copied synchronously
+// (re-layouts are rare and the arena may be reallocated).
+int Engine::upload() {
+  dlay = lay;
   if (!has_device) { full_image = false; return VMQG_OK; }
   hipSetDevice(device);
   // tables must not change under a match still reading them (queued on any

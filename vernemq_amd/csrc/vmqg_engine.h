@@ -117,11 +117,28 @@ class FlatIndex {
 // 64-bit hash, id, length and first 16 bytes, so looking up a word of at most
 // 16 bytes touches one cache line — the publish hot path (vmqg_prepare_publish*)
 // is one such lookup per word, and the batched form prefetches a block of
-// topics' slots before resolving any.  Lookups never write: readers share the
-// dictionary under the host view's read lock; inserts come from writers.
+// topics' slots before resolving any.
+//
+// One writer, any number of readers, no lock (vmq_reg_trie's tables are
+// read_concurrency ETS, vmq_reg_trie.erl:136-137): lookups never write and
+// never wait.  A slot is filled before its id is published (release; readers
+// load the id with acquire, then the rest); a table that grows is rebuilt
+// aside and swapped in whole, the old one kept until the dictionary dies
+// (readers may still be probing it; all retired tables together are smaller
+// than the live one); word texts live in fixed chunks that never move.  A
+// reader that started before an insert may miss that word: the batch layer's
+// generation check (vmqgb_batch_recheck) prepares such publishes again.
 class WordDict {
  public:
   static constexpr uint32_t kVoid = 0xFFFFFFFFu;
+  WordDict() : dir_(new std::atomic<std::string*>[kChunks]) {
+    for (uint32_t i = 0; i < kChunks; i++) dir_[i].store(nullptr, std::memory_order_relaxed);
+  }
+  ~WordDict() {
+    for (uint32_t i = 0; i < kChunks; i++) delete[] dir_[i].load(std::memory_order_relaxed);
+  }
+  WordDict(const WordDict&) = delete;
+  WordDict& operator=(const WordDict&) = delete;
   // a word as the lookup sees it: hash and its first 16 bytes, zero padded
   struct Key { uint64_t h, k0, k1; const uint8_t* p; size_t n; };
   static Key key(const uint8_t* p, size_t n) {
@@ -154,53 +171,84 @@ class WordDict {
     return k;
   }
   void prefetch(const Key& k) const {
-    if (mask_) __builtin_prefetch(&slots_[k.h & mask_]);
+    const Table* t = tab_.load(std::memory_order_acquire);
+    if (t) __builtin_prefetch(&t->slots[k.h & t->mask]);
   }
   uint32_t find(const Key& k) const {
-    if (!mask_) return kVoid;
-    for (uint64_t i = k.h & mask_;; i = (i + 1) & mask_) {
-      const Slot& s = slots_[i];
-      if (s.id == kVoid) return kVoid;
-      if (s.h == k.h && s.len == k.n && s.k0 == k.k0 && s.k1 == k.k1 &&
-          (k.n <= 16 || memcmp(text_[s.id].data() + 16, k.p + 16, k.n - 16) == 0))
-        return s.id;
-    }
+    const Table* t = tab_.load(std::memory_order_acquire);
+    return t ? find_in(*t, k) : kVoid;
   }
-  // id of the word, added as the next dense id when absent
+  // id of the word, added as the next dense id when absent (the writer only)
   uint32_t intern(const Key& k) {
     const uint32_t f = find(k);
     if (f != kVoid) return f;
-    if ((text_.size() + 1) * 2 > slots_.size()) regrow(std::max<uint64_t>(1024, slots_.size() * 2));
-    const uint32_t id = (uint32_t)text_.size();
-    text_.emplace_back(reinterpret_cast<const char*>(k.p), k.n);
-    put(Slot{k.h, id, (uint32_t)k.n, k.k0, k.k1});
-    count_.store(text_.size(), std::memory_order_release);
+    const uint64_t n = count_.load(std::memory_order_relaxed);
+    if (n >= 0xFFFFFF00ull) throw std::bad_alloc();   // ids above are reserved (kUnknownWord, ...)
+    const Table* t = tab_.load(std::memory_order_relaxed);
+    if (!t || (n + 1) * 2 > t->mask + 1) t = regrow(std::max<uint64_t>(1024, t ? (t->mask + 1) * 2 : 0));
+    const uint32_t id = (uint32_t)n;
+    std::string* chunk = dir_[id >> kChunkBits].load(std::memory_order_relaxed);
+    if (!chunk) {
+      chunk = new std::string[kChunkWords];
+      dir_[id >> kChunkBits].store(chunk, std::memory_order_release);
+    }
+    chunk[id & (kChunkWords - 1)].assign(reinterpret_cast<const char*>(k.p), k.n);
+    put(*t, Slot{k.h, id, (uint32_t)k.n, k.k0, k.k1});
+    count_.store(n + 1, std::memory_order_release);
     return id;
   }
-  const std::string& text(uint32_t id) const { return text_[id]; }
-  size_t size() const { return text_.size(); }
-  // words interned so far, readable without the lock (the batch layer's
-  // staleness check of prepared publishes that held unknown words)
+  const std::string& text(uint32_t id) const {
+    return dir_[id >> kChunkBits].load(std::memory_order_acquire)[id & (kChunkWords - 1)];
+  }
+  size_t size() const { return count_.load(std::memory_order_acquire); }
+  // words interned so far (the batch layer's staleness check of prepared
+  // publishes that held unknown words)
   uint64_t generation() const { return count_.load(std::memory_order_acquire); }
 
  private:
+  static constexpr uint32_t kChunkBits = 16, kChunkWords = 1u << kChunkBits, kChunks = 1u << 16;
   struct alignas(32) Slot { uint64_t h; uint32_t id, len; uint64_t k0, k1; };
-  void put(const Slot& s) {
-    for (uint64_t i = s.h & mask_;; i = (i + 1) & mask_)
-      if (slots_[i].id == kVoid) { slots_[i] = s; return; }
+  struct Table {
+    HugeVec<Slot> slots;
+    uint64_t mask;
+  };
+  static uint32_t load_id(const Slot& s) { return __atomic_load_n(&s.id, __ATOMIC_ACQUIRE); }
+  uint32_t find_in(const Table& t, const Key& k) const {
+    for (uint64_t i = k.h & t.mask;; i = (i + 1) & t.mask) {
+      const Slot& s = t.slots[i];
+      const uint32_t id = load_id(s);
+      if (id == kVoid) return kVoid;
+      if (s.h == k.h && s.len == k.n && s.k0 == k.k0 && s.k1 == k.k1 &&
+          (k.n <= 16 || memcmp(text(id).data() + 16, k.p + 16, k.n - 16) == 0))
+        return id;
+    }
   }
-  void regrow(uint64_t want) {
+  // the id is stored last: a reader that sees it sees the slot's other fields
+  static void put(const Table& t, const Slot& s) {
+    Slot* sl = const_cast<Slot*>(t.slots.data());
+    for (uint64_t i = s.h & t.mask;; i = (i + 1) & t.mask)
+      if (sl[i].id == kVoid) {
+        sl[i].h = s.h; sl[i].len = s.len; sl[i].k0 = s.k0; sl[i].k1 = s.k1;
+        __atomic_store_n(&sl[i].id, s.id, __ATOMIC_RELEASE);
+        return;
+      }
+  }
+  const Table* regrow(uint64_t want) {
     uint64_t cap = 1;
     while (cap < want) cap <<= 1;
-    HugeVec<Slot> old;
-    old.swap(slots_);
-    slots_.assign(cap, Slot{0, kVoid, 0, 0, 0});
-    mask_ = cap - 1;
-    for (const Slot& s : old) if (s.id != kVoid) put(s);
+    auto nt = std::make_unique<Table>();
+    nt->slots.assign(cap, Slot{0, kVoid, 0, 0, 0});
+    nt->mask = cap - 1;
+    if (const Table* old = tab_.load(std::memory_order_relaxed))
+      for (const Slot& s : old->slots) if (s.id != kVoid) put(*nt, s);
+    const Table* t = nt.get();
+    tables_.push_back(std::move(nt));       // the old tables stay: readers may be probing them
+    tab_.store(t, std::memory_order_release);
+    return t;
   }
-  HugeVec<Slot> slots_;
-  uint64_t mask_ = 0;
-  std::vector<std::string> text_;
+  std::atomic<const Table*> tab_{nullptr};
+  std::vector<std::unique_ptr<Table>> tables_;
+  std::unique_ptr<std::atomic<std::string*>[]> dir_;   // word texts, kChunkWords per chunk
   std::atomic<uint64_t> count_{0};
 };
 
@@ -273,7 +321,8 @@ struct Engine {
   uint64_t n_trie_nodes = 0, n_trie_topics = 0, n_subs_objects = 0, n_fanout = 0, n_remote_keys = 0;
 
   // ---- mirror of the device arena
-  Layout lay{};
+  Layout lay{};                     // the host mirror's layout (the writer's)
+  Layout dlay{};                    // the device arena's: what match calls read (set by commit)
   HugeVec<uint64_t> mirror;         // lay.total_bytes / 8 words
   HugeVec<uint64_t> dirty_bits;     // one bit per 16-B chunk
   std::vector<uint64_t> dirty_chunks;
@@ -281,7 +330,12 @@ struct Engine {
   uint64_t edge_live = 0, edge_tomb = 0, exact_live = 0, exact_tomb = 0;
   uint64_t rec_top = 0, rec_garbage = 0, kl_top = 0, kl_garbage = 0, xw_top = 0, xw_garbage = 0;
   bool full_image = false;          // the pending upload is a whole image
+  // epoch: the tables the device holds (matches queued now see them); an
+  // apply is staged on the host (staged_epoch = epoch + 1) while matches
+  // run, then committed: shipped to the device, epoch = staged_epoch
   uint64_t epoch = 0, rebuilds = 0;
+  uint64_t staged_epoch = 0;
+  bool staged = false, patches_ready = false;
   uint32_t max_depth = 0;           // deepest path interned (sizes the wave tier's stack)
   std::vector<Patch> last_patches;
   bool last_full = false;
@@ -341,6 +395,23 @@ struct Engine {
   // arena): range results of an older epoch index records that may have
   // changed (vmqg_records_at refuses them)
   uint64_t rec_epoch = 0;
+  // Readers' copies of the record table (vmqg_records_pin, option
+  // "reader_records"): two buffers, left-right.  Readers pin the buffer whose
+  // epochs cover their round's and never wait; the writer brings the other
+  // one up to date (the records its last two applies changed) once the
+  // readers still on it have left, then directs new readers to it.
+  struct RecBuf {
+    HugeVec<Record> recs;
+    uint64_t epoch = 0, rec_epoch = 0;   // content = the tables of every epoch in [rec_epoch, epoch]
+    std::atomic<uint32_t> readers{0};
+    std::atomic<uint32_t> closed{1};     // the writer is updating it: no new readers
+  };
+  RecBuf rb[2];
+  std::atomic<uint32_t> rb_active{0};
+  bool rb_on = false;
+  bool rb_full_next = true;             // the inactive buffer needs a whole copy (re-layout)
+  std::vector<uint64_t> rb_prev, rb_changed;   // record slots the last / this apply changed
+  uint64_t rb_waits = 0, rb_wait_ns = 0;       // the writer waited for readers to leave a buffer
   // device status: two per-call counter sets of kStatusSet words, then the sticky error word
   static constexpr uint32_t kStatusSet = 32, kStatusBytes = 512;
   static constexpr uint32_t kStatusDdMode = 100;   // persistent word: the dedupe mode the last call chose
@@ -359,7 +430,14 @@ struct Engine {
   const std::string& word_text(uint32_t id) const { return dict.text(id); }
 
   // state machine (vmq_reg_trie.erl:253-539)
-  int apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords);
+  int apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords);   // stage + commit
+  int stage_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords);   // host half
+  int commit();                                                                         // device half
+  void stage_patches();
+  void publish_records();
+  int records_pin(uint64_t ep, const Record** recs, uint64_t* n, uint32_t* pin);
+  void records_unpin(uint32_t pin) { rb[pin & 1].readers.fetch_sub(1, std::memory_order_release); }
+  void enable_reader_records();
   void handle_add(const vmqg_op& op, const uint32_t* w);
   void handle_delete(const vmqg_op& op, const uint32_t* w);
   void add_complex_topic(uint32_t mp, const uint32_t* w, uint32_t L, Nog nog, bool wildcard);
@@ -406,7 +484,7 @@ struct Engine {
   // out_rng == null: records mode into out; else range mode into out_rng
   int match_device(const vmqg_pub* d_pubs, uint32_t npub, const uint32_t* d_words, Record* d_out,
                    uint64_t out_cap, vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets, hipStream_t st);
-  uint32_t stack_depth() const { return (uint32_t)std::max<uint64_t>(max_depth, lay.max_depth); }
+  uint32_t stack_depth() const { return dlay.max_depth; }   // the device tables' deepest path
   int match_status(hipStream_t st);
   void collect_times();
 
