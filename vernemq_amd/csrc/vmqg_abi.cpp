@@ -661,6 +661,8 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   if (n == "fast_g") {
     if (value != 1 && value != 2 && value != 4) return VMQG_E_INVAL;
     e.opt_fast_g = (uint32_t)value;
+  } else if (n == "root_flags") {
+    e.opt_flags = value ? (e.opt_flags | vmqg::kOptRootFlags) : (e.opt_flags & ~vmqg::kOptRootFlags);
   } else if (n == "nt_stores") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptNtStores) : (e.opt_flags & ~vmqg::kOptNtStores);
   } else if (n == "dedupe") {

@@ -56,6 +56,9 @@ constexpr uint32_t kNodeTopic = 2u;     // ... and its `topic` field is set
 constexpr uint32_t kNodeFilter = 4u;    // vmq_trie_topic entry exists for the path
 constexpr uint32_t kNodeDollarSkip = 8u;  // path is [#] or starts with + (:285-288)
 constexpr uint32_t kNodeHigh = 16u;       // remote nodes >= 64 listed at {hi_off, hi_cnt} (keylist pool)
+// a root (path id < max_mountpoints) has no incoming edge slot to cache its
+// child flags: its own record carries them, kHas* << kRootFlagShift
+constexpr uint32_t kRootFlagShift = 5;
 constexpr uint32_t kNodeEmits = kNodeRec | kNodeTopic | kNodeFilter;
 
 // child flags cached in EdgeSlot.flags
@@ -118,7 +121,7 @@ struct Layout {
   uint64_t pad[11];
 };
 static_assert(sizeof(Layout) == 256, "layout must be 256 bytes");
-constexpr uint64_t kLayoutMagic = 0x33676D7176ull;  // "vmqg3" (64-B exact slots with inline words; exbits one per slot)
+constexpr uint64_t kLayoutMagic = 0x34676D7176ull;  // "vmqg4" (64-B exact slots with inline words; exbits one per slot; root child flags)
 
 // 24-byte patch record: write 16 bytes at arena offset `off` (16-B aligned).
 struct Patch { uint64_t off; uint32_t data[4]; };

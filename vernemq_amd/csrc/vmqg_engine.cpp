@@ -213,7 +213,8 @@ void Engine::touch(uint64_t off, uint64_t bytes) {
 // skip probes that must miss).
 void Engine::refresh_incoming_flags(uint32_t node) {
   const PathInfo& P = paths[node];
-  if (P.parent == kNone || P.in_slot == ~0ull) return;   // roots are always probed for both
+  if (P.parent == kNone) { mark_path(node); return; }   // a root: its own record carries them (write_path)
+  if (P.in_slot == ~0ull) return;
   EdgeSlot& s = region<EdgeSlot>(lay.edge_off)[P.in_slot];
   if (s.flags != P.eflags) {
     s.flags = P.eflags;
@@ -408,6 +409,7 @@ bool Engine::write_path(uint32_t p) {
   if (P.rec && P.topic_set) flags |= kNodeTopic;
   if (P.filter) flags |= kNodeFilter;
   if (P.dollar_skip) flags |= kNodeDollarSkip;
+  if (P.parent == kNone) flags |= (uint32_t)(P.eflags & kHasAll) << kRootFlagShift;
   std::vector<uint32_t> ks;
   std::vector<uint32_t>& high = scratch_u32;
   high.clear();
@@ -1164,23 +1166,25 @@ int Engine::ensure_wave_scratch(hipStream_t st) {
   return VMQG_OK;
 }
 
+// The device tables as the last commit left them (dlay): a stage running
+// beside this call may be re-laying the host mirror out (lay).
 MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* words, uint64_t* offs) const {
   MatchArgs a{};
-  a.edges = reinterpret_cast<const EdgeSlot*>(d_arena + lay.edge_off);
-  a.edge_mask = lay.edge_buckets - 1;
-  a.nodes = reinterpret_cast<const NodeRec*>(d_arena + lay.node_off);
-  a.node_cap = lay.node_cap;
-  a.keydesc = reinterpret_cast<const KeyDesc*>(d_arena + lay.keydesc_off);
-  a.key_cap = lay.key_cap;
-  a.keylist = reinterpret_cast<const uint32_t*>(d_arena + lay.keylist_off);
-  a.records = reinterpret_cast<const Record*>(d_arena + lay.rec_off);
-  a.exact = reinterpret_cast<const ExactSlot*>(d_arena + lay.exact_off);
-  a.exact_mask = lay.exact_buckets - 1;
-  a.exwords = reinterpret_cast<const uint32_t*>(d_arena + lay.exwords_off);
-  a.exbits = reinterpret_cast<const uint32_t*>(d_arena + lay.exbits_off);
-  a.exbits_mask = lay.exbits_words * 32 - 1;
-  a.max_mp = (uint32_t)lay.max_mountpoints;
-  a.local_node = (uint32_t)lay.local_node;
+  a.edges = reinterpret_cast<const EdgeSlot*>(d_arena + dlay.edge_off);
+  a.edge_mask = dlay.edge_buckets - 1;
+  a.nodes = reinterpret_cast<const NodeRec*>(d_arena + dlay.node_off);
+  a.node_cap = dlay.node_cap;
+  a.keydesc = reinterpret_cast<const KeyDesc*>(d_arena + dlay.keydesc_off);
+  a.key_cap = dlay.key_cap;
+  a.keylist = reinterpret_cast<const uint32_t*>(d_arena + dlay.keylist_off);
+  a.records = reinterpret_cast<const Record*>(d_arena + dlay.rec_off);
+  a.exact = reinterpret_cast<const ExactSlot*>(d_arena + dlay.exact_off);
+  a.exact_mask = dlay.exact_buckets - 1;
+  a.exwords = reinterpret_cast<const uint32_t*>(d_arena + dlay.exwords_off);
+  a.exbits = reinterpret_cast<const uint32_t*>(d_arena + dlay.exbits_off);
+  a.exbits_mask = dlay.exbits_words * 32 - 1;
+  a.max_mp = (uint32_t)dlay.max_mountpoints;
+  a.local_node = (uint32_t)dlay.local_node;
   a.pubs = pubs; a.words = words; a.npub = npub;
   a.offsets = offs;
   a.keycache = d_keycache;
@@ -1286,7 +1290,9 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
                          uint64_t out_cap, vmqg_range* d_rng, uint64_t rng_cap, uint64_t* d_offsets,
                          hipStream_t st) {
   if (!has_device) return VMQG_E_DEVICE;
-  if (!d_arena) return VMQG_E_STATE;
+  // the tables the device holds, as their layout says (a layout larger than
+  // the arena would send every read past it)
+  if (!d_arena || d_arena_bytes < dlay.total_bytes || dlay.magic != kLayoutMagic) return VMQG_E_STATE;
   hipSetDevice(device);
   // table changes (patches, images) land before this match: the primary's on
   // the context stream, a replica's on whatever stream the caller gave

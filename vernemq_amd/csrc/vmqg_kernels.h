@@ -59,6 +59,7 @@ struct MatchArgs {
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
+constexpr uint32_t kOptRootFlags = 2u;  // a walk starts from its root's cached child flags (else probes all three)
 
 // mode 0 = COUNT, 1 = EMIT; tier 0 = fast groups, 1 = wave tier (grid a.o_waves / 4).
 // t0 / t1 (both or neither): timing events recorded by the kernel's own

@@ -327,6 +327,14 @@ __device__ __forceinline__ StepOut probe_step(const MatchArgs& a, const Group<G>
   return o;
 }
 
+// The child flags of a mountpoint's root (its own record caches them: a
+// root has no incoming edge slot); a trie-less mountpoint (R1: exact
+// subscriptions only) then walks nothing.
+__device__ __forceinline__ uint32_t root_flags(const MatchArgs& a, uint32_t mp) {
+  if (!(a.opts & kOptRootFlags)) return kHasAll;
+  return (a.nodes[mp].meta >> kRootFlagShift) & kHasAll;
+}
+
 // Exact-topic fingerprint of the publish, computed by the G lanes of a group;
 // `wild`: the publish holds a '+' / '#' word (only a wildcard topic, which
 // has no filter bit, can equal it).
@@ -453,7 +461,7 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
   Matched m{0, 0, 0, 0, 0, false, false, false, 0, 0, 0, 0};
   uint32_t nc = 0, sp = 0;
   if (mp_ok) {
-    if (g.lane == 0) s.st(0) = make_uint2(pub.mountpoint, kHasAll << 28);   // {MP, root}: probe all
+    if (g.lane == 0) s.st(0) = make_uint2(pub.mountpoint, root_flags(a, pub.mountpoint) << 28);   // {MP, root}
     sp = 1;
   }
   wave_sync();
@@ -1282,7 +1290,7 @@ struct WaveWalk {
     const uint32_t wreg = lane < L ? w[lane] : kUnknownWord;
     for (uint32_t i = lane; i < kHiWords; i += 64) W.hb[i] = 0;
     uint32_t sp = 0;
-    if (mp_ok) { if (lane == 0) stack[0] = make_uint2(pub.mountpoint, kHasAll << 28); sp = 1; }
+    if (mp_ok) { if (lane == 0) stack[0] = make_uint2(pub.mountpoint, root_flags(a, pub.mountpoint) << 28); sp = 1; }
     wave_sync();
     while (sp > 0) {
       const uint32_t k = sp < 64u ? sp : 64u;
