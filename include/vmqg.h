@@ -179,6 +179,9 @@ typedef struct vmqg_stats_s {
   uint64_t error_bits;      /* device error bits the last check collected: 2 a  */
                             /* frontier stack overflowed or none was free, 4    */
                             /* output overflow, 8 count mismatch, 16 look-back  */
+  /* ABI 6: the readers' record buffers (vmqg_records_pin)                       */
+  uint64_t reader_waits;    /* stages that waited for readers to leave a buffer */
+  uint64_t reader_wait_ns;  /*   ... and how long in all                         */
 } vmqg_stats_t;
 
 /* ---- lifecycle ------------------------------------------------------- */

@@ -2,11 +2,19 @@
  * vmqg_batch.c — see vmqg_batch.h.  Plain C99, no OTP, no HIP: only the
  * libvmqgpu C ABI.
  */
+#define _POSIX_C_SOURCE 200809L   /* clock_gettime under -std=c99 */
 #include "vmqg_batch.h"
 
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+
+static uint64_t mono_ns(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
 
 /* ------------------------------------------------------------ interner */
 struct vmqgb_interner {
@@ -627,15 +635,28 @@ void vmqgb_view_write_end(vmqgb_view* v) { pthread_mutex_unlock(&v->wr); }
  * ops are consumed either way. */
 int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
   __atomic_thread_fence(__ATOMIC_RELEASE);   /* the caller's term tables before the ids reach any result */
+  const uint64_t t0 = mono_ns();
   int rc = o->n ? vmqg_apply_stage(v->ctx, o->ops, o->n, o->words, o->nwords) : VMQG_OK;
   if (rc == VMQG_E_INVAL || rc == VMQG_E_LIMIT || rc == VMQG_E_STATE) {   /* rejected: nothing staged */
     o->n = o->nwords = 0;
     return rc;
   }
+  const uint64_t t1 = mono_ns();
   pthread_mutex_lock(&v->device);
+  const uint64_t t2 = mono_ns();
   const int rc2 = vmqg_apply_commit(v->ctx, epoch);
   pthread_mutex_unlock(&v->device);
+  const uint64_t t3 = mono_ns();
   o->n = o->nwords = 0;
+  pthread_mutex_lock(&v->q_mu);
+  v->st.applies++;
+  v->st.stage_ns += t1 - t0;
+  v->st.dev_wait_ns += t2 - t1;
+  v->st.commit_ns += t3 - t2;
+  if (t1 - t0 > v->st.stage_max_ns) v->st.stage_max_ns = t1 - t0;
+  if (t2 - t1 > v->st.dev_wait_max_ns) v->st.dev_wait_max_ns = t2 - t1;
+  if (t3 - t2 > v->st.commit_max_ns) v->st.commit_max_ns = t3 - t2;
+  pthread_mutex_unlock(&v->q_mu);
   return rc ? rc : rc2;
 }
 
@@ -657,6 +678,12 @@ void vmqgb_view_set_inflight(vmqgb_view* v, int n) {
 void vmqgb_view_get_stats(vmqgb_view* v, vmqgb_view_stats* out) {
   pthread_mutex_lock(&v->q_mu);
   *out = v->st;
+  pthread_mutex_unlock(&v->q_mu);
+}
+
+void vmqgb_view_reset_stats(vmqgb_view* v) {
+  pthread_mutex_lock(&v->q_mu);
+  memset(&v->st, 0, sizeof v->st);
   pthread_mutex_unlock(&v->q_mu);
 }
 

@@ -232,8 +232,12 @@ typedef struct vmqgb_view_stats {
   uint64_t rounds, round_publishes, round_batches, max_round_publishes;
   uint64_t expanded_batches, device_record_batches, state_retries, stale_rematches;
   uint64_t overflow_retries;
+  /* the writer's applies (vmqgb_view_apply_ops): host stage, wait for the
+   * device mutex, commit — sums and maxima, ns */
+  uint64_t applies, stage_ns, stage_max_ns, dev_wait_ns, dev_wait_max_ns, commit_ns, commit_max_ns;
 } vmqgb_view_stats;
 void vmqgb_view_get_stats(vmqgb_view* v, vmqgb_view_stats* out);
+void vmqgb_view_reset_stats(vmqgb_view* v);
 
 #ifdef __cplusplus
 }

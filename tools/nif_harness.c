@@ -276,11 +276,31 @@ static void* loader(void* p) {
 /* ----------------------------------------------------------------- run */
 static uint64_t checksum;
 
+/* the cgroup's CPU throttling (cgroup v2 cpu.stat): a quota-bound run stalls
+ * every thread for the rest of a 100 ms period */
+static void cpu_throttle(uint64_t* periods, uint64_t* usec) {
+  *periods = *usec = 0;
+  FILE* f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+  if (!f) return;
+  char k[64];
+  unsigned long long x;
+  while (fscanf(f, "%63s %llu", k, &x) == 2) {
+    if (!strcmp(k, "nr_throttled")) *periods = x;
+    if (!strcmp(k, "throttled_usec")) *usec = x;
+  }
+  fclose(f);
+}
+
 static int run(const char* section, int T, size_t B, int ranges, double secs, churn_t* cc, load_t* ld) {
   bt_t a[64];
   pthread_t th[64], cw[2];
   vmqgb_view_stats s0, s1;
+  vmqgb_view_reset_stats(view);
   vmqgb_view_get_stats(view, &s0);
+  vmqg_stats_t e0, e1;
+  vmqg_stats(ctx, &e0);
+  uint64_t thr0, thu0, thr1, thu1;
+  cpu_throttle(&thr0, &thu0);
   const double tstart = now(), t_end = tstart + secs;
   if (cc) {
     cc->t_end = t_end;
@@ -306,6 +326,8 @@ static int run(const char* section, int T, size_t B, int ranges, double secs, ch
   if (ld) { pthread_join(cw[0], NULL); if (ld->err) { fprintf(stderr, "load failed %d\n", ld->err); err = 6; } }
   const double el = now() - tstart;
   vmqgb_view_get_stats(view, &s1);
+  vmqg_stats(ctx, &e1);
+  cpu_throttle(&thr1, &thu1);
   const uint64_t rounds = s1.rounds - s0.rounds;
   printf("{\"section\": \"%s\", \"mode\": \"%s\", \"fold\": \"%s\", \"batchers\": %d, \"batch\": %zu, \"seconds\": %.2f, "
          "\"publishes\": %llu, \"entries\": %llu, \"publishes_per_s\": %.4g, \"entries_per_s\": %.4g, "
@@ -328,16 +350,25 @@ static int run(const char* section, int T, size_t B, int ranges, double secs, ch
     printf(", \"churn\": {\"delivery\": \"%s\", \"events_per_s_offered\": %.4g, \"events_applied_per_s\": %.4g, "
            "\"applies\": %llu, \"mean_events_per_apply\": %.1f, \"max_events_per_apply\": %llu, "
            "\"backlog_at_end\": %llu, \"max_backlog\": %zu, \"lag_ms\": {\"p50\": %.3f, \"p99\": %.3f, \"max\": %.3f}, "
-           "\"max_write_lock_wait_ms\": %.3f, \"mean_apply_section_ms\": %.3f}",
+           "\"max_write_lock_wait_ms\": %.3f, \"mean_apply_section_ms\": %.3f, "
+           "\"writer_ms\": {\"stage_mean\": %.3f, \"stage_max\": %.3f, \"device_wait_mean\": %.3f, "
+           "\"device_wait_max\": %.3f, \"commit_mean\": %.3f, \"commit_max\": %.3f}, "
+           "\"reader_buffer_waits\": %llu, \"reader_buffer_wait_ms\": %.3f}",
            cc->coalesce ? "coalesced" : "single", cc->produced / el, cc->applied / el, (unsigned long long)cc->applies,
            cc->applies ? (double)cc->applied / cc->applies : 0.0, (unsigned long long)cc->max_group,
            (unsigned long long)(cc->produced - cc->applied), cc->max_backlog, p50 * 1e3, p99 * 1e3, cc->lag_max * 1e3,
-           cc->wait_max * 1e3, cc->applies ? cc->apply_sum * 1e3 / cc->applies : 0.0);
+           cc->wait_max * 1e3, cc->applies ? cc->apply_sum * 1e3 / cc->applies : 0.0,
+           s1.applies ? s1.stage_ns * 1e-6 / s1.applies : 0.0, s1.stage_max_ns * 1e-6,
+           s1.applies ? s1.dev_wait_ns * 1e-6 / s1.applies : 0.0, s1.dev_wait_max_ns * 1e-6,
+           s1.applies ? s1.commit_ns * 1e-6 / s1.applies : 0.0, s1.commit_max_ns * 1e-6,
+           (unsigned long long)(e1.reader_waits - e0.reader_waits), (e1.reader_wait_ns - e0.reader_wait_ns) * 1e-6);
   }
   if (ld)
     printf(", \"load\": {\"subscriptions_added_per_s\": %.4g, \"applies\": %llu, \"max_write_lock_wait_ms\": %.3f}",
            ld->added / el, (unsigned long long)ld->applies, ld->wait_max * 1e3);
-  printf(", \"build\": \"%s\"}\n", vmqg_build_id());
+  printf(", \"rebuilds\": %llu, \"cpu_throttled\": {\"periods\": %llu, \"ms\": %.1f}, \"build\": \"%s\"}\n",
+         (unsigned long long)(e1.rebuilds - e0.rebuilds), (unsigned long long)(thr1 - thr0), (thu1 - thu0) * 1e-3,
+         vmqg_build_id());
   fflush(stdout);
   return err;
 }

@@ -81,7 +81,7 @@ class Stats(ctypes.Structure):
                  "fanout_objects", "remote_keys", "epoch", "rebuilds", "paths", "words",
                  "deferred_tier1", "deferred_tier2", "ops_applied", "apply_host_ns", "apply_upload_ns", "apply_wait_ns", "patch_bytes",
                  "image_bytes", "max_depth", "many_key", "retried", "wave_entries", "wide_entries",
-                 "dedup", "dedup_walked", "error_bits")]
+                 "dedup", "dedup_walked", "error_bits", "reader_waits", "reader_wait_ns")]
 
 
 class RConfig(ctypes.Structure):

@@ -640,6 +640,8 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->dedup = e.last_dedup;
   out->dedup_walked = e.last_dedup_walked;
   out->error_bits = e.last_err_bits;
+  out->reader_waits = e.rb_waits;
+  out->reader_wait_ns = e.rb_wait_ns;
   return VMQG_OK;
 }
 
