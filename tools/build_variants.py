@@ -40,6 +40,9 @@ VARIANTS = {
     "rt_u2": ["-DVMQR_U=2"],
     "rt_u8": ["-DVMQR_U=8"],
     "nofence": ["-DVMQG_STACK_FENCES=0"],
+    "excount0": ["-DVMQG_EX_COUNT=0"],
+    "exfrt0": ["-DVMQG_EXFILTER_RUNTIME=0"],
+    "excount0_exfrt0": ["-DVMQG_EX_COUNT=0", "-DVMQG_EXFILTER_RUNTIME=0"],
 }
 
 

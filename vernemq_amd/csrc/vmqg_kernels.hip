@@ -369,7 +369,10 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
   xst = wild ? 0u : 1u;
 #if VMQG_EXACT_FILTER
   // the filter's bit (an L2-resident word) before the table's random line
-  if (a.exfilter && !wild) {
+#ifndef VMQG_EXFILTER_RUNTIME
+#define VMQG_EXFILTER_RUNTIME 1   // A/B: 0 = the filter always on (no runtime switch)
+#endif
+  if ((!VMQG_EXFILTER_RUNTIME || a.exfilter) && !wild) {
     const uint64_t xb = exbit_of(fp, a.exbits_mask + 1);
     if (!((a.exbits[xb >> 5] >> (xb & 31)) & 1u)) return nullptr;
   }
@@ -723,8 +726,12 @@ struct CountAgg {
 
 // The exact-lookup bits of a wave's groups (find_exact's xst on each
 // group's lane 0) into the block's counters: three ballots, one LDS atomic each.
+#ifndef VMQG_EX_COUNT
+#define VMQG_EX_COUNT 1   // A/B: 0 = no exact-lookup counters (the auto filter then never switches)
+#endif
 template <int G>
 __device__ __forceinline__ void count_exact(CountAgg* agg, const Group<G>& g, bool valid, uint32_t xst) {
+  if (!VMQG_EX_COUNT) return;
   const bool l0 = valid && g.lane == 0;
   const uint32_t nt = (uint32_t)__popcll(__ballot(l0 && (xst & 1u)));
   const uint32_t np = (uint32_t)__popcll(__ballot(l0 && (xst & 3u) == 3u));
