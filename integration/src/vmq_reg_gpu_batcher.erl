@@ -31,7 +31,7 @@
 
 -record(state, {ctx,           % vmqg_nif view resource
                 batch,         % this batcher's vmqg_nif batch resource
-                mode=records,  % records | ranges (app env gpu_reg_view_output)
+                mode=ranges,   % ranges | records (app env gpu_reg_view_output)
                 pending=[],    % [{From, MP, Topic}], newest first (Topic: the word list fold/4 got)
                 npending=0}).
 

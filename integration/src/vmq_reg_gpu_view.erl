@@ -179,7 +179,10 @@ init([]) ->
     true = ets:insert(?SHADOW, [{every, application:get_env(vmq_server, gpu_reg_view_shadow, 0)},
                                 {sampled, 0}, {mismatched, 0}]),
     %% fold/4 batchers, one per scheduler (linked: they die with the view)
-    Mode = application:get_env(vmq_server, gpu_reg_view_output, records),
+    %% ranges (the default): the device returns {record off, count} per key and
+    %% the entries are built straight from the pinned record table of the
+    %% match's epoch; records: each batch gets its own copy of its records first
+    Mode = application:get_env(vmq_server, gpu_reg_view_output, ranges),
     Batchers = list_to_tuple(
                  [begin {ok, Pid} = vmq_reg_gpu_batcher:start_link(Ctx, Mode), Pid end
                   || _ <- lists:seq(1, erlang:system_info(schedulers))]),
