@@ -724,14 +724,23 @@ struct CountAgg {
   uint32_t def[kDefBuf];
 };
 
-// The exact-lookup bits of a wave's groups (find_exact's xst on each
-// group's lane 0) into the block's counters: three ballots, one LDS atomic each.
+// The exact-lookup bits of a group (find_exact's xst on its lane 0) into
+// the lane's packed counters (looked up | probed << 10 | found << 20, each
+// saturating at 1,023 publishes per lane: the auto filter wants ratios),
+// added to the block's counters once, at the end of the launch
+// (count_exact_flush).  Per-wave ballots and LDS atomics instead cost the
+// one-lane COUNT 13 us of 92 on config C (profiles/ab_r05_excount/).
 #ifndef VMQG_EX_COUNT
-#define VMQG_EX_COUNT 1   // A/B: 0 = no exact-lookup counters (the auto filter then never switches)
+#define VMQG_EX_COUNT 2   // A/B: 0 = no exact-lookup counters (the auto filter then never switches), 1 = per-wave ballots
 #endif
 template <int G>
-__device__ __forceinline__ void count_exact(CountAgg* agg, const Group<G>& g, bool valid, uint32_t xst) {
-  if (!VMQG_EX_COUNT) return;
+__device__ __forceinline__ void count_exact(CountAgg* agg, const Group<G>& g, bool valid, uint32_t xst, uint32_t& xc) {
+  if (VMQG_EX_COUNT == 2) {
+    if (valid && g.lane == 0 && (xc & 1023u) < 1023u)
+      xc += (xst & 1u) + (((xst & 3u) == 3u) ? 1024u : 0u) + (((xst & 5u) == 5u) ? (1u << 20) : 0u);
+    return;
+  }
+  if (VMQG_EX_COUNT != 1) return;
   const bool l0 = valid && g.lane == 0;
   const uint32_t nt = (uint32_t)__popcll(__ballot(l0 && (xst & 1u)));
   const uint32_t np = (uint32_t)__popcll(__ballot(l0 && (xst & 3u) == 3u));
@@ -741,6 +750,12 @@ __device__ __forceinline__ void count_exact(CountAgg* agg, const Group<G>& g, bo
     atomicAdd(&agg->expass, np);
     atomicAdd(&agg->exhit, nh);
   }
+}
+__device__ __forceinline__ void count_exact_flush(CountAgg* agg, uint32_t xc) {
+  if (VMQG_EX_COUNT != 2 || xc == 0) return;
+  atomicAdd(&agg->extry, xc & 1023u);   // LDS
+  atomicAdd(&agg->expass, (xc >> 10) & 1023u);
+  atomicAdd(&agg->exhit, xc >> 20);
 }
 
 // FEAT: batch dedupe and output groups compiled in (the COUNT variant the
@@ -1592,6 +1607,7 @@ void k_match_fast(MatchArgs a) {
     __syncthreads();
   }
   const uint32_t stride = gridDim.x * kWaves * GPW;
+  uint32_t xc = 0;   // COUNT: this lane's exact-lookup counters (count_exact)
   if constexpr (MODE == 0 && FEAT) {
     if (a.dd_claimed) {
       // batch dedupe on: only the representatives k_dd_classify listed (list
@@ -1608,7 +1624,7 @@ void k_match_fast(MatchArgs a) {
           p = R[base + g.gidx];
           c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, p, s, g, fl, agg, &xst);
         }
-        count_exact<G>(agg, g, g.gidx < n, xst);
+        count_exact<G>(agg, g, g.gidx < n, xst, xc);
         if (g.gidx < n && g.lane == 0) {
           const uint32_t ch = p / a.gpw;
           if (c) atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + ch), (unsigned long long)c);
@@ -1636,7 +1652,7 @@ void k_match_fast(MatchArgs a) {
       uint64_t c = 0;
       uint32_t fl = 0, xst = 0;
       if (g.gidx < n) c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, base + g.gidx, s, g, fl, agg, &xst);
-      count_exact<G>(agg, g, g.gidx < n, xst);
+      count_exact<G>(agg, g, g.gidx < n, xst, xc);
       // the chunk's total (publishes the wave tier takes add theirs later)
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
@@ -1658,6 +1674,7 @@ void k_match_fast(MatchArgs a) {
     wave_sync();
   }
   if (MODE == 0) {   // the block's counters and deferred publishes, one global atomic each
+    count_exact_flush(agg, xc);
     __syncthreads();
     const uint32_t nd = agg->ndef < kDefBuf ? agg->ndef : kDefBuf;
     if (threadIdx.x == 0) agg->base = nd ? atomicAdd(&a.status[kStDeferred], nd) : 0u;
