@@ -432,8 +432,9 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *                          they emit and written group by group by the EMIT tail
  *                          (default 0: it loses its A/B)
  *   "exfilter"  0 | 1 | 2  exact-topic lookups behind the 1-bit-per-slot filter:
- *                          off, on, or auto (2, the default: the device's counts
- *                          of a call of >= 4,096 lookups decide the next calls)
+ *                          off, on, or auto (2, the default: on the first call
+ *                          and every 64th, 4,096 sampled publishes' filter bits
+ *                          decide the next calls — on while fewer than half pass)
  *   "heavy_min" 0..2^30    records mode: publishes of >= that many records from
  *                          <= 2 keys are copied by the EMIT tail on the XCD their
  *                          first key hashes to (0, the default: off)

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--opt", action="append", default=[], help="name=v1,v2,...")
-    ap.add_argument("--config", default="C", choices=["C", "D", "E"])
+    ap.add_argument("--config", default="C", choices=["A", "C", "D", "E"])
     ap.add_argument("--e-scale", type=float, default=0.2)
     ap.add_argument("--d-scale", type=float, default=1.0)
     ap.add_argument("--n-dev", type=int, default=1_000_000)
@@ -33,8 +33,8 @@ def main():
     from vernemq_amd import workloads as W
     from vernemq_amd.reg_view import RegGpuView
     dev = torch.device("cuda", 0)
-    if args.config == "C":
-        w = W.config_c(n_dev=args.n_dev)
+    if args.config in ("A", "C"):
+        w = W.config_c(n_dev=args.n_dev) if args.config == "C" else W.config_a()
         v = RegGpuView(node=w.self_node, device=0, nodes=w.nodes)
         w.load_into(v)
     elif args.config == "E":
@@ -54,7 +54,7 @@ def main():
     pubs, words = w.publish_arrays(v)
     d_pubs = torch.from_numpy(pubs.view(np.uint32).reshape(-1).copy()).to(dev)
     d_words = torch.from_numpy(words.astype(np.int32)).to(dev)
-    cap = {"C": 66, "D": 520, "E": 400}[args.config] * len(pubs)
+    cap = {"A": 120, "C": 66, "D": 520, "E": 400}[args.config] * len(pubs)
     d_out = torch.empty(cap * 4, dtype=torch.int32, device=dev)
     d_offs = torch.zeros(len(pubs) + 1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream().cuda_stream

@@ -1316,6 +1316,11 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
     if (a.dd_claimed) for (int k = 10; k < 16; k++) hipEventCreate(&ev[k]);
     t_ev.push_back(ev);
   }
+  // exact-filter auto mode: the sampler on the first call and every 64th
+  if (opt_exfilter == 2 && npub >= 1024 && call_seq > ex_next) {
+    ex_next = call_seq + 63;
+    if (launch_ex_sample(a, st) != hipSuccess) return VMQG_E_DEVICE;
+  }
   // dedupe on: the claim and classify passes (timed with COUNT)
   if (a.dd_claimed && (launch_dd_claim(a, st, ev[10], ev[11]) != hipSuccess ||
                        launch_dd_classify(a, st, ev[12], ev[13]) != hipSuccess))

@@ -364,6 +364,7 @@ struct Engine {
   uint32_t opt_dd_g = 4;                                   // vmqg_set_option "dd_g": lanes per representative (1|4)
   uint32_t opt_groups = 0;                                 // vmqg_set_option "groups": 0 off (default: A/B, DESIGN), 1 on
   uint32_t opt_exfilter = 2;                               // vmqg_set_option "exfilter": 0 off, 1 on, 2 auto (default)
+  uint64_t ex_next = 0;                                    // auto: the sampler runs on calls after this one (k_ex_sample)
   uint32_t opt_heavy_min = 0;                              // vmqg_set_option "heavy_min": records mode, EMIT tail by XCD (0 off)
   // host-buffer match staging
   void* d_pubs = nullptr; uint64_t d_pubs_cap = 0;
@@ -415,6 +416,7 @@ struct Engine {
   // device status: two per-call counter sets of kStatusSet words, then the sticky error word
   static constexpr uint32_t kStatusSet = 32, kStatusBytes = 512;
   static constexpr uint32_t kStatusDdMode = 100;   // persistent word: the dedupe mode the last call chose
+                                                   // (words 104-106: k_ex_sample's counts and ticket)
   // per-launch timing: COUNT fast tier, COUNT wave tier, scan, EMIT fast tier, EMIT wave tier
   static constexpr int kTimedStages = 5, kTimedEvents = 8;   // + the dedupe claim / classify / fix-up passes (into COUNT)
   std::vector<std::array<hipEvent_t, 2 * kTimedEvents>> t_ev;

@@ -55,7 +55,7 @@ struct MatchArgs {
   uint8_t* heavybyte;                             // per publish: 1 + its first key's bucket if heavy, else 0
   uint32_t heavy_min, pad3;                       // records mode: heavy publishes have >= this many records (0 off)
   uint32_t* dd_host;                              // host-mapped words: [0] the dedupe mode, [1] the exbits-filter
-                                                  // mode for the next calls
+                                                  // mode for the next calls (k_ex_sample)
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records
@@ -78,5 +78,8 @@ hipError_t launch_dd_claim(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = n
 hipError_t launch_dd_classify(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // after COUNT: duplicates take their representative's results, or join list 0
 hipError_t launch_dd_fixup(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+// exact-filter auto mode: samples 4,096 publishes' filter bits, the last
+// block writes the next calls' filter mode to dd_host[1]
+hipError_t launch_ex_sample(const MatchArgs& a, hipStream_t st);
 
 }  // namespace vmqg

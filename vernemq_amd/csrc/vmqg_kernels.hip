@@ -139,9 +139,6 @@ enum : uint32_t { kStDeferred = 0, kStTier2 = 1, kStTicket = 2, kStWalked = 3, k
                   kStHuge = 11 /* huge publishes listed for the tail */,
                   kStGrouped = 12 /* publishes in output groups */,
                   kStReps = 13 /* dedupe on: publishes COUNT walks (list 2) */,
-                  kStExTry = 14 /* COUNT's fast pass: publishes that looked up their exact topic */,
-                  kStExPass = 15 /* ... of those, the exbits filter let probe the table */,
-                  kStExHit = 16 /* ... of those, found their topic */,
                   kStHeavy = 17 /* heavy publishes the EMIT tail copies by XCD */,
                   kStWords = 32 };
 #ifndef VMQG_WIDE_RECORDS
@@ -362,7 +359,7 @@ __device__ __forceinline__ uint64_t publish_fp(const vmqg_pub& pub, const uint32
 // turns it off while most lookups pass it and on while most miss (exmode).
 template <int G>
 __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, const uint32_t* w, uint32_t wreg,
-                                       const Group<G>& g, uint32_t& xst) {
+                                       const Group<G>& g, uint32_t& xst, bool use_filter) {
   const uint32_t L = pub.nwords;
   bool wild;
   const uint64_t fp = publish_fp<G>(pub, w, wreg, g, wild);
@@ -372,7 +369,7 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
 #ifndef VMQG_EXFILTER_RUNTIME
 #define VMQG_EXFILTER_RUNTIME 1   // A/B: 0 = the filter always on (no runtime switch)
 #endif
-  if ((!VMQG_EXFILTER_RUNTIME || a.exfilter) && !wild) {
+  if ((!VMQG_EXFILTER_RUNTIME || use_filter) && !wild) {
     const uint64_t xb = exbit_of(fp, a.exbits_mask + 1);
     if (!((a.exbits[xb >> 5] >> (xb & 31)) & 1u)) return nullptr;
   }
@@ -401,6 +398,11 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
     b = (b + 1) & a.exact_mask;
   }
   return nullptr;
+}
+template <int G>
+__device__ __forceinline__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, const uint32_t* w,
+                                                       uint32_t wreg, const Group<G>& g, uint32_t& xst) {
+  return find_exact<G>(a, pub, w, wreg, g, xst, a.exfilter != 0);
 }
 
 // ============================================================== fast tier
@@ -433,7 +435,6 @@ struct Matched {
   bool walk_ovf;                        // ... because the frontier or candidate list overflowed
   bool many;                            // more keys than the key list holds: totals only (nk, keys unset);
   uint32_t nc, ex_off, ex_cnt;          // the candidates stay in the LDS list, the exact key is {ex_off, ex_cnt}
-  uint32_t xst;                         // find_exact's lookup bits (1 looked up, 2 probed, 4 found)
 };
 
 // Records and non-empty keys of one multi-key candidate (its keylist ids ->
@@ -461,7 +462,7 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
   const bool mp_ok = pub.mountpoint < a.max_mp;   // L == 0: the root alone (trie_match/4 :361-363)
   // lane i of the group keeps word i (i < G); deeper words come from memory
   const uint32_t wreg = g.lane < L ? w[g.lane] : kUnknownWord;
-  Matched m{0, 0, 0, 0, 0, false, false, false, 0, 0, 0, 0};
+  Matched m{0, 0, 0, 0, 0, false, false, false, 0, 0, 0};
   uint32_t nc = 0, sp = 0;
   if (mp_ok) {
     if (g.lane == 0) s.st(0) = make_uint2(pub.mountpoint, root_flags(a, pub.mountpoint) << 28);   // {MP, root}
@@ -558,7 +559,8 @@ __device__ Matched walk_publish(const MatchArgs& a, const vmqg_pub& pub, const F
 
   // ---- the exact candidate {Topic, node()} and remote exact subscribers (:62, :514-520)
   if (!m.overflow && mp_ok) {
-    const ExactSlot* e = find_exact<G>(a, pub, w, wreg, g, m.xst);
+    uint32_t xst;
+    const ExactSlot* e = find_exact<G>(a, pub, w, wreg, g, xst);
     if (e) {
       const uint4 q = *reinterpret_cast<const uint4*>(&e->off);   // {off, count, rmask lo, hi}
       rmask |= ((uint64_t)q.w << 32) | q.z;
@@ -717,57 +719,22 @@ __device__ bool group_insert(const MatchArgs& a, uint64_t sig64, uint32_t p) {
 // block at the end (a full buffer falls back to the global counter).
 constexpr uint32_t kDefBuf = 509;
 struct CountAgg {
-  uint32_t many, walkovf, grouped, extry;   // per-block sums of the status counters
+  uint32_t many, walkovf, grouped, pad0;    // per-block sums of the status counters
   uint32_t ndef, base;                      // buffered deferred publishes; their list-0 base
-  uint32_t expass, exhit;                   // exact lookups: probed, found (extry: looked up)
+  uint32_t pad1, pad2;
   uint32_t heavy;                           // heavy publishes marked for the EMIT tail
   uint32_t def[kDefBuf];
 };
-
-// The exact-lookup bits of a group (find_exact's xst on its lane 0) into
-// the lane's packed counters (looked up | probed << 10 | found << 20, each
-// saturating at 1,023 publishes per lane: the auto filter wants ratios),
-// added to the block's counters once, at the end of the launch
-// (count_exact_flush).  Per-wave ballots and LDS atomics instead cost the
-// one-lane COUNT 13 us of 92 on config C (profiles/ab_r05_excount/).
-#ifndef VMQG_EX_COUNT
-#define VMQG_EX_COUNT 2   // A/B: 0 = no exact-lookup counters (the auto filter then never switches), 1 = per-wave ballots
-#endif
-template <int G>
-__device__ __forceinline__ void count_exact(CountAgg* agg, const Group<G>& g, bool valid, uint32_t xst, uint32_t& xc) {
-  if (VMQG_EX_COUNT == 2) {
-    if (valid && g.lane == 0 && (xc & 1023u) < 1023u)
-      xc += (xst & 1u) + (((xst & 3u) == 3u) ? 1024u : 0u) + (((xst & 5u) == 5u) ? (1u << 20) : 0u);
-    return;
-  }
-  if (VMQG_EX_COUNT != 1) return;
-  const bool l0 = valid && g.lane == 0;
-  const uint32_t nt = (uint32_t)__popcll(__ballot(l0 && (xst & 1u)));
-  const uint32_t np = (uint32_t)__popcll(__ballot(l0 && (xst & 3u) == 3u));
-  const uint32_t nh = (uint32_t)__popcll(__ballot(l0 && (xst & 5u) == 5u));
-  if (__lane_id() == 0 && nt) {
-    atomicAdd(&agg->extry, nt);
-    atomicAdd(&agg->expass, np);
-    atomicAdd(&agg->exhit, nh);
-  }
-}
-__device__ __forceinline__ void count_exact_flush(CountAgg* agg, uint32_t xc) {
-  if (VMQG_EX_COUNT != 2 || xc == 0) return;
-  atomicAdd(&agg->extry, xc & 1023u);   // LDS
-  atomicAdd(&agg->expass, (xc >> 10) & 1023u);
-  atomicAdd(&agg->exhit, xc >> 20);
-}
 
 // FEAT: batch dedupe and output groups compiled in (the COUNT variant the
 // host picks when either is on: their code costs the lean variant scratch
 // spills, 79 -> 90 us on config C)
 template <int G, int OUT, bool RETRY = false, uint32_t SL = kWaves * (64 / G), bool FEAT = true>
 __device__ uint32_t count_publish(const MatchArgs& a, uint32_t p, const FastScratch<G, SL>& s, const Group<G>& g,
-                                  uint32_t& fl, CountAgg* agg = nullptr, uint32_t* xst = nullptr) {
+                                  uint32_t& fl, CountAgg* agg = nullptr) {
   const vmqg_pub pub = a.pubs[p];
   const Matched m = walk_publish<G, SL>(a, pub, s, g);
   fl = 0;
-  if (xst) *xst = m.xst;
   // wide publishes — more keys than the spill slots hold — are written by a
   // whole wave in the EMIT tail launch, expanded again from their candidates
   const bool many = !m.overflow && (m.many || m.nk > VMQG_SPILL_KEYS || m.ksum >= VMQG_WIDE_RECORDS);
@@ -1607,7 +1574,6 @@ void k_match_fast(MatchArgs a) {
     __syncthreads();
   }
   const uint32_t stride = gridDim.x * kWaves * GPW;
-  uint32_t xc = 0;   // COUNT: this lane's exact-lookup counters (count_exact)
   if constexpr (MODE == 0 && FEAT) {
     if (a.dd_claimed) {
       // batch dedupe on: only the representatives k_dd_classify listed (list
@@ -1618,13 +1584,12 @@ void k_match_fast(MatchArgs a) {
       const uint32_t* R = a.deferred + 2ull * a.npub;
       for (uint32_t base = (blockIdx.x * kWaves + wv) * GPW; base < nr; base += stride) {
         const uint32_t n = nr - base < (uint32_t)GPW ? nr - base : (uint32_t)GPW;
-        uint32_t fl = 2, p = 0, xst = 0;
+        uint32_t fl = 2, p = 0;
         uint64_t c = 0;
         if (g.gidx < n) {
           p = R[base + g.gidx];
-          c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, p, s, g, fl, agg, &xst);
+          c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, p, s, g, fl, agg);
         }
-        count_exact<G>(agg, g, g.gidx < n, xst, xc);
         if (g.gidx < n && g.lane == 0) {
           const uint32_t ch = p / a.gpw;
           if (c) atomicAdd(reinterpret_cast<unsigned long long*>(a.chunk + ch), (unsigned long long)c);
@@ -1650,9 +1615,8 @@ void k_match_fast(MatchArgs a) {
     if (MODE == 0) {
       if (FEAT && a.dd_claimed) break;   // the representatives' loop above did the work
       uint64_t c = 0;
-      uint32_t fl = 0, xst = 0;
-      if (g.gidx < n) c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, base + g.gidx, s, g, fl, agg, &xst);
-      count_exact<G>(agg, g, g.gidx < n, xst, xc);
+      uint32_t fl = 0;
+      if (g.gidx < n) c = count_publish<G, OUT, false, kWaves * (64 / G), FEAT>(a, base + g.gidx, s, g, fl, agg);
       // the chunk's total (publishes the wave tier takes add theirs later)
       const uint64_t tot = __shfl(wave_incl_scan64(c), 63, 64);
       if (__lane_id() == 0) a.chunk[base / GPW] = tot;
@@ -1674,7 +1638,6 @@ void k_match_fast(MatchArgs a) {
     wave_sync();
   }
   if (MODE == 0) {   // the block's counters and deferred publishes, one global atomic each
-    count_exact_flush(agg, xc);
     __syncthreads();
     const uint32_t nd = agg->ndef < kDefBuf ? agg->ndef : kDefBuf;
     if (threadIdx.x == 0) agg->base = nd ? atomicAdd(&a.status[kStDeferred], nd) : 0u;
@@ -1682,11 +1645,6 @@ void k_match_fast(MatchArgs a) {
     if (threadIdx.x == 128 && agg->walkovf) atomicAdd(&a.status[kStWalkOvf], agg->walkovf);
     if (threadIdx.x == 192 && agg->grouped) atomicAdd(&a.status[kStGrouped], agg->grouped);
     if (threadIdx.x == 96 && agg->heavy) atomicAdd(&a.status[kStHeavy], agg->heavy);
-    if (threadIdx.x == 32 && agg->extry) {
-      atomicAdd(&a.status[kStExTry], agg->extry);
-      atomicAdd(&a.status[kStExPass], agg->expass);
-      atomicAdd(&a.status[kStExHit], agg->exhit);
-    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) a.deferred[agg->base + i] = agg->def[i];
   }
@@ -1737,16 +1695,6 @@ void k_match_wave(MatchArgs a) {
         const uint32_t mode = dups * 2u > tried ? 1u : 0u;
         *a.dd_mode = mode;
         if (a.dd_host) *a.dd_host = mode;   // host-mapped: the host reads it before its next calls
-      }
-    }
-    // the exbits filter for the next calls: off while more than 3/4 of the
-    // lookups pass it (its line is then an extra line per publish: R1), on
-    // while fewer than half find their topic (C: none has one)
-    if (gw == 0 && lane == 1 && a.dd_host) {
-      const uint32_t t = a.status[kStExTry], q = a.status[kStExPass], h = a.status[kStExHit];
-      if (t >= 4096) {
-        const uint32_t mode = a.exfilter ? (q * 4u > t * 3u ? 0u : 1u) : (h * 2u < t ? 1u : 0u);
-        a.dd_host[1] = mode + 2u;   // 2 off, 3 on (0: never decided)
       }
     }
     // COUNT's deferred publishes (list 0), sixteen per wave, then the
@@ -2002,6 +1950,57 @@ __device__ __forceinline__ bool lane_words_equal(const uint32_t* x, const uint32
     eq = ((x[k] ^ y[k]) | (x[k + 1] ^ y[k + 1]) | (x[k + 2] ^ y[k + 2]) | (x[k + 3] ^ y[k + 3])) == 0;
   for (; eq && k < n; k++) eq = x[k] == y[k];
   return eq;
+}
+
+// ------------------------------------------------ exact-filter sampling
+// The exbits filter is worth its (L2-resident) word per lookup only while
+// most exact lookups would miss the table: C's publishes never have an exact
+// topic (filter on), R1's always do (filter off: it is then one more line per
+// publish).  With option "exfilter" 2 (auto) the host launches this sampler
+// before COUNT on the first call and every 64th: 4,096 publishes spread over
+// the batch test their filter bit; the launch's last block turns the counts
+// into the mode of the next calls (host-mapped dd_host[1]: 2 off, 3 on) —
+// on while fewer than half of the lookups pass the filter.  COUNT itself
+// counts nothing: per-publish counters cost the one-lane COUNT 13-25 us of
+// 80 on config C (profiles/ab_r05_excount/).
+constexpr uint32_t kExSamples = 4096;
+__global__ __launch_bounds__(256) void k_ex_sample(MatchArgs a) {
+  __shared__ uint32_t s_t, s_q;
+  if (threadIdx.x == 0) { s_t = 0; s_q = 0; }
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool looked = false, pass = false;
+  if (i < kExSamples && a.npub) {
+    const uint32_t p = (uint32_t)((uint64_t)i * a.npub / kExSamples);
+    const vmqg_pub pub = a.pubs[p];
+    if (pub.mountpoint < a.max_mp && pub.nwords > 0) {
+      const uint32_t* w = a.words + pub.word_off;
+      bool wild;
+      const uint64_t fp = publish_fp<1>(pub, w, w[0], Group<1>(), wild);
+      if (!wild) {
+        looked = true;
+        const uint64_t xb = exbit_of(fp, a.exbits_mask + 1);
+        pass = ((a.exbits[xb >> 5] >> (xb & 31)) & 1u) != 0;
+      }
+    }
+  }
+  const uint32_t nt = (uint32_t)__popcll(__ballot(looked)), nq = (uint32_t)__popcll(__ballot(pass));
+  if (__lane_id() == 0 && nt) { atomicAdd(&s_t, nt); atomicAdd(&s_q, nq); }   // LDS
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint32_t* acc = a.dd_mode + 4;   // persistent words: looked up, passed, blocks done
+  if (s_t) { atomicAdd(&acc[0], s_t); atomicAdd(&acc[1], s_q); }
+  __threadfence();
+  if (atomicAdd(&acc[2], 1u) != gridDim.x - 1) return;
+  // the last block: every block's counts are in (each fenced before its ticket)
+  const uint32_t t = atomicExch(&acc[0], 0u), q = atomicExch(&acc[1], 0u);
+  atomicExch(&acc[2], 0u);
+  if (t >= 256 && a.dd_host) a.dd_host[1] = (q * 2u < t ? 1u : 0u) + 2u;
+}
+
+hipError_t launch_ex_sample(const MatchArgs& a, hipStream_t st) {
+  k_ex_sample<<<kExSamples / 256, 256, 0, st>>>(a);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------ dedupe claim
