@@ -412,6 +412,9 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "fast_g"    1 | 2 | 4  lanes per publish in the fast tier (default 1: one lane per
  *                          publish in COUNT, two in EMIT over the same 64-publish chunks)
  *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
+ *   "trieless"  0 | 1      tables without any wildcard / $share filter: COUNT is
+ *                          one exact-table probe per publish, four publishes per
+ *                          lane in flight (default 1; 0: the general walk)
  *   "root_flags" 0 | 1     a walk starts from its root's cached child flags, so a
  *                          mountpoint without wildcard / $share filters walks
  *                          nothing (default 1; 0: the root's three probes)

@@ -1227,3 +1227,67 @@ def test_dedupe_keeps_dollar_topics_apart(mode):
         for i in list(range(0, 4000, 7)) + list(range(3990, 4000)):
             got = sorted(H.canon(v.decode(recs[j])) for j in range(int(offs[i]), int(offs[i + 1])))
             assert got == want[order[i]], (i, topics[order[i]])
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_trieless_tables_take_the_exact_only_count(mode):
+    """Tables without any wildcard or $share filter (every subscription exact:
+    bench_single_lookups' shape, vmq_reg_trie_bench_SUITE.erl:114-150): COUNT
+    is one exact probe per publish, four per lane in flight (option
+    "trieless").  Against the oracle and byte-identical to the general walk
+    (trieless 0), with local and remote subscribers, remote nodes >= 64 (the
+    slot's high list: the wave tier takes the publish), two mountpoints, topics
+    longer than the slot's 7 inline words, publishes that hold '+' or unknown
+    words, empty lists and an unknown mountpoint; heavy routing on and off."""
+    import random
+    nodes = ["n%d@h" % i for i in range(80)]
+    prod = _driver(nodes[0], mode, nodes=nodes)
+    orc = O.TrieOracle(nodes[0])
+    r = random.Random(5)
+    vocab = [b"a", b"b", b"c", b"dev", b"x%d" % 7]
+    topics = []
+    for k in range(3000):
+        L = r.choice([1, 2, 3, 4, 8, 9])
+        topics.append(tuple([r.choice(vocab) for _ in range(L - 1)] + [b"t%d" % k]))
+    evs = []
+    for k, t in enumerate(topics):
+        mp = "" if k % 5 else "m2"
+        for j in range(r.choice([1, 1, 2, 3, 40])):
+            x = r.random()
+            node = nodes[0] if x < 0.7 else (r.choice(nodes[1:60]) if x < 0.95 else r.choice(nodes[64:]))
+            evs.append(("updated", (mp, b"c%d_%d" % (k, j)), None, [(node, True, [(t, j % 3)])]))
+    prod.apply(evs)
+    orc.apply(evs)
+    pubs = []
+    for i in range(20000):
+        x = r.random()
+        if x < 0.7:
+            k = r.randrange(len(topics))
+            pubs.append(("" if k % 5 else "m2", topics[k]))
+        elif x < 0.8:
+            pubs.append(("", tuple(r.choice(vocab) for _ in range(3))))
+        elif x < 0.85:
+            pubs.append(("", (b"a", b"+")))
+        elif x < 0.9:
+            pubs.append(("", ()))
+        elif x < 0.95:
+            pubs.append(("nomp", (b"a", b"t1")))
+        else:
+            pubs.append(("", (b"zz", b"t%d" % r.randrange(3000))))
+    want = [sorted(x) for x in orc.fold_batch([(mp, b"p", t) for mp, t in pubs])]
+    v = prod.view
+    outs = {}
+    for tl, hm in ((1, 0), (0, 0), (1, 8), (0, 8)):
+        v.set_option("trieless", tl)
+        v.set_option("heavy_min", hm)
+        arr, words = v.prepare([(mp, tuple(t)) for mp, t in pubs])
+        recs, offs = prod.match_arrays(arr, words)
+        outs[tl, hm] = (np.asarray(offs).copy(), np.asarray(recs).view(np.uint8).copy())
+        got = prod.fold_batch(pubs)
+        bad = [i for i in range(len(pubs)) if sorted(got[i]) != want[i]]
+        assert not bad, (tl, hm, len(bad), pubs[bad[0]], sorted(got[bad[0]])[:4], want[bad[0]][:4])
+    for hm in (0, 8):
+        a, b = outs[1, hm], outs[0, hm]
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), hm
+    v.set_option("trieless", 1)
+    v.set_option("heavy_min", 0)

@@ -663,6 +663,9 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   if (n == "fast_g") {
     if (value != 1 && value != 2 && value != 4) return VMQG_E_INVAL;
     e.opt_fast_g = (uint32_t)value;
+  } else if (n == "trieless") {
+    if (value < 0 || value > 1) return VMQG_E_INVAL;
+    e.opt_trieless = (uint32_t)value;
   } else if (n == "root_flags") {
     e.opt_flags = value ? (e.opt_flags | vmqg::kOptRootFlags) : (e.opt_flags & ~vmqg::kOptRootFlags);
   } else if (n == "nt_stores") {

@@ -1022,6 +1022,7 @@ int Engine::records_pin(uint64_t ep, const Record** recs, uint64_t* n, uint32_t*
 // (re-layouts are rare and the arena may be reallocated).
 int Engine::upload() {
   dlay = lay;
+  d_trieless = edge_live == 0;   // every subscription exact: COUNT is one exact probe per publish
   if (!has_device) { full_image = false; return VMQG_OK; }
   hipSetDevice(device);
   // tables must not change under a match still reading them (queued on any
@@ -1195,6 +1196,7 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.fastdone = reinterpret_cast<uint32_t*>(a.ddmask + (keycache_cap / 16 + 2));
   a.heavybyte = reinterpret_cast<uint8_t*>(a.fastdone + (keycache_cap / 32 + 2));
   a.heavy_min = opt_heavy_min;
+  a.trieless = opt_trieless && d_trieless && !replica ? 1u : 0u;
   a.dd_key = static_cast<uint64_t*>(d_dd);
   a.dd_rep = reinterpret_cast<uint32_t*>(static_cast<char*>(d_dd) + dd_slots * 8);
   a.dd_mask = dd_slots - 1;

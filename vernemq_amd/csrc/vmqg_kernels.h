@@ -53,7 +53,8 @@ struct MatchArgs {
   uint64_t* ddmask;                               // per chunk: its duplicates (COUNT -> the fix-up)
   uint32_t dd_claimed, dd_g;                      // dedupe on this call; lanes per representative in COUNT (1|2|4)
   uint8_t* heavybyte;                             // per publish: 1 + its first key's bucket if heavy, else 0
-  uint32_t heavy_min, pad3;                       // records mode: heavy publishes have >= this many records (0 off)
+  uint32_t heavy_min;                             // records mode: heavy publishes have >= this many records (0 off)
+  uint32_t trieless;                              // the device tables have no trie edge: only exact topics match
   uint32_t* dd_host;                              // host-mapped words: [0] the dedupe mode, [1] the exbits-filter
                                                   // mode for the next calls (k_ex_sample)
 };

@@ -2237,6 +2237,161 @@ hipError_t launch_scan(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEve
   return hipGetLastError();
 }
 
+// ============================================ COUNT over trie-less tables
+// When the device tables hold no trie edge (every subscription exact: the
+// reference's bench_single_lookups, R1; one hot topic, R2), a publish's
+// only candidates are its exact topic's local key and remote subscribers
+// (vmq_reg_trie.erl:62, 73-84, 514-520): COUNT is one exact-table probe.
+// The walk's machinery (LDS stacks, per-step ballots) is skipped, and each
+// lane takes K publishes of K chunks at once — their publish, word and
+// bucket loads issued together — so K random lines per lane are in flight
+// instead of one dependent chain after another (the one-lane COUNT waits
+// 83 % of its cycles on memory on R1: SQ_WAIT_ANY / SQ_WAVE_CYCLES).
+// Writes exactly what the fast COUNT writes for such a publish: offsets,
+// the key cache (<= 1 key), heavy bytes, chunk totals, chunk wide masks (0);
+// a publish with remote nodes >= 64 goes to list 0 for the wave tier, a huge
+// one to the tail's list.
+constexpr uint32_t kExK = 4;
+template <int OUT>
+__global__ __launch_bounds__(256) void k_count_exact(MatchArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x < kStWords) a.status_next[threadIdx.x] = 0;
+  const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+  const uint32_t nchunks = (a.npub + 63) / 64;
+  const uint32_t step = gridDim.x * kWaves * kExK;
+  for (uint32_t c0 = (blockIdx.x * kWaves + wv) * kExK; c0 < nchunks; c0 += step) {
+    vmqg_pub pub[kExK];
+    bool look[kExK];
+    uint64_t fp[kExK];
+#pragma unroll
+    for (uint32_t k = 0; k < kExK; k++) {
+      const uint32_t p = (c0 + k) * 64 + lane;
+      pub[k] = p < a.npub ? a.pubs[p] : vmqg_pub{0xFFFFFFFFu, 0, 0, 0};
+    }
+    // fingerprints: every publish's words in flight together
+#pragma unroll
+    for (uint32_t k = 0; k < kExK; k++) {
+      const uint32_t L = pub[k].nwords;
+      const uint32_t* w = a.words + pub[k].word_off;
+      look[k] = pub[k].mountpoint < a.max_mp && L > 0;
+      uint64_t part = 0;
+      bool wild = false;
+      for (uint32_t i = 0; look[k] && i < L; i++) {
+        const uint32_t x = w[i];
+        part += fp_word(x, i);
+        wild |= x == kPlus || x == kHash;
+      }
+      fp[k] = fp_final(part, pub[k].mountpoint, L);
+      // a '+' / '#' word equals only a wildcard topic, which has no filter bit
+      if (look[k] && !wild && a.exfilter) {
+        const uint64_t xb = exbit_of(fp[k], a.exbits_mask + 1);
+        look[k] = ((a.exbits[xb >> 5] >> (xb & 31)) & 1u) != 0;
+      }
+    }
+    // the buckets' first slots, all in flight
+    uint4 h0[kExK], h1[kExK];
+#pragma unroll
+    for (uint32_t k = 0; k < kExK; k++) {
+      if (look[k]) {
+        const ExactSlot* bk = a.exact + (fp[k] & a.exact_mask) * kExactSlotsPerBucket;
+        h0[k] = *reinterpret_cast<const uint4*>(&bk[0]);   // {fp lo, fp hi, nwords, words_off}
+        h1[k] = *reinterpret_cast<const uint4*>(&bk[1]);
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kExK; k++) {
+      const uint32_t p = (c0 + k) * 64 + lane;
+      const bool valid = p < a.npub;
+      const uint32_t L = pub[k].nwords;
+      const uint32_t* w = a.words + pub[k].word_off;
+      const ExactSlot* found = nullptr;
+      if (look[k]) {
+        uint64_t b = fp[k] & a.exact_mask;
+        uint4 s0 = h0[k], s1 = h1[k];
+        for (uint64_t iter = 0; iter <= a.exact_mask && !found; iter++) {
+          const ExactSlot* bk = a.exact + b * kExactSlotsPerBucket;
+          bool empty = false;
+#pragma unroll
+          for (uint32_t j = 0; j < kExactSlotsPerBucket; j++) {
+            const uint4 sj = j == 0 ? s0 : s1;
+            if (found || empty) continue;
+            if (sj.z == kEmpty) { empty = true; continue; }
+            const uint64_t f = ((uint64_t)sj.y << 32) | sj.x;
+            if (f != fp[k] || (sj.z & ~kExactHigh) != L || bk[j].mp != pub[k].mountpoint) continue;
+            bool diff = false;
+            const uint32_t Li = L < kExactInline ? L : kExactInline;
+            for (uint32_t i = 0; i < Li; i++) diff |= bk[j].w[i] != w[i];
+            for (uint32_t i = kExactInline; i < L; i++) diff |= a.exwords[sj.w + (i - kExactInline)] != w[i];
+            if (!diff) found = &bk[j];
+          }
+          if (found || empty) break;
+          b = (b + 1) & a.exact_mask;   // the bucket is full: the next one
+          const ExactSlot* nb = a.exact + b * kExactSlotsPerBucket;
+          s0 = *reinterpret_cast<const uint4*>(&nb[0]);
+          s1 = *reinterpret_cast<const uint4*>(&nb[1]);
+        }
+      }
+      // the fold of fold_/5 and lookup_subs/1 for the one candidate
+      uint32_t off = 0, cnt = 0;
+      uint64_t rmask = 0;
+      bool deferred = false;
+      if (found) {
+        const uint4 q = *reinterpret_cast<const uint4*>(&found->off);   // {off, count, rmask lo, hi}
+        rmask = ((uint64_t)q.w << 32) | q.z;
+        off = q.x;
+        cnt = q.y;
+        deferred = (found->nwords & kExactHigh) != 0;   // remote nodes >= 64: the wave tier
+      }
+      if (a.local_node < kLowNodes) rmask &= ~(1ull << a.local_node);
+      const uint32_t nk = cnt ? 1u : 0u;
+      const uint32_t total = OUT ? nk + (uint32_t)__popcll(rmask) : cnt + (uint32_t)__popcll(rmask);
+      uint32_t hb = 0, cnt_out = 0;
+      bool heavy = false;
+      if (valid) {
+        uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
+        if (deferred) {
+          const uint32_t idx = atomicAdd(&a.status[kStDeferred], 1u);
+          a.deferred[idx] = p;
+          a.offsets[p] = 0;
+          kc[0] = make_uint4(0, kDeferred, 0, 0);
+        } else {
+          cnt_out = total;
+          a.offsets[p] = total;
+          const bool huge = OUT == 0 && total >= kHugeRecords;
+          uint32_t hf = huge ? kHugeFlag : 0u;
+          if (huge) a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
+          else if (OUT == 0 && a.heavy_min && total >= a.heavy_min) {
+            hf = kHeavyFlag;
+            heavy = true;
+            hb = 1 + heavy_bucket(nk ? off : 0u);
+          }
+          kc[0] = make_uint4(total, nk | hf, (uint32_t)rmask, (uint32_t)(rmask >> 32));
+          kc[1] = make_uint4(nk ? off : 0u, cnt, 0u, 0u);
+        }
+        a.heavybyte[p] = (uint8_t)hb;
+      }
+      // the chunk's total and (empty) wide mask: what the fast pass stores
+      const uint64_t tot = __shfl(wave_incl_scan64(cnt_out), 63, 64);
+      const uint32_t nh = (uint32_t)__popcll(__ballot(heavy));
+      if (lane == 0 && c0 + k < nchunks) {
+        a.chunk[c0 + k] = tot;
+        a.widemask[c0 + k] = 0;
+        if (nh) atomicAdd(&a.status[kStHeavy], nh);
+      }
+    }
+  }
+}
+
+template <int OUT>
+static void launch_count_exact(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  const uint32_t nchunks = (a.npub + 63) / 64;
+  uint32_t g = div_up(nchunks, kWaves * kExK);
+  const uint32_t cap = (uint32_t)a.cus * 8u;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  if (t0) hipExtLaunchKernelGGL(k_count_exact<OUT>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+  else k_count_exact<OUT><<<g, 256, 0, st>>>(a);
+}
+
 template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
 static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   // COUNT with dedupe or output groups on: the FEAT variant
@@ -2253,6 +2408,11 @@ static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEve
 
 template <int MODE, int OUT>
 static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  // trie-less tables (every subscription exact): COUNT is one exact probe per publish
+  if (MODE == 0 && a.trieless && !a.dd_claimed && a.groups == nullptr && a.fast_g == 1 && a.gpw == 64) {
+    launch_count_exact<OUT>(a, st, t0, t1);
+    return;
+  }
   if (MODE == 0 && a.dd_claimed && a.dd_g == 4 && a.fast_g != 4) {
     // dedupe on: the representatives are few, so COUNT gives each four lanes
     // (more waves to hide each walk's dependent steps; lists 4x larger)
