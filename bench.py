@@ -692,7 +692,7 @@ def bench_other(args):
         "data": "synthetic: SURVEY.md §8(d) config %s generator" % args.config,
         "config": {"workload": "%s: %d subs, %d publishes per step%s"
                                % (args.config, n, npub, ", %d mountpoints" % len(w.mps) if len(w.mps) > 1 else ""),
-                   "fast_g": fast_g or 1},
+                   "fast_g": fast_g or "auto"},
         "pairs_per_s": em * args.steps / el, "emissions_per_step": em,
         "kernel_us": stages,
         "roofline": roof, "survey_bytes_per_publish": b_p, "oracle_sample": parity, "cpu_baseline": cpu,

@@ -409,8 +409,10 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out);
 int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
 
 /* Tuning knobs of the match kernels (no effect on results):
- *   "fast_g"    1 | 2 | 4  lanes per publish in the fast tier (default 1: one lane per
- *                          publish in COUNT, two in EMIT over the same 64-publish chunks)
+ *   "fast_g"    0 | 1 | 2 | 4  lanes per publish in the fast tier (1: one lane per
+ *                          publish in COUNT, two in EMIT over the same 64-publish
+ *                          chunks; default 0 = auto: 1 from 262,144 publishes a
+ *                          call, 2 below — a small batch needs the waves)
  *   "nt_stores" 0 | 1      non-temporal stores for emitted records (default 1)
  *   "trieless"  0 | 1      tables without any wildcard / $share filter: COUNT is
  *                          one exact-table probe per publish, four publishes per
@@ -419,7 +421,7 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *                          mountpoint without wildcard / $share filters walks
  *                          nothing (default 1; 0: the root's three probes)
  *   "count_bpc", "emit_bpc" 0..32  fast-tier grid cap, blocks per CU (0 = 8;
- *                          defaults 4 and 16)
+ *                          defaults 5 and 16)
  *   "dedupe"    0 | 1 | 2  batch-wide dedupe of repeated (MP, topic) publishes in
  *                          COUNT: off, on (a claim and a classify pass, COUNT
  *                          walks one representative per topic, a fix-up pass

@@ -661,7 +661,7 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   Engine& e = ctx->e;
   const std::string n(name);
   if (n == "fast_g") {
-    if (value != 1 && value != 2 && value != 4) return VMQG_E_INVAL;
+    if (value != 0 && value != 1 && value != 2 && value != 4) return VMQG_E_INVAL;
     e.opt_fast_g = (uint32_t)value;
   } else if (n == "trieless") {
     if (value < 0 || value > 1) return VMQG_E_INVAL;

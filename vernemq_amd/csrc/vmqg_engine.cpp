@@ -1232,12 +1232,16 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.dd_mode = d_status + kStatusDdMode;
   a.groups = opt_groups ? d_groups : nullptr;
   a.gs_mask = gs_slots - 1;
-  a.gpw = 64 / (opt_fast_g == 4 ? 4 : opt_fast_g == 1 ? 1 : 2);   // publishes per chunk
+  // lanes per publish: auto (0) gives a call of fewer than 262,144 publishes
+  // two lanes (twice the waves: a small batch fills the chip; config A 184 ->
+  // 172 us per call), a larger one one lane in COUNT (config C, A/B-tuned)
+  const uint32_t fg = opt_fast_g ? opt_fast_g : (npub >= kFastG1Min ? 1u : 2u);
+  a.gpw = 64 / (fg == 4 ? 4 : fg == 1 ? 1 : 2);   // publishes per chunk
   a.status = d_status + kStatusSet * (call_seq & 1);
   a.status_next = d_status + kStatusSet * ((call_seq + 1) & 1);
   a.err = d_status + 2 * kStatusSet;
   a.deferred = d_deferred;
-  a.fast_g = opt_fast_g; a.opts = opt_flags;
+  a.fast_g = fg; a.opts = opt_flags;
   a.count_bpc = opt_count_bpc; a.emit_bpc = opt_emit_bpc;
   a.cus = (uint32_t)cu_count;
   a.lookback = d_lookback; a.lb_tag = lb_tag;

@@ -376,8 +376,9 @@ struct Engine {
   hipEvent_t ev_match_done = nullptr;   // recorded by order_on when the stream changes
   hipStream_t ev_stream = vmqg::no_stream();      // the stream table changes / matches were last queued on
   bool timing = false;
-  uint32_t opt_fast_g = 1, opt_flags = kOptNtStores | kOptRootFlags;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
-  uint32_t opt_count_bpc = 4, opt_emit_bpc = 16;       // fast-tier grid caps, blocks per CU (A/B-tuned)
+  uint32_t opt_fast_g = 0, opt_flags = kOptNtStores | kOptRootFlags;   // vmqg_set_option (defaults: A/B-tuned on MI355X)
+  static constexpr uint32_t kFastG1Min = 262144;       // fast_g auto: one lane per publish from this many publishes
+  uint32_t opt_count_bpc = 5, opt_emit_bpc = 16;       // fast-tier grid caps, blocks per CU (A/B-tuned)
   // look-back granules (tagged per call), global stack of the tier-2 wave path
   uint64_t* d_lookback = nullptr; uint64_t lookback_cap = 0; uint32_t lb_tag = 0;
   uint2* d_ostack = nullptr; uint64_t ostack_bytes = 0;

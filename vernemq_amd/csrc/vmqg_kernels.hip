@@ -2118,7 +2118,7 @@ __global__ __launch_bounds__(256) void k_dd_fixup(MatchArgs a) {
   for (uint32_t b0 = (blockIdx.x * kWaves + wv) * 64; b0 < a.npub; b0 += stride) {
     const uint32_t p = b0 + lane;
     const bool valid = p < a.npub && ((a.ddmask[p / a.gpw] >> (p % a.gpw)) & 1);
-    bool ok = false, grouped = false, walk = false;
+    bool ok = false, grouped = false, walk = false, heavy = false;
     uint64_t add = 0;
     if (valid) {
       const uint32_t rep = a.deferred[3ull * a.npub + p];
@@ -2156,7 +2156,7 @@ __global__ __launch_bounds__(256) void k_dd_fixup(MatchArgs a) {
           a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
         } else if (h.y & kHeavyFlag) {   // the representative's bucket: the same first key
           a.heavybyte[p] = (uint8_t)(1 + heavy_bucket(k1.x));
-          atomicAdd(&a.status[kStHeavy], 1u);
+          heavy = true;   // counted per wave below (one global atomic, not one per duplicate)
         }
       } else {
         a.offsets[p] = 0;
@@ -2172,6 +2172,8 @@ __global__ __launch_bounds__(256) void k_dd_fixup(MatchArgs a) {
     }
     const uint32_t nm = (uint32_t)__popcll(__ballot(ok && !grouped && reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2].y == kMany));
     const uint32_t ng = (uint32_t)__popcll(__ballot(grouped));
+    const uint32_t nhv = (uint32_t)__popcll(__ballot(heavy));
+    if (lane == 0 && nhv) atomicAdd(&a.status[kStHeavy], nhv);
     const uint64_t wm = __ballot(walk);
     if (lane == 0) {
       if (nm) atomicAdd(&n_many, nm);
@@ -2369,14 +2371,19 @@ __global__ __launch_bounds__(256) void k_count_exact(MatchArgs a) {
         }
         a.heavybyte[p] = (uint8_t)hb;
       }
-      // the chunk's total and (empty) wide mask: what the fast pass stores
-      const uint64_t tot = __shfl(wave_incl_scan64(cnt_out), 63, 64);
+      // the totals and (empty) wide masks of the gpw-publish chunks these 64
+      // publishes make up: what the fast pass stores
+      const uint64_t incl = wave_incl_scan64(cnt_out);
+      const uint32_t gpw = a.gpw;
+      const uint32_t first = lane & ~(gpw - 1), last = first + gpw - 1;
+      const uint64_t hi = __shfl(incl, (int)last, 64);
+      const uint64_t lo = __shfl(incl, first ? (int)first - 1 : 0, 64);
       const uint32_t nh = (uint32_t)__popcll(__ballot(heavy));
-      if (lane == 0 && c0 + k < nchunks) {
-        a.chunk[c0 + k] = tot;
-        a.widemask[c0 + k] = 0;
-        if (nh) atomicAdd(&a.status[kStHeavy], nh);
+      if (lane == first && p < a.npub) {
+        a.chunk[p / gpw] = hi - (first ? lo : 0ull);
+        a.widemask[p / gpw] = 0;
       }
+      if (lane == 0 && nh) atomicAdd(&a.status[kStHeavy], nh);
     }
   }
 }
@@ -2409,7 +2416,7 @@ static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEve
 template <int MODE, int OUT>
 static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   // trie-less tables (every subscription exact): COUNT is one exact probe per publish
-  if (MODE == 0 && a.trieless && !a.dd_claimed && a.groups == nullptr && a.fast_g == 1 && a.gpw == 64) {
+  if (MODE == 0 && a.trieless && !a.dd_claimed && a.groups == nullptr) {
     launch_count_exact<OUT>(a, st, t0, t1);
     return;
   }
