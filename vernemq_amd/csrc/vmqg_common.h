@@ -35,6 +35,7 @@
 //             bit is clear skips the exact-table probe (a publish holding a
 //             '+' / '#' word always probes).
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__) || defined(__HIP__)
@@ -92,6 +93,9 @@ struct alignas(64) ExactSlot {
 };
 static_assert(sizeof(EdgeSlot) == 16 && sizeof(NodeRec) == 32 && sizeof(Record) == 16, "");
 static_assert(sizeof(ExactSlot) == 64 && sizeof(KeyDesc) == 8, "");
+// the exact-only COUNT reads a slot as four 16-B quarters
+static_assert(offsetof(ExactSlot, nwords) == 8 && offsetof(ExactSlot, off) == 16 && offsetof(ExactSlot, rmask) == 24 &&
+              offsetof(ExactSlot, mp) == 32 && offsetof(ExactSlot, w) == 36, "ExactSlot quarters");
 // exwords entries before a slot's high-node list
 VMQG_HD uint32_t exact_tail_words(uint32_t L) { return L > kExactInline ? L - kExactInline : 0u; }
 

@@ -2305,7 +2305,12 @@ __global__ __launch_bounds__(256) void k_count_exact(MatchArgs a) {
       const bool valid = p < a.npub;
       const uint32_t L = pub[k].nwords;
       const uint32_t* w = a.words + pub[k].word_off;
-      const ExactSlot* found = nullptr;
+      // the slot is read as whole 16-B quarters ({fp, nwords, words_off},
+      // {off, count, rmask}, {mp, w0..w2}, {w3..w6}): each load instruction is
+      // one L2 request per lane, so a field-by-field read costs the probe
+      // several requests to the same line
+      bool found = false, deferred = false;
+      uint4 hit{0, 0, 0, 0};
       if (look[k]) {
         uint64_t b = fp[k] & a.exact_mask;
         uint4 s0 = h0[k], s1 = h1[k];
@@ -2318,12 +2323,21 @@ __global__ __launch_bounds__(256) void k_count_exact(MatchArgs a) {
             if (found || empty) continue;
             if (sj.z == kEmpty) { empty = true; continue; }
             const uint64_t f = ((uint64_t)sj.y << 32) | sj.x;
-            if (f != fp[k] || (sj.z & ~kExactHigh) != L || bk[j].mp != pub[k].mountpoint) continue;
-            bool diff = false;
-            const uint32_t Li = L < kExactInline ? L : kExactInline;
-            for (uint32_t i = 0; i < Li; i++) diff |= bk[j].w[i] != w[i];
-            for (uint32_t i = kExactInline; i < L; i++) diff |= a.exwords[sj.w + (i - kExactInline)] != w[i];
-            if (!diff) found = &bk[j];
+            if (f != fp[k] || (sj.z & ~kExactHigh) != L) continue;
+            const uint4* q = reinterpret_cast<const uint4*>(&bk[j]);
+            const uint4 q2 = q[2];   // {mp, w0, w1, w2}
+            bool diff = q2.x != pub[k].mountpoint;
+            diff |= (L > 0 && q2.y != w[0]) || (L > 1 && q2.z != w[1]) || (L > 2 && q2.w != w[2]);
+            if (!diff && L > 3) {
+              const uint4 q3 = q[3];   // {w3, w4, w5, w6}
+              diff |= q3.x != w[3] || (L > 4 && q3.y != w[4]) || (L > 5 && q3.z != w[5]) || (L > 6 && q3.w != w[6]);
+            }
+            for (uint32_t i = kExactInline; !diff && i < L; i++) diff |= a.exwords[sj.w + (i - kExactInline)] != w[i];
+            if (!diff) {
+              found = true;
+              hit = q[1];   // {off, count, rmask lo, hi}
+              deferred = (sj.z & kExactHigh) != 0;   // remote nodes >= 64: the wave tier
+            }
           }
           if (found || empty) break;
           b = (b + 1) & a.exact_mask;   // the bucket is full: the next one
@@ -2333,16 +2347,8 @@ __global__ __launch_bounds__(256) void k_count_exact(MatchArgs a) {
         }
       }
       // the fold of fold_/5 and lookup_subs/1 for the one candidate
-      uint32_t off = 0, cnt = 0;
-      uint64_t rmask = 0;
-      bool deferred = false;
-      if (found) {
-        const uint4 q = *reinterpret_cast<const uint4*>(&found->off);   // {off, count, rmask lo, hi}
-        rmask = ((uint64_t)q.w << 32) | q.z;
-        off = q.x;
-        cnt = q.y;
-        deferred = (found->nwords & kExactHigh) != 0;   // remote nodes >= 64: the wave tier
-      }
+      const uint32_t off = hit.x, cnt = hit.y;
+      uint64_t rmask = ((uint64_t)hit.w << 32) | hit.z;
       if (a.local_node < kLowNodes) rmask &= ~(1ull << a.local_node);
       const uint32_t nk = cnt ? 1u : 0u;
       const uint32_t total = OUT ? nk + (uint32_t)__popcll(rmask) : cnt + (uint32_t)__popcll(rmask);
