@@ -40,10 +40,7 @@ VARIANTS = {
     "rt_u2": ["-DVMQR_U=2"],
     "rt_u8": ["-DVMQR_U=8"],
     "nofence": ["-DVMQG_STACK_FENCES=0"],
-    "excount0": ["-DVMQG_EX_COUNT=0"],
-    "excount1": ["-DVMQG_EX_COUNT=1"],
-    "exfrt0": ["-DVMQG_EXFILTER_RUNTIME=0"],
-    "excount0_exfrt0": ["-DVMQG_EX_COUNT=0", "-DVMQG_EXFILTER_RUNTIME=0"],
+    "emitk4_0": ["-DVMQG_EMIT_K4=0"],
 }
 
 

@@ -839,9 +839,13 @@ __device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g,
 struct GroupMeta {
   uint32_t rel, span, nk, ksum;      // output start relative to the wave's first publish, length
   uint32_t rm_lo, rm_hi, crel, c0;   // crel: start among the wave's copied records
-  uint32_t off0, off1, pad0, pad1;   // nk <= 2 (key cache): key 0 = [off0, +c0), key 1 = [off1, +ksum-c0)
-  uint4 pre0, pre1;                  // a one-record key's record, loaded during the resolve
+  uint32_t off0, off1, off2, off3;   // nk <= 4: key i's records start at off_i (key 0 = [off0, +c0),
+  uint32_t c1, c2, pad0, pad1;       // key 1 = [off1, +(c1 or ksum) - c0), key 2 from c1, key 3 from c2)
+  uint4 pre0, pre1;                  // nk <= 2: a one-record key's record, loaded during the resolve
 };
+#ifndef VMQG_EMIT_K4
+#define VMQG_EMIT_K4 1   // A/B: 0 = publishes of 3..4 keys find each record's key by binary search
+#endif
 
 // Resolve publish first + gidx of a wave from the key cache (<= 2 keys) or
 // the spill slots (3..8 keys).  Leaves the keys {off, cum start} in the
@@ -1055,7 +1059,7 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
   // the middle of the copy (key 0's by lane 0, key 1's by lane 1, or by
   // lane 0 too when a group is one lane)
   constexpr uint32_t kPre1Lane = G > 1 ? 1u : 0u;
-  uint32_t off0 = 0, off1 = 0, c0 = 0;
+  uint32_t off0 = 0, off1 = 0, off2 = 0, off3 = 0, c0 = 0, c1 = 0, c2 = 0;
   uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = make_uint4(0, 0, 0, 0);
   if (ok && nk <= 2) {
     const uint2 k0 = s.ky(0), k1 = s.ky(1);
@@ -1064,11 +1068,18 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
     c0 = nk >= 2 ? k1.y : ksum;
     if (g.lane == 0 && nk >= 1 && c0 == 1) pre0 = *reinterpret_cast<const uint4*>(a.records + off0);
     if (g.lane == kPre1Lane && nk == 2 && ksum - c0 == 1) pre1 = *reinterpret_cast<const uint4*>(a.records + off1);
+  } else if (VMQG_EMIT_K4 && ok && nk <= 4 && g.lane == 0) {
+    // 3..4 spilled keys {off, cum start}: the copy picks each record's key by
+    // three compares instead of a binary search over the LDS key list
+    const uint2 k0 = s.ky(0), k1 = s.ky(1), k2 = s.ky(2);
+    const uint2 k3 = nk > 3 ? s.ky(3) : make_uint2(0u, ksum);
+    off0 = k0.x; off1 = k1.x; off2 = k2.x; off3 = k3.x;
+    c0 = k1.y; c1 = k2.y; c2 = k3.y;
   }
   if (g.lane == 0)
     gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : 0u, ok ? (uint32_t)(oend - obase) : 0u,
                            nk == 0 ? 1 : nk, ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), 0u, c0,
-                           off0, off1, 0u, 0u, pre0, make_uint4(0, 0, 0, 0)};
+                           off0, off1, off2, off3, c1, c2, 0u, 0u, pre0, make_uint4(0, 0, 0, 0)};
   wave_sync();
   if (g.lane == kPre1Lane) gm[g.gidx].pre1 = pre1;
   // compact the copied ranges: crel = exclusive scan of the ok spans
@@ -1098,6 +1109,15 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
           if (q < mc0) v[u] = mc0 == 1 ? m.pre0 : *reinterpret_cast<const uint4*>(a.records + m.off0 + q);
           else if (q < ks) v[u] = ks - mc0 == 1 ? m.pre1 : *reinterpret_cast<const uint4*>(a.records + m.off1 + (q - mc0));
           else v[u] = make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rm, q - ks), kNone, kNone, kNone);
+        } else if (VMQG_EMIT_K4 && mk <= 4) {   // 3..4 keys: starts c0 < c1 < c2 (<= ksum)
+          const uint32_t mc1 = m.c1, mc2 = m.c2;
+          if (q < ks) {
+            const uint32_t src = q < mc0 ? m.off0 + q : q < mc1 ? m.off1 + (q - mc0)
+                               : q < mc2 ? m.off2 + (q - mc1) : m.off3 + (q - mc2);
+            v[u] = *reinterpret_cast<const uint4*>(a.records + src);
+          } else {
+            v[u] = make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rm, q - ks), kNone, kNone, kNone);
+          }
         } else {   // re-walked: keys {off, cum start} in the group's LDS list
           FastScratch<G> sj = s;
           sj.slot = slot0 + j;
