@@ -1804,18 +1804,65 @@ void k_match_wave(MatchArgs a) {
     bool heavy_on = OUT == 0 && uni(a.status[kStHeavy]) != 0;
     bool wide_on = uni(a.status[kStMany]) != 0;
     uint64_t written = 0;
-    if (groups_on || heavy_on || wide_on) {
-      const GroupSlot* gs = reinterpret_cast<const GroupSlot*>(a.groups);
-      const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
-      uint64_t si = gw, cur = 0, m = 0;
-      uint32_t j = 0, gn = 0, c = (uint32_t)gw, cc = 0;
+    if (OUT == 0 && heavy_on) {
       // heavy publishes: the blocks b = x (mod kXcds) — on XCD x — take the
-      // bucket-x publishes, their waves striding over 64-publish blocks
+      // bucket-x publishes, their waves striding over 64-publish blocks; one
+      // publish ahead: the next one's offsets and key cache load while this
+      // one copies (a heavy list copies in about the time those two dependent
+      // loads take)
       const uint32_t nblk = (a.npub + 63) / 64;
       const uint32_t hx = blockIdx.x & (kXcds - 1);
       const uint32_t hstride = (gridDim.x - hx + kXcds - 1) / kXcds * kWaves;
       uint32_t hc = (blockIdx.x / kXcds) * kWaves + wv, hcc = 0;
       uint64_t hm = 0;
+      auto next_heavy = [&](uint32_t& q) -> bool {
+        while (hm == 0 && hc < nblk) {   // 64 publishes' bucket bytes per step, one per lane
+          const uint32_t x = hc * 64 + lane;
+          hm = __ballot(x < a.npub && a.heavybyte[x] == 1 + hx);
+          hcc = hc;
+          hc += hstride;
+        }
+        if (!hm) return false;
+        q = hcc * 64 + (uint32_t)__builtin_ctzll(hm);
+        hm &= hm - 1;
+        return true;
+      };
+      uint32_t p = 0;
+      bool have = next_heavy(p);
+      uint64_t ob_n = 0, oe_n = 0;   // loaded per lane (uniform values): made scalar only when used
+      uint4 h_n{0, 0, 0, 0}, k_n{0, 0, 0, 0};
+      if (have && p < a.npub) {
+        ob_n = a.offsets[p]; oe_n = a.offsets[p + 1];
+        h_n = reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2];
+        k_n = reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2 + 1];
+      }
+      while (have) {
+        const uint32_t pc = p;
+        const uint64_t obv = ob_n, oev = oe_n;
+        const uint4 hv = h_n, kv = k_n;
+        have = next_heavy(p);
+        if (have && p < a.npub) {
+          ob_n = a.offsets[p]; oe_n = a.offsets[p + 1];
+          h_n = reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2];
+          k_n = reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2 + 1];
+        }
+        if (pc >= a.npub) { if (lane == 0) atomicOr(a.err, kErrMismatch); continue; }
+        const uint64_t ob = uni64(obv), oe = uni64(oev);
+        if (oe > cap || ob > oe) {
+          if (lane == 0) atomicOr(a.err, kErrOverflow);
+          continue;
+        }
+        emit_keys2<NT>(a, hv, kv, ob, oe);
+        written += oe - ob;
+        wave_sync();
+      }
+      heavy_on = false;
+    }
+    if (groups_on || wide_on) {
+      const GroupSlot* gs = reinterpret_cast<const GroupSlot*>(a.groups);
+      const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
+      uint64_t si = gw, cur = 0, m = 0;
+      uint32_t j = 0, gn = 0, c = (uint32_t)gw, cc = 0;
       for (;;) {
         uint32_t p = 0;
         bool have = false;
@@ -1829,22 +1876,6 @@ void k_match_wave(MatchArgs a) {
           }
           if (j < gn) { p = uni(gs[cur].m[j]); j++; have = true; }
           else groups_on = false;
-        }
-        if (!have && heavy_on) {
-          // 64 publishes' bucket bytes per step, one per lane
-          while (hm == 0 && hc < nblk) {
-            const uint32_t q = hc * 64 + lane;
-            hm = __ballot(q < a.npub && a.heavybyte[q] == 1 + hx);
-            hcc = hc;
-            hc += hstride;
-          }
-          if (hm) {
-            p = hcc * 64 + (uint32_t)__builtin_ctzll(hm);
-            hm &= hm - 1;
-            have = true;
-          } else {
-            heavy_on = false;
-          }
         }
         if (!have && wide_on) {
           while (m == 0 && c < nchunks) { m = uni64(a.widemask[c]); cc = c; c += nwaves; }
