@@ -379,11 +379,15 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
   for (uint64_t iter = 0; iter <= a.exact_mask; iter++) {
     const ExactSlot* bk = a.exact + b * kExactSlotsPerBucket;
     bool seen_empty = false;
+    // one slot at a time: each 64-B slot is a memory request of its own, so
+    // the second is read only when the first is not the topic
+#pragma unroll 1
     for (uint32_t j = 0; j < kExactSlotsPerBucket; j++) {
       const ExactSlot& e = bk[j];
-      const uint32_t nw = e.nwords;
+      const uint4 h = *reinterpret_cast<const uint4*>(&e);   // {fp lo, fp hi, nwords, words_off}
+      const uint32_t nw = h.z;
       if (nw == kEmpty) { seen_empty = true; break; }
-      if (e.fp != fp || (nw & ~kExactHigh) != L || e.mp != pub.mountpoint) continue;
+      if ((((uint64_t)h.y << 32) | h.x) != fp || (nw & ~kExactHigh) != L || e.mp != pub.mountpoint) continue;
       // inline words, then the rest (two loops: one loop selecting between
       // the two loads costs the one-lane COUNT 16 B of scratch spills)
       bool diff = false;
@@ -839,13 +843,9 @@ __device__ __forceinline__ void mark_wide(const MatchArgs& a, const Group<G>& g,
 struct GroupMeta {
   uint32_t rel, span, nk, ksum;      // output start relative to the wave's first publish, length
   uint32_t rm_lo, rm_hi, crel, c0;   // crel: start among the wave's copied records
-  uint32_t off0, off1, off2, off3;   // nk <= 4: key i's records start at off_i (key 0 = [off0, +c0),
-  uint32_t c1, c2, pad0, pad1;       // key 1 = [off1, +(c1 or ksum) - c0), key 2 from c1, key 3 from c2)
-  uint4 pre0, pre1;                  // nk <= 2: a one-record key's record, loaded during the resolve
+  uint32_t off0, off1, pad0, pad1;   // nk <= 2 (key cache): key 0 = [off0, +c0), key 1 = [off1, +ksum-c0)
+  uint4 pre0, pre1;                  // a one-record key's record, loaded during the resolve
 };
-#ifndef VMQG_EMIT_K4
-#define VMQG_EMIT_K4 1   // A/B: 0 = publishes of 3..4 keys find each record's key by binary search
-#endif
 
 // Resolve publish first + gidx of a wave from the key cache (<= 2 keys) or
 // the spill slots (3..8 keys).  Leaves the keys {off, cum start} in the
@@ -1059,7 +1059,7 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
   // the middle of the copy (key 0's by lane 0, key 1's by lane 1, or by
   // lane 0 too when a group is one lane)
   constexpr uint32_t kPre1Lane = G > 1 ? 1u : 0u;
-  uint32_t off0 = 0, off1 = 0, off2 = 0, off3 = 0, c0 = 0, c1 = 0, c2 = 0;
+  uint32_t off0 = 0, off1 = 0, c0 = 0;
   uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = make_uint4(0, 0, 0, 0);
   if (ok && nk <= 2) {
     const uint2 k0 = s.ky(0), k1 = s.ky(1);
@@ -1068,18 +1068,11 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
     c0 = nk >= 2 ? k1.y : ksum;
     if (g.lane == 0 && nk >= 1 && c0 == 1) pre0 = *reinterpret_cast<const uint4*>(a.records + off0);
     if (g.lane == kPre1Lane && nk == 2 && ksum - c0 == 1) pre1 = *reinterpret_cast<const uint4*>(a.records + off1);
-  } else if (VMQG_EMIT_K4 && ok && nk <= 4 && g.lane == 0) {
-    // 3..4 spilled keys {off, cum start}: the copy picks each record's key by
-    // three compares instead of a binary search over the LDS key list
-    const uint2 k0 = s.ky(0), k1 = s.ky(1), k2 = s.ky(2);
-    const uint2 k3 = nk > 3 ? s.ky(3) : make_uint2(0u, ksum);
-    off0 = k0.x; off1 = k1.x; off2 = k2.x; off3 = k3.x;
-    c0 = k1.y; c1 = k2.y; c2 = k3.y;
   }
   if (g.lane == 0)
     gm[g.gidx] = GroupMeta{valid ? (uint32_t)(obase - wbase) : 0u, ok ? (uint32_t)(oend - obase) : 0u,
                            nk == 0 ? 1 : nk, ksum, (uint32_t)rmask, (uint32_t)(rmask >> 32), 0u, c0,
-                           off0, off1, off2, off3, c1, c2, 0u, 0u, pre0, make_uint4(0, 0, 0, 0)};
+                           off0, off1, 0u, 0u, pre0, make_uint4(0, 0, 0, 0)};
   wave_sync();
   if (g.lane == kPre1Lane) gm[g.gidx].pre1 = pre1;
   // compact the copied ranges: crel = exclusive scan of the ok spans
@@ -1109,15 +1102,6 @@ __device__ void emit_wave(const MatchArgs& a, uint32_t first, uint32_t n, const 
           if (q < mc0) v[u] = mc0 == 1 ? m.pre0 : *reinterpret_cast<const uint4*>(a.records + m.off0 + q);
           else if (q < ks) v[u] = ks - mc0 == 1 ? m.pre1 : *reinterpret_cast<const uint4*>(a.records + m.off1 + (q - mc0));
           else v[u] = make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rm, q - ks), kNone, kNone, kNone);
-        } else if (VMQG_EMIT_K4 && mk <= 4) {   // 3..4 keys: starts c0 < c1 < c2 (<= ksum)
-          const uint32_t mc1 = m.c1, mc2 = m.c2;
-          if (q < ks) {
-            const uint32_t src = q < mc0 ? m.off0 + q : q < mc1 ? m.off1 + (q - mc0)
-                               : q < mc2 ? m.off2 + (q - mc1) : m.off3 + (q - mc2);
-            v[u] = *reinterpret_cast<const uint4*>(a.records + src);
-          } else {
-            v[u] = make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rm, q - ks), kNone, kNone, kNone);
-          }
         } else {   // re-walked: keys {off, cum start} in the group's LDS list
           FastScratch<G> sj = s;
           sj.slot = slot0 + j;
@@ -2340,14 +2324,14 @@ __global__ __launch_bounds__(256) void k_count_exact(MatchArgs a) {
         look[k] = ((a.exbits[xb >> 5] >> (xb & 31)) & 1u) != 0;
       }
     }
-    // the buckets' first slots, all in flight
-    uint4 h0[kExK], h1[kExK];
+    // the buckets' first slots, all in flight (the second slot is a 64-B
+    // memory request of its own: read only when the first does not match)
+    uint4 h0[kExK];
 #pragma unroll
     for (uint32_t k = 0; k < kExK; k++) {
       if (look[k]) {
         const ExactSlot* bk = a.exact + (fp[k] & a.exact_mask) * kExactSlotsPerBucket;
         h0[k] = *reinterpret_cast<const uint4*>(&bk[0]);   // {fp lo, fp hi, nwords, words_off}
-        h1[k] = *reinterpret_cast<const uint4*>(&bk[1]);
       }
     }
 #pragma unroll
@@ -2364,14 +2348,14 @@ __global__ __launch_bounds__(256) void k_count_exact(MatchArgs a) {
       uint4 hit{0, 0, 0, 0};
       if (look[k]) {
         uint64_t b = fp[k] & a.exact_mask;
-        uint4 s0 = h0[k], s1 = h1[k];
+        uint4 s0 = h0[k];
         for (uint64_t iter = 0; iter <= a.exact_mask && !found; iter++) {
           const ExactSlot* bk = a.exact + b * kExactSlotsPerBucket;
           bool empty = false;
 #pragma unroll
           for (uint32_t j = 0; j < kExactSlotsPerBucket; j++) {
-            const uint4 sj = j == 0 ? s0 : s1;
             if (found || empty) continue;
+            const uint4 sj = j == 0 ? s0 : *reinterpret_cast<const uint4*>(&bk[j]);
             if (sj.z == kEmpty) { empty = true; continue; }
             const uint64_t f = ((uint64_t)sj.y << 32) | sj.x;
             if (f != fp[k] || (sj.z & ~kExactHigh) != L) continue;
@@ -2392,9 +2376,7 @@ __global__ __launch_bounds__(256) void k_count_exact(MatchArgs a) {
           }
           if (found || empty) break;
           b = (b + 1) & a.exact_mask;   // the bucket is full: the next one
-          const ExactSlot* nb = a.exact + b * kExactSlotsPerBucket;
-          s0 = *reinterpret_cast<const uint4*>(&nb[0]);
-          s1 = *reinterpret_cast<const uint4*>(&nb[1]);
+          s0 = *reinterpret_cast<const uint4*>(&a.exact[b * kExactSlotsPerBucket]);
         }
       }
       // the fold of fold_/5 and lookup_subs/1 for the one candidate
