@@ -1277,17 +1277,22 @@ def test_trieless_tables_take_the_exact_only_count(mode):
     want = [sorted(x) for x in orc.fold_batch([(mp, b"p", t) for mp, t in pubs])]
     v = prod.view
     outs = {}
-    for tl, hm in ((1, 0), (0, 0), (1, 8), (0, 8)):
-        v.set_option("trieless", tl)
-        v.set_option("heavy_min", hm)
-        arr, words = v.prepare([(mp, tuple(t)) for mp, t in pubs])
-        recs, offs = prod.match_arrays(arr, words)
-        outs[tl, hm] = (np.asarray(offs).copy(), np.asarray(recs).view(np.uint8).copy())
-        got = prod.fold_batch(pubs)
-        bad = [i for i in range(len(pubs)) if sorted(got[i]) != want[i]]
-        assert not bad, (tl, hm, len(bad), pubs[bad[0]], sorted(got[bad[0]])[:4], want[bad[0]][:4])
-    for hm in (0, 8):
-        a, b = outs[1, hm], outs[0, hm]
-        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), hm
+    # fast_g 1 / 2 / 4: chunks of 64 / 32 / 16 publishes, which the trie-less
+    # EMIT (k_emit_exact, 64-publish blocks) must position alike
+    for fg in (1, 2, 4):
+        v.set_option("fast_g", fg)
+        for tl, hm in ((1, 0), (0, 0), (1, 8), (0, 8)):
+            v.set_option("trieless", tl)
+            v.set_option("heavy_min", hm)
+            arr, words = v.prepare([(mp, tuple(t)) for mp, t in pubs])
+            recs, offs = prod.match_arrays(arr, words)
+            outs[tl, hm, fg] = (np.asarray(offs).copy(), np.asarray(recs).view(np.uint8).copy())
+            got = prod.fold_batch(pubs)
+            bad = [i for i in range(len(pubs)) if sorted(got[i]) != want[i]]
+            assert not bad, (fg, tl, hm, len(bad), pubs[bad[0]], sorted(got[bad[0]])[:4], want[bad[0]][:4])
+        for hm in (0, 8):
+            a, b = outs[1, hm, fg], outs[0, hm, fg]
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), (fg, hm)
+    v.set_option("fast_g", 0)
     v.set_option("trieless", 1)
     v.set_option("heavy_min", 0)

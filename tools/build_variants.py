@@ -41,6 +41,10 @@ VARIANTS = {
     "rt_u8": ["-DVMQR_U=8"],
     "nofence": ["-DVMQG_STACK_FENCES=0"],
     "emitk4_0": ["-DVMQG_EMIT_K4=0"],
+    "nosplit": ["-DVMQG_TAIL_SPLIT=0"],
+    "noemitex": ["-DVMQG_EMIT_EXACT=0"],
+    "emitexk2": ["-DVMQG_EMIT_EXK=2"],
+    "emitexk8": ["-DVMQG_EMIT_EXK=8"],
 }
 
 

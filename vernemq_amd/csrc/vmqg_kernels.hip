@@ -1723,6 +1723,9 @@ void k_match_wave(MatchArgs a) {
     // the whole-wave walks (list 1); a walk that outgrows its LDS stack
     // borrows a global one (this grid has more waves than there are stacks)
     const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
+#ifndef VMQG_TAIL_SPLIT
+#define VMQG_TAIL_SPLIT 1   // A/B: 0 = one wave per chunk's wide publishes whatever the batch size
+#endif
 #ifndef VMQG_TAIL_NOWALK
 #define VMQG_TAIL_NOWALK 0   // A/B only (wrong with walked publishes): the tail without its walker
 #endif
@@ -1845,8 +1848,15 @@ void k_match_wave(MatchArgs a) {
     if (groups_on || wide_on) {
       const GroupSlot* gs = reinterpret_cast<const GroupSlot*>(a.groups);
       const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
+      // fewer chunks than waves (a small batch, config A): `rep` waves share
+      // each chunk, wave `sub` of them taking the chunk's wide publishes of
+      // rank sub, sub + rep, ... — a chunk with several wide publishes is not
+      // copied one after another by one wave while other waves have none
+      const uint32_t rep = VMQG_TAIL_SPLIT && nchunks && nchunks * 2 <= nwaves
+                               ? (nwaves / nchunks < 64 ? nwaves / nchunks : 64u) : 1u;
+      const uint32_t sub = rep > 1 ? (uint32_t)gw / nchunks : 0u;
       uint64_t si = gw, cur = 0, m = 0;
-      uint32_t j = 0, gn = 0, c = (uint32_t)gw, cc = 0;
+      uint32_t j = 0, gn = 0, c = rep > 1 ? (sub < rep ? (uint32_t)gw % nchunks : nchunks) : (uint32_t)gw, cc = 0;
       for (;;) {
         uint32_t p = 0;
         bool have = false;
@@ -1862,7 +1872,20 @@ void k_match_wave(MatchArgs a) {
           else groups_on = false;
         }
         if (!have && wide_on) {
-          while (m == 0 && c < nchunks) { m = uni64(a.widemask[c]); cc = c; c += nwaves; }
+          while (m == 0 && c < nchunks) {
+            m = uni64(a.widemask[c]);
+            cc = c;
+            c = rep > 1 ? nchunks : c + nwaves;
+            if (rep > 1) {   // this wave's ranks of the chunk's wide publishes
+              uint64_t keep = 0;
+              uint32_t r = 0;
+              for (uint64_t mm = m; mm; mm &= mm - 1) {
+                if (r == sub) keep |= mm & (~mm + 1);
+                r = r + 1 == rep ? 0u : r + 1;
+              }
+              m = keep;
+            }
+          }
           if (m) {
             p = cc * a.gpw + (uint32_t)__builtin_ctzll(m);
             m &= m - 1;
@@ -2438,6 +2461,191 @@ static void launch_count_exact(const MatchArgs& a, hipStream_t st, hipEvent_t t0
   else k_count_exact<OUT><<<g, 256, 0, st>>>(a);
 }
 
+#ifndef VMQG_EMIT_EXACT
+#define VMQG_EMIT_EXACT 1   // A/B: 0 = trie-less batches take the general EMIT
+#endif
+#ifndef VMQG_EMIT_EXK
+#define VMQG_EMIT_EXK 4   // 64-publish blocks per wave in flight in k_emit_exact
+#endif
+constexpr uint32_t kExE = VMQG_EMIT_EXK;
+#ifndef VMQG_EMIT_EXACT_WPE
+#define VMQG_EMIT_EXACT_WPE 1   // waves per SIMD the register budget must allow (1: no bound)
+#endif
+// ============================================= EMIT over trie-less tables
+// The EMIT of a k_count_exact COUNT: a publish has at most its exact
+// topic's key (its records) and remote nodes, so nothing needs resolving —
+// one lane per publish, kExK 64-publish blocks per wave with their offset,
+// key-cache and chunk-base loads in flight together (the general EMIT takes
+// a 64-publish chunk at a time, two lanes per publish, through the key-cache
+// resolve and LDS GroupMeta: R1 spends 190 us there for one record a
+// publish).  Writes what the general EMIT writes: every publish's final
+// offset, and the records (or ranges) of the publishes it serves; deferred
+// (kDeferred), wide (kMany), huge and heavy publishes are left to the wave
+// tier / EMIT tail as there.  Records mode: a block whose publishes emit at
+// most one record each is written lane by lane (consecutive positions: the
+// stores coalesce); any other block is copied by the whole wave over the
+// concatenated record spans, U records per lane in flight.
+struct ExEmitLds {
+  uint4 h[64], k[64];   // key-cache words of the block's publishes
+  uint64_t ob[64];      // their output positions
+  uint32_t crel[65];    // exclusive scan of the served spans
+};
+
+__device__ __forceinline__ uint4 exact_emission(const MatchArgs& a, uint32_t p, uint4 h, uint4 k, uint32_t r) {
+  const uint32_t nk = h.y, c0 = k.y, ks = k.y + k.w;
+  const uint64_t rm = ((uint64_t)h.w << 32) | h.z;
+  if (nk > 2) {   // spilled keys (not produced by a trie-less COUNT; kept general)
+    const uint2* sp = a.keyspill + (uint64_t)p * kSpillKeys;
+    return emission(a, [&](uint32_t i) -> uint2 { return sp[i]; }, nk, ks, rm, r);
+  }
+  if (r < c0) return *reinterpret_cast<const uint4*>(a.records + k.x + r);
+  if (r < ks) return *reinterpret_cast<const uint4*>(a.records + k.z + (r - c0));
+  return make_uint4((VMQG_EMIT_REMOTE << 24) | select_bit(rm, r - ks), kNone, kNone, kNone);
+}
+
+template <int OUT, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VMQG_EMIT_EXACT_WPE)))
+void k_emit_exact(MatchArgs a) {
+  __shared__ ExEmitLds lds[kWaves];
+  const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+  ExEmitLds& L = lds[wv];
+  const uint32_t nblk = (a.npub + 63) / 64;
+  const uint32_t step = gridDim.x * kWaves * kExE;
+  const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
+  const uint32_t gpw = a.gpw;
+  const uint32_t seg = lane & ~(gpw - 1);   // first lane of this lane's gpw-publish chunk
+  for (uint32_t b0 = (blockIdx.x * kWaves + wv) * kExE; b0 < nblk; b0 += step) {
+    uint64_t cnt[kExE], cb[kExE];
+    uint4 h[kExE], k[kExE];
+#pragma unroll
+    for (uint32_t j = 0; j < kExE; j++) {
+      const uint32_t p = (b0 + j) * 64 + lane;
+      const bool valid = p < a.npub;
+      cnt[j] = valid ? a.offsets[p] : 0ull;
+      cb[j] = valid ? a.chunk[p / gpw] : 0ull;
+      const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+      h[j] = valid ? kc[0] : make_uint4(0, kDeferred, 0, 0);
+      k[j] = valid ? kc[1] : make_uint4(0, 0, 0, 0);
+    }
+    // positions: the chunk's base plus the exclusive prefix within the chunk
+    uint64_t ob[kExE];
+    bool ok[kExE];
+    uint32_t single = 0;   // bit j: block j's served publishes emit <= 1 entry each
+#pragma unroll
+    for (uint32_t j = 0; j < kExE; j++) {
+      const uint32_t p = (b0 + j) * 64 + lane;
+      const bool valid = p < a.npub;
+      const uint64_t incl = wave_incl_scan64(cnt[j]);
+      const uint64_t lo = __shfl(incl, seg ? (int)seg - 1 : 0, 64);
+      ob[j] = cb[j] + incl - cnt[j] - (seg ? lo : 0ull);
+      if (valid) a.offsets[p] = ob[j];
+      const uint32_t hy = h[j].y;
+      ok[j] = valid && hy != kDeferred && hy != kMany && !(hy & (kHugeFlag | kGroupFlag | kHeavyFlag));
+      if (ok[j] && ob[j] + cnt[j] > cap) { atomicOr(a.err, kErrOverflow); ok[j] = false; }
+      if (ok[j] && cnt[j] != h[j].x) { atomicOr(a.err, kErrMismatch); ok[j] = false; }
+      if (__ballot(ok[j] && (cnt[j] > 1 || hy > 2)) == 0) single |= 1u << j;
+    }
+    if constexpr (OUT == 1) {
+      // ranges: {record off, count} per non-empty key, then {node, 0} per
+      // remote node (emit_ranges_group's order)
+#pragma unroll
+      for (uint32_t j = 0; j < kExE; j++) {
+        if (!ok[j]) continue;
+        const uint32_t p = (b0 + j) * 64 + lane;
+        const uint32_t nk = h[j].y;
+        const uint64_t rm = ((uint64_t)h[j].w << 32) | h[j].z;
+        uint64_t o = ob[j];
+        if (nk > 2) {
+          const uint2* sp = a.keyspill + (uint64_t)p * kSpillKeys;
+          const uint32_t ks = k[j].y + k[j].w;
+          for (uint32_t i = 0; i < nk; i++) {
+            const uint2 e = sp[i];
+            const uint32_t c = (i + 1 < nk ? sp[i + 1].y : ks) - e.y;
+            if (c) store_range(a.out_rng, o++, e.x, c);
+          }
+        } else {
+          if (k[j].y) store_range(a.out_rng, o++, k[j].x, k[j].y);
+          if (k[j].w) store_range(a.out_rng, o++, k[j].z, k[j].w);
+        }
+        for (uint64_t m = rm; m; m &= m - 1) store_range(a.out_rng, o++, (uint32_t)__builtin_ctzll(m), 0u);
+      }
+    } else {
+      // blocks of <= 1 record per publish: every lane's record loaded, then stored
+      uint4 v[kExE];
+#pragma unroll
+      for (uint32_t j = 0; j < kExE; j++)
+        if ((single >> j) & 1u && ok[j] && cnt[j] == 1) {   // key 0's record, key 1's, or the one remote node
+          const uint64_t rm = ((uint64_t)h[j].w << 32) | h[j].z;
+          v[j] = k[j].y ? *reinterpret_cast<const uint4*>(a.records + k[j].x)
+                 : k[j].w ? *reinterpret_cast<const uint4*>(a.records + k[j].z)
+                          : make_uint4((VMQG_EMIT_REMOTE << 24) | (uint32_t)__builtin_ctzll(rm), kNone, kNone, kNone);
+        }
+#pragma unroll
+      for (uint32_t j = 0; j < kExE; j++)
+        if ((single >> j) & 1u && ok[j] && cnt[j] == 1) store_rec<NT>(a.out, ob[j], v[j]);
+      // the other blocks: the whole wave over the block's served spans (the
+      // key cache and the positions just written re-read, L2 hits, rather
+      // than held in registers across the blocks: 88 VGPRs instead of 132)
+      uint32_t okm = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kExE; j++) okm |= ok[j] ? 1u << j : 0u;
+#pragma unroll 1
+      for (uint32_t j = 0; j < kExE; j++) {
+        if ((single >> j) & 1u) continue;
+        const uint32_t p = (b0 + j) * 64 + lane;
+        const bool okj = (okm >> j) & 1u;
+        const uint4* kc = reinterpret_cast<const uint4*>(a.keycache) + (uint64_t)p * 2;
+        const uint4 hj = okj ? kc[0] : make_uint4(0, 0, 0, 0), kj = okj ? kc[1] : make_uint4(0, 0, 0, 0);
+        const uint32_t sp = okj ? hj.x : 0u;   // == its count (checked above)
+        const uint32_t incl = wave_incl_scan32(sp);
+        L.h[lane] = hj;
+        L.k[lane] = kj;
+        L.ob[lane] = okj ? a.offsets[p] : 0ull;
+        L.crel[lane] = incl - sp;
+        if (lane == 63) L.crel[64] = incl;
+        wave_sync();
+        const uint32_t T = L.crel[64];
+        constexpr int U = 4;
+        uint32_t q = 0;   // the publish of record r: a cursor moving forward with r
+        for (uint32_t r0 = lane; r0 < T; r0 += 64 * U) {
+          uint4 v2[U];
+          uint64_t dst[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const uint32_t r = r0 + 64 * u;
+            if (r < T) {
+              while (q + 1 < 64 && L.crel[q + 1] <= r) q++;
+              const uint32_t rr = r - L.crel[q];
+              v2[u] = exact_emission(a, (b0 + j) * 64 + q, L.h[q], L.k[q], rr);
+              dst[u] = L.ob[q] + rr;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            if (r0 + 64 * u < T) store_rec<NT>(a.out, dst[u], v2[u]);
+        }
+        wave_sync();
+      }
+    }
+  }
+}
+
+template <int OUT>
+static void launch_emit_exact(const MatchArgs& a, bool nt, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  const uint32_t nblk = (a.npub + 63) / 64;
+  uint32_t g = div_up(nblk, kWaves * kExE);
+  const uint32_t cap = (uint32_t)a.cus * 8u;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  if (nt) {
+    if (t0) hipExtLaunchKernelGGL(k_emit_exact<OUT, true>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+    else k_emit_exact<OUT, true><<<g, 256, 0, st>>>(a);
+  } else {
+    if (t0) hipExtLaunchKernelGGL(k_emit_exact<OUT, false>, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+    else k_emit_exact<OUT, false><<<g, 256, 0, st>>>(a);
+  }
+}
+
 template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
 static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   // COUNT with dedupe or output groups on: the FEAT variant
@@ -2455,9 +2663,10 @@ static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEve
 template <int MODE, int OUT>
 static void launch_fast(const MatchArgs& a, uint32_t g, bool nt, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   // trie-less tables (every subscription exact): COUNT is one exact probe per publish
-  if (MODE == 0 && a.trieless && !a.dd_claimed && a.groups == nullptr) {
-    launch_count_exact<OUT>(a, st, t0, t1);
-    return;
+  if (a.trieless && !a.dd_claimed && a.groups == nullptr) {
+    if (MODE == 0) launch_count_exact<OUT>(a, st, t0, t1);
+    else if (VMQG_EMIT_EXACT) launch_emit_exact<OUT>(a, nt, st, t0, t1);
+    if (MODE == 0 || VMQG_EMIT_EXACT) return;
   }
   if (MODE == 0 && a.dd_claimed && a.dd_g == 4 && a.fast_g != 4) {
     // dedupe on: the representatives are few, so COUNT gives each four lanes
