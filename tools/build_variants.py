@@ -41,10 +41,12 @@ VARIANTS = {
     "rt_u8": ["-DVMQR_U=8"],
     "nofence": ["-DVMQG_STACK_FENCES=0"],
     "emitk4_0": ["-DVMQG_EMIT_K4=0"],
-    "nosplit": ["-DVMQG_TAIL_SPLIT=0"],
     "noemitex": ["-DVMQG_EMIT_EXACT=0"],
     "emitexk2": ["-DVMQG_EMIT_EXK=2"],
     "emitexk8": ["-DVMQG_EMIT_EXK=8"],
+    "emitexk1": ["-DVMQG_EMIT_EXK=1"],
+    "emitexk4": ["-DVMQG_EMIT_EXK=4"],
+    "ddpct67": ["-DVMQG_DD_ON_PCT=67"],
 }
 
 

@@ -89,6 +89,9 @@ constexpr uint32_t kHugeFlag = 0x40000000u;  // key cache word 1 (nk <= 8): a hu
 #ifndef VMQG_WALK_U
 #define VMQG_WALK_U 4   // records in flight per lane in a whole-wave walk's copy (8: the tail at 151 VGPRs, 3 waves/SIMD; 4: 128, 4)
 #endif
+#ifndef VMQG_DD_ON_PCT
+#define VMQG_DD_ON_PCT 50   // dedupe auto mode: on while more than this % of the sampled publishes repeat
+#endif
 #ifndef VMQG_TAIL_U
 #define VMQG_TAIL_U 8   // records in flight per lane in the tail's copies (wide, grouped, huge)
 #endif
@@ -1696,7 +1699,7 @@ void k_match_wave(MatchArgs a) {
     if (gw == 0 && lane == 0 && a.dd_claimed) {
       const uint32_t tried = a.status[kStDupTried], dups = a.status[kStDup];
       if (tried >= 256) {
-        const uint32_t mode = dups * 2u > tried ? 1u : 0u;
+        const uint32_t mode = (uint64_t)dups * 100u > (uint64_t)tried * VMQG_DD_ON_PCT ? 1u : 0u;
         *a.dd_mode = mode;
         if (a.dd_host) *a.dd_host = mode;   // host-mapped: the host reads it before its next calls
       }
@@ -1723,9 +1726,6 @@ void k_match_wave(MatchArgs a) {
     // the whole-wave walks (list 1); a walk that outgrows its LDS stack
     // borrows a global one (this grid has more waves than there are stacks)
     const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
-#ifndef VMQG_TAIL_SPLIT
-#define VMQG_TAIL_SPLIT 1   // A/B: 0 = one wave per chunk's wide publishes whatever the batch size
-#endif
 #ifndef VMQG_TAIL_NOWALK
 #define VMQG_TAIL_NOWALK 0   // A/B only (wrong with walked publishes): the tail without its walker
 #endif
@@ -1848,15 +1848,8 @@ void k_match_wave(MatchArgs a) {
     if (groups_on || wide_on) {
       const GroupSlot* gs = reinterpret_cast<const GroupSlot*>(a.groups);
       const uint32_t nchunks = (a.npub + a.gpw - 1) / a.gpw;
-      // fewer chunks than waves (a small batch, config A): `rep` waves share
-      // each chunk, wave `sub` of them taking the chunk's wide publishes of
-      // rank sub, sub + rep, ... — a chunk with several wide publishes is not
-      // copied one after another by one wave while other waves have none
-      const uint32_t rep = VMQG_TAIL_SPLIT && nchunks && nchunks * 2 <= nwaves
-                               ? (nwaves / nchunks < 64 ? nwaves / nchunks : 64u) : 1u;
-      const uint32_t sub = rep > 1 ? (uint32_t)gw / nchunks : 0u;
       uint64_t si = gw, cur = 0, m = 0;
-      uint32_t j = 0, gn = 0, c = rep > 1 ? (sub < rep ? (uint32_t)gw % nchunks : nchunks) : (uint32_t)gw, cc = 0;
+      uint32_t j = 0, gn = 0, c = (uint32_t)gw, cc = 0;
       for (;;) {
         uint32_t p = 0;
         bool have = false;
@@ -1872,20 +1865,7 @@ void k_match_wave(MatchArgs a) {
           else groups_on = false;
         }
         if (!have && wide_on) {
-          while (m == 0 && c < nchunks) {
-            m = uni64(a.widemask[c]);
-            cc = c;
-            c = rep > 1 ? nchunks : c + nwaves;
-            if (rep > 1) {   // this wave's ranks of the chunk's wide publishes
-              uint64_t keep = 0;
-              uint32_t r = 0;
-              for (uint64_t mm = m; mm; mm &= mm - 1) {
-                if (r == sub) keep |= mm & (~mm + 1);
-                r = r + 1 == rep ? 0u : r + 1;
-              }
-              m = keep;
-            }
-          }
+          while (m == 0 && c < nchunks) { m = uni64(a.widemask[c]); cc = c; c += nwaves; }
           if (m) {
             p = cc * a.gpw + (uint32_t)__builtin_ctzll(m);
             m &= m - 1;
@@ -2465,7 +2445,7 @@ static void launch_count_exact(const MatchArgs& a, hipStream_t st, hipEvent_t t0
 #define VMQG_EMIT_EXACT 1   // A/B: 0 = trie-less batches take the general EMIT
 #endif
 #ifndef VMQG_EMIT_EXK
-#define VMQG_EMIT_EXK 4   // 64-publish blocks per wave in flight in k_emit_exact
+#define VMQG_EMIT_EXK 2   // 64-publish blocks per wave in flight in k_emit_exact (A/B on R1: 1 / 2 / 4 / 8)
 #endif
 constexpr uint32_t kExE = VMQG_EMIT_EXK;
 #ifndef VMQG_EMIT_EXACT_WPE
