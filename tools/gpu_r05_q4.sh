@@ -12,3 +12,7 @@ for c in RT AC SS; do
   tail -c 300 $O/bench_$c.json
 done
 timeout -k 10 420 ./tools/bin/nif_harness 3 scale churn load > $O/harness.jsonl 2> $O/harness.err || { tail -20 $O/harness.err; exit 5; }
+tail -3 $O/harness.jsonl
+# N = 2 without a launcher (bench.py spawns its ranks; both on this box's one GPU)
+timeout -k 10 300 python -u bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline --no-e2e > $O/bench_C_n2.json 2> $O/bench_C_n2.err || { tail -5 $O/bench_C_n2.err; exit 6; }
+tail -c 300 $O/bench_C_n2.json
