@@ -950,7 +950,9 @@ def bench_d(args):
     if rank == 0:
         ops_n = st1["ops_applied"] - st0["ops_applied"]
         wait_ns = st1["apply_wait_ns"] - st0["apply_wait_ns"]
-        host_ns = st1["apply_host_ns"] - st0["apply_host_ns"] - wait_ns   # host work, without GPU back-pressure
+        # host work: apply_host_ns times the host stage alone (ABI 6: the
+        # device commit, where GPU back-pressure waits, is timed apart)
+        host_ns = st1["apply_host_ns"] - st0["apply_host_ns"]
         # Each EMIT launch is charged only the records it writes (counted on
         # the device): the fast EMIT launch writes every publish's records
         # except the wide ones' ($share groups on 4 nodes: 40 keys; alarm
