@@ -128,11 +128,32 @@ def launch_ranks(args):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
+    # a rank that fails ends the others (they would wait for it in the
+    # rendezvous or a collective until a watchdog fired)
+    import time as _time
+    rcs = [None] * len(procs)
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        _time.sleep(0.2)
     bad = [rc for rc in rcs if rc != 0]
     if bad:
         log("rank exit codes %s" % rcs)
-    return bad[0] if bad else 0
+    # the failing rank's code, not that of a rank this parent ended
+    return next((rc for rc in bad if rc > 0), 1) if bad else 0
 
 
 def main():
@@ -161,6 +182,8 @@ def main():
     ap.add_argument("--fast-g", type=int, default=None,
                     help="vmqg option fast_g for the secondary configs (A/B only; default: the library's own, 1)")
     ap.add_argument("--r-n", type=int, default=1_000_000, help="R1 / R2: N (the reference suite goes to 4,096,000)")
+    ap.add_argument("--exact-hint-mult", type=float, default=1.0,
+                    help="A / B / R1 / R2: exact-table size hint as a multiple of the subscriptions (A/B of its load)")
     ap.add_argument("--d-scale", type=float, default=1.0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--force-device", type=int, default=-1, help="rehearsal: every rank on this device")
@@ -533,7 +556,8 @@ def bench_other(args):
     n = w.n_subs
     # the exact table holds every topic with a local key or remote entries (at
     # most one per subscription): sized for n, it is planned at load <= 0.5
-    hints = {"edges": 2 * n, "paths": 2 * n, "keys": n * 5 // 4, "records": n * 5 // 4, "exact": n}
+    hints = {"edges": 2 * n, "paths": 2 * n, "keys": n * 5 // 4, "records": n * 5 // 4,
+             "exact": int(n * args.exact_hint_mult)}
     view = RegGpuView(node=w.self_node, device=0, nodes=w.nodes, max_mountpoints=max(1024, len(w.mps) + 1),
                       hints=hints)
     t0 = time.time()
