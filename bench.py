@@ -555,7 +555,7 @@ def bench_other(args):
     gen_s = time.time() - t0
     n = w.n_subs
     # the exact table holds every topic with a local key or remote entries (at
-    # most one per subscription): sized for n, it is planned at load <= 0.5
+    # most one per subscription): sized for n, it is planned at load <= 0.25
     hints = {"edges": 2 * n, "paths": 2 * n, "keys": n * 5 // 4, "records": n * 5 // 4,
              "exact": int(n * args.exact_hint_mult)}
     view = RegGpuView(node=w.self_node, device=0, nodes=w.nodes, max_mountpoints=max(1024, len(w.mps) + 1),

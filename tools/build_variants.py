@@ -47,7 +47,7 @@ VARIANTS = {
     "emitexk1": ["-DVMQG_EMIT_EXK=1"],
     "emitexk4": ["-DVMQG_EMIT_EXK=4"],
     "ddpct67": ["-DVMQG_DD_ON_PCT=67"],
-    "exact4x": ["-DVMQG_EXACT_SLOTS_PER_TOPIC=4"],
+    "exact2x": ["-DVMQG_EXACT_SLOTS_PER_TOPIC=2"],
 }
 
 

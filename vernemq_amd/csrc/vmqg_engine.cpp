@@ -6,7 +6,7 @@
 #include "vmqg_engine.h"
 
 #ifndef VMQG_EXACT_SLOTS_PER_TOPIC
-#define VMQG_EXACT_SLOTS_PER_TOPIC 2   // A/B: 4
+#define VMQG_EXACT_SLOTS_PER_TOPIC 4   // exact-table slots per topic (A/B: 2)
 #endif
 
 #include <algorithm>
@@ -308,10 +308,11 @@ Layout Engine::plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) c
   // sized from the hints too, so a bulk load does not re-lay the arena out
   L.keylist_cap = std::max<uint64_t>({4096, kl * 2, cfg.hint_keys / 16});
   L.rec_cap = std::max<uint64_t>({16384, recs * 2, cfg.hint_records * 2});
-  // exact slots per topic: a lookup that misses its bucket's first slot
-  // reads a second 64-B slot (or the next bucket) — one more memory request
-  // in a probe that is one request otherwise (R1 COUNT at load 0.49 / 0.24
-  // / 0.12: 336 / 285 / 273 us, profiles/ab_r05_exact_load/)
+  // exact slots per topic (load <= 0.25): a lookup that misses its bucket's
+  // first slot reads a second 64-B slot (or the next bucket) — one more
+  // memory request in a probe that is one request otherwise.  R1's COUNT at
+  // load 0.49 / 0.24 / 0.12: 336 / 285 / 273 us; D's +10 us (its 8M topics'
+  // table 1 -> 2 GB), E's -8 us, A's -2 us (profiles/ab_r05_exact_load/)
   const uint64_t spt = VMQG_EXACT_SLOTS_PER_TOPIC;
   const uint64_t exact_slots = next_pow2(std::max<uint64_t>(4096, std::max<uint64_t>(ex * spt + 1024, cfg.hint_exact * spt)));
   L.exact_buckets = exact_slots / kExactSlotsPerBucket;
