@@ -1001,6 +1001,7 @@ def bench_d(args):
             v["frac"] = v["GBps"] / PEAK_HBM_GBS if v["GBps"] else None
         dom_key = max(per_kernel, key=lambda k: per_kernel[k]["us"])
         dom = per_kernel[dom_key]
+        d_traffic = load_pmc_traffic("k_match_fast<1" if dom_key == "emit" else "k_match_wave<1", "pmc_d.json")
         alg_emit = dom["bytes"]
         achieved = dom["GBps"]
         step_level = {"bytes_written": 16 * emitted, "gpu_us_per_batch": stages["per_call"],
@@ -1038,8 +1039,9 @@ def bench_d(args):
                        "dedup": st1["dedup"], "dedup_walked": st1["dedup_walked"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS if achieved else None,
-                         "traffic": load_pmc_traffic("k_match_fast<1" if dom_key == "emit" else "k_match_wave<1",
-                                                     "pmc_d.json"),
+                         "traffic": d_traffic,
+                         "frac_physical": d_traffic / (dom["us"] * 1e3) / PEAK_HBM_GBS
+                         if d_traffic and dom["us"] else None,
                          "kernel": dom["kernel"], "algorithmic_bytes_per_launch": alg_emit,
                          "bytes_model": "16 B written per record this launch writes (compulsory lower bound)",
                          "per_kernel": per_kernel, "step_level": step_level,
