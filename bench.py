@@ -498,6 +498,7 @@ def main():
                        "dedup": served["dedup"], "dedup_walked": served["dedup_walked"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
+                         "frac_physical": traffic / emit_ns / PEAK_HBM_GBS if traffic and emit_ns > 0 else None,
                          "kernel": "k_match_fast<1,0,2,true,64> (EMIT)",
                          "algorithmic_bytes_per_launch": alg["emit_compulsory"],
                          "bytes_model": "16 B written per emission + 40 B read per publish + 16 B per distinct "
