@@ -70,6 +70,9 @@ extern "C" {
 
 #define VMQG_MAX_NODES 4096u    /* cluster nodes (vmq_trie_remote_subs / node lists are unbounded in
                                    the reference; 4,096 is this library's node-id space)            */
+#define VMQG_MAX_MOUNTPOINTS (1u << 24)   /* mountpoint ids: the roots grow on demand up to this many
+                                            (vmq_reg_trie has no limit: a mountpoint is part of every
+                                            key, vmq_reg_trie.erl:60, 279-281, 320)                  */
 
 /* ---- configuration --------------------------------------------------- */
 #define VMQG_CFG_REPLICA 1u     /* no host engine: device tables arrive as
@@ -79,7 +82,11 @@ typedef struct vmqg_config {
   int32_t device;            /* HIP device ordinal; -1 = host engine only     */
   uint32_t local_node;       /* node id that plays node() (< max_nodes)       */
   uint32_t max_nodes;        /* <= VMQG_MAX_NODES (0 = VMQG_MAX_NODES)        */
-  uint32_t max_mountpoints;  /* mountpoint ids are dense in [0, max)          */
+  uint32_t max_mountpoints;  /* initial root range (0 = 1024): mountpoint ids  */
+                             /* are dense; an op on an id past the range grows */
+                             /* it (a re-layout), up to VMQG_MAX_MOUNTPOINTS;  */
+                             /* a publish on VMQG_NONE (an unknown mountpoint) */
+                             /* matches nothing                                */
   uint32_t flags;            /* VMQG_CFG_*                                    */
   uint32_t reserved;
   uint64_t hint_edges;       /* sizing hints; 0 = small defaults, tables grow */
@@ -272,7 +279,13 @@ int vmqg_apply_ops(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* 
  *   vmqg_apply_commit  the device half: ships the staged patches (or image)
  *                      on the context stream; matches queued after it see the
  *                      new tables, *epoch_out = their epoch.  A device call.
- *                      No-op when nothing is staged. */
+ *                      No-op when nothing is staged.  If the upload fails
+ *                      (VMQG_E_DEVICE / VMQG_E_NOMEM) the stage stays pending:
+ *                      the epoch does not move, matches keep answering from
+ *                      the tables the device holds, the next commit (retry)
+ *                      ships the whole image, and a further vmqg_apply_stage
+ *                      adds to the pending one instead of returning
+ *                      VMQG_E_STATE — no change is lost. */
 int vmqg_apply_stage(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords);
 int vmqg_apply_commit(vmqg_ctx* ctx, uint64_t* epoch_out);
 
@@ -444,7 +457,9 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *                          <= 2 keys are copied by the EMIT tail on the XCD their
  *                          first key hashes to (0, the default: off)
  *   "reader_records" 1     keep the readers' record buffers (vmqg_records_pin);
- *                          a writer call, made before readers start */
+ *                          a writer call, made before readers start
+ *   "fail_commits" 0..1000 test hook: the next n commits fail with VMQG_E_DEVICE
+ *                          before touching the device (the recovery path above) */
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value);
 
 /* Average duration (ns) of the match kernels over the last

@@ -641,6 +641,8 @@ int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
     o->n = o->nwords = 0;
     return rc;
   }
+  /* a failed commit leaves the stage pending (the library's contract): the
+   * changes are kept and go out with the next commit, whatever its trigger */
   const uint64_t t1 = mono_ns();
   pthread_mutex_lock(&v->device);
   const uint64_t t2 = mono_ns();
@@ -658,6 +660,36 @@ int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
   if (t3 - t2 > v->st.commit_max_ns) v->st.commit_max_ns = t3 - t2;
   pthread_mutex_unlock(&v->q_mu);
   return rc ? rc : rc2;
+}
+
+int vmqgb_view_commit(vmqgb_view* v, uint64_t* epoch) {
+  vmqgb_view_write_begin(v);
+  pthread_mutex_lock(&v->device);
+  const int rc = vmqg_apply_commit(v->ctx, epoch);
+  pthread_mutex_unlock(&v->device);
+  vmqgb_view_write_end(v);
+  return rc;
+}
+
+int vmqgb_view_set_option(vmqgb_view* v, const char* name, int64_t value) {
+  vmqgb_view_write_begin(v);
+  pthread_mutex_lock(&v->device);
+  const int rc = vmqg_set_option(v->ctx, name, value);
+  pthread_mutex_unlock(&v->device);
+  vmqgb_view_write_end(v);
+  return rc;
+}
+
+int vmqgb_view_ctx_stats(vmqgb_view* v, vmqg_stats_t* out) {
+  /* the writer's fields under the writer mutex, the device calls' (epoch,
+   * arena size, last-call counters) under the device mutex: the order an
+   * apply takes them in */
+  vmqgb_view_write_begin(v);
+  pthread_mutex_lock(&v->device);
+  const int rc = vmqg_stats(v->ctx, out);
+  pthread_mutex_unlock(&v->device);
+  vmqgb_view_write_end(v);
+  return rc;
 }
 
 int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
@@ -872,6 +904,8 @@ static int expand_ranges(vmqgb_batch* b, const uint64_t* o, const vmqg_range* g,
 
 /* without a device (host-engine contexts): one synchronous call, which
  * reports VMQG_E_DEVICE */
+static int match_records(vmqgb_view* v, vmqgb_batch* b, vmqgb_req* qp, int dev_ranges);
+
 static int match_direct(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
   (void)recs; (void)nrecs;
   pthread_mutex_lock(&v->device);
@@ -882,6 +916,7 @@ static int match_direct(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_em
 
 int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
   vmqgb_view_release(v, b);
+  b->out_ranges = ranges;
   if (recs) *recs = NULL;
   if (nrecs) *nrecs = 0;
   if (b->n == 0) {   /* nothing to match: empty results */
@@ -911,12 +946,20 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
       uint64_t nrt = 0;
       int rc = vmqg_records_pin(v->ctx, b->epoch, &rt, &nrt, &b->rec_pin);
       if (rc == 0) b->rec_pinned = 1;
-      if (rc == VMQG_E_STATE && attempt < 16) {   /* two applies rewrote record slots since the round */
+      if (rc == VMQG_E_STATE) {   /* two applies rewrote record slots since the round */
         vmqgb_view_release(v, b);
         pthread_mutex_lock(&v->q_mu);
         v->st.state_retries++;
         pthread_mutex_unlock(&v->q_mu);
-        continue;
+        if (attempt < 3) continue;
+        /* applies keep outrunning the rounds: this batch takes the records
+         * path with device-copied records (no pin needed), as records mode
+         * does; the caller folds b->out (b->out_ranges == 0) */
+        b->out_ranges = 0;
+        pthread_mutex_lock(&v->q_mu);
+        v->st.ranges_fallbacks++;
+        pthread_mutex_unlock(&v->q_mu);
+        return match_records(v, b, &q, 0);
       }
       if (rc) return rc;
       rc = vmqgb_batch_recheck(b, v->ctx);   /* a word became known after the prepare */
@@ -936,7 +979,11 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
   }
   /* records: the records are copied out of the round (the expansion pins
    * the record table of the round's epoch for the copy only) */
-  int dev_ranges = !v->device_records;
+  return match_records(v, b, &q, !v->device_records);
+}
+
+static int match_records(vmqgb_view* v, vmqgb_batch* b, vmqgb_req* qp, int dev_ranges) {
+  vmqgb_req q = *qp;
   for (int attempt = 0;; attempt++) {
     q.dev_ranges = dev_ranges;
     combine(v, &q);

@@ -89,6 +89,9 @@ typedef struct vmqgb_batch {
   uint32_t rec_pin;     /* range mode: the record table pinned for the fold (vmqg_records_pin) */
   int rec_pinned;
   uint32_t stale_rematches;   /* matches repeated because a publish's unknown word became known */
+  int out_ranges;       /* set by vmqgb_view_match: 1 the results are ranges, 0 records (a
+                           ranges request falls back to records when applies keep rewriting
+                           the record slots its rounds index) */
 } vmqgb_batch;
 
 /* unk raw length flag: the raw bytes are a word list ({u32 len, bytes} per
@@ -225,13 +228,21 @@ void vmqgb_view_write_begin(vmqgb_view* v);
 void vmqgb_view_write_end(vmqgb_view* v);
 int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);   /* inside write_begin/end */
 int vmqgb_view_apply(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch);       /* write_begin, apply, write_end */
+/* Retries a commit that failed (VMQG_E_DEVICE): the pending changes are
+ * shipped as a whole image; 0 when nothing is pending. */
+int vmqgb_view_commit(vmqgb_view* v, uint64_t* epoch);
+/* vmqg_stats under the writer and the device mutex (the fields the writer
+ * and the device calls update) */
+int vmqgb_view_ctx_stats(vmqgb_view* v, vmqg_stats_t* out);
+/* vmqg_set_option under both mutexes */
+int vmqgb_view_set_option(vmqgb_view* v, const char* name, int64_t value);
 /* Knobs and counters of the submitter (tools/nif_harness.c reports them). */
 void vmqgb_view_set_device_records(vmqgb_view* v, int on);   /* records over PCIe instead of host expansion */
 void vmqgb_view_set_inflight(vmqgb_view* v, int n);          /* rounds in the kernels at once: 1..VMQGB_ROUNDS-1 (2) */
 typedef struct vmqgb_view_stats {
   uint64_t rounds, round_publishes, round_batches, max_round_publishes;
   uint64_t expanded_batches, device_record_batches, state_retries, stale_rematches;
-  uint64_t overflow_retries;
+  uint64_t overflow_retries, ranges_fallbacks;
   /* the writer's applies (vmqgb_view_apply_ops): host stage, wait for the
    * device mutex, commit — sums and maxima, ns */
   uint64_t applies, stage_ns, stage_max_ns, dev_wait_ns, dev_wait_max_ns, commit_ns, commit_max_ns;

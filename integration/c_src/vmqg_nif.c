@@ -65,7 +65,6 @@ typedef struct {
   vmqgb_interner *mps, *nodes, *subs, *infos;
   term_store node_t, sub_t, info_t, group_t;   /* group_t indexed by word id */
   vmqgb_ops ops;                  /* apply/3 and add_init/6 accumulation (under the write lock) */
-  uint32_t max_mountpoints;
 } vmqg_res;
 
 typedef struct {                  /* one batcher's batch (batch_new/1) */
@@ -75,7 +74,8 @@ typedef struct {                  /* one batcher's batch (batch_new/1) */
 
 static ErlNifResourceType* RES;
 static ErlNifResourceType* BRES;
-static ERL_NIF_TERM a_ok, a_error, a_invalid_topic, a_device, a_nomem, a_badarg, a_records, a_ranges;
+static ERL_NIF_TERM a_ok, a_error, a_invalid_topic, a_device, a_nomem, a_badarg, a_limit, a_busy, a_internal,
+    a_records, a_ranges;
 
 /* ------------------------------------------------------------ helpers */
 static int store_init(term_store* s) {
@@ -133,9 +133,16 @@ static int mp_id(vmqg_res* r, ErlNifEnv* env, ERL_NIF_TERM t, uint32_t* id) {
   return ok;
 }
 
+/* {error, Reason}: invalid_topic (a malformed change or Topic: nothing
+ * applied), limit (a change past VMQG_MAX_NODES nodes or VMQG_MAX_MOUNTPOINTS
+ * mountpoints: nothing applied), nomem, device (an apply whose upload failed
+ * stays pending and lands with the next commit; a match that failed), busy
+ * (applies kept rewriting what a match read: retry), internal (anything
+ * else).  vmq_reg_gpu_view tells them apart. */
 static ERL_NIF_TERM error_term(ErlNifEnv* env, int rc) {
   ERL_NIF_TERM r = rc == VMQG_E_INVAL ? a_invalid_topic : rc == VMQG_E_NOMEM ? a_nomem
-                 : rc == VMQG_E_DEVICE ? a_device : a_badarg;
+                 : rc == VMQG_E_DEVICE ? a_device : rc == VMQG_E_LIMIT ? a_limit
+                 : rc == VMQG_E_STATE ? a_busy : a_internal;
   return enif_make_tuple2(env, a_error, r);
 }
 
@@ -185,7 +192,6 @@ static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     return error_term(env, VMQG_E_NOMEM);
   }
   vmqgb_ops_init(&r->ops);
-  r->max_mountpoints = 1024;
   uint32_t id;
   term_id(r->mps, NULL, env, enif_make_string(env, "", ERL_NIF_LATIN1), &id);   /* "" is mountpoint 0 */
   term_id(r->nodes, &r->node_t, env, local, &id);                               /* node() is node 0 */
@@ -194,7 +200,8 @@ static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   cfg.device = device;
   cfg.local_node = 0;
   cfg.max_nodes = VMQG_MAX_NODES;
-  cfg.max_mountpoints = r->max_mountpoints;
+  cfg.max_mountpoints = 1024;   /* the initial root range: more mountpoints grow it (no limit below
+                                   VMQG_MAX_MOUNTPOINTS, as vmq_reg_trie has none) */
   int err = 0;
   r->ctx = vmqg_create(&cfg, &err);
   if (r->ctx && !(r->view = vmqgb_view_new(r->ctx))) err = VMQG_E_NOMEM;
@@ -211,9 +218,11 @@ static int add_change(ErlNifEnv* env, vmqg_res* r, uint32_t kind, ERL_NIF_TERM s
   const ERL_NIF_TERM* sid_el;
   if (!enif_get_tuple(env, sid, &arity, &sid_el) || arity != 2) return VMQG_E_INVAL;
   uint32_t mp, sub, info, nd;
-  if (!mp_id(r, env, sid_el[0], &mp) || mp >= r->max_mountpoints) return VMQG_E_LIMIT;
-  if (!term_id(r->subs, &r->sub_t, env, sid, &sub) || !term_id(r->infos, &r->info_t, env, subinfo, &info) ||
-      !term_id(r->nodes, &r->node_t, env, node, &nd))
+  /* the id spaces checked here, change by change, so that one change past a
+   * limit is refused alone (the library would refuse its whole op batch) */
+  if (!mp_id(r, env, sid_el[0], &mp) || !term_id(r->nodes, &r->node_t, env, node, &nd)) return VMQG_E_NOMEM;
+  if (mp >= VMQG_MAX_MOUNTPOINTS || nd >= VMQG_MAX_NODES) return VMQG_E_LIMIT;
+  if (!term_id(r->subs, &r->sub_t, env, sid, &sub) || !term_id(r->infos, &r->info_t, env, subinfo, &info))
     return VMQG_E_NOMEM;
   unsigned len;
   if (!enif_get_list_length(env, topic, &len) || len == 0 || len > 65536) return VMQG_E_INVAL;
@@ -333,6 +342,31 @@ static ERL_NIF_TERM nif_flush_init(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
   return rc ? error_term(env, rc) : a_ok;
 }
 
+/* commit(Ctx) -> ok | {error, _}: ships changes still pending after an apply
+ * whose upload failed ({error, device}): vmq_reg_gpu_view retries on a timer,
+ * so a transient device error delays changes and loses none. */
+static ERL_NIF_TERM nif_commit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  if (!r) return enif_make_badarg(env);
+  const int rc = vmqgb_view_commit(r->view, NULL);
+  return rc ? error_term(env, rc) : a_ok;
+}
+
+/* set_option(Ctx, Name, Value) -> ok | {error, _}: vmqg_set_option (kernel
+ * knobs from app env; "fail_commits" for tests) under the writer and device
+ * locks */
+static ERL_NIF_TERM nif_set_option(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  char name[64];
+  ErlNifSInt64 value;
+  if (!r || enif_get_atom(env, argv[1], name, sizeof name, ERL_NIF_LATIN1) <= 0 || !enif_get_int64(env, argv[2], &value))
+    return enif_make_badarg(env);
+  const int rc = vmqgb_view_set_option(r->view, name, (int64_t)value);
+  return rc ? error_term(env, rc) : a_ok;
+}
+
 /* ---------------------------------------------------------------- match */
 typedef struct {
   ErlNifEnv* env;
@@ -422,7 +456,7 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
    * MP of the previous publish is reused when identical (one term_to_binary
    * per distinct mountpoint run, not per publish) */
   ERL_NIF_TERM head, tail = argv[2], last_mp = 0;
-  uint32_t last_id = r->max_mountpoints;
+  uint32_t last_id = VMQG_NONE;
   size_t total = 0;
   for (unsigned i = 0; i < n; i++) {
     int arity;
@@ -442,7 +476,7 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     if (!last_mp || !enif_is_identical(el[0], last_mp)) {
       ErlNifBinary mpb;
       last_mp = el[0];
-      last_id = r->max_mountpoints;   /* an unknown mountpoint has no subscriptions: an id past every root */
+      last_id = VMQG_NONE;   /* an unknown mountpoint has no subscriptions: an id no root ever takes */
       if (enif_term_to_binary(env, el[0], &mpb)) {
         uint32_t id;
         enif_mutex_lock(r->mp_mu);
@@ -495,15 +529,15 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   for (unsigned i = 0; i < n; i++) {
     if (idx[i] < 0 || rc) { res[i] = error_term(env, idx[i] < 0 ? (int)idx[i] : rc); continue; }
     size_t cnt = 0;
-    if (ranges) {
+    if (b->out_ranges) {
       for (uint64_t k = b->offsets[idx[i]]; k < b->offsets[idx[i] + 1]; k++) cnt += b->rng[k].count ? b->rng[k].count : 1;
     } else {
       cnt = vmqgb_count_of(b, (size_t)idx[i]);
     }
     fold_acc acc = {env, r, (ERL_NIF_TERM*)enif_alloc((cnt ? cnt : 1) * sizeof(ERL_NIF_TERM)), 0};
     if (i + VMQGB_PREFETCH_AHEAD < n && idx[i + VMQGB_PREFETCH_AHEAD] >= 0)
-      vmqgb_prefetch_entries(b, ranges, recs, nrecs, (size_t)idx[i + VMQGB_PREFETCH_AHEAD]);
-    const int frc = vmqgb_fold_spans(b, ranges, recs, nrecs, (size_t)idx[i], make_entries, &acc);
+      vmqgb_prefetch_entries(b, b->out_ranges, recs, nrecs, (size_t)idx[i + VMQGB_PREFETCH_AHEAD]);
+    const int frc = vmqgb_fold_spans(b, b->out_ranges, recs, nrecs, (size_t)idx[i], make_entries, &acc);
     /* a fold that stops early (a range beyond the table) is this publish's error, never a partial list */
     res[i] = frc ? error_term(env, frc) : enif_make_tuple2(env, a_ok, enif_make_list_from_array(env, acc.out, (unsigned)acc.n));
     enif_free(acc.out);
@@ -520,9 +554,7 @@ static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   vmqg_res* r = get_res(env, argv[0]);
   if (!r) return enif_make_badarg(env);
   vmqg_stats_t st;
-  vmqgb_view_write_begin(r->view);   /* the writer's turn, never the device's: polling does not wait for a match */
-  const int rc = vmqg_stats(r->ctx, &st);
-  vmqgb_view_write_end(r->view);
+  const int rc = vmqgb_view_ctx_stats(r->view, &st);   /* writer mutex, then device mutex (the apply's order) */
   if (rc) return error_term(env, rc);
   return enif_make_tuple2(env, enif_make_uint64(env, st.subs), enif_make_uint64(env, st.device_bytes));
 }
@@ -549,6 +581,8 @@ RESCHEDULE(d_add_init, nif_add_init, ERL_NIF_DIRTY_JOB_CPU_BOUND)
 RESCHEDULE(d_flush_init, nif_flush_init, ERL_NIF_DIRTY_JOB_CPU_BOUND)
 RESCHEDULE(d_match, nif_match, ERL_NIF_DIRTY_JOB_CPU_BOUND)
 RESCHEDULE(d_stats, nif_stats, ERL_NIF_DIRTY_JOB_CPU_BOUND)
+RESCHEDULE(d_commit, nif_commit, ERL_NIF_DIRTY_JOB_CPU_BOUND)
+RESCHEDULE(d_set_option, nif_set_option, ERL_NIF_DIRTY_JOB_CPU_BOUND)
 
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   (void)priv; (void)info;
@@ -563,6 +597,9 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   a_device = enif_make_atom(env, "device");
   a_nomem = enif_make_atom(env, "nomem");
   a_badarg = enif_make_atom(env, "badarg");
+  a_limit = enif_make_atom(env, "limit");
+  a_busy = enif_make_atom(env, "busy");
+  a_internal = enif_make_atom(env, "internal");
   a_records = enif_make_atom(env, "records");
   a_ranges = enif_make_atom(env, "ranges");
   return RES && BRES ? 0 : 1;
@@ -577,6 +614,8 @@ static ErlNifFunc funcs[] = {
     {"batch_new", 1, nif_batch_new, 0},
     {"match", 4, d_match, 0},
     {"stats", 1, d_stats, 0},
+    {"commit", 1, d_commit, 0},
+    {"set_option", 3, d_set_option, 0},
 };
 
 ERL_NIF_INIT(vmqg_nif, funcs, load, NULL, NULL, NULL)

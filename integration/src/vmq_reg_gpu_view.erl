@@ -61,7 +61,8 @@
 -export([start_link/0,
          fold/4,
          stats/0,
-         shadow_stats/0]).
+         shadow_stats/0,
+         fallbacks/0]).
 
 %% gen_server callbacks
 -export([init/1,
@@ -80,6 +81,12 @@
 -define(WINDOW_EVENTS, 1000).
 %% shadow-compare counters (public: every fold caller bumps them)
 -define(SHADOW, vmq_reg_gpu_view_shadow).
+%% a fold the device refuses as busy (applies kept rewriting the records its
+%% round read) is asked again this many times
+-define(MATCH_RETRIES, 3).
+%% an apply whose upload failed stays pending in the library; the commit is
+%% retried after this many ms (and by the next apply)
+-define(COMMIT_RETRY_MS, 100).
 
 -record(state, {ctx,                    % vmqg_nif resource (vmqg_ctx + term tables)
                 batchers,               % tuple of vmq_reg_gpu_batcher pids
@@ -98,17 +105,41 @@ start_link() ->
 %% Topic goes to the NIF as the word list it is (vmq_reg_trie:fold/4 walks it
 %% as given, vmq_reg_trie.erl:59-66: a plugin publish is not validated,
 %% vmq_reg.erl:572-594) — '+' / '#' words, words holding '/', [] included.
-fold({MP, _} = SubscriberId, Topic, FoldFun, Acc) when is_list(Topic) ->
-    Entries = match(MP, Topic),
+fold(SubscriberId, Topic, FoldFun, Acc) when is_list(Topic) ->
+    Entries = entries(SubscriberId, Topic),
     shadow(SubscriberId, Topic, Entries),
     lists:foldl(fun(Entry, AccAcc) -> FoldFun(Entry, SubscriberId, AccAcc) end, Acc, Entries).
+
+%% The FoldFun entries of one publish.  vmq_reg_trie:fold/4 has no failure
+%% mode (vmq_reg_trie.erl:59-98), so neither may this: a match the device
+%% refuses as busy is asked again; any other refusal (device, nomem) is
+%% answered by vmq_reg_trie when it runs beside this view (reg_views =
+%% [vmq_reg_trie, vmq_reg_gpu_view]: a CPU copy of the same tables, fed the
+%% same events) and counted (fallbacks/0); only a view with no CPU copy
+%% raises, as it has no answer to give.
+entries(SubscriberId, Topic) ->
+    entries(SubscriberId, Topic, ?MATCH_RETRIES).
+
+entries({MP, _} = SubscriberId, Topic, Retries) ->
+    case match(MP, Topic) of
+        {ok, Entries} -> Entries;
+        {error, busy} when Retries > 0 -> entries(SubscriberId, Topic, Retries - 1);
+        {error, Reason} -> cpu_fold(SubscriberId, Topic, Reason)
+    end.
 
 match(MP, Topic) ->
     Batchers = ets:lookup_element(?MODULE, batchers, 2),
     Batcher = element(erlang:system_info(scheduler_id) rem tuple_size(Batchers) + 1, Batchers),
-    case gen_server:call(Batcher, {match, MP, Topic}, infinity) of
-        {ok, Entries} -> Entries;
-        {error, Reason} -> error({vmq_reg_gpu_view, Reason})
+    gen_server:call(Batcher, {match, MP, Topic}, infinity).
+
+cpu_fold(SubscriberId, Topic, Reason) ->
+    case whereis(vmq_reg_trie) of
+        undefined ->
+            error({vmq_reg_gpu_view, Reason});
+        _ ->
+            ets:update_counter(?SHADOW, fallbacks, 1),
+            Collect = fun(E, _, A) -> [E | A] end,
+            lists:reverse(vmq_reg_trie:fold(SubscriberId, Topic, Collect, []))
     end.
 
 %% Shadow compare.  With reg_views = [vmq_reg_trie, vmq_reg_gpu_view] both
@@ -139,7 +170,7 @@ shadow_compare({MP, _} = SubscriberId, Topic, Entries) ->
         Trie ->
             ok;
         _ ->
-            Gpu2 = lists:sort(match(MP, Topic)),
+            Gpu2 = lists:sort(entries(SubscriberId, Topic)),
             case lists:sort(vmq_reg_trie:fold(SubscriberId, Topic, Collect, [])) of
                 Gpu2 ->
                     ok;
@@ -154,6 +185,13 @@ shadow_stats() ->
     case catch ets:lookup(?SHADOW, sampled) of
         [{sampled, S}] -> {S, ets:lookup_element(?SHADOW, mismatched, 2)};
         _ -> {0, 0}
+    end.
+
+%% folds answered by vmq_reg_trie because the device refused them
+fallbacks() ->
+    case catch ets:lookup_element(?SHADOW, fallbacks, 2) of
+        N when is_integer(N) -> N;
+        _ -> 0
     end.
 
 %% stats/0 as vmq_reg_trie:stats/0 (vmq_reg_trie.erl:101-112):
@@ -171,13 +209,20 @@ stats() ->
 init([]) ->
     Device = application:get_env(vmq_server, gpu_reg_view_device, 0),
     {ok, Ctx} = vmqg_nif:create(#{device => Device, local_node => node()}),
+    %% kernel knobs (include/vmqg.h vmqg_set_option), [{Name, Value}]
+    lists:foreach(fun({Name, Value}) ->
+                          case vmqg_nif:set_option(Ctx, Name, Value) of
+                              ok -> ok;
+                              {error, R} -> lager:warning("~p: option ~p = ~p refused: ~p", [?MODULE, Name, Value, R])
+                          end
+                  end, application:get_env(vmq_server, gpu_reg_view_options, [])),
     %% the callers' lookups: a read_concurrency table this process owns
     %% (gone with it), as vmq_reg_trie's tables are (vmq_reg_trie.erl:136-143)
     ?MODULE = ets:new(?MODULE, [named_table, protected, {read_concurrency, true}]),
     true = ets:insert(?MODULE, {ctx, Ctx}),
     ?SHADOW = ets:new(?SHADOW, [named_table, public, {write_concurrency, true}, {read_concurrency, true}]),
     true = ets:insert(?SHADOW, [{every, application:get_env(vmq_server, gpu_reg_view_shadow, 0)},
-                                {sampled, 0}, {mismatched, 0}]),
+                                {sampled, 0}, {mismatched, 0}, {fallbacks, 0}]),
     %% fold/4 batchers, one per scheduler (linked: they die with the view)
     %% ranges (the default): the device returns {record off, count} per key and
     %% the entries are built straight from the pinned record table of the
@@ -190,13 +235,31 @@ init([]) ->
     Self = self(),
     spawn_link(
       fun() ->
-              %% initialize_trie/2 (vmq_reg_trie.erl:305-316), batched
-              ok = vmq_reg:fold_subscriptions(
-                     fun({MP, Topic, {SubscriberId, SubInfo, Node}}, ok) ->
-                             vmqg_nif:add_init(Ctx, MP, Topic, SubscriberId, SubInfo, Node)
-                     end, ok),
-              ok = vmqg_nif:flush_init(Ctx),
-              Self ! subscribers_loaded
+              %% initialize_trie/2 (vmq_reg_trie.erl:305-316), batched.  It
+              %% has no failure mode, so neither has this load: a
+              %% subscription the view cannot hold (past a limit: logged) is
+              %% skipped and the load goes on; an upload that failed stays
+              %% pending and is retried (retry_commit)
+              Skipped = vmq_reg:fold_subscriptions(
+                          fun({MP, Topic, {SubscriberId, SubInfo, Node}}, N) ->
+                                  case vmqg_nif:add_init(Ctx, MP, Topic, SubscriberId, SubInfo, Node) of
+                                      ok ->
+                                          N;
+                                      {error, device} ->
+                                          Self ! retry_commit,
+                                          N;
+                                      {error, Reason} ->
+                                          lager:warning("~p: subscription ~p of ~p not loaded: ~p",
+                                                        [?MODULE, Topic, SubscriberId, Reason]),
+                                          N + 1
+                                  end
+                          end, 0),
+              case vmqg_nif:flush_init(Ctx) of
+                  ok -> ok;
+                  {error, device} -> Self ! retry_commit;
+                  {error, Reason} -> exit({vmqg_load_failed, Reason})
+              end,
+              Self ! {subscribers_loaded, Skipped}
       end),
     EventHandler = vmq_reg:subscribe_subscriber_changes(),
     {ok, #state{ctx=Ctx, batchers=Batchers, event_handler=EventHandler}}.
@@ -210,12 +273,23 @@ handle_call(_Request, _From, State) ->
 handle_cast(_Msg, State) ->
     {noreply, State}.
 
-handle_info(subscribers_loaded, #state{event_queue=Q} = State) ->
+handle_info({subscribers_loaded, Skipped}, #state{event_queue=Q} = State) ->
     %% the events queued during the initial load, replayed in order (:198-205)
     State1 = replay(queue:to_list(Q), State#state{status=ready}),
     {Subs, _} = stats(),
-    lager:info("loaded ~p subscriptions into ~p", [Subs, ?MODULE]),
+    lager:info("loaded ~p subscriptions into ~p (~p skipped)", [Subs, ?MODULE, Skipped]),
     {noreply, State1#state{event_queue=undefined}};
+handle_info(retry_commit, #state{ctx=Ctx} = State) ->
+    %% changes of an apply whose upload failed: pending in the library until
+    %% a commit goes through (this one, or the next apply's)
+    case vmqg_nif:commit(Ctx) of
+        ok ->
+            ok;
+        {error, Reason} ->
+            lager:warning("~p: commit failed (~p), retrying", [?MODULE, Reason]),
+            erlang:send_after(?COMMIT_RETRY_MS, self(), retry_commit)
+    end,
+    {noreply, State};
 handle_info(Event, #state{status=init, event_queue=Q} = State) ->
     {noreply, State#state{event_queue=queue:in(Event, Q)}};
 handle_info(Event, State) ->
@@ -266,13 +340,18 @@ replay(Events, State) ->
 
 %% handle_event/2 (vmq_reg_trie.erl:240-251) for a group of events: the same
 %% diff per event, the same order (deletes, then adds; event after event);
-%% the NIF turns the whole group into one vmqg_apply_ops.  If the group is
-%% refused as malformed (invalid_topic / badarg: validated before anything
-%% is applied) the events are applied one by one, so only the offending one
-%% fails, as it would alone.  Any other failure (nomem, device) may have left
-%% part of the group applied: replaying it would apply that part twice, so
-%% the view stops instead, and its supervisor's restart loads the tables
-%% afresh (initialize_trie, vmq_reg_trie.erl:305-316).
+%% the NIF turns the whole group into one vmqg_apply_ops.  vmq_reg_trie's
+%% handler cannot fail, so this one never stops the view:
+%%   - refused before anything is applied (invalid_topic: a malformed change;
+%%     limit: a change past the node / mountpoint id space): the events are
+%%     applied one by one, so only the offending event is skipped (logged),
+%%     as it would be alone;
+%%   - device: the group is applied on the host and pending in the library
+%%     (folds answer from the previous tables meanwhile); a timer retries the
+%%     commit, and the next apply ships it too — nothing is lost;
+%%   - nomem: the group may be partly applied and cannot be replayed (that
+%%     would apply its first part twice); logged, the view keeps answering,
+%%     and the shadow compare (or a restart) is what shows the difference.
 handle_events(Events, #state{ctx=Ctx, event_handler=Handler} = State) ->
     AllChanges = lists:foldr(fun(E, Acc) ->
                                      case event_changes(Handler, E) of
@@ -287,15 +366,28 @@ handle_events(Events, #state{ctx=Ctx, event_handler=Handler} = State) ->
             case vmqg_nif:apply_many(Ctx, Changes) of
                 ok ->
                     ok;
-                {error, Malformed} when Malformed =:= invalid_topic; Malformed =:= badarg ->
-                    lists:foreach(fun({SubscriberId, Ch}) ->
-                                          ok = vmqg_nif:apply(Ctx, SubscriberId, Ch)
-                                  end, Changes);
+                {error, Refused} when Refused =:= invalid_topic; Refused =:= limit ->
+                    lists:foreach(fun(C) -> apply_one(Ctx, C) end, Changes);
                 {error, Reason} ->
-                    exit({vmqg_apply_failed, Reason})
+                    apply_failed(Reason, length(Changes))
             end
     end,
     State.
+
+apply_one(Ctx, {SubscriberId, Ch}) ->
+    case vmqg_nif:apply(Ctx, SubscriberId, Ch) of
+        ok ->
+            ok;
+        {error, Refused} when Refused =:= invalid_topic; Refused =:= limit ->
+            lager:warning("~p: event of ~p skipped: ~p (~p)", [?MODULE, SubscriberId, Refused, Ch]);
+        {error, Reason} ->
+            apply_failed(Reason, 1)
+    end.
+
+apply_failed(device, _N) ->
+    erlang:send_after(?COMMIT_RETRY_MS, self(), retry_commit);
+apply_failed(Reason, N) ->
+    lager:error("~p: applying ~p subscriber events failed: ~p", [?MODULE, N, Reason]).
 
 %% {SubscriberId, [{Kind, Topic, SubInfo, Node}]} of one event, or ignore
 event_changes(Handler, Event) ->

@@ -121,7 +121,7 @@ static int one_batch(bt_t* a, vmqgb_batch* b, long* idx, size_t lo, size_t n, ch
     char h[64];
     int frc = idx[i] < 0 ? (int)idx[i] : rc;
     sput(&s, "");
-    if (!frc) frc = a->ranges ? vmqgb_fold_ranges(b, recs, nrecs, (size_t)idx[i], put_entry, &s)
+    if (!frc) frc = b->out_ranges ? vmqgb_fold_ranges(b, recs, nrecs, (size_t)idx[i], put_entry, &s)
                               : vmqgb_fold(b, (size_t)idx[i], put_entry, &s);
     if (wout) snprintf(h, sizeof h, "%zu %llu %d", lo + i, (unsigned long long)b->epoch, frc);
     else snprintf(h, sizeof h, "%zu %d", lo + i, frc);

@@ -84,7 +84,11 @@ ERL_NIF_TERM enif_make_copy(ErlNifEnv* dst_env, ERL_NIF_TERM src_term);
 ERL_NIF_TERM enif_make_resource(ErlNifEnv* env, void* obj);
 
 /* term inspection */
+typedef int64_t ErlNifSInt64;
 int enif_get_int(ErlNifEnv* env, ERL_NIF_TERM term, int* ip);
+int enif_get_int64(ErlNifEnv* env, ERL_NIF_TERM term, ErlNifSInt64* ip);
+/* bytes written including the NUL, 0 if not an atom or it does not fit */
+int enif_get_atom(ErlNifEnv* env, ERL_NIF_TERM atom, char* buf, unsigned size, ErlNifCharEncoding encoding);
 int enif_get_uint(ErlNifEnv* env, ERL_NIF_TERM term, unsigned* ip);
 int enif_get_tuple(ErlNifEnv* env, ERL_NIF_TERM term, int* arity, const ERL_NIF_TERM** array);
 int enif_get_list_length(ErlNifEnv* env, ERL_NIF_TERM term, unsigned* len);

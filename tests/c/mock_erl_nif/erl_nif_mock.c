@@ -128,6 +128,19 @@ int enif_get_int(ErlNifEnv* env, ERL_NIF_TERM term, int* ip) {
   *ip = (int)C(term)->i;
   return 1;
 }
+int enif_get_int64(ErlNifEnv* env, ERL_NIF_TERM term, ErlNifSInt64* ip) {
+  (void)env;
+  if (C(term)->type != T_INT) return 0;
+  *ip = C(term)->i;
+  return 1;
+}
+int enif_get_atom(ErlNifEnv* env, ERL_NIF_TERM atom, char* buf, unsigned size, ErlNifCharEncoding encoding) {
+  (void)env; (void)encoding;
+  if (C(atom)->type != T_ATOM || C(atom)->n + 1 > size) return 0;
+  memcpy(buf, C(atom)->bytes, C(atom)->n);
+  buf[C(atom)->n] = 0;
+  return (int)C(atom)->n + 1;
+}
 int enif_get_uint(ErlNifEnv* env, ERL_NIF_TERM term, unsigned* ip) {
   (void)env;
   if (C(term)->type != T_INT || C(term)->i < 0 || C(term)->i > 0xFFFFFFFFll) return 0;

@@ -18,6 +18,8 @@
  *                                       inside a word, "~x" the atom x, "!" the empty list)
  *   M <records|ranges>                  match(Ctx, Batch, every publish so far, Mode)
  *   T                                   stats(Ctx)
+ *   X <name> <value>                    set_option(Ctx, name, value)
+ *   R                                   commit(Ctx)
  * output: "A <result>", "S <result>...", "T <subs>", "M <n>" then per
  * publish "<i> ok <entries>" (A,<mp>,<client>,<qos> | B,<node>,<group>,<mp>,
  * <client>,<qos> | C,<node>, space separated) or "<i> error <reason>". */
@@ -247,6 +249,17 @@ int main(int argc, char** argv) {
         }
         fputc('\n', out);
       }
+    } else if (line[0] == 'X') {
+      long long v;
+      if (sscanf(line + 2, "%63s %lld", a1, &v) != 2) return 11;
+      const ERL_NIF_TERM args[3] = {ctx, enif_make_atom(env, a1), mock_make_int(v)};
+      fprintf(out, "X ");
+      mock_print(out, call("set_option", 3, args));
+      fputc('\n', out);
+    } else if (line[0] == 'R') {
+      fprintf(out, "R ");
+      mock_print(out, call("commit", 1, &ctx));
+      fputc('\n', out);
     } else if (line[0] == 'T') {
       const ERL_NIF_TERM r = call("stats", 1, &ctx);
       int ar, subs = -1;

@@ -382,6 +382,35 @@ def test_mountpoints_are_disjoint_roots():
     _compare_batches(prod, orc, pubs, "mp")
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_5000_mountpoints_grow_the_roots(mode):
+    """5,000 mountpoints (vmq_reg_trie has no limit: vmq_reg_trie.erl:60,
+    279-281, 320) on a context created with 16 roots: the root range grows by
+    re-layouts while subscriptions arrive, and every publish — each
+    mountpoint's own topics, other tenants' topics, an unknown mountpoint —
+    folds to the oracle's entries, before and after deletes."""
+    from tests.test_host_engine import _mp_events
+    node = "n@h"
+    prod = _driver(node, mode, max_mountpoints=16)
+    orc = O.TrieOracle(node)
+    adds, dels = _mp_events(5000, node)
+    for lo in range(0, len(adds), 4000):
+        prod.apply(adds[lo:lo + 4000])
+        orc.apply(adds[lo:lo + 4000])
+    import random
+    r = random.Random(7)
+    pubs = []
+    for _ in range(6000):
+        mp = "t%d" % r.randrange(5200)    # ~4 % unknown mountpoints
+        pubs.append((mp, (b"w%d" % r.randrange(4), b"x%d" % r.randrange(3)) + ((b"z",) if r.random() < 0.3 else ())))
+    pubs.append(("", (b"w0", b"x0")))
+    _compare_batches(prod, orc, pubs, "5000 mountpoints")
+    assert sum(len(x) for x in prod.fold_batch(pubs[:500])) > 500
+    prod.apply(dels)
+    orc.apply(dels)
+    _compare_batches(prod, orc, pubs, "5000 mountpoints after deletes")
+
+
 def test_empty_batch_and_output_growth():
     prod = _driver("n@h")
     v = prod.view

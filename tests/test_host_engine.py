@@ -114,3 +114,57 @@ def test_record_epochs_refuse_stale_ranges():
         v.records(epoch=e1)                           # a slot was rewritten
     recs = v.records(epoch=e2)
     assert len(recs) > 0
+
+
+def _mp_events(n_mps, node="n@h", seed=5):
+    """Per mountpoint t<k>: a wildcard, a '#', a $share and an exact filter
+    (different subscribers), remote subscribers on every 7th; every 3rd
+    mountpoint later loses two of them (deletes walk the trie paths back)."""
+    import random
+    r = random.Random(seed)
+    adds, dels = [], []
+    for k in range(n_mps):
+        mp = "t%d" % k
+        w = (b"w%d" % r.randrange(4), b"x%d" % r.randrange(3))
+        subs = [(b"a", (w[0], b"+"), r.randint(0, 2)), (b"b", (w[0], b"#"), 1),
+                (b"c", (b"$share", b"g%d" % (k % 3), w[0], w[1]), 0), (b"d", w, 2)]
+        for cid, t, q in subs:
+            nd = "n%d@h" % (1 + k % 3) if (k % 7 == 0 and cid == b"d") else node
+            adds.append(("updated", (mp, cid), None, [(nd, True, [(t, q)])]))
+        if k % 3 == 0:
+            for cid, t, q in subs[:2]:
+                dels.append(("deleted", (mp, cid), [(node, True, [(t, q)])]))
+    return adds, dels
+
+
+def test_mountpoints_grow_past_the_initial_roots():
+    """vmq_reg_trie has no mountpoint limit (a mountpoint is part of every
+    key, vmq_reg_trie.erl:60, 279-281, 320): 5,000 mountpoints on a context
+    created with 16 roots grow the root range (re-layouts renumbering every
+    path) and the tables stay equal to the oracle's, through the deletes too."""
+    node = "n@h"
+    prod = H.ProductDriver(node, device=-1, max_mountpoints=16)
+    orc = O.TrieOracle(node)
+    adds, dels = _mp_events(5000, node)
+    for lo in range(0, len(adds), 4000):   # several applies, each growing the roots
+        prod.apply(adds[lo:lo + 4000])
+        orc.apply(adds[lo:lo + 4000])
+    _compare(prod, orc, "5000 mountpoints")
+    prod.apply(dels)
+    orc.apply(dels)
+    _compare(prod, orc, "5000 mountpoints after deletes")
+    assert prod.view.stats_raw()["paths"] >= 5000
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_churn_over_growing_mountpoints(seed):
+    """Churn whose clients live on 40 mountpoints, on a context created with
+    2 roots: growth happens between and inside event batches."""
+    wl = H.ChurnWorkload(seed, mps=[""] + ["m%d" % i for i in range(39)])
+    prod = H.ProductDriver(wl.self_node, device=-1, max_mountpoints=2)
+    orc = O.TrieOracle(wl.self_node)
+    for step in range(40):
+        evs = [wl.event() for _ in range(8)]
+        prod.apply(evs)
+        orc.apply(evs)
+        _compare(prod, orc, "seed %d step %d" % (seed, step))

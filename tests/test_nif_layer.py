@@ -652,3 +652,139 @@ def test_acl_nif_glue_matches_the_oracle_on_the_gpu(tmp_path):
     assert got[-1] == "{error,function_clause}"
     assert got[:-1] == ["true" if w == 1 else "false" for w in want]
     assert 0 < sum(want) < len(want)
+
+
+# ------------------------------------------------- limits and device errors
+def _nif_limits_script(device, n_mps=5000, n_pubs=3000, seed=21):
+    """Through the NIF: an initial load over 5,000 mountpoints (the library
+    starts with 1,024 roots and grows them), 4,100 distinct remote nodes (ids
+    past VMQG_MAX_NODES refused one by one: {error, limit}), publishes on
+    known, other and unknown mountpoints; then a group whose upload is forced
+    to fail ({error, device}: matches keep answering from the previous
+    tables, commit/1 ships it), then a group holding one change on a node past
+    the limit (apply_many refused with limit, then per event: only that
+    event refused).  Returns the script and the oracle history per phase."""
+    import random
+    r = random.Random(seed)
+    f2t = lambda f: tuple(x.encode() for x in f.split("/"))
+    ev = lambda mp, cid, nd, f, q: ("updated", (mp, cid), None, [("n%d@h" % nd, True, [(f2t(f), q)])])
+    lines = ["N %d" % device]
+    load = []
+    for k in range(n_mps):
+        mp = "t%d" % k
+        w0, w1 = "w%d" % r.randrange(4), "x%d" % r.randrange(3)
+        for cid, f, q in (("a", w0 + "/+", r.randint(0, 2)), ("b", w0 + "/#", 1),
+                          ("c", "$share/g%d/%s/%s" % (k % 3, w0, w1), 0), ("d", w0 + "/" + w1, 2)):
+            lines.append("I 0 %s %s %d %s" % (mp, cid, q, f))
+            load.append(ev(mp, cid.encode(), 0, f, q))
+    for nd in range(1, 4101):
+        lines.append("I %d t1 r%d 1 w0/x0" % (nd, nd))
+        if nd < 4096:
+            load.append(ev("t1", b"r%d" % nd, nd, "w0/x0", 1))
+    lines += ["F", "T"]
+    for _ in range(n_pubs):
+        mp = "t%d" % r.randrange(n_mps + 200)
+        t = "w%d/x%d" % (r.randrange(4), r.randrange(3)) + ("/z" if r.random() < 0.3 else "")
+        lines.append("P %s %s" % (mp, t))
+    lines += ["P t1 w0/x0", "P - w0/x0", "M records", "M ranges"]
+    # a group whose commit fails
+    g1 = []
+    lines.append("X fail_commits 1")
+    for k in range(40):
+        mp = "t%d" % r.randrange(n_mps)
+        f = "w%d/+" % r.randrange(4)
+        lines += ["V %s e%d" % (mp, k), "C add 0 2 %s" % f]
+        g1.append(ev(mp, b"e%d" % k, 0, f, 2))
+    lines += ["A", "T", "M records", "M ranges", "R", "T", "M records", "M ranges"]
+    # a group with one change past the node limit
+    g2, g2_lines = [], []
+    for k in range(20):
+        mp = "t%d" % r.randrange(n_mps)
+        nd = 4200 if k == 7 else 0
+        g2_lines += ["V %s h%d" % (mp, k), "C add %d 1 w1/#" % nd]
+        if nd == 0:
+            g2.append(ev(mp, b"h%d" % k, 0, "w1/#", 1))
+    lines += g2_lines + ["A"] + g2_lines + ["S", "T", "M records", "M ranges"]
+    return "\n".join(lines) + "\n", load, g1, g2
+
+
+def _run_limits(tmp_path, device):
+    exe = _build_nif_check(tmp_path)
+    script, load, g1, g2 = _nif_limits_script(device)
+    (tmp_path / "l.txt").write_text(script)
+    r = subprocess.run([str(exe), str(tmp_path / "l.txt"), str(tmp_path / "o.txt")], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr
+    return script, (tmp_path / "o.txt").read_text().splitlines(), load, g1, g2
+
+
+def test_nif_limits_and_device_errors_over_the_erl_nif_double(tmp_path):
+    """Host context: 5,000 mountpoints load (no mountpoint limit, as in
+    vmq_reg_trie); the 5 changes on nodes past VMQG_MAX_NODES are refused
+    alone with {error, limit} (add_init) and the load goes on; a forced
+    commit failure answers {error, device} and commit/1 then ships it;
+    apply_many with one change past the node limit answers {error, limit}
+    and apply/3 event by event refuses only that event.  stats/1 follows
+    the oracle at every step."""
+    from oracle import oracle as O
+    script, out, load, g1, g2 = _run_limits(tmp_path, -1)
+    res = [l for l in out if not l[0].isdigit() and not l.startswith("M ")]
+    assert res[:5] == ["I {error,limit}"] * 5, res[:8]
+    orc = O.TrieOracle("n0@h")
+    orc.apply(load)
+    s0 = orc.sizes()["stats_subs"]
+    orc.apply(g1)
+    s1 = orc.sizes()["stats_subs"]
+    orc.apply(g2)
+    s2 = orc.sizes()["stats_subs"]
+    assert res[5:] == ["F ok", "T %d" % s0, "X ok", "A {error,device}", "T %d" % s1, "R ok", "T %d" % s1,
+                       "A {error,limit}", "S " + " ".join(["ok"] * 7 + ["{error,limit}"] + ["ok"] * 12),
+                       "T %d" % s2], res[5:]
+
+
+@pytest.mark.gpu
+def test_nif_limits_and_device_errors_on_the_gpu(tmp_path):
+    """The same script on the GPU: every match/4 block (records and ranges)
+    equals the oracle's fold/4 of its phase — 5,000 mountpoints and a
+    4,095-node remote list answered; after the failed commit the view still
+    answers, from the tables before the group; after commit/1, with it; after
+    the refused event, without it."""
+    from oracle import oracle as O
+    script, out, load, g1, g2 = _run_limits(tmp_path, 0)
+    pubs = []
+    for l in script.splitlines():
+        if l.startswith("P "):
+            _, mp, t = l.split(" ", 2)
+            pubs.append(("" if mp == "-" else mp, _script_topic(t)))
+    orc = O.TrieOracle("n0@h")
+    orc.apply(load)
+    w0 = [sorted(x) for x in orc.fold_batch([(mp, b"pub", t) for mp, t in pubs])]
+    orc.apply(g1)
+    w1 = [sorted(x) for x in orc.fold_batch([(mp, b"pub", t) for mp, t in pubs])]
+    orc.apply(g2)
+    w2 = [sorted(x) for x in orc.fold_batch([(mp, b"pub", t) for mp, t in pubs])]
+    assert w0 != w1 != w2
+    blocks, cur = [], None
+    for l in out:
+        if l.startswith("M "):
+            cur = []
+            blocks.append(cur)
+        elif cur is not None and l[0].isdigit():
+            cur.append(l)
+    assert len(blocks) == 8
+    for b, want in zip(blocks, [w0, w0, w0, w0, w1, w1, w2, w2]):
+        assert len(b) == len(pubs)
+        for i, l in enumerate(b):
+            f = l.split(" ")
+            assert f[1] == "ok", l
+            ents = []
+            for e in f[2:]:
+                p = e.split(",")
+                if p[0] == "A":
+                    ents.append(("A", (p[1], p[2].encode()), O.subinfo_repr(int(p[3]))))
+                elif p[0] == "B":
+                    ents.append(("B", p[1], p[2].encode(), (p[3], p[4].encode()), O.subinfo_repr(int(p[5]))))
+                else:
+                    ents.append(("C", p[1]))
+            assert sorted(ents) == want[i], (i, pubs[i], sorted(ents)[:4], want[i][:4])
+    assert max(len(x) for x in w0) >= 4095

@@ -96,7 +96,7 @@ def test_prepare_word_lists_is_the_dictionary_lookup():
         assert arr[i]["flags"] == (_lib.PUB_DOLLAR if dollar else 0) | (_lib.PUB_UNKNOWN if unknown else 0), t
         k += len(t)
     assert words[0:2].tolist()[1] == _lib.WORD_PLUS
-    assert arr[-1]["mountpoint"] == v.max_mountpoints      # an unknown mountpoint matches nothing
+    assert arr[-1]["mountpoint"] == _lib.NONE      # an unknown mountpoint matches nothing
 
 
 # ------------------------------------------------------------------ GPU side

@@ -119,10 +119,10 @@ static void* batcher(void* p) {
     const double t2 = now();
     for (size_t i = 0; !rc && i < b.n; i++) {
       if (fold_spans) {
-        vmqgb_prefetch_entries(&b, a->ranges, recs, nrecs, i + VMQGB_PREFETCH_AHEAD);
-        rc = vmqgb_fold_spans(&b, a->ranges, recs, nrecs, i, sum_span, acc);
+        vmqgb_prefetch_entries(&b, b.out_ranges, recs, nrecs, i + VMQGB_PREFETCH_AHEAD);
+        rc = vmqgb_fold_spans(&b, b.out_ranges, recs, nrecs, i, sum_span, acc);
       }
-      else rc = a->ranges ? vmqgb_fold_ranges(&b, recs, nrecs, i, sum_entry, acc) : vmqgb_fold(&b, i, sum_entry, acc);
+      else rc = b.out_ranges ? vmqgb_fold_ranges(&b, recs, nrecs, i, sum_entry, acc) : vmqgb_fold(&b, i, sum_entry, acc);
     }
     vmqgb_view_release(view, &b);
     const double t3 = now();

@@ -658,6 +658,7 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len) {
 
 int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   if (!ctx || !name) return VMQG_E_INVAL;
+  GUARD_BEGIN   // "reader_records" copies the record table twice: bad_alloc -> VMQG_E_NOMEM
   Engine& e = ctx->e;
   const std::string n(name);
   if (n == "fast_g") {
@@ -691,10 +692,14 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   } else if (n == "count_bpc" || n == "emit_bpc") {
     if (value < 0 || value > 32) return VMQG_E_INVAL;
     (n == "count_bpc" ? e.opt_count_bpc : e.opt_emit_bpc) = (uint32_t)value;
+  } else if (n == "fail_commits") {   // test hook: the next `value` commits fail as a device error would
+    if (value < 0 || value > 1000 || e.replica) return VMQG_E_INVAL;
+    e.fault_commits = (uint32_t)value;
   } else {
     return VMQG_E_INVAL;
   }
   return VMQG_OK;
+  GUARD_END
 }
 
 int vmqg_set_timing(vmqg_ctx* ctx, int enable) {

@@ -102,6 +102,7 @@ VMQG_HD uint32_t exact_tail_words(uint32_t L) { return L > kExactInline ? L - kE
 constexpr uint32_t kEdgeSlotsPerBucket = 4;
 constexpr uint32_t kMaxNodes = 4096;        // VMQG_MAX_NODES: one 64-bit bitset word per lane
 constexpr uint32_t kLowNodes = 64;          // nodes held in the inline 64-bit masks
+constexpr uint32_t kMaxMountpoints = 1u << 24;   // mountpoint ids (roots grow on demand up to this)
 constexpr uint32_t kExactSlotsPerBucket = 2;   // 128-B buckets: one L2 line per probe
 
 // Arena layout.  Fixed-size POD: it is what a replica needs to read an image

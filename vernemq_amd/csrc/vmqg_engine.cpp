@@ -50,7 +50,7 @@ int Engine::init(const vmqg_config& c) {
   if (cfg.max_mountpoints == 0) cfg.max_mountpoints = 1024;
   if (cfg.max_nodes > VMQG_MAX_NODES || cfg.local_node >= cfg.max_nodes) return VMQG_E_LIMIT;
   static_assert(VMQG_MAX_NODES == kMaxNodes, "the wave tier's node set is kMaxNodes bits");
-  if (cfg.max_mountpoints > (1u << 24)) return VMQG_E_LIMIT;
+  if (cfg.max_mountpoints > kMaxMountpoints) return VMQG_E_LIMIT;
   replica = (cfg.flags & VMQG_CFG_REPLICA) != 0;
   // reserved words
   for (const char* s : {"+", "#", "$share"}) intern(reinterpret_cast<const uint8_t*>(s), strlen(s), true);
@@ -382,6 +382,45 @@ void Engine::rebuild(uint64_t extra_edges, bool compact) {
   for (auto& t : topics) t.dirty = 0;
   dirty_keys.clear(); dirty_paths.clear(); dirty_topics.clear();
   rebuilds++;
+}
+
+// Mountpoint m's root is path m (a walk starts at path pub.mountpoint), so
+// the roots are the first cfg.max_mountpoints path ids.  In vmq_reg_trie a
+// mountpoint is only part of every key (vmq_reg_trie.erl:60, 279-281, 320):
+// there is no limit.  A change on a mountpoint past the root range grows it
+// (doubling): every other path id moves up by the growth, the edges in the
+// mirror are renumbered, and the arena is re-laid out (a full image: the
+// next commit ships it, replicas reload it).  Called at the start of a stage,
+// before any handler has marked anything dirty.
+void Engine::grow_mountpoints(uint32_t need) {
+  const uint32_t old = cfg.max_mountpoints;
+  uint64_t m = old ? old : 1;
+  while (m < need) m *= 2;
+  m = std::min<uint64_t>(m, kMaxMountpoints);
+  const uint32_t shift = (uint32_t)m - old;
+  if (!shift) return;
+  auto mv = [old, shift](uint32_t p) { return p == kNone || p < old ? p : p + shift; };
+  // the live edges, renumbered where rebuild() collects them
+  if (!mirror.empty()) {
+    EdgeSlot* t = region<EdgeSlot>(lay.edge_off);
+    for (uint64_t i = 0; i < lay.edge_buckets * kEdgeSlotsPerBucket; i++)
+      if (t[i].parent != kEmpty && t[i].parent != kTomb) { t[i].parent = mv(t[i].parent); t[i].child = mv(t[i].child); }
+  }
+  paths.insert(paths.begin() + old, shift, PathInfo{});
+  for (uint32_t r = old; r < (uint32_t)m; r++) {
+    paths[r].parent = kNone; paths[r].word = kNone; paths[r].mp = r; paths[r].depth = 0;
+  }
+  FlatIndex idx;
+  idx.reserve(paths.size());
+  for (uint64_t p = m; p < paths.size(); p++) {
+    paths[p].parent = mv(paths[p].parent);
+    idx.insert(((uint64_t)paths[p].parent << 32) | paths[p].word, (uint32_t)p);
+  }
+  path_index = std::move(idx);
+  for (auto& t : topics) t.path = mv(t.path);
+  for (auto& p : dirty_paths) p = mv(p);
+  cfg.max_mountpoints = (uint32_t)m;
+  rebuild(0);
 }
 
 bool Engine::write_key(uint32_t k) {
@@ -857,14 +896,18 @@ int Engine::apply_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
 // running (they read only the device side: dlay, the arena, scratch).
 int Engine::stage_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords) {
   if (replica) return VMQG_E_STATE;
-  if (staged) return VMQG_E_STATE;   // the previous stage is not committed yet
+  // the previous stage is not committed yet (unless its commit failed: this
+  // one adds to it, and the next commit ships both as one image)
+  if (staged && !commit_failed) return VMQG_E_STATE;
   const auto t0 = std::chrono::steady_clock::now();
   // validate the whole batch before touching state
   uint64_t add_words = 0;
+  uint32_t top_mp = 0;
   for (size_t i = 0; i < n; i++) {
     const vmqg_op& o = ops[i];
     if (o.kind != VMQG_OP_ADD && o.kind != VMQG_OP_DEL) return VMQG_E_INVAL;
-    if (o.mountpoint >= cfg.max_mountpoints || o.node >= cfg.max_nodes) return VMQG_E_LIMIT;
+    if (o.mountpoint >= kMaxMountpoints || o.node >= cfg.max_nodes) return VMQG_E_LIMIT;
+    if (o.mountpoint >= top_mp) top_mp = o.mountpoint + 1;
     if (o.nwords == 0 || (uint64_t)o.word_off + o.nwords > nwords) return VMQG_E_INVAL;
     const uint32_t* w = words + o.word_off;
     for (uint32_t j = 0; j < o.nwords; j++) if (w[j] >= dict.size()) return VMQG_E_INVAL;
@@ -874,8 +917,11 @@ int Engine::stage_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
     if (o.kind == VMQG_OP_ADD && ((o.nwords >= 3 && w[0] == kShare) || contains_wildcard(w, o.nwords)))
       add_words += o.nwords;
   }
+  const bool on_top = staged;
   staged = true;
   staged_epoch = epoch + 1;
+  if (on_top) full_image = true;   // the failed commit's changes and this stage's: one image
+  if (top_mp > cfg.max_mountpoints) grow_mountpoints(top_mp);   // a new mountpoint past the roots
   // the edge table must absorb every edge this batch could add
   if ((edge_live + edge_tomb + add_words) * 10 > lay.edge_buckets * kEdgeSlotsPerBucket * 7) rebuild(add_words);
   for (size_t i = 0; i < n; i++) {
@@ -914,7 +960,20 @@ int Engine::commit() {
     if (rb_on) publish_records();
   }
   const auto t1 = std::chrono::steady_clock::now();
-  const int rc = upload();
+  int rc;
+  if (fault_commits) { fault_commits--; rc = VMQG_E_DEVICE; }
+  else rc = upload();
+  if (rc) {
+    // The device tables are those of `epoch` (or, after a device fault, in
+    // doubt): the stage stays pending, matches keep answering from `epoch`,
+    // and the next commit re-uploads the whole mirror (authoritative).
+    commit_failed = true;
+    full_image = true;
+    apply_upload_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           std::chrono::steady_clock::now() - t1).count();
+    return rc;
+  }
+  commit_failed = false;
   staged = false;
   patches_ready = false;
   epoch = staged_epoch;
@@ -994,8 +1053,12 @@ void Engine::publish_records() {
 void Engine::enable_reader_records() {
   if (rb_on) return;
   const Record* src = region<Record>(lay.rec_off);
+  // both copies made before either is committed: an allocation failure
+  // (bad_alloc, VMQG_E_NOMEM at the ABI) leaves the option off and nothing changed
+  HugeVec<Record> c0(src, src + lay.rec_cap), c1(src, src + lay.rec_cap);
+  rb[0].recs.swap(c0);
+  rb[1].recs.swap(c1);
   for (RecBuf& b : rb) {
-    b.recs.assign(src, src + lay.rec_cap);
     b.epoch = epoch;
     b.rec_epoch = rec_epoch;
     b.closed.store(0, std::memory_order_seq_cst);
@@ -1039,6 +1102,7 @@ int Engine::upload() {
   // stream: order_on chains them)
   if (order_on(stream) != VMQG_OK) return VMQG_E_DEVICE;
   if (full_image) {
+    last_full = true;   // replicas reload the image too (a retried commit's patches were not shipped)
     if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
     if (d_arena_bytes < lay.total_bytes) {
       if (d_arena) hipFree(d_arena);

@@ -336,6 +336,11 @@ struct Engine {
   uint64_t epoch = 0, rebuilds = 0;
   uint64_t staged_epoch = 0;
   bool staged = false, patches_ready = false;
+  // a commit whose upload failed: the stage stays pending (epoch unchanged,
+  // matches keep answering from the device's tables), the next commit ships
+  // the whole image, and a stage may be added on top of it meanwhile
+  bool commit_failed = false;
+  uint32_t fault_commits = 0;       // vmqg_set_option "fail_commits": test hook, the next n uploads fail
   uint32_t max_depth = 0;           // deepest path interned (sizes the wave tier's stack)
   std::vector<Patch> last_patches;
   bool last_full = false;
@@ -472,6 +477,7 @@ struct Engine {
   bool write_high_list(uint32_t& off, uint32_t& cap, const std::vector<uint32_t>& nodes);
   Layout plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) const;
   void rebuild(uint64_t extra_edges, bool compact = false);
+  void grow_mountpoints(uint32_t need);
   bool flush_incremental();
   bool write_key(uint32_t k);
   bool write_path(uint32_t p);

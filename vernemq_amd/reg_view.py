@@ -92,6 +92,9 @@ class RegGpuView:
             raise _lib.VmqgError(err.value, "vmqg_create")
         self._h = h
         self.device = device
+        # the initial root range only: a new mountpoint past it grows the
+        # roots (vmq_reg_trie has no mountpoint limit); an unknown mountpoint
+        # is prepared as NONE, an id no root ever takes
         self.max_mountpoints = max_mountpoints
 
     def close(self):
@@ -149,8 +152,6 @@ class RegGpuView:
                       self.subinfos.get(si, _subinfo_key(si)), 0)
             allw.extend(topic)
             off += len(topic)
-        if len(self.mountpoints) > self.max_mountpoints:
-            raise _lib.VmqgError(_lib.E_LIMIT, "mountpoints")
         if len(self.nodes) > _lib.MAX_NODES:
             raise _lib.VmqgError(_lib.E_LIMIT, "nodes")
         return arr, self.intern_words(allw, create=True)
@@ -197,7 +198,7 @@ class RegGpuView:
                 if st != "ok":
                     raise ValueError("invalid publish topic %r: %s" % (topic, words))
                 topic = words
-            mid = self.mountpoints.ids.get(mp, self.max_mountpoints)   # unknown MP: matches nothing
+            mid = self.mountpoints.ids.get(mp, _lib.NONE)   # unknown MP: matches nothing
             flags = _lib.PUB_DOLLAR if topic and topic[0][:1] == b"$" else 0
             arr[i] = (mid, off, len(topic), flags)
             allw.extend(topic)
@@ -212,7 +213,7 @@ class RegGpuView:
         has (one holding a '/', say) is UNKNOWN, an empty list has no words."""
         pubs = list(pubs)
         n = len(pubs)
-        mps = np.array([self.mountpoints.ids.get(mp, self.max_mountpoints) for mp, _ in pubs], dtype=np.uint32)
+        mps = np.array([self.mountpoints.ids.get(mp, _lib.NONE) for mp, _ in pubs], dtype=np.uint32)
         counts = np.array([len(t) for _, t in pubs], dtype=np.uint32)
         flat = [bytes(w) for _, t in pubs for w in t]
         nw = len(flat)

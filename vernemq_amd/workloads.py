@@ -154,7 +154,7 @@ class Workload:
     def publish_arrays(self, view, lo: int = 0, hi: int | None = None):
         """PUB_DTYPE + word-id arrays for publishes [lo, hi) (ids looked up, not created)."""
         pwid = view.intern_words(self.pub_words, create=False).astype(np.uint32)
-        mp_id = np.array([view.mountpoints.ids.get(m, view.max_mountpoints) for m in self.mps], dtype=np.uint32)
+        mp_id = np.array([view.mountpoints.ids.get(m, _lib.NONE) for m in self.mps], dtype=np.uint32)
         return self.publish_arrays_ids(pwid, mp_id, lo, hi)
 
     def publish_arrays_ids(self, pwid: np.ndarray, mp_id: np.ndarray, lo: int = 0, hi: int | None = None):
