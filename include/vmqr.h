@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct vmqr_config {
   int32_t device;            /* HIP device ordinal; -1 = host tables only        */
-  uint32_t max_mountpoints;  /* mountpoint ids are dense in [0, max)             */
+  uint32_t max_mountpoints;  /* initial range (0 = 1024): a retained topic on a mountpoint id past it grows it, up to VMQG_MAX_MOUNTPOINTS; VMQG_NONE in a filter matches nothing */
   uint64_t hint_topics;      /* sizing hint (retained entries); 0 = grow         */
 } vmqr_config;
 

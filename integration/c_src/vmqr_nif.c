@@ -34,7 +34,6 @@ typedef struct {
   vmqr_ctx* ctx;
   pthread_mutex_t mu;
   vmqgb_interner* mps;
-  uint32_t max_mountpoints;
 } vmqr_res;
 
 static ErlNifResourceType* RES;
@@ -59,8 +58,9 @@ static vmqr_res* get_res(ErlNifEnv* env, ERL_NIF_TERM t) {
   return enif_get_resource(env, t, RES, (void**)&r) ? r : NULL;
 }
 
-/* mountpoint id of MP; create: intern it (a retained topic), else
- * max_mountpoints for an unseen one (it holds nothing) */
+/* mountpoint id of MP; create: intern it (a retained topic: the library
+ * grows its per-mountpoint lists), else VMQG_NONE for an unseen one (it
+ * holds nothing) */
 static int mp_id(ErlNifEnv* env, vmqr_res* r, ERL_NIF_TERM mp, int create, uint32_t* id) {
   ErlNifBinary b;
   if (!enif_term_to_binary(env, mp, &b)) return VMQG_E_NOMEM;
@@ -68,9 +68,9 @@ static int mp_id(ErlNifEnv* env, vmqr_res* r, ERL_NIF_TERM mp, int create, uint3
   if (create) {
     *id = vmqgb_intern(r->mps, b.data, b.size);
     if (*id == VMQG_NONE) rc = VMQG_E_NOMEM;
-    else if (*id >= r->max_mountpoints) rc = VMQG_E_LIMIT;
+    else if (*id >= VMQG_MAX_MOUNTPOINTS) rc = VMQG_E_LIMIT;
   } else if (vmqgb_lookup(r->mps, b.data, b.size, id) != 0) {
-    *id = r->max_mountpoints;
+    *id = VMQG_NONE;
   }
   enif_release_binary(&b);
   return rc;
@@ -125,13 +125,12 @@ static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   memset(r, 0, sizeof(*r));
   pthread_mutex_init(&r->mu, NULL);
   r->mps = vmqgb_interner_new();
-  r->max_mountpoints = 1024;
   uint32_t id;
   mp_id(env, r, enif_make_string(env, "", ERL_NIF_LATIN1), 1, &id);   /* "" is mountpoint 0 */
   vmqr_config cfg;
   memset(&cfg, 0, sizeof cfg);
   cfg.device = device;
-  cfg.max_mountpoints = r->max_mountpoints;
+  cfg.max_mountpoints = 1024;   /* the initial range: more mountpoints grow it */
   int err = 0;
   r->ctx = r->mps ? vmqr_create(&cfg, &err) : NULL;
   if (!r->mps) err = VMQG_E_NOMEM;
@@ -179,6 +178,28 @@ static ERL_NIF_TERM nif_apply(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
 /* match(Ctx, [{MP, Filter}]) -> [[Id]] | {error, _}: match_fold/4 (:75-99)
  * for a batch of filters — per filter the message ids of the retained
  * topics it matches (an ets set has no order: the ids are sorted) */
+/* Sorts n message ids: insertion sort for a short span, else an LSD radix
+ * sort (8-bit digits, a digit on which every id agrees is skipped) through
+ * tmp (n entries) — O(n), since one '#' filter may match every retained
+ * message (match_fold/4 walks the whole table, vmq_retain_srv.erl:75-99). */
+static void sort_ids(uint32_t* a, size_t n, uint32_t* tmp) {
+  if (n <= 32) {
+    for (size_t i = 1; i < n; i++)
+      for (size_t j = i; j > 0 && a[j - 1] > a[j]; j--) { const uint32_t x = a[j]; a[j] = a[j - 1]; a[j - 1] = x; }
+    return;
+  }
+  uint32_t *src = a, *dst = tmp;
+  for (int shift = 0; shift < 32; shift += 8) {
+    size_t cnt[257] = {0};
+    for (size_t i = 0; i < n; i++) cnt[((src[i] >> shift) & 255u) + 1]++;
+    if (cnt[((src[0] >> shift) & 255u) + 1] == n) continue;   /* one bucket: the digit orders nothing */
+    for (int d = 0; d < 256; d++) cnt[d + 1] += cnt[d];
+    for (size_t i = 0; i < n; i++) dst[cnt[(src[i] >> shift) & 255u]++] = src[i];
+    uint32_t* x = src; src = dst; dst = x;
+  }
+  if (src != a) memcpy(a, src, n * sizeof(uint32_t));
+}
+
 static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   (void)argc;
   vmqr_res* r = get_res(env, argv[0]);
@@ -218,17 +239,20 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   } else {
     ERL_NIF_TERM* lists = (ERL_NIF_TERM*)enif_alloc((n ? n : 1) * sizeof(ERL_NIF_TERM));
     ERL_NIF_TERM* ids = (ERL_NIF_TERM*)enif_alloc((got ? got : 1) * sizeof(ERL_NIF_TERM));
+    uint64_t span = 0;
+    for (unsigned i = 0; i < n; i++) if (offs[i + 1] - offs[i] > span) span = offs[i + 1] - offs[i];
+    uint32_t* tmp = span > 32 ? (uint32_t*)enif_alloc(span * sizeof(uint32_t)) : NULL;
+    if (span > 32 && !tmp) { enif_free(lists); lists = NULL; }
     for (unsigned i = 0; lists && ids && i < n; i++) {
       const uint64_t lo = offs[i], hi = offs[i + 1];
-      /* insertion sort of the (few) ids of one filter */
-      for (uint64_t a = lo + 1; a < hi; a++)
-        for (uint64_t b = a; b > lo && out[b - 1] > out[b]; b--) { const uint32_t x = out[b]; out[b] = out[b - 1]; out[b - 1] = x; }
+      sort_ids(out + lo, (size_t)(hi - lo), tmp);   /* a '#' filter can match every retained message */
       for (uint64_t k = lo; k < hi; k++) ids[k] = enif_make_uint(env, out[k]);
       lists[i] = enif_make_list_from_array(env, ids + lo, (unsigned)(hi - lo));
     }
     ret = lists && ids ? enif_make_list_from_array(env, lists, n) : error_term(env, VMQG_E_NOMEM);
     enif_free(lists);
     enif_free(ids);
+    enif_free(tmp);
   }
   enif_free(f);
   enif_free(offs);

@@ -9,7 +9,10 @@
  *     records of epoch E for a key the writer rewrites at every apply (its 64
  *     records all carry the SubInfo of that apply: no torn or mixed table),
  *     and stays so until unpinned while the writer keeps applying;
- *   - readers are never refused a pin of the current epoch.
+ *   - readers are never refused a pin of the current epoch;
+ * then the view's writer-side calls beside each other (applies, some with a
+ * failed commit, commit retries, stats polls): no change lost.
+ * tests/test_nif_layer.py also runs it built with -fsanitize=thread.
  * Prints "ok" and exits 0; otherwise a message and non-zero. */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -24,12 +27,12 @@
 #define SUB0 1000u
 
 static vmqg_ctx* ctx;
-static volatile int done;
+static _Atomic int done;
 static uint32_t expect_id[NWORDS];          /* written by the writer before it bumps `published` */
 static volatile uint32_t published;          /* words whose ids are in expect_id */
 static volatile uint64_t info_of_epoch[1u << 16];   /* the SubInfo the key's records carry at each epoch */
 static uint64_t key_off = ~0ull;             /* the rewritten key's record range [key_off, +NSUB) */
-static volatile int failed;
+static _Atomic int failed;
 static uint64_t total_pins;
 
 #define FAIL(...) do { fprintf(stderr, __VA_ARGS__); fputc('\n', stderr); failed = 1; } while (0)
@@ -132,6 +135,52 @@ static void* reader(void* p) {
   return NULL;
 }
 
+/* phase 2: the view's writer-side entry points beside each other — applies
+ * (some of whose commits are made to fail: fail_commits), commit retries and
+ * stats polls (vmqgb_view_ctx_stats: writer mutex, then device mutex) */
+static _Atomic int done2;
+#define ROUNDS2 3000
+
+static void* view_writer(void* p) {
+  vmqgb_view* v = (vmqgb_view*)p;
+  vmqgb_ops ops;
+  vmqgb_ops_init(&ops);
+  for (uint32_t r = 0; r < ROUNDS2 && !failed; r++) {
+    char f[32];
+    const int l = snprintf(f, sizeof f, "y/%u", r);
+    if (r % 50 == 7 && vmqgb_view_set_option(v, "fail_commits", 1)) FAIL("set_option");
+    vmqgb_view_write_begin(v);
+    if (vmqgb_ops_add_filter(&ops, ctx, VMQG_OP_ADD, 0, (const uint8_t*)f, (size_t)l, 0, 9000 + r, 1)) FAIL("add y");
+    const int rc = vmqgb_view_apply_ops(v, &ops, NULL);
+    vmqgb_view_write_end(v);
+    if (rc && rc != VMQG_E_DEVICE) FAIL("apply y/%u: %d", r, rc);
+  }
+  vmqgb_ops_free(&ops);
+  done2 = 1;
+  return NULL;
+}
+
+static void* view_committer(void* p) {
+  vmqgb_view* v = (vmqgb_view*)p;
+  while (!done2 && !failed) {
+    const int rc = vmqgb_view_commit(v, NULL);
+    if (rc && rc != VMQG_E_DEVICE) FAIL("commit: %d", rc);
+  }
+  return NULL;
+}
+
+static void* view_stats(void* p) {
+  vmqgb_view* v = (vmqgb_view*)p;
+  uint64_t last = 0;
+  while (!done2 && !failed) {
+    vmqg_stats_t st;
+    if (vmqgb_view_ctx_stats(v, &st)) FAIL("stats");
+    if (st.subs < last) FAIL("stats: subs went back %llu -> %llu", (unsigned long long)last, (unsigned long long)st.subs);
+    last = st.subs;
+  }
+  return NULL;
+}
+
 int main(void) {
   vmqg_config cfg;
   memset(&cfg, 0, sizeof cfg);
@@ -165,6 +214,22 @@ int main(void) {
   pthread_create(&w, NULL, writer, NULL);
   pthread_join(w, NULL);
   for (int t = 0; t < 6; t++) pthread_join(rd[t], NULL);
+  if (!failed) {
+    vmqgb_view* v = vmqgb_view_new(ctx);
+    vmqg_stats_t s0, s1;
+    if (!v || vmqgb_view_ctx_stats(v, &s0)) FAIL("view");
+    pthread_t pw, pc, ps;
+    pthread_create(&ps, NULL, view_stats, v);
+    pthread_create(&pc, NULL, view_committer, v);
+    pthread_create(&pw, NULL, view_writer, v);
+    pthread_join(pw, NULL);
+    pthread_join(pc, NULL);
+    pthread_join(ps, NULL);
+    if (vmqgb_view_commit(v, NULL)) FAIL("final commit");   /* a pending failed commit goes out */
+    if (vmqgb_view_ctx_stats(v, &s1) || s1.subs != s0.subs + ROUNDS2)
+      FAIL("view phase: subs %llu, want %llu", (unsigned long long)s1.subs, (unsigned long long)s0.subs + ROUNDS2);
+    vmqgb_view_free(v);
+  }
   vmqgb_ops_free(&ops);
   vmqg_destroy(ctx);
   if (failed) return 1;

@@ -788,3 +788,61 @@ def test_nif_limits_and_device_errors_on_the_gpu(tmp_path):
                     ents.append(("C", p[1]))
             assert sorted(ents) == want[i], (i, pubs[i], sorted(ents)[:4], want[i][:4])
     assert max(len(x) for x in w0) >= 4095
+
+
+@pytest.mark.gpu
+def test_retain_nif_sorts_a_filter_matching_every_message(tmp_path):
+    """One '#' filter over 100,000 retained messages (match_fold/4 walks the
+    whole table, vmq_retain_srv.erl:75-99) and 'r/+' over the same: the ids
+    come back sorted, all of them — in linear time (radix sort in
+    vmqr_nif.c; the insertion sort it replaces was quadratic)."""
+    import random
+    import time
+    r = random.Random(4)
+    ids = list(range(100000))
+    r.shuffle(ids)
+    lines = ["N 0"] + ["I - r/%d %d" % (i, mid) for i, mid in enumerate(ids)] + ["A", "Q - #", "Q - r/+", "Q - x", "M"]
+    t0 = time.time()
+    out = _run_aux(tmp_path, "retain", "\n".join(lines) + "\n")
+    assert out[0] == "A ok" and out[1] == "M 3"
+    for l in out[2:4]:
+        got = [int(x) for x in l.split()[1:]]
+        assert got == sorted(ids)
+    assert out[4].split() == ["2"]
+    assert time.time() - t0 < 60
+
+
+def _tsan_lib():
+    """libvmqgpu's vmqg sources built with ThreadSanitizer on the host code
+    (-Xarch_host -fsanitize=thread; device code as usual), cached under
+    build/tsan/<source id> so a test run rebuilds it only when they change."""
+    from vernemq_amd import _lib
+    d = os.path.join(ROOT, "build", "tsan", _lib.source_id())
+    so = os.path.join(d, "libvmqgpu.so")
+    if not os.path.exists(so):
+        os.makedirs(d, exist_ok=True)
+        csrc = os.path.join(ROOT, "vernemq_amd", "csrc")
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O1", "-g", "-std=c++17", "-fPIC", "-shared",
+                        "-Xarch_host", "-fsanitize=thread", "-o", so + ".tmp",
+                        os.path.join(csrc, "vmqg_engine.cpp"), os.path.join(csrc, "vmqg_abi.cpp"),
+                        os.path.join(csrc, "vmqg_kernels.hip")], check=True, capture_output=True)
+        os.replace(so + ".tmp", so)
+    return d
+
+
+def test_readers_beside_the_writer_under_thread_sanitizer(tmp_path):
+    """rcu_check (readers beside the writer: lock-free dictionary, left-right
+    record buffers; then the view's applies, failed commits, commit retries
+    and stats polls beside each other) with the library's host code and the
+    check built with ThreadSanitizer: no data race reported."""
+    d = _tsan_lib()
+    exe = tmp_path / "rcu_check_tsan"
+    subprocess.run(["/opt/rocm/llvm/bin/clang", "-std=gnu11", "-O1", "-g", "-fsanitize=thread", "-pthread",
+                    "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "integration", "c_src"),
+                    "-o", str(exe), os.path.join(ROOT, "tests", "c", "rcu_check.c"),
+                    os.path.join(ROOT, "integration", "c_src", "vmqg_batch.c"),
+                    "-L", d, "-l:libvmqgpu.so", "-Wl,-rpath," + d], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66"))
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr[-6000:]
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-6000:]

@@ -148,6 +148,25 @@ def test_host_engine_table_matches_oracle():
     assert got == live
 
 
+def test_host_engine_grows_mountpoint_lists():
+    """Retained topics on 3,000 mountpoints on a store created with 4:
+    the per-mountpoint lists grow (re-layouts) and the host table stays the
+    oracle's (vmq_retain_srv keys by {MP, Topic}, no limit)."""
+    from vernemq_amd.retain import RetainGpuSrv
+    ops, _ = random_store(11, n_ops=6000, mps=tuple("m%d" % i for i in range(3000)))
+    r = RetainGpuSrv(device=-1, max_mountpoints=4)
+    live = {}
+    for k in range(0, len(ops), 500):
+        r.apply(ops[k:k + 500])
+    for op in ops:
+        if op[0] == "insert":
+            live[(op[1], op[2])] = op[3]
+        else:
+            live.pop((op[1], op[2]), None)
+    assert r.stats()[0] == len(live)
+    assert len(r.dump().splitlines()) == len(live)
+
+
 # ------------------------------------------------------------------ GPU
 @pytest.mark.gpu
 @pytest.mark.parametrize("scen", RETAIN, ids=[s["name"] for s in RETAIN])
@@ -298,3 +317,25 @@ def test_retain_position_lists_and_long_topics():
     got, want = prod.fold_batch(filters), orc.fold_batch(filters)
     assert [len(g) for g in got] == [len(w) for w in want]
     assert got == want
+
+
+@pytest.mark.gpu
+def test_retain_parity_over_growing_mountpoints():
+    """Filters on 3,000 mountpoints (and unknown ones) of a store created
+    with 4 mountpoint lists: every filter's message ids equal the oracle's
+    match_fold/4 after each growing apply."""
+    from vernemq_amd.retain import RetainGpuSrv
+    ops, filters = random_store(12, n_ops=6000, n_filters=600, mps=tuple("m%d" % i for i in range(3000)))
+    prod, orc = ProductDriver(), OracleDriver()
+    prod.r = RetainGpuSrv(device=0, max_mountpoints=4)
+    for k in range(0, len(ops), 2000):
+        batch = ops[k:k + 2000]
+        prod.r.apply(batch)
+        for op in batch:
+            if op[0] == "insert":
+                orc.insert(op[1], op[2], op[3])
+            else:
+                orc.delete(op[1], op[2])
+        got, want = prod.fold_batch(filters), orc.fold_batch(filters)
+        bad = [i for i in range(len(filters)) if got[i] != want[i]]
+        assert not bad, (k, filters[bad[0]], got[bad[0]][:5], want[bad[0]][:5])

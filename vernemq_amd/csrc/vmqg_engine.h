@@ -333,7 +333,9 @@ struct Engine {
   // epoch: the tables the device holds (matches queued now see them); an
   // apply is staged on the host (staged_epoch = epoch + 1) while matches
   // run, then committed: shipped to the device, epoch = staged_epoch
-  uint64_t epoch = 0, rebuilds = 0;
+  // (atomic: vmqg_epoch is a reader call, made beside the writer's commit)
+  std::atomic<uint64_t> epoch{0};
+  uint64_t rebuilds = 0;
   uint64_t staged_epoch = 0;
   bool staged = false, patches_ready = false;
   // a commit whose upload failed: the stage stays pending (epoch unchanged,

@@ -34,7 +34,7 @@ RetainEngine::~RetainEngine() {
 int RetainEngine::init(const vmqr_config& c) {
   cfg = c;
   if (cfg.max_mountpoints == 0) cfg.max_mountpoints = 1024;
-  if (cfg.max_mountpoints > (1u << 24)) return VMQG_E_LIMIT;
+  if (cfg.max_mountpoints > vmqg::kMaxMountpoints) return VMQG_E_LIMIT;
   for (const char* s : {"+", "#", "$share"}) intern(reinterpret_cast<const uint8_t*>(s), strlen(s), true);
   mplists.resize(cfg.max_mountpoints);
   rebuild();
@@ -340,15 +340,28 @@ void RetainEngine::erase(uint32_t mp, const uint32_t* w, uint32_t L) {
 }
 
 int RetainEngine::apply(const vmqr_op* ops, size_t n, const uint32_t* words, size_t nwords) {
+  uint32_t top_mp = 0;
   for (size_t i = 0; i < n; i++) {   // validate the whole batch first
     const vmqr_op& o = ops[i];
     if (o.kind != VMQR_OP_INSERT && o.kind != VMQR_OP_DELETE) return VMQG_E_INVAL;
-    if (o.mountpoint >= cfg.max_mountpoints) return VMQG_E_LIMIT;
+    if (o.mountpoint >= vmqg::kMaxMountpoints) return VMQG_E_LIMIT;
+    if (o.mountpoint >= top_mp) top_mp = o.mountpoint + 1;
     if (o.nwords == 0 || (uint64_t)o.word_off + o.nwords > nwords) return VMQG_E_INVAL;
     for (uint32_t j = 0; j < o.nwords; j++) if (words[o.word_off + j] >= word_text.size()) return VMQG_E_INVAL;
   }
+  // a retained topic on a mountpoint past the per-mountpoint lists grows
+  // them (doubling; vmq_retain_srv keys by {MP, Topic} with no limit,
+  // vmq_retain_srv.erl:53-66): a re-layout before any op touches the arena
+  if (top_mp > cfg.max_mountpoints) {
+    uint64_t m = cfg.max_mountpoints;
+    while (m < top_mp) m *= 2;
+    cfg.max_mountpoints = (uint32_t)std::min<uint64_t>(m, vmqg::kMaxMountpoints);
+    mplists.resize(cfg.max_mountpoints);
+    rebuild();
+  }
   // a capacity miss inside insert/erase sets full_image: the logical state
   // stays exact, touches stop, and the arena is laid out anew below
+  const bool grown = full_image;
   full_image = false;
   for (size_t i = 0; i < n; i++) {
     const vmqr_op& o = ops[i];
@@ -356,6 +369,7 @@ int RetainEngine::apply(const vmqr_op* ops, size_t n, const uint32_t* words, siz
     else erase(o.mountpoint, words + o.word_off, o.nwords);
   }
   if (full_image || lists_garbage > lay.lists_cap / 2) rebuild();
+  else if (grown) full_image = true;   // the re-layout above: the upload ships the image
   epoch++;
   return upload();
 }

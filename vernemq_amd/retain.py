@@ -79,12 +79,9 @@ class RetainGpuSrv:
         return out
 
     def _mp(self, mp: str, create: bool) -> int:
-        if create:
-            m = self.mountpoints.get(mp)
-            if m >= self.max_mountpoints:
-                raise _lib.VmqgError(_lib.E_LIMIT, "mountpoint")
-            return m
-        return self.mountpoints.ids.get(mp, self.max_mountpoints)
+        if create:   # a new mountpoint past the initial range grows the library's lists
+            return self.mountpoints.get(mp)
+        return self.mountpoints.ids.get(mp, _lib.NONE)   # unknown: holds nothing
 
     # ------------------------------------------------------------ deltas
     def apply_op_arrays(self, ops: np.ndarray, words: np.ndarray):
