@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define VMQG_ABI_VERSION 6
+#define VMQG_ABI_VERSION 7
 
 /* ---- status codes ---------------------------------------------------- */
 #define VMQG_OK 0
@@ -500,6 +500,24 @@ int vmqg_replica_sync_layout(vmqg_ctx* ctx, const uint8_t* layout);
  * (after every match already queued on the context; matches queued later, on
  * any stream, see them).  Asynchronous. */
 int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t bytes, void* stream);
+
+/* Replica side, one call per primary apply (ABI 7): brings the replica to the
+ * primary's committed tables — the primary's last patch list when the
+ * replica holds the epoch before it and that apply shipped patches, else the
+ * whole image from the primary's host mirror — on the replica's own stream,
+ * after the matches already queued on it.  The replica then reports the
+ * primary's epoch (vmqg_epoch), so its range results index the primary's
+ * record table of that epoch (vmqg_records_pin on the primary).  VMQG_E_STATE
+ * while the primary's stage is pending after a failed commit (the replica
+ * keeps its older tables; call again after the commit).  A device call on the
+ * replica that reads the primary's writer state: made by the primary's writer
+ * (after its commit, before its next stage).  Replaces, for contexts in one
+ * process, the RCCL image / patch broadcast of vernemq_amd/dist.py. */
+int vmqg_replica_follow(vmqg_ctx* replica, vmqg_ctx* primary);
+
+/* Digest of the device arena's bytes (a device call; tests compare a
+ * replica's with its primary's after every apply). */
+int vmqg_arena_digest(vmqg_ctx* ctx, uint64_t* digest);
 
 #ifdef __cplusplus
 }

@@ -562,6 +562,7 @@ struct vmqgb_req {
   int done, rc;
   size_t base;               /* first publish of the batch in its round */
   struct vmqgb_round* round;
+  struct vmqgb_lane* lane;   /* the context its rounds run on */
   vmqgb_req* next;
 };
 
@@ -575,54 +576,135 @@ typedef struct vmqgb_round {
   uint64_t epoch;
 } vmqgb_round;
 
-struct vmqgb_view {
+/* One device context of the view: lane 0 the primary (host engine + its
+ * device tables), lanes 1.. replicas that follow it (vmqg_replica_follow
+ * after every commit).  Each lane has its own device mutex, queue and
+ * rounds, so the lanes' device calls run side by side. */
+typedef struct vmqgb_lane {
   vmqg_ctx* ctx;
-  pthread_mutex_t wr;        /* writers: interning, applies (batchers never take it) */
-  pthread_mutex_t device;    /* the context's device side (submits, commits) */
-  pthread_mutex_t q_mu;      /* the queue, the rounds, the counters */
-  pthread_cond_t q_cv;
-  vmqgb_req* q_head;
+  pthread_mutex_t device;    /* the context's device side (submits, commits, follows) */
+  vmqgb_req* q_head;         /* under the view's q_mu */
   vmqgb_req* q_tail;
   int in_kernels;            /* rounds submitted whose offsets are not back */
-  int inflight;              /* ... at most this many */
+  int ok;                    /* a replica holding a committed epoch of the primary (atomic) */
+  int idx;
+  vmqgb_round rounds[VMQGB_ROUNDS];
+} vmqgb_lane;
+
+struct vmqgb_view {
+  vmqg_ctx* ctx;             /* the primary: dictionary, host engine, readers' record tables */
+  pthread_mutex_t wr;        /* writers: interning, applies (batchers never take it) */
+  pthread_mutex_t q_mu;      /* the queues, the rounds, the counters */
+  pthread_cond_t q_cv;
+  int inflight;              /* rounds in the kernels per lane, at most */
   int pipelined;             /* the context has a device: hbatch rounds */
   int device_records;
-  vmqgb_round rounds[VMQGB_ROUNDS];
+  int nlanes;
+  unsigned next_lane;        /* vmqgb_view_bind: round robin */
+  vmqgb_lane lanes[VMQGB_MAX_LANES];
   vmqgb_view_stats st;
 };
+
+static int lane_init(vmqgb_lane* l, vmqg_ctx* ctx, int idx) {
+  memset(l, 0, sizeof(*l));
+  l->ctx = ctx;
+  l->idx = idx;
+  if (pthread_mutex_init(&l->device, NULL)) return 0;
+  int all = 1;
+  for (int i = 0; i < VMQGB_ROUNDS; i++) {
+    l->rounds[i].hb = vmqg_hbatch_new(ctx);   /* NULL on a host-engine-only context */
+    if (!l->rounds[i].hb) all = 0;
+  }
+  return all ? 1 : -1;
+}
+
+static void lane_free(vmqgb_lane* l) {
+  for (int i = 0; i < VMQGB_ROUNDS; i++) vmqg_hbatch_free(l->rounds[i].hb);
+  pthread_mutex_destroy(&l->device);
+}
 
 vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx) {
   vmqgb_view* v = (vmqgb_view*)calloc(1, sizeof(*v));
   if (!v) return NULL;
   v->ctx = ctx;
   const int r1 = pthread_mutex_init(&v->wr, NULL);
-  const int r2 = pthread_mutex_init(&v->device, NULL);
   const int r3 = pthread_mutex_init(&v->q_mu, NULL);
   const int r4 = pthread_cond_init(&v->q_cv, NULL);
-  if (r1 || r2 || r3 || r4) { free(v); return NULL; }
-  v->pipelined = 1;
+  const int r2 = lane_init(&v->lanes[0], ctx, 0);
+  if (r1 || r3 || r4 || !r2) { free(v); return NULL; }
+  v->nlanes = 1;
+  v->lanes[0].ok = 1;
+  v->pipelined = r2 == 1;
   v->inflight = 2;
-  for (int i = 0; i < VMQGB_ROUNDS; i++) {
-    v->rounds[i].hb = vmqg_hbatch_new(ctx);   /* NULL on a host-engine-only context */
-    if (!v->rounds[i].hb) v->pipelined = 0;
-  }
   /* the readers' record buffers: records-mode expansion and range folds read
    * them while the writer stages the next apply */
   if (v->pipelined && vmqg_set_option(ctx, "reader_records", 1) != VMQG_OK) v->pipelined = 0;
   return v;
 }
 
+int vmqgb_view_add_replica(vmqgb_view* v, vmqg_ctx* replica) {
+  if (!v->pipelined || !replica) return VMQG_E_STATE;
+  if (v->nlanes >= VMQGB_MAX_LANES) return VMQG_E_LIMIT;
+  vmqgb_lane* l = &v->lanes[v->nlanes];
+  if (lane_init(l, replica, v->nlanes) != 1) { lane_free(l); return VMQG_E_NOMEM; }
+  vmqgb_view_write_begin(v);
+  pthread_mutex_lock(&l->device);
+  const int rc = vmqg_replica_follow(replica, v->ctx);   /* the primary's tables as committed now */
+  pthread_mutex_unlock(&l->device);
+  vmqgb_view_write_end(v);
+  if (rc) { lane_free(l); return rc; }
+  __atomic_store_n(&l->ok, 1, __ATOMIC_RELEASE);
+  pthread_mutex_lock(&v->q_mu);
+  v->nlanes++;
+  pthread_mutex_unlock(&v->q_mu);
+  return 0;
+}
+
+int vmqgb_view_lanes(vmqgb_view* v) { return v->nlanes; }
+
+void vmqgb_view_bind(vmqgb_view* v, vmqgb_batch* b) {
+  b->lane = __atomic_fetch_add(&v->next_lane, 1u, __ATOMIC_RELAXED) % (unsigned)v->nlanes;
+}
+
 void vmqgb_view_free(vmqgb_view* v) {
   if (!v) return;
-  for (int i = 0; i < VMQGB_ROUNDS; i++) vmqg_hbatch_free(v->rounds[i].hb);
+  for (int k = 0; k < v->nlanes; k++) lane_free(&v->lanes[k]);
   pthread_mutex_destroy(&v->wr);
-  pthread_mutex_destroy(&v->device);
   pthread_mutex_destroy(&v->q_mu);
   pthread_cond_destroy(&v->q_cv);
   free(v);
 }
 
 vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v) { return v->ctx; }
+
+/* After the primary's commit (writer mutex held): every replica brought to
+ * its tables.  A replica that fails keeps answering nothing (its batchers go
+ * to the primary) until a later follow succeeds. */
+static void follow_replicas(vmqgb_view* v) {
+  for (int k = 1; k < v->nlanes; k++) {
+    vmqgb_lane* l = &v->lanes[k];
+    const uint64_t t0 = mono_ns();
+    pthread_mutex_lock(&l->device);
+    const int rc = vmqg_replica_follow(l->ctx, v->ctx);
+    pthread_mutex_unlock(&l->device);
+    const uint64_t t1 = mono_ns();
+    __atomic_store_n(&l->ok, rc == 0, __ATOMIC_RELEASE);
+    pthread_mutex_lock(&v->q_mu);
+    v->st.follow_ns += t1 - t0;
+    if (rc) v->st.follow_failures++;
+    pthread_mutex_unlock(&v->q_mu);
+  }
+}
+
+int vmqgb_view_digests(vmqgb_view* v, uint64_t* out, int n) {
+  int rc = 0;
+  for (int k = 0; k < v->nlanes && k < n && !rc; k++) {
+    pthread_mutex_lock(&v->lanes[k].device);
+    rc = vmqg_arena_digest(v->lanes[k].ctx, &out[k]);
+    pthread_mutex_unlock(&v->lanes[k].device);
+  }
+  return rc;
+}
 void vmqgb_view_write_begin(vmqgb_view* v) { pthread_mutex_lock(&v->wr); }
 void vmqgb_view_write_end(vmqgb_view* v) { pthread_mutex_unlock(&v->wr); }
 
@@ -644,11 +726,12 @@ int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
   /* a failed commit leaves the stage pending (the library's contract): the
    * changes are kept and go out with the next commit, whatever its trigger */
   const uint64_t t1 = mono_ns();
-  pthread_mutex_lock(&v->device);
+  pthread_mutex_lock(&v->lanes[0].device);
   const uint64_t t2 = mono_ns();
   const int rc2 = vmqg_apply_commit(v->ctx, epoch);
-  pthread_mutex_unlock(&v->device);
+  pthread_mutex_unlock(&v->lanes[0].device);
   const uint64_t t3 = mono_ns();
+  if (!rc2 && v->nlanes > 1) follow_replicas(v);
   o->n = o->nwords = 0;
   pthread_mutex_lock(&v->q_mu);
   v->st.applies++;
@@ -664,18 +747,25 @@ int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
 
 int vmqgb_view_commit(vmqgb_view* v, uint64_t* epoch) {
   vmqgb_view_write_begin(v);
-  pthread_mutex_lock(&v->device);
+  pthread_mutex_lock(&v->lanes[0].device);
   const int rc = vmqg_apply_commit(v->ctx, epoch);
-  pthread_mutex_unlock(&v->device);
+  pthread_mutex_unlock(&v->lanes[0].device);
+  if (!rc && v->nlanes > 1) follow_replicas(v);
   vmqgb_view_write_end(v);
   return rc;
 }
 
 int vmqgb_view_set_option(vmqgb_view* v, const char* name, int64_t value) {
   vmqgb_view_write_begin(v);
-  pthread_mutex_lock(&v->device);
+  pthread_mutex_lock(&v->lanes[0].device);
   const int rc = vmqg_set_option(v->ctx, name, value);
-  pthread_mutex_unlock(&v->device);
+  pthread_mutex_unlock(&v->lanes[0].device);
+  /* kernel knobs on the replicas too (the primary-only ones they refuse) */
+  for (int k = 1; !rc && k < v->nlanes; k++) {
+    pthread_mutex_lock(&v->lanes[k].device);
+    vmqg_set_option(v->lanes[k].ctx, name, value);
+    pthread_mutex_unlock(&v->lanes[k].device);
+  }
   vmqgb_view_write_end(v);
   return rc;
 }
@@ -685,9 +775,9 @@ int vmqgb_view_ctx_stats(vmqgb_view* v, vmqg_stats_t* out) {
    * arena size, last-call counters) under the device mutex: the order an
    * apply takes them in */
   vmqgb_view_write_begin(v);
-  pthread_mutex_lock(&v->device);
+  pthread_mutex_lock(&v->lanes[0].device);
   const int rc = vmqg_stats(v->ctx, out);
-  pthread_mutex_unlock(&v->device);
+  pthread_mutex_unlock(&v->lanes[0].device);
   vmqgb_view_write_end(v);
   return rc;
 }
@@ -743,7 +833,7 @@ void vmqgb_view_release(vmqgb_view* v, vmqgb_batch* b) {
 /* A combiner's round: the taken batches' publishes and words concatenated
  * into the hbatch's pinned inputs, one submit under the device mutex, the
  * offsets (the next round may start then), the entries, the hand-out. */
-static void run_round(vmqgb_view* v, vmqgb_round* r, vmqgb_req* list) {
+static void run_round(vmqgb_view* v, vmqgb_lane* lane, vmqgb_round* r, vmqgb_req* list) {
   size_t n = 0, nw = 0;
   for (vmqgb_req* q = list; q; q = q->next) { q->base = n; n += q->b->n; nw += q->b->nwords; }
   vmqg_pub* P = NULL;
@@ -765,9 +855,9 @@ static void run_round(vmqgb_view* v, vmqgb_round* r, vmqgb_req* list) {
   const uint64_t* offs = NULL;
   uint64_t total = 0, epoch = 0;
   for (int attempt = 0; !rc; attempt++) {
-    pthread_mutex_lock(&v->device);
-    rc = vmqg_hbatch_submit(v->ctx, r->hb, n, nw, r->dev_ranges);
-    pthread_mutex_unlock(&v->device);
+    pthread_mutex_lock(&lane->device);
+    rc = vmqg_hbatch_submit(lane->ctx, r->hb, n, nw, r->dev_ranges);
+    pthread_mutex_unlock(&lane->device);
     if (rc) break;
     rc = vmqg_hbatch_offsets(r->hb, &offs, &total, &epoch);
     if ((rc == VMQG_E_OVERFLOW || rc == VMQG_E_FRONTIER) && attempt < 8) {   /* larger output / stack: again */
@@ -780,7 +870,7 @@ static void run_round(vmqgb_view* v, vmqgb_round* r, vmqgb_req* list) {
     break;
   }
   pthread_mutex_lock(&v->q_mu);
-  v->in_kernels--;
+  lane->in_kernels--;
   pthread_cond_broadcast(&v->q_cv);
   pthread_mutex_unlock(&v->q_mu);
   const void* out = NULL;
@@ -790,6 +880,7 @@ static void run_round(vmqgb_view* v, vmqgb_round* r, vmqgb_req* list) {
   r->epoch = epoch;
   pthread_mutex_lock(&v->q_mu);
   v->st.rounds++;
+  v->st.lane_rounds[lane->idx]++;
   v->st.round_publishes += n;
   if (n > v->st.max_round_publishes) v->st.max_round_publishes = n;
   r->refs = 0;
@@ -810,19 +901,20 @@ static void run_round(vmqgb_view* v, vmqgb_round* r, vmqgb_req* list) {
  * v->inflight rounds are in the kernels and a round is free: it takes the
  * queued batches of the head's device mode, up to VMQGB_ROUND_MAX publishes. */
 static void combine(vmqgb_view* v, vmqgb_req* req) {
+  vmqgb_lane* lane = req->lane;
   pthread_mutex_lock(&v->q_mu);
   req->done = 0;
   req->next = NULL;
-  if (v->q_tail) v->q_tail->next = req; else v->q_head = req;
-  v->q_tail = req;
+  if (lane->q_tail) lane->q_tail->next = req; else lane->q_head = req;
+  lane->q_tail = req;
   while (!req->done) {
     vmqgb_round* r = NULL;
-    if (v->q_head && v->in_kernels < v->inflight)
-      for (int i = 0; i < VMQGB_ROUNDS && !r; i++) if (!v->rounds[i].busy) r = &v->rounds[i];
+    if (lane->q_head && lane->in_kernels < v->inflight)
+      for (int i = 0; i < VMQGB_ROUNDS && !r; i++) if (!lane->rounds[i].busy) r = &lane->rounds[i];
     if (!r) { pthread_cond_wait(&v->q_cv, &v->q_mu); continue; }
     /* take the head's mode, FIFO, up to the round's publish budget */
-    const int mode = v->q_head->dev_ranges;
-    vmqgb_req *list = NULL, *tail = NULL, **pp = &v->q_head, *last = NULL;
+    const int mode = lane->q_head->dev_ranges;
+    vmqgb_req *list = NULL, *tail = NULL, **pp = &lane->q_head, *last = NULL;
     size_t n = 0;
     while (*pp) {
       vmqgb_req* q = *pp;
@@ -837,12 +929,12 @@ static void combine(vmqgb_view* v, vmqgb_req* req) {
         pp = &q->next;
       }
     }
-    v->q_tail = last;
+    lane->q_tail = last;
     r->busy = 1;
     r->dev_ranges = mode;
-    v->in_kernels++;
+    lane->in_kernels++;
     pthread_mutex_unlock(&v->q_mu);
-    run_round(v, r, list);
+    run_round(v, lane, r, list);
     pthread_mutex_lock(&v->q_mu);
   }
   pthread_mutex_unlock(&v->q_mu);
@@ -908,9 +1000,9 @@ static int match_records(vmqgb_view* v, vmqgb_batch* b, vmqgb_req* qp, int dev_r
 
 static int match_direct(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
   (void)recs; (void)nrecs;
-  pthread_mutex_lock(&v->device);
+  pthread_mutex_lock(&v->lanes[0].device);
   const int rc = ranges ? vmqgb_match_ranges(b, v->ctx) : vmqgb_match(b, v->ctx);
-  pthread_mutex_unlock(&v->device);
+  pthread_mutex_unlock(&v->lanes[0].device);
   return rc ? rc : VMQG_E_DEVICE;
 }
 
@@ -929,6 +1021,11 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
   vmqgb_req q;
   memset(&q, 0, sizeof q);
   q.b = b;
+  /* the batch's lane, unless that replica is not following (then the primary's) */
+  {
+    const unsigned k = b->lane < (unsigned)v->nlanes ? b->lane : 0u;
+    q.lane = &v->lanes[k && __atomic_load_n(&v->lanes[k].ok, __ATOMIC_ACQUIRE) ? k : 0];
+  }
   if (ranges) {
     /* the round's entries stay in its buffers and the record table of its
      * epoch stays pinned until the caller has folded (vmqgb_view_release) */

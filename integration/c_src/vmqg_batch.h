@@ -89,6 +89,7 @@ typedef struct vmqgb_batch {
   uint32_t rec_pin;     /* range mode: the record table pinned for the fold (vmqg_records_pin) */
   int rec_pinned;
   uint32_t stale_rematches;   /* matches repeated because a publish's unknown word became known */
+  unsigned lane;        /* the view context its matches go to (vmqgb_view_bind; 0: the primary) */
   int out_ranges;       /* set by vmqgb_view_match: 1 the results are ranges, 0 records (a
                            ranges request falls back to records when applies keep rewriting
                            the record slots its rounds index) */
@@ -187,7 +188,26 @@ int vmqgb_ops_apply(vmqgb_ops* o, vmqg_ctx* ctx, uint64_t* epoch);
 typedef struct vmqgb_view vmqgb_view;
 
 vmqgb_view* vmqgb_view_new(vmqg_ctx* ctx);
-void vmqgb_view_free(vmqgb_view* v);   /* does not destroy the context */
+void vmqgb_view_free(vmqgb_view* v);   /* does not destroy the contexts */
+/* Multi-GPU (the trie replicated, publish batches spread over
+ * the GPUs): a replica context (VMQG_CFG_REPLICA, any device) becomes one
+ * more lane of the view.  It follows the primary after every commit
+ * (vmqg_replica_follow: the commit's patches, or the whole image) under the
+ * writer mutex, and batches bound to it (vmqgb_view_bind) are matched on it
+ * — their rounds run beside the other lanes', each lane with its own device
+ * mutex, queue and rounds; ranges index the primary's record table of the
+ * same epoch.  Call before batchers start.  VMQG_E_STATE on a view without a
+ * device, VMQG_E_LIMIT past VMQGB_MAX_LANES. */
+int vmqgb_view_add_replica(vmqgb_view* v, vmqg_ctx* replica);
+int vmqgb_view_lanes(vmqgb_view* v);
+/* A batcher's batch bound to a lane, round robin over the lanes (the NIF
+ * binds each batcher's batch once: one batcher per scheduler, so scheduler
+ * k's publishes go to context k mod N). */
+void vmqgb_view_bind(vmqgb_view* v, vmqgb_batch* b);
+/* Device-arena digests of the lanes (out[k], k < n): tests check that every
+ * replica's tables are the primary's byte for byte.  Takes each lane's
+ * device mutex; call with the writer mutex held (between applies). */
+int vmqgb_view_digests(vmqgb_view* v, uint64_t* out, int n);
 vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v);
 /* A batcher's sequence: vmqgb_batch_add* for its publishes, vmqgb_view_match,
  * the fold, vmqgb_view_release.  Any number of batchers at once, no lock
@@ -207,6 +227,7 @@ vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v);
  * to what the device would have copied; if two applies have rewritten record
  * slots since, the batch is matched again with device-side records). */
 #define VMQGB_ROUNDS 6
+#define VMQGB_MAX_LANES 16   /* device contexts of one view: the primary + replicas */
 #define VMQGB_ROUND_MAX (1u << 17)   /* publishes per combined round */
 /* The batch's results (offsets + out in records mode, offsets + rng in range
  * mode) — every publish's answer from the tables of one epoch, b->epoch —
@@ -243,6 +264,8 @@ typedef struct vmqgb_view_stats {
   uint64_t rounds, round_publishes, round_batches, max_round_publishes;
   uint64_t expanded_batches, device_record_batches, state_retries, stale_rematches;
   uint64_t overflow_retries, ranges_fallbacks;
+  uint64_t lane_rounds[VMQGB_MAX_LANES];   /* rounds per device context */
+  uint64_t follow_ns, follow_failures;      /* replicas brought to each commit */
   /* the writer's applies (vmqgb_view_apply_ops): host stage, wait for the
    * device mutex, commit — sums and maxima, ns */
   uint64_t applies, stage_ns, stage_max_ns, dev_wait_ns, dev_wait_max_ns, commit_ns, commit_max_ns;

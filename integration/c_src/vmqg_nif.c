@@ -59,7 +59,9 @@ typedef struct {
 } term_store;
 
 typedef struct {
-  vmqg_ctx* ctx;
+  vmqg_ctx* ctx;                  /* the primary (host engine + its device tables) */
+  vmqg_ctx* replicas[VMQGB_MAX_LANES];   /* devices => [D0, D1, ...]: replicas on D1, ... */
+  int nreplicas;
   vmqgb_view* view;               /* batchers (readers) vs. table changes (writers) */
   ErlNifMutex* mp_mu;             /* the mountpoint interner: batchers look up, writers add */
   vmqgb_interner *mps, *nodes, *subs, *infos;
@@ -149,13 +151,15 @@ static ERL_NIF_TERM error_term(ErlNifEnv* env, int rc) {
 static void res_dtor(ErlNifEnv* env, void* obj) {
   (void)env;
   vmqg_res* r = (vmqg_res*)obj;
+  vmqgb_view_free(r->view);   /* its rounds, before the contexts they ran on */
+  r->view = NULL;
+  for (int k = 0; k < r->nreplicas; k++) vmqg_destroy(r->replicas[k]);
   if (r->ctx) vmqg_destroy(r->ctx);
   vmqgb_interner_free(r->mps); vmqgb_interner_free(r->nodes);
   vmqgb_interner_free(r->subs); vmqgb_interner_free(r->infos);
   term_store* ts[4] = {&r->node_t, &r->sub_t, &r->info_t, &r->group_t};
   for (int i = 0; i < 4; i++) store_free(ts[i]);
   vmqgb_ops_free(&r->ops);
-  vmqgb_view_free(r->view);
   if (r->mp_mu) enif_mutex_destroy(r->mp_mu);
 }
 
@@ -172,8 +176,11 @@ static vmqg_res* get_res(ErlNifEnv* env, ERL_NIF_TERM t) {
 }
 
 /* ------------------------------------------------------------- create/1 */
-/* create(#{device => D, local_node => node()}) -> {ok, Ctx} | {error, _}
- * (vmq_reg_trie:init/1, vmq_reg_trie.erl:135-151) */
+/* create(#{device => D, local_node => node()[, devices => [D0, D1, ...]]})
+ * -> {ok, Ctx} | {error, _} (vmq_reg_trie:init/1, vmq_reg_trie.erl:135-151).
+ * devices: the primary on D0 and a replica of its tables on each further
+ * device (the same device may repeat); the view spreads the batchers over
+ * them (the trie replicated, publish batches sharded). */
 static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   (void)argc;
   ERL_NIF_TERM v;
@@ -202,9 +209,29 @@ static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   cfg.max_nodes = VMQG_MAX_NODES;
   cfg.max_mountpoints = 1024;   /* the initial root range: more mountpoints grow it (no limit below
                                    VMQG_MAX_MOUNTPOINTS, as vmq_reg_trie has none) */
+  int devs[VMQGB_MAX_LANES], ndev = 0;
+  ERL_NIF_TERM dl;
+  if (enif_get_map_value(env, argv[0], enif_make_atom(env, "devices"), &dl)) {
+    ERL_NIF_TERM h, t = dl;
+    while (enif_get_list_cell(env, t, &h, &t)) {
+      if (ndev == VMQGB_MAX_LANES || !enif_get_int(env, h, &devs[ndev])) { enif_release_resource(r); return enif_make_badarg(env); }
+      ndev++;
+    }
+    if (ndev) cfg.device = devs[0];
+  }
   int err = 0;
   r->ctx = vmqg_create(&cfg, &err);
   if (r->ctx && !(r->view = vmqgb_view_new(r->ctx))) err = VMQG_E_NOMEM;
+  for (int k = 1; r->view && !err && k < ndev; k++) {
+    vmqg_config rc = cfg;
+    rc.device = devs[k];
+    rc.flags = VMQG_CFG_REPLICA;
+    vmqg_ctx* x = vmqg_create(&rc, &err);
+    if (!x) break;
+    r->replicas[r->nreplicas++] = x;
+    err = vmqgb_view_add_replica(r->view, x);
+  }
+  if (err && r->ctx) { vmqgb_view_free(r->view); r->view = NULL; }
   ERL_NIF_TERM ret = r->ctx && r->view ? enif_make_tuple2(env, a_ok, enif_make_resource(env, r)) : error_term(env, err);
   enif_release_resource(r);
   return ret;
@@ -414,6 +441,7 @@ static ERL_NIF_TERM nif_batch_new(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
   vmqg_bres* br = (vmqg_bres*)enif_alloc_resource(BRES, sizeof(vmqg_bres));
   memset(br, 0, sizeof(*br));
   if (vmqgb_batch_init(&br->b, 4096)) { enif_release_resource(br); return error_term(env, VMQG_E_NOMEM); }
+  vmqgb_view_bind(r->view, &br->b);   /* batcher k's publishes go to device context k mod N */
   enif_keep_resource(r);
   br->owner = r;
   ERL_NIF_TERM t = enif_make_resource(env, br);

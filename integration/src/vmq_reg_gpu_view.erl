@@ -208,7 +208,11 @@ stats() ->
 %%%===================================================================
 init([]) ->
     Device = application:get_env(vmq_server, gpu_reg_view_device, 0),
-    {ok, Ctx} = vmqg_nif:create(#{device => Device, local_node => node()}),
+    %% gpu_reg_view_devices = [D0, D1, ...]: the tables on D0 and a replica of
+    %% them on each further GPU (SURVEY §8e); scheduler k's batcher matches
+    %% on device k mod N (vmqgb_view_bind in the NIF's batch_new/1)
+    Devices = application:get_env(vmq_server, gpu_reg_view_devices, [Device]),
+    {ok, Ctx} = vmqg_nif:create(#{device => hd(Devices), devices => Devices, local_node => node()}),
     %% kernel knobs (include/vmqg.h vmqg_set_option), [{Name, Value}]
     lists:foreach(fun({Name, Value}) ->
                           case vmqg_nif:set_option(Ctx, Name, Value) of

@@ -44,6 +44,14 @@
  *                                         then "v <rounds> <stale rematches>
  *                                         <batches>"; the groups are then
  *                                         forgotten (the next X opens anew)
+ *   R <n>                                 adds n replica contexts on device 0
+ *                                         as lanes of the view (vmqgb_view_add_replica;
+ *                                         batchers are bound round robin); after
+ *                                         every apply the lanes' arena digests
+ *                                         are compared (the last line of <out>:
+ *                                         "H <applies checked> <mismatches>"),
+ *                                         and each "v" line ends with the rounds
+ *                                         per lane
  * group is the $share group's text ("-" for none).
  * Exit 0 after writing everything; non-zero with a message otherwise. */
 #define _GNU_SOURCE
@@ -62,6 +70,19 @@ static pub_t* pubs;
 static size_t npubs, pcap;
 static char** gname;     /* group text by word id */
 static size_t gcap;
+static vmqg_ctx* replicas[VMQGB_MAX_LANES];
+static int nreplicas;
+static uint64_t digests_checked, digests_mismatched;
+
+/* with replicas: every lane's arena digest equals the primary's (writer mutex held) */
+static void check_digests(void) {
+  if (!nreplicas) return;
+  uint64_t d[VMQGB_MAX_LANES];
+  const int n = vmqgb_view_lanes(view);
+  digests_checked++;
+  if (vmqgb_view_digests(view, d, n)) { digests_mismatched++; return; }
+  for (int k = 1; k < n; k++) if (d[k] != d[0]) { digests_mismatched++; return; }
+}
 
 typedef struct { char* buf; size_t n, cap; } sbuf;
 
@@ -141,6 +162,7 @@ static void* batcher(void* p) {
   bt_t* a = (bt_t*)p;
   vmqgb_batch b;
   if (vmqgb_batch_init(&b, a->B)) { a->err = VMQG_E_NOMEM; return NULL; }
+  vmqgb_view_bind(view, &b);   /* as the NIF's batch_new: batcher k on lane k mod N */
   long* idx = (long*)malloc(a->B * sizeof(long));
   for (int pass = 0; !a->err; pass++) {
     if (a->wout ? (pass >= a->passes && writer_done) : pass >= 1) break;
@@ -168,6 +190,7 @@ static void* churner(void* p) {   /* a writer: S/U pairs nobody's publishes matc
     vmqgb_view_write_begin(view);
     int rc = vmqgb_ops_add_filter(&ops, ctx, kind, 0, (const uint8_t*)f, (size_t)l, 0, 900000 + (uint32_t)(r % 97), 0);
     if (!rc) rc = vmqgb_view_apply_ops(view, &ops, NULL);
+    if (!rc) check_digests();
     vmqgb_view_write_end(view);
     if (rc) c->err = rc;
   }
@@ -234,6 +257,7 @@ static void* group_writer(void* p) {
     for (char** l = groups[k]; *l && !w->err; l++)
       if (add_change_line(&ops, *l + 2, (*l)[0] == 'S' ? VMQG_OP_ADD : VMQG_OP_DEL)) w->err = VMQG_E_INVAL;
     if (!w->err) w->err = vmqgb_view_apply_ops(view, &ops, &w->epochs[k]);
+    if (!w->err) check_digests();
     vmqgb_ops_reset(&ops);
     vmqgb_view_write_end(view);
   }
@@ -317,8 +341,21 @@ int main(int argc, char** argv) {
       g[k] = strdup(line + 2);
       g[k + 1] = NULL;
       groups[ngroups - 1] = g;
+    } else if (line[0] == 'R') {
+      int n = 0;
+      if (sscanf(line + 2, "%d", &n) != 1 || n < 1 || n >= VMQGB_MAX_LANES) return 12;
+      for (int k = 0; k < n; k++) {
+        vmqg_config rc = cfg;
+        rc.flags = VMQG_CFG_REPLICA;
+        vmqg_ctx* x = vmqg_create(&rc, &err);
+        if (!x || (err = vmqgb_view_add_replica(view, x))) { fprintf(stderr, "replica: %d\n", err); return 13; }
+        replicas[nreplicas++] = x;
+      }
     } else if (line[0] == 'A') {
-      const int rc = vmqgb_view_apply(view, &ops, NULL);
+      vmqgb_view_write_begin(view);
+      const int rc = vmqgb_view_apply_ops(view, &ops, NULL);
+      if (!rc) check_digests();
+      vmqgb_view_write_end(view);
       if (rc) { fprintf(stderr, "apply: %d\n", rc); return 7; }
     } else if (line[0] == 'P') {
       unsigned mp;
@@ -339,9 +376,12 @@ int main(int argc, char** argv) {
       const int rc = run_w(out, strcmp(mode, "ranges") == 0, T, B, passes);
       if (rc) { fprintf(stderr, "W: %d\n", rc); return 11; }
       vmqgb_view_get_stats(view, &s1);
-      fprintf(out, "v %llu %llu %llu\n", (unsigned long long)(s1.rounds - s0.rounds),
+      fprintf(out, "v %llu %llu %llu", (unsigned long long)(s1.rounds - s0.rounds),
               (unsigned long long)(s1.stale_rematches - s0.stale_rematches),
               (unsigned long long)(s1.round_batches - s0.round_batches));
+      for (int k = 0; k < vmqgb_view_lanes(view); k++)
+        fprintf(out, " %llu", (unsigned long long)(s1.lane_rounds[k] - s0.lane_rounds[k]));
+      fputc('\n', out);
       for (size_t k = 0; k < ngroups; k++) { for (char** l = groups[k]; *l; l++) free(*l); free(groups[k]); }
       ngroups = 0;
       group_open = 0;
@@ -354,8 +394,10 @@ int main(int argc, char** argv) {
       if (rc) { fprintf(stderr, "match: %d\n", rc); return 10; }
     }
   }
+  if (nreplicas) fprintf(out, "H %llu %llu\n", (unsigned long long)digests_checked, (unsigned long long)digests_mismatched);
   fclose(out);
   vmqgb_view_free(view);
+  for (int k = 0; k < nreplicas; k++) vmqg_destroy(replicas[k]);
   vmqg_destroy(ctx);
   return 0;
 }

@@ -7,7 +7,7 @@
  * printed FoldFun entries with the oracle.
  *
  * usage: nif_mock_check <script> <out>; script lines:
- *   N <device>                          create(#{device => D, local_node => 'n0@h'})
+ *   N <device> [<lanes>]                create(#{device => D, local_node => 'n0@h'[, devices => [D x lanes]]})
  *   I <node> <mp> <client> <qos> <filter>   add_init(Ctx, MP, Topic, {MP, Client}, QoS, Node)
  *   F                                   flush_init(Ctx)
  *   V <mp> <client>                     opens an event of SubscriberId {MP, Client}
@@ -165,10 +165,13 @@ int main(int argc, char** argv) {
     char a1[64], a2[256], a3[64], topic[4096];
     int d, node, qos;
     if (line[0] == 'N') {
-      sscanf(line + 2, "%d", &d);
-      ERL_NIF_TERM k[2] = {enif_make_atom(env, "device"), enif_make_atom(env, "local_node")};
-      ERL_NIF_TERM v[2] = {mock_make_int(d), node_term(0)};
-      const ERL_NIF_TERM arg = mock_make_map(2, k, v);
+      int lanes = 1;
+      sscanf(line + 2, "%d %d", &d, &lanes);
+      ERL_NIF_TERM dev[16];
+      for (int i = 0; i < lanes && i < 16; i++) dev[i] = mock_make_int(d);
+      ERL_NIF_TERM k[3] = {enif_make_atom(env, "device"), enif_make_atom(env, "local_node"), enif_make_atom(env, "devices")};
+      ERL_NIF_TERM v[3] = {mock_make_int(d), node_term(0), enif_make_list_from_array(env, dev, (unsigned)(lanes < 16 ? lanes : 16))};
+      const ERL_NIF_TERM arg = mock_make_map(lanes > 1 ? 3 : 2, k, v);
       const ERL_NIF_TERM r = call("create", 1, &arg);
       int ar;
       const ERL_NIF_TERM* el;
@@ -179,7 +182,8 @@ int main(int argc, char** argv) {
         return 4;
       }
       ctx = el[1];
-      const ERL_NIF_TERM rb = call("batch_new", 1, &ctx);
+      ERL_NIF_TERM rb = call("batch_new", 1, &ctx);
+      if (lanes > 1) rb = call("batch_new", 1, &ctx);   /* batches are bound round robin: this one to lane 1 */
       enif_get_tuple(env, rb, &ar, &el);
       batch = el[1];
     } else if (line[0] == 'I') {

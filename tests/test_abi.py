@@ -32,7 +32,7 @@ def test_every_declared_symbol_is_exported():
     assert not missing, missing
     bound = {name for name, _, _ in _lib.SIGNATURES}
     assert set(decl) == bound, set(decl) ^ bound
-    assert L.vmqg_abi_version() == 6
+    assert L.vmqg_abi_version() == 7
 
 
 def test_struct_layouts_match_header(tmp_path):

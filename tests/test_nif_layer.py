@@ -248,7 +248,8 @@ def _churn_script(seed=23, n_subs=2000, n_pubs=2000, n_groups=30):
 
 
 @pytest.mark.gpu
-def test_batchers_while_a_writer_changes_the_answers(tmp_path):
+@pytest.mark.parametrize("replicas", [0, 1])
+def test_batchers_while_a_writer_changes_the_answers(tmp_path, replicas):
     """Verdict r3 next-round item 1: batchers of 600 publishes match over and
     over while a writer applies 30 groups of subscribes / unsubscribes that
     change what the publishes match — some bringing words that publishes
@@ -257,11 +258,17 @@ def test_batchers_while_a_writer_changes_the_answers(tmp_path):
     tables (the stage re-lays the host mirror out while rounds run on the
     old device tables).  Every matched publish's entries must equal the
     oracle's at the epoch its batch reports (the combined round's epoch);
-    both device-side modes."""
+    both device-side modes.  replicas=1: the view has a second device
+    context (a replica on the same GPU) that follows every
+    commit — patches, and the whole image after the re-layout — and half the
+    batchers match on it: the same parity on both lanes, and after every
+    apply the replica's arena digest equals the primary's."""
     from oracle import oracle as O
     exe = os.path.join(ROOT, "tools", "bin", "batch_gpu_check")
     assert os.path.exists(exe), "tools/bin/batch_gpu_check not built (__graft_entry__.build())"
     script, nodes, node_ids, pubs, init_events, runs = _churn_script()
+    if replicas:
+        script = "R %d\n" % replicas + script
     (tmp_path / "s.txt").write_text(script)
     r = subprocess.run([exe, str(tmp_path / "s.txt"), str(tmp_path / "o.txt")], capture_output=True, text=True,
                        timeout=600)
@@ -281,6 +288,7 @@ def test_batchers_while_a_writer_changes_the_answers(tmp_path):
         body = text[pos + 1 + ng: pos + 1 + ng + nl]
         stats = text[pos + 1 + ng + nl].split()
         assert stats[0] == "v" and int(stats[1]) > 0
+        assert len(stats) == 5 + replicas and all(int(x) > 0 for x in stats[4:]), stats   # every lane matched
         pos += 2 + ng + nl
         by_state = {}
         for ln in body:
@@ -313,6 +321,9 @@ def test_batchers_while_a_writer_changes_the_answers(tmp_path):
             for i, got in by_state.get(j, []):
                 assert got == want[i], (j, i, pubs[i], got[:4], want[i][:4])
         assert changed > 0   # the writer's groups did change answers
+    if replicas:
+        h = text[-1].split()
+        assert h[0] == "H" and int(h[1]) >= 1 + sum(len(g) for g in runs) and int(h[2]) == 0, h
 
 
 def _build_nif_check(tmp_path):
@@ -416,9 +427,11 @@ def _nif_glue_script(device, seed=5, n_subs=1500, n_pubs=1200):
     return "\n".join(lines) + "\n", node_names, node_ids, events, oracle_groups
 
 
-def _run_nif_check(tmp_path, device):
+def _run_nif_check(tmp_path, device, lanes=1):
     exe = _build_nif_check(tmp_path)
     script, node_names, node_ids, events, groups = _nif_glue_script(device)
+    if lanes > 1:
+        script = script.replace("N %d\n" % device, "N %d %d\n" % (device, lanes), 1)
     (tmp_path / "n.txt").write_text(script)
     r = subprocess.run([str(exe), str(tmp_path / "n.txt"), str(tmp_path / "o.txt")], capture_output=True, text=True,
                        timeout=300)
@@ -454,14 +467,17 @@ def test_nif_glue_runs_over_the_erl_nif_double(tmp_path):
 
 
 @pytest.mark.gpu
-def test_nif_glue_matches_the_oracle_on_the_gpu(tmp_path):
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_nif_glue_matches_the_oracle_on_the_gpu(tmp_path, lanes):
     """The same NIF calls on the GPU: after the initial load and the
     coalesced / single event applies, match/4 (records and ranges) returns,
     per publish, the FoldFun entries the oracle's fold/4 gives — built as
     Erlang terms by the glue ({SubscriberId, SubInfo}, {Node, Group,
-    SubscriberId, SubInfo}, Node) and read back from the terms."""
+    SubscriberId, SubInfo}, Node) and read back from the terms.  lanes=2:
+    create/1 with devices => [0, 0] (a replica context beside the primary;
+    the check's batch is bound to the replica's lane)."""
     from oracle import oracle as O
-    script, out, node_names, node_ids, events, groups = _run_nif_check(tmp_path, 0)
+    script, out, node_names, node_ids, events, groups = _run_nif_check(tmp_path, 0, lanes)
     name = {"n%d@h" % nid: node_names[i] for i, nid in enumerate(node_ids)}
     orc = O.TrieOracle(node_names[0])
     orc.apply(events)

@@ -29,7 +29,8 @@
  *            subscriptions as vmqg_nif:add_init does (the writer mutex, an
  *            apply every 65,536) while 16 batchers run
  * Prints one JSON line per configuration.  Needs a GPU.  argv[1]: seconds
- * per configuration (default 3).
+ * per configuration (default 3).  VMQGB_REPLICAS=n adds n replica contexts
+ * on device 0 as lanes of the view (batchers spread over them).
  *
  * build: see tools/Makefile (gcc -O2 -pthread ... integration/c_src/vmqg_batch.c -l:libvmqgpu.so)
  */
@@ -102,6 +103,7 @@ static void* batcher(void* p) {
   bt_t* a = (bt_t*)p;
   vmqgb_batch b;
   vmqgb_batch_init(&b, a->B);
+  vmqgb_view_bind(view, &b);   /* batcher k on device context k mod N, as the NIF's batch_new */
   long* idx = (long*)malloc(a->B * sizeof(long));
   uint64_t acc[2] = {0, 0};
   size_t lo = ((size_t)a->tid * a->B * 7919) % NPUB;
@@ -366,6 +368,11 @@ static int run(const char* section, int T, size_t B, int ranges, double secs, ch
   if (ld)
     printf(", \"load\": {\"subscriptions_added_per_s\": %.4g, \"applies\": %llu, \"max_write_lock_wait_ms\": %.3f}",
            ld->added / el, (unsigned long long)ld->applies, ld->wait_max * 1e3);
+  printf(", \"lanes\": %d, \"lane_rounds\": [", vmqgb_view_lanes(view));
+  for (int k = 0; k < vmqgb_view_lanes(view); k++)
+    printf("%s%llu", k ? ", " : "", (unsigned long long)(s1.lane_rounds[k] - s0.lane_rounds[k]));
+  printf("], \"follow_ms_mean\": %.3f, \"follow_failures\": %llu",
+         s1.applies ? s1.follow_ns * 1e-6 / s1.applies : 0.0, (unsigned long long)s1.follow_failures);
   printf(", \"rebuilds\": %llu, \"cpu_throttled\": {\"periods\": %llu, \"ms\": %.1f}, \"build\": \"%s\"}\n",
          (unsigned long long)(e1.rebuilds - e0.rebuilds), (unsigned long long)(thr1 - thr0), (thu1 - thu0) * 1e-3,
          vmqg_build_id());
@@ -408,6 +415,15 @@ int main(int argc, char** argv) {
     vmqgb_view_write_end(view);
   }
   const double load_s = now() - t0;
+  /* VMQGB_REPLICAS=n: n replica contexts on device 0 as more lanes of the
+   * view (the multi-GPU drop-in, rehearsed on one GPU) */
+  const int nrep = getenv("VMQGB_REPLICAS") ? atoi(getenv("VMQGB_REPLICAS")) : 0;
+  for (int k = 0; k < nrep; k++) {
+    vmqg_config rc = cfg;
+    rc.flags = VMQG_CFG_REPLICA;
+    vmqg_ctx* x = vmqg_create(&rc, &err);
+    if (!x || (err = vmqgb_view_add_replica(view, x))) { fprintf(stderr, "replica: %d\n", err); return 1; }
+  }
   /* raw publish topics */
   topics = (char*)calloc(NPUB, 40);
   tlen = (size_t*)calloc(NPUB, sizeof(size_t));

@@ -127,6 +127,8 @@ _P = ctypes.c_void_p
 _U32, _U64, _SZ = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 SIGNATURES = [
     ("vmqg_abi_version", ctypes.c_int, []),
+    ("vmqg_replica_follow", ctypes.c_int, [_P, _P]),
+    ("vmqg_arena_digest", ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
     ("vmqg_build_id", ctypes.c_char_p, []),
     ("vmqg_create", _P, [ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_int)]),
     ("vmqg_destroy", None, [_P]),

@@ -808,6 +808,20 @@ int vmqg_replica_sync_layout(vmqg_ctx* ctx, const uint8_t* layout) {
   return VMQG_OK;
 }
 
+int vmqg_replica_follow(vmqg_ctx* replica, vmqg_ctx* primary) {
+  if (!replica || !primary) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  return replica->e.follow(primary->e);
+  GUARD_END
+}
+
+int vmqg_arena_digest(vmqg_ctx* ctx, uint64_t* digest) {
+  if (!ctx || !digest) return VMQG_E_INVAL;
+  GUARD_BEGIN
+  return ctx->e.arena_digest(digest);
+  GUARD_END
+}
+
 int vmqg_apply_patches_device(vmqg_ctx* ctx, const void* d_patches, uint64_t bytes, void* stream) {
   if (!ctx || (bytes && !d_patches) || bytes % sizeof(vmqg::Patch)) return VMQG_E_INVAL;
   Engine& e = ctx->e;

@@ -1116,7 +1116,14 @@ int Engine::upload() {
     std::fill(dirty_bits.begin(), dirty_bits.end(), 0);
     return VMQG_OK;
   }
-  const uint64_t np = last_patches.size();
+  return ship_patches(last_patches);
+}
+
+// A patch list through the staging ring onto the context stream (after
+// everything queued before it): the primary's own applies, and a replica
+// following its primary (vmqg_replica_follow).
+int Engine::ship_patches(const std::vector<Patch>& pl) {
+  const uint64_t np = pl.size();
   if (np == 0) return VMQG_OK;
   Stage& sg = stage[stage_next];
   stage_next = (stage_next + 1) % kStage;
@@ -1135,12 +1142,69 @@ int Engine::upload() {
     if (hipMalloc(&sg.d, cap * sizeof(Patch)) != hipSuccess) return VMQG_E_NOMEM;
     sg.cap = cap;
   }
-  memcpy(sg.h, last_patches.data(), np * sizeof(Patch));
+  memcpy(sg.h, pl.data(), np * sizeof(Patch));
   if (hipMemcpyAsync(sg.d, sg.h, np * sizeof(Patch), hipMemcpyHostToDevice, stream) != hipSuccess)
     return VMQG_E_DEVICE;
   if (launch_patches(d_arena, sg.d, np, stream) != hipSuccess) return VMQG_E_DEVICE;
   if (hipEventRecord(sg.ev, stream) != hipSuccess) return VMQG_E_DEVICE;
   sg.used = true;
+  return VMQG_OK;
+}
+
+// A replica context brought to its primary's committed tables (include/vmqg.h
+// vmqg_replica_follow): the primary's last patch list when the replica holds
+// the epoch just before and that apply shipped patches, else the whole image
+// from the primary's host mirror (byte-identical to the primary's device
+// arena while no stage is pending).  Runs on the replica's stream after the
+// matches already queued there; the replica then answers at the primary's
+// epoch, so range results index the primary's record table of that epoch.
+int Engine::follow(const Engine& p) {
+  if (!replica || p.replica) return VMQG_E_STATE;
+  if (!has_device) return VMQG_E_DEVICE;
+  const uint64_t pe = p.epoch;
+  if (follow_ok && epoch == pe) return VMQG_OK;
+  hipSetDevice(device);
+  Layout a = p.dlay, b = dlay;
+  a.max_depth = b.max_depth = 0;
+  const bool same_regions = memcmp(&a, &b, sizeof(a)) == 0;
+  const bool patches = follow_ok && epoch + 1 == pe && !p.last_full && same_regions && d_arena;
+  follow_ok = false;   // until this call has shipped everything
+  if (order_on(stream) != VMQG_OK) return VMQG_E_DEVICE;
+  if (patches) {
+    const int rc = ship_patches(p.last_patches);
+    if (rc) return rc;
+  } else {
+    // the mirror is ahead of the primary's device tables while its stage is
+    // pending (a failed commit): the replica stays at its epoch until then
+    if (p.staged) return VMQG_E_STATE;
+    const uint64_t bytes = p.dlay.total_bytes;
+    if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
+    if (d_arena_bytes < bytes) {
+      if (d_arena) hipFree(d_arena);
+      d_arena = nullptr; d_arena_bytes = 0;
+      if (hipMalloc(&d_arena, bytes) != hipSuccess) return VMQG_E_NOMEM;
+      d_arena_bytes = bytes;
+    }
+    if (hipMemcpy(d_arena, p.mirror.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return VMQG_E_DEVICE;
+  }
+  lay = dlay = p.dlay;
+  d_trieless = p.d_trieless;
+  epoch = pe;
+  follow_ok = true;
+  return VMQG_OK;
+}
+
+// FNV-style digest of the device arena's first dlay.total_bytes (tests:
+// a replica's tables are the primary's byte for byte).
+int Engine::arena_digest(uint64_t* out) {
+  if (!has_device || !d_arena) return VMQG_E_DEVICE;
+  hipSetDevice(device);
+  std::vector<uint64_t> h(dlay.total_bytes / 8);
+  if (hipStreamSynchronize(stream) != hipSuccess) return VMQG_E_DEVICE;
+  if (hipMemcpy(h.data(), d_arena, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return VMQG_E_DEVICE;
+  uint64_t d = 0xcbf29ce484222325ull;
+  for (uint64_t w : h) d = (d ^ w) * 0x100000001b3ull;
+  *out = d ^ dlay.total_bytes;
   return VMQG_OK;
 }
 
@@ -1270,7 +1334,7 @@ MatchArgs Engine::args_for(const vmqg_pub* pubs, uint32_t npub, const uint32_t* 
   a.fastdone = reinterpret_cast<uint32_t*>(a.ddmask + (keycache_cap / 16 + 2));
   a.heavybyte = reinterpret_cast<uint8_t*>(a.fastdone + (keycache_cap / 32 + 2));
   a.heavy_min = opt_heavy_min;
-  a.trieless = opt_trieless && d_trieless && !replica ? 1u : 0u;
+  a.trieless = opt_trieless && d_trieless ? 1u : 0u;   // replicas: as their primary's (follow)
   a.dd_key = static_cast<uint64_t*>(d_dd);
   a.dd_rep = reinterpret_cast<uint32_t*>(static_cast<char*>(d_dd) + dd_slots * 8);
   a.dd_mask = dd_slots - 1;

@@ -489,6 +489,10 @@ struct Engine {
 
   // device
   int upload();
+  int ship_patches(const std::vector<Patch>& pl);
+  bool follow_ok = false;           // replica: its tables are a committed epoch of its primary's
+  int follow(const Engine& primary);
+  int arena_digest(uint64_t* out);
   int order_on(hipStream_t st);
   int ensure_match_scratch(uint64_t npub, hipStream_t st);
   int ensure_lookback(uint64_t granules, hipStream_t st);
