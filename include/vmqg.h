@@ -189,6 +189,14 @@ typedef struct vmqg_stats_s {
   /* ABI 6: the readers' record buffers (vmqg_records_pin)                       */
   uint64_t reader_waits;    /* stages that waited for readers to leave a buffer */
   uint64_t reader_wait_ns;  /*   ... and how long in all                         */
+  /* ABI 7: reclamation (the host tables follow the live set, as ETS does)      */
+  uint64_t keys;            /* live subscriber-list keys (`paths`: live paths)   */
+  uint64_t topics;          /* live (MP, Topic) terms                           */
+  uint64_t words_retired;   /* words nothing holds, awaiting vmqg_dict_release  */
+  uint64_t words_released;  /* words dropped by vmqg_dict_release so far         */
+  uint64_t host_bytes;      /* the engine's tables on the host: mirror, path /   */
+                            /* key / topic arrays, indexes, dictionary, readers' */
+                            /* record copies (not the per-key value lists)       */
 } vmqg_stats_t;
 
 /* ---- lifecycle ------------------------------------------------------- */
@@ -250,6 +258,30 @@ int vmqg_prepare_publishes(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints,
 int vmqg_prepare_word_lists(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints, const uint32_t* counts,
                             const uint8_t* const* words, const size_t* lens, vmqg_pub* pubs_out,
                             uint32_t* words_out, size_t wcap, size_t* nwords_out);
+
+/* ---- reclamation (ABI 7) ---------------------------------------------
+ * vmq_reg_trie's tables hold only what live subscriptions need (rows are
+ * deleted with their last value, vmq_reg_trie.erl:417-441, 472-539).  Here a
+ * trie path, an (MP, Topic) term and a subscriber-list key nothing holds any
+ * more are dropped at the end of the stage that emptied them (their ids
+ * reused).  Two kinds of ids are shared with the caller's readers and are
+ * released only through the caller's grace periods:
+ *   words          a word no path, topic or $share key holds is retired at the
+ *                  stage end; vmqg_dict_grace_token (a writer call) takes a
+ *                  token, and once every reader that was running then has
+ *                  finished — every vmqg_prepare_* / vmqg_intern_words lookup
+ *                  call, and every publish prepared before it is matched and
+ *                  folded — vmqg_dict_release(token) drops the words retired
+ *                  before the token (their ids reusable).  Without release
+ *                  calls no word is dropped.
+ *   SubscriberId / SubInfo ids (the caller's): vmqg_released_ids lists those
+ *                  the last stage's ops named, or whose last record it
+ *                  removed, that no record holds now (kind 0 subscribers, 1
+ *                  SubInfos; valid until the next stage).  The caller drops
+ *                  their terms once matches of earlier epochs are folded. */
+uint64_t vmqg_dict_grace_token(vmqg_ctx* ctx);
+int vmqg_dict_release(vmqg_ctx* ctx, uint64_t token);
+int vmqg_released_ids(vmqg_ctx* ctx, uint32_t kind, const uint32_t** ids, size_t* n);
 
 /* Words interned so far: grows whenever a filter brings a new word.  A
  * publish prepared with VMQG_PUB_UNKNOWN before the dictionary grew may name

@@ -1325,3 +1325,35 @@ def test_trieless_tables_take_the_exact_only_count(mode):
     v.set_option("fast_g", 0)
     v.set_option("trieless", 1)
     v.set_option("heavy_min", 0)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_reclaimed_ids_keep_parity(mode):
+    """Subscribe -> unsubscribe cycles with unique client ids and words
+    (paths, keys, topics dropped at each unsubscribe, words released after
+    every cycle and their ids reused by the next): every cycle's publishes —
+    on its own live topics and on the previous cycle's dead ones — fold to
+    the oracle's entries, and the device arena does not grow."""
+    from tests.test_host_engine import _cycle_events
+    node = "n@h"
+    prod = _driver(node, mode)
+    orc = O.TrieOracle(node)
+    arena = []
+    for c in range(16):
+        adds, dels = _cycle_events(c, n=200, node=node)
+        prod.apply(adds)
+        orc.apply(adds)
+        pubs = []
+        for cc in (c, c - 1):
+            for i in range(0, 200, 3):
+                u = b"u%d_%d" % (cc, i)
+                pubs += [("", (b"dev", u, b"state")), ("", (b"dev", u, b"x")), ("", (b"all", u, b"y", b"z")),
+                         ("", (b"jobs", u))]
+        _compare_batches(prod, orc, pubs, "cycle %d" % c)
+        prod.apply(dels)
+        orc.apply(dels)
+        prod.view.reclaim_words()
+        _compare_batches(prod, orc, pubs[:100], "cycle %d after deletes" % c)
+        arena.append(prod.view.stats_raw()["device_bytes"])
+    assert prod.view.stats_raw()["words_released"] > 0
+    assert arena[-1] <= arena[3], arena

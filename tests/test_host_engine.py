@@ -168,3 +168,56 @@ def test_random_churn_over_growing_mountpoints(seed):
         prod.apply(evs)
         orc.apply(evs)
         _compare(prod, orc, "seed %d step %d" % (seed, step))
+
+
+def _cycle_events(c, n=300, node="n@h"):
+    """Cycle c: n subscribers with unique client ids subscribe to filters
+    holding words of their own (an exact topic, a '+' filter, a '#' filter,
+    a $share group named after the cycle, a remote subscription), then the
+    deletes of all of them."""
+    subs = []
+    for i in range(n):
+        u = b"u%d_%d" % (c, i)
+        t = [((b"dev", u, b"state"), 1), ((b"dev", u, b"+"), 0), ((b"all", u, b"#"), 2)]
+        if i % 10 == 0:
+            t.append(((b"$share", b"g%d" % c, b"jobs", u), 1))
+        nd = "n2@h" if i % 7 == 0 else node
+        subs.append((("", b"client_%d_%d" % (c, i)), [(nd, True, sorted(t))]))
+    adds = [("updated", sid, None, v) for sid, v in subs]
+    dels = [("deleted", sid, v) for sid, v in subs]
+    return adds, dels
+
+
+def test_reclamation_follows_the_live_set():
+    """Subscribe -> unsubscribe cycles with unique client ids and unique
+    topic words: vmq_reg_trie deletes its rows with their last value
+    (vmq_reg_trie.erl:417-441, 472-539), so its tables track the live set;
+    here paths, keys, topics and (after vmqg_dict_release) words are dropped
+    too and their ids reused — the counts stay within 2x of one cycle's, the
+    tables equal the oracle's throughout, and the host bytes stop growing."""
+    node = "n@h"
+    prod = H.ProductDriver(node, device=-1)
+    orc = O.TrieOracle(node)
+    peak, hb = None, []
+    for c in range(60):
+        adds, dels = _cycle_events(c, node=node)
+        prod.apply(adds)
+        orc.apply(adds)
+        st = prod.view.stats_raw()
+        if peak is None:
+            peak = {k: st[k] for k in ("paths", "keys", "topics", "words")}
+        for k, v in peak.items():
+            assert st[k] <= 2 * v + 16, (c, k, st[k], v)
+        if c % 15 == 7:
+            _compare(prod, orc, "cycle %d live" % c)
+        prod.apply(dels)
+        orc.apply(dels)
+        prod.view.reclaim_words()
+        st = prod.view.stats_raw()
+        assert st["keys"] == 0 and st["topics"] == 0, (c, st["keys"], st["topics"])
+        assert st["paths"] <= 1024 + 4 and st["words"] <= 3 + 4, (c, st["paths"], st["words"])
+        hb.append(st["host_bytes"])
+        if c % 15 == 14:
+            _compare(prod, orc, "cycle %d empty" % c)
+    assert st["words_released"] >= 59 * 300
+    assert hb[-1] <= hb[10] * 1.25 + (1 << 20), (hb[10], hb[-1])

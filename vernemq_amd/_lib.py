@@ -81,7 +81,8 @@ class Stats(ctypes.Structure):
                  "fanout_objects", "remote_keys", "epoch", "rebuilds", "paths", "words",
                  "deferred_tier1", "deferred_tier2", "ops_applied", "apply_host_ns", "apply_upload_ns", "apply_wait_ns", "patch_bytes",
                  "image_bytes", "max_depth", "many_key", "retried", "wave_entries", "wide_entries",
-                 "dedup", "dedup_walked", "error_bits", "reader_waits", "reader_wait_ns")]
+                 "dedup", "dedup_walked", "error_bits", "reader_waits", "reader_wait_ns",
+                 "keys", "topics", "words_retired", "words_released", "host_bytes")]
 
 
 class RConfig(ctypes.Structure):
@@ -128,6 +129,9 @@ _U32, _U64, _SZ = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 SIGNATURES = [
     ("vmqg_abi_version", ctypes.c_int, []),
     ("vmqg_replica_follow", ctypes.c_int, [_P, _P]),
+    ("vmqg_dict_grace_token", _U64, [_P]),
+    ("vmqg_dict_release", ctypes.c_int, [_P, _U64]),
+    ("vmqg_released_ids", ctypes.c_int, [_P, _U32, ctypes.POINTER(_P), ctypes.POINTER(_SZ)]),
     ("vmqg_arena_digest", ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
     ("vmqg_build_id", ctypes.c_char_p, []),
     ("vmqg_create", _P, [ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_int)]),

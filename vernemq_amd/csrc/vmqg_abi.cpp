@@ -81,7 +81,7 @@ static inline bool split_publish_topic(const uint8_t* p, size_t len, F&& on_word
   for (size_t i = 0; i < len; i += 8) {
     const size_t m = len - i < 8 ? len - i : 8;
     uint64_t x = 0;
-#if defined(__SANITIZE_ADDRESS__)
+#if defined(VMQG_NO_OVERREAD)
     constexpr bool kWide = false;   // a page-safe over-read is still one to ASan
 #else
     constexpr bool kWide = true;
@@ -248,6 +248,24 @@ int vmqg_prepare_word_lists(vmqg_ctx* ctx, size_t n, const uint32_t* mountpoints
 }
 
 uint64_t vmqg_dict_generation(vmqg_ctx* ctx) { return ctx ? ctx->e.dict.generation() : 0; }
+
+int vmqg_released_ids(vmqg_ctx* ctx, uint32_t kind, const uint32_t** ids, size_t* n) {
+  if (!ctx || kind > 1 || !ids || !n) return VMQG_E_INVAL;
+  *ids = ctx->e.term_released[kind].data();
+  *n = ctx->e.term_released[kind].size();
+  return VMQG_OK;
+}
+
+uint64_t vmqg_dict_grace_token(vmqg_ctx* ctx) { return ctx ? ++ctx->e.dict.retire_token : 0; }
+
+int vmqg_dict_release(vmqg_ctx* ctx, uint64_t token) {
+  if (!ctx) return VMQG_E_INVAL;
+  if (ctx->e.replica) return VMQG_E_STATE;
+  GUARD_BEGIN
+  ctx->e.release_words(token);
+  return VMQG_OK;
+  GUARD_END
+}
 
 int vmqg_apply_stage(vmqg_ctx* ctx, const vmqg_op* ops, size_t n, const uint32_t* words, size_t nwords) {
   if (!ctx || (n && !ops) || (nwords && !words)) return VMQG_E_INVAL;
@@ -622,8 +640,13 @@ int vmqg_stats(vmqg_ctx* ctx, vmqg_stats_t* out) {
   out->remote_keys = e.n_remote_keys;
   out->epoch = e.epoch;
   out->rebuilds = e.rebuilds;
-  out->paths = e.paths.size();
+  out->paths = e.paths.size() - e.free_paths.size();
   out->words = e.dict.size();
+  out->keys = e.keys.size() - e.free_keys.size();
+  out->topics = e.topics.size() - e.free_topics.size();
+  out->words_retired = e.word_retired.size();
+  out->words_released = e.words_released;
+  out->host_bytes = e.host_bytes();
   out->deferred_tier1 = e.last_deferred[0];
   out->deferred_tier2 = e.last_deferred[1];
   out->ops_applied = e.ops_applied;

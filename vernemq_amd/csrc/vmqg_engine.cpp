@@ -97,7 +97,57 @@ uint32_t Engine::intern(const uint8_t* b, size_t n, bool create) {
     const uint32_t id = dict.find(k);
     return id == WordDict::kVoid ? kUnknownWord : id;
   }
-  return dict.intern(k);
+  const uint32_t id = dict.intern(k);
+  if (id >= word_refs.size()) {
+    const size_t m = std::max<size_t>(1024, (size_t)id * 2);
+    word_refs.resize(m, 0);
+    word_tag.resize(m, 0);
+    word_state.resize(m, 0);
+  }
+  if (word_state[id] == 2) word_state[id] = 0;   // a released id taken by a new word
+  if (word_refs[id] == 0 && id >= 3) word_zero.push_back(id);   // retired at the stage end unless used
+  return id;
+}
+
+// Stage end: words nothing holds any more become retired (tagged with the
+// grace token now); a retired word used again is simply in use again.
+void Engine::retire_words() {
+  for (uint32_t w : word_zero) {
+    if (word_refs[w] != 0) continue;
+    word_tag[w] = dict.retire_token;
+    if (word_state[w] == 0) { word_state[w] = 1; word_retired.push_back(w); }
+  }
+  word_zero.clear();
+}
+
+void Engine::collect_released_terms() {
+  for (int k = 0; k < 2; k++) {
+    term_released[k].clear();
+    if (term_mark[k].size() < term_refs[k].size()) term_mark[k].resize(term_refs[k].size(), 0);
+    for (uint32_t id : term_cand[k]) {
+      if (id < term_refs[k].size() && term_refs[k][id]) continue;
+      if (id >= term_mark[k].size()) term_mark[k].resize(std::max<size_t>(1024, (size_t)id * 2), 0);
+      if (term_mark[k][id]) continue;
+      term_mark[k][id] = 1;
+      term_released[k].push_back(id);
+    }
+    for (uint32_t id : term_released[k]) term_mark[k][id] = 0;
+    term_cand[k].clear();
+  }
+}
+
+// vmqg_dict_release: words retired before `token` was taken and still
+// unreferenced are dropped from the dictionary and their ids become
+// reusable; dictionary tables replaced before it are freed.
+void Engine::release_words(uint64_t token) {
+  size_t k = 0;
+  for (uint32_t w : word_retired) {
+    if (word_refs[w] != 0) { word_state[w] = 0; continue; }
+    if (word_tag[w] < token) { dict.remove(w); word_state[w] = 2; words_released++; continue; }
+    word_retired[k++] = w;
+  }
+  word_retired.resize(k);
+  dict.free_tables_before(token);
 }
 
 // ------------------------------------------------------------- paths/keys
@@ -106,14 +156,17 @@ uint32_t Engine::path_child(uint32_t parent, uint32_t word, bool create) {
   const uint32_t found = path_index.find(k);
   if (found != FlatIndex::kVoid) return found;
   if (!create) return kNone;
-  const uint32_t id = (uint32_t)paths.size();
   PathInfo pi;
   pi.parent = parent; pi.word = word; pi.mp = paths[parent].mp; pi.depth = paths[parent].depth + 1;
   // MQTT-4.7.2-1 filters: exactly [#], or starting with + (vmq_reg_trie.erl:285-288)
   pi.first_plus = pi.depth == 1 ? (word == kPlus) : paths[parent].first_plus;
   pi.dollar_skip = pi.first_plus || (pi.depth == 1 && word == kHash);
   if (pi.depth > max_depth) max_depth = pi.depth;
-  paths.push_back(std::move(pi));
+  uint32_t id;
+  if (!free_paths.empty()) { id = free_paths.back(); free_paths.pop_back(); paths[id] = std::move(pi); }
+  else { id = (uint32_t)paths.size(); paths.push_back(std::move(pi)); }
+  paths[parent].nchild++;
+  word_ref(word);
   path_index.insert(k, id);
   return id;
 }
@@ -168,20 +221,32 @@ uint32_t Engine::topic_id(uint32_t mp, const uint32_t* w, uint32_t L, bool creat
   });
   if (found != FlatIndex::kVoid) return found;
   if (!create) return kNone;
-  const uint32_t id = (uint32_t)topics.size();
   TopicInfo t;
   t.mp = mp;
   t.words.assign(w, w + L);
   for (uint32_t i = 0; i < L; i++) if (w[i] == kPlus || w[i] == kHash) t.wild = 1;
-  topics.push_back(std::move(t));
+  uint32_t id;
+  if (!free_topics.empty()) { id = free_topics.back(); free_topics.pop_back(); topics[id] = std::move(t); }
+  else { id = (uint32_t)topics.size(); topics.push_back(std::move(t)); }
+  for (uint32_t i = 0; i < L; i++) word_ref(w[i]);
   topic_index.insert(h, id);
   return id;
 }
 
+static uint32_t new_key(HugeVec<KeyInfo>& keys, std::vector<uint32_t>& free_keys) {
+  if (!free_keys.empty()) {
+    const uint32_t k = free_keys.back();
+    free_keys.pop_back();
+    keys[k] = KeyInfo();
+    return k;
+  }
+  keys.emplace_back();
+  return (uint32_t)keys.size() - 1;
+}
+
 uint32_t Engine::local_key(uint32_t tid, bool create) {
   if (topics[tid].local_key != kNone || !create) return topics[tid].local_key;
-  const uint32_t k = (uint32_t)keys.size();
-  keys.emplace_back();
+  const uint32_t k = new_key(keys, free_keys);
   keys[k].topic_id = tid;
   topics[tid].local_key = k;
   mark_key(k);
@@ -193,10 +258,11 @@ uint32_t Engine::group_key(uint32_t tid, uint32_t group, bool create) {
   const uint32_t found = group_key_index.find(gk);
   if (found != FlatIndex::kVoid) return found;
   if (!create) return kNone;
-  const uint32_t k = (uint32_t)keys.size();
-  keys.emplace_back();
+  const uint32_t k = new_key(keys, free_keys);
   keys[k].topic_id = tid;
   keys[k].group = group;
+  topics[tid].ngroup++;
+  word_ref(group);
   group_key_index.insert(gk, k);
   mark_key(k);
   return k;
@@ -384,6 +450,102 @@ void Engine::rebuild(uint64_t extra_edges, bool compact) {
   rebuilds++;
 }
 
+// An empty subscriber-list key is dropped: vmq_reg_trie deletes the
+// vmq_trie_subs row of its last value (vmq_reg_trie.erl:472-496), and a later
+// subscription makes a new key.  The paths and the exact slot that named it
+// are rewritten in the same flush (marked here), so no device record keeps
+// the id, which the next key may take.
+void Engine::free_key(uint32_t k) {
+  KeyInfo& K = keys[k];
+  const uint32_t tid = K.topic_id;
+  TopicInfo& t = topics[tid];
+  if (K.group != kNone) {
+    group_key_index.erase(((uint64_t)tid << 32) | K.group, k);
+    t.ngroup--;
+    word_unref(K.group);
+  } else if (t.local_key == k) {
+    t.local_key = kNone;
+  }
+  rec_garbage += K.cap;
+  K.vals = std::vector<Record>();
+  K.idx.reset();
+  K.dirty_pos = std::vector<uint32_t>();
+  K.off = K.cap = 0;
+  K.topic_id = kNone;
+  K.group = kNone;
+  KeyDesc* kd = region<KeyDesc>(lay.keydesc_off) + k;
+  if (k < lay.key_cap && (kd->off | kd->count)) {
+    kd->off = 0; kd->count = 0;
+    touch(lay.keydesc_off + (uint64_t)k * sizeof(KeyDesc), sizeof(KeyDesc));
+  }
+  free_keys.push_back(k);
+  reclaimed_keys++;
+  if (t.path != kNone) mark_path(t.path);
+  mark_topic(tid);
+}
+
+// After the flush: paths and topics nothing holds any more are dropped
+// (their ids reused), so the host tables and the arena follow the live set
+// as vmq_reg_trie's ETS tables do (trie_delete_path / del_trie_subs /
+// del_remote_subscriber delete rows, vmq_reg_trie.erl:417-441, 472-539).
+//   a path: not a root, no vmq_trie_node record, no incoming edge, no child
+//     path, no vmq_trie_topic entry — its parent may follow;
+//   a topic: no local key, no group key, no remote refcounts, no trie path,
+//     no exact slot.
+// A dropped path's device record is cleared (no edge leads to it: no walk
+// reads it; the clear keeps the image exact for a reused id).
+void Engine::reclaim() {
+  std::vector<uint32_t> work(dirty_paths.begin(), dirty_paths.end());
+  std::vector<uint32_t> tw(dirty_topics.begin(), dirty_topics.end());
+  const NodeRec empty{0, kNone, 0, 0, 0, 0, 0, 0};
+  while (!work.empty()) {
+    const uint32_t p = work.back();
+    work.pop_back();
+    PathInfo& P = paths[p];
+    if (p < cfg.max_mountpoints || P.parent == kNone || P.rec || P.filter || P.in_slot != ~0ull || P.nchild ||
+        !P.nodes.empty())
+      continue;
+    path_index.erase(((uint64_t)P.parent << 32) | P.word, p);
+    const uint32_t parent = P.parent;
+    paths[parent].nchild--;
+    work.push_back(parent);
+    if (P.topic_id != kNone) {
+      topics[P.topic_id].path = kNone;
+      tw.push_back(P.topic_id);
+    }
+    kl_garbage += P.kl_cap + P.hn_cap;
+    word_unref(P.word);
+    if (p < lay.node_cap) {
+      NodeRec* nr = region<NodeRec>(lay.node_off);
+      if (memcmp(&nr[p], &empty, sizeof empty)) { nr[p] = empty; touch(lay.node_off + (uint64_t)p * sizeof(NodeRec), sizeof(NodeRec)); }
+      if (memcmp(&nr[lay.node_cap + p], &empty, sizeof empty)) {
+        nr[lay.node_cap + p] = empty;
+        touch(lay.node_off + (lay.node_cap + p) * sizeof(NodeRec), sizeof(NodeRec));
+      }
+    }
+    const uint8_t was_dirty = P.dirty;
+    P = PathInfo();
+    P.parent = kNone; P.word = kNone; P.mp = kNone; P.depth = 0;
+    P.dirty = was_dirty;   // still listed in dirty_paths: the stage clears the flag
+    free_paths.push_back(p);
+    reclaimed_paths++;
+  }
+  for (uint32_t t : tw) {
+    TopicInfo& T = topics[t];
+    if (T.words.empty() && T.mp == kNone) continue;   // dropped already (listed twice)
+    if (T.local_key != kNone || T.ngroup || !T.remote.empty() || T.path != kNone || T.slot != ~0ull) continue;
+    topic_index.erase(topic_hash(T.mp, T.words.data(), (uint32_t)T.words.size()), t);
+    for (uint32_t w : T.words) word_unref(w);
+    xw_garbage += T.xw_len;
+    const uint8_t was_dirty = T.dirty;
+    T = TopicInfo();
+    T.mp = kNone;
+    T.dirty = was_dirty;
+    free_topics.push_back(t);
+    reclaimed_topics++;
+  }
+}
+
 // Mountpoint m's root is path m (a walk starts at path pub.mountpoint), so
 // the roots are the first cfg.max_mountpoints path ids.  In vmq_reg_trie a
 // mountpoint is only part of every key (vmq_reg_trie.erl:60, 279-281, 320):
@@ -413,12 +575,14 @@ void Engine::grow_mountpoints(uint32_t need) {
   FlatIndex idx;
   idx.reserve(paths.size());
   for (uint64_t p = m; p < paths.size(); p++) {
+    if (paths[p].parent == kNone) continue;   // a reclaimed id (free_paths)
     paths[p].parent = mv(paths[p].parent);
     idx.insert(((uint64_t)paths[p].parent << 32) | paths[p].word, (uint32_t)p);
   }
   path_index = std::move(idx);
   for (auto& t : topics) t.path = mv(t.path);
   for (auto& p : dirty_paths) p = mv(p);
+  for (auto& p : free_paths) p = mv(p);
   cfg.max_mountpoints = (uint32_t)m;
   rebuild(0);
 }
@@ -662,10 +826,11 @@ bool Engine::flush_incremental() {
     if (i + 4 < dirty_keys.size()) __builtin_prefetch(&keys[dirty_keys[i + 4]]);
     if (i + 2 < dirty_keys.size()) {
       const KeyInfo& K = keys[dirty_keys[i + 2]];
-      __builtin_prefetch(&topics[K.topic_id]);
+      if (K.topic_id != kNone) __builtin_prefetch(&topics[K.topic_id]);
       __builtin_prefetch(region<KeyDesc>(lay.keydesc_off) + dirty_keys[i + 2]);
     }
     const uint32_t k = dirty_keys[i];
+    if (keys[k].topic_id == kNone) continue;   // dropped (free_key): its rows were cleared there
     if (!write_key(k)) return false;
     const TopicInfo& t = topics[keys[k].topic_id];
     if (t.path != kNone) mark_path(t.path);
@@ -792,6 +957,7 @@ void Engine::insert_trie_subs(uint32_t key, const Record& v) {
   if (n == 1) n_fanout += 2;                                  // :458-463 promote both
   else if (n >= 2) n_fanout++;                                // :456-457
   K.vals.push_back(v);
+  record_in(v);
   K.dirty_pos.push_back((uint32_t)K.vals.size() - 1);
   if (!K.idx && K.vals.size() > 32) {
     K.idx.reset(new std::unordered_map<Record, uint32_t, RecordHash, RecordEq>());
@@ -808,6 +974,7 @@ void Engine::del_trie_subs(uint32_t key, const Record& v) {
   const size_t n = K.vals.size();
   if (n == 0) return;                                         // :474-476
   if (n == 1) {                                               // :494-495 value-blind (Q3)
+    record_out(K.vals[0]);
     K.vals.clear();
     n_subs_objects--;
     mark_key(key);
@@ -818,6 +985,7 @@ void Engine::del_trie_subs(uint32_t key, const Record& v) {
   if (K.idx) { auto it = K.idx->find(v); if (it != K.idx->end()) pos = it->second; }
   else { RecordEq eq; for (size_t i = 0; i < n; i++) if (eq(K.vals[i], v)) { pos = i; break; } }
   if (pos == ~(size_t)0) return;
+  record_out(K.vals[pos]);
   if (K.idx) {
     K.idx->erase(v);
     if (pos != n - 1) { K.vals[pos] = K.vals[n - 1]; (*K.idx)[K.vals[pos]] = (uint32_t)pos; }
@@ -910,7 +1078,8 @@ int Engine::stage_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
     if (o.mountpoint >= top_mp) top_mp = o.mountpoint + 1;
     if (o.nwords == 0 || (uint64_t)o.word_off + o.nwords > nwords) return VMQG_E_INVAL;
     const uint32_t* w = words + o.word_off;
-    for (uint32_t j = 0; j < o.nwords; j++) if (w[j] >= dict.size()) return VMQG_E_INVAL;
+    for (uint32_t j = 0; j < o.nwords; j++)   // ids the dictionary handed out and has not released
+      if (w[j] >= dict.id_bound() || (w[j] < word_state.size() && word_state[w[j]] == 2)) return VMQG_E_INVAL;
     // [<<"$share">>, Group] has no topic: triples([]) has no clause (vmq_topic.erl:71)
     if (o.nwords == 2 && w[0] == kShare) return VMQG_E_INVAL;
     // only wildcard and $share topics enter the trie (add_complex_topic/4 :318-319)
@@ -932,11 +1101,23 @@ int Engine::stage_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
     if (ops[i].kind == VMQG_OP_ADD) handle_add(ops[i], w);
     else handle_delete(ops[i], w);
   }
+  // subscriber-list keys left empty go before the flush writes the paths and
+  // exact slots that name them (vmq_reg_trie deletes such rows,
+  // vmq_reg_trie.erl:472-496)
+  for (size_t i = 0; i < dirty_keys.size(); i++)
+    if (keys[dirty_keys[i]].vals.empty() && keys[dirty_keys[i]].topic_id != kNone) free_key(dirty_keys[i]);
   const bool garbage_heavy = rec_garbage > lay.rec_cap / 2 || kl_garbage > lay.keylist_cap / 2 ||
                              xw_garbage > lay.exwords_cap / 2 ||
                              exact_tomb * 4 > lay.exact_buckets * kExactSlotsPerBucket;
   if (garbage_heavy) rebuild(0, true);                // compaction
   else if (!flush_incremental()) rebuild(0);         // growth (writes every dirty item too)
+  reclaim();   // paths and topics nothing holds any more (after their last writes)
+  retire_words();
+  for (size_t i = 0; i < n; i++) {   // the ops' terms: reported if no record holds them
+    term_cand[0].push_back(ops[i].subscriber);
+    term_cand[1].push_back(ops[i].subinfo);
+  }
+  collect_released_terms();
   for (uint32_t k : dirty_keys) keys[k].dirty = 0;
   for (uint32_t p : dirty_paths) paths[p].dirty = 0;
   for (uint32_t t : dirty_topics) topics[t].dirty = 0;

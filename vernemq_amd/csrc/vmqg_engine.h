@@ -61,13 +61,15 @@ struct Nog {
   bool operator==(const Nog& o) const { return node == o.node && group == o.group; }
 };
 
-// Open-addressed uint64 -> uint32 index (linear probing, load <= 1/2, no
-// erase: paths, topics and keys are interned for the context's lifetime).
-// Several values may share a key (topic_index keys by a 64-bit hash of MP +
-// words): find() takes a predicate that verifies the stored value.
+// Open-addressed uint64 -> uint32 index (linear probing, load <= 1/2
+// counting tombstones).  Several values may share a key (topic_index keys by
+// a 64-bit hash of MP + words): find() takes a predicate that verifies the
+// stored value.  Paths, topics and keys are erased when vmq_reg_trie would
+// no longer hold them (Engine::reclaim), so the index follows the live set.
 class FlatIndex {
  public:
   static constexpr uint32_t kVoid = 0xFFFFFFFFu;
+  static constexpr uint32_t kGone = 0xFFFFFFFEu;   // erased: probes continue past it
   void reserve(uint64_t n) { if (n * 2 > slots_.size()) regrow(n * 2); }
   // first value stored under `key` for which ok(value) holds, else kVoid
   template <class Ok>
@@ -77,7 +79,7 @@ class FlatIndex {
     for (uint64_t i = mix64(key) & m;; i = (i + 1) & m) {
       const Slot& s = slots_[i];
       if (s.val == kVoid) return kVoid;
-      if (s.key == key && ok(s.val)) return s.val;
+      if (s.val != kGone && s.key == key && ok(s.val)) return s.val;
     }
   }
   uint32_t find(uint64_t key) const { return find(key, [](uint32_t) { return true; }); }
@@ -86,11 +88,23 @@ class FlatIndex {
     if (!slots_.empty()) __builtin_prefetch(&slots_[mix64(key) & (slots_.size() - 1)]);
   }
   void insert(uint64_t key, uint32_t val) {
-    if ((n_ + 1) * 2 > slots_.size()) regrow(std::max<uint64_t>(1024, slots_.size() * 2));
+    if ((n_ + gone_ + 1) * 2 > slots_.size())   // mostly tombstones: rehash at the same size
+      regrow(std::max<uint64_t>(1024, (n_ + 1) * 4 > slots_.size() ? slots_.size() * 2 : slots_.size()));
     put(key, val);
     n_++;
   }
+  // erases the entry (key, val); false if absent
+  bool erase(uint64_t key, uint32_t val) {
+    if (slots_.empty()) return false;
+    const uint64_t m = slots_.size() - 1;
+    for (uint64_t i = mix64(key) & m;; i = (i + 1) & m) {
+      Slot& s = slots_[i];
+      if (s.val == kVoid) return false;
+      if (s.val == val && s.key == key) { s.val = kGone; n_--; gone_++; return true; }
+    }
+  }
   uint64_t size() const { return n_; }
+  uint64_t bytes() const { return slots_.size() * sizeof(Slot); }
 
  private:
   struct Slot { uint64_t key; uint32_t val; };
@@ -106,10 +120,11 @@ class FlatIndex {
     HugeVec<Slot> old;
     old.swap(slots_);
     slots_.assign(cap, Slot{0, kVoid});
-    for (const Slot& s : old) if (s.val != kVoid) put(s.key, s.val);
+    for (const Slot& s : old) if (s.val != kVoid && s.val != kGone) put(s.key, s.val);
+    gone_ = 0;
   }
   HugeVec<Slot> slots_;
-  uint64_t n_ = 0;
+  uint64_t n_ = 0, gone_ = 0;
 };
 
 // Word dictionary: topic words -> dense ids (vmq_topic words; the interning
@@ -143,7 +158,7 @@ class WordDict {
   struct Key { uint64_t h, k0, k1; const uint8_t* p; size_t n; };
   static Key key(const uint8_t* p, size_t n) {
     Key k{0, 0, 0, p, n};
-#if defined(__SANITIZE_ADDRESS__)
+#if defined(VMQG_NO_OVERREAD)
     constexpr bool kWide = false;   // the page-safe over-read below is still an over-read to ASan
 #else
     constexpr bool kWide = true;
@@ -178,15 +193,19 @@ class WordDict {
     const Table* t = tab_.load(std::memory_order_acquire);
     return t ? find_in(*t, k) : kVoid;
   }
-  // id of the word, added as the next dense id when absent (the writer only)
+  // id of the word, added when absent (the writer only): a released id
+  // (remove) first, else the next dense one
   uint32_t intern(const Key& k) {
     const uint32_t f = find(k);
     if (f != kVoid) return f;
     const uint64_t n = count_.load(std::memory_order_relaxed);
-    if (n >= 0xFFFFFF00ull) throw std::bad_alloc();   // ids above are reserved (kUnknownWord, ...)
+    if (free_.empty() && n >= 0xFFFFFF00ull) throw std::bad_alloc();   // ids above are reserved (kUnknownWord, ...)
     const Table* t = tab_.load(std::memory_order_relaxed);
-    if (!t || (n + 1) * 2 > t->mask + 1) t = regrow(std::max<uint64_t>(1024, t ? (t->mask + 1) * 2 : 0));
-    const uint32_t id = (uint32_t)n;
+    if (!t || (live_ + gone_ + 1) * 2 > t->mask + 1)   // full, or full of erased slots: rebuilt aside
+      t = regrow(std::max<uint64_t>(1024, t && (live_ + 1) * 4 <= t->mask + 1 ? t->mask + 1 : (t ? (t->mask + 1) * 2 : 0)));
+    uint32_t id;
+    if (!free_.empty()) { id = free_.back(); free_.pop_back(); }
+    else id = (uint32_t)n;
     std::string* chunk = dir_[id >> kChunkBits].load(std::memory_order_relaxed);
     if (!chunk) {
       chunk = new std::string[kChunkWords];
@@ -194,16 +213,55 @@ class WordDict {
     }
     chunk[id & (kChunkWords - 1)].assign(reinterpret_cast<const char*>(k.p), k.n);
     put(*t, Slot{k.h, id, (uint32_t)k.n, k.k0, k.k1});
-    count_.store(n + 1, std::memory_order_release);
+    live_++;
+    gen_.fetch_add(1, std::memory_order_release);
+    if (id == n) count_.store(n + 1, std::memory_order_release);
     return id;
+  }
+  // Drops a word and releases its id for reuse (the writer only).  The caller
+  // guarantees that no reader that could still probe for it or hold its id
+  // is running (vmqg_dict_release's grace): its slot is marked erased (probes
+  // continue past it), its text freed.
+  void remove(uint32_t id) {
+    const std::string& w = text(id);
+    const Key k = key(reinterpret_cast<const uint8_t*>(w.data()), w.size());
+    const Table* t = tab_.load(std::memory_order_relaxed);
+    Slot* sl = const_cast<Slot*>(t->slots.data());
+    for (uint64_t i = k.h & t->mask;; i = (i + 1) & t->mask) {
+      const uint32_t v = sl[i].id;
+      if (v == kVoid) break;   // not in the table (cannot happen for a live id)
+      if (v == id) { __atomic_store_n(&sl[i].id, kGone, __ATOMIC_RELEASE); gone_++; break; }
+    }
+    std::string().swap(dir_[id >> kChunkBits].load(std::memory_order_relaxed)[id & (kChunkWords - 1)]);
+    live_--;
+    free_.push_back(id);
   }
   const std::string& text(uint32_t id) const {
     return dir_[id >> kChunkBits].load(std::memory_order_acquire)[id & (kChunkWords - 1)];
   }
-  size_t size() const { return count_.load(std::memory_order_acquire); }
-  // words interned so far (the batch layer's staleness check of prepared
-  // publishes that held unknown words)
-  uint64_t generation() const { return count_.load(std::memory_order_acquire); }
+  // ids handed out so far are < id_bound(); live words = size()
+  uint64_t id_bound() const { return count_.load(std::memory_order_acquire); }
+  size_t size() const { return live_; }
+  // words interned so far, reused ids included (the batch layer's staleness
+  // check of prepared publishes that held unknown words)
+  uint64_t generation() const { return gen_.load(std::memory_order_acquire); }
+  // tables replaced by a rebuild, kept for readers still probing them until
+  // a grace period ends (free_tables_before)
+  void free_tables_before(uint64_t token) {
+    size_t k = 0;
+    for (size_t i = 0; i < retired_.size(); i++) {
+      if (retired_[i].second < token) retired_[i].first.reset();
+      else retired_[k++] = std::move(retired_[i]);
+    }
+    retired_.resize(k);
+  }
+  uint64_t retire_token = 0;   // the writer's grace token now (vmqg_dict_grace_token)
+  uint64_t bytes() const {
+    const Table* t = tab_.load(std::memory_order_relaxed);
+    uint64_t b = t ? (t->mask + 1) * sizeof(Slot) : 0;
+    for (auto& r : retired_) b += (r.first->mask + 1) * sizeof(Slot);
+    return b + (count_.load(std::memory_order_relaxed) + kChunkWords - 1) / kChunkWords * kChunkWords * sizeof(std::string);
+  }
 
  private:
   static constexpr uint32_t kChunkBits = 16, kChunkWords = 1u << kChunkBits, kChunks = 1u << 16;
@@ -212,12 +270,14 @@ class WordDict {
     HugeVec<Slot> slots;
     uint64_t mask;
   };
+  static constexpr uint32_t kGone = 0xFFFFFFFEu;   // an erased slot: probes continue
   static uint32_t load_id(const Slot& s) { return __atomic_load_n(&s.id, __ATOMIC_ACQUIRE); }
   uint32_t find_in(const Table& t, const Key& k) const {
     for (uint64_t i = k.h & t.mask;; i = (i + 1) & t.mask) {
       const Slot& s = t.slots[i];
       const uint32_t id = load_id(s);
       if (id == kVoid) return kVoid;
+      if (id == kGone) continue;
       if (s.h == k.h && s.len == k.n && s.k0 == k.k0 && s.k1 == k.k1 &&
           (k.n <= 16 || memcmp(text(id).data() + 16, k.p + 16, k.n - 16) == 0))
         return id;
@@ -240,16 +300,23 @@ class WordDict {
     nt->slots.assign(cap, Slot{0, kVoid, 0, 0, 0});
     nt->mask = cap - 1;
     if (const Table* old = tab_.load(std::memory_order_relaxed))
-      for (const Slot& s : old->slots) if (s.id != kVoid) put(*nt, s);
+      for (const Slot& s : old->slots) if (s.id != kVoid && s.id != kGone) put(*nt, s);
+    gone_ = 0;
     const Table* t = nt.get();
-    tables_.push_back(std::move(nt));       // the old tables stay: readers may be probing them
+    // the old table stays until a grace period taken after now ends: readers may be probing it
+    if (cur_) retired_.emplace_back(std::move(cur_), retire_token);
+    cur_ = std::move(nt);
     tab_.store(t, std::memory_order_release);
     return t;
   }
   std::atomic<const Table*> tab_{nullptr};
-  std::vector<std::unique_ptr<Table>> tables_;
+  std::unique_ptr<Table> cur_;
+  std::vector<std::pair<std::unique_ptr<Table>, uint64_t>> retired_;   // {table, token when retired}
   std::unique_ptr<std::atomic<std::string*>[]> dir_;   // word texts, kChunkWords per chunk
-  std::atomic<uint64_t> count_{0};
+  std::atomic<uint64_t> count_{0};   // id bound
+  std::atomic<uint64_t> gen_{0};     // interns, reused ids included
+  uint64_t live_ = 0, gone_ = 0;     // live words, erased slots of the current table
+  std::vector<uint32_t> free_;       // released ids
 };
 
 struct PathInfo {
@@ -257,6 +324,7 @@ struct PathInfo {
   uint64_t in_slot = ~0ull;         // edge-table slot of the edge (parent, word) -> this path, if present
   uint8_t eflags = 0;               // this path's own '#' / '+' / literal edges present (kHas*)
   uint32_t nlit = 0;                // its live literal-word edges (kHasWord while > 0)
+  uint32_t nchild = 0;              // interned child paths (a path with any is not reclaimed)
   uint32_t topic_id = kNone;        // (MP, path words) term, once known
   uint32_t kl_off = 0, kl_cap = 0;  // keylist range owned by this path
   uint32_t hn_off = 0, hn_cap = 0;  // keylist range of its remote nodes >= 64
@@ -299,6 +367,7 @@ struct TopicInfo {
   uint8_t dirty = 0, wild = 0;      // wild: a '+' / '#' word (no exbits filter bit: only such a publish equals it)
   std::vector<std::pair<uint32_t, int64_t>> remote;
   uint64_t slot = ~0ull;
+  uint32_t ngroup = 0;              // $share group keys {MP, Group, Topic} of this topic
   uint32_t words_off = kNone;
   uint32_t xw_len = 0;              // exwords entries owned: words beyond the inline ones, [count, remote nodes >= 64]
 };
@@ -310,6 +379,45 @@ struct Engine {
 
   // ---- dictionary
   WordDict dict;
+  // Word reclamation: a word is held by the trie paths, exact/filter topics
+  // and $share group keys that name it; one nothing holds any more is
+  // retired at the end of the stage, and dropped (its id reusable) by
+  // vmqg_dict_release once the caller's readers have passed a grace period
+  // (vmq_reg_trie's tables hold no word that no row uses).
+  HugeVec<uint32_t> word_refs;
+  HugeVec<uint64_t> word_tag;        // the grace token when it last became unreferenced
+  std::vector<uint8_t> word_state;   // 0 in use or fresh, 1 retired (pending), 2 released
+  std::vector<uint32_t> word_zero;   // unreferenced (or freshly interned) during this stage
+  std::vector<uint32_t> word_retired;
+  uint64_t words_released = 0;
+  void word_ref(uint32_t w) { if (w >= 3) word_refs[w]++; }
+  void word_unref(uint32_t w) { if (w >= 3 && --word_refs[w] == 0) word_zero.push_back(w); }
+  void retire_words();
+  void release_words(uint64_t token);
+  // The caller's SubscriberId / SubInfo ids held by records (vmq_trie_subs
+  // values): ids the last stage's ops named, or whose last record it
+  // removed, that no record holds now are reported (vmqg_released_ids) so the
+  // caller can drop their terms.
+  HugeVec<uint32_t> term_refs[2];          // [0] subscriber ids, [1] subinfo ids
+  std::vector<uint32_t> term_cand[2], term_released[2];
+  std::vector<uint8_t> term_mark[2];
+  void term_ref(int kind, uint32_t id) {
+    if (id >= term_refs[kind].size()) term_refs[kind].resize(std::max<size_t>(1024, (size_t)id * 2), 0);
+    term_refs[kind][id]++;
+  }
+  void term_unref(int kind, uint32_t id) { if (--term_refs[kind][id] == 0) term_cand[kind].push_back(id); }
+  void record_in(const Record& r) { term_ref(0, r.subscriber); term_ref(1, r.subinfo); }
+  void record_out(const Record& r) { term_unref(0, r.subscriber); term_unref(1, r.subinfo); }
+  void collect_released_terms();
+  uint64_t host_bytes() const {
+    uint64_t b = mirror.capacity() * 8 + dirty_bits.capacity() * 8 + paths.capacity() * sizeof(PathInfo) +
+                 keys.capacity() * sizeof(KeyInfo) + topics.capacity() * sizeof(TopicInfo) + path_index.bytes() +
+                 topic_index.bytes() + group_key_index.bytes() + dict.bytes() +
+                 word_refs.capacity() * 4 + word_tag.capacity() * 8 + word_state.capacity() +
+                 term_refs[0].capacity() * 4 + term_refs[1].capacity() * 4;
+    for (const RecBuf& r : rb) b += r.recs.capacity() * sizeof(Record);
+    return b;
+  }
 
   // ---- logical state
   HugeVec<PathInfo> paths;                              // ids [0, max_mp) are roots
@@ -318,6 +426,9 @@ struct Engine {
   FlatIndex group_key_index;                                // topic<<32|group -> key
   HugeVec<TopicInfo> topics;
   FlatIndex topic_index;                                    // hash(mp, words) -> topic (verified)
+  // ids of reclaimed paths / keys / topics, reused before new ones (Engine::reclaim)
+  std::vector<uint32_t> free_paths, free_keys, free_topics;
+  uint64_t reclaimed_paths = 0, reclaimed_keys = 0, reclaimed_topics = 0;
   uint64_t n_trie_nodes = 0, n_trie_topics = 0, n_subs_objects = 0, n_fanout = 0, n_remote_keys = 0;
 
   // ---- mirror of the device arena
@@ -480,6 +591,8 @@ struct Engine {
   Layout plan_layout(uint64_t extra_edges, uint32_t scale, bool compact) const;
   void rebuild(uint64_t extra_edges, bool compact = false);
   void grow_mountpoints(uint32_t need);
+  void free_key(uint32_t k);
+  void reclaim();
   bool flush_incremental();
   bool write_key(uint32_t k);
   bool write_path(uint32_t p);

@@ -138,6 +138,16 @@ class RegGpuView:
     def word_text(self, wid: int) -> bytes:
         return self._word_text[wid]
 
+    def reclaim_words(self) -> int:
+        """Drops the words no subscription holds any more (vmqg_dict_grace_token +
+        vmqg_dict_release: this mirror has no concurrent readers, so the grace
+        period is over at once); their ids may be reused, so the word -> id
+        cache starts afresh.  Returns the words released so far."""
+        tok = self._L.vmqg_dict_grace_token(self._h)
+        _lib.check(self._L.vmqg_dict_release(self._h, tok), "vmqg_dict_release")
+        self._words = {b"+": _lib.WORD_PLUS, b"#": _lib.WORD_HASH, b"$share": _lib.WORD_SHARE}
+        return self.stats_raw()["words_released"]
+
     # ------------------------------------------------------------ deltas
     def _ops_array(self, ops):
         """ops: iterable of (kind 'add'|'del', subscriber_id, topic, subinfo, node)."""
