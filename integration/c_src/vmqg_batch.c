@@ -17,14 +17,23 @@ static uint64_t mono_ns(void) {
 }
 
 /* ------------------------------------------------------------ interner */
+/* Open addressing over (hash, id + 1); an erased slot holds ERASED and
+ * probes continue past it.  Keys live back to back in `bytes` (offs / lens
+ * per id); a removed key's bytes are garbage until the buffer is packed.
+ * Ids removed and then released are reused, lowest-released first out. */
+#define ERASED 0xFFFFFFFFu
 struct vmqgb_interner {
   uint8_t* bytes;       /* every key, back to back */
-  size_t nbytes, bcap;
-  uint64_t* offs;       /* id -> start in bytes (offs[id + 1] = end) */
-  uint32_t n, ocap;
-  uint32_t* slots;      /* open addressing: id + 1, 0 = empty */
+  size_t nbytes, bcap, garbage;
+  uint64_t* offs;       /* id -> start in bytes */
+  uint32_t* lens;       /* id -> length; ERASED: not a live key */
+  uint32_t n, ocap;     /* ids handed out: [0, n) */
+  uint32_t live, erased;
+  uint32_t* slots;      /* open addressing: id + 1, 0 = empty, ERASED = erased */
   uint64_t* hashes;     /* per slot */
   uint32_t mask;
+  uint32_t* free_ids;   /* released ids */
+  uint32_t nfree, fcap;
 };
 
 static uint64_t hash_bytes(const void* p, size_t len) {   /* FNV-1a, then a 64-bit finaliser */
@@ -42,28 +51,27 @@ vmqgb_interner* vmqgb_interner_new(void) {
   t->slots = (uint32_t*)calloc(1024, sizeof(uint32_t));
   t->hashes = (uint64_t*)calloc(1024, sizeof(uint64_t));
   t->ocap = 1024;
-  t->offs = (uint64_t*)calloc(t->ocap + 1, sizeof(uint64_t));
-  if (!t->slots || !t->hashes || !t->offs) { vmqgb_interner_free(t); return NULL; }
+  t->offs = (uint64_t*)calloc(t->ocap, sizeof(uint64_t));
+  t->lens = (uint32_t*)calloc(t->ocap, sizeof(uint32_t));
+  if (!t->slots || !t->hashes || !t->offs || !t->lens) { vmqgb_interner_free(t); return NULL; }
   return t;
 }
 
 void vmqgb_interner_free(vmqgb_interner* t) {
   if (!t) return;
-  free(t->bytes); free(t->offs); free(t->slots); free(t->hashes); free(t);
+  free(t->bytes); free(t->offs); free(t->lens); free(t->slots); free(t->hashes); free(t->free_ids); free(t);
 }
 
 static int eq_at(const vmqgb_interner* t, uint32_t id, const void* bytes, size_t len) {
-  const uint64_t a = t->offs[id], e = t->offs[id + 1];
-  return e - a == len && memcmp(t->bytes + a, bytes, len) == 0;
+  return t->lens[id] == len && memcmp(t->bytes + t->offs[id], bytes, len) == 0;
 }
 
-static void rehash(vmqgb_interner* t) {
-  const uint32_t ncap = (t->mask + 1) * 2;
+static void rehash(vmqgb_interner* t, uint32_t ncap) {
   uint32_t* s = (uint32_t*)calloc(ncap, sizeof(uint32_t));
   uint64_t* h = (uint64_t*)calloc(ncap, sizeof(uint64_t));
   if (!s || !h) { free(s); free(h); return; }   /* keeps the old table: still correct, only fuller */
   for (uint32_t i = 0; i <= t->mask; i++) {
-    if (!t->slots[i]) continue;
+    if (!t->slots[i] || t->slots[i] == ERASED) continue;
     uint32_t j = (uint32_t)t->hashes[i] & (ncap - 1);
     while (s[j]) j = (j + 1) & (ncap - 1);
     s[j] = t->slots[i];
@@ -71,6 +79,25 @@ static void rehash(vmqgb_interner* t) {
   }
   free(t->slots); free(t->hashes);
   t->slots = s; t->hashes = h; t->mask = ncap - 1;
+  t->erased = 0;
+}
+
+/* the live keys packed to the front of a fresh buffer (removed keys' bytes dropped) */
+static void pack(vmqgb_interner* t) {
+  uint8_t* nb = (uint8_t*)malloc(t->nbytes - t->garbage + 1);
+  if (!nb) return;
+  size_t o = 0;
+  for (uint32_t id = 0; id < t->n; id++) {
+    if (t->lens[id] == ERASED) continue;
+    memcpy(nb + o, t->bytes + t->offs[id], t->lens[id]);
+    t->offs[id] = o;
+    o += t->lens[id];
+  }
+  free(t->bytes);
+  t->bytes = nb;
+  t->bcap = t->nbytes - t->garbage + 1;
+  t->nbytes = o;
+  t->garbage = 0;
 }
 
 int vmqgb_lookup(const vmqgb_interner* t, const void* bytes, size_t len, uint32_t* id) {
@@ -78,18 +105,23 @@ int vmqgb_lookup(const vmqgb_interner* t, const void* bytes, size_t len, uint32_
   for (uint32_t j = (uint32_t)hv & t->mask;; j = (j + 1) & t->mask) {
     const uint32_t v = t->slots[j];
     if (!v) return -1;
-    if (t->hashes[j] == hv && eq_at(t, v - 1, bytes, len)) { if (id) *id = v - 1; return 0; }
+    if (v != ERASED && t->hashes[j] == hv && eq_at(t, v - 1, bytes, len)) { if (id) *id = v - 1; return 0; }
   }
 }
 
-uint32_t vmqgb_intern(vmqgb_interner* t, const void* bytes, size_t len) {
+uint32_t vmqgb_intern(vmqgb_interner* t, const void* bytes, size_t len) { return vmqgb_intern_ex(t, bytes, len, NULL); }
+
+uint32_t vmqgb_intern_ex(vmqgb_interner* t, const void* bytes, size_t len, int* created) {
   const uint64_t hv = hash_bytes(bytes, len);
   uint32_t j = (uint32_t)hv & t->mask;
+  if (created) *created = 0;
   for (;; j = (j + 1) & t->mask) {
     const uint32_t v = t->slots[j];
     if (!v) break;
-    if (t->hashes[j] == hv && eq_at(t, v - 1, bytes, len)) return v - 1;
+    if (v != ERASED && t->hashes[j] == hv && eq_at(t, v - 1, bytes, len)) return v - 1;
   }
+  if (created) *created = 1;
+  if (len >= ERASED) return VMQG_NONE;
   if (t->nbytes + len > t->bcap) {
     size_t c = t->bcap ? t->bcap * 2 : 4096;
     while (c < t->nbytes + len) c *= 2;
@@ -97,28 +129,69 @@ uint32_t vmqgb_intern(vmqgb_interner* t, const void* bytes, size_t len) {
     if (!nb) return VMQG_NONE;
     t->bytes = nb; t->bcap = c;
   }
-  if (t->n + 1 >= t->ocap) {
-    uint64_t* no = (uint64_t*)realloc(t->offs, (size_t)(t->ocap * 2 + 1) * sizeof(uint64_t));
-    if (!no) return VMQG_NONE;
-    t->offs = no; t->ocap *= 2;
+  uint32_t id;
+  if (t->nfree) {
+    id = t->free_ids[--t->nfree];
+  } else {
+    if (t->n + 1 >= t->ocap) {
+      uint64_t* no = (uint64_t*)realloc(t->offs, (size_t)t->ocap * 2 * sizeof(uint64_t));
+      if (!no) return VMQG_NONE;
+      t->offs = no;
+      uint32_t* nl = (uint32_t*)realloc(t->lens, (size_t)t->ocap * 2 * sizeof(uint32_t));
+      if (!nl) return VMQG_NONE;
+      t->lens = nl;
+      t->ocap *= 2;
+    }
+    id = t->n++;
   }
-  const uint32_t id = t->n++;
   if (len) memcpy(t->bytes + t->nbytes, bytes, len);
+  t->offs[id] = t->nbytes;
+  t->lens[id] = (uint32_t)len;
   t->nbytes += len;
-  t->offs[id + 1] = t->nbytes;
   t->slots[j] = id + 1;
   t->hashes[j] = hv;
-  if ((uint64_t)t->n * 2 > t->mask + 1) rehash(t);
+  t->live++;
+  if ((uint64_t)(t->live + t->erased) * 2 > t->mask + 1) rehash(t, (uint64_t)t->live * 4 > t->mask + 1 ? (t->mask + 1) * 2 : t->mask + 1);
   return id;
 }
 
+int vmqgb_interner_remove(vmqgb_interner* t, uint32_t id) {
+  if (id >= t->n || t->lens[id] == ERASED) return -1;
+  const uint64_t hv = hash_bytes(t->bytes + t->offs[id], t->lens[id]);
+  for (uint32_t j = (uint32_t)hv & t->mask;; j = (j + 1) & t->mask) {
+    const uint32_t v = t->slots[j];
+    if (!v) return -1;
+    if (v == id + 1) { t->slots[j] = ERASED; break; }
+  }
+  t->garbage += t->lens[id];
+  t->lens[id] = ERASED;
+  t->live--;
+  t->erased++;
+  if (t->garbage > 4096 && t->garbage * 2 > t->nbytes) pack(t);
+  return 0;
+}
+
+int vmqgb_interner_release(vmqgb_interner* t, uint32_t id) {
+  if (id >= t->n || t->lens[id] != ERASED) return -1;
+  if (t->nfree == t->fcap) {
+    const uint32_t c = t->fcap ? t->fcap * 2 : 1024;
+    uint32_t* nf = (uint32_t*)realloc(t->free_ids, (size_t)c * sizeof(uint32_t));
+    if (!nf) return -1;   /* the id stays unused: only memory */
+    t->free_ids = nf;
+    t->fcap = c;
+  }
+  t->free_ids[t->nfree++] = id;
+  return 0;
+}
+
 const uint8_t* vmqgb_bytes(const vmqgb_interner* t, uint32_t id, size_t* len) {
-  if (id >= t->n) return NULL;
-  if (len) *len = (size_t)(t->offs[id + 1] - t->offs[id]);
+  if (id >= t->n || t->lens[id] == ERASED) return NULL;
+  if (len) *len = t->lens[id];
   return t->bytes + t->offs[id];
 }
 
 uint32_t vmqgb_count(const vmqgb_interner* t) { return t->n; }
+uint32_t vmqgb_live(const vmqgb_interner* t) { return t->live; }
 
 /* -------------------------------------------------------------- batches */
 static int grow(void** p, size_t* cap, size_t need, size_t esz) {
@@ -591,8 +664,27 @@ typedef struct vmqgb_lane {
   vmqgb_round rounds[VMQGB_ROUNDS];
 } vmqgb_lane;
 
+/* deferred writer work (vmqgb_view_defer) */
+typedef struct vmqgb_deferred {
+  void (*fn)(void* arg, uint64_t u);
+  void* arg;
+  uint64_t u;
+  struct vmqgb_deferred* next;
+} vmqgb_deferred;
+
 struct vmqgb_view {
   vmqg_ctx* ctx;             /* the primary: dictionary, host engine, readers' record tables */
+  /* grace periods: readers are batches between vmqgb_view_enter and
+   * vmqgb_view_release, counted per era parity; deferred work waits for a
+   * commit that shipped its stage to every lane (pending -> armed), then
+   * for the era to flip and the older era's readers to leave (flipped) */
+  unsigned era;              /* atomic */
+  long readers[2];           /* atomic */
+  vmqgb_deferred *pending, *armed, *flipped;   /* the writer's (writer mutex) */
+  unsigned flipped_era;
+  uint64_t deferred_runs;
+  void (*stage_hook)(void* arg, vmqgb_view* v);
+  void* stage_hook_arg;
   pthread_mutex_t wr;        /* writers: interning, applies (batchers never take it) */
   pthread_mutex_t q_mu;      /* the queues, the rounds, the counters */
   pthread_cond_t q_cv;
@@ -666,8 +758,20 @@ void vmqgb_view_bind(vmqgb_view* v, vmqgb_batch* b) {
   b->lane = __atomic_fetch_add(&v->next_lane, 1u, __ATOMIC_RELAXED) % (unsigned)v->nlanes;
 }
 
+static void arm_pending(vmqgb_view* v);
+static void run_list(vmqgb_view* v, vmqgb_deferred* d);
+
 void vmqgb_view_free(vmqgb_view* v) {
   if (!v) return;
+  /* no reader is left: every deferred free runs now (and what they defer) */
+  for (;;) {
+    arm_pending(v);
+    vmqgb_deferred* d = v->flipped;
+    v->flipped = NULL;
+    if (!d) { d = v->armed; v->armed = NULL; }
+    if (!d) break;
+    run_list(v, d);
+  }
   for (int k = 0; k < v->nlanes; k++) lane_free(&v->lanes[k]);
   pthread_mutex_destroy(&v->wr);
   pthread_mutex_destroy(&v->q_mu);
@@ -676,6 +780,95 @@ void vmqgb_view_free(vmqgb_view* v) {
 }
 
 vmqg_ctx* vmqgb_view_ctx(vmqgb_view* v) { return v->ctx; }
+
+/* ------------------------------------------------------- grace periods */
+void vmqgb_view_enter(vmqgb_view* v, vmqgb_batch* b) {
+  if (b->in_reader) return;
+  for (;;) {
+    const unsigned e = __atomic_load_n(&v->era, __ATOMIC_SEQ_CST);
+    __atomic_fetch_add(&v->readers[e & 1], 1, __ATOMIC_SEQ_CST);
+    if (__atomic_load_n(&v->era, __ATOMIC_SEQ_CST) == e) { b->reader_era = e; b->in_reader = 1; return; }
+    __atomic_fetch_sub(&v->readers[e & 1], 1, __ATOMIC_SEQ_CST);   /* flipped meanwhile: count in the new era */
+  }
+}
+
+static void reader_exit(vmqgb_view* v, vmqgb_batch* b) {
+  if (!b->in_reader) return;
+  __atomic_fetch_sub(&v->readers[b->reader_era & 1], 1, __ATOMIC_SEQ_CST);
+  b->in_reader = 0;
+}
+
+int vmqgb_view_defer(vmqgb_view* v, void (*fn)(void*, uint64_t), void* arg, uint64_t u, int after_commit) {
+  vmqgb_deferred* d = (vmqgb_deferred*)malloc(sizeof(*d));
+  if (!d) return VMQG_E_NOMEM;
+  d->fn = fn; d->arg = arg; d->u = u;
+  vmqgb_deferred** l = after_commit ? &v->pending : &v->armed;
+  d->next = *l;
+  *l = d;
+  return 0;
+}
+
+static void run_list(vmqgb_view* v, vmqgb_deferred* d) {
+  while (d) {
+    vmqgb_deferred* n = d->next;
+    d->fn(d->arg, d->u);
+    free(d);
+    v->deferred_runs++;
+    d = n;
+  }
+}
+
+/* the writer: runs what the readers have let go of, flips the era for what
+ * is armed (writer mutex held) */
+void vmqgb_view_reclaim(vmqgb_view* v) {
+  for (int round = 0; round < 2; round++) {
+    if (v->flipped) {
+      if (__atomic_load_n(&v->readers[v->flipped_era & 1], __ATOMIC_SEQ_CST) != 0) return;
+      vmqgb_deferred* d = v->flipped;
+      v->flipped = NULL;
+      run_list(v, d);
+    }
+    if (!v->armed) return;
+    v->flipped = v->armed;
+    v->armed = NULL;
+    v->flipped_era = __atomic_load_n(&v->era, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&v->era, v->flipped_era + 1, __ATOMIC_SEQ_CST);
+  }
+}
+
+static void arm_pending(vmqgb_view* v) {
+  while (v->pending) {
+    vmqgb_deferred* d = v->pending;
+    v->pending = d->next;
+    d->next = v->armed;
+    v->armed = d;
+  }
+}
+
+void vmqgb_view_set_stage_hook(vmqgb_view* v, void (*fn)(void*, vmqgb_view*), void* arg) {
+  v->stage_hook = fn;
+  v->stage_hook_arg = arg;
+}
+
+/* the dictionary's retired words: released after a grace period */
+static void dict_release_fn(void* arg, uint64_t token) { vmqg_dict_release((vmqg_ctx*)arg, token); }
+
+/* after a commit (writer mutex held): if every lane holds the committed
+ * tables, the stages' deferred work is armed, the words the stages retired
+ * are queued for release, and due work runs */
+static void after_commit(vmqgb_view* v, int ok) {
+  for (int k = 1; ok && k < v->nlanes; k++) ok = __atomic_load_n(&v->lanes[k].ok, __ATOMIC_ACQUIRE);
+  if (ok) {
+    arm_pending(v);
+    vmqgb_view_defer(v, dict_release_fn, v->ctx, vmqg_dict_grace_token(v->ctx), 0);
+  }
+  vmqgb_view_reclaim(v);
+}
+
+void vmqgb_view_grace_stats(vmqgb_view* v, uint64_t* runs, int* waiting) {
+  if (runs) *runs = v->deferred_runs;
+  if (waiting) *waiting = (v->pending != NULL) + (v->armed != NULL) + (v->flipped != NULL);
+}
 
 /* After the primary's commit (writer mutex held): every replica brought to
  * its tables.  A replica that fails keeps answering nothing (its batchers go
@@ -733,6 +926,8 @@ int vmqgb_view_apply_ops(vmqgb_view* v, vmqgb_ops* o, uint64_t* epoch) {
   const uint64_t t3 = mono_ns();
   if (!rc2 && v->nlanes > 1) follow_replicas(v);
   o->n = o->nwords = 0;
+  if (!rc && v->stage_hook) v->stage_hook(v->stage_hook_arg, v);   /* the stage's released ids (pending) */
+  after_commit(v, rc2 == 0);
   pthread_mutex_lock(&v->q_mu);
   v->st.applies++;
   v->st.stage_ns += t1 - t0;
@@ -751,6 +946,7 @@ int vmqgb_view_commit(vmqgb_view* v, uint64_t* epoch) {
   const int rc = vmqg_apply_commit(v->ctx, epoch);
   pthread_mutex_unlock(&v->lanes[0].device);
   if (!rc && v->nlanes > 1) follow_replicas(v);
+  after_commit(v, rc == 0);
   vmqgb_view_write_end(v);
   return rc;
 }
@@ -816,7 +1012,15 @@ static void round_release(vmqgb_view* v, vmqgb_round* r) {   /* q_mu held */
   }
 }
 
+/* the batch's pinned record table and round buffers (its reader section goes on) */
+static void release_lease(vmqgb_view* v, vmqgb_batch* b);
+
 void vmqgb_view_release(vmqgb_view* v, vmqgb_batch* b) {
+  release_lease(v, b);
+  reader_exit(v, b);
+}
+
+static void release_lease(vmqgb_view* v, vmqgb_batch* b) {
   if (b->rec_pinned) {
     vmqg_records_unpin(v->ctx, b->rec_pin);
     b->rec_pinned = 0;
@@ -1007,7 +1211,8 @@ static int match_direct(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_em
 }
 
 int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit** recs, uint64_t* nrecs) {
-  vmqgb_view_release(v, b);
+  release_lease(v, b);
+  vmqgb_view_enter(v, b);   /* no-op when the batch entered before its prepare */
   b->out_ranges = ranges;
   if (recs) *recs = NULL;
   if (nrecs) *nrecs = 0;
@@ -1044,7 +1249,7 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
       int rc = vmqg_records_pin(v->ctx, b->epoch, &rt, &nrt, &b->rec_pin);
       if (rc == 0) b->rec_pinned = 1;
       if (rc == VMQG_E_STATE) {   /* two applies rewrote record slots since the round */
-        vmqgb_view_release(v, b);
+        release_lease(v, b);
         pthread_mutex_lock(&v->q_mu);
         v->st.state_retries++;
         pthread_mutex_unlock(&v->q_mu);
@@ -1063,7 +1268,7 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
       if (rc < 0) return rc;
       if (rc == 1 && attempt < 16) {
         b->stale_rematches++;
-        vmqgb_view_release(v, b);
+        release_lease(v, b);
         pthread_mutex_lock(&v->q_mu);
         v->st.stale_rematches++;
         pthread_mutex_unlock(&v->q_mu);

@@ -53,10 +53,18 @@ vmqgb_interner* vmqgb_interner_new(void);
 void vmqgb_interner_free(vmqgb_interner* t);
 /* id of `bytes`, created when new (ids are dense from 0) */
 uint32_t vmqgb_intern(vmqgb_interner* t, const void* bytes, size_t len);
+/* the same; *created = 1 when the key was not there (a new or reused id) */
+uint32_t vmqgb_intern_ex(vmqgb_interner* t, const void* bytes, size_t len, int* created);
 /* 0 and *id when present, -1 when not */
 int vmqgb_lookup(const vmqgb_interner* t, const void* bytes, size_t len, uint32_t* id);
 const uint8_t* vmqgb_bytes(const vmqgb_interner* t, uint32_t id, size_t* len);
-uint32_t vmqgb_count(const vmqgb_interner* t);
+uint32_t vmqgb_count(const vmqgb_interner* t);   /* ids handed out so far (a bound: reused ids count once) */
+uint32_t vmqgb_live(const vmqgb_interner* t);    /* keys interned now */
+/* Takes key `id` out (later interns of its bytes get another id); the id
+ * stays reserved until vmqgb_interner_release makes it reusable — after the
+ * readers that could still hold it are gone (the caller's grace period). */
+int vmqgb_interner_remove(vmqgb_interner* t, uint32_t id);
+int vmqgb_interner_release(vmqgb_interner* t, uint32_t id);
 
 /* ---- publish batches ------------------------------------------------ */
 typedef struct vmqgb_batch {
@@ -90,6 +98,8 @@ typedef struct vmqgb_batch {
   int rec_pinned;
   uint32_t stale_rematches;   /* matches repeated because a publish's unknown word became known */
   unsigned lane;        /* the view context its matches go to (vmqgb_view_bind; 0: the primary) */
+  int in_reader;        /* inside a reader section of the view (vmqgb_view_enter .. _release) */
+  unsigned reader_era;
   int out_ranges;       /* set by vmqgb_view_match: 1 the results are ranges, 0 records (a
                            ranges request falls back to records when applies keep rewriting
                            the record slots its rounds index) */
@@ -204,6 +214,24 @@ int vmqgb_view_lanes(vmqgb_view* v);
  * binds each batcher's batch once: one batcher per scheduler, so scheduler
  * k's publishes go to context k mod N). */
 void vmqgb_view_bind(vmqgb_view* v, vmqgb_batch* b);
+/* Grace periods.  A batcher's reader section runs from vmqgb_view_enter
+ * (before its prepare: word ids are looked up there) to vmqgb_view_release
+ * (after its fold: term ids are read there); vmqgb_view_match enters if the
+ * batch has not.  Writer-side work that frees what readers may still hold —
+ * the dictionary's retired words (vmqg_dict_release), the caller's terms
+ * (its stage hook) — is deferred: vmqgb_view_defer(after_commit = 1) waits
+ * for a commit that shipped the current stage to every lane, then for every
+ * reader section open at that point to end; after_commit = 0 skips the
+ * commit.  Deferred work runs in the writer (its mutex held): at applies,
+ * commits, and vmqgb_view_reclaim.  The view itself queues the word release
+ * after every commit. */
+void vmqgb_view_enter(vmqgb_view* v, vmqgb_batch* b);
+int vmqgb_view_defer(vmqgb_view* v, void (*fn)(void* arg, uint64_t u), void* arg, uint64_t u, int after_commit);
+void vmqgb_view_reclaim(vmqgb_view* v);   /* writer mutex held */
+/* fn(arg, v) after every stage that applied ops (writer mutex held, before
+ * the commit): the NIF collects vmqg_released_ids there */
+void vmqgb_view_set_stage_hook(vmqgb_view* v, void (*fn)(void* arg, vmqgb_view* v), void* arg);
+void vmqgb_view_grace_stats(vmqgb_view* v, uint64_t* runs, int* waiting);
 /* Device-arena digests of the lanes (out[k], k < n): tests check that every
  * replica's tables are the primary's byte for byte.  Takes each lane's
  * device mutex; call with the writer mutex held (between applies). */

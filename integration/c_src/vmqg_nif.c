@@ -46,19 +46,30 @@
 #include "vmqg.h"
 #include "vmqg_batch.h"
 
-/* Terms by id: TS_CHUNK-term chunks published whole (release) before any
- * result can carry one of their ids; a chunk never moves, so a batcher reads
- * a term while the writer adds others.  Terms of a process-independent env
- * stay where they are as the env grows. */
+/* Terms by id, TS_CHUNK ids per chunk.  A chunk owns a process-independent
+ * environment holding its terms (enif_make_copy) and is published whole
+ * (release) before any result can carry one of its ids; readers (batchers
+ * folding) index it without a lock while the writer adds terms.  Ids are
+ * reused once their terms are dropped (the view's grace period has passed),
+ * so a chunk's environment accumulates dead copies: when they outnumber the
+ * live ones the writer copies the live terms into a fresh chunk, publishes
+ * it, and frees the old one after another grace period (vmqgb_view_defer). */
 #define TS_CHUNK_BITS 14
 #define TS_CHUNK (1u << TS_CHUNK_BITS)
 #define TS_CHUNKS (1u << 18)      /* ids < 2^32 */
 typedef struct {
-  ErlNifEnv* env;                 /* owns the stored terms */
-  ERL_NIF_TERM** dir;             /* TS_CHUNKS chunk pointers */
-} term_store;
+  ErlNifEnv* env;                 /* owns the chunk's stored terms */
+  uint32_t live, dead;            /* terms stored / dead copies in env */
+  ERL_NIF_TERM t[TS_CHUNK];
+} ts_chunk;
 
 typedef struct {
+  ts_chunk** dir;                 /* TS_CHUNKS chunk pointers */
+  uint64_t live, chunks, compactions;
+} term_store;
+
+typedef struct vmqg_res vmqg_res;
+struct vmqg_res {
   vmqg_ctx* ctx;                  /* the primary (host engine + its device tables) */
   vmqg_ctx* replicas[VMQGB_MAX_LANES];   /* devices => [D0, D1, ...]: replicas on D1, ... */
   int nreplicas;
@@ -67,7 +78,8 @@ typedef struct {
   vmqgb_interner *mps, *nodes, *subs, *infos;
   term_store node_t, sub_t, info_t, group_t;   /* group_t indexed by word id */
   vmqgb_ops ops;                  /* apply/3 and add_init/6 accumulation (under the write lock) */
-} vmqg_res;
+  uint64_t terms_dropped;
+};
 
 typedef struct {                  /* one batcher's batch (batch_new/1) */
   vmqg_res* owner;                /* kept alive while the batch lives */
@@ -81,50 +93,142 @@ static ERL_NIF_TERM a_ok, a_error, a_invalid_topic, a_device, a_nomem, a_badarg,
 
 /* ------------------------------------------------------------ helpers */
 static int store_init(term_store* s) {
-  s->env = enif_alloc_env();
-  s->dir = (ERL_NIF_TERM**)enif_alloc(TS_CHUNKS * sizeof(ERL_NIF_TERM*));
-  if (!s->env || !s->dir) return 0;
-  memset(s->dir, 0, TS_CHUNKS * sizeof(ERL_NIF_TERM*));
+  s->dir = (ts_chunk**)enif_alloc(TS_CHUNKS * sizeof(ts_chunk*));
+  if (!s->dir) return 0;
+  memset(s->dir, 0, TS_CHUNKS * sizeof(ts_chunk*));
+  s->live = s->chunks = s->compactions = 0;
   return 1;
+}
+
+static void chunk_free(ts_chunk* c) {
+  if (!c) return;
+  enif_free_env(c->env);
+  enif_free(c);
 }
 
 static void store_free(term_store* s) {
   if (s->dir)
-    for (size_t c = 0; c < TS_CHUNKS; c++) if (s->dir[c]) enif_free(s->dir[c]);
+    for (size_t c = 0; c < TS_CHUNKS; c++) chunk_free(s->dir[c]);
   enif_free(s->dir);
-  if (s->env) enif_free_env(s->env);
+}
+
+static ts_chunk* chunk_new(void) {
+  ts_chunk* c = (ts_chunk*)enif_alloc(sizeof(ts_chunk));
+  if (!c) return NULL;
+  memset(c, 0, sizeof(*c));
+  c->env = enif_alloc_env();
+  if (!c->env) { enif_free(c); return NULL; }
+  return c;
 }
 
 /* the writer only */
 static int store_put(term_store* s, size_t id, ERL_NIF_TERM t) {
   if (!s->dir || (id >> TS_CHUNK_BITS) >= TS_CHUNKS) return 0;
-  ERL_NIF_TERM* ch = s->dir[id >> TS_CHUNK_BITS];
+  ts_chunk* ch = s->dir[id >> TS_CHUNK_BITS];
   if (!ch) {
-    ch = (ERL_NIF_TERM*)enif_alloc(TS_CHUNK * sizeof(ERL_NIF_TERM));
-    if (!ch) return 0;
-    memset(ch, 0, TS_CHUNK * sizeof(ERL_NIF_TERM));
+    if (!(ch = chunk_new())) return 0;
     __atomic_store_n(&s->dir[id >> TS_CHUNK_BITS], ch, __ATOMIC_RELEASE);
+    s->chunks++;
   }
-  ch[id & (TS_CHUNK - 1)] = enif_make_copy(s->env, t);
+  ERL_NIF_TERM* slot = &ch->t[id & (TS_CHUNK - 1)];
+  if (*slot) ch->dead++; else { ch->live++; s->live++; }   /* a group word's term replaced */
+  *slot = enif_make_copy(ch->env, t);
   return 1;
 }
 
 /* readers: an id from a match result (stored before the apply that made it reachable) */
 static ERL_NIF_TERM store_get(const term_store* s, uint32_t id) {
-  const ERL_NIF_TERM* ch = __atomic_load_n(&s->dir[id >> TS_CHUNK_BITS], __ATOMIC_ACQUIRE);
-  return ch ? ch[id & (TS_CHUNK - 1)] : 0;
+  const ts_chunk* ch = __atomic_load_n(&s->dir[id >> TS_CHUNK_BITS], __ATOMIC_ACQUIRE);
+  return ch ? ch->t[id & (TS_CHUNK - 1)] : 0;
 }
 
-/* id of a term (created on first sight), its copy stored under the id */
+/* The writer: when id's chunk holds more dead copies than live terms (and
+ * at least 1,024), its live terms are copied into a fresh chunk, which is
+ * published; the old chunk is returned for the caller to free after a
+ * grace period (readers may still index it). */
+static ts_chunk* store_compact(term_store* s, uint32_t id) {
+  ts_chunk* ch = s->dir[id >> TS_CHUNK_BITS];
+  if (!ch || ch->dead < 1024 || ch->dead <= ch->live) return NULL;
+  ts_chunk* nc = chunk_new();
+  if (!nc) return NULL;   /* stays as it is: only memory */
+  for (uint32_t i = 0; i < TS_CHUNK; i++)
+    if (ch->t[i]) { nc->t[i] = enif_make_copy(nc->env, ch->t[i]); nc->live++; }
+  __atomic_store_n(&s->dir[id >> TS_CHUNK_BITS], nc, __ATOMIC_RELEASE);
+  s->compactions++;
+  return ch;
+}
+
+/* the writer, after a grace period: id's term is dead (its copy stays in
+ * the chunk's environment until the chunk is compacted: store_compact) */
+static ts_chunk* store_drop(term_store* s, uint32_t id) {
+  ts_chunk* ch = s->dir[id >> TS_CHUNK_BITS];
+  if (!ch || !ch->t[id & (TS_CHUNK - 1)]) return NULL;
+  ch->t[id & (TS_CHUNK - 1)] = 0;
+  ch->live--;
+  ch->dead++;
+  s->live--;
+  return store_compact(s, id);
+}
+
+/* id of a term (created on first sight, possibly a reused id), its copy
+ * stored under the id */
 static int term_id(vmqgb_interner* in, term_store* st, ErlNifEnv* env, ERL_NIF_TERM t, uint32_t* id) {
   ErlNifBinary b;
   if (!enif_term_to_binary(env, t, &b)) return 0;
-  const uint32_t before = vmqgb_count(in);
-  *id = vmqgb_intern(in, b.data, b.size);
+  int created = 0;
+  *id = vmqgb_intern_ex(in, b.data, b.size, &created);
   enif_release_binary(&b);
   if (*id == VMQG_NONE) return 0;
-  if (st && *id >= before) return store_put(st, *id, t);
+  if (st && created) return store_put(st, *id, t);
   return 1;
+}
+
+/* ------------------------------------------------------- term reclamation */
+/* SubscriberId / SubInfo terms no record holds any more (vmqg_released_ids
+ * after each stage): taken out of the interner at once — a later
+ * subscription of the same term gets a fresh id — and, once the view's grace
+ * period has passed (no batcher can still fold a record naming them),
+ * dropped from the store and their ids made reusable.  Memory thus follows
+ * the live subscriptions, as vmq_reg_trie's ETS rows do
+ * (vmq_reg_trie.erl:472-496). */
+typedef struct {
+  vmqg_res* r;
+  uint32_t kind, n;
+  uint32_t ids[];
+} drop_batch;
+
+static void chunk_retire_fn(void* arg, uint64_t u) { (void)u; chunk_free((ts_chunk*)arg); }
+
+static void drop_terms_fn(void* arg, uint64_t u) {
+  (void)u;
+  drop_batch* d = (drop_batch*)arg;
+  vmqg_res* r = d->r;
+  vmqgb_interner* in = d->kind ? r->infos : r->subs;
+  term_store* st = d->kind ? &r->info_t : &r->sub_t;
+  for (uint32_t i = 0; i < d->n; i++) {
+    ts_chunk* old = store_drop(st, d->ids[i]);
+    if (old) vmqgb_view_defer(r->view, chunk_retire_fn, old, 0, 0);   /* after readers of it leave (if the
+                                                                         defer cannot allocate, it is kept) */
+    vmqgb_interner_release(in, d->ids[i]);
+    r->terms_dropped++;
+  }
+  enif_free(d);
+}
+
+static void stage_hook(void* arg, vmqgb_view* v) {
+  vmqg_res* r = (vmqg_res*)arg;
+  for (uint32_t kind = 0; kind < 2; kind++) {
+    const uint32_t* ids = NULL;
+    size_t n = 0;
+    if (vmqg_released_ids(r->ctx, kind, &ids, &n) || !n) continue;
+    vmqgb_interner* in = kind ? r->infos : r->subs;
+    drop_batch* d = (drop_batch*)enif_alloc(sizeof(drop_batch) + n * sizeof(uint32_t));
+    if (!d) continue;   /* the terms stay: only memory */
+    d->r = r; d->kind = kind; d->n = 0;
+    for (size_t i = 0; i < n; i++)
+      if (vmqgb_interner_remove(in, ids[i]) == 0) d->ids[d->n++] = ids[i];
+    if (!d->n || vmqgb_view_defer(v, drop_terms_fn, d, 0, 1)) enif_free(d);
+  }
 }
 
 /* the mountpoint interner is shared with the batchers' lookups */
@@ -232,6 +336,7 @@ static ERL_NIF_TERM nif_create(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     err = vmqgb_view_add_replica(r->view, x);
   }
   if (err && r->ctx) { vmqgb_view_free(r->view); r->view = NULL; }
+  if (r->view) vmqgb_view_set_stage_hook(r->view, stage_hook, r);
   ERL_NIF_TERM ret = r->ctx && r->view ? enif_make_tuple2(env, a_ok, enif_make_resource(env, r)) : error_term(env, err);
   enif_release_resource(r);
   return ret;
@@ -273,8 +378,20 @@ static int add_change(ErlNifEnv* env, vmqg_res* r, uint32_t kind, ERL_NIF_TERM s
   enif_free(wp);
   enif_free(wl);
   if (rc) return rc;
-  /* $share/Group/...: remember the group binary under its word id (decoding kind-B entries) */
-  if (len >= 3 && r->ops.words[w0] == VMQG_WORD_SHARE) store_put(&r->group_t, r->ops.words[w0 + 1], group);
+  /* $share/Group/...: remember the group binary under its word id (decoding
+   * kind-B entries) — unless it is there already: a word id released and
+   * reused for another word gets its new binary, the old copy becomes dead */
+  if (len >= 3 && r->ops.words[w0] == VMQG_WORD_SHARE) {
+    const uint32_t gw = r->ops.words[w0 + 1];
+    const ERL_NIF_TERM have = store_get(&r->group_t, gw);
+    ErlNifBinary hb, gb;
+    if (!have || !enif_inspect_binary(env, have, &hb) || !enif_inspect_binary(env, group, &gb) || hb.size != gb.size ||
+        memcmp(hb.data, gb.data, gb.size) != 0) {
+      store_put(&r->group_t, gw, group);
+      ts_chunk* old = store_compact(&r->group_t, gw);
+      if (old) vmqgb_view_defer(r->view, chunk_retire_fn, old, 0, 0);
+    }
+  }
   return 0;
 }
 
@@ -535,6 +652,7 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
     }
   }
   vmqgb_batch_reset(b);
+  vmqgb_view_enter(r->view, b);   /* word ids from here to the fold: the grace period's reader */
   /* the batched prepare: rejected terms keep their error, the others are
    * prepared together */
   {
@@ -576,6 +694,36 @@ static ERL_NIF_TERM nif_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   return list;
 }
 
+/* counts(Ctx) -> [{Name, N}]: what the view holds now — live terms and
+ * ids, the library's live tables and memory (the reclamation's evidence;
+ * vmq_metrics can report them) */
+static ERL_NIF_TERM nif_counts(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  vmqg_res* r = get_res(env, argv[0]);
+  if (!r) return enif_make_badarg(env);
+  vmqg_stats_t st;
+  vmqgb_view_write_begin(r->view);
+  const uint64_t v[] = {vmqgb_live(r->subs), vmqgb_live(r->infos), vmqgb_live(r->nodes), vmqgb_live(r->mps),
+                        r->sub_t.live, r->info_t.live, r->sub_t.chunks + r->info_t.chunks + r->group_t.chunks,
+                        r->sub_t.compactions + r->info_t.compactions, r->terms_dropped};
+  uint64_t runs = 0;
+  int waiting = 0;
+  vmqgb_view_grace_stats(r->view, &runs, &waiting);
+  vmqgb_view_write_end(r->view);
+  const int rc = vmqgb_view_ctx_stats(r->view, &st);
+  if (rc) return error_term(env, rc);
+  const char* names[] = {"subscriber_ids", "subinfo_ids", "node_ids", "mountpoint_ids", "subscriber_terms",
+                         "subinfo_terms", "term_chunks", "term_compactions", "terms_dropped",
+                         "words", "paths", "keys", "topics", "host_bytes", "device_bytes", "subs",
+                         "deferred_runs", "deferred_lists_waiting"};
+  const uint64_t w[] = {st.words, st.paths, st.keys, st.topics, st.host_bytes, st.device_bytes, st.subs,
+                        runs, (uint64_t)waiting};
+  ERL_NIF_TERM items[18];
+  for (int i = 0; i < 18; i++)
+    items[i] = enif_make_tuple2(env, enif_make_atom(env, names[i]), enif_make_uint64(env, i < 9 ? v[i] : w[i - 9]));
+  return enif_make_list_from_array(env, items, 18);
+}
+
 /* stats(Ctx) -> {NrOfSubs + NrOfRemoteSubs, DeviceBytes} (vmq_reg_trie.erl:101-112) */
 static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   (void)argc;
@@ -610,6 +758,7 @@ RESCHEDULE(d_flush_init, nif_flush_init, ERL_NIF_DIRTY_JOB_CPU_BOUND)
 RESCHEDULE(d_match, nif_match, ERL_NIF_DIRTY_JOB_CPU_BOUND)
 RESCHEDULE(d_stats, nif_stats, ERL_NIF_DIRTY_JOB_CPU_BOUND)
 RESCHEDULE(d_commit, nif_commit, ERL_NIF_DIRTY_JOB_CPU_BOUND)
+RESCHEDULE(d_counts, nif_counts, ERL_NIF_DIRTY_JOB_CPU_BOUND)
 RESCHEDULE(d_set_option, nif_set_option, ERL_NIF_DIRTY_JOB_CPU_BOUND)
 
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
@@ -643,6 +792,7 @@ static ErlNifFunc funcs[] = {
     {"match", 4, d_match, 0},
     {"stats", 1, d_stats, 0},
     {"commit", 1, d_commit, 0},
+    {"counts", 1, d_counts, 0},
     {"set_option", 3, d_set_option, 0},
 };
 

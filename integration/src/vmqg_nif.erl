@@ -1,7 +1,7 @@
 %% vmqg_nif — NIF stubs of c_src/vmqg_nif.c (libvmqgpu behind vmq_reg_gpu_view).
 -module(vmqg_nif).
 -export([create/1, apply/3, apply_many/2, add_init/6, flush_init/1, batch_new/1, match/4, stats/1,
-         commit/1, set_option/3]).
+         commit/1, set_option/3, counts/1]).
 -on_load(init/0).
 
 init() ->
@@ -31,6 +31,8 @@ stats(_Ctx) -> erlang:nif_error(nif_not_loaded).
 %% Ctx -> ok | {error, term()}: ships changes left pending by an apply whose
 %% upload failed ({error, device}: they are kept, not lost)
 commit(_Ctx) -> erlang:nif_error(nif_not_loaded).
+%% Ctx -> [{atom(), non_neg_integer()}]: live terms, ids, tables and memory
+counts(_Ctx) -> erlang:nif_error(nif_not_loaded).
 %% Ctx, atom(), integer() -> ok | {error, term()} (vmqg_set_option)
 set_option(_Ctx, _Name, _Value) -> erlang:nif_error(nif_not_loaded).
 %% Errors: {error, invalid_topic | limit | nomem | device | busy | internal}

@@ -123,6 +123,7 @@ static volatile int writer_done;
  * anywhere); one output line per publish */
 static int one_batch(bt_t* a, vmqgb_batch* b, long* idx, size_t lo, size_t n, char** lines, sbuf* wout) {
   vmqgb_batch_reset(b);
+  vmqgb_view_enter(view, b);   /* as vmqg_nif.c: the reader section covers the prepare */
   const uint8_t** tp = (const uint8_t**)malloc(n * sizeof(*tp));
   size_t* tl = (size_t*)malloc(n * sizeof(size_t));
   uint32_t* mp = (uint32_t*)malloc(n * sizeof(uint32_t));

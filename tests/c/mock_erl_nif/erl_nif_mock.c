@@ -25,7 +25,11 @@ typedef struct cell {
   void* res;                 /* T_RES */
 } cell;
 
-struct enif_environment_t { int unused; };
+/* an environment owns the cells copied into it (enif_make_copy) and frees
+ * them with itself: a NIF that reads a term of a freed environment reads
+ * freed memory (ASan / the test's cell count see it) */
+struct enif_environment_t { struct cell** owned; size_t n, cap; };
+static long env_cells;   /* cells owned by live environments (mock_env_cells) */
 struct enif_resource_type_t { ErlNifResourceDtor* dtor; char name[64]; };
 
 typedef struct { ErlNifResourceType* type; long refs; } res_hdr;
@@ -46,7 +50,18 @@ void* enif_alloc(size_t size) { return malloc(size ? size : 1); }
 void* enif_realloc(void* ptr, size_t size) { return realloc(ptr, size ? size : 1); }
 void enif_free(void* ptr) { free(ptr); }
 ErlNifEnv* enif_alloc_env(void) { return (ErlNifEnv*)calloc(1, sizeof(ErlNifEnv)); }
-void enif_free_env(ErlNifEnv* env) { free(env); }
+void enif_free_env(ErlNifEnv* env) {
+  if (!env) return;
+  for (size_t i = 0; i < env->n; i++) {
+    free(env->owned[i]->bytes);
+    free(env->owned[i]->el);
+    free(env->owned[i]);
+  }
+  __atomic_fetch_sub(&env_cells, (long)env->n, __ATOMIC_RELAXED);
+  free(env->owned);
+  free(env);
+}
+long mock_env_cells(void) { return __atomic_load_n(&env_cells, __ATOMIC_RELAXED); }
 
 /* atoms are interned: one cell per name */
 static cell** atoms;
@@ -113,7 +128,34 @@ ERL_NIF_TERM enif_make_tuple_from_array(ErlNifEnv* env, const ERL_NIF_TERM arr[]
   return make_tuple(cnt, arr);
 }
 ERL_NIF_TERM enif_make_badarg(ErlNifEnv* env) { return enif_make_atom(env, "$badarg_exception"); }
-ERL_NIF_TERM enif_make_copy(ErlNifEnv* dst_env, ERL_NIF_TERM src_term) { (void)dst_env; return src_term; }
+static cell* owned_cell(ErlNifEnv* e, int type) {
+  cell* c = new_cell(type);
+  if (e->n == e->cap) {
+    e->cap = e->cap ? 2 * e->cap : 64;
+    e->owned = (cell**)realloc(e->owned, e->cap * sizeof(cell*));
+  }
+  e->owned[e->n++] = c;
+  __atomic_fetch_add(&env_cells, 1, __ATOMIC_RELAXED);
+  return c;
+}
+/* a deep copy owned by dst_env (atoms, [] and resources are shared, as in OTP) */
+ERL_NIF_TERM enif_make_copy(ErlNifEnv* dst_env, ERL_NIF_TERM src_term) {
+  const cell* a = C(src_term);
+  if (!dst_env || a->type == T_ATOM || a->type == T_NIL || a->type == T_RES) return src_term;
+  cell* c = owned_cell(dst_env, a->type);
+  c->i = a->i;
+  c->n = a->n;
+  if (a->type == T_BIN) {
+    c->bytes = (unsigned char*)malloc(a->n ? a->n : 1);
+    memcpy(c->bytes, a->bytes, a->n);
+  }
+  const size_t k = a->type == T_TUPLE ? a->n : a->type == T_MAP ? 2 * a->n : a->type == T_CONS ? 2 : 0;
+  if (k || a->type == T_TUPLE) {
+    c->el = (ERL_NIF_TERM*)malloc((k ? k : 1) * sizeof(ERL_NIF_TERM));
+    for (size_t i = 0; i < k; i++) c->el[i] = enif_make_copy(dst_env, a->el[i]);
+  }
+  return T(c);
+}
 ERL_NIF_TERM enif_make_resource(ErlNifEnv* env, void* obj) {
   (void)env;
   cell* c = new_cell(T_RES);

@@ -18,6 +18,13 @@
  *                                       inside a word, "~x" the atom x, "!" the empty list)
  *   M <records|ranges>                  match(Ctx, Batch, every publish so far, Mode)
  *   T                                   stats(Ctx)
+ *   Y <rounds> <per_round> <every>      churn cycles: per round, <per_round> new subscribers
+ *                                       (unique client ids and topic words: dev/<u>/state,
+ *                                       all/<u>/#, $share/g<r%5>/jobs/<u>) in one
+ *                                       apply_many, then all of them deleted in another;
+ *                                       every <every> rounds "Y <round> peak <counts>" and
+ *                                       "Y <round> empty <counts>" (counts/1 + the mock's
+ *                                       environment cells)
  *   X <name> <value>                    set_option(Ctx, name, value)
  *   R                                   commit(Ctx)
  * output: "A <result>", "S <result>...", "T <subs>", "M <n>" then per
@@ -36,6 +43,7 @@ ERL_NIF_TERM mock_make_int(int64_t v);
 ERL_NIF_TERM mock_make_map(size_t n, const ERL_NIF_TERM* keys, const ERL_NIF_TERM* vals);
 ERL_NIF_TERM mock_make_tuple(size_t n, const ERL_NIF_TERM* el);
 const char* mock_atom_name(ERL_NIF_TERM t);
+long mock_env_cells(void);
 void mock_print(FILE* f, ERL_NIF_TERM t);
 
 static ErlNifEntry* E;
@@ -253,6 +261,59 @@ int main(int argc, char** argv) {
         }
         fputc('\n', out);
       }
+    } else if (line[0] == 'Y') {
+      int rounds = 0, per = 0, every = 1;
+      if (sscanf(line + 2, "%d %d %d", &rounds, &per, &every) != 3 || per < 1 || every < 1) return 12;
+      ERL_NIF_TERM* ev = (ERL_NIF_TERM*)malloc((size_t)per * sizeof(ERL_NIF_TERM));
+      ERL_NIF_TERM* del = (ERL_NIF_TERM*)malloc((size_t)per * sizeof(ERL_NIF_TERM));
+      const ERL_NIF_TERM a_add = enif_make_atom(env, "add"), a_del = enif_make_atom(env, "del");
+      for (int rd = 0; rd < rounds; rd++) {
+        for (int i = 0; i < per; i++) {
+          char u[48], cid[48], grp[16];
+          snprintf(u, sizeof u, "u%d_%d", rd, i);
+          snprintf(cid, sizeof cid, "client_%d_%d", rd, i);
+          snprintf(grp, sizeof grp, "g%d", rd % 5);
+          const ERL_NIF_TERM sid = sid_term("-", cid);
+          const ERL_NIF_TERM t1[3] = {mock_make_binary("dev", 3), mock_make_binary(u, strlen(u)), mock_make_binary("state", 5)};
+          const ERL_NIF_TERM t2[3] = {mock_make_binary("all", 3), mock_make_binary(u, strlen(u)), mock_make_binary("#", 1)};
+          const ERL_NIF_TERM t3[4] = {mock_make_binary("$share", 6), mock_make_binary(grp, strlen(grp)),
+                                      mock_make_binary("jobs", 4), mock_make_binary(u, strlen(u))};
+          const ERL_NIF_TERM tops[3] = {enif_make_list_from_array(env, t1, 3), enif_make_list_from_array(env, t2, 3),
+                                        enif_make_list_from_array(env, t3, 4)};
+          ERL_NIF_TERM ca[3], cd[3];
+          for (int k = 0; k < 3; k++) {
+            const ERL_NIF_TERM el[4] = {a_add, tops[k], mock_make_int(k % 3), node_term(i % 9 == 0 ? 2u : 0u)};
+            const ERL_NIF_TERM eld[4] = {a_del, tops[k], mock_make_int(k % 3), node_term(i % 9 == 0 ? 2u : 0u)};
+            ca[k] = mock_make_tuple(4, el);
+            cd[k] = mock_make_tuple(4, eld);
+          }
+          const ERL_NIF_TERM e1[2] = {sid, enif_make_list_from_array(env, ca, 3)};
+          const ERL_NIF_TERM e2[2] = {sid, enif_make_list_from_array(env, cd, 3)};
+          ev[i] = mock_make_tuple(2, e1);
+          del[i] = mock_make_tuple(2, e2);
+        }
+        for (int ph = 0; ph < 2; ph++) {
+          const ERL_NIF_TERM args[2] = {ctx, enif_make_list_from_array(env, ph ? del : ev, (unsigned)per)};
+          const ERL_NIF_TERM r = call("apply_many", 2, args);
+          if (!enif_is_identical(r, ok)) { fprintf(out, "Y %d apply ", rd); mock_print(out, r); fputc('\n', out); }
+          if ((rd + 1) % every == 0 || rd == 0) {
+            fprintf(out, "Y %d %s", rd, ph ? "empty" : "peak");
+            const ERL_NIF_TERM cl = call("counts", 1, &ctx);
+            ERL_NIF_TERM h, t = cl;
+            while (enif_get_list_cell(env, t, &h, &t)) {
+              int ar;
+              const ERL_NIF_TERM* el;
+              ErlNifSInt64 x = 0;
+              enif_get_tuple(env, h, &ar, &el);
+              enif_get_int64(env, el[1], &x);
+              fprintf(out, " %s=%lld", mock_atom_name(el[0]), (long long)x);
+            }
+            fprintf(out, " env_cells=%ld\n", mock_env_cells());
+          }
+        }
+      }
+      free(ev);
+      free(del);
     } else if (line[0] == 'X') {
       long long v;
       if (sscanf(line + 2, "%63s %lld", a1, &v) != 2) return 11;

@@ -110,6 +110,7 @@ static void* batcher(void* p) {
   while (now() < a->t_end) {
     const double t0 = now();
     vmqgb_batch_reset(&b);
+    vmqgb_view_enter(view, &b);   /* as vmqg_nif.c: the reader section covers the prepare */
     if (lo + a->B > NPUB) lo = 0;
     if (vmqgb_batch_add_word_lists(&b, ctx, a->B, tmp0 + lo, wcnt + lo, wptr + woff[lo], wlen + woff[lo], idx))
       a->err = 1;

@@ -109,13 +109,17 @@ uint32_t Engine::intern(const uint8_t* b, size_t n, bool create) {
   return id;
 }
 
-// Stage end: words nothing holds any more become retired (tagged with the
-// grace token now); a retired word used again is simply in use again.
+// Stage end: words nothing holds any more are retired: taken out of the
+// dictionary at once (a lookup from now on misses them, as a word no filter
+// ever had), their ids reserved until a grace period taken after now ends
+// (vmqg_dict_release): readers that found them before still hold the ids.
 void Engine::retire_words() {
   for (uint32_t w : word_zero) {
-    if (word_refs[w] != 0) continue;
+    if (word_refs[w] != 0 || word_state[w] != 0) continue;
+    dict.erase(w);
     word_tag[w] = dict.retire_token;
-    if (word_state[w] == 0) { word_state[w] = 1; word_retired.push_back(w); }
+    word_state[w] = 1;
+    word_retired.push_back(w);
   }
   word_zero.clear();
 }
@@ -136,14 +140,14 @@ void Engine::collect_released_terms() {
   }
 }
 
-// vmqg_dict_release: words retired before `token` was taken and still
-// unreferenced are dropped from the dictionary and their ids become
-// reusable; dictionary tables replaced before it are freed.
+// vmqg_dict_release: the ids of words retired before `token` was taken are
+// reusable (their texts freed); dictionary tables replaced before it are
+// freed.  A retired word an op named again was revived (stage_ops).
 void Engine::release_words(uint64_t token) {
   size_t k = 0;
   for (uint32_t w : word_retired) {
-    if (word_refs[w] != 0) { word_state[w] = 0; continue; }
-    if (word_tag[w] < token) { dict.remove(w); word_state[w] = 2; words_released++; continue; }
+    if (word_state[w] != 1) continue;   // revived
+    if (word_tag[w] < token) { dict.release(w); word_state[w] = 2; words_released++; continue; }
     word_retired[k++] = w;
   }
   word_retired.resize(k);
@@ -495,8 +499,13 @@ void Engine::free_key(uint32_t k) {
 // A dropped path's device record is cleared (no edge leads to it: no walk
 // reads it; the clear keeps the image exact for a reused id).
 void Engine::reclaim() {
-  std::vector<uint32_t> work(dirty_paths.begin(), dirty_paths.end());
-  std::vector<uint32_t> tw(dirty_topics.begin(), dirty_topics.end());
+  // the stage's dirty paths and topics (as flush_incremental found them),
+  // plus the paths and topics free_key marked (already in those lists)
+  std::vector<uint32_t> work, tw;
+  work.swap(reclaim_paths);
+  tw.swap(reclaim_topics);
+  for (uint32_t p : dirty_paths) work.push_back(p);   // a flush without re-layout leaves them listed
+  for (uint32_t t : dirty_topics) tw.push_back(t);
   const NodeRec empty{0, kNone, 0, 0, 0, 0, 0, 0};
   while (!work.empty()) {
     const uint32_t p = work.back();
@@ -1090,6 +1099,13 @@ int Engine::stage_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
   staged = true;
   staged_epoch = epoch + 1;
   if (on_top) full_image = true;   // the failed commit's changes and this stage's: one image
+  // a word retired at an earlier stage end that an op names (interned before
+  // it retired, applied after) is put back under its id
+  for (size_t i = 0; i < n; i++)
+    for (uint32_t j = 0; j < ops[i].nwords; j++) {
+      const uint32_t w = words[ops[i].word_off + j];
+      if (w < word_state.size() && word_state[w] == 1) { dict.revive(w); word_state[w] = 0; word_zero.push_back(w); }
+    }
   if (top_mp > cfg.max_mountpoints) grow_mountpoints(top_mp);   // a new mountpoint past the roots
   // the edge table must absorb every edge this batch could add
   if ((edge_live + edge_tomb + add_words) * 10 > lay.edge_buckets * kEdgeSlotsPerBucket * 7) rebuild(add_words);
@@ -1109,6 +1125,9 @@ int Engine::stage_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
   const bool garbage_heavy = rec_garbage > lay.rec_cap / 2 || kl_garbage > lay.keylist_cap / 2 ||
                              xw_garbage > lay.exwords_cap / 2 ||
                              exact_tomb * 4 > lay.exact_buckets * kExactSlotsPerBucket;
+  // the candidates of reclaim(): a re-layout below clears the dirty lists
+  reclaim_paths.assign(dirty_paths.begin(), dirty_paths.end());
+  reclaim_topics.assign(dirty_topics.begin(), dirty_topics.end());
   if (garbage_heavy) rebuild(0, true);                // compaction
   else if (!flush_incremental()) rebuild(0);         // growth (writes every dirty item too)
   reclaim();   // paths and topics nothing holds any more (after their last writes)

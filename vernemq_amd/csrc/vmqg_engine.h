@@ -218,28 +218,40 @@ class WordDict {
     if (id == n) count_.store(n + 1, std::memory_order_release);
     return id;
   }
-  // Drops a word and releases its id for reuse (the writer only).  The caller
-  // guarantees that no reader that could still probe for it or hold its id
-  // is running (vmqg_dict_release's grace): its slot is marked erased (probes
-  // continue past it), its text freed.
-  void remove(uint32_t id) {
+  // Takes a word out of the table (the writer only): later lookups miss it
+  // (its slot is marked erased, probes continue past it); its id stays
+  // reserved and its text readable for the readers that found it before.
+  void erase(uint32_t id) {
     const std::string& w = text(id);
     const Key k = key(reinterpret_cast<const uint8_t*>(w.data()), w.size());
     const Table* t = tab_.load(std::memory_order_relaxed);
     Slot* sl = const_cast<Slot*>(t->slots.data());
     for (uint64_t i = k.h & t->mask;; i = (i + 1) & t->mask) {
       const uint32_t v = sl[i].id;
-      if (v == kVoid) break;   // not in the table (cannot happen for a live id)
-      if (v == id) { __atomic_store_n(&sl[i].id, kGone, __ATOMIC_RELEASE); gone_++; break; }
+      if (v == kVoid) return;   // not in the table
+      if (v == id) { __atomic_store_n(&sl[i].id, kGone, __ATOMIC_RELEASE); gone_++; live_--; return; }
     }
+  }
+  // An erased word put back under its id (an op that names it after all).
+  void revive(uint32_t id) {
+    const std::string& w = text(id);
+    const Key k = key(reinterpret_cast<const uint8_t*>(w.data()), w.size());
+    if (find(k) != kVoid) return;
+    const Table* t = tab_.load(std::memory_order_relaxed);
+    if ((live_ + gone_ + 1) * 2 > t->mask + 1) t = regrow((t->mask + 1) * 2);
+    put(*t, Slot{k.h, id, (uint32_t)k.n, k.k0, k.k1});
+    live_++;
+  }
+  // Frees an erased word's text and makes its id reusable (the writer only,
+  // once no reader that could hold the id is running: vmqg_dict_release).
+  void release(uint32_t id) {
     std::string().swap(dir_[id >> kChunkBits].load(std::memory_order_relaxed)[id & (kChunkWords - 1)]);
-    live_--;
     free_.push_back(id);
   }
   const std::string& text(uint32_t id) const {
     return dir_[id >> kChunkBits].load(std::memory_order_acquire)[id & (kChunkWords - 1)];
   }
-  // ids handed out so far are < id_bound(); live words = size()
+  // ids handed out so far are < id_bound(); words in the table = size()
   uint64_t id_bound() const { return count_.load(std::memory_order_acquire); }
   size_t size() const { return live_; }
   // words interned so far, reused ids included (the batch layer's staleness
@@ -428,6 +440,7 @@ struct Engine {
   FlatIndex topic_index;                                    // hash(mp, words) -> topic (verified)
   // ids of reclaimed paths / keys / topics, reused before new ones (Engine::reclaim)
   std::vector<uint32_t> free_paths, free_keys, free_topics;
+  std::vector<uint32_t> reclaim_paths, reclaim_topics;   // this stage's candidates (reclaim)
   uint64_t reclaimed_paths = 0, reclaimed_keys = 0, reclaimed_topics = 0;
   uint64_t n_trie_nodes = 0, n_trie_topics = 0, n_subs_objects = 0, n_fanout = 0, n_remote_keys = 0;
 
