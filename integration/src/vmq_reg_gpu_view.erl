@@ -87,6 +87,10 @@
 %% an apply whose upload failed stays pending in the library; the commit is
 %% retried after this many ms (and by the next apply)
 -define(COMMIT_RETRY_MS, 100).
+%% reclamation of dropped terms / words waits for the batchers' grace periods
+%% and runs in the writer: at every apply, and at least this often when
+%% subscriptions are quiet (vmqg_nif:commit/1 with nothing pending)
+-define(RECLAIM_MS, 1000).
 
 -record(state, {ctx,                    % vmqg_nif resource (vmqg_ctx + term tables)
                 batchers,               % tuple of vmq_reg_gpu_batcher pids
@@ -266,6 +270,7 @@ init([]) ->
               Self ! {subscribers_loaded, Skipped}
       end),
     EventHandler = vmq_reg:subscribe_subscriber_changes(),
+    erlang:send_after(?RECLAIM_MS, self(), reclaim),
     {ok, #state{ctx=Ctx, batchers=Batchers, event_handler=EventHandler}}.
 
 handle_call({event, Event}, _From, State) ->
@@ -283,6 +288,10 @@ handle_info({subscribers_loaded, Skipped}, #state{event_queue=Q} = State) ->
     {Subs, _} = stats(),
     lager:info("loaded ~p subscriptions into ~p (~p skipped)", [Subs, ?MODULE, Skipped]),
     {noreply, State1#state{event_queue=undefined}};
+handle_info(reclaim, #state{ctx=Ctx} = State) ->
+    _ = vmqg_nif:commit(Ctx),   % runs the reclamation that is due (c_src/vmqg_batch.c grace periods)
+    erlang:send_after(?RECLAIM_MS, self(), reclaim),
+    {noreply, State};
 handle_info(retry_commit, #state{ctx=Ctx} = State) ->
     %% changes of an apply whose upload failed: pending in the library until
     %% a commit goes through (this one, or the next apply's)
