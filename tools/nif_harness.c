@@ -17,6 +17,7 @@
  * Sections (argv[2..], default all):
  *   scale    1..48 batchers, records and ranges
  *   devrec   records copied by the device over PCIe (vmqgb_view_set_device_records)
+ *   (VMQGB_RECLAIM=0: dropped rows kept, for an A/B of reclamation)
  *   churn    subscriber events at 100k/s (config D's 1 %/s of 10M) while 16
  *            and 32 batchers run, applied the way the Erlang view applies
  *            them (vmq_reg_gpu_view's drain_events + vmqg_nif:apply_many):
@@ -399,6 +400,7 @@ int main(int argc, char** argv) {
   ctx = vmqg_create(&cfg, &err);
   if (!ctx) { fprintf(stderr, "vmqg_create: %d\n", err); return 1; }
   view = vmqgb_view_new(ctx);
+  if (getenv("VMQGB_RECLAIM")) vmqg_set_option(ctx, "reclaim", atoi(getenv("VMQGB_RECLAIM")));   /* A/B of reclamation */
   /* subscriptions through the NIF's op layer; subscriber id = device index
    * (c{d}), the wildcard subscribers after them */
   vmqgb_ops ops;

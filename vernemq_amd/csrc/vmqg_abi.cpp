@@ -715,6 +715,9 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   } else if (n == "count_bpc" || n == "emit_bpc") {
     if (value < 0 || value > 32) return VMQG_E_INVAL;
     (n == "count_bpc" ? e.opt_count_bpc : e.opt_emit_bpc) = (uint32_t)value;
+  } else if (n == "reclaim") {   // 0: dropped paths / keys / topics / words are kept (memory for speed)
+    if (value < 0 || value > 1 || e.replica) return VMQG_E_INVAL;
+    e.opt_reclaim = (uint32_t)value;
   } else if (n == "fail_commits") {   // test hook: the next `value` commits fail as a device error would
     if (value < 0 || value > 1000 || e.replica) return VMQG_E_INVAL;
     e.fault_commits = (uint32_t)value;

@@ -1120,18 +1120,23 @@ int Engine::stage_ops(const vmqg_op* ops, size_t n, const uint32_t* words, size_
   // subscriber-list keys left empty go before the flush writes the paths and
   // exact slots that name them (vmq_reg_trie deletes such rows,
   // vmq_reg_trie.erl:472-496)
-  for (size_t i = 0; i < dirty_keys.size(); i++)
-    if (keys[dirty_keys[i]].vals.empty() && keys[dirty_keys[i]].topic_id != kNone) free_key(dirty_keys[i]);
+  if (opt_reclaim)
+    for (size_t i = 0; i < dirty_keys.size(); i++)
+      if (keys[dirty_keys[i]].vals.empty() && keys[dirty_keys[i]].topic_id != kNone) free_key(dirty_keys[i]);
   const bool garbage_heavy = rec_garbage > lay.rec_cap / 2 || kl_garbage > lay.keylist_cap / 2 ||
                              xw_garbage > lay.exwords_cap / 2 ||
                              exact_tomb * 4 > lay.exact_buckets * kExactSlotsPerBucket;
   // the candidates of reclaim(): a re-layout below clears the dirty lists
-  reclaim_paths.assign(dirty_paths.begin(), dirty_paths.end());
-  reclaim_topics.assign(dirty_topics.begin(), dirty_topics.end());
+  if (opt_reclaim) {
+    reclaim_paths.assign(dirty_paths.begin(), dirty_paths.end());
+    reclaim_topics.assign(dirty_topics.begin(), dirty_topics.end());
+  }
   if (garbage_heavy) rebuild(0, true);                // compaction
   else if (!flush_incremental()) rebuild(0);         // growth (writes every dirty item too)
-  reclaim();   // paths and topics nothing holds any more (after their last writes)
-  retire_words();
+  if (opt_reclaim) {
+    reclaim();   // paths and topics nothing holds any more (after their last writes)
+    retire_words();
+  }
   for (size_t i = 0; i < n; i++) {   // the ops' terms: reported if no record holds them
     term_cand[0].push_back(ops[i].subscriber);
     term_cand[1].push_back(ops[i].subinfo);

@@ -441,6 +441,7 @@ struct Engine {
   // ids of reclaimed paths / keys / topics, reused before new ones (Engine::reclaim)
   std::vector<uint32_t> free_paths, free_keys, free_topics;
   std::vector<uint32_t> reclaim_paths, reclaim_topics;   // this stage's candidates (reclaim)
+  uint32_t opt_reclaim = 1;                                // vmqg_set_option "reclaim": 0 keeps dropped rows
   uint64_t reclaimed_paths = 0, reclaimed_keys = 0, reclaimed_topics = 0;
   uint64_t n_trie_nodes = 0, n_trie_topics = 0, n_subs_objects = 0, n_fanout = 0, n_remote_keys = 0;
 
