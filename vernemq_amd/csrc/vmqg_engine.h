@@ -87,10 +87,18 @@ class FlatIndex {
   void prefetch(uint64_t key) const {
     if (!slots_.empty()) __builtin_prefetch(&slots_[mix64(key) & (slots_.size() - 1)]);
   }
+  // (key, val) must not be stored already; an erased slot on the probe path
+  // is taken before an empty one, so erase + insert churn leaves no trail of
+  // tombstones (a table full of them would be rehashed: a stall of the stage)
   void insert(uint64_t key, uint32_t val) {
     if ((n_ + gone_ + 1) * 2 > slots_.size())   // mostly tombstones: rehash at the same size
       regrow(std::max<uint64_t>(1024, (n_ + 1) * 4 > slots_.size() ? slots_.size() * 2 : slots_.size()));
-    put(key, val);
+    const uint64_t m = slots_.size() - 1;
+    uint64_t i = mix64(key) & m, reuse = ~0ull;
+    for (; slots_[i].val != kVoid; i = (i + 1) & m)
+      if (slots_[i].val == kGone && reuse == ~0ull) reuse = i;
+    if (reuse != ~0ull) { i = reuse; gone_--; }
+    slots_[i] = Slot{key, val};
     n_++;
   }
   // erases the entry (key, val); false if absent
@@ -212,7 +220,7 @@ class WordDict {
       dir_[id >> kChunkBits].store(chunk, std::memory_order_release);
     }
     chunk[id & (kChunkWords - 1)].assign(reinterpret_cast<const char*>(k.p), k.n);
-    put(*t, Slot{k.h, id, (uint32_t)k.n, k.k0, k.k1});
+    if (put(*t, Slot{k.h, id, (uint32_t)k.n, k.k0, k.k1})) gone_--;
     live_++;
     gen_.fetch_add(1, std::memory_order_release);
     if (id == n) count_.store(n + 1, std::memory_order_release);
@@ -239,7 +247,7 @@ class WordDict {
     if (find(k) != kVoid) return;
     const Table* t = tab_.load(std::memory_order_relaxed);
     if ((live_ + gone_ + 1) * 2 > t->mask + 1) t = regrow((t->mask + 1) * 2);
-    put(*t, Slot{k.h, id, (uint32_t)k.n, k.k0, k.k1});
+    if (put(*t, Slot{k.h, id, (uint32_t)k.n, k.k0, k.k1})) gone_--;
     live_++;
   }
   // Frees an erased word's text and makes its id reusable (the writer only,
@@ -295,15 +303,23 @@ class WordDict {
         return id;
     }
   }
-  // the id is stored last: a reader that sees it sees the slot's other fields
-  static void put(const Table& t, const Slot& s) {
+  // The id is stored last: a reader that sees it sees the slot's other
+  // fields.  An erased slot on the probe path is taken before an empty one
+  // (churn leaves no trail of tombstones to rehash); a reader that loaded the
+  // erased word's id before compares the new fields with its key: no match
+  // unless it is the same word, interned again — then it returns the old id,
+  // which its grace period keeps from being reused (a lookup from before the
+  // new subscription).  Returns whether an erased slot was taken.
+  static bool put(const Table& t, const Slot& s) {
     Slot* sl = const_cast<Slot*>(t.slots.data());
-    for (uint64_t i = s.h & t.mask;; i = (i + 1) & t.mask)
-      if (sl[i].id == kVoid) {
+    for (uint64_t i = s.h & t.mask;; i = (i + 1) & t.mask) {
+      const uint32_t v = sl[i].id;
+      if (v == kVoid || v == kGone) {
         sl[i].h = s.h; sl[i].len = s.len; sl[i].k0 = s.k0; sl[i].k1 = s.k1;
         __atomic_store_n(&sl[i].id, s.id, __ATOMIC_RELEASE);
-        return;
+        return v == kGone;
       }
+    }
   }
   const Table* regrow(uint64_t want) {
     uint64_t cap = 1;
