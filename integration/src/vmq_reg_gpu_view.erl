@@ -73,8 +73,10 @@
          code_change/3]).
 
 -define(SERVER, ?MODULE).
-%% subscriber events applied per vmqg_nif:apply_many/2 at most
--define(MAX_COALESCE, 10000).
+%% subscriber events applied per vmqg_nif:apply_many/2 at most: a backlog
+%% goes out in slices of this many (each lands within ~1 ms of host stage, so
+%% the first events of a backlog do not wait for the last)
+-define(MAX_COALESCE, 1000).
 %% the coalescing window: an apply waits at most this long after its first
 %% event for more, or until it has this many
 -define(WINDOW_MS, 2).

@@ -200,7 +200,7 @@ static void* applier(void* p) {   /* the vmq_reg_gpu_view gen_server */
     /* the window: 2 ms after its first event, or 1,000 events (vmq_reg_gpu_view) */
     if (c->coalesce && n && n < 1000 && now() - c->q[c->head % c->cap].t < 0.002) n = 0;
     if (!c->coalesce && n > 1) n = 1;
-    if (n > 10000) n = 10000;
+    if (n > 1000) n = 1000;   /* one apply takes at most 1,000 events: a backlog goes out in slices (vmq_reg_gpu_view ?MAX_COALESCE) */
     for (size_t i = 0; i < n; i++) grp[i] = c->q[(c->head + i) % c->cap];
     c->head += n;
     pthread_mutex_unlock(&c->mu);
