@@ -462,6 +462,9 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "trieless"  0 | 1      tables without any wildcard / $share filter: COUNT is
  *                          one exact-table probe per publish, four publishes per
  *                          lane in flight (default 1; 0: the general walk)
+ *   "fused"     0 | 1      trie-less tables: COUNT, the offset scan and EMIT in one
+ *                          launch, tiles chained by look-back (default 1; 0: the
+ *                          three trie-less launches)
  *   "root_flags" 0 | 1     a walk starts from its root's cached child flags, so a
  *                          mountpoint without wildcard / $share filters walks
  *                          nothing (default 1; 0: the root's three probes)

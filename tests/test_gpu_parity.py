@@ -1308,23 +1308,26 @@ def test_trieless_tables_take_the_exact_only_count(mode):
     outs = {}
     # fast_g 1 / 2 / 4: chunks of 64 / 32 / 16 publishes, which the trie-less
     # EMIT (k_emit_exact, 64-publish blocks) must position alike
+    # fused 1 (the default): the trie-less COUNT, scan and EMIT in one launch
     for fg in (1, 2, 4):
         v.set_option("fast_g", fg)
-        for tl, hm in ((1, 0), (0, 0), (1, 8), (0, 8)):
+        for tl, hm, fu in ((1, 0, 1), (1, 0, 0), (0, 0, 1), (1, 8, 1), (0, 8, 1)):
             v.set_option("trieless", tl)
             v.set_option("heavy_min", hm)
+            v.set_option("fused", fu)
             arr, words = v.prepare([(mp, tuple(t)) for mp, t in pubs])
             recs, offs = prod.match_arrays(arr, words)
-            outs[tl, hm, fg] = (np.asarray(offs).copy(), np.asarray(recs).view(np.uint8).copy())
+            outs[tl, hm, fg, fu] = (np.asarray(offs).copy(), np.asarray(recs).view(np.uint8).copy())
             got = prod.fold_batch(pubs)
             bad = [i for i in range(len(pubs)) if sorted(got[i]) != want[i]]
-            assert not bad, (fg, tl, hm, len(bad), pubs[bad[0]], sorted(got[bad[0]])[:4], want[bad[0]][:4])
-        for hm in (0, 8):
-            a, b = outs[1, hm, fg], outs[0, hm, fg]
-            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), (fg, hm)
+            assert not bad, (fg, tl, hm, fu, len(bad), pubs[bad[0]], sorted(got[bad[0]])[:4], want[bad[0]][:4])
+        for a, b in (((1, 0, fg, 1), (1, 0, fg, 0)), ((1, 0, fg, 0), (0, 0, fg, 1)), ((1, 8, fg, 1), (0, 8, fg, 1))):
+            assert np.array_equal(outs[a][0], outs[b][0]), (a, b, "offsets")
+            assert np.array_equal(outs[a][1], outs[b][1]), (a, b, "entries")
     v.set_option("fast_g", 0)
     v.set_option("trieless", 1)
     v.set_option("heavy_min", 0)
+    v.set_option("fused", 1)
 
 
 @pytest.mark.parametrize("mode", MODES)

@@ -48,11 +48,16 @@ VARIANTS = {
     "emitexk4": ["-DVMQG_EMIT_EXK=4"],
     "ddpct67": ["-DVMQG_DD_ON_PCT=67"],
     "exact2x": ["-DVMQG_EXACT_SLOTS_PER_TOPIC=2"],
+    "fxk2": ["-DVMQG_FX_K=2"],
+    "fxk8": ["-DVMQG_FX_K=8"],
+    "fxbpc8": ["-DVMQG_FX_BPC=8"],
+    "fxk2bpc8": ["-DVMQG_FX_K=2", "-DVMQG_FX_BPC=8"],
 }
+OUT_DIR = os.environ.get("VMQG_AB_DIR", os.path.join(ROOT, "build", "ab"))
 
 
 def build(name, flags):
-    out = os.path.join(ROOT, "build", "ab", "lib_%s.so" % name)
+    out = os.path.join(OUT_DIR, "lib_%s.so" % name)
     srcs = _lib.SOURCES
     if name.startswith("git_"):   # the library as committed at a revision (sources exported to build/ab/src_<rev>)
         rev = name[4:]
@@ -69,7 +74,7 @@ def build(name, flags):
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
-    os.makedirs(os.path.join(ROOT, "build", "ab"), exist_ok=True)
+    os.makedirs(OUT_DIR, exist_ok=True)
     with ThreadPoolExecutor(4) as ex:
         for name, rc, err in ex.map(lambda n: build(n, VARIANTS.get(n, [])), names):
             print(name, "ok" if rc == 0 else "FAILED\n" + err)

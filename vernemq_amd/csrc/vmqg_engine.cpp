@@ -1648,7 +1648,8 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   if (order_on(st) != VMQG_OK) return VMQG_E_DEVICE;
   if (npub == 0) return hipMemsetAsync(d_offsets, 0, 8, st) == hipSuccess ? VMQG_OK : VMQG_E_DEVICE;
   int rc;
-  if ((rc = ensure_match_scratch(npub, st)) || (rc = ensure_lookback(scan_tiles((npub + 15) / 16), st)) ||
+  if ((rc = ensure_match_scratch(npub, st)) ||
+      (rc = ensure_lookback(std::max<uint64_t>(scan_tiles((npub + 15) / 16), exact_fused_tiles(npub)), st)) ||
       (rc = ensure_wave_scratch(st)))
     return rc;
   MatchArgs a = args_for(d_pubs_, npub, d_words_, d_offsets);
@@ -1674,6 +1675,17 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   if (a.dd_claimed && (launch_dd_claim(a, st, ev[10], ev[11]) != hipSuccess ||
                        launch_dd_classify(a, st, ev[12], ev[13]) != hipSuccess))
     return VMQG_E_DEVICE;
+  // trie-less tables: COUNT, scan and EMIT in one launch, then the EMIT tail
+  // (huge publishes); the stages it replaces record no time
+  if (opt_fused && a.trieless && !a.dd_claimed && a.groups == nullptr && a.heavy_min == 0) {
+    if (timing)
+      for (int k = 2; k < 8; k++) { hipEventDestroy(ev[k]); ev[k] = nullptr; t_ev.back()[k] = nullptr; }
+    if (launch_exact_fused(a, st, ev[0], ev[1]) != hipSuccess) return VMQG_E_DEVICE;
+    debug_sync(st, "fused COUNT/EMIT");
+    if (launch_match(a, 1, 1, st, ev[8], ev[9]) != hipSuccess) return VMQG_E_DEVICE;
+    debug_sync(st, "EMIT tail");
+    return VMQG_OK;
+  }
   // COUNT: fast groups (with dedupe on, the representatives, then the
   // duplicates' fix-up), then the wave tier for what they deferred
   if (launch_match(a, 0, 0, st, ev[0], ev[1]) != hipSuccess) return VMQG_E_DEVICE;

@@ -82,5 +82,10 @@ hipError_t launch_dd_fixup(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = n
 // exact-filter auto mode: samples 4,096 publishes' filter bits, the last
 // block writes the next calls' filter mode to dd_host[1]
 hipError_t launch_ex_sample(const MatchArgs& a, hipStream_t st);
+// trie-less tables: COUNT, scan and EMIT (records or ranges) in one launch,
+// tiles chained by look-back (a.lookback >= exact_fused_tiles granules);
+// huge records-mode publishes are left to the EMIT tail
+hipError_t launch_exact_fused(const MatchArgs& a, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+uint32_t exact_fused_tiles(uint64_t npub);
 
 }  // namespace vmqg

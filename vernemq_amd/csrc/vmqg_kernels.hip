@@ -2626,6 +2626,254 @@ static void launch_emit_exact(const MatchArgs& a, bool nt, hipStream_t st, hipEv
   }
 }
 
+// ================ COUNT, scan and EMIT in one launch over trie-less tables
+// (option "fused", on by default).  The trie-less COUNT above hands EMIT a
+// 32-B key cache, a heavy byte and an offset per publish through HBM and
+// EMIT reads them back behind a scan launch; here one kernel probes, counts,
+// scans and writes: tiles of kFxTile publishes taken by ticket, each wave
+// kFxK 64-publish chunks with all their probes in flight (as
+// k_count_exact), the tile's base from a decoupled look-back, then every
+// publish's offset and entries.  Nothing is handed over except a huge
+// records-mode publish (>= kHugeRecords records): its key cache and the
+// tail's list, as k_count_exact leaves them.  Remote nodes >= 64 (the exact
+// slot's high list) are emitted here too, from exwords.
+#ifndef VMQG_FX_K
+#define VMQG_FX_K 4   // 64-publish chunks per wave per tile (A/B on R1)
+#endif
+#ifndef VMQG_FX_BPC
+#define VMQG_FX_BPC 4   // fused blocks per CU
+#endif
+constexpr uint32_t kFxK = VMQG_FX_K;
+constexpr uint32_t kFxTile = kWaves * kFxK * 64;
+struct FxWave {
+  uint32_t off[64], cnt[64], hoff[64], nh[64];
+  uint64_t rm[64], ob[64];
+  uint32_t crel[65];
+};
+struct FxLds {
+  uint64_t wtot[kWaves];
+  uint64_t base;
+  uint32_t tile;
+  FxWave w[kWaves];
+};
+
+// the r-th entry of a publish: its key's records, then its remote nodes
+// (< 64 from the mask, then the high list), as fold_/5 (vmq_reg_trie.erl:68-84)
+__device__ __forceinline__ uint4 fx_emission(const MatchArgs& a, uint32_t off, uint32_t cnt, uint64_t rm, uint32_t hoff,
+                                             uint32_t r) {
+  if (r < cnt) return *reinterpret_cast<const uint4*>(a.records + off + r);
+  const uint32_t nr = (uint32_t)__popcll(rm);
+  const uint32_t node = r - cnt < nr ? select_bit(rm, r - cnt) : a.exwords[hoff + 1 + (r - cnt - nr)];
+  return make_uint4((VMQG_EMIT_REMOTE << 24) | node, kNone, kNone, kNone);
+}
+
+template <int OUT, bool NT>
+__global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
+  __shared__ FxLds S;
+  if (blockIdx.x == 0 && threadIdx.x < kStWords) a.status_next[threadIdx.x] = 0;
+  const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+  FxWave& W = S.w[wv];
+  const uint32_t ntiles = (a.npub + kFxTile - 1) / kFxTile;
+  const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
+  for (;;) {
+    if (threadIdx.x == 0) S.tile = atomicAdd(&a.status[kStTicket], 1u);
+    __syncthreads();
+    const uint32_t tile = S.tile;
+    if (tile >= ntiles) break;
+    const uint32_t p0 = tile * kFxTile + wv * (kFxK * 64);
+    // ---- probes (k_count_exact's, kFxK chunks in flight)
+    vmqg_pub pub[kFxK];
+    bool look[kFxK];
+    uint64_t fp[kFxK];
+#pragma unroll
+    for (uint32_t k = 0; k < kFxK; k++) {
+      const uint32_t p = p0 + k * 64 + lane;
+      pub[k] = p < a.npub ? a.pubs[p] : vmqg_pub{0xFFFFFFFFu, 0, 0, 0};
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kFxK; k++) {
+      const uint32_t L = pub[k].nwords;
+      const uint32_t* w = a.words + pub[k].word_off;
+      look[k] = pub[k].mountpoint < a.max_mp && L > 0;
+      uint64_t part = 0;
+      bool wild = false;
+      for (uint32_t i = 0; look[k] && i < L; i++) {
+        const uint32_t x = w[i];
+        part += fp_word(x, i);
+        wild |= x == kPlus || x == kHash;
+      }
+      fp[k] = fp_final(part, pub[k].mountpoint, L);
+      if (look[k] && !wild && a.exfilter) {
+        const uint64_t xb = exbit_of(fp[k], a.exbits_mask + 1);
+        look[k] = ((a.exbits[xb >> 5] >> (xb & 31)) & 1u) != 0;
+      }
+    }
+    uint4 h0[kFxK];
+#pragma unroll
+    for (uint32_t k = 0; k < kFxK; k++)
+      if (look[k]) h0[k] = *reinterpret_cast<const uint4*>(&a.exact[(fp[k] & a.exact_mask) * kExactSlotsPerBucket]);
+    uint32_t off[kFxK], cnt[kFxK], hoff[kFxK], nh[kFxK], tot[kFxK];
+    uint64_t rm[kFxK];
+    uint4 one[kFxK];   // a one-record publish's record, loaded while the tile is scanned
+#pragma unroll
+    for (uint32_t k = 0; k < kFxK; k++) {
+      const uint32_t L = pub[k].nwords;
+      const uint32_t* w = a.words + pub[k].word_off;
+      bool found = false;
+      uint4 hit{0, 0, 0, 0};
+      uint32_t hi_at = kNone;
+      if (look[k]) {
+        uint64_t b = fp[k] & a.exact_mask;
+        uint4 s0 = h0[k];
+        for (uint64_t iter = 0; iter <= a.exact_mask && !found; iter++) {
+          const ExactSlot* bk = a.exact + b * kExactSlotsPerBucket;
+          bool empty = false;
+#pragma unroll
+          for (uint32_t j = 0; j < kExactSlotsPerBucket; j++) {
+            if (found || empty) continue;
+            const uint4 sj = j == 0 ? s0 : *reinterpret_cast<const uint4*>(&bk[j]);
+            if (sj.z == kEmpty) { empty = true; continue; }
+            const uint64_t f = ((uint64_t)sj.y << 32) | sj.x;
+            if (f != fp[k] || (sj.z & ~kExactHigh) != L) continue;
+            const uint4* q = reinterpret_cast<const uint4*>(&bk[j]);
+            const uint4 q2 = q[2];
+            bool diff = q2.x != pub[k].mountpoint;
+            diff |= (L > 0 && q2.y != w[0]) || (L > 1 && q2.z != w[1]) || (L > 2 && q2.w != w[2]);
+            if (!diff && L > 3) {
+              const uint4 q3 = q[3];
+              diff |= q3.x != w[3] || (L > 4 && q3.y != w[4]) || (L > 5 && q3.z != w[5]) || (L > 6 && q3.w != w[6]);
+            }
+            for (uint32_t i = kExactInline; !diff && i < L; i++) diff |= a.exwords[sj.w + (i - kExactInline)] != w[i];
+            if (!diff) {
+              found = true;
+              hit = q[1];
+              if (sj.z & kExactHigh) hi_at = sj.w + exact_tail_words(L);   // {count, node ids} of nodes >= 64
+            }
+          }
+          if (found || empty) break;
+          b = (b + 1) & a.exact_mask;
+          s0 = *reinterpret_cast<const uint4*>(&a.exact[b * kExactSlotsPerBucket]);
+        }
+      }
+      off[k] = hit.x;
+      cnt[k] = hit.y;
+      if (OUT == 0 && hit.y == 1) one[k] = *reinterpret_cast<const uint4*>(a.records + hit.x);
+      rm[k] = ((uint64_t)hit.w << 32) | hit.z;
+      if (a.local_node < kLowNodes) rm[k] &= ~(1ull << a.local_node);
+      hoff[k] = hi_at;
+      nh[k] = hi_at != kNone ? a.exwords[hi_at] : 0u;
+      const uint32_t nr = (uint32_t)__popcll(rm[k]) + nh[k];
+      tot[k] = OUT ? (cnt[k] ? 1u : 0u) + nr : cnt[k] + nr;
+    }
+    // ---- offsets: lane, chunk and wave prefixes, the tile's base by look-back
+    uint64_t incl[kFxK], cpre[kFxK], wsum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kFxK; k++) {
+      incl[k] = wave_incl_scan64(tot[k]);
+      cpre[k] = wsum;
+      wsum += __shfl(incl[k], 63, 64);
+    }
+    if (lane == 0) S.wtot[wv] = wsum;
+    __syncthreads();
+    if (wv == 0) {
+      uint64_t agg = 0;
+#pragma unroll
+      for (uint32_t x = 0; x < kWaves; x++) agg += S.wtot[x];
+      const uint64_t b = lookback(a.lookback, a.lb_tag, a.err, tile, agg);
+      if (lane == 0) {
+        S.base = b;
+        if (tile == ntiles - 1) a.offsets[a.npub] = b + agg;   // the batch total
+      }
+    }
+    __syncthreads();
+    uint64_t wbase = S.base;
+    for (uint32_t x = 0; x < wv; x++) wbase += S.wtot[x];
+    // ---- entries
+#pragma unroll 1
+    for (uint32_t k = 0; k < kFxK; k++) {
+      const uint32_t p = p0 + k * 64 + lane;
+      const bool valid = p < a.npub;
+      const uint64_t ob = wbase + cpre[k] + incl[k] - tot[k];
+      if (valid) a.offsets[p] = ob;
+      bool ok = valid && tot[k] > 0;
+      if (ok && ob + tot[k] > cap) { atomicOr(a.err, kErrOverflow); ok = false; }
+      if constexpr (OUT == 1) {
+        if (ok) {
+          uint64_t o = ob;
+          if (cnt[k]) store_range(a.out_rng, o++, off[k], cnt[k]);
+          for (uint64_t m = rm[k]; m; m &= m - 1) store_range(a.out_rng, o++, (uint32_t)__builtin_ctzll(m), 0u);
+          for (uint32_t i = 0; i < nh[k]; i++) store_range(a.out_rng, o++, a.exwords[hoff[k] + 1 + i], 0u);
+        }
+      } else {
+        // a huge publish: the EMIT tail copies it with every wave (its key cache and list, as k_count_exact)
+        const bool huge = ok && tot[k] >= kHugeRecords && nh[k] == 0;
+        if (huge) {
+          uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
+          const uint32_t nk = cnt[k] ? 1u : 0u;
+          kc[0] = make_uint4(tot[k], nk | kHugeFlag, (uint32_t)rm[k], (uint32_t)(rm[k] >> 32));
+          kc[1] = make_uint4(nk ? off[k] : 0u, cnt[k], 0u, 0u);
+          a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
+          ok = false;
+        }
+        if (ok && tot[k] == 1) {   // one entry: this lane writes it (the chunk's stores coalesce)
+          store_rec<NT>(a.out, ob, cnt[k] == 1 ? one[k] : fx_emission(a, off[k], cnt[k], rm[k], hoff[k], 0));
+          ok = false;
+        }
+        // the others: the whole wave over their concatenated entries, U per lane in flight
+        if (__ballot(ok)) {
+          const uint32_t sp = ok ? tot[k] : 0u;
+          const uint32_t in32 = wave_incl_scan32(sp);
+          W.off[lane] = off[k]; W.cnt[lane] = cnt[k]; W.rm[lane] = rm[k]; W.hoff[lane] = hoff[k];
+          W.ob[lane] = ob;
+          W.crel[lane] = in32 - sp;
+          if (lane == 63) W.crel[64] = in32;
+          wave_sync();
+          const uint32_t T = W.crel[64];
+          constexpr int U = 4;
+          uint32_t q = 0;
+          for (uint32_t r0 = lane; r0 < T; r0 += 64 * U) {
+            uint4 v[U];
+            uint64_t dst[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+              const uint32_t r = r0 + 64 * u;
+              if (r < T) {
+                while (q + 1 < 64 && W.crel[q + 1] <= r) q++;
+                const uint32_t rr = r - W.crel[q];
+                v[u] = fx_emission(a, W.off[q], W.cnt[q], W.rm[q], W.hoff[q], rr);
+                dst[u] = W.ob[q] + rr;
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+              if (r0 + 64 * u < T) store_rec<NT>(a.out, dst[u], v[u]);
+          }
+          wave_sync();
+        }
+      }
+    }
+    __syncthreads();   // the next tile reuses S
+  }
+}
+
+hipError_t launch_exact_fused(const MatchArgs& a, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+  uint32_t g = (a.npub + kFxTile - 1) / kFxTile;
+  const uint32_t cap = (uint32_t)a.cus * VMQG_FX_BPC;   // only started blocks take tickets: no look-back waits on an unstarted tile
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  const bool nt = (a.opts & kOptNtStores) != 0;
+  auto go = [&](auto kern) {
+    if (t0) hipExtLaunchKernelGGL(kern, dim3(g), dim3(256), 0, st, t0, t1, 0, a);
+    else kern<<<g, 256, 0, st>>>(a);
+  };
+  if (a.out_rng) go(k_match_exact_fused<1, false>);
+  else if (nt) go(k_match_exact_fused<0, true>);
+  else go(k_match_exact_fused<0, false>);
+  return hipGetLastError();
+}
+
+uint32_t exact_fused_tiles(uint64_t npub) { return (uint32_t)((npub + kFxTile - 1) / kFxTile); }
+
 template <int MODE, int OUT, int G, bool NT, int CH = 64 / G>
 static void launch_fast_k(const MatchArgs& a, uint32_t g, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
   // COUNT with dedupe or output groups on: the FEAT variant
