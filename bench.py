@@ -569,6 +569,7 @@ def bench_other(args):
             last[0] = time.time()
             log("config %s: %d / %d subscriptions loaded (%.0fs)" % (args.config, done, total, time.time() - t0))
 
+    apply_opts(view, args)   # layout knobs ("exact_one") take effect on the load
     w.load_into(view, progress=progress)
     load_s = time.time() - t0
     fast_g = args.fast_g

@@ -465,6 +465,10 @@ int vmqg_dump(vmqg_ctx* ctx, const char** text, size_t* len);
  *   "fused"     0 | 1      trie-less tables: COUNT, the offset scan and EMIT in one
  *                          launch, tiles chained by look-back (default 1; 0: the
  *                          three trie-less launches)
+ *   "exact_one" 0 | 1      a topic of <= 3 words with one local record keeps the
+ *                          record in its exact slot, so the trie-less match
+ *                          writes it without reading the record table (default
+ *                          1; applies to slots written from then on)
  *   "root_flags" 0 | 1     a walk starts from its root's cached child flags, so a
  *                          mountpoint without wildcard / $share filters walks
  *                          nothing (default 1; 0: the root's three probes)

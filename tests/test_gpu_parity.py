@@ -1331,6 +1331,65 @@ def test_trieless_tables_take_the_exact_only_count(mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+def test_one_record_slots_follow_their_key_under_churn(mode):
+    """Short exact topics (<= 3 words) with one local record keep it in the
+    exact slot (option "exact_one"): every change of that record — a new
+    SubInfo, the subscriber replaced, a second subscriber added and removed,
+    remote nodes, the topic emptied and reused — must rewrite the slot.  Each
+    round is folded against the oracle and byte-compared with a context that
+    keeps no record in its slots (exact_one 0), fused and unfused."""
+    import random
+    nodes = ["n%d@h" % i for i in range(4)]
+    prods = {}
+    for one in (1, 0):
+        p = _driver(nodes[0], mode, nodes=nodes)
+        p.view.set_option("exact_one", one)
+        prods[one] = p
+    orc = O.TrieOracle(nodes[0])
+    r = random.Random(11)
+    topics = [tuple(b"w%d" % r.randrange(50) for _ in range(r.choice([1, 2, 3, 3, 4]) - 1)) + (b"t%d" % k,)
+              for k in range(600)]
+    subs = {}   # topic index -> {client: subscriber value}
+
+    def val(k, node, qos):
+        return [(node, True, [(topics[k], qos)])]
+
+    for rnd in range(6):
+        evs = []
+        for k in range(len(topics)):
+            x = r.random()
+            cur = subs.setdefault(k, {})
+            if not cur or x < 0.3:   # (re)subscribe a client: QoS and node may change
+                sid = ("" if k % 3 else "m", b"c%d_%d" % (k, r.randrange(3)))
+                node = nodes[0] if r.random() < 0.8 else r.choice(nodes[1:])
+                new = val(k, node, r.randrange(3))
+                evs.append(("updated", sid, cur.get(sid), new))
+                cur[sid] = new
+            elif x < 0.5:            # drop one
+                sid = r.choice(sorted(cur))
+                evs.append(("deleted", sid, cur.pop(sid)))
+        for p in prods.values():
+            p.apply(evs)
+        orc.apply(evs)
+        pubs = [("" if k % 3 else "m", topics[k]) for k in range(len(topics))] * 3
+        want = [sorted(x) for x in orc.fold_batch([(mp, b"p", t) for mp, t in pubs])]
+        outs = {}
+        for one, p in prods.items():
+            for fu in (1, 0):
+                p.view.set_option("fused", fu)
+                arr, words = p.view.prepare(pubs)
+                recs, offs = p.match_arrays(arr, words)
+                outs[one, fu] = (np.asarray(offs).copy(), np.asarray(recs).view(np.uint8).copy())
+                got = p.fold_batch(pubs)
+                bad = [i for i in range(len(pubs)) if sorted(got[i]) != want[i]]
+                assert not bad, (rnd, one, fu, len(bad), pubs[bad[0]], sorted(got[bad[0]]), want[bad[0]])
+            p.view.set_option("fused", 1)
+        for key in ((1, 0), (0, 1), (0, 0)):
+            assert np.array_equal(outs[1, 1][0], outs[key][0]), (rnd, key, "offsets")
+            assert np.array_equal(outs[1, 1][1], outs[key][1]), (rnd, key, "entries")
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_reclaimed_ids_keep_parity(mode):
     """Subscribe -> unsubscribe cycles with unique client ids and words
     (paths, keys, topics dropped at each unsubscribe, words released after

@@ -52,6 +52,10 @@ VARIANTS = {
     "fxk8": ["-DVMQG_FX_K=8"],
     "fxbpc8": ["-DVMQG_FX_BPC=8"],
     "fxk2bpc8": ["-DVMQG_FX_K=2", "-DVMQG_FX_BPC=8"],
+    "fxk2u2": ["-DVMQG_FX_K=2", "-DVMQG_FX_U=2"],
+    "fxk2u2bpc5": ["-DVMQG_FX_K=2", "-DVMQG_FX_U=2", "-DVMQG_FX_BPC=5"],
+    "fxk3": ["-DVMQG_FX_K=3"],
+    "fxpf": ["-DVMQG_FX_PREFETCH=1"],
 }
 OUT_DIR = os.environ.get("VMQG_AB_DIR", os.path.join(ROOT, "build", "ab"))
 

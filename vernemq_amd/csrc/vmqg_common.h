@@ -91,7 +91,13 @@ struct alignas(16) Record { uint32_t kind_node, group, subscriber, subinfo; };
 // ids}, after the words beyond the inline ones); the slot's rmask holds the
 // nodes < 64.
 constexpr uint32_t kExactHigh = 0x40000000u;
+// ExactSlot.nwords bit: a topic of <= 3 words whose local key holds one
+// record keeps that record in w[3..6] (the slot's last 16 B), so the
+// trie-less match writes it without a second random read
+constexpr uint32_t kExactOne = 0x20000000u;
+constexpr uint32_t kExactFlags = kExactHigh | kExactOne;
 constexpr uint32_t kExactInline = 7;   // words held in the slot itself
+constexpr uint32_t kExactOneMaxWords = 3;
 struct alignas(64) ExactSlot {
   uint64_t fp;
   uint32_t nwords, words_off;   // nwords == kEmpty / kTomb marks free slots; exwords[words_off..]: words [7, L),

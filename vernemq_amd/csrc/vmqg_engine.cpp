@@ -818,13 +818,20 @@ bool Engine::write_topic(uint32_t ti) {
   s.rmask = rmask;
   s.mp = t.mp;
   for (uint32_t i = 0; i < L && i < kExactInline; i++) s.w[i] = t.words[i];
+  if (opt_exact_one && L <= kExactOneMaxWords && s.count == 1) {   // the one record inline (keys are written first)
+    s.nwords |= kExactOne;
+    memcpy(&s.w[kExactOneMaxWords], &keys[t.local_key].vals[0], sizeof(Record));
+  }
   ExactSlot& d = tab[t.slot];
+  // an update changes the first half (records, remote nodes) and, for a
+  // short topic, the inline record
+  const size_t upd = L <= kExactOneMaxWords ? sizeof(ExactSlot) : 32;
   if (fresh) {
     d = s;
     touch(lay.exact_off + t.slot * sizeof(ExactSlot), sizeof(ExactSlot));
-  } else if (memcmp(&d, &s, 32) != 0) {   // an update changes only the first half (records, remote nodes)
-    memcpy(&d, &s, 32);
-    touch(lay.exact_off + t.slot * sizeof(ExactSlot), 32);
+  } else if (memcmp(&d, &s, upd) != 0) {
+    memcpy(&d, &s, upd);
+    touch(lay.exact_off + t.slot * sizeof(ExactSlot), upd);
   }
   return true;
 }

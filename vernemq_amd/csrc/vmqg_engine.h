@@ -514,6 +514,7 @@ struct Engine {
   uint32_t opt_exfilter = 2;                               // vmqg_set_option "exfilter": 0 off, 1 on, 2 auto (default)
   uint64_t ex_next = 0;                                    // auto: the sampler runs on calls after this one (k_ex_sample)
   uint32_t opt_trieless = 1;                               // vmqg_set_option "trieless": the exact-only COUNT when no edge exists
+  uint32_t opt_exact_one = 1;                              // vmqg_set_option "exact_one": a short topic's one record inline in its exact slot
   uint32_t opt_fused = 1;                                  // vmqg_set_option "fused": trie-less COUNT + scan + EMIT in one launch
   bool d_trieless = false;                                 // the device tables have no trie edge (set by commit)
   uint32_t opt_heavy_min = 0;                              // vmqg_set_option "heavy_min": records mode, EMIT tail by XCD (0 off)

@@ -390,7 +390,7 @@ __device__ const ExactSlot* find_exact(const MatchArgs& a, const vmqg_pub& pub, 
       const uint4 h = *reinterpret_cast<const uint4*>(&e);   // {fp lo, fp hi, nwords, words_off}
       const uint32_t nw = h.z;
       if (nw == kEmpty) { seen_empty = true; break; }
-      if ((((uint64_t)h.y << 32) | h.x) != fp || (nw & ~kExactHigh) != L || e.mp != pub.mountpoint) continue;
+      if ((((uint64_t)h.y << 32) | h.x) != fp || (nw & ~kExactFlags) != L || e.mp != pub.mountpoint) continue;
       // inline words, then the rest (two loops: one loop selecting between
       // the two loads costs the one-lane COUNT 16 B of scratch spills)
       bool diff = false;
@@ -2361,7 +2361,7 @@ __global__ __launch_bounds__(256) void k_count_exact(MatchArgs a) {
             const uint4 sj = j == 0 ? s0 : *reinterpret_cast<const uint4*>(&bk[j]);
             if (sj.z == kEmpty) { empty = true; continue; }
             const uint64_t f = ((uint64_t)sj.y << 32) | sj.x;
-            if (f != fp[k] || (sj.z & ~kExactHigh) != L) continue;
+            if (f != fp[k] || (sj.z & ~kExactFlags) != L) continue;
             const uint4* q = reinterpret_cast<const uint4*>(&bk[j]);
             const uint4 q2 = q[2];   // {mp, w0, w1, w2}
             bool diff = q2.x != pub[k].mountpoint;
@@ -2640,6 +2640,12 @@ static void launch_emit_exact(const MatchArgs& a, bool nt, hipStream_t st, hipEv
 #ifndef VMQG_FX_K
 #define VMQG_FX_K 4   // 64-publish chunks per wave per tile (A/B on R1)
 #endif
+#ifndef VMQG_FX_PREFETCH
+#define VMQG_FX_PREFETCH 0   // 1: a one-record publish's record loaded before the look-back (A/B: more VGPRs)
+#endif
+#ifndef VMQG_FX_U
+#define VMQG_FX_U 4   // entries per lane in flight in the whole-wave copy
+#endif
 #ifndef VMQG_FX_BPC
 #define VMQG_FX_BPC 4   // fused blocks per CU
 #endif
@@ -2714,12 +2720,13 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
       if (look[k]) h0[k] = *reinterpret_cast<const uint4*>(&a.exact[(fp[k] & a.exact_mask) * kExactSlotsPerBucket]);
     uint32_t off[kFxK], cnt[kFxK], hoff[kFxK], nh[kFxK], tot[kFxK];
     uint64_t rm[kFxK];
-    uint4 one[kFxK];   // a one-record publish's record, loaded while the tile is scanned
+    uint4 one[kFxK];   // a one-record publish's record, from its slot (or loaded while the tile is scanned)
+    uint32_t onem = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kFxK; k++) {
       const uint32_t L = pub[k].nwords;
       const uint32_t* w = a.words + pub[k].word_off;
-      bool found = false;
+      bool found = false, has_one = false;
       uint4 hit{0, 0, 0, 0};
       uint32_t hi_at = kNone;
       if (look[k]) {
@@ -2734,19 +2741,22 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
             const uint4 sj = j == 0 ? s0 : *reinterpret_cast<const uint4*>(&bk[j]);
             if (sj.z == kEmpty) { empty = true; continue; }
             const uint64_t f = ((uint64_t)sj.y << 32) | sj.x;
-            if (f != fp[k] || (sj.z & ~kExactHigh) != L) continue;
+            if (f != fp[k] || (sj.z & ~kExactFlags) != L) continue;
             const uint4* q = reinterpret_cast<const uint4*>(&bk[j]);
-            const uint4 q2 = q[2];
+            // the rest of the slot's line at once: its words, records and,
+            // for a short topic with one record, that record (kExactOne)
+            const bool inl = OUT == 0 && (sj.z & kExactOne) != 0;
+            const uint4 q1 = q[1], q2 = q[2];
+            const uint4 q3 = (L > 3 || inl) ? q[3] : make_uint4(0, 0, 0, 0);
             bool diff = q2.x != pub[k].mountpoint;
             diff |= (L > 0 && q2.y != w[0]) || (L > 1 && q2.z != w[1]) || (L > 2 && q2.w != w[2]);
-            if (!diff && L > 3) {
-              const uint4 q3 = q[3];
+            if (L > 3)
               diff |= q3.x != w[3] || (L > 4 && q3.y != w[4]) || (L > 5 && q3.z != w[5]) || (L > 6 && q3.w != w[6]);
-            }
             for (uint32_t i = kExactInline; !diff && i < L; i++) diff |= a.exwords[sj.w + (i - kExactInline)] != w[i];
             if (!diff) {
               found = true;
-              hit = q[1];
+              hit = q1;
+              if (inl) { one[k] = q3; has_one = true; }
               if (sj.z & kExactHigh) hi_at = sj.w + exact_tail_words(L);   // {count, node ids} of nodes >= 64
             }
           }
@@ -2757,7 +2767,10 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
       }
       off[k] = hit.x;
       cnt[k] = hit.y;
-      if (OUT == 0 && hit.y == 1) one[k] = *reinterpret_cast<const uint4*>(a.records + hit.x);
+#if VMQG_FX_PREFETCH
+      if (OUT == 0 && hit.y == 1 && !has_one) { one[k] = *reinterpret_cast<const uint4*>(a.records + hit.x); has_one = true; }
+#endif
+      onem |= has_one ? 1u << k : 0u;
       rm[k] = ((uint64_t)hit.w << 32) | hit.z;
       if (a.local_node < kLowNodes) rm[k] &= ~(1ull << a.local_node);
       hoff[k] = hi_at;
@@ -2789,7 +2802,7 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
     uint64_t wbase = S.base;
     for (uint32_t x = 0; x < wv; x++) wbase += S.wtot[x];
     // ---- entries
-#pragma unroll 1
+#pragma unroll
     for (uint32_t k = 0; k < kFxK; k++) {
       const uint32_t p = p0 + k * 64 + lane;
       const bool valid = p < a.npub;
@@ -2816,7 +2829,7 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
           ok = false;
         }
         if (ok && tot[k] == 1) {   // one entry: this lane writes it (the chunk's stores coalesce)
-          store_rec<NT>(a.out, ob, cnt[k] == 1 ? one[k] : fx_emission(a, off[k], cnt[k], rm[k], hoff[k], 0));
+          store_rec<NT>(a.out, ob, (onem >> k) & 1u ? one[k] : fx_emission(a, off[k], cnt[k], rm[k], hoff[k], 0));
           ok = false;
         }
         // the others: the whole wave over their concatenated entries, U per lane in flight
@@ -2829,7 +2842,7 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
           if (lane == 63) W.crel[64] = in32;
           wave_sync();
           const uint32_t T = W.crel[64];
-          constexpr int U = 4;
+          constexpr int U = VMQG_FX_U;
           uint32_t q = 0;
           for (uint32_t r0 = lane; r0 < T; r0 += 64 * U) {
             uint4 v[U];
