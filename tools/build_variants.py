@@ -55,6 +55,7 @@ VARIANTS = {
     "fxk2u2": ["-DVMQG_FX_K=2", "-DVMQG_FX_U=2"],
     "fxk2u2bpc5": ["-DVMQG_FX_K=2", "-DVMQG_FX_U=2", "-DVMQG_FX_BPC=5"],
     "fxk3": ["-DVMQG_FX_K=3"],
+    "fxk6": ["-DVMQG_FX_K=6"],
     "fxpf": ["-DVMQG_FX_PREFETCH=1"],
 }
 OUT_DIR = os.environ.get("VMQG_AB_DIR", os.path.join(ROOT, "build", "ab"))

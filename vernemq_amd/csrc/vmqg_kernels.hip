@@ -2718,7 +2718,7 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k < kFxK; k++)
       if (look[k]) h0[k] = *reinterpret_cast<const uint4*>(&a.exact[(fp[k] & a.exact_mask) * kExactSlotsPerBucket]);
-    uint32_t off[kFxK], cnt[kFxK], hoff[kFxK], nh[kFxK], tot[kFxK];
+    uint32_t off[kFxK], cnt[kFxK], hoff[kFxK], tot[kFxK];   // held across the look-back: kept lean
     uint64_t rm[kFxK];
     uint4 one[kFxK];   // a one-record publish's record, from its slot (or loaded while the tile is scanned)
     uint32_t onem = 0;
@@ -2774,17 +2774,16 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
       rm[k] = ((uint64_t)hit.w << 32) | hit.z;
       if (a.local_node < kLowNodes) rm[k] &= ~(1ull << a.local_node);
       hoff[k] = hi_at;
-      nh[k] = hi_at != kNone ? a.exwords[hi_at] : 0u;
-      const uint32_t nr = (uint32_t)__popcll(rm[k]) + nh[k];
+      const uint32_t nr = (uint32_t)__popcll(rm[k]) + (hi_at != kNone ? a.exwords[hi_at] : 0u);
       tot[k] = OUT ? (cnt[k] ? 1u : 0u) + nr : cnt[k] + nr;
     }
     // ---- offsets: lane, chunk and wave prefixes, the tile's base by look-back
-    uint64_t incl[kFxK], cpre[kFxK], wsum = 0;
+    uint64_t excl[kFxK], wsum = 0;   // each publish's offset within its wave's entries
 #pragma unroll
     for (uint32_t k = 0; k < kFxK; k++) {
-      incl[k] = wave_incl_scan64(tot[k]);
-      cpre[k] = wsum;
-      wsum += __shfl(incl[k], 63, 64);
+      const uint64_t incl = wave_incl_scan64(tot[k]);
+      excl[k] = wsum + incl - tot[k];
+      wsum += __shfl(incl, 63, 64);
     }
     if (lane == 0) S.wtot[wv] = wsum;
     __syncthreads();
@@ -2806,7 +2805,8 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
     for (uint32_t k = 0; k < kFxK; k++) {
       const uint32_t p = p0 + k * 64 + lane;
       const bool valid = p < a.npub;
-      const uint64_t ob = wbase + cpre[k] + incl[k] - tot[k];
+      const uint64_t ob = wbase + excl[k];
+      const uint32_t nh = hoff[k] != kNone ? a.exwords[hoff[k]] : 0u;   // remote nodes >= 64 (rare: re-read)
       if (valid) a.offsets[p] = ob;
       bool ok = valid && tot[k] > 0;
       if (ok && ob + tot[k] > cap) { atomicOr(a.err, kErrOverflow); ok = false; }
@@ -2815,11 +2815,11 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
           uint64_t o = ob;
           if (cnt[k]) store_range(a.out_rng, o++, off[k], cnt[k]);
           for (uint64_t m = rm[k]; m; m &= m - 1) store_range(a.out_rng, o++, (uint32_t)__builtin_ctzll(m), 0u);
-          for (uint32_t i = 0; i < nh[k]; i++) store_range(a.out_rng, o++, a.exwords[hoff[k] + 1 + i], 0u);
+          for (uint32_t i = 0; i < nh; i++) store_range(a.out_rng, o++, a.exwords[hoff[k] + 1 + i], 0u);
         }
       } else {
         // a huge publish: the EMIT tail copies it with every wave (its key cache and list, as k_count_exact)
-        const bool huge = ok && tot[k] >= kHugeRecords && nh[k] == 0;
+        const bool huge = ok && tot[k] >= kHugeRecords && nh == 0;
         if (huge) {
           uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
           const uint32_t nk = cnt[k] ? 1u : 0u;
