@@ -706,7 +706,16 @@ def bench_other(args):
     if count_ns or emit_ns:
         pmc = "pmc_%s.json" % args.config.lower()
         survey = None
-        if count_ns >= emit_ns + tail_ns:
+        fused = bool(stages) and stages["scan"] == 0 and stages["emit"] == 0 and count_ns > 0
+        if fused and count_ns >= tail_ns:
+            # trie-less tables: COUNT, scan and EMIT are one launch
+            # (k_match_exact_fused), priced with all three's compulsory bytes
+            alg = (b_p["lookup"] + 8) * npub + 16 * em if b_p else None
+            kn, traffic = load_pmc_traffic_any(["k_match_exact_fused"], pmc)
+            kern, ns = "k_match_exact_fused (COUNT + scan + EMIT)", count_ns
+            model = ("8(L+1) + 16 S_p per publish (lookup, S_p averaged over the oracle sample) + 8-B offset per "
+                     "publish + 16 B written per emission")
+        elif count_ns >= emit_ns + tail_ns:
             alg = b_p["lookup"] * npub if b_p else None
             kn, traffic = load_pmc_traffic_any(["k_match_fast<0", "k_count_exact"], pmc)
             kern, ns, model = "%s,...> (COUNT)" % (kn or "k_match_fast<0"), count_ns, \
@@ -716,6 +725,11 @@ def bench_other(args):
             kn, traffic = load_pmc_traffic_any(["k_match_fast<1", "k_emit_exact"], pmc)
             kern, ns = "%s,...> (EMIT)" % (kn or "k_match_fast<1"), emit_ns
             model = "16 B written per emission + 8-B offset and 32-B key cache per publish"
+        elif fused:   # R2: the fused match hands its one huge publish to the tail, which writes it
+            alg, survey = 16 * em + 40 * npub, 32 * em
+            kern, ns = "EMIT tail (k_match_wave<1>, after k_match_exact_fused)", tail_ns
+            model = "16 B written per emission + 8-B offset and 32-B key cache per publish"
+            traffic = load_pmc_traffic("k_match_wave<1", pmc)
         else:
             alg, survey = 16 * em + 40 * npub, 32 * em
             kn, t1 = load_pmc_traffic_any(["k_match_fast<1", "k_emit_exact"], pmc)
