@@ -15,5 +15,5 @@ done
 timeout -k 10 420 ./tools/bin/nif_harness 3 scale churn load > $O/harness.jsonl 2> $O/harness.err || { tail -20 $O/harness.err; exit 5; }
 VMQGB_REPLICAS=1 timeout -k 10 300 ./tools/bin/nif_harness 3 churn > $O/harness_lanes2.jsonl 2> $O/harness_lanes2.err || { tail -20 $O/harness_lanes2.err; exit 6; }
 tail -3 $O/harness_lanes2.jsonl
-timeout -k 10 300 python -u bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline --no-e2e > $O/bench_C_n2.json 2> $O/bench_C_n2.err || { tail -5 $O/bench_C_n2.err; exit 7; }
+timeout -k 10 300 python -u bench.py --gpus 2 --force-device 0 --dist-backend gloo --steps 20 --warmup 3 --no-cpu-baseline --no-e2e > $O/bench_C_n2.json 2> $O/bench_C_n2.err || { tail -5 $O/bench_C_n2.err; exit 7; }
 tail -c 300 $O/bench_C_n2.json
