@@ -187,6 +187,9 @@ def main():
     ap.add_argument("--d-scale", type=float, default=1.0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--force-device", type=int, default=-1, help="rehearsal: every rank on this device")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="config C: matcher contexts on the GPU (primary + replicas), consecutive steps on "
+                         "consecutive contexts and streams")
     ap.add_argument("--churn-batch", type=int, default=10_000)
     ap.add_argument("--churn-rate-batches", type=float, default=10.0, help="delta batches per second (1%%/s at 10M)")
     ap.add_argument("--vmqg-opt", action="append", default=[], metavar="NAME=VALUE",
@@ -271,18 +274,39 @@ def main():
         view.match_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), d_out.data_ptr(), out_cap,
                           d_offs.data_ptr(), sp)
 
+    # --lanes L: L contexts on this GPU (the primary and L - 1 replicas
+    # loaded from its arena, as the drop-in's view holds them), each with
+    # its own stream and output buffers; consecutive steps go to
+    # consecutive lanes, so one batch's COUNT can run beside another's EMIT
+    lanes = [(view, stream, d_out, d_offs)]
+    for _ in range(1, args.lanes):
+        rv = RegGpuView(node=w.self_node, device=local, replica=True)
+        ap, _, lay = view.arena()
+        rv.replica_load(lay, ap, sp)
+        apply_opts(rv, args)
+        lanes.append((rv, torch.cuda.Stream(device=dev), torch.empty_like(d_out), torch.zeros_like(d_offs)))
+    torch.cuda.synchronize()
+    seq = [0]
+
+    def step_lanes():
+        v, s, o, f = lanes[seq[0] % len(lanes)]
+        seq[0] += 1
+        v.match_device(d_pubs.data_ptr(), npub, d_words.data_ptr(), o.data_ptr(), out_cap, f.data_ptr(), s.cuda_stream)
+
     for _ in range(args.warmup):
         step()
+    for _ in range(len(lanes) * max(1, args.warmup)):
+        step_lanes()
     torch.cuda.synchronize()
-    rc = view.match_status(sp)
-    if rc != 0:
-        raise RuntimeError("match status %d after warmup" % rc)
+    for v, s, _, _ in lanes:
+        rc = v.match_status(s.cuda_stream)
+        if rc != 0:
+            raise RuntimeError("match status %d after warmup" % rc)
     # size-independent parity check of the step's output (every publish: 64
     # wildcard subscribers + its own device subscriber when d < n_dev)
     d_idx = w.pw[1::4] - 18
     want = np.where(d_idx < args.n_dev, w.notes["n_wild"] + 1, w.notes["n_wild"])
-    got = np.diff(d_offs.cpu().numpy())
-    verified = bool(np.array_equal(got, want))
+    verified = all(bool(np.array_equal(np.diff(f.cpu().numpy()), want)) for _, _, _, f in lanes)
     if not verified:
         raise RuntimeError("per-publish emission counts differ from config C's known answer")
 
@@ -294,14 +318,15 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step_lanes()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    rc = view.match_status(sp)
-    if rc != 0:
-        raise RuntimeError("match status %d in timed region" % rc)
+    for v, s, _, _ in lanes:
+        rc = v.match_status(s.cuda_stream)
+        if rc != 0:
+            raise RuntimeError("match status %d in timed region" % rc)
     # a second, instrumented pass (never `value`): the per-step median SURVEY
     # §8(d) asks for, from events recorded on the launch stream between steps,
     # then the per-launch kernel times (HIP event pairs around every launch)
@@ -488,7 +513,8 @@ def main():
                                    "%d publishes/step/GPU devices/{d}/telemetry/{m}, d < %d"
                                    % (w.n_subs, args.n_dev, w.notes["n_wild"], npub, int(args.n_dev * 1.25)),
                        "subs": w.n_subs, "publishes_per_step_per_gpu": npub,
-                       "parallelism": "trie replicated (RCCL broadcast), publishes sharded x%d" % world},
+                       "parallelism": "trie replicated (RCCL broadcast), publishes sharded x%d" % world,
+                       "contexts_per_gpu": len(lanes)},
             "pairs_per_s": total_emit / t_max,
             "emissions_per_step_per_gpu": emissions,
             "verified_counts": verified,
