@@ -690,6 +690,7 @@ struct vmqgb_view {
   pthread_cond_t q_cv;
   int inflight;              /* rounds in the kernels per lane, at most */
   int pipelined;             /* the context has a device: hbatch rounds */
+  int force_pin_state;       /* tests: the next n range pins answer VMQG_E_STATE */
   int device_records;
   int nlanes;
   unsigned next_lane;        /* vmqgb_view_bind: round robin */
@@ -952,6 +953,11 @@ int vmqgb_view_commit(vmqgb_view* v, uint64_t* epoch) {
 }
 
 int vmqgb_view_set_option(vmqgb_view* v, const char* name, int64_t value) {
+  if (strcmp(name, "force_pin_state") == 0) {   /* the batch layer's own (tests: the ranges fallback) */
+    if (value < 0 || value > (1 << 30)) return VMQG_E_INVAL;
+    __atomic_store_n(&v->force_pin_state, (int)value, __ATOMIC_RELAXED);
+    return 0;
+  }
   vmqgb_view_write_begin(v);
   pthread_mutex_lock(&v->lanes[0].device);
   const int rc = vmqg_set_option(v->ctx, name, value);
@@ -1248,6 +1254,9 @@ int vmqgb_view_match(vmqgb_view* v, vmqgb_batch* b, int ranges, const vmqg_emit*
       uint64_t nrt = 0;
       int rc = vmqg_records_pin(v->ctx, b->epoch, &rt, &nrt, &b->rec_pin);
       if (rc == 0) b->rec_pinned = 1;
+      if (rc == 0 && __atomic_load_n(&v->force_pin_state, __ATOMIC_RELAXED) > 0 &&
+          __atomic_sub_fetch(&v->force_pin_state, 1, __ATOMIC_RELAXED) >= 0)
+        rc = VMQG_E_STATE;   /* as if two applies had rewritten the record slots (release_lease unpins) */
       if (rc == VMQG_E_STATE) {   /* two applies rewrote record slots since the round */
         release_lease(v, b);
         pthread_mutex_lock(&v->q_mu);

@@ -283,7 +283,10 @@ int vmqgb_view_commit(vmqgb_view* v, uint64_t* epoch);
 /* vmqg_stats under the writer and the device mutex (the fields the writer
  * and the device calls update) */
 int vmqgb_view_ctx_stats(vmqgb_view* v, vmqg_stats_t* out);
-/* vmqg_set_option under both mutexes */
+/* vmqg_set_option under both mutexes, on every lane's context; the batch
+ * layer's own "force_pin_state" n (tests) makes the next n range-mode record
+ * pins answer VMQG_E_STATE, so the ranges mode's fallback to device records
+ * (after three refused pins) can be exercised */
 int vmqgb_view_set_option(vmqgb_view* v, const char* name, int64_t value);
 /* Knobs and counters of the submitter (tools/nif_harness.c reports them). */
 void vmqgb_view_set_device_records(vmqgb_view* v, int on);   /* records over PCIe instead of host expansion */

@@ -71,7 +71,7 @@ static size_t npubs, pcap;
 static char** gname;     /* group text by word id */
 static size_t gcap;
 static vmqg_ctx* replicas[VMQGB_MAX_LANES];
-static int nreplicas;
+static int nreplicas, forced;
 static uint64_t digests_checked, digests_mismatched;
 
 /* with replicas: every lane's arena digest equals the primary's (writer mutex held) */
@@ -352,6 +352,10 @@ int main(int argc, char** argv) {
         if (!x || (err = vmqgb_view_add_replica(view, x))) { fprintf(stderr, "replica: %d\n", err); return 13; }
         replicas[nreplicas++] = x;
       }
+    } else if (line[0] == 'F') {   /* F n: the next n range pins answer E_STATE (the ranges fallback) */
+      long n = 0;
+      if (sscanf(line + 2, "%ld", &n) != 1 || vmqgb_view_set_option(view, "force_pin_state", n)) return 14;
+      forced = 1;
     } else if (line[0] == 'A') {
       vmqgb_view_write_begin(view);
       const int rc = vmqgb_view_apply_ops(view, &ops, NULL);
@@ -396,6 +400,11 @@ int main(int argc, char** argv) {
     }
   }
   if (nreplicas) fprintf(out, "H %llu %llu\n", (unsigned long long)digests_checked, (unsigned long long)digests_mismatched);
+  if (forced) {
+    vmqgb_view_stats vs;
+    vmqgb_view_get_stats(view, &vs);
+    fprintf(out, "F %llu\n", (unsigned long long)vs.ranges_fallbacks);
+  }
   fclose(out);
   vmqgb_view_free(view);
   for (int k = 0; k < nreplicas; k++) vmqg_destroy(replicas[k]);

@@ -25,6 +25,21 @@ def test_batch_layer_unit(tmp_path):
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
 
 
+def test_reader_records_out_of_memory_is_an_answer(tmp_path):
+    """tests/c/nomem_check.c: vmqg_set_option("reader_records") under an
+    address-space limit that the two reader copies exceed answers
+    VMQG_E_NOMEM (the bad_alloc is caught inside the ABI) and leaves the
+    context usable; without the limit the same call succeeds."""
+    from vernemq_amd import _lib
+    lib_dir = os.path.dirname(_lib.LIB_PATH)
+    exe = tmp_path / "nomem_check"
+    subprocess.run(["gcc", "-std=gnu11", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    "-o", str(exe), os.path.join(ROOT, "tests", "c", "nomem_check.c"),
+                    "-L", lib_dir, "-l:libvmqgpu.so", "-Wl,-rpath," + lib_dir], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+
+
 def test_readers_beside_the_writer_on_a_host_context(tmp_path):
     """tests/c/rcu_check.c: six reader threads prepare word lists and pin the
     readers' record table while one writer interns words and rewrites a key
@@ -269,12 +284,17 @@ def test_batchers_while_a_writer_changes_the_answers(tmp_path, replicas):
     script, nodes, node_ids, pubs, init_events, runs = _churn_script()
     if replicas:
         script = "R %d\n" % replicas + script
+    else:   # 40 refused range pins: batches fall back to device records, same parity
+        script = "F 40\n" + script
     (tmp_path / "s.txt").write_text(script)
     r = subprocess.run([exe, str(tmp_path / "s.txt"), str(tmp_path / "o.txt")], capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0, r.stderr
     name = {nid: nodes[i] for i, nid in enumerate(node_ids)}
     text = (tmp_path / "o.txt").read_text().splitlines()
+    if not replicas:
+        assert text[-1].startswith("F ") and int(text[-1].split()[1]) >= 1, text[-1]
+        text = text[:-1]
     orc = O.TrieOracle(nodes[0])
     orc.apply(init_events)
     pos = 0
