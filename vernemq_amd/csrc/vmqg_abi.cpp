@@ -693,9 +693,6 @@ int vmqg_set_option(vmqg_ctx* ctx, const char* name, int64_t value) {
   } else if (n == "fused") {
     if (value < 0 || value > 1) return VMQG_E_INVAL;
     e.opt_fused = (uint32_t)value;
-  } else if (n == "tail_overlap") {
-    if (value < 0 || value > 1) return VMQG_E_INVAL;
-    e.opt_tail_overlap = (uint32_t)value;
   } else if (n == "exact_one") {   // slots written from now on; either kind is matched alike
     if (value < 0 || value > 1) return VMQG_E_INVAL;
     e.opt_exact_one = (uint32_t)value;

@@ -30,9 +30,6 @@ Engine::~Engine() {
     if (stream) hipStreamSynchronize(stream);
     for (auto& ev : t_ev) for (auto e : ev) hipEventDestroy(e);
     if (ev_match_done) hipEventDestroy(ev_match_done);
-    if (tail_stream) hipStreamSynchronize(tail_stream);
-    if (ev_fork) hipEventDestroy(ev_fork);
-    if (ev_join) hipEventDestroy(ev_join);
     for (Stage& sg : stage) {
       if (sg.ev) hipEventDestroy(sg.ev);
       if (sg.h) hipHostFree(sg.h);
@@ -44,7 +41,6 @@ Engine::~Engine() {
     hipFree(d_lookback); hipFree(d_ostack);
     hipFree(d_pubs); hipFree(d_words); hipFree(d_offs); hipFree(d_out);
     if (stream) hipStreamDestroy(stream);
-    if (tail_stream) hipStreamDestroy(tail_stream);
   }
 }
 
@@ -72,11 +68,6 @@ int Engine::init(const vmqg_config& c) {
     if (hipSetDevice(device) != hipSuccess) return VMQG_E_DEVICE;
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return VMQG_E_DEVICE;
     if (hipEventCreateWithFlags(&ev_match_done, hipEventDisableTiming) != hipSuccess) return VMQG_E_DEVICE;
-    // non-blocking: a caller on the legacy default stream must not serialise the fork
-    if (hipStreamCreateWithFlags(&tail_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) != hipSuccess)
-      return VMQG_E_DEVICE;
     has_device = true;
     if (hipMalloc(&d_status, kStatusBytes) != hipSuccess) return VMQG_E_NOMEM;
     if (hipMemset(d_status, 0, kStatusBytes) != hipSuccess) return VMQG_E_DEVICE;
@@ -1711,20 +1702,7 @@ int Engine::match_device(const vmqg_pub* d_pubs_, uint32_t npub, const uint32_t*
   debug_sync(st, "COUNT wave tier");
   if (launch_scan(a, st, ev[4], ev[5]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "scan");
-  // EMIT: the fast tier and the tail (whole-wave walks, wide and huge
-  // publishes) write disjoint output ranges, so the tail runs beside the
-  // fast EMIT on the context's tail stream (its ranges from the chunk bases
-  // and the key cache, tail_pos) and the caller's stream joins it after
-  if (opt_tail_overlap && !a.dbg) {
-    a.tail_pos = 1;
-    if (hipEventRecord(ev_fork, st) != hipSuccess || hipStreamWaitEvent(tail_stream, ev_fork, 0) != hipSuccess)
-      return VMQG_E_DEVICE;
-    if (launch_match(a, 1, 1, tail_stream, ev[8], ev[9]) != hipSuccess) return VMQG_E_DEVICE;
-    if (launch_match(a, 1, 0, st, ev[6], ev[7]) != hipSuccess) return VMQG_E_DEVICE;
-    if (hipEventRecord(ev_join, tail_stream) != hipSuccess || hipStreamWaitEvent(st, ev_join, 0) != hipSuccess)
-      return VMQG_E_DEVICE;
-    return VMQG_OK;
-  }
+  // EMIT: the fast tier, then the tail (whole-wave walks, wide publishes)
   if (launch_match(a, 1, 0, st, ev[6], ev[7]) != hipSuccess) return VMQG_E_DEVICE;
   debug_sync(st, "EMIT");
   if (launch_match(a, 1, 1, st, ev[8], ev[9]) != hipSuccess) return VMQG_E_DEVICE;

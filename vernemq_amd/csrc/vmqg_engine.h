@@ -494,8 +494,6 @@ struct Engine {
   // ---- device
   int device = -1;
   hipStream_t stream = nullptr;
-  hipStream_t tail_stream = nullptr;              // the EMIT tail beside the fast EMIT (fork / join by the two events)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint8_t* d_arena = nullptr; uint64_t d_arena_bytes = 0;
   // patch staging ring: pinned host + device buffers, each reusable once its
   // event (recorded after the patch kernel) has fired, so vmqg_apply_ops
@@ -517,7 +515,6 @@ struct Engine {
   uint64_t ex_next = 0;                                    // auto: the sampler runs on calls after this one (k_ex_sample)
   uint32_t opt_trieless = 1;                               // vmqg_set_option "trieless": the exact-only COUNT when no edge exists
   uint32_t opt_exact_one = 1;                              // vmqg_set_option "exact_one": a short topic's one record inline in its exact slot
-  uint32_t opt_tail_overlap = 1;                           // vmqg_set_option "tail_overlap": the EMIT tail on a second stream
   uint32_t opt_fused = 1;                                  // vmqg_set_option "fused": trie-less COUNT + scan + EMIT in one launch
   bool d_trieless = false;                                 // the device tables have no trie edge (set by commit)
   uint32_t opt_heavy_min = 0;                              // vmqg_set_option "heavy_min": records mode, EMIT tail by XCD (0 off)

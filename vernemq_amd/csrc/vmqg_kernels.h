@@ -57,9 +57,6 @@ struct MatchArgs {
   uint32_t trieless;                              // the device tables have no trie edge: only exact topics match
   uint32_t* dd_host;                              // host-mapped words: [0] the dedupe mode, [1] the exbits-filter
                                                   // mode for the next calls (k_ex_sample)
-  uint32_t tail_pos;                              // 1: the EMIT tail runs beside the fast EMIT and takes its
-                                                  // publishes' output ranges from the chunk bases and the key
-                                                  // cache's counts (offsets[] is being rewritten meanwhile)
 };
 
 constexpr uint32_t kOptNtStores = 1u;   // non-temporal stores for the emitted records

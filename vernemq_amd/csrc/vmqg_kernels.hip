@@ -1674,26 +1674,6 @@ void k_match_fast(MatchArgs a) {
 #ifndef VMQG_TAIL_WPE
 #define VMQG_TAIL_WPE 8   // EMIT tail: asks for 8 waves per SIMD; gfx950 build (round 4): 128 VGPRs, 4 waves (groups, huge, wide, walks in one kernel)
 #endif
-// The EMIT tail's output range of publish p (uniform across the wave).
-// With a.tail_pos the tail runs beside the fast EMIT on a second stream,
-// while EMIT turns offsets[] from counts into positions: the range is the
-// chunk's base (the scan's) plus the counts of the chunk's earlier
-// publishes, which COUNT (and its wave tier, and the dedupe fix-up) left in
-// every publish's key cache (kc[0].x) — one load per lane, one wave sum.
-__device__ __forceinline__ void tail_range(const MatchArgs& a, uint32_t p, uint64_t& ob, uint64_t& oe) {
-  if (!a.tail_pos) {
-    ob = uni64(a.offsets[p]);
-    oe = uni64(a.offsets[p + 1]);
-    return;
-  }
-  const uint4* kc = reinterpret_cast<const uint4*>(a.keycache);
-  const uint32_t q = p - p % a.gpw + __lane_id();   // gpw <= 64: one publish per lane
-  const uint64_t c = q < p ? (uint64_t)kc[(uint64_t)q * 2].x : 0ull;
-  const uint64_t before = __shfl(wave_incl_scan64(c), 63, 64);
-  ob = uni64(a.chunk[p / a.gpw] + before);
-  oe = ob + uni(kc[(uint64_t)p * 2].x);
-}
-
 template <int MODE, int OUT, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? VMQG_TAIL_WPE : 1)))
 void k_match_wave(MatchArgs a) {
@@ -1752,8 +1732,7 @@ void k_match_wave(MatchArgs a) {
     const uint32_t n = VMQG_TAIL_NOWALK ? 0u : uni(a.status[kStWalked]);
     for (uint32_t d = (uint32_t)gw; d < n; d += nwaves) {
       const uint32_t p = uni(a.deferred[(uint64_t)a.npub + d]);
-      uint64_t ob, oe;
-      tail_range(a, p, ob, oe);
+      const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
       if (oe > cap || ob > oe) {
         if (lane == 0) atomicOr(a.err, kErrOverflow);
         continue;
@@ -1765,8 +1744,7 @@ void k_match_wave(MatchArgs a) {
       const uint32_t nh = uni(a.status[kStHuge]);
       for (uint32_t hi = 0; hi < nh; hi++) {
         const uint32_t p = uni(a.deferred[4ull * a.npub + hi]);
-        uint64_t ob, oe;
-        tail_range(a, p, ob, oe);
+        const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
         if (oe > cap || ob > oe) {
           if (gw == 0 && lane == 0) atomicOr(a.err, kErrOverflow);
           continue;
@@ -1838,22 +1816,25 @@ void k_match_wave(MatchArgs a) {
       };
       uint32_t p = 0;
       bool have = next_heavy(p);
+      uint64_t ob_n = 0, oe_n = 0;   // loaded per lane (uniform values): made scalar only when used
       uint4 h_n{0, 0, 0, 0}, k_n{0, 0, 0, 0};
       if (have && p < a.npub) {
+        ob_n = a.offsets[p]; oe_n = a.offsets[p + 1];
         h_n = reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2];
         k_n = reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2 + 1];
       }
       while (have) {
         const uint32_t pc = p;
+        const uint64_t obv = ob_n, oev = oe_n;
         const uint4 hv = h_n, kv = k_n;
         have = next_heavy(p);
         if (have && p < a.npub) {
+          ob_n = a.offsets[p]; oe_n = a.offsets[p + 1];
           h_n = reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2];
           k_n = reinterpret_cast<const uint4*>(a.keycache)[(uint64_t)p * 2 + 1];
         }
         if (pc >= a.npub) { if (lane == 0) atomicOr(a.err, kErrMismatch); continue; }
-        uint64_t ob, oe;
-        tail_range(a, pc, ob, oe);
+        const uint64_t ob = uni64(obv), oe = uni64(oev);
         if (oe > cap || ob > oe) {
           if (lane == 0) atomicOr(a.err, kErrOverflow);
           continue;
@@ -1895,8 +1876,7 @@ void k_match_wave(MatchArgs a) {
         }
         if (!have) break;
         if (p >= a.npub) { if (lane == 0) atomicOr(a.err, kErrMismatch); continue; }
-        uint64_t ob, oe;
-        tail_range(a, p, ob, oe);
+        const uint64_t ob = uni64(a.offsets[p]), oe = uni64(a.offsets[p + 1]);
         if (oe > cap || ob > oe) {
           if (lane == 0) atomicOr(a.err, kErrOverflow);
           continue;
