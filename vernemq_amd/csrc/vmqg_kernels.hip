@@ -2638,7 +2638,7 @@ static void launch_emit_exact(const MatchArgs& a, bool nt, hipStream_t st, hipEv
 // tail's list, as k_count_exact leaves them.  Remote nodes >= 64 (the exact
 // slot's high list) are emitted here too, from exwords.
 #ifndef VMQG_FX_K
-#define VMQG_FX_K 4   // 64-publish chunks per wave per tile (A/B on R1)
+#define VMQG_FX_K 2   // 64-publish chunks per wave per tile (A/B on R1: 1, 2, 3, 4, 6, 8)
 #endif
 #ifndef VMQG_FX_PREFETCH
 #define VMQG_FX_PREFETCH 0   // 1: a one-record publish's record loaded before the look-back (A/B: more VGPRs)
@@ -2649,6 +2649,9 @@ static void launch_emit_exact(const MatchArgs& a, bool nt, hipStream_t st, hipEv
 #ifndef VMQG_FX_BPC
 #define VMQG_FX_BPC 4   // fused blocks per CU
 #endif
+#ifndef VMQG_FX_DEFER
+#define VMQG_FX_DEFER 1   // a tile's look-back and entries one iteration after its probes (0: at once)
+#endif
 constexpr uint32_t kFxK = VMQG_FX_K;
 constexpr uint32_t kFxTile = kWaves * kFxK * 64;
 struct FxWave {
@@ -2656,11 +2659,22 @@ struct FxWave {
   uint64_t rm[64], ob[64];
   uint32_t crel[65];
 };
+// one tile's per-publish results, held from its probes to its entries (the
+// tile's look-back is resolved one iteration later: VMQG_FX_DEFER)
+struct FxState {
+  uint32_t off[kFxK][64], cnt[kFxK][64], hoff[kFxK][64], tot[kFxK][64];
+  uint64_t rm[kFxK][64];
+  uint4 one[kFxK][64];
+  uint32_t onem[64];
+};
 struct FxLds {
-  uint64_t wtot[kWaves];
-  uint64_t base;
+  uint64_t wtot[kWaves], wprev[kWaves];
+  uint64_t base, agg, agg_prev;
   uint32_t tile;
   FxWave w[kWaves];
+#if VMQG_FX_DEFER
+  FxState t[kWaves];
+#endif
 };
 
 // the r-th entry of a publish: its key's records, then its remote nodes
@@ -2673,6 +2687,75 @@ __device__ __forceinline__ uint4 fx_emission(const MatchArgs& a, uint32_t off, u
   return make_uint4((VMQG_EMIT_REMOTE << 24) | node, kNone, kNone, kNone);
 }
 
+// One 64-publish chunk's offsets and entries (lane = publish p at output
+// offset ob): ranges; records — a huge publish left for the EMIT tail, a
+// one-entry publish by its own lane, the rest by the whole wave over their
+// concatenated entries, U per lane in flight.
+template <int OUT, bool NT>
+__device__ __forceinline__ void fx_emit_chunk(const MatchArgs& a, FxWave& W, uint32_t p, uint64_t ob, uint64_t cap,
+                                              uint32_t off, uint32_t cnt, uint32_t hoff, uint32_t tot, uint64_t rm,
+                                              bool has_one, uint4 one) {
+  const uint32_t lane = __lane_id();
+  const bool valid = p < a.npub;
+  const uint32_t nh = hoff != kNone ? a.exwords[hoff] : 0u;   // remote nodes >= 64 (rare: re-read)
+  if (valid) a.offsets[p] = ob;
+  bool ok = valid && tot > 0;
+  if (ok && ob + tot > cap) { atomicOr(a.err, kErrOverflow); ok = false; }
+  if constexpr (OUT == 1) {
+    if (ok) {
+      uint64_t o = ob;
+      if (cnt) store_range(a.out_rng, o++, off, cnt);
+      for (uint64_t m = rm; m; m &= m - 1) store_range(a.out_rng, o++, (uint32_t)__builtin_ctzll(m), 0u);
+      for (uint32_t i = 0; i < nh; i++) store_range(a.out_rng, o++, a.exwords[hoff + 1 + i], 0u);
+    }
+  } else {
+    // a huge publish: the EMIT tail copies it with every wave (its key cache and list, as k_count_exact)
+    const bool huge = ok && tot >= kHugeRecords && nh == 0;
+    if (huge) {
+      uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
+      const uint32_t nk = cnt ? 1u : 0u;
+      kc[0] = make_uint4(tot, nk | kHugeFlag, (uint32_t)rm, (uint32_t)(rm >> 32));
+      kc[1] = make_uint4(nk ? off : 0u, cnt, 0u, 0u);
+      a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
+      ok = false;
+    }
+    if (ok && tot == 1) {   // one entry: this lane writes it (the chunk's stores coalesce)
+      store_rec<NT>(a.out, ob, has_one ? one : fx_emission(a, off, cnt, rm, hoff, 0));
+      ok = false;
+    }
+    if (__ballot(ok)) {
+      const uint32_t sp = ok ? tot : 0u;
+      const uint32_t in32 = wave_incl_scan32(sp);
+      W.off[lane] = off; W.cnt[lane] = cnt; W.rm[lane] = rm; W.hoff[lane] = hoff;
+      W.ob[lane] = ob;
+      W.crel[lane] = in32 - sp;
+      if (lane == 63) W.crel[64] = in32;
+      wave_sync();
+      const uint32_t T = W.crel[64];
+      constexpr int U = VMQG_FX_U;
+      uint32_t q = 0;
+      for (uint32_t r0 = lane; r0 < T; r0 += 64 * U) {
+        uint4 v[U];
+        uint64_t dst[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t r = r0 + 64 * u;
+          if (r < T) {
+            while (q + 1 < 64 && W.crel[q + 1] <= r) q++;
+            const uint32_t rr = r - W.crel[q];
+            v[u] = fx_emission(a, W.off[q], W.cnt[q], W.rm[q], W.hoff[q], rr);
+            dst[u] = W.ob[q] + rr;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if (r0 + 64 * u < T) store_rec<NT>(a.out, dst[u], v[u]);
+      }
+      wave_sync();
+    }
+  }
+}
+
 template <int OUT, bool NT>
 __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
   __shared__ FxLds S;
@@ -2681,12 +2764,30 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
   FxWave& W = S.w[wv];
   const uint32_t ntiles = (a.npub + kFxTile - 1) / kFxTile;
   const uint64_t cap = OUT ? a.rng_cap : a.out_cap;
+#if VMQG_FX_DEFER
+  FxState& T = S.t[wv];
+  uint32_t prev = kNone;   // the tile probed in the previous iteration, entries not yet written (block-uniform)
+#endif
   for (;;) {
+#if VMQG_FX_DEFER
+    // the block that holds the last tile knows no later ticket is a tile
+    if (threadIdx.x == 0)
+      S.tile = prev != kNone && prev + 1 >= ntiles ? ntiles : atomicAdd(&a.status[kStTicket], 1u);
+#else
     if (threadIdx.x == 0) S.tile = atomicAdd(&a.status[kStTicket], 1u);
+#endif
     __syncthreads();
     const uint32_t tile = S.tile;
+#if VMQG_FX_DEFER
+    const bool have = tile < ntiles;
+    if (!have && prev == kNone) break;
+    const bool probe_on = have;   // a block past the last tile still writes its previous tile's entries
+    const uint32_t p0 = (have ? tile : 0u) * kFxTile + wv * (kFxK * 64);
+#else
     if (tile >= ntiles) break;
+    constexpr bool probe_on = true;
     const uint32_t p0 = tile * kFxTile + wv * (kFxK * 64);
+#endif
     // ---- probes (k_count_exact's, kFxK chunks in flight)
     vmqg_pub pub[kFxK];
     bool look[kFxK];
@@ -2694,7 +2795,7 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k < kFxK; k++) {
       const uint32_t p = p0 + k * 64 + lane;
-      pub[k] = p < a.npub ? a.pubs[p] : vmqg_pub{0xFFFFFFFFu, 0, 0, 0};
+      pub[k] = probe_on && p < a.npub ? a.pubs[p] : vmqg_pub{0xFFFFFFFFu, 0, 0, 0};
     }
 #pragma unroll
     for (uint32_t k = 0; k < kFxK; k++) {
@@ -2777,7 +2878,7 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
       const uint32_t nr = (uint32_t)__popcll(rm[k]) + (hi_at != kNone ? a.exwords[hi_at] : 0u);
       tot[k] = OUT ? (cnt[k] ? 1u : 0u) + nr : cnt[k] + nr;
     }
-    // ---- offsets: lane, chunk and wave prefixes, the tile's base by look-back
+    // ---- offsets: lane, chunk and wave prefixes; the tile's aggregate
     uint64_t excl[kFxK], wsum = 0;   // each publish's offset within its wave's entries
 #pragma unroll
     for (uint32_t k = 0; k < kFxK; k++) {
@@ -2787,6 +2888,54 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
     }
     if (lane == 0) S.wtot[wv] = wsum;
     __syncthreads();
+#if VMQG_FX_DEFER
+    // post this tile's aggregate now (successors can look past it at once),
+    // then resolve the previous tile: its predecessors have long posted, so
+    // its look-back does not wait; then write the previous tile's entries
+    // from LDS while this tile's results stay in registers
+    if (have && threadIdx.x == 0) {
+      uint64_t agg = 0;
+      for (uint32_t x = 0; x < kWaves; x++) agg += S.wtot[x];
+      S.agg = agg;
+      lb_store(a.lookback + tile, lb_pack(a.lb_tag, tile == 0 ? kLbIncl : kLbAgg, agg));
+    }
+    if (prev != kNone) {
+      if (wv == 0) {
+        const uint64_t b = lookback(a.lookback, a.lb_tag, a.err, prev, S.agg_prev);
+        if (lane == 0) {
+          S.base = b;
+          if (prev == ntiles - 1) a.offsets[a.npub] = b + S.agg_prev;   // the batch total
+        }
+      }
+      __syncthreads();
+      uint64_t wb = S.base;
+      for (uint32_t x = 0; x < wv; x++) wb += S.wprev[x];
+      const uint32_t q0 = prev * kFxTile + wv * (kFxK * 64);
+      const uint32_t om = T.onem[lane];
+      uint64_t run = 0;
+#pragma unroll 1
+      for (uint32_t k = 0; k < kFxK; k++) {
+        const uint32_t t = T.tot[k][lane];
+        const uint64_t incl = wave_incl_scan64(t);
+        fx_emit_chunk<OUT, NT>(a, W, q0 + k * 64 + lane, wb + run + incl - t, cap, T.off[k][lane], T.cnt[k][lane],
+                               T.hoff[k][lane], t, T.rm[k][lane], (om >> k) & 1u, T.one[k][lane]);
+        run += __shfl(incl, 63, 64);
+      }
+    }
+    __syncthreads();   // the previous tile's state and sums are consumed
+    if (!have) break;
+#pragma unroll
+    for (uint32_t k = 0; k < kFxK; k++) {
+      T.off[k][lane] = off[k]; T.cnt[k][lane] = cnt[k]; T.hoff[k][lane] = hoff[k]; T.tot[k][lane] = tot[k];
+      T.rm[k][lane] = rm[k];
+      if ((onem >> k) & 1u) T.one[k][lane] = one[k];
+    }
+    T.onem[lane] = onem;
+    if (lane == 0) S.wprev[wv] = S.wtot[wv];
+    if (threadIdx.x == 0) S.agg_prev = S.agg;
+    prev = tile;
+    (void)excl;
+#else
     if (wv == 0) {
       uint64_t agg = 0;
 #pragma unroll
@@ -2802,70 +2951,11 @@ __global__ __launch_bounds__(256) void k_match_exact_fused(MatchArgs a) {
     for (uint32_t x = 0; x < wv; x++) wbase += S.wtot[x];
     // ---- entries
 #pragma unroll
-    for (uint32_t k = 0; k < kFxK; k++) {
-      const uint32_t p = p0 + k * 64 + lane;
-      const bool valid = p < a.npub;
-      const uint64_t ob = wbase + excl[k];
-      const uint32_t nh = hoff[k] != kNone ? a.exwords[hoff[k]] : 0u;   // remote nodes >= 64 (rare: re-read)
-      if (valid) a.offsets[p] = ob;
-      bool ok = valid && tot[k] > 0;
-      if (ok && ob + tot[k] > cap) { atomicOr(a.err, kErrOverflow); ok = false; }
-      if constexpr (OUT == 1) {
-        if (ok) {
-          uint64_t o = ob;
-          if (cnt[k]) store_range(a.out_rng, o++, off[k], cnt[k]);
-          for (uint64_t m = rm[k]; m; m &= m - 1) store_range(a.out_rng, o++, (uint32_t)__builtin_ctzll(m), 0u);
-          for (uint32_t i = 0; i < nh; i++) store_range(a.out_rng, o++, a.exwords[hoff[k] + 1 + i], 0u);
-        }
-      } else {
-        // a huge publish: the EMIT tail copies it with every wave (its key cache and list, as k_count_exact)
-        const bool huge = ok && tot[k] >= kHugeRecords && nh == 0;
-        if (huge) {
-          uint4* kc = reinterpret_cast<uint4*>(a.keycache) + (uint64_t)p * 2;
-          const uint32_t nk = cnt[k] ? 1u : 0u;
-          kc[0] = make_uint4(tot[k], nk | kHugeFlag, (uint32_t)rm[k], (uint32_t)(rm[k] >> 32));
-          kc[1] = make_uint4(nk ? off[k] : 0u, cnt[k], 0u, 0u);
-          a.deferred[4ull * a.npub + atomicAdd(&a.status[kStHuge], 1u)] = p;
-          ok = false;
-        }
-        if (ok && tot[k] == 1) {   // one entry: this lane writes it (the chunk's stores coalesce)
-          store_rec<NT>(a.out, ob, (onem >> k) & 1u ? one[k] : fx_emission(a, off[k], cnt[k], rm[k], hoff[k], 0));
-          ok = false;
-        }
-        // the others: the whole wave over their concatenated entries, U per lane in flight
-        if (__ballot(ok)) {
-          const uint32_t sp = ok ? tot[k] : 0u;
-          const uint32_t in32 = wave_incl_scan32(sp);
-          W.off[lane] = off[k]; W.cnt[lane] = cnt[k]; W.rm[lane] = rm[k]; W.hoff[lane] = hoff[k];
-          W.ob[lane] = ob;
-          W.crel[lane] = in32 - sp;
-          if (lane == 63) W.crel[64] = in32;
-          wave_sync();
-          const uint32_t T = W.crel[64];
-          constexpr int U = VMQG_FX_U;
-          uint32_t q = 0;
-          for (uint32_t r0 = lane; r0 < T; r0 += 64 * U) {
-            uint4 v[U];
-            uint64_t dst[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-              const uint32_t r = r0 + 64 * u;
-              if (r < T) {
-                while (q + 1 < 64 && W.crel[q + 1] <= r) q++;
-                const uint32_t rr = r - W.crel[q];
-                v[u] = fx_emission(a, W.off[q], W.cnt[q], W.rm[q], W.hoff[q], rr);
-                dst[u] = W.ob[q] + rr;
-              }
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++)
-              if (r0 + 64 * u < T) store_rec<NT>(a.out, dst[u], v[u]);
-          }
-          wave_sync();
-        }
-      }
-    }
+    for (uint32_t k = 0; k < kFxK; k++)
+      fx_emit_chunk<OUT, NT>(a, W, p0 + k * 64 + lane, wbase + excl[k], cap, off[k], cnt[k], hoff[k], tot[k], rm[k],
+                             (onem >> k) & 1u, one[k]);
     __syncthreads();   // the next tile reuses S
+#endif
   }
 }
 
