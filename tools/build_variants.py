@@ -52,6 +52,15 @@ VARIANTS = {
     "fxk8": ["-DVMQG_FX_K=8"],
     "fxbpc8": ["-DVMQG_FX_BPC=8"],
     "fxk2bpc8": ["-DVMQG_FX_K=2", "-DVMQG_FX_BPC=8"],
+    # the deferred look-back (r06s / r06t scripts: VMQG_AB_DIR=build/ab8, names without the fx prefix there)
+    "nodefer": ["-DVMQG_FX_DEFER=0"],
+    "k1bpc6": ["-DVMQG_FX_K=1", "-DVMQG_FX_BPC=6"],
+    "k1bpc8": ["-DVMQG_FX_K=1", "-DVMQG_FX_BPC=8"],
+    "k2bpc5": ["-DVMQG_FX_K=2", "-DVMQG_FX_BPC=5"],
+    "k2bpc6": ["-DVMQG_FX_K=2", "-DVMQG_FX_BPC=6"],
+    "k3": ["-DVMQG_FX_K=3"],
+    "k4": ["-DVMQG_FX_K=4"],
+    "bpc8": ["-DVMQG_FX_BPC=8"],
     "fxk2u2": ["-DVMQG_FX_K=2", "-DVMQG_FX_U=2"],
     "fxk2u2bpc5": ["-DVMQG_FX_K=2", "-DVMQG_FX_U=2", "-DVMQG_FX_BPC=5"],
     "fxk3": ["-DVMQG_FX_K=3"],

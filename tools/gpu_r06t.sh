@@ -1,4 +1,5 @@
 # R1: the deferred-look-back fused match, tile-shape variants
+# libraries: VMQG_AB_DIR=build/ab8 python tools/build_variants.py k2 k1bpc6 k1bpc8 k2bpc5 k2bpc6 k3 bpc8
 set -o pipefail
 O=gpurun_out/r06t2
 mkdir -p $O
