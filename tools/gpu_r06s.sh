@@ -1,6 +1,6 @@
 # fused trie-less match with the deferred look-back: parity tests on it and
-# libraries: VMQG_AB_DIR=build/ab8 python tools/build_variants.py nodefer
 # on the immediate variant, then R1 A/B
+# libraries: VMQG_AB_DIR=build/ab8 python tools/build_variants.py nodefer
 set -o pipefail
 O=gpurun_out/r06s
 mkdir -p $O
